@@ -1,0 +1,57 @@
+# Native build: host C++ (g++) + HIP/CDNA4 kernels (hipcc, gfx950) -> one shared library plus the
+# worker_node / gateway / loadgen binaries.  `make -j8` here; the artefacts travel to the GPU box.
+PKG      := distributed-inference-engine-cpp_amd
+SRC      := $(PKG)/csrc
+BUILD    := build
+ROCM     ?= /opt/rocm
+ARCH     ?= gfx950
+CXX      := g++
+HIPCC    := $(ROCM)/bin/hipcc
+LIBDIR   := $(PKG)/lib
+BINDIR   := $(PKG)/bin
+
+CXXFLAGS := -std=c++17 -O3 -march=x86-64-v3 -fPIC -fopenmp -g -Wall -Wextra -Wno-unused-parameter \
+            -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
+HIPFLAGS := -std=c++17 -O3 --offload-arch=$(ARCH) -fPIC -g -Wall -Wno-unused-parameter -Wno-unused-result \
+            -munsafe-fp-atomics
+LDLIBS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread
+
+HOST_SRCS := core/json.cpp core/http.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
+             serve/worker.cpp serve/gateway.cpp serve/loadgen.cpp onnx/onnx_model.cpp \
+             engine/engine.cpp engine/cpu_exec.cpp capi/capi.cpp
+HIP_SRCS  := $(notdir $(wildcard $(SRC)/engine/*.hip)) $(notdir $(wildcard $(SRC)/kernels/*.hip))
+HOST_OBJS := $(addprefix $(BUILD)/host/,$(HOST_SRCS:.cpp=.o))
+HIP_OBJS  := $(patsubst %.hip,$(BUILD)/hip/%.o,$(HIP_SRCS))
+APPS      := worker_node gateway loadgen
+
+all: $(LIBDIR)/libdie.so $(addprefix $(BINDIR)/,$(APPS))
+
+$(BUILD)/host/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*/*.h)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -MMD -c $< -o $@
+
+$(BUILD)/hip/%.o: $(SRC)/engine/%.hip $(wildcard $(SRC)/*/*.h) $(wildcard $(SRC)/kernels/*.h)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/hip/%.o: $(SRC)/kernels/%.hip $(wildcard $(SRC)/kernels/*.h)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libdie.so: $(HOST_OBJS) $(HIP_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ $(LDLIBS)
+
+$(BINDIR)/%: $(SRC)/apps/%_main.cpp $(LIBDIR)/libdie.so
+	@mkdir -p $(BINDIR)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -Wl,-rpath,'$$ORIGIN/../lib' -ldie $(LDLIBS)
+
+$(BINDIR)/worker_node: $(SRC)/apps/worker_main.cpp $(LIBDIR)/libdie.so
+	@mkdir -p $(BINDIR)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(LIBDIR) -Wl,-rpath,'$$ORIGIN/../lib' -ldie $(LDLIBS)
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR) $(BINDIR)
+
+.PHONY: all clean
+-include $(HOST_OBJS:.o=.d)

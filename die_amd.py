@@ -1,0 +1,13 @@
+"""Import shim: the framework lives in `distributed-inference-engine-cpp_amd/`, a directory name
+that is not a valid Python identifier.  `import die_amd` loads it as a package (submodules such as
+`die_amd.models.resnet_v2` resolve through its `__path__`)."""
+import importlib.util as _ilu
+import os as _os
+import sys as _sys
+
+_PKG_DIR = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "distributed-inference-engine-cpp_amd")
+_spec = _ilu.spec_from_file_location(__name__, _os.path.join(_PKG_DIR, "__init__.py"),
+                                     submodule_search_locations=[_PKG_DIR])
+_mod = _ilu.module_from_spec(_spec)
+_sys.modules[__name__] = _mod
+_spec.loader.exec_module(_mod)

@@ -1,0 +1,430 @@
+// C ABI over the native runtime, loaded from Python with ctypes (die_amd/native.py).
+// Options travel as JSON strings; returned strings are malloc'ed and released with die_free().
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../core/json.h"
+#include "../engine/cpu_exec.h"
+#include "../engine/engine.h"
+#include "../serve/circuit_breaker.h"
+#include "../serve/consistent_hash.h"
+#include "../serve/gateway.h"
+#include "../serve/loadgen.h"
+#include "../serve/lru_cache.h"
+#include "../serve/worker.h"
+
+using namespace die;
+
+namespace {
+
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  return p;
+}
+
+void set_err(char** err, const std::string& m) {
+  if (err) *err = dup(m);
+}
+
+template <typename T>
+T jget(const Json& j, const char* k, T d);
+template <>
+int jget(const Json& j, const char* k, int d) {
+  auto* v = j.find(k);
+  return v ? static_cast<int>(v->as_int()) : d;
+}
+template <>
+long jget(const Json& j, const char* k, long d) {
+  auto* v = j.find(k);
+  return v ? static_cast<long>(v->as_int()) : d;
+}
+template <>
+double jget(const Json& j, const char* k, double d) {
+  auto* v = j.find(k);
+  return v ? v->as_double() : d;
+}
+template <>
+bool jget(const Json& j, const char* k, bool d) {
+  auto* v = j.find(k);
+  return v ? v->as_bool() : d;
+}
+template <>
+std::string jget(const Json& j, const char* k, std::string d) {
+  auto* v = j.find(k);
+  return v ? v->as_string() : d;
+}
+
+EngineOptions engine_opts(const Json& j) {
+  EngineOptions e;
+  e.device = jget<std::string>(j, "device", e.device);
+  e.device_id = jget<int>(j, "device_id", e.device_id);
+  e.max_batch = jget<int>(j, "max_batch", e.max_batch);
+  e.pipeline_depth = jget<int>(j, "pipeline_depth", e.pipeline_depth);
+  e.use_graphs = jget<bool>(j, "use_graphs", e.use_graphs);
+  e.precision = jget<std::string>(j, "precision", e.precision);
+  e.shard_id = jget<int>(j, "shard_id", e.shard_id);
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+void die_free(void* p) { std::free(p); }
+
+const char* die_version() { return "die_amd 0.1.0"; }
+
+// ---- JSON ----
+char* die_json_roundtrip(const char* text, char** err) {
+  try {
+    return dup(Json::parse(text).dump());
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+// Parses an /infer body: writes up to `cap` floats, returns count (-1 on error, message in err).
+long die_parse_infer(const char* body, long n, float* out, long cap, char** id_out, char** err) {
+  struct S : InferBodySink {
+    float* o;
+    size_t c;
+    size_t n = 0;
+    std::string id;
+    void on_request_id(std::string_view s) override { id = s; }
+    float* input_buffer() override { return o; }
+    size_t input_capacity() const override { return c; }
+    void on_input_count(size_t k) override { n = k; }
+  } s;
+  s.o = out;
+  s.c = static_cast<size_t>(cap);
+  try {
+    std::string b(body, static_cast<size_t>(n));
+    b.reserve(b.size() + 64);
+    parse_infer_body(b, s);
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return -1;
+  }
+  if (id_out) *id_out = dup(s.id);
+  return static_cast<long>(s.n);
+}
+
+char* die_format_floats(const float* v, long n) {
+  std::string s;
+  append_float_array(s, v, static_cast<size_t>(n));
+  return dup(s);
+}
+
+// ---- ring / breaker / cache (unit tests) ----
+uint32_t die_fnv1a(const char* s) { return ConsistentHash::fnv1a(s); }
+
+void* die_ring_create(int vnodes) { return new ConsistentHash(vnodes); }
+void die_ring_destroy(void* r) { delete static_cast<ConsistentHash*>(r); }
+void die_ring_add(void* r, const char* n) { static_cast<ConsistentHash*>(r)->addNode(n); }
+void die_ring_remove(void* r, const char* n) { static_cast<ConsistentHash*>(r)->removeNode(n); }
+char* die_ring_get(void* r, const char* k) { return dup(static_cast<ConsistentHash*>(r)->getNode(k)); }
+char* die_ring_nodes(void* r) {
+  Json a = Json::array();
+  for (auto& n : static_cast<ConsistentHash*>(r)->getAllNodes()) a.push_back(n);
+  return dup(a.dump());
+}
+long die_ring_size(void* r) { return static_cast<long>(static_cast<ConsistentHash*>(r)->ringSize()); }
+
+struct FakeClockBreaker {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::time_point{} + std::chrono::hours(1);
+  std::unique_ptr<CircuitBreaker> b;
+};
+void* die_breaker_create(int fail_thr, int succ_thr, long timeout_ms) {
+  auto* f = new FakeClockBreaker();
+  f->b = std::make_unique<CircuitBreaker>(fail_thr, succ_thr, std::chrono::milliseconds(timeout_ms),
+                                          [f] { return f->t; });
+  return f;
+}
+void die_breaker_destroy(void* p) { delete static_cast<FakeClockBreaker*>(p); }
+void die_breaker_advance(void* p, long ms) { static_cast<FakeClockBreaker*>(p)->t += std::chrono::milliseconds(ms); }
+int die_breaker_allow(void* p) { return static_cast<FakeClockBreaker*>(p)->b->allowRequest() ? 1 : 0; }
+void die_breaker_success(void* p) { static_cast<FakeClockBreaker*>(p)->b->recordSuccess(); }
+void die_breaker_failure(void* p) { static_cast<FakeClockBreaker*>(p)->b->recordFailure(); }
+char* die_breaker_state(void* p) {
+  auto* b = static_cast<FakeClockBreaker*>(p)->b.get();
+  Json j = Json::object();
+  j["state"] = b->getStateString();
+  j["failures"] = b->getFailureCount();
+  j["successes"] = b->getSuccessCount();
+  return dup(j.dump());
+}
+
+using FCache = LRUCache<InputKey, std::vector<float>, InputKeyHash>;
+void* die_cache_create(long cap) { return new FCache(static_cast<size_t>(cap)); }
+void die_cache_destroy(void* c) { delete static_cast<FCache*>(c); }
+void die_cache_put(void* c, const float* k, long kn, const float* v, long vn) {
+  static_cast<FCache*>(c)->put(hash_floats(k, static_cast<size_t>(kn)), std::vector<float>(v, v + vn));
+}
+// Returns value length (copied into out up to cap), or -1 on miss.
+long die_cache_get(void* c, const float* k, long kn, float* out, long cap) {
+  auto r = static_cast<FCache*>(c)->get(hash_floats(k, static_cast<size_t>(kn)));
+  if (!r) return -1;
+  std::memcpy(out, r->data(), sizeof(float) * std::min<size_t>(r->size(), static_cast<size_t>(cap)));
+  return static_cast<long>(r->size());
+}
+char* die_cache_stats(void* c) {
+  auto* p = static_cast<FCache*>(c);
+  Json j = Json::object();
+  j["size"] = static_cast<long long>(p->size());
+  j["hits"] = static_cast<long long>(p->getHits());
+  j["misses"] = static_cast<long long>(p->getMisses());
+  j["hit_rate"] = p->getHitRate();
+  return dup(j.dump());
+}
+
+// ---- batcher (unit tests): echo batches, records batch sizes ----
+struct TestBatcher {
+  std::unique_ptr<BatchProcessor<int, int>> bp;
+  std::mutex mu;
+  std::vector<int> sizes;
+  int delay_ms = 0;
+};
+void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int delay_ms) {
+  auto* t = new TestBatcher();
+  t->delay_ms = delay_ms;
+  t->bp = std::make_unique<BatchProcessor<int, int>>(
+      static_cast<size_t>(max_batch), std::chrono::milliseconds(timeout_ms),
+      [t](const std::vector<int>& reqs) {
+        {
+          std::lock_guard<std::mutex> g(t->mu);
+          t->sizes.push_back(static_cast<int>(reqs.size()));
+        }
+        if (t->delay_ms) std::this_thread::sleep_for(std::chrono::milliseconds(t->delay_ms));
+        std::vector<int> out;
+        for (int r : reqs) {
+          if (r < 0) throw std::runtime_error("negative request");
+          out.push_back(r * 2);
+        }
+        return out;
+      },
+      deadline_policy ? BatchPolicy::DEADLINE : BatchPolicy::GREEDY);
+  t->bp->start();
+  return t;
+}
+int die_batcher_process(void* p, int v, char** err) {
+  try {
+    return static_cast<TestBatcher*>(p)->bp->process(v);
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return -1;
+  }
+}
+char* die_batcher_metrics(void* p) {
+  auto* t = static_cast<TestBatcher*>(p);
+  auto m = t->bp->getMetrics();
+  Json j = Json::object();
+  j["total_requests"] = static_cast<long long>(m.total_requests);
+  j["total_batches"] = static_cast<long long>(m.total_batches);
+  j["timeout_batches"] = static_cast<long long>(m.timeout_batches);
+  j["full_batches"] = static_cast<long long>(m.full_batches);
+  j["avg_batch_size"] = m.avg_batch_size;
+  Json s = Json::array();
+  {
+    std::lock_guard<std::mutex> g(t->mu);
+    for (int v : t->sizes) s.push_back(v);
+  }
+  j["sizes"] = s;
+  return dup(j.dump());
+}
+void die_batcher_stop(void* p) { static_cast<TestBatcher*>(p)->bp->stop(); }
+void die_batcher_destroy(void* p) { delete static_cast<TestBatcher*>(p); }
+
+// ---- engine ----
+void* die_engine_create(const char* model_path, const char* opts_json, char** err) {
+  try {
+    Json j = opts_json && *opts_json ? Json::parse(opts_json) : Json::object();
+    return create_engine(model_path, engine_opts(j)).release();
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+void die_engine_destroy(void* e) { delete static_cast<Engine*>(e); }
+char* die_engine_info(void* p) {
+  auto* e = static_cast<Engine*>(p);
+  Json j = e->stats();
+  j["name"] = e->name();
+  Json in = Json::array(), out = Json::array();
+  for (auto d : e->getInputShape()) in.push_back(static_cast<long long>(d));
+  for (auto d : e->getOutputShape()) out.push_back(static_cast<long long>(d));
+  j["input_shape"] = in;
+  j["output_shape"] = out;
+  j["max_batch"] = e->max_batch();
+  return dup(j.dump());
+}
+// `in`: B samples of `len` floats each (len <= input numel; zero-padded).  `out`: B * output numel.
+int die_engine_run(void* p, const float* in, long B, long len, float* out, char** err) {
+  auto* e = static_cast<Engine*>(p);
+  try {
+    std::vector<std::vector<float>> xs(static_cast<size_t>(B));
+    for (long b = 0; b < B; ++b) xs[b].assign(in + b * len, in + (b + 1) * len);
+    auto ys = e->batchPredict(xs);
+    const size_t on = e->output_numel();
+    for (long b = 0; b < B; ++b) std::memcpy(out + b * on, ys[b].data(), on * sizeof(float));
+    return 0;
+  } catch (const std::exception& ex) {
+    set_err(err, ex.what());
+    return -1;
+  }
+}
+
+// ---- CPU executor oracle: full input tensor, returns output (malloc'ed) ----
+float* die_cpu_run(const char* model_path, const float* in, const int64_t* shape, int rank, int64_t* out_shape,
+                   int* out_rank, char** err) {
+  try {
+    CpuExecutor ex(onnx::load_onnx(model_path));
+    auto x = std::make_shared<CpuValue>();
+    x->shape.assign(shape, shape + rank);
+    x->f.assign(in, in + x->numel());
+    auto y = ex.run(x);
+    *out_rank = static_cast<int>(y->shape.size());
+    for (size_t k = 0; k < y->shape.size(); ++k) out_shape[k] = y->shape[k];
+    float* o = static_cast<float*>(std::malloc(sizeof(float) * y->f.size()));
+    std::memcpy(o, y->f.data(), sizeof(float) * y->f.size());
+    return o;
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+char* die_onnx_summary(const char* model_path, char** err) {
+  try {
+    auto m = onnx::load_onnx(model_path);
+    Json j = Json::object();
+    j["ir_version"] = static_cast<long long>(m.ir_version);
+    j["opset"] = static_cast<long long>(m.opset());
+    j["nodes"] = static_cast<long long>(m.nodes.size());
+    j["initializers"] = static_cast<long long>(m.initializers.size());
+    j["param_bytes"] = static_cast<long long>(m.param_bytes_f32());
+    Json ops = Json::object();
+    for (auto& n : m.nodes) ops[n.op_type] = ops[n.op_type].is_null() ? Json(1) : Json(ops[n.op_type].as_int() + 1);
+    j["ops"] = ops;
+    Json ins = Json::array();
+    for (auto& vi : m.inputs) {
+      Json v = Json::object();
+      v["name"] = vi.name;
+      Json d = Json::array();
+      for (auto x : vi.dims) d.push_back(static_cast<long long>(x));
+      v["dims"] = d;
+      ins.push_back(v);
+    }
+    j["inputs"] = ins;
+    Json outs = Json::array();
+    for (auto& vi : m.outputs) {
+      Json v = Json::object();
+      v["name"] = vi.name;
+      Json d = Json::array();
+      for (auto x : vi.dims) d.push_back(static_cast<long long>(x));
+      v["dims"] = d;
+      outs.push_back(v);
+    }
+    j["outputs"] = outs;
+    return dup(j.dump());
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+// ---- worker / gateway / loadgen ----
+void* die_worker_create(const char* opts_json, char** err) {
+  try {
+    Json j = Json::parse(opts_json);
+    WorkerOptions o;
+    o.node_id = jget<std::string>(j, "node_id", o.node_id);
+    o.host = jget<std::string>(j, "host", "127.0.0.1");
+    o.port = jget<int>(j, "port", 0);
+    o.model_path = jget<std::string>(j, "model_path", "");
+    o.cache_capacity = static_cast<size_t>(jget<long>(j, "cache_capacity", 1000));
+    o.max_batch = jget<int>(j, "max_batch", 32);
+    o.batch_timeout = std::chrono::milliseconds(jget<long>(j, "batch_timeout_ms", 20));
+    o.policy = jget<std::string>(j, "policy", "greedy") == "deadline" ? BatchPolicy::DEADLINE : BatchPolicy::GREEDY;
+    o.http_threads = jget<int>(j, "http_threads", 0);
+    o.engine = engine_opts(j.contains("engine") ? j.at("engine") : Json::object());
+    o.fault_fail_rate = jget<double>(j, "fault_fail_rate", 0.0);
+    o.fault_latency_ms = jget<int>(j, "fault_latency_ms", 0);
+    auto* w = new WorkerNode(o);
+    if (w->start() < 0) {
+      delete w;
+      set_err(err, "cannot bind worker port");
+      return nullptr;
+    }
+    return w;
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+int die_worker_port(void* w) { return static_cast<WorkerNode*>(w)->port(); }
+char* die_worker_health(void* w) { return dup(static_cast<WorkerNode*>(w)->getHealth().dump()); }
+void die_worker_stop(void* w) { static_cast<WorkerNode*>(w)->stop(); }
+void die_worker_destroy(void* w) { delete static_cast<WorkerNode*>(w); }
+
+void* die_gateway_create(const char* opts_json, char** err) {
+  try {
+    Json j = Json::parse(opts_json);
+    GatewayOptions o;
+    for (auto& w : j.at("workers").as_array()) o.workers.push_back(w.as_string());
+    o.host = jget<std::string>(j, "host", "127.0.0.1");
+    o.port = jget<int>(j, "port", 0);
+    o.failure_threshold = jget<int>(j, "failure_threshold", 5);
+    o.success_threshold = jget<int>(j, "success_threshold", 2);
+    o.breaker_timeout = std::chrono::milliseconds(static_cast<long>(jget<double>(j, "breaker_timeout_s", 30.0) * 1000));
+    o.vnodes = jget<int>(j, "vnodes", 150);
+    o.connect_timeout = std::chrono::milliseconds(jget<long>(j, "connect_timeout_ms", 5000));
+    o.read_timeout = std::chrono::milliseconds(jget<long>(j, "read_timeout_ms", 5000));
+    o.forward_threads = jget<int>(j, "forward_threads", 64);
+    o.http_threads = jget<int>(j, "http_threads", 0);
+    auto* g = new Gateway(o);
+    if (g->start() < 0) {
+      delete g;
+      set_err(err, "cannot bind gateway port");
+      return nullptr;
+    }
+    return g;
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+int die_gateway_port(void* g) { return static_cast<Gateway*>(g)->port(); }
+char* die_gateway_stats(void* g) { return dup(static_cast<Gateway*>(g)->getStats().dump()); }
+void die_gateway_stop(void* g) { static_cast<Gateway*>(g)->stop(); }
+void die_gateway_destroy(void* g) { delete static_cast<Gateway*>(g); }
+
+char* die_loadgen_run(const char* opts_json, char** err) {
+  try {
+    Json j = Json::parse(opts_json);
+    LoadgenOptions o;
+    o.host = jget<std::string>(j, "host", o.host);
+    o.port = jget<int>(j, "port", o.port);
+    o.path = jget<std::string>(j, "path", o.path);
+    o.connections = jget<int>(j, "connections", o.connections);
+    o.requests = jget<long>(j, "requests", o.requests);
+    o.warmup = jget<long>(j, "warmup", o.warmup);
+    o.payload = jget<std::string>(j, "payload", o.payload);
+    o.input_numel = static_cast<size_t>(jget<long>(j, "input_numel", static_cast<long>(o.input_numel)));
+    o.decimals = jget<int>(j, "decimals", o.decimals);
+    o.distinct = jget<long>(j, "distinct", o.distinct);
+    o.timeout_ms = jget<int>(j, "timeout_ms", o.timeout_ms);
+    o.seed = static_cast<uint64_t>(jget<long>(j, "seed", static_cast<long>(o.seed)));
+    o.id_prefix = jget<std::string>(j, "id_prefix", o.id_prefix);
+    return dup(run_loadgen(o).dump());
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+}  // extern "C"

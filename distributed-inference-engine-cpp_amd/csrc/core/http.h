@@ -1,0 +1,139 @@
+// In-tree HTTP/1.1 server (epoll reactors) and pooled keep-alive client.
+//
+// Replaces cpp-httplib v0.14.3 (reference setup.sh:42; used at src/worker_node.cpp:172-202,
+// src/gateway.cpp:29-33,99-103,174-198).  Differences that matter for throughput:
+//  * handlers are asynchronous: a handler receives a Responder and may complete it later from any
+//    thread, so a request waiting on the batcher never pins a server thread;
+//  * the client keeps a pool of keep-alive connections per upstream instead of one mutex-guarded
+//    connection, so concurrent gateway->worker requests are not serialised.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+namespace die {
+
+struct HttpRequest {
+  std::string method;
+  std::string path;    // without query string
+  std::string query;   // raw query string (after '?'), may be empty
+  std::vector<std::pair<std::string, std::string>> headers;  // names lower-cased
+  std::string body;    // capacity always >= size + 64 (slack for SIMD parsers)
+  bool keep_alive = true;
+  std::string_view header(std::string_view name) const;  // name must be lower-case
+};
+
+struct HttpResponse {
+  int status = 200;
+  std::string content_type = "application/json";
+  std::string body;
+  bool close = false;
+};
+
+const char* http_status_text(int status);
+
+class HttpServer;
+
+// One-shot completion handle for a request.  Copyable; only the first send() has an effect.
+class Responder {
+ public:
+  Responder() = default;
+  // Complete with a ready response (any thread).
+  void send(HttpResponse resp) const;
+  // Complete by running `build` on the connection's reactor thread (spreads serialisation work
+  // over the reactors instead of the thread that finished the request).
+  void defer(std::function<HttpResponse()> build) const;
+  bool valid() const { return static_cast<bool>(state_); }
+
+ private:
+  friend class HttpServer;
+  struct State;
+  std::shared_ptr<State> state_;
+};
+
+class HttpServer {
+ public:
+  using Handler = std::function<void(HttpRequest& req, Responder res)>;
+
+  HttpServer();
+  ~HttpServer();
+  HttpServer(const HttpServer&) = delete;
+  HttpServer& operator=(const HttpServer&) = delete;
+
+  void route(const std::string& method, const std::string& path, Handler h);
+  // Bind and start `threads` reactor threads (0 = hardware concurrency, capped at 32).
+  // port 0 picks an ephemeral port; returns the bound port, or -1 on failure.
+  int start(const std::string& host, int port, int threads = 0);
+  // Block until stop() is called.
+  void wait();
+  void stop();
+  int port() const { return port_; }
+  bool running() const { return running_.load(); }
+  uint64_t requests_served() const { return served_.load(); }
+  size_t max_body_bytes = 512u << 20;
+
+ private:
+  struct Reactor;
+  struct Conn;
+  friend class Responder;
+  void reactor_loop(Reactor* r);
+  void dispatch(Reactor* r, Conn* c);
+
+  std::vector<std::pair<std::pair<std::string, std::string>, Handler>> routes_;
+  std::vector<std::unique_ptr<Reactor>> reactors_;
+  std::vector<std::thread> threads_;
+  int listen_fd_ = -1;
+  int port_ = -1;
+  std::atomic<bool> running_{false};
+  std::atomic<uint64_t> served_{0};
+  std::mutex wait_mu_, stop_mu_;
+  std::condition_variable wait_cv_;
+};
+
+// Blocking HTTP/1.1 client with a keep-alive connection pool; safe for concurrent use.
+class HttpClient {
+ public:
+  HttpClient(std::string host, int port, std::chrono::milliseconds connect_timeout = std::chrono::seconds(5),
+             std::chrono::milliseconds read_timeout = std::chrono::seconds(5), size_t max_idle = 256);
+  ~HttpClient();
+  // Returns nullopt on transport failure (connect/send/recv/timeout/malformed response);
+  // `error` then holds a description.
+  std::optional<HttpResponse> request(const std::string& method, const std::string& path, std::string_view body,
+                                      const std::string& content_type = "application/json",
+                                      std::string* error = nullptr);
+  std::optional<HttpResponse> post(const std::string& path, std::string_view body,
+                                   const std::string& content_type = "application/json", std::string* error = nullptr) {
+    return request("POST", path, body, content_type, error);
+  }
+  std::optional<HttpResponse> get(const std::string& path, std::string* error = nullptr) {
+    return request("GET", path, {}, "", error);
+  }
+  const std::string& host() const { return host_; }
+  int port() const { return port_; }
+
+ private:
+  int connect_new(std::string* error);
+  void release(int fd);
+  std::string host_;
+  int port_;
+  std::chrono::milliseconds connect_timeout_, read_timeout_;
+  size_t max_idle_;
+  std::mutex mu_;
+  std::vector<int> idle_;
+};
+
+// Parse "host:port", "http://host:port/..." -> (host, port); default port 8080 like the
+// reference's Gateway::parseUrl (src/gateway.cpp:130-154).
+std::pair<std::string, int> parse_host_port(const std::string& url);
+
+}  // namespace die

@@ -1,0 +1,858 @@
+#include "json.h"
+
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <emmintrin.h>
+
+namespace die {
+
+// ------------------------------------------------------------------------------------------------
+// DOM
+// ------------------------------------------------------------------------------------------------
+
+Json::Json(const std::vector<float>& v) : type_(Type::Array) {
+  a_.reserve(v.size());
+  for (float f : v) a_.emplace_back(f);
+}
+
+bool Json::as_bool() const {
+  if (type_ != Type::Bool) throw JsonError("type must be boolean");
+  return b_;
+}
+int64_t Json::as_int() const {
+  if (type_ == Type::Int) return i_;
+  if (type_ == Type::Float) return static_cast<int64_t>(d_);
+  throw JsonError("type must be number");
+}
+double Json::as_double() const {
+  if (type_ == Type::Float) return d_;
+  if (type_ == Type::Int) return static_cast<double>(i_);
+  throw JsonError("type must be number");
+}
+const std::string& Json::as_string() const {
+  if (type_ != Type::String) throw JsonError("type must be string");
+  return s_;
+}
+const Json::Array& Json::as_array() const {
+  if (type_ != Type::Array) throw JsonError("type must be array");
+  return a_;
+}
+Json::Array& Json::as_array() {
+  if (type_ != Type::Array) throw JsonError("type must be array");
+  return a_;
+}
+const Json::Object& Json::as_object() const {
+  if (type_ != Type::Object) throw JsonError("type must be object");
+  return o_;
+}
+
+Json& Json::operator[](const std::string& key) {
+  if (type_ == Type::Null) type_ = Type::Object;
+  if (type_ != Type::Object) throw JsonError("cannot use operator[] with a string argument");
+  for (auto& kv : o_)
+    if (kv.first == key) return kv.second;
+  o_.emplace_back(key, Json());
+  return o_.back().second;
+}
+const Json* Json::find(const std::string& key) const {
+  if (type_ != Type::Object) return nullptr;
+  for (auto& kv : o_)
+    if (kv.first == key) return &kv.second;
+  return nullptr;
+}
+const Json& Json::at(const std::string& key) const {
+  const Json* j = find(key);
+  if (!j) throw JsonError("key '" + key + "' not found");
+  return *j;
+}
+void Json::push_back(Json v) {
+  if (type_ == Type::Null) type_ = Type::Array;
+  if (type_ != Type::Array) throw JsonError("cannot use push_back() with non-array");
+  a_.push_back(std::move(v));
+}
+const Json& Json::operator[](size_t i) const {
+  if (type_ != Type::Array) throw JsonError("cannot use operator[] with a numeric argument");
+  return a_.at(i);
+}
+size_t Json::size() const {
+  if (type_ == Type::Array) return a_.size();
+  if (type_ == Type::Object) return o_.size();
+  if (type_ == Type::Null) return 0;
+  return 1;
+}
+
+void append_json_string(std::string& out, std::string_view s) {
+  out.push_back('"');
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\b': out += "\\b"; break;
+      case '\f': out += "\\f"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char buf[8];
+          std::snprintf(buf, sizeof buf, "\\u%04x", c);
+          out += buf;
+        } else {
+          out.push_back(static_cast<char>(c));
+        }
+    }
+  }
+  out.push_back('"');
+}
+
+static inline void append_double(std::string& out, double d, bool f32) {
+  if (!std::isfinite(d)) {
+    out += "null";
+    return;
+  }
+  char buf[40];
+  std::to_chars_result r = f32 ? std::to_chars(buf, buf + sizeof buf, static_cast<float>(d))
+                               : std::to_chars(buf, buf + sizeof buf, d);
+  // Keep a visible fraction/exponent so the value reads back as a float, like nlohmann does.
+  bool has_dot = false;
+  for (char* q = buf; q < r.ptr; ++q)
+    if (*q == '.' || *q == 'e' || *q == 'n' || *q == 'i') has_dot = true;
+  out.append(buf, r.ptr);
+  if (!has_dot) out += ".0";
+}
+
+void append_float_array(std::string& out, const float* v, size_t n) {
+  out.reserve(out.size() + n * 12 + 2);
+  out.push_back('[');
+  char buf[32];
+  for (size_t i = 0; i < n; ++i) {
+    if (i) out.push_back(',');
+    float f = v[i];
+    if (!std::isfinite(f)) {
+      out += "null";
+      continue;
+    }
+    auto r = std::to_chars(buf, buf + sizeof buf, f);
+    out.append(buf, r.ptr);
+  }
+  out.push_back(']');
+}
+
+void Json::dump_to(std::string& out) const {
+  switch (type_) {
+    case Type::Null: out += "null"; break;
+    case Type::Bool: out += b_ ? "true" : "false"; break;
+    case Type::Int: {
+      char buf[24];
+      auto r = std::to_chars(buf, buf + sizeof buf, i_);
+      out.append(buf, r.ptr);
+      break;
+    }
+    case Type::Float: append_double(out, d_, is_f32_); break;
+    case Type::String: append_json_string(out, s_); break;
+    case Type::Array: {
+      out.push_back('[');
+      for (size_t i = 0; i < a_.size(); ++i) {
+        if (i) out.push_back(',');
+        a_[i].dump_to(out);
+      }
+      out.push_back(']');
+      break;
+    }
+    case Type::Object: {
+      out.push_back('{');
+      for (size_t i = 0; i < o_.size(); ++i) {
+        if (i) out.push_back(',');
+        append_json_string(out, o_[i].first);
+        out.push_back(':');
+        o_[i].second.dump_to(out);
+      }
+      out.push_back('}');
+      break;
+    }
+  }
+}
+
+std::string Json::dump() const {
+  std::string s;
+  dump_to(s);
+  return s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Parser
+// ------------------------------------------------------------------------------------------------
+
+namespace {
+
+struct Cursor {
+  const char* p;
+  const char* end;
+  const char* begin;
+
+  [[noreturn]] void fail(const char* what) const {
+    throw JsonError(std::string("[json.exception.parse_error] syntax error at byte ") +
+                    std::to_string(p - begin + 1) + ": " + what);
+  }
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  char peek() {
+    ws();
+    if (p >= end) fail("unexpected end of input");
+    return *p;
+  }
+  void expect(char c) {
+    if (peek() != c) {
+      char msg[64];
+      std::snprintf(msg, sizeof msg, "expected '%c'", c);
+      fail(msg);
+    }
+    ++p;
+  }
+};
+
+void append_utf8(std::string& out, uint32_t cp) {
+  if (cp < 0x80) {
+    out.push_back(static_cast<char>(cp));
+  } else if (cp < 0x800) {
+    out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else if (cp < 0x10000) {
+    out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else {
+    out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  }
+}
+
+uint32_t parse_hex4(Cursor& c) {
+  if (c.end - c.p < 4) c.fail("bad \\u escape");
+  uint32_t v = 0;
+  for (int i = 0; i < 4; ++i) {
+    char h = *c.p++;
+    v <<= 4;
+    if (h >= '0' && h <= '9') v |= h - '0';
+    else if (h >= 'a' && h <= 'f') v |= h - 'a' + 10;
+    else if (h >= 'A' && h <= 'F') v |= h - 'A' + 10;
+    else c.fail("bad \\u escape");
+  }
+  return v;
+}
+
+std::string parse_string(Cursor& c) {
+  c.expect('"');
+  std::string out;
+  const char* run = c.p;
+  while (true) {
+    if (c.p >= c.end) c.fail("unterminated string");
+    char ch = *c.p;
+    if (ch == '"') {
+      out.append(run, c.p);
+      ++c.p;
+      return out;
+    }
+    if (static_cast<unsigned char>(ch) < 0x20) c.fail("control character in string");
+    if (ch == '\\') {
+      out.append(run, c.p);
+      ++c.p;
+      if (c.p >= c.end) c.fail("unterminated escape");
+      char e = *c.p++;
+      switch (e) {
+        case '"': out.push_back('"'); break;
+        case '\\': out.push_back('\\'); break;
+        case '/': out.push_back('/'); break;
+        case 'b': out.push_back('\b'); break;
+        case 'f': out.push_back('\f'); break;
+        case 'n': out.push_back('\n'); break;
+        case 'r': out.push_back('\r'); break;
+        case 't': out.push_back('\t'); break;
+        case 'u': {
+          uint32_t cp = parse_hex4(c);
+          if (cp >= 0xD800 && cp <= 0xDBFF) {
+            if (c.end - c.p >= 6 && c.p[0] == '\\' && c.p[1] == 'u') {
+              c.p += 2;
+              uint32_t lo = parse_hex4(c);
+              if (lo < 0xDC00 || lo > 0xDFFF) c.fail("bad surrogate pair");
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            } else {
+              c.fail("bad surrogate pair");
+            }
+          }
+          append_utf8(out, cp);
+          break;
+        }
+        default: c.fail("bad escape");
+      }
+      run = c.p;
+    } else {
+      ++c.p;
+    }
+  }
+}
+
+// Skip a string without materialising it.
+void skip_string(Cursor& c) {
+  c.expect('"');
+  while (true) {
+    const char* q = static_cast<const char*>(std::memchr(c.p, '"', c.end - c.p));
+    if (!q) c.fail("unterminated string");
+    // count preceding backslashes
+    const char* b = q;
+    while (b > c.p && b[-1] == '\\') --b;
+    c.p = q + 1;
+    if (((q - b) & 1) == 0) return;
+  }
+}
+
+const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                         1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+const float kPow10f[] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+
+// Scan a JSON number; returns mantissa digits etc.  Used by both float and DOM paths.
+struct NumScan {
+  uint64_t mant = 0;
+  int digits = 0;      // significant digits accumulated into mant (<= 19)
+  int exp10 = 0;       // value = mant * 10^exp10 (when !overflow)
+  bool neg = false;
+  bool is_int = true;  // no fraction / exponent
+  bool truncated = false;
+  const char* start = nullptr;
+  const char* stop = nullptr;
+};
+
+inline bool scan_number(const char*& p, const char* end, NumScan& s) {
+  s.start = p;
+  if (p < end && *p == '-') {
+    s.neg = true;
+    ++p;
+  }
+  if (p >= end) return false;
+  if (*p == '0') {
+    ++p;
+  } else if (*p >= '1' && *p <= '9') {
+    while (p < end && static_cast<unsigned>(*p - '0') < 10u) {
+      if (s.digits < 19) {
+        s.mant = s.mant * 10 + static_cast<unsigned>(*p - '0');
+        if (s.mant) ++s.digits;
+      } else {
+        ++s.exp10;
+        s.truncated = true;
+      }
+      ++p;
+    }
+  } else {
+    return false;
+  }
+  if (p < end && *p == '.') {
+    s.is_int = false;
+    ++p;
+    if (p >= end || static_cast<unsigned>(*p - '0') >= 10u) return false;
+    while (p < end && static_cast<unsigned>(*p - '0') < 10u) {
+      if (s.digits < 19) {
+        s.mant = s.mant * 10 + static_cast<unsigned>(*p - '0');
+        if (s.mant) ++s.digits;
+        --s.exp10;
+      } else {
+        s.truncated = true;
+      }
+      ++p;
+    }
+  }
+  if (p < end && (*p == 'e' || *p == 'E')) {
+    s.is_int = false;
+    ++p;
+    bool eneg = false;
+    if (p < end && (*p == '+' || *p == '-')) {
+      eneg = *p == '-';
+      ++p;
+    }
+    if (p >= end || static_cast<unsigned>(*p - '0') >= 10u) return false;
+    int e = 0;
+    while (p < end && static_cast<unsigned>(*p - '0') < 10u) {
+      if (e < 100000) e = e * 10 + (*p - '0');
+      ++p;
+    }
+    s.exp10 += eneg ? -e : e;
+  }
+  s.stop = p;
+  return true;
+}
+
+float slow_float(const char* b, const char* e) {
+  float v = 0.f;
+  auto r = std::from_chars(b, e, v);
+  if (r.ec == std::errc::result_out_of_range) {
+    // from_chars leaves v untouched on range errors: mirror strtof (inf / 0).
+    std::string tmp(b, e);
+    v = std::strtof(tmp.c_str(), nullptr);
+  }
+  return v;
+}
+
+double slow_double(const char* b, const char* e) {
+  std::string tmp(b, e);
+  return std::strtod(tmp.c_str(), nullptr);
+}
+
+inline float scan_to_float(const NumScan& s) {
+  if (s.mant == 0) return s.neg ? -0.f : 0.f;
+  if (!s.truncated) {
+    // Clinger fast path in float: exact mantissa and exact power of ten -> one rounding.
+    if (s.mant <= (1u << 24) && s.exp10 >= -10 && s.exp10 <= 10) {
+      float m = static_cast<float>(s.mant);
+      float v = s.exp10 < 0 ? m / kPow10f[-s.exp10] : m * kPow10f[s.exp10];
+      return s.neg ? -v : v;
+    }
+    // Clinger in double (one correct rounding), then to float.  Double rounding can only go
+    // wrong when the double lands exactly on a float halfway point: detect that and fall back.
+    if (s.mant <= (1ull << 53) && s.exp10 >= -22 && s.exp10 <= 22) {
+      double m = static_cast<double>(s.mant);
+      double d = s.exp10 < 0 ? m / kPow10[-s.exp10] : m * kPow10[s.exp10];
+      uint64_t bits;
+      std::memcpy(&bits, &d, sizeof bits);
+      const uint64_t low = bits & ((1ull << 29) - 1);
+      const int bexp = static_cast<int>((bits >> 52) & 0x7FF) - 1023;
+      if (low != (1ull << 28) && bexp > -126 && bexp < 127) {
+        float v = static_cast<float>(d);
+        return s.neg ? -v : v;
+      }
+    }
+  }
+  return slow_float(s.start, s.stop);
+}
+
+// ---- SWAR fast path for the common "-?d{1,8}(.d{1,8})?" numbers ----------------------------------
+
+inline uint64_t load8(const char* p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);
+  return v;
+}
+// Number of leading ASCII digits (0..8) in the 8 bytes at p (little-endian: first char = low byte).
+inline int leading_digits(uint64_t v) {
+  const uint64_t x = (v & 0xF0F0F0F0F0F0F0F0ull) | (((v + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) >> 4);
+  const uint64_t nd = x ^ 0x3333333333333333ull;
+  if (nd == 0) return 8;
+  return __builtin_ctzll(nd) >> 3;
+}
+// Value of the first k (1..8) digits of v.
+inline uint32_t swar_digits(uint64_t v, int k) {
+  uint64_t val = (v & 0x0F0F0F0F0F0F0F0Full) << (8 * (8 - k));
+  val = (val * 2561) >> 8;
+  val = ((val & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+  return static_cast<uint32_t>(((val & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32);
+}
+const uint32_t kPow10u[] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000, 100000000};
+
+// Returns true and advances p if the number has the simple form; false leaves p untouched.
+inline bool fast_simple_float(const char*& p, const char* end, float& out) {
+  const char* q = p;
+  if (end - q < 20) return false;
+  const bool neg = *q == '-';
+  q += neg;
+  const uint64_t vi = load8(q);
+  const int ki = leading_digits(vi);
+  if (ki == 0 || ki == 8) return false;
+  if (ki > 1 && *q == '0') return false;  // leading zero: let the strict scanner reject it
+  uint64_t mant = swar_digits(vi, ki);
+  q += ki;
+  int exp10 = 0;
+  if (*q == '.') {
+    ++q;
+    const uint64_t vf = load8(q);
+    const int kf = leading_digits(vf);
+    if (kf == 0 || kf == 8) return false;
+    mant = mant * kPow10u[kf] + swar_digits(vf, kf);
+    exp10 = -kf;
+    q += kf;
+  }
+  if (*q == 'e' || *q == 'E') return false;
+  float v;
+  if (mant <= (1u << 24)) {
+    const float m = static_cast<float>(mant);
+    v = m / kPow10f[-exp10];
+  } else {
+    // <= 16 significant digits: exact in double; one correctly rounded division, then the
+    // halfway check of scan_to_float.
+    const double d = static_cast<double>(mant) / kPow10[-exp10];
+    uint64_t bits;
+    std::memcpy(&bits, &d, sizeof bits);
+    if ((bits & ((1ull << 29) - 1)) == (1ull << 28)) return false;
+    v = static_cast<float>(d);
+  }
+  out = neg ? -v : v;
+  p = q;
+  return true;
+}
+
+// Parse one token [b, e) known to be delimited by separators (no whitespace inside).  Independent
+// of every other token, so consecutive calls overlap in the out-of-order core.
+inline bool parse_token(const char* b, const char* e, float& out) {
+  const bool neg = *b == '-';
+  b += neg;
+  const long len = e - b;
+  if (len <= 0 || len > 17) return false;
+  const uint64_t vi = load8(b);
+  int ki = leading_digits(vi);
+  if (ki > len) ki = static_cast<int>(len);
+  if (ki == 0 || ki == 8) return false;
+  if (ki > 1 && *b == '0') return false;
+  uint64_t mant = swar_digits(vi, ki);
+  int exp10 = 0;
+  if (ki != len) {
+    if (b[ki] != '.') return false;
+    const int kf = static_cast<int>(len) - ki - 1;
+    if (kf <= 0 || kf > 8) return false;
+    const uint64_t vf = load8(b + ki + 1);
+    if (leading_digits(vf) < kf) return false;
+    mant = mant * kPow10u[kf] + swar_digits(vf, kf);
+    exp10 = -kf;
+  }
+  float v;
+  if (mant <= (1u << 24)) {
+    v = static_cast<float>(mant) / kPow10f[-exp10];
+  } else {
+    const double d = static_cast<double>(mant) / kPow10[-exp10];
+    uint64_t bits;
+    std::memcpy(&bits, &d, sizeof bits);
+    if ((bits & ((1ull << 29) - 1)) == (1ull << 28)) return false;
+    v = static_cast<float>(d);
+  }
+  // Branch-free sign: random signs would otherwise mispredict half the time.
+  uint32_t bits;
+  std::memcpy(&bits, &v, 4);
+  bits |= static_cast<uint32_t>(neg) << 31;
+  std::memcpy(&out, &bits, 4);
+  return true;
+}
+
+// 64-bit masks of ',' and ']' in the 64 bytes at p (SSE2).
+inline void sep_masks(const char* p, uint64_t& comma, uint64_t& close) {
+  const __m128i c1 = _mm_set1_epi8(',');
+  const __m128i c2 = _mm_set1_epi8(']');
+  comma = 0;
+  close = 0;
+  for (int i = 0; i < 4; ++i) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * i));
+    comma |= static_cast<uint64_t>(static_cast<uint32_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(v, c1)))) << (16 * i);
+    close |= static_cast<uint64_t>(static_cast<uint32_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(v, c2)))) << (16 * i);
+  }
+}
+
+// Bulk path for the body of a float array starting right after '['.  Consumes whole tokens while
+// they are "simple" and complete 64-byte blocks are available; returns the position of the first
+// unconsumed byte (the start of a token, or one past the closing ']' when *done is set).
+inline const char* bulk_float_array(const char* p, const char* end, float* dst, size_t cap, size_t& n,
+                                    bool& done) {
+  done = false;
+  const char* tok = p;
+  const char* base = p;
+  while (end - base >= 64 + 24) {  // 24 bytes of slack so token loads stay in bounds
+    uint64_t comma, close;
+    sep_masks(base, comma, close);
+    uint64_t m = comma | close;
+    while (m) {
+      const int s = __builtin_ctzll(m);
+      const char* sep = base + s;
+      float v;
+      if (sep == tok || !parse_token(tok, sep, v)) return tok;  // let the strict path decide
+      if (n < cap) dst[n] = v;
+      ++n;
+      tok = sep + 1;
+      if ((close >> s) & 1) {
+        done = true;
+        return tok;
+      }
+      m &= m - 1;
+    }
+    base += 64;
+  }
+  return tok;
+}
+
+Json parse_value(Cursor& c, int depth);
+
+Json parse_number(Cursor& c) {
+  NumScan s;
+  const char* p = c.p;
+  if (!scan_number(p, c.end, s)) c.fail("invalid number");
+  c.p = p;
+  if (s.is_int && !s.truncated && s.mant <= static_cast<uint64_t>(INT64_MAX)) {
+    int64_t v = static_cast<int64_t>(s.mant);
+    return Json(static_cast<long long>(s.neg ? -v : v));
+  }
+  return Json(slow_double(s.start, s.stop));
+}
+
+Json parse_value(Cursor& c, int depth) {
+  if (depth > 512) c.fail("nesting too deep");
+  char ch = c.peek();
+  switch (ch) {
+    case '{': {
+      ++c.p;
+      Json obj = Json::object();
+      if (c.peek() == '}') {
+        ++c.p;
+        return obj;
+      }
+      while (true) {
+        std::string key = parse_string(c);
+        c.expect(':');
+        obj[key] = parse_value(c, depth + 1);
+        char n = c.peek();
+        if (n == ',') {
+          ++c.p;
+          continue;
+        }
+        if (n == '}') {
+          ++c.p;
+          return obj;
+        }
+        c.fail("expected ',' or '}'");
+      }
+    }
+    case '[': {
+      ++c.p;
+      Json arr = Json::array();
+      if (c.peek() == ']') {
+        ++c.p;
+        return arr;
+      }
+      while (true) {
+        arr.push_back(parse_value(c, depth + 1));
+        char n = c.peek();
+        if (n == ',') {
+          ++c.p;
+          continue;
+        }
+        if (n == ']') {
+          ++c.p;
+          return arr;
+        }
+        c.fail("expected ',' or ']'");
+      }
+    }
+    case '"': return Json(parse_string(c));
+    case 't':
+      if (c.end - c.p >= 4 && std::memcmp(c.p, "true", 4) == 0) {
+        c.p += 4;
+        return Json(true);
+      }
+      c.fail("invalid literal");
+    case 'f':
+      if (c.end - c.p >= 5 && std::memcmp(c.p, "false", 5) == 0) {
+        c.p += 5;
+        return Json(false);
+      }
+      c.fail("invalid literal");
+    case 'n':
+      if (c.end - c.p >= 4 && std::memcmp(c.p, "null", 4) == 0) {
+        c.p += 4;
+        return Json();
+      }
+      c.fail("invalid literal");
+    default:
+      if (ch == '-' || (ch >= '0' && ch <= '9')) return parse_number(c);
+      c.fail("invalid literal");
+  }
+}
+
+void skip_value(Cursor& c, int depth) {
+  if (depth > 512) c.fail("nesting too deep");
+  char ch = c.peek();
+  if (ch == '"') {
+    skip_string(c);
+    return;
+  }
+  if (ch == '{' || ch == '[') {
+    char close = ch == '{' ? '}' : ']';
+    ++c.p;
+    if (c.peek() == close) {
+      ++c.p;
+      return;
+    }
+    while (true) {
+      if (ch == '{') {
+        skip_string(c);
+        c.expect(':');
+      }
+      skip_value(c, depth + 1);
+      char n = c.peek();
+      if (n == ',') {
+        ++c.p;
+        continue;
+      }
+      if (n == close) {
+        ++c.p;
+        return;
+      }
+      c.fail("expected separator");
+    }
+  }
+  if (ch == '-' || (ch >= '0' && ch <= '9')) {
+    NumScan s;
+    const char* p = c.p;
+    if (!scan_number(p, c.end, s)) c.fail("invalid number");
+    c.p = p;
+    return;
+  }
+  parse_value(c, depth);  // literals
+}
+
+}  // namespace
+
+Json Json::parse(std::string_view text) {
+  Cursor c{text.data(), text.data() + text.size(), text.data()};
+  Json v = parse_value(c, 0);
+  c.ws();
+  if (c.p != c.end) c.fail("unexpected trailing characters");
+  return v;
+}
+
+bool parse_json_float(const char*& p, const char* end, float& out) {
+  if (fast_simple_float(p, end, out)) return true;
+  NumScan s;
+  if (!scan_number(p, end, s)) return false;
+  out = scan_to_float(s);
+  return true;
+}
+
+int parse_infer_body(std::string_view body, InferBodySink& sink) {
+  Cursor c{body.data(), body.data() + body.size(), body.data()};
+  int seen = 0;
+  c.expect('{');
+  if (c.peek() == '}') {
+    ++c.p;
+  } else {
+    while (true) {
+      std::string key = parse_string(c);
+      c.expect(':');
+      if (key == "input_data") {
+        if (c.peek() != '[') throw JsonError("[json.exception.type_error.302] type must be array, but is " +
+                                             std::string(c.peek() == '"' ? "string" : "other"));
+        ++c.p;
+        float* dst = sink.input_buffer();
+        const size_t cap = sink.input_capacity();
+        size_t n = 0;
+        c.ws();
+        if (c.p < c.end && *c.p == ']') {
+          ++c.p;
+        } else {
+          const char* p = c.p;
+          const char* end = c.end;
+          bool done = false;
+          p = bulk_float_array(p, end, dst, cap, n, done);
+          while (!done) {
+            while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+            float fv;
+            if (fast_simple_float(p, end, fv)) {
+              if (n < cap) dst[n] = fv;
+              ++n;
+              if (*p == ',') {
+                ++p;
+                continue;
+              }
+              while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+              if (p < end && *p == ',') {
+                ++p;
+                continue;
+              }
+              if (p < end && *p == ']') {
+                ++p;
+                break;
+              }
+              c.p = p;
+              c.fail("expected ',' or ']'");
+            }
+            NumScan s;
+            const char* q = p;
+            if (!scan_number(q, end, s)) {
+              c.p = p;
+              if (p < end && (*p == '"' || *p == 't' || *p == 'f' || *p == 'n' || *p == '[' || *p == '{'))
+                throw JsonError("[json.exception.type_error.302] type must be number");
+              c.fail("invalid number in input_data");
+            }
+            if (n < cap) dst[n] = scan_to_float(s);
+            ++n;
+            p = q;
+            while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+            if (p >= end) {
+              c.p = p;
+              c.fail("unexpected end of input");
+            }
+            if (*p == ',') {
+              ++p;
+              continue;
+            }
+            if (*p == ']') {
+              ++p;
+              break;
+            }
+            c.p = p;
+            c.fail("expected ',' or ']'");
+          }
+          c.p = p;
+        }
+        sink.on_input_count(n);
+        seen |= 2;
+      } else if (key == "request_id") {
+        if (c.peek() != '"') throw JsonError("[json.exception.type_error.302] type must be string");
+        std::string id = parse_string(c);
+        sink.on_request_id(id);
+        seen |= 1;
+      } else {
+        Json v = parse_value(c, 1);
+        sink.on_other_key(key, v);
+      }
+      char n = c.peek();
+      if (n == ',') {
+        ++c.p;
+        continue;
+      }
+      if (n == '}') {
+        ++c.p;
+        break;
+      }
+      c.fail("expected ',' or '}'");
+    }
+  }
+  c.ws();
+  if (c.p != c.end) c.fail("unexpected trailing characters");
+  return seen;
+}
+
+bool find_top_level_string(std::string_view body, std::string_view key, std::string& out) {
+  try {
+    Cursor c{body.data(), body.data() + body.size(), body.data()};
+    c.expect('{');
+    if (c.peek() == '}') return false;
+    while (true) {
+      std::string k = parse_string(c);
+      c.expect(':');
+      if (k == key) {
+        if (c.peek() != '"') return false;
+        out = parse_string(c);
+        return true;
+      }
+      skip_value(c, 1);
+      char n = c.peek();
+      if (n == ',') {
+        ++c.p;
+        continue;
+      }
+      return false;
+    }
+  } catch (const JsonError&) {
+    return false;
+  }
+}
+
+}  // namespace die

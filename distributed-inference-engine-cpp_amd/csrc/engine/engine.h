@@ -1,0 +1,124 @@
+// Engine interface: what the worker's batcher drives.
+//
+// Public surface mirrors the reference InferenceEngine (include/inference_engine.h:10-22):
+// predict, batchPredict, getInputShape, getOutputShape, getModelPath.  Shapes report dynamic dims
+// as 1 like the reference (src/inference_engine.cpp:44-51,62-68).  Beyond parity, engines take
+// batches asynchronously (`submit`) so the worker can pipeline H2D / compute / D2H across batches,
+// and they own the host staging memory the HTTP layer parses request floats into (pinned host
+// memory for the HIP engine, so the H2D copy is a DMA straight from where the JSON was decoded).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../core/json.h"
+
+namespace die {
+
+// A per-sample host buffer of input_numel floats (pinned when the engine is a GPU engine).
+struct SampleBuffer {
+  float* data = nullptr;
+  size_t capacity = 0;  // floats
+};
+
+// Pool of equally sized host buffers.  `alloc_fn` provides chunks (pinned or pageable).
+class SamplePool {
+ public:
+  using AllocFn = std::function<void*(size_t bytes)>;
+  using FreeFn = std::function<void(void*)>;
+  SamplePool(size_t floats_per_sample, AllocFn a = nullptr, FreeFn f = nullptr, size_t chunk = 64);
+  ~SamplePool();
+  SampleBuffer acquire();
+  void release(SampleBuffer b);
+  size_t allocated() const { return allocated_; }
+
+ private:
+  size_t floats_;
+  AllocFn alloc_;
+  FreeFn free_;
+  size_t chunk_;
+  std::mutex mu_;
+  std::vector<float*> free_list_;
+  std::vector<void*> chunks_;
+  size_t allocated_ = 0;
+};
+
+struct BatchItem {
+  const float* input = nullptr;  // host pointer (usually a SampleBuffer)
+  size_t len = 0;                // valid floats; engine zero-pads to input_numel
+};
+
+struct BatchResult {
+  bool ok = true;
+  std::string error;
+  const float* outputs = nullptr;  // B * output_numel floats, valid during the callback only
+  size_t output_numel = 0;
+  double wall_us = 0;    // submit -> outputs on host
+  double device_us = 0;  // forward time on the device (0 for CPU)
+};
+
+using BatchDone = std::function<void(BatchResult&)>;
+
+class Engine {
+ public:
+  virtual ~Engine() = default;
+
+  virtual std::string name() const = 0;
+  virtual const std::string& getModelPath() const = 0;
+  // Batch dim reported as 1 (reference semantics).
+  virtual std::vector<int64_t> getInputShape() const = 0;
+  virtual std::vector<int64_t> getOutputShape() const = 0;
+  size_t input_numel() const;
+  size_t output_numel() const;
+  int getShardId() const { return shard_id_; }
+
+  // Largest batch one submit() may carry.
+  virtual int max_batch() const = 0;
+  // Asynchronous batch execution.  Blocks while the engine's pipeline is full (backpressure).
+  // `done` runs on an engine thread once outputs are on the host.
+  virtual void submit(std::vector<BatchItem> items, BatchDone done) = 0;
+  // Block until a submit() would not block.
+  virtual void wait_for_slot() {}
+  // Drain everything in flight.
+  virtual void synchronize() = 0;
+
+  // Host staging allocation for request inputs.
+  virtual SamplePool& sample_pool() = 0;
+
+  // Synchronous helpers with the reference's padding rules: predict() pads or truncates to the
+  // model input (src/inference_engine.cpp:100-103); batchPredict() pads short inputs and, unlike
+  // the reference, rejects oversized ones instead of shifting later samples.
+  std::vector<float> predict(const std::vector<float>& input);
+  std::vector<std::vector<float>> batchPredict(const std::vector<std::vector<float>>& inputs);
+
+  virtual Json stats() const { return Json::object(); }
+
+ protected:
+  int shard_id_ = 0;
+};
+
+struct EngineOptions {
+  std::string device = "auto";   // auto | cpu | hip
+  int device_id = 0;             // HIP device ordinal
+  int max_batch = 32;
+  int pipeline_depth = 2;        // batches in flight (HIP)
+  bool use_graphs = true;        // hipGraph per batch bucket (HIP)
+  std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
+  int cpu_threads = 0;
+  int shard_id = 0;
+};
+
+// Factory: HIP engine when a GPU is visible and device != cpu, else the CPU executor (the
+// reference's ORT CUDA-EP -> CPU-EP fallback, src/inference_engine.cpp:21-29, made explicit).
+std::unique_ptr<Engine> create_engine(const std::string& model_path, const EngineOptions& opt);
+
+std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const EngineOptions& opt);
+// Defined in the HIP translation unit; returns nullptr (with `why` set) when no GPU is usable.
+std::unique_ptr<Engine> create_hip_engine(const std::string& model_path, const EngineOptions& opt, std::string* why);
+
+}  // namespace die

@@ -1,0 +1,193 @@
+#include "loadgen.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <thread>
+
+#include "../core/http.h"
+
+namespace die {
+
+namespace {
+
+struct Template {
+  std::string body;
+  size_t id_pos = 0, id_len = 0;  // fixed-width decimal request number
+  size_t v0_pos = 0, v1_pos = 0;  // fixed-width "0.dddd" values patched per request
+};
+
+constexpr int kIdDigits = 10;
+
+Template make_full_template(const LoadgenOptions& o, uint64_t seed) {
+  Template t;
+  std::mt19937_64 rng(seed);
+  std::string& b = t.body;
+  b.reserve(o.input_numel * (o.decimals + 3) + 64);
+  b += "{\"request_id\":\"";
+  b += o.id_prefix;
+  t.id_pos = b.size();
+  t.id_len = kIdDigits;
+  b.append(kIdDigits, '0');
+  b += "\",\"input_data\":[";
+  const int d = std::max(1, std::min(o.decimals, 8));
+  uint64_t scale = 1;
+  for (int k = 0; k < d; ++k) scale *= 10;
+  char buf[32];
+  for (size_t i = 0; i < o.input_numel; ++i) {
+    if (i) b.push_back(',');
+    if (i == 0) t.v0_pos = b.size();
+    if (i == 1) t.v1_pos = b.size();
+    const uint64_t v = rng() % scale;
+    int n = std::snprintf(buf, sizeof buf, "0.%0*llu", d, static_cast<unsigned long long>(v));
+    b.append(buf, static_cast<size_t>(n));
+  }
+  b += "]}";
+  return t;
+}
+
+void patch_digits(std::string& b, size_t pos, size_t width, uint64_t v) {
+  for (size_t k = 0; k < width; ++k) {
+    b[pos + width - 1 - k] = static_cast<char>('0' + v % 10);
+    v /= 10;
+  }
+}
+
+struct Gate {
+  std::mutex mu;
+  std::condition_variable cv;
+  int waiting = 0, total = 0, gen = 0;
+  void arrive() {
+    std::unique_lock<std::mutex> lk(mu);
+    const int g = gen;
+    if (++waiting == total) {
+      waiting = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+}  // namespace
+
+Json run_loadgen(const LoadgenOptions& o) {
+  const int C = std::max(1, o.connections);
+  std::atomic<long> next_warm{0}, next{0};
+  std::vector<std::vector<double>> lat(C);
+  std::vector<long> ok(C, 0), fail(C, 0);
+  std::vector<std::map<std::string, long>> errs(C);
+  Gate gate;
+  gate.total = C + 1;
+  std::chrono::steady_clock::time_point t0, t1;
+  const bool full = o.payload == "full";
+  const int d = std::max(1, std::min(o.decimals, 8));
+  uint64_t scale = 1;
+  for (int k = 0; k < d; ++k) scale *= 10;
+
+  std::vector<std::thread> threads;
+  for (int c = 0; c < C; ++c) {
+    threads.emplace_back([&, c] {
+      HttpClient client(o.host, o.port, std::chrono::milliseconds(o.timeout_ms), std::chrono::milliseconds(o.timeout_ms), 2);
+      Template tpl;
+      if (full) tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(c));
+      auto body_for = [&](long id) -> std::string& {
+        static thread_local std::string small;
+        const long key = o.distinct > 0 ? id % o.distinct : id;
+        if (full) {
+          patch_digits(tpl.body, tpl.id_pos, tpl.id_len, static_cast<uint64_t>(id));
+          // unique input: encode (key, connection) in the first two values
+          const uint64_t u = static_cast<uint64_t>(key) * 64 + static_cast<uint64_t>(c);
+          patch_digits(tpl.body, tpl.v0_pos + 2, static_cast<size_t>(d), u % scale);
+          patch_digits(tpl.body, tpl.v1_pos + 2, static_cast<size_t>(d), (u / scale) % scale);
+          return tpl.body;
+        }
+        const long a = key % 10;
+        small = "{\"request_id\":\"" + o.id_prefix + std::to_string(id) + "\",\"input_data\":[" +
+                std::to_string(a) + ".0," + std::to_string(a + 1) + ".0," + std::to_string(a + 2) + ".0]}";
+        return small;
+      };
+      auto one = [&](long id, bool record) {
+        std::string& body = body_for(id);
+        auto s = std::chrono::steady_clock::now();
+        std::string err;
+        auto r = client.post(o.path, body, "application/json", &err);
+        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s).count();
+        if (!record) return;
+        if (r && r->status == 200) {
+          ++ok[c];
+          lat[c].push_back(ms);
+        } else {
+          ++fail[c];
+          errs[c][r ? "HTTP " + std::to_string(r->status) : err]++;
+        }
+      };
+      while (true) {
+        long id = next_warm.fetch_add(1);
+        if (id >= o.warmup) break;
+        one(1000000000L + id, false);
+      }
+      gate.arrive();  // all warm
+      gate.arrive();  // timed start
+      while (true) {
+        long id = next.fetch_add(1);
+        if (id >= o.requests) break;
+        one(id, true);
+      }
+      gate.arrive();
+    });
+  }
+  gate.arrive();
+  t0 = std::chrono::steady_clock::now();
+  gate.arrive();
+  gate.arrive();
+  t1 = std::chrono::steady_clock::now();
+  for (auto& t : threads) t.join();
+
+  std::vector<double> all;
+  long n_ok = 0, n_fail = 0;
+  std::map<std::string, long> merged;
+  for (int c = 0; c < C; ++c) {
+    all.insert(all.end(), lat[c].begin(), lat[c].end());
+    n_ok += ok[c];
+    n_fail += fail[c];
+    for (auto& kv : errs[c]) merged[kv.first] += kv.second;
+  }
+  std::sort(all.begin(), all.end());
+  const double wall = std::chrono::duration<double>(t1 - t0).count();
+  auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, static_cast<size_t>(all.size() * p))]; };
+  double mean = 0;
+  for (double v : all) mean += v;
+  if (!all.empty()) mean /= all.size();
+  Json j = Json::object();
+  j["requests"] = static_cast<long long>(o.requests);
+  j["ok"] = static_cast<long long>(n_ok);
+  j["failed"] = static_cast<long long>(n_fail);
+  j["connections"] = C;
+  j["wall_s"] = wall;
+  j["rps"] = wall > 0 ? n_ok / wall : 0.0;
+  Json l = Json::object();
+  l["mean"] = mean;
+  l["p50"] = pct(0.50);
+  l["p90"] = pct(0.90);
+  l["p95"] = pct(0.95);
+  l["p99"] = pct(0.99);
+  l["min"] = all.empty() ? 0.0 : all.front();
+  l["max"] = all.empty() ? 0.0 : all.back();
+  j["latency_ms"] = l;
+  Json e = Json::object();
+  for (auto& kv : merged) e[kv.first] = static_cast<long long>(kv.second);
+  j["errors"] = e;
+  j["payload"] = o.payload;
+  j["body_bytes"] = static_cast<long long>(full ? make_full_template(o, 1).body.size() : 60);
+  return j;
+}
+
+}  // namespace die

@@ -1,0 +1,39 @@
+// Closed-loop HTTP load generator (C++): the reference's benchmark.py (benchmark.py:9-128) drives
+// load from Python threads, which cannot produce 150,528-float ResNet payloads fast enough to
+// measure an MI355X worker.  This generator keeps one keep-alive connection per client thread and
+// patches a pre-serialised body per request (unique request_id and unique leading input values, so
+// nothing is served from the result cache unless asked for).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../core/json.h"
+
+namespace die {
+
+struct LoadgenOptions {
+  std::string host = "127.0.0.1";
+  int port = 8000;
+  std::string path = "/infer";
+  int connections = 50;
+  long requests = 10000;
+  long warmup = 0;
+  // "ref": reference payload [a, a+1, a+2], a = id % 10 (benchmark.py:21-24)
+  // "full": `input_numel` values with `decimals` decimals, unique per request
+  std::string payload = "ref";
+  size_t input_numel = 3 * 224 * 224;
+  int decimals = 4;
+  uint64_t seed = 1234;
+  int timeout_ms = 10000;
+  std::string id_prefix = "req_";
+  // Distinct payloads cycled (0 = every request unique).  With "ref" this is always 10.
+  long distinct = 0;
+};
+
+// Runs warmup then the timed phase; returns {"ok","failed","wall_s","rps","latency_ms":{...},
+// "errors":{...}}.
+Json run_loadgen(const LoadgenOptions& opt);
+
+}  // namespace die

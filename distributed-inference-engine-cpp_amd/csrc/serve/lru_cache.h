@@ -1,0 +1,137 @@
+// Thread-safe LRU result cache.
+//
+// Same semantics as the reference (include/lru_cache.h:13-81): a recency list plus a hash map of
+// list iterators, `get` promotes, `put` overwrites-and-promotes or evicts the tail at capacity, and
+// hit/miss counters.  The worker keys it with `InputKey` instead of the raw vector<float>: the
+// reference's VectorHash samples only 3 elements (include/lru_cache.h:84-96), which turns
+// 150,528-float ResNet inputs into long collision chains, and storing the raw key costs 600 KB per
+// entry.  InputKey is (length, 128-bit hash of every float's bits); equal inputs always map to the
+// same key, and two different inputs collide with probability ~2^-128.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <list>
+#include <mutex>
+#include <optional>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace die {
+
+template <typename Key, typename Value, typename Hash = std::hash<Key>>
+class LRUCache {
+ public:
+  explicit LRUCache(size_t capacity) : capacity_(capacity) {}
+
+  std::optional<Value> get(const Key& key) {
+    std::lock_guard<std::mutex> g(mutex_);
+    auto it = map_.find(key);
+    if (it == map_.end()) {
+      misses_.fetch_add(1, std::memory_order_relaxed);
+      return std::nullopt;
+    }
+    list_.splice(list_.begin(), list_, it->second);
+    hits_.fetch_add(1, std::memory_order_relaxed);
+    return it->second->second;
+  }
+
+  void put(const Key& key, const Value& value) {
+    std::lock_guard<std::mutex> g(mutex_);
+    if (capacity_ == 0) return;
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      it->second->second = value;
+      list_.splice(list_.begin(), list_, it->second);
+      return;
+    }
+    if (list_.size() >= capacity_) {
+      map_.erase(list_.back().first);
+      list_.pop_back();
+    }
+    list_.emplace_front(key, value);
+    map_[key] = list_.begin();
+  }
+
+  void clear() {
+    std::lock_guard<std::mutex> g(mutex_);
+    map_.clear();
+    list_.clear();
+    hits_ = 0;
+    misses_ = 0;
+  }
+  size_t size() const {
+    std::lock_guard<std::mutex> g(mutex_);
+    return list_.size();
+  }
+  size_t capacity() const { return capacity_; }
+  size_t getHits() const { return hits_.load(); }
+  size_t getMisses() const { return misses_.load(); }
+  double getHitRate() const {
+    const size_t h = hits_.load(), m = misses_.load();
+    return h + m ? static_cast<double>(h) / static_cast<double>(h + m) : 0.0;
+  }
+  // Keys from most to least recently used (tests).
+  std::vector<Key> keys() const {
+    std::lock_guard<std::mutex> g(mutex_);
+    std::vector<Key> k;
+    for (auto& e : list_) k.push_back(e.first);
+    return k;
+  }
+
+ private:
+  size_t capacity_;
+  std::list<std::pair<Key, Value>> list_;
+  std::unordered_map<Key, typename std::list<std::pair<Key, Value>>::iterator, Hash> map_;
+  mutable std::mutex mutex_;
+  std::atomic<size_t> hits_{0};
+  std::atomic<size_t> misses_{0};
+};
+
+struct InputKey {
+  uint64_t len = 0;
+  uint64_t h0 = 0, h1 = 0;
+  bool operator==(const InputKey& o) const { return len == o.len && h0 == o.h0 && h1 == o.h1; }
+};
+struct InputKeyHash {
+  size_t operator()(const InputKey& k) const { return static_cast<size_t>(k.h0 ^ (k.h1 * 0x9E3779B97F4A7C15ull)); }
+};
+
+// 128-bit hash over the bit patterns of n floats (two independent multiply-mix lanes).
+inline InputKey hash_floats(const float* v, size_t n) {
+  auto mum = [](uint64_t a, uint64_t b) {
+    __uint128_t r = static_cast<__uint128_t>(a) * b;
+    return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
+  };
+  const uint64_t k0 = 0xa0761d6478bd642full, k1 = 0xe7037ed1a0b428dbull, k2 = 0x8ebc6af09c88c6e3ull,
+                 k3 = 0x589965cc75374cc3ull;
+  uint64_t a = 0x243F6A8885A308D3ull ^ n, b = 0x13198A2E03707344ull + n;
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(v);
+  size_t bytes = n * sizeof(float);
+  size_t i = 0;
+  for (; i + 16 <= bytes; i += 16) {
+    uint64_t w0, w1;
+    std::memcpy(&w0, p + i, 8);
+    std::memcpy(&w1, p + i + 8, 8);
+    a = mum(a ^ w0 ^ k0, w1 ^ k1);
+    b = mum(b ^ w1 ^ k2, w0 ^ k3) + a;
+  }
+  uint64_t t0 = 0, t1 = 0;
+  if (i < bytes) {
+    unsigned char tail[16] = {0};
+    std::memcpy(tail, p + i, bytes - i);
+    std::memcpy(&t0, tail, 8);
+    std::memcpy(&t1, tail + 8, 8);
+  }
+  a = mum(a ^ t0 ^ k1, t1 ^ k2 ^ bytes);
+  b = mum(b ^ t1 ^ k3, t0 ^ k0 ^ a);
+  InputKey key;
+  key.len = n;
+  key.h0 = mum(a, k3) ^ b;
+  key.h1 = mum(b, k1) ^ a;
+  return key;
+}
+
+}  // namespace die

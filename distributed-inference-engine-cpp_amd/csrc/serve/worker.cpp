@@ -1,0 +1,237 @@
+#include "worker.h"
+
+#include <algorithm>
+#include <iostream>
+#include <random>
+#include <thread>
+
+namespace die {
+
+namespace {
+
+struct SampleSink : InferBodySink {
+  SampleBuffer buf;
+  std::string id;
+  size_t n = 0;
+  void on_request_id(std::string_view s) override { id.assign(s); }
+  float* input_buffer() override { return buf.data; }
+  size_t input_capacity() const override { return buf.capacity; }
+  void on_input_count(size_t k) override { n = k; }
+};
+
+thread_local std::mt19937_64 tl_rng{std::random_device{}()};
+
+std::string build_response(const std::string& id, const float* out, size_t n, const std::string& node, bool cached,
+                           int64_t us) {
+  std::string s;
+  s.reserve(n * 12 + 160 + id.size());
+  s += "{\"request_id\":";
+  append_json_string(s, id);
+  s += ",\"output_data\":";
+  append_float_array(s, out, n);
+  s += ",\"node_id\":";
+  append_json_string(s, node);
+  s += cached ? ",\"cached\":true" : ",\"cached\":false";
+  s += ",\"inference_time_us\":";
+  s += std::to_string(us);
+  s += '}';
+  return s;
+}
+
+}  // namespace
+
+WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
+    : opt_(std::move(opt)), engine_(std::move(engine)), cache_(opt_.cache_capacity) {
+  if (!engine_) {
+    EngineOptions eo = opt_.engine;
+    eo.max_batch = opt_.max_batch;
+    engine_ = create_engine(opt_.model_path, eo);
+  }
+  fault_fail_rate_ = opt_.fault_fail_rate;
+  fault_latency_ms_ = opt_.fault_latency_ms;
+  Engine* eng = engine_.get();
+  auto batch_fn = [eng](std::vector<Pending>&& reqs,
+                        std::function<void(std::vector<Result>&&, std::exception_ptr)> finish) {
+    std::vector<BatchItem> items;
+    items.reserve(reqs.size());
+    for (auto& r : reqs) items.push_back(BatchItem{r.buf.data, r.len});
+    const size_t B = reqs.size();
+    eng->submit(std::move(items), [B, finish](BatchResult& br) {
+      if (!br.ok) {
+        finish({}, std::make_exception_ptr(std::runtime_error(br.error)));
+        return;
+      }
+      std::vector<Result> out(B);
+      const int64_t per = B ? static_cast<int64_t>(br.wall_us) / static_cast<int64_t>(B) : 0;
+      for (size_t i = 0; i < B; ++i) {
+        out[i].output.assign(br.outputs + i * br.output_numel, br.outputs + (i + 1) * br.output_numel);
+        out[i].inference_time_us = per;
+      }
+      finish(std::move(out), nullptr);
+    });
+  };
+  batcher_ = std::make_unique<BatchProcessor<Pending, Result>>(
+      static_cast<size_t>(std::max(1, std::min(opt_.max_batch, engine_->max_batch()))), opt_.batch_timeout, batch_fn,
+      [eng] { eng->wait_for_slot(); }, opt_.policy);
+  batcher_->start();
+
+  server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) { handle_infer(req, res); });
+  server_.route("GET", "/health", [this](HttpRequest&, Responder res) {
+    HttpResponse r;
+    r.body = getHealth().dump();
+    res.send(std::move(r));
+  });
+  server_.route("POST", "/admin/fault", [this](HttpRequest& req, Responder res) { handle_admin_fault(req, res); });
+  started_ = std::chrono::steady_clock::now();
+}
+
+WorkerNode::~WorkerNode() { stop(); }
+
+int WorkerNode::start() { return server_.start(opt_.host, opt_.port, opt_.http_threads); }
+void WorkerNode::wait() { server_.wait(); }
+
+void WorkerNode::stop() {
+  server_.stop();
+  if (batcher_) batcher_->stop();
+  if (engine_) engine_->synchronize();
+}
+
+HttpResponse WorkerNode::error_response(int status, const std::string& msg) const {
+  HttpResponse r;
+  r.status = status;
+  Json j = Json::object();
+  j["error"] = msg;
+  r.body = j.dump();
+  return r;
+}
+
+void WorkerNode::handle_admin_fault(HttpRequest& req, Responder res) {
+  try {
+    Json j = Json::parse(req.body);
+    if (auto* v = j.find("fail_rate")) fault_fail_rate_ = v->as_double();
+    if (auto* v = j.find("latency_ms")) fault_latency_ms_ = static_cast<int>(v->as_int());
+    Json o = Json::object();
+    o["fail_rate"] = fault_fail_rate_.load();
+    o["latency_ms"] = fault_latency_ms_.load();
+    HttpResponse r;
+    r.body = o.dump();
+    res.send(std::move(r));
+  } catch (const std::exception& e) {
+    res.send(error_response(500, e.what()));
+  }
+}
+
+void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
+  total_requests_.fetch_add(1, std::memory_order_relaxed);
+  const int lat = fault_latency_ms_.load(std::memory_order_relaxed);
+  if (lat > 0) std::this_thread::sleep_for(std::chrono::milliseconds(lat));
+  const double fr = fault_fail_rate_.load(std::memory_order_relaxed);
+  if (fr > 0 && std::uniform_real_distribution<double>(0, 1)(tl_rng) < fr) {
+    errors_++;
+    res.send(error_response(500, "injected fault"));
+    return;
+  }
+
+  Engine& eng = *engine_;
+  SamplePool& pool = eng.sample_pool();
+  SampleSink sink;
+  sink.buf = pool.acquire();
+  const size_t numel = eng.input_numel();
+  sink.buf.capacity = std::min(sink.buf.capacity, numel);
+  int seen = 0;
+  try {
+    seen = parse_infer_body(req.body, sink);
+    if (!(seen & 1)) throw JsonError("key 'request_id' not found");
+    if (!(seen & 2)) throw JsonError("key 'input_data' not found");
+    if (sink.n > numel)
+      throw std::runtime_error("input_data has " + std::to_string(sink.n) + " values; model input holds " +
+                               std::to_string(numel));
+  } catch (const std::exception& e) {
+    pool.release(sink.buf);
+    errors_++;
+    res.send(error_response(500, e.what()));
+    return;
+  }
+  // Free the request body now: at ResNet size it is ~1 MB we no longer need.
+  std::string().swap(req.body);
+
+  const InputKey key = hash_floats(sink.buf.data, sink.n);
+  if (auto hit = cache_.get(key)) {
+    cache_hits_.fetch_add(1, std::memory_order_relaxed);
+    pool.release(sink.buf);
+    auto out = std::make_shared<std::vector<float>>(std::move(*hit));
+    std::string id = std::move(sink.id);
+    std::string node = opt_.node_id;
+    res.defer([out, id = std::move(id), node = std::move(node)] {
+      HttpResponse r;
+      r.body = build_response(id, out->data(), out->size(), node, true, 50);
+      return r;
+    });
+    return;
+  }
+
+  Pending p;
+  p.request_id = std::move(sink.id);
+  p.buf = sink.buf;
+  p.len = sink.n;
+  p.key = key;
+  std::string id_copy = p.request_id;
+  batcher_->submit(std::move(p), [this, res, key, buf = sink.buf, id = std::move(id_copy)](
+                                     Result* r, std::exception_ptr err) mutable {
+    engine_->sample_pool().release(buf);
+    if (err) {
+      errors_++;
+      std::string msg = "inference failed";
+      try {
+        std::rethrow_exception(err);
+      } catch (const std::exception& e) {
+        msg = e.what();
+      } catch (...) {
+      }
+      res.send(error_response(500, msg));
+      return;
+    }
+    cache_.put(key, r->output);
+    auto out = std::make_shared<std::vector<float>>(std::move(r->output));
+    const int64_t us = r->inference_time_us;
+    std::string node = opt_.node_id;
+    res.defer([out, id = std::move(id), node = std::move(node), us] {
+      HttpResponse resp;
+      resp.body = build_response(id, out->data(), out->size(), node, false, us);
+      return resp;
+    });
+  });
+}
+
+Json WorkerNode::getHealth() const {
+  auto m = batcher_->getMetrics();
+  Json h = Json::object();
+  h["healthy"] = true;
+  h["node_id"] = opt_.node_id;
+  h["total_requests"] = static_cast<long long>(total_requests_.load());
+  h["cache_hits"] = static_cast<long long>(cache_hits_.load());
+  h["cache_size"] = static_cast<long long>(cache_.size());
+  h["cache_hit_rate"] = cache_.getHitRate();
+  Json b = Json::object();
+  b["total_batches"] = static_cast<long long>(m.total_batches);
+  b["avg_batch_size"] = m.avg_batch_size;
+  b["timeout_batches"] = static_cast<long long>(m.timeout_batches);
+  b["full_batches"] = static_cast<long long>(m.full_batches);
+  b["total_requests"] = static_cast<long long>(m.total_requests);
+  b["queue_depth"] = static_cast<long long>(batcher_->queue_depth());
+  h["batch_processor"] = b;
+  // extras (superset of the reference keys)
+  h["errors"] = static_cast<long long>(errors_.load());
+  h["engine"] = engine_->stats();
+  h["engine"]["name"] = engine_->name();
+  Json ins = Json::array();
+  for (auto d : engine_->getInputShape()) ins.push_back(static_cast<long long>(d));
+  Json outs = Json::array();
+  for (auto d : engine_->getOutputShape()) outs.push_back(static_cast<long long>(d));
+  h["input_shape"] = ins;
+  h["output_shape"] = outs;
+  h["uptime_s"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count();
+  return h;
+}
+
+}  // namespace die

@@ -1,0 +1,87 @@
+// Worker node: HTTP /infer + /health in front of an LRU cache, a dynamic batcher and an Engine.
+//
+// Reference: WorkerNode (src/worker_node.cpp:27-143) and its main (:145-204).  Same routes, JSON
+// keys, status codes, cache-hit constants (`cached:true`, `inference_time_us:50`) and miss timing
+// (batch wall time / batch size).  Differences: async request handling (no HTTP thread blocked per
+// request), floats decoded straight into engine-owned (pinned) staging, full-input cache keys,
+// oversized inputs rejected with 500 instead of corrupting the batch, optional fault
+// injection for resilience tests.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../core/http.h"
+#include "../core/json.h"
+#include "../engine/engine.h"
+#include "batcher.h"
+#include "lru_cache.h"
+
+namespace die {
+
+struct WorkerOptions {
+  std::string node_id = "worker";
+  std::string host = "0.0.0.0";
+  int port = 8001;
+  std::string model_path;
+  size_t cache_capacity = 1000;                          // src/worker_node.cpp:33
+  int max_batch = 32;                                    // :35
+  std::chrono::milliseconds batch_timeout{20};           // :36
+  BatchPolicy policy = BatchPolicy::GREEDY;
+  int http_threads = 0;
+  EngineOptions engine;
+  // fault injection (tests / fault drills)
+  double fault_fail_rate = 0.0;
+  int fault_latency_ms = 0;
+  bool verbose = false;
+};
+
+class WorkerNode {
+ public:
+  // Takes ownership of an engine (tests inject custom engines); nullptr = create from options.
+  explicit WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine = nullptr);
+  ~WorkerNode();
+
+  int start();  // returns bound port (or -1)
+  void wait();
+  void stop();
+  int port() const { return server_.port(); }
+
+  Json getHealth() const;
+  Engine& engine() { return *engine_; }
+  const WorkerOptions& options() const { return opt_; }
+
+  struct Pending {
+    std::string request_id;
+    SampleBuffer buf;
+    size_t len = 0;
+    InputKey key;
+  };
+  struct Result {
+    std::vector<float> output;
+    int64_t inference_time_us = 0;
+  };
+
+ private:
+  void handle_infer(HttpRequest& req, Responder res);
+  void handle_admin_fault(HttpRequest& req, Responder res);
+  HttpResponse error_response(int status, const std::string& msg) const;
+
+  WorkerOptions opt_;
+  std::unique_ptr<Engine> engine_;
+  LRUCache<InputKey, std::vector<float>, InputKeyHash> cache_;
+  std::unique_ptr<BatchProcessor<Pending, Result>> batcher_;
+  HttpServer server_;
+  std::atomic<int64_t> total_requests_{0};
+  std::atomic<int64_t> cache_hits_{0};
+  std::atomic<int64_t> errors_{0};
+  std::atomic<double> fault_fail_rate_{0.0};
+  std::atomic<int> fault_latency_ms_{0};
+  std::chrono::steady_clock::time_point started_;
+};
+
+}  // namespace die

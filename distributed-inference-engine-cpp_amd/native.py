@@ -1,0 +1,378 @@
+"""ctypes bindings to the native runtime (`lib/libdie.so`, built by `make` / `__graft_entry__.build`).
+
+Everything performance-relevant runs in C++/HIP; Python only configures and observes it.  Objects
+wrap opaque handles; options travel as JSON.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import LIB_DIR
+
+_LIB: Optional[C.CDLL] = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return os.path.join(LIB_DIR, "libdie.so")
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise NativeError("native library missing: %s (run `make -j8` or __graft_entry__.build())" % path)
+        L = C.CDLL(path)
+        vp, cp, i64p, f32p = C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_float)
+        errp = C.POINTER(C.c_void_p)
+
+        def sig(name, res, *args):
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = list(args)
+
+        sig("die_free", None, vp)
+        sig("die_version", cp)
+        sig("die_json_roundtrip", vp, cp, errp)
+        sig("die_parse_infer", C.c_long, cp, C.c_long, f32p, C.c_long, errp, errp)
+        sig("die_format_floats", vp, f32p, C.c_long)
+        sig("die_fnv1a", C.c_uint32, cp)
+        sig("die_ring_create", vp, C.c_int)
+        sig("die_ring_destroy", None, vp)
+        sig("die_ring_add", None, vp, cp)
+        sig("die_ring_remove", None, vp, cp)
+        sig("die_ring_get", vp, vp, cp)
+        sig("die_ring_nodes", vp, vp)
+        sig("die_ring_size", C.c_long, vp)
+        sig("die_breaker_create", vp, C.c_int, C.c_int, C.c_long)
+        sig("die_breaker_destroy", None, vp)
+        sig("die_breaker_advance", None, vp, C.c_long)
+        sig("die_breaker_allow", C.c_int, vp)
+        sig("die_breaker_success", None, vp)
+        sig("die_breaker_failure", None, vp)
+        sig("die_breaker_state", vp, vp)
+        sig("die_cache_create", vp, C.c_long)
+        sig("die_cache_destroy", None, vp)
+        sig("die_cache_put", None, vp, f32p, C.c_long, f32p, C.c_long)
+        sig("die_cache_get", C.c_long, vp, f32p, C.c_long, f32p, C.c_long)
+        sig("die_cache_stats", vp, vp)
+        sig("die_batcher_create", vp, C.c_int, C.c_int, C.c_int, C.c_int)
+        sig("die_batcher_process", C.c_int, vp, C.c_int, errp)
+        sig("die_batcher_metrics", vp, vp)
+        sig("die_batcher_stop", None, vp)
+        sig("die_batcher_destroy", None, vp)
+        sig("die_engine_create", vp, cp, cp, errp)
+        sig("die_engine_destroy", None, vp)
+        sig("die_engine_info", vp, vp)
+        sig("die_engine_run", C.c_int, vp, f32p, C.c_long, C.c_long, f32p, errp)
+        sig("die_cpu_run", vp, cp, f32p, i64p, C.c_int, i64p, C.POINTER(C.c_int), errp)
+        sig("die_onnx_summary", vp, cp, errp)
+        sig("die_worker_create", vp, cp, errp)
+        sig("die_worker_port", C.c_int, vp)
+        sig("die_worker_health", vp, vp)
+        sig("die_worker_stop", None, vp)
+        sig("die_worker_destroy", None, vp)
+        sig("die_gateway_create", vp, cp, errp)
+        sig("die_gateway_port", C.c_int, vp)
+        sig("die_gateway_stats", vp, vp)
+        sig("die_gateway_stop", None, vp)
+        sig("die_gateway_destroy", None, vp)
+        sig("die_loadgen_run", vp, cp, errp)
+        _LIB = L
+    return _LIB
+
+
+def _take_str(p) -> str:
+    if not p:
+        return ""
+    s = C.cast(p, C.c_char_p).value.decode("utf-8", "replace")
+    lib().die_free(p)
+    return s
+
+
+def _err_box():
+    return C.c_void_p(None)
+
+
+def _raise_if(err, what: str):
+    if err.value:
+        raise NativeError("%s: %s" % (what, _take_str(err.value)))
+    raise NativeError(what)
+
+
+def _f32(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+# ---- JSON / parsing -------------------------------------------------------------------------------
+
+def json_roundtrip(text: str) -> str:
+    err = _err_box()
+    p = lib().die_json_roundtrip(text.encode(), C.byref(err))
+    if not p:
+        _raise_if(err, "json")
+    return _take_str(p)
+
+
+def parse_infer(body: bytes, cap: int) -> Tuple[str, np.ndarray, int]:
+    out = np.zeros(cap, np.float32)
+    err, idp = _err_box(), C.c_void_p(None)
+    n = lib().die_parse_infer(body, len(body), _f32(out), cap, C.byref(idp), C.byref(err))
+    if n < 0:
+        _raise_if(err, "parse_infer")
+    return _take_str(idp.value), out[: min(n, cap)], n
+
+
+def format_floats(v: np.ndarray) -> str:
+    v = np.ascontiguousarray(v, np.float32)
+    return _take_str(lib().die_format_floats(_f32(v), v.size))
+
+
+# ---- control plane ------------------------------------------------------------------------------
+
+def fnv1a(s: str) -> int:
+    return lib().die_fnv1a(s.encode())
+
+
+class Ring:
+    def __init__(self, vnodes: int = 150):
+        self.h = lib().die_ring_create(vnodes)
+
+    def add(self, n: str):
+        lib().die_ring_add(self.h, n.encode())
+
+    def remove(self, n: str):
+        lib().die_ring_remove(self.h, n.encode())
+
+    def get(self, k: str) -> str:
+        return _take_str(lib().die_ring_get(self.h, k.encode()))
+
+    def nodes(self) -> List[str]:
+        return json.loads(_take_str(lib().die_ring_nodes(self.h)))
+
+    def __len__(self):
+        return lib().die_ring_size(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().die_ring_destroy(self.h)
+            self.h = None
+
+
+class Breaker:
+    """Circuit breaker driven by a fake clock (advance(ms))."""
+
+    def __init__(self, failure_threshold=5, success_threshold=2, timeout_ms=30000):
+        self.h = lib().die_breaker_create(failure_threshold, success_threshold, timeout_ms)
+
+    def allow(self) -> bool:
+        return bool(lib().die_breaker_allow(self.h))
+
+    def success(self):
+        lib().die_breaker_success(self.h)
+
+    def failure(self):
+        lib().die_breaker_failure(self.h)
+
+    def advance(self, ms: int):
+        lib().die_breaker_advance(self.h, ms)
+
+    def state(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_breaker_state(self.h)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().die_breaker_destroy(self.h)
+            self.h = None
+
+
+class Cache:
+    def __init__(self, capacity: int):
+        self.h = lib().die_cache_create(capacity)
+
+    def put(self, key: np.ndarray, value: np.ndarray):
+        k = np.ascontiguousarray(key, np.float32)
+        v = np.ascontiguousarray(value, np.float32)
+        lib().die_cache_put(self.h, _f32(k), k.size, _f32(v), v.size)
+
+    def get(self, key: np.ndarray, cap: int = 4096) -> Optional[np.ndarray]:
+        k = np.ascontiguousarray(key, np.float32)
+        out = np.zeros(cap, np.float32)
+        n = lib().die_cache_get(self.h, _f32(k), k.size, _f32(out), cap)
+        return None if n < 0 else out[:n]
+
+    def stats(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_cache_stats(self.h)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().die_cache_destroy(self.h)
+            self.h = None
+
+
+class TestBatcher:
+    """BatchProcessor<int,int> doubling each request (unit tests)."""
+
+    def __init__(self, max_batch: int, timeout_ms: int, deadline: bool = False, delay_ms: int = 0):
+        self.h = lib().die_batcher_create(max_batch, timeout_ms, int(deadline), delay_ms)
+
+    def process(self, v: int) -> int:
+        err = _err_box()
+        r = lib().die_batcher_process(self.h, v, C.byref(err))
+        if err.value:
+            raise NativeError(_take_str(err.value))
+        return r
+
+    def metrics(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_batcher_metrics(self.h)))
+
+    def stop(self):
+        lib().die_batcher_stop(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().die_batcher_destroy(self.h)
+            self.h = None
+
+
+# ---- engines ----------------------------------------------------------------------------------------
+
+class Engine:
+    def __init__(self, model_path: str, **opts):
+        err = _err_box()
+        self.h = lib().die_engine_create(model_path.encode(), json.dumps(opts).encode(), C.byref(err))
+        if not self.h:
+            _raise_if(err, "engine")
+        self.info = json.loads(_take_str(lib().die_engine_info(self.h)))
+
+    def refresh_info(self) -> Dict[str, Any]:
+        self.info = json.loads(_take_str(lib().die_engine_info(self.h)))
+        return self.info
+
+    @property
+    def input_numel(self) -> int:
+        return int(np.prod(self.info["input_shape"]))
+
+    @property
+    def output_numel(self) -> int:
+        return int(np.prod(self.info["output_shape"]))
+
+    def run(self, x: np.ndarray) -> np.ndarray:
+        """x: [B, L] (L <= input numel, zero-padded) -> [B, output numel]."""
+        x = np.ascontiguousarray(x, np.float32)
+        B = x.shape[0]
+        L = int(np.prod(x.shape[1:]))
+        out = np.zeros((B, self.output_numel), np.float32)
+        err = _err_box()
+        if lib().die_engine_run(self.h, _f32(x), B, L, _f32(out), C.byref(err)) != 0:
+            _raise_if(err, "engine run")
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().die_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def cpu_run(model_path: str, x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    shape = (C.c_int64 * x.ndim)(*x.shape)
+    out_shape = (C.c_int64 * 8)()
+    out_rank = C.c_int(0)
+    err = _err_box()
+    p = lib().die_cpu_run(model_path.encode(), _f32(x), shape, x.ndim, out_shape, C.byref(out_rank), C.byref(err))
+    if not p:
+        _raise_if(err, "cpu_run")
+    shp = tuple(out_shape[i] for i in range(out_rank.value))
+    arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(int(np.prod(shp)),)).copy()
+    lib().die_free(p)
+    return arr.reshape(shp)
+
+
+def onnx_summary(model_path: str) -> Dict[str, Any]:
+    err = _err_box()
+    p = lib().die_onnx_summary(model_path.encode(), C.byref(err))
+    if not p:
+        _raise_if(err, "onnx_summary")
+    return json.loads(_take_str(p))
+
+
+# ---- servers ------------------------------------------------------------------------------------------
+
+class Worker:
+    """In-process worker node (HTTP on 127.0.0.1:<port>, port 0 = ephemeral)."""
+
+    def __init__(self, model_path: str, node_id: str = "w1", port: int = 0, **opts):
+        o = dict(opts)
+        o.update(model_path=model_path, node_id=node_id, port=port)
+        err = _err_box()
+        self.h = lib().die_worker_create(json.dumps(o).encode(), C.byref(err))
+        if not self.h:
+            _raise_if(err, "worker")
+        self.port = lib().die_worker_port(self.h)
+        self.url = "http://127.0.0.1:%d" % self.port
+
+    def health(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_worker_health(self.h)))
+
+    def stop(self):
+        if getattr(self, "h", None):
+            lib().die_worker_stop(self.h)
+            lib().die_worker_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass
+
+
+class GatewayServer:
+    def __init__(self, workers: Sequence[str], port: int = 0, **opts):
+        o = dict(opts)
+        o.update(workers=list(workers), port=port)
+        err = _err_box()
+        self.h = lib().die_gateway_create(json.dumps(o).encode(), C.byref(err))
+        if not self.h:
+            _raise_if(err, "gateway")
+        self.port = lib().die_gateway_port(self.h)
+        self.url = "http://127.0.0.1:%d" % self.port
+
+    def stats(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_gateway_stats(self.h)))
+
+    def stop(self):
+        if getattr(self, "h", None):
+            lib().die_gateway_stop(self.h)
+            lib().die_gateway_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass
+
+
+def loadgen(**opts) -> Dict[str, Any]:
+    err = _err_box()
+    p = lib().die_loadgen_run(json.dumps(opts).encode(), C.byref(err))
+    if not p:
+        _raise_if(err, "loadgen")
+    return json.loads(_take_str(p))
