@@ -1,0 +1,155 @@
+"""Headline benchmark: requests/sec (+ p50/p99 latency) of ResNet50-v2 `/infer` on MI355X.
+
+Reference headline (README.md:276-289): 522.64 req/s, p50 84.6 ms at 10k requests /
+50 client threads through HTTP/JSON.  Here every rank runs the full serving path on its own GPU:
+an in-process worker node (C++ epoll HTTP server, JSON decode straight into pinned staging, LRU
+cache, dynamic batcher at max batch 32, HIP engine with hipGraph-captured forward) driven by a
+C++ closed-loop client with 50 keep-alive connections per GPU.  Payloads are ResNet-shaped
+(3x224x224 floats, 4 decimals, ~1.1 MB of JSON) and unique per request, so every request is a real
+inference (no cache hits).  Weights are random-init (no checkpoint offline).
+
+A "step" = one batch worth (32) of requests per GPU.  W warmup steps, then exactly K timed steps
+bracketed by barrier + torch.cuda.synchronize(); the max wall time over ranks is the job time and
+`value` = total successful requests / that time (whole job, all GPUs).
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_RPS = 522.64  # BASELINE.md / README.md:282
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--connections", type=int, default=50, help="client connections per GPU (reference: 50 threads)")
+    ap.add_argument("--mode", choices=["http", "engine"], default="http")
+    ap.add_argument("--model", default="")
+    ap.add_argument("--pipeline-depth", type=int, default=2)
+    args = ap.parse_args()
+
+    import torch  # first: one HIP runtime per process (see native.lib)
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    import die_amd  # noqa: F401
+    from die_amd import native
+    from die_amd.models import resnet_v2 as r
+
+    cfg = r.ResNetConfig()
+    model = args.model
+    tmpdir = None
+    if not model:
+        tmpdir = tempfile.mkdtemp(prefix="die_bench_%d_" % rank)
+        model = os.path.join(tmpdir, "resnet50-v2-7.onnx")
+        blob, _ = r.build_onnx(cfg)
+        with open(model, "wb") as f:
+            f.write(blob)
+    torch.cuda.set_device(local_rank)
+    B = args.batch
+    numel = cfg.in_ch * cfg.image * cfg.image
+    extra = {}
+
+    if args.mode == "http":
+        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
+                           engine={"device": "hip", "device_id": local_rank, "max_batch": B,
+                                   "pipeline_depth": args.pipeline_depth})
+        lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
+                  seed=1000 + rank, timeout_ms=60000)
+        native.loadgen(requests=args.warmup * B, warmup=0, id_prefix="warm%d_" % rank, **lg)
+        h0 = wk.health()
+        barrier()
+        t0 = time.perf_counter()
+        res = native.loadgen(requests=args.steps * B, warmup=0, id_prefix="r%d_" % rank, **lg)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        h1 = wk.health()
+        ok = res["ok"]
+        failed = res["failed"]
+        bp0, bp1 = h0["batch_processor"], h1["batch_processor"]
+        nb = bp1["total_batches"] - bp0["total_batches"]
+        e0, e1 = h0["engine"], h1["engine"]
+        extra = {
+            "p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
+            "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+            "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
+            "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
+            "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
+        }
+        wk.stop()
+    else:
+        import numpy as np
+
+        eng = native.Engine(model, device="hip", device_id=local_rank, max_batch=B,
+                            pipeline_depth=args.pipeline_depth)
+        x = r.synthetic_input(B, cfg, seed=rank).reshape(B, -1)
+        for _ in range(args.warmup):
+            eng.run(x)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.run(x)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        ok, failed = args.steps * B, 0
+        extra = {"engine": eng.refresh_info()["name"], "device_ms_per_batch": eng.info.get("avg_device_ms")}
+        eng.close()
+
+    if dist is not None:
+        t = torch.tensor([elapsed, float(ok), float(failed)], dtype=torch.float64)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, ok, failed = mx[0].item(), t[1].item(), t[2].item()
+        lat = torch.tensor([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], dtype=torch.float64)
+        dist.all_reduce(lat, op=dist.ReduceOp.MAX)
+        extra["p50_ms"], extra["p99_ms"] = lat[0].item(), lat[1].item()
+    value = ok / elapsed
+    if rank == 0:
+        out = {
+            "metric": "requests/sec + p50/p99 latency, ResNet50 ONNX /infer at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "requests/s",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1000.0 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / BASELINE_RPS,
+            "dtype": "bf16",
+            "data": "synthetic: unique ResNet-shaped JSON payloads (3x224x224 floats, 4 decimals), random-init weights",
+            "config": {"model": "ResNet50-v2-7 (ONNX, generated)", "global_batch": B * args.gpus, "seq_len": 0,
+                       "parallelism": "dp%d" % args.gpus, "mode": args.mode, "max_batch_per_gpu": B,
+                       "requests": int(ok + failed)},
+        }
+        out.update({k: v for k, v in extra.items() if v is not None})
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+// C ABI for launching individual HIP kernels on caller-provided device pointers (numerics tests
+// compare them with torch on the GPU box).  Pointers/streams travel as uint64 (torch data_ptr()
+// and torch.cuda.current_stream().cuda_stream).
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../core/json.h"
+#include "../engine/hip_plan.h"
+#include "../kernels/kernels.h"
+#include "../onnx/onnx_model.h"
+
+using namespace die;
+
+namespace {
+template <typename T>
+T* P(uint64_t v) {
+  return reinterpret_cast<T*>(static_cast<uintptr_t>(v));
+}
+hipStream_t S(uint64_t v) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(v)); }
+int geti(const Json& j, const char* k, int d) {
+  auto* v = j.find(k);
+  return v ? static_cast<int>(v->as_int()) : d;
+}
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.data(), s.size() + 1);
+  return p;
+}
+}  // namespace
+
+extern "C" {
+
+// geometry JSON: B,H,W,Cin,Ho,Wo,N,KH,KW,stride,pad_h,pad_w,dil,K,Kpad,relu,relu2
+int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint64_t res, uint64_t out,
+                  uint64_t out_f32, uint64_t scale2, uint64_t shift2, uint64_t out2, int tile, uint64_t stream) {
+  try {
+    Json j = Json::parse(geom);
+    kern::ConvArgs a;
+    a.B = geti(j, "B", 1);
+    a.H = geti(j, "H", 1);
+    a.W = geti(j, "W", 1);
+    a.Cin = geti(j, "Cin", 1);
+    a.Ho = geti(j, "Ho", 1);
+    a.Wo = geti(j, "Wo", 1);
+    a.N = geti(j, "N", 1);
+    a.KH = geti(j, "KH", 1);
+    a.KW = geti(j, "KW", 1);
+    a.stride = geti(j, "stride", 1);
+    a.pad_h = geti(j, "pad_h", 0);
+    a.pad_w = geti(j, "pad_w", 0);
+    a.dil = geti(j, "dil", 1);
+    a.K = geti(j, "K", a.KH * a.KW * a.Cin);
+    a.Kpad = geti(j, "Kpad", (a.K + 63) / 64 * 64);
+    a.M = a.B * a.Ho * a.Wo;
+    a.relu = geti(j, "relu", 0);
+    a.relu2 = geti(j, "relu2", 0);
+    a.x = P<const uint16_t>(x);
+    a.w = P<const uint16_t>(w);
+    a.bias = P<const float>(bias);
+    a.res = P<const uint16_t>(res);
+    a.out = P<uint16_t>(out);
+    a.out_f32 = P<float>(out_f32);
+    a.scale2 = P<const float>(scale2);
+    a.shift2 = P<const float>(shift2);
+    a.out2 = P<uint16_t>(out2);
+    if (tile < 0) tile = kern::choose_tile(a.M, a.N, a.K);
+    return static_cast<int>(kern::conv_igemm(a, tile, S(stream)));
+  } catch (...) {
+    return -1;
+  }
+}
+
+int die_kern_input_prep(uint64_t x, uint64_t scale, uint64_t shift, uint64_t out, int B, int C, int H, int W, int Cp,
+                        uint64_t stream) {
+  return static_cast<int>(
+      kern::input_prep(P<const float>(x), P<const float>(scale), P<const float>(shift), P<uint16_t>(out), B, C, H, W, Cp, S(stream)));
+}
+
+int die_kern_pool2d(uint64_t x, uint64_t y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                    int ph, int pw, int is_max, int cip, uint64_t stream) {
+  return static_cast<int>(kern::pool2d(P<const uint16_t>(x), P<uint16_t>(y), B, H, W, C, Ho, Wo, kh, kw, sh, sw, ph,
+                                       pw, is_max, cip, S(stream)));
+}
+
+int die_kern_gap(uint64_t x, uint64_t out, uint64_t out_f32, uint64_t scale, uint64_t shift, int relu, int B, int HW,
+                 int C, uint64_t stream) {
+  return static_cast<int>(kern::global_avgpool(P<const uint16_t>(x), P<uint16_t>(out), P<float>(out_f32),
+                                               P<const float>(scale), P<const float>(shift), relu, B, HW, C, S(stream)));
+}
+
+int die_kern_affine(uint64_t x, uint64_t z, uint64_t scale, uint64_t shift, int act, uint64_t y, long long M, int C,
+                    uint64_t stream) {
+  return static_cast<int>(kern::affine_act(P<const uint16_t>(x), P<const uint16_t>(z), P<const float>(scale),
+                                           P<const float>(shift), act, P<uint16_t>(y), M, C, S(stream)));
+}
+
+int die_kern_nhwc_to_nchw(uint64_t x, uint64_t y, int B, int H, int W, int C, uint64_t stream) {
+  return static_cast<int>(kern::nhwc_to_nchw_f32(P<const uint16_t>(x), P<float>(y), B, H, W, C, S(stream)));
+}
+
+// Plan summary of a model (op list with fused epilogues), for tests and docs.
+char* die_plan_summary(const char* model_path, int max_batch, char** err) {
+  try {
+    Plan p = build_plan(onnx::load_onnx(model_path), max_batch);
+    Json j = Json::object();
+    j["summary"] = p.summary();
+    j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
+    j["param_bytes"] = static_cast<long long>(p.params.size());
+    j["gflop_per_sample"] = p.flops_per_sample / 1e9;
+    Json ops = Json::array();
+    for (auto& o : p.ops) {
+      Json e = Json::object();
+      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32"};
+      e["kind"] = kinds[o.kind];
+      e["name"] = o.name;
+      if (o.kind == PlanOp::CONV) {
+        e["N"] = o.conv.N;
+        e["K"] = o.conv.K;
+        e["KH"] = o.conv.KH;
+        e["stride"] = o.conv.stride;
+        e["relu"] = o.conv.relu;
+        e["residual"] = o.in2 >= 0;
+        e["dual_store"] = o.out2 >= 0;
+        e["store_main"] = o.out >= 0 || o.out_f32 != -1;
+        e["relu2"] = o.conv.relu2;
+      }
+      ops.push_back(e);
+    }
+    j["ops"] = ops;
+    Json in = Json::array(), out = Json::array();
+    for (auto d : p.input_shape) in.push_back(static_cast<long long>(d));
+    for (auto d : p.output_shape) out.push_back(static_cast<long long>(d));
+    j["input_shape"] = in;
+    j["output_shape"] = out;
+    return dup(j.dump());
+  } catch (const std::exception& e) {
+    if (err) *err = dup(e.what());
+    return nullptr;
+  }
+}
+
+}  // extern "C"

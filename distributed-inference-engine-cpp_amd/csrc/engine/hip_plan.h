@@ -1,0 +1,66 @@
+// Lowering of an ONNX graph to a fused, NHWC/bf16 device program for gfx950.
+//
+// Passes (one walk over the topologically sorted nodes, with lookahead):
+//  * BatchNormalization directly on the graph input -> folded into the input-prep kernel that also
+//    converts NCHW fp32 -> NHWC bf16 (it cannot be folded into the stem weights exactly, because the
+//    stem's zero padding is applied after the BN);
+//  * Conv -> BatchNormalization -> Relu  -> one conv with folded weights/bias and ReLU epilogue;
+//  * Conv -> Add(other) [-> Relu]        -> residual epilogue (other operand already computed);
+//  * value -> BatchNormalization [-> Relu] consumed next to the value itself (pre-activation units)
+//    -> the producing conv's second output (dual store), so ResNet-v2 has no standalone BN/ReLU/Add;
+//  * Gemm / MatMul(2-D initializer) -> the same MFMA kernel as a 1x1 conv over rows;
+//  * GlobalAveragePool / MaxPool / AveragePool -> NHWC kernels; Flatten of 1x1 maps -> view.
+// Anything else falls back to standalone affine/add/relu kernels, or is rejected with a clear
+// error (the CPU executor still runs such models).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.h"
+#include "../onnx/onnx_model.h"
+
+namespace die {
+
+struct PlanBuf {
+  size_t bytes_per_sample = 0;  // scaled by the batch size at allocation time
+  size_t offset = 0;            // arena offset (max batch), assigned by the planner
+  int first_use = -1, last_use = -1;
+};
+
+struct PlanOp {
+  enum Kind { INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32 } kind;
+  std::string name;
+  // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
+  int in = -1, in2 = -1, out = -1, out2 = -1, out_f32 = -1;
+  // parameter offsets (bytes) into the device parameter blob
+  size_t w_off = 0, bias_off = SIZE_MAX, s2_off = SIZE_MAX, b2_off = SIZE_MAX, scale_off = SIZE_MAX,
+         shift_off = SIZE_MAX;
+  // conv geometry (per sample; ConvArgs B/M are set at launch)
+  kern::ConvArgs conv;
+  int tile_bmax = 0;
+  // generic geometry
+  int C = 0, H = 0, W = 0, Ho = 0, Wo = 0, Cp = 0;
+  int kh = 0, kw = 0, sh = 1, sw = 1, ph = 0, pw = 0, is_max = 0, cip = 0, act = 0;
+  long long rows_per_sample = 0;  // AFFINE: rows of C per sample
+  double flops_per_sample = 0;
+};
+
+struct Plan {
+  std::vector<PlanOp> ops;
+  std::vector<PlanBuf> bufs;
+  std::vector<uint8_t> params;  // host copy of the packed device parameters
+  size_t arena_bytes_per_sample = 0;  // sum of per-sample sizes at the chosen offsets (scaled by Bmax)
+  size_t arena_bytes = 0;             // for max_batch
+  std::vector<int64_t> input_shape;   // [1, C, H, W]
+  std::vector<int64_t> output_shape;  // [1, ...]
+  size_t input_numel = 0, output_numel = 0;
+  double flops_per_sample = 0;
+  std::string summary() const;
+};
+
+// Build the plan for batches up to max_batch.  Throws on unsupported graphs.
+Plan build_plan(const onnx::Model& m, int max_batch);
+
+}  // namespace die

@@ -1,0 +1,65 @@
+// Host-side launch API of the hand-written gfx950 kernels.  Every launcher is asynchronous on the
+// given stream and capture-safe (no allocation, no synchronisation), so the engine can record a
+// whole forward pass into a hipGraph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace die {
+namespace kern {
+
+// Implicit-GEMM convolution / GEMM on MFMA (bf16 in, f32 accumulate), NHWC activations.
+//   out[m, n] = epilogue( sum_k X[m, k] * W[n, k] )      m = (b, oh, ow), k = (ky, kx, ci)
+// W is [Npad][Kpad] bf16 (K contiguous, zero padded to the tile multiples).
+// Epilogue (all optional): + bias[n]; + res[m, n]; relu; store out (bf16) or out_f32 (f32);
+//   second output out2 = act2(v * scale2[n] + shift2[n])  (pre-activation BN of the next unit).
+struct ConvArgs {
+  const uint16_t* x = nullptr;
+  const uint16_t* w = nullptr;
+  int B = 1, H = 1, W = 1, Cin = 1;       // input NHWC (Cin = storage channels)
+  int Ho = 1, Wo = 1, N = 1;              // output spatial and channels
+  int KH = 1, KW = 1, stride = 1, pad_h = 0, pad_w = 0, dil = 1;
+  int K = 1, Kpad = 64;                   // K = KH*KW*Cin
+  int M = 1;                              // B*Ho*Wo
+  const float* bias = nullptr;
+  const uint16_t* res = nullptr;          // [M][N] bf16
+  int relu = 0;
+  uint16_t* out = nullptr;                // [M][N] bf16
+  float* out_f32 = nullptr;               // [M][N] f32 (instead of / in addition to out)
+  const float* scale2 = nullptr;
+  const float* shift2 = nullptr;
+  int relu2 = 0;
+  uint16_t* out2 = nullptr;
+};
+
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3 };
+// BM (pixels) x BN (channels) of a config.
+void tile_dims(int cfg, int& bm, int& bn);
+// Heuristic tile choice for a problem shape.
+int choose_tile(int M, int N, int K);
+// Launch; `vec` = 8 (Cin % 8 == 0) or 4 (Cin % 4 == 0).  Returns hipSuccess or an error for an
+// unsupported configuration (checked on the host before launch).
+hipError_t conv_igemm(const ConvArgs& a, int tile_cfg, hipStream_t s);
+
+// fp32 NCHW -> (x * scale[c] + shift[c]) -> bf16 NHWC with Cp >= C channels (pad channels = 0).
+hipError_t input_prep(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
+                      int W, int Cp, hipStream_t s);
+// NHWC bf16 max / average pooling (C % 8 == 0).
+hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
+                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s);
+// [B, HW, C] bf16 -> [B, C] (mean over HW), optional y = relu(x*scale+shift) before averaging;
+// writes bf16 `out` and/or f32 `out_f32`.
+hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
+                          int relu, int B, int HW, int C, hipStream_t s);
+// Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional)
+hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
+                      uint16_t* y, long long M, int C, hipStream_t s);
+// bf16 NHWC [B,H,W,C] -> f32 NCHW [B,C,H,W]
+hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s);
+// f32 -> bf16 / bf16 -> f32 copies
+hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
+hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
+
+}  // namespace kern
+}  // namespace die

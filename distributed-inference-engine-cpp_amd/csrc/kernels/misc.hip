@@ -1,0 +1,255 @@
+// Memory-bound NHWC kernels for gfx950: input preparation, pooling, global average pooling,
+// standalone affine/activation, layout conversion.  All loads/stores are 16-byte vectors (8 bf16)
+// except where the layout forbids it; grids are capped and grid-strided.
+#include "common.h"
+#include "kernels.h"
+
+namespace die {
+namespace kern {
+
+using namespace die::k;
+
+namespace {
+
+inline int grid_for(long long work, int block = 256, int cap = 4096) {
+  long long g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  return static_cast<int>(g > cap ? cap : g);
+}
+
+// fp32 NCHW -> affine -> bf16 NHWC (Cp channels; Cp in {4, 8}), one thread per pixel.
+template <int CP>
+__global__ void input_prep_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                  const float* __restrict__ shift, uint16_t* __restrict__ out, int B, int C, int HW) {
+  const long long total = static_cast<long long>(B) * HW;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long b = i / HW;
+    const long long p = i - b * HW;
+    float v[CP];
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      if (c < C) {
+        const float xv = x[(b * C + c) * HW + p];
+        v[c] = scale ? xv * scale[c] + shift[c] : xv;
+      } else {
+        v[c] = 0.f;
+      }
+    }
+    if (CP == 4) {
+      *reinterpret_cast<uint2*>(out + i * 4) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    } else {
+      *reinterpret_cast<uint4*>(out + i * 8) =
+          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    }
+  }
+}
+
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  unpack2(q.x, v[0], v[1]);
+  unpack2(q.y, v[2], v[3]);
+  unpack2(q.z, v[4], v[5]);
+  unpack2(q.w, v[6], v[7]);
+}
+__device__ __forceinline__ void store8(uint16_t* p, const float* v) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+}
+
+// One thread per (output pixel, 8-channel group).
+__global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
+                              int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int cip) {
+  const int CG = C / 8;
+  const long long total = static_cast<long long>(B) * Ho * Wo * CG;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int cg = static_cast<int>(i % CG);
+    long long r = i / CG;
+    const int ow = static_cast<int>(r % Wo);
+    r /= Wo;
+    const int oh = static_cast<int>(r % Ho);
+    const int b = static_cast<int>(r / Ho);
+    float acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = is_max ? -INFINITY : 0.f;
+    int cnt = 0;
+    for (int ky = 0; ky < kh; ++ky) {
+      const int ih = oh * sh - ph + ky;
+      for (int kx = 0; kx < kw; ++kx) {
+        const int iw = ow * sw - pw + kx;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
+          if (cip && ih < H + ph && iw < W + pw) ++cnt;
+          continue;
+        }
+        float v[8];
+        load8(x + ((static_cast<long long>(b) * H + ih) * W + iw) * C + cg * 8, v);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = is_max ? fmaxf(acc[t], v[t]) : acc[t] + v[t];
+        ++cnt;
+      }
+    }
+    if (!is_max) {
+      const float inv = cnt ? 1.f / cnt : 0.f;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] *= inv;
+    }
+    store8(y + i * 8, acc);
+  }
+}
+
+// Grid: (C/8 groups / 64, B) blocks of 256 threads = 64 channel groups x 4 row-slices.
+__global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
+                           const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C) {
+  __shared__ float part[4][64][8];
+  const int b = blockIdx.y;
+  const int g = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int slice = threadIdx.x >> 6;
+  const int CG = C / 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float sc[8], sf[8];
+  if (g < CG) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      sc[t] = scale ? scale[g * 8 + t] : 1.f;
+      sf[t] = scale ? shift[g * 8 + t] : 0.f;
+    }
+    for (int p = slice; p < HW; p += 4) {
+      float v[8];
+      load8(x + (static_cast<long long>(b) * HW + p) * C + g * 8, v);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        float u = v[t] * sc[t] + sf[t];
+        if (relu) u = fmaxf(u, 0.f);
+        acc[t] += u;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) part[slice][threadIdx.x & 63][t] = acc[t];
+  __syncthreads();
+  if (slice == 0 && g < CG) {
+    const float inv = 1.f / HW;
+    float r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      r[t] = (part[0][threadIdx.x][t] + part[1][threadIdx.x][t] + part[2][threadIdx.x][t] + part[3][threadIdx.x][t]) * inv;
+    if (out) store8(out + static_cast<long long>(b) * C + g * 8, r);
+    if (out_f32) {
+      float4* o = reinterpret_cast<float4*>(out_f32 + static_cast<long long>(b) * C + g * 8);
+      o[0] = make_float4(r[0], r[1], r[2], r[3]);
+      o[1] = make_float4(r[4], r[5], r[6], r[7]);
+    }
+  }
+}
+
+// act: 0 none, 1 relu.  One thread per 8 elements of a row of C (C % 8 == 0).
+__global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ z,
+                                  const float* __restrict__ scale, const float* __restrict__ shift, int act,
+                                  uint16_t* __restrict__ y, long long M, int C) {
+  const int CG = C / 8;
+  const long long total = M * CG;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int c0 = static_cast<int>(i % CG) * 8;
+    float v[8];
+    load8(x + i * 8, v);
+    if (scale) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = v[t] * scale[c0 + t] + shift[c0 + t];
+    }
+    if (z) {
+      float w[8];
+      load8(z + i * 8, w);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += w[t];
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
+    store8(y + i * 8, v);
+  }
+}
+
+__global__ void nhwc_to_nchw_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int B, int HW, int C) {
+  const long long total = static_cast<long long>(B) * HW * C;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    // i indexes the OUTPUT (NCHW) so the f32 stores are coalesced.
+    const long long p = i % HW;
+    long long r = i / HW;
+    const long long c = r % C;
+    const long long b = r / C;
+    y[i] = bf2f(x[(b * HW + p) * C + c]);
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long long n) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+__global__ void bf16_to_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, long long n) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+    y[i] = bf2f(x[i]);
+}
+
+}  // namespace
+
+hipError_t input_prep(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
+                      int W, int Cp, hipStream_t s) {
+  if (C > Cp || (Cp != 4 && Cp != 8)) return hipErrorInvalidValue;
+  const long long work = static_cast<long long>(B) * H * W;
+  if (Cp == 4)
+    hipLaunchKernelGGL(input_prep_kernel<4>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W);
+  else
+    hipLaunchKernelGGL(input_prep_kernel<8>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W);
+  return hipGetLastError();
+}
+
+hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
+                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(pool2d_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, kh, kw, sh, sw,
+                     ph, pw, is_max, count_include_pad);
+  return hipGetLastError();
+}
+
+hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
+                          int relu, int B, int HW, int C, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int CG = C / 8;
+  dim3 grid((CG + 63) / 64, B);
+  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C);
+  return hipGetLastError();
+}
+
+hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
+                      uint16_t* y, long long M, int C, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(M * (C / 8))), dim3(256), 0, s, x, z, scale, shift, act, y, M,
+                     C);
+  return hipGetLastError();
+}
+
+hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s) {
+  const long long work = static_cast<long long>(B) * H * W * C;
+  hipLaunchKernelGGL(nhwc_to_nchw_f32_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H * W, C);
+  return hipGetLastError();
+}
+
+hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace die

@@ -31,6 +31,15 @@ def lib() -> C.CDLL:
         path = lib_path()
         if not os.path.exists(path):
             raise NativeError("native library missing: %s (run `make -j8` or __graft_entry__.build())" % path)
+        # torch wheels bundle their own libamdhip64.so (SONAME libamdhip64.so.7, same as /opt/rocm's).
+        # If torch is loaded first, libdie.so's NEEDED libamdhip64.so.7 resolves to torch's copy and
+        # the process has ONE HIP runtime; loading libdie.so first and torch later would map a second
+        # runtime (torch NEEDs the unversioned name).  So bring torch in first whenever it exists.
+        if os.environ.get("DIE_NO_TORCH") != "1":
+            try:
+                import torch  # noqa: F401
+            except Exception:
+                pass
         L = C.CDLL(path)
         vp, cp, i64p, f32p = C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_float)
         errp = C.POINTER(C.c_void_p)
@@ -376,3 +385,42 @@ def loadgen(**opts) -> Dict[str, Any]:
     if not p:
         _raise_if(err, "loadgen")
     return json.loads(_take_str(p))
+
+
+# ---- plan / kernels ---------------------------------------------------------------------------------
+
+def _sig_kernels():
+    L = lib()
+    if getattr(L, "_kern_sigs", False):
+        return L
+    u64, i = C.c_uint64, C.c_int
+    L.die_plan_summary.restype = C.c_void_p
+    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.die_kern_conv.restype = i
+    L.die_kern_conv.argtypes = [C.c_char_p] + [u64] * 9 + [i, u64]
+    L.die_kern_input_prep.restype = i
+    L.die_kern_input_prep.argtypes = [u64] * 4 + [i] * 5 + [u64]
+    L.die_kern_pool2d.restype = i
+    L.die_kern_pool2d.argtypes = [u64, u64] + [i] * 14 + [u64]
+    L.die_kern_gap.restype = i
+    L.die_kern_gap.argtypes = [u64] * 5 + [i] * 4 + [u64]
+    L.die_kern_affine.restype = i
+    L.die_kern_affine.argtypes = [u64] * 4 + [i, u64, C.c_longlong, i, u64]
+    L.die_kern_nhwc_to_nchw.restype = i
+    L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64]
+    L._kern_sigs = True
+    return L
+
+
+def plan_summary(model_path: str, max_batch: int = 32) -> Dict[str, Any]:
+    L = _sig_kernels()
+    err = _err_box()
+    p = L.die_plan_summary(model_path.encode(), max_batch, C.byref(err))
+    if not p:
+        _raise_if(err, "plan")
+    return json.loads(_take_str(p))
+
+
+def kernels():
+    """The raw kernel-launch entry points (see ops/kernels.py for the torch-facing wrappers)."""
+    return _sig_kernels()

@@ -1,0 +1,136 @@
+"""torch-facing wrappers around the hand-written gfx950 kernels (csrc/kernels/*.hip).
+
+Used by the GPU numerics tests: each wrapper takes torch tensors on `cuda`, launches the native
+kernel on torch's current stream through the C ABI (`capi_kernels.cpp`), and returns torch tensors.
+They fail loudly (NativeError) when the native library is missing; there is no eager fallback.
+"""
+from __future__ import annotations
+
+import json
+from typing import Optional
+
+import numpy as np
+
+from .. import native
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _stream() -> int:
+    import torch
+
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise native.NativeError("%s launch failed (hipError %d)" % (what, rc))
+
+
+def bf16_bits(t):
+    """bf16 tensor -> int16 view (the kernels take raw uint16 storage)."""
+    import torch
+
+    return t.contiguous().view(torch.int16)
+
+
+def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128):
+    """[Cout, Cin, KH, KW] float -> [Npad][Kpad] bf16 with k = (ky*KW + kx)*Cin_store + ci."""
+    import torch
+
+    cout, cin, kh, kw = w.shape
+    cs = cin_store or cin
+    K = kh * kw * cs
+    Kpad = (K + 63) // 64 * 64
+    Np = (cout + npad - 1) // npad * npad
+    wp = torch.zeros((Np, kh, kw, cs), dtype=torch.float32, device=w.device)
+    wp[:cout, :, :, :cin] = w.permute(0, 2, 3, 1).float()
+    wp = wp.reshape(Np, K)
+    out = torch.zeros((Np, Kpad), dtype=torch.bfloat16, device=w.device)
+    out[:, :K] = wp.to(torch.bfloat16)
+    return out, K, Kpad
+
+
+def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
+                scale2=None, shift2=None, relu2=False, tile=-1):
+    """Implicit-GEMM conv.  x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float.
+    Returns (out, out2) in NHWC ([B,Ho,Wo,Cout]); out is f32 if out_f32 else bf16."""
+    import torch
+
+    B, H, W, Cs = x_nhwc.shape
+    cout, cin, kh, kw = w.shape
+    wp, K, Kpad = pack_conv_weight(w, Cs)
+    Ho = (H + 2 * pad - dil * (kh - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (kw - 1) - 1) // stride + 1
+    dev = x_nhwc.device
+
+    def padded(v):
+        if v is None:
+            return None
+        n = (v.numel() + 127) // 128 * 128
+        o = torch.zeros(n, dtype=torch.float32, device=dev)
+        o[: v.numel()] = v.float()
+        return o
+
+    bias_p, s2_p, b2_p = padded(bias), padded(scale2), padded(shift2)
+    out = torch.empty((B, Ho, Wo, cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
+    out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
+    geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad, pad_w=pad,
+                dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2))
+    L = native.kernels()
+    rc = L.die_kern_conv(json.dumps(geom).encode(), _ptr(x_nhwc.contiguous()), _ptr(wp), _ptr(bias_p),
+                         _ptr(res.contiguous() if res is not None else None), 0 if out_f32 else _ptr(out),
+                         _ptr(out) if out_f32 else 0, _ptr(s2_p), _ptr(b2_p), _ptr(out2), tile, _stream())
+    _check(rc, "conv_igemm")
+    return out, out2
+
+
+def input_prep(x_nchw, scale=None, shift=None, cp=4):
+    import torch
+
+    B, C, H, W = x_nchw.shape
+    out = torch.empty((B, H, W, cp), dtype=torch.bfloat16, device=x_nchw.device)
+    L = native.kernels()
+    rc = L.die_kern_input_prep(_ptr(x_nchw.contiguous().float()), _ptr(scale), _ptr(shift), _ptr(out), B, C, H, W, cp,
+                               _stream())
+    _check(rc, "input_prep")
+    return out
+
+
+def pool2d_nhwc(x, k, stride, pad, is_max=True, count_include_pad=False):
+    import torch
+
+    B, H, W, C = x.shape
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    rc = native.kernels().die_kern_pool2d(_ptr(x.contiguous()), _ptr(y), B, H, W, C, Ho, Wo, k, k, stride, stride, pad,
+                                          pad, int(is_max), int(count_include_pad), _stream())
+    _check(rc, "pool2d")
+    return y
+
+
+def global_avgpool_nhwc(x, scale=None, shift=None, relu=False):
+    import torch
+
+    B, H, W, C = x.shape
+    out = torch.empty((B, C), dtype=torch.bfloat16, device=x.device)
+    out32 = torch.empty((B, C), dtype=torch.float32, device=x.device)
+    rc = native.kernels().die_kern_gap(_ptr(x.contiguous()), _ptr(out), _ptr(out32), _ptr(scale), _ptr(shift),
+                                       int(relu), B, H * W, C, _stream())
+    _check(rc, "global_avgpool")
+    return out, out32
+
+
+def affine_act(x, scale=None, shift=None, z=None, relu=False):
+    import torch
+
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty_like(x)
+    rc = native.kernels().die_kern_affine(_ptr(x.contiguous()), _ptr(z), _ptr(scale), _ptr(shift), int(relu), _ptr(y),
+                                          M, C, _stream())
+    _check(rc, "affine_act")
+    return y

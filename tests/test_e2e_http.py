@@ -1,0 +1,199 @@
+"""End-to-end serving tests on the CPU engine: gateway + 3 workers in-process on ephemeral ports.
+
+Mirrors the reference's only test strategy (diagnostics.sh / benchmark.py against live processes,
+SURVEY §4) and adds what it lacks: API-parity assertions on every key, routing parity with the
+reference ring, cache semantics, error bodies, and breaker fail-over/recovery."""
+import json
+import os
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+import numpy as np
+import pytest
+
+from test_core import py_get, py_ring
+
+
+def post(url, obj=None, raw=None, timeout=30):
+    data = raw if raw is not None else json.dumps(obj).encode()
+    req = urllib.request.Request(url, data=data, headers={"Content-Type": "application/json"})
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status, json.loads(r.read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def get(url, timeout=10):
+    with urllib.request.urlopen(url, timeout=timeout) as r:
+        return r.status, json.loads(r.read())
+
+
+@pytest.fixture(scope="module")
+def cluster(native, models):
+    path = models["tiny"][0]
+    workers = [native.Worker(path, node_id="w%d" % i, engine={"device": "cpu"}) for i in range(3)]
+    names = ["127.0.0.1:%d" % w.port for w in workers]
+    gw = native.GatewayServer(names, breaker_timeout_s=0.5)
+    yield {"workers": workers, "names": names, "gw": gw, "path": path}
+    gw.stop()
+    for w in workers:
+        w.stop()
+
+
+def test_infer_through_gateway_api_parity(cluster):
+    gw = cluster["gw"]
+    st, out = post(gw.url + "/infer", {"request_id": "req_42", "input_data": [1.0, 2.0, 3.0]})
+    assert st == 200
+    assert set(out) == {"request_id", "output_data", "node_id", "cached", "inference_time_us"}
+    assert out["request_id"] == "req_42"
+    assert len(out["output_data"]) == 10
+    assert out["cached"] is False and out["inference_time_us"] > 0
+    # same request id -> same worker -> cache hit with the reference's constant 50 us
+    st, out2 = post(gw.url + "/infer", {"request_id": "req_42", "input_data": [1.0, 2.0, 3.0]})
+    assert st == 200 and out2["cached"] is True and out2["inference_time_us"] == 50
+    assert out2["output_data"] == out["output_data"] and out2["node_id"] == out["node_id"]
+
+
+def test_routing_matches_reference_ring(cluster):
+    names = cluster["names"]
+    ring, keys = py_ring(names)
+    by_port = {w.port: "w%d" % i for i, w in enumerate(cluster["workers"])}
+    for i in range(30):
+        rid = "route_%d" % i
+        st, out = post(cluster["gw"].url + "/infer", {"request_id": rid, "input_data": [0.1 * i]})
+        assert st == 200
+        expect = py_get(ring, keys, rid)
+        assert out["node_id"] == by_port[int(expect.split(":")[1])]
+
+
+def test_health_and_stats_keys(cluster):
+    st, h = get(cluster["workers"][0].url.replace("127.0.0.1", "127.0.0.1") + "/health")
+    assert st == 200
+    for k in ["healthy", "node_id", "total_requests", "cache_hits", "cache_size", "cache_hit_rate", "batch_processor"]:
+        assert k in h
+    for k in ["total_batches", "avg_batch_size", "timeout_batches", "full_batches"]:
+        assert k in h["batch_processor"]
+    st, s = get(cluster["gw"].url + "/stats")
+    assert st == 200 and s["total_workers"] == 3
+    nodes = [b["node"] for b in s["circuit_breakers"]]
+    assert nodes == sorted(nodes)
+    for b in s["circuit_breakers"]:
+        assert set(b) >= {"node", "state", "failures", "successes"}
+
+
+def test_direct_worker_errors(cluster):
+    w = cluster["workers"][0]
+    st, out = post(w.url + "/infer", raw=b"{not json")
+    assert st == 500 and "error" in out
+    st, out = post(w.url + "/infer", {"request_id": "x"})
+    assert st == 500 and "input_data" in out["error"]
+    st, out = post(w.url + "/infer", {"request_id": "x", "input_data": [0.0] * (3 * 64 * 64 + 1)})
+    assert st == 500  # oversized input rejected (reference: silently shifts the batch)
+    st, out = post(w.url + "/infer", {"input_data": [1.0], "request_id": "ok"})
+    assert st == 200
+
+
+def test_padding_semantics_match_cpu_executor(cluster, native):
+    w = cluster["workers"][1]
+    x = np.zeros(3 * 64 * 64, np.float32)
+    x[:5] = [0.5, 0.25, 0.125, 1.0, 2.0]
+    st, out = post(w.url + "/infer", {"request_id": "pad", "input_data": x[:5].tolist()})
+    ref = native.cpu_run(cluster["path"], x.reshape(1, 3, 64, 64))[0]
+    np.testing.assert_allclose(np.array(out["output_data"], np.float32), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_concurrent_load_and_batching(cluster, native):
+    res = native.loadgen(port=cluster["gw"].port, connections=24, requests=600, payload="ref")
+    assert res["ok"] == 600 and res["failed"] == 0
+    batches = [w.health()["batch_processor"] for w in cluster["workers"]]
+    assert sum(b["total_batches"] for b in batches) > 0
+
+
+def test_full_payload_unique_requests(native, models):
+    path = models["tiny"][0]
+    w = native.Worker(path, node_id="solo", engine={"device": "cpu"})
+    try:
+        res = native.loadgen(port=w.port, connections=8, requests=64, payload="full", input_numel=3 * 64 * 64)
+        assert res["ok"] == 64, res
+        h = w.health()
+        assert h["cache_hits"] == 0 and h["cache_size"] == 64
+    finally:
+        w.stop()
+
+
+def test_failover_and_breaker_recovery(native, models):
+    path = models["tiny"][0]
+    workers = [native.Worker(path, node_id="f%d" % i, engine={"device": "cpu"}) for i in range(2)]
+    names = ["127.0.0.1:%d" % w.port for w in workers]
+    gw = native.GatewayServer(names, breaker_timeout_s=0.5, failure_threshold=5, success_threshold=2,
+                              connect_timeout_ms=500, read_timeout_ms=2000)
+    try:
+        dead_port = workers[0].port
+        workers[0].stop()
+        dead = "127.0.0.1:%d" % dead_port
+        ok = 0
+        for i in range(40):
+            st, out = post(gw.url + "/infer", {"request_id": "fo_%d" % i, "input_data": [float(i)]})
+            ok += st == 200
+            if st == 200:
+                assert out["node_id"] == "f1"
+        assert ok == 40  # zero client-visible failures while another worker is healthy
+        states = {b["node"]: b for b in gw.stats()["circuit_breakers"]}
+        assert states[dead]["state"] == "OPEN"
+        # restart a worker on the same port; after the timeout the breaker half-opens and closes
+        workers[0] = native.Worker(path, node_id="f0b", port=dead_port, engine={"device": "cpu"})
+        time.sleep(0.7)
+        ring, keys = py_ring(names)
+        rids = [r for r in ("rec_%d" % i for i in range(400)) if py_get(ring, keys, r) == dead][:4]
+        for rid in rids:
+            st, out = post(gw.url + "/infer", {"request_id": rid, "input_data": [1.0]})
+            assert st == 200
+        states = {b["node"]: b for b in gw.stats()["circuit_breakers"]}
+        assert states[dead]["state"] == "CLOSED"
+    finally:
+        gw.stop()
+        for w in workers:
+            w.stop()
+
+
+def test_all_workers_down_error(native):
+    gw = native.GatewayServer(["127.0.0.1:1", "127.0.0.1:2"], connect_timeout_ms=200)
+    try:
+        st, out = post(gw.url + "/infer", {"request_id": "x", "input_data": [1.0]})
+        assert st == 500 and out["error"] == "All workers failed or circuit breakers open"
+        st, out = post(gw.url + "/infer", raw=b"[1,2")
+        assert st == 500 and "error" in out
+    finally:
+        gw.stop()
+
+
+def test_binaries_cli(native, models, tmp_path):
+    """worker_node/gateway binaries: positional CLI, MODEL_PATH fallback, graceful SIGTERM."""
+    from die_amd import BIN_DIR
+
+    path = models["tiny"][0]
+    env = dict(os.environ, MODEL_PATH=path)
+    w = subprocess.Popen([os.path.join(BIN_DIR, "worker_node"), "18931", "cliw", "--device", "cpu"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    g = subprocess.Popen([os.path.join(BIN_DIR, "gateway"), "localhost:18931", "--port", "18930"],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        for _ in range(100):
+            try:
+                st, out = post("http://127.0.0.1:18930/infer", {"request_id": "c1", "input_data": [1.0, 2.0]})
+                if st == 200:
+                    break
+            except Exception:
+                time.sleep(0.1)
+        assert st == 200 and out["node_id"] == "cliw"
+    finally:
+        w.terminate()
+        g.terminate()
+        assert w.wait(timeout=20) == 0
+        assert g.wait(timeout=20) == 0
+    usage = subprocess.run([os.path.join(BIN_DIR, "worker_node")], capture_output=True, text=True)
+    assert usage.returncode == 1 and "Usage" in usage.stderr

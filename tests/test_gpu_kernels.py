@@ -1,0 +1,147 @@
+"""Numerics of the hand-written gfx950 kernels vs a plain PyTorch fp32 reference of the same op.
+
+Inputs/weights are rounded to bf16 first, so the reference differs from the kernel only by the
+accumulation order (f32) and the bf16 rounding of the output."""
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+
+def _t():
+    import torch
+
+    return torch
+
+
+def rel_err(a, b):
+    t = _t()
+    a = a.float()
+    b = b.float()
+    return (t.linalg.vector_norm(a - b) / t.linalg.vector_norm(b).clamp_min(1e-12)).item()
+
+
+CONV_SHAPES = [
+    # B, H, Cin, Cout, k, stride, pad
+    (2, 56, 64, 64, 1, 1, 0),
+    (2, 56, 64, 64, 3, 1, 1),
+    (2, 56, 64, 256, 1, 1, 0),
+    (2, 56, 256, 128, 1, 2, 0),
+    (2, 56, 128, 128, 3, 2, 1),
+    (3, 28, 512, 256, 1, 1, 0),
+    (3, 14, 256, 256, 3, 1, 1),
+    (4, 7, 512, 2048, 1, 1, 0),
+    (4, 7, 512, 512, 3, 1, 1),
+    (1, 9, 24, 40, 3, 1, 1),      # ragged: K not a multiple of 64, N not of 64
+    (5, 1, 2048, 1000, 1, 1, 0),  # FC head as a 1x1 "conv"
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_matches_torch(native, shape):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B, H, Cin, Cout, k, s, p = shape
+    g = torch.Generator(device="cuda").manual_seed(hash(shape) % 2**31)
+    x = torch.randn(B, Cin, H, H, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, k, k, device="cuda", generator=g) / (Cin * k * k) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Cout, device="cuda", generator=g)
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), bias, stride=s, padding=p)
+    out, _ = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), w.float(), bias=bias, stride=s, pad=p, out_f32=True)
+    torch.cuda.synchronize()
+    got = out.permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 2e-3, rel_err(got, ref)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_conv_all_tiles_and_epilogue(native, tile):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B, H, Cin, Cout = 2, 20, 64, 192
+    g = torch.Generator(device="cuda").manual_seed(7 + tile)
+    x = torch.randn(B, Cin, H, H, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, device="cuda", generator=g) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Cout, device="cuda", generator=g)
+    res = torch.randn(B, H, H, Cout, device="cuda", generator=g).to(torch.bfloat16)
+    s2 = torch.rand(Cout, device="cuda", generator=g) + 0.5
+    b2 = torch.randn(Cout, device="cuda", generator=g)
+    out, out2 = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), w.float(), bias=bias, stride=1, pad=1, relu=True,
+                              res=res, scale2=s2, shift2=b2, relu2=True, tile=tile)
+    torch.cuda.synchronize()
+    v = torch.nn.functional.conv2d(x.float(), w.float(), bias, padding=1).permute(0, 2, 3, 1) + res.float()
+    v = torch.relu(v)
+    u = torch.relu(v * s2 + b2)
+    assert rel_err(out, v) < 5e-3
+    assert rel_err(out2, u) < 5e-3
+
+
+def test_stem_conv_with_input_prep(native):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B = 2
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(B, 3, 224, 224, device="cuda", generator=g)
+    sc = torch.rand(3, device="cuda", generator=g) + 0.5
+    sh = torch.randn(3, device="cuda", generator=g)
+    xp = K.input_prep(x, sc, sh, cp=4)
+    ref_in = (x * sc.view(1, 3, 1, 1) + sh.view(1, 3, 1, 1))
+    torch.cuda.synchronize()
+    assert rel_err(xp[..., :3].permute(0, 3, 1, 2), ref_in) < 4e-3
+    assert xp[..., 3].abs().max().item() == 0
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) / 12.0).to(torch.bfloat16)
+    out, _ = K.conv2d_nhwc(xp, w.float(), stride=2, pad=3, out_f32=True)
+    ref = torch.nn.functional.conv2d(xp[..., :3].permute(0, 3, 1, 2).float(), w.float(), stride=2, padding=3)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-3
+
+
+def test_conv_repeatable_bitwise(native):
+    """Race screen: repeated launches at several shapes must agree bit for bit."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    for (B, H, Cin, Cout, k) in [(4, 28, 128, 128, 3), (8, 14, 256, 1024, 1)]:
+        x = torch.randn(B, H, H, Cin, device="cuda").to(torch.bfloat16)
+        w = torch.randn(Cout, Cin, k, k, device="cuda") * 0.05
+        first, _ = K.conv2d_nhwc(x, w, pad=k // 2)
+        for _ in range(10):
+            again, _ = K.conv2d_nhwc(x, w, pad=k // 2)
+            assert torch.equal(first.view(torch.int16), again.view(torch.int16))
+
+
+@pytest.mark.parametrize("cfg", [(2, 112, 64, 3, 2, 1, True), (2, 14, 128, 2, 2, 0, False), (3, 9, 16, 3, 1, 1, False)])
+def test_pool(native, cfg):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B, H, C, k, s, p, is_max = cfg
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16)
+    y = K.pool2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), k, s, p, is_max=is_max)
+    if is_max:
+        ref = torch.nn.functional.max_pool2d(x.float(), k, s, p)
+    else:
+        ref = torch.nn.functional.avg_pool2d(x.float(), k, s, p, count_include_pad=False)
+    torch.cuda.synchronize()
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < 4e-3
+
+
+def test_gap_and_affine(native):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    x = torch.randn(6, 7, 7, 2048, device="cuda").to(torch.bfloat16)
+    sc = torch.rand(2048, device="cuda") + 0.5
+    sh = torch.randn(2048, device="cuda")
+    out, out32 = K.global_avgpool_nhwc(x, sc, sh, relu=True)
+    ref = torch.relu(x.float() * sc + sh).mean(dim=(1, 2))
+    torch.cuda.synchronize()
+    assert rel_err(out32, ref) < 1e-5
+    assert rel_err(out, ref) < 4e-3
+    z = torch.randn_like(x)
+    y = K.affine_act(x, sc, sh, z=z, relu=True)
+    torch.cuda.synchronize()
+    assert rel_err(y, torch.relu(x.float() * sc + sh + z.float())) < 4e-3
