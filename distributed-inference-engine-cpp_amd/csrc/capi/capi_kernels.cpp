@@ -115,6 +115,7 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
       static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32"};
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
+      e["gflop"] = o.flops_per_sample / 1e9;
       if (o.kind == PlanOp::CONV) {
         e["N"] = o.conv.N;
         e["K"] = o.conv.K;
