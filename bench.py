@@ -97,6 +97,7 @@ def main():
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
             "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
+            "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
         }
         wk.stop()
     else:

@@ -108,6 +108,7 @@ struct EngineOptions {
   int max_batch = 32;
   int pipeline_depth = 2;        // batches in flight (HIP)
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
+  bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
   std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
   int cpu_threads = 0;
   int shard_id = 0;

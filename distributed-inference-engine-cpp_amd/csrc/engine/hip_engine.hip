@@ -83,9 +83,13 @@ class HipEngine : public Engine {
         },
         [](void* p) { (void)hipHostFree(p); }, 32);
 
-    // Validate every op eagerly at the largest bucket, then capture one graph per (bucket, slot).
+    ws_bytes_ = 64u << 20;  // split-K partials (choose_splits / autotune stay within it)
+    HIP_CHECK(hipMalloc(&ws_, ws_bytes_));
+    // Validate every op eagerly at the largest bucket, tune, then capture one graph per
+    // (bucket, slot).
     for (int s = 0; s < depth_; ++s) encode_forward(max_batch_, s, s_compute_);
     HIP_CHECK(hipStreamSynchronize(s_compute_));
+    if (opt.autotune) autotune();
     if (opt.use_graphs) {
       graphs_.assign(buckets_.size() * depth_, nullptr);
       for (size_t bi = 0; bi < buckets_.size(); ++bi)
@@ -129,6 +133,7 @@ class HipEngine : public Engine {
     pool_.reset();
     (void)hipFree(params_);
     (void)hipFree(arena_);
+    (void)hipFree(ws_);
     (void)hipStreamDestroy(s_compute_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -232,22 +237,122 @@ class HipEngine : public Engine {
     j["gflop_per_image"] = plan_.flops_per_sample / 1e9;
     j["arena_mib"] = static_cast<double>(plan_.arena_bytes) / (1 << 20);
     j["pinned_samples"] = static_cast<long long>(pool_->allocated());
+    j["autotuned"] = !tune_.empty();
+    j["tuned_conv_us_at_max_batch"] = tuned_conv_us_;
+    if (!tune_.empty()) {
+      Json t = Json::array();
+      for (size_t oi = 0; oi < plan_.ops.size(); ++oi)
+        if (plan_.ops[oi].kind == PlanOp::CONV) {
+          const Tune& x = tune_.back()[oi];
+          t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits));
+        }
+      j["tile_split_at_max_batch"] = t;
+    }
     return j;
+  }
+
+  struct Tune {
+    int tile = 0;
+    int splits = 1;
+  };
+
+  void* buf_ptr(int id, int s) {
+    Slot& sl = slots_[s];
+    if (id == -2) return sl.d_in;
+    if (id == -3) return sl.d_out;
+    if (id < 0) return nullptr;
+    return arena_ + plan_.bufs[id].offset;
+  }
+  const float* prm_ptr(size_t off) const {
+    return off == SIZE_MAX ? nullptr : reinterpret_cast<const float*>(params_ + off);
+  }
+
+  kern::ConvArgs conv_args(const PlanOp& op, int B, int s) {
+    kern::ConvArgs a = op.conv;
+    a.B = B;
+    a.M = B * a.Ho * a.Wo;
+    a.x = static_cast<const uint16_t*>(buf_ptr(op.in, s));
+    a.w = reinterpret_cast<const uint16_t*>(params_ + op.w_off);
+    a.bias = prm_ptr(op.bias_off);
+    a.res = static_cast<const uint16_t*>(buf_ptr(op.in2, s));
+    a.out = static_cast<uint16_t*>(buf_ptr(op.out, s));
+    a.out_f32 = static_cast<float*>(buf_ptr(op.out_f32, s));
+    a.scale2 = prm_ptr(op.s2_off);
+    a.shift2 = prm_ptr(op.b2_off);
+    a.out2 = static_cast<uint16_t*>(buf_ptr(op.out2, s));
+    return a;
+  }
+
+  size_t bucket_index(int B) const {
+    size_t bi = 0;
+    while (bi + 1 < buckets_.size() && buckets_[bi] < B) ++bi;
+    return bi;
+  }
+
+  Tune tune_for(int B, size_t op_index) const {
+    const size_t bi = bucket_index(B);
+    if (bi < tune_.size() && op_index < tune_[bi].size() && tune_[bi][op_index].tile >= 0) return tune_[bi][op_index];
+    const PlanOp& op = plan_.ops[op_index];
+    const int M = B * op.conv.Ho * op.conv.Wo;
+    Tune t;
+    t.tile = kern::choose_tile(M, op.conv.N, op.conv.K);
+    t.splits = kern::choose_splits(M, op.conv.N, op.conv.K, t.tile);
+    return t;
+  }
+
+  // Time every (tile, split-K) candidate of every conv at every bucket and keep the fastest.
+  // Runs once at start-up on the real buffers (a full forward first, so inputs hold real data).
+  void autotune() {
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    tune_.assign(buckets_.size(), std::vector<Tune>(plan_.ops.size(), Tune{-1, 1}));
+    double total_best_us = 0;
+    for (size_t bi = 0; bi < buckets_.size(); ++bi) {
+      const int B = buckets_[bi];
+      encode_forward(B, 0, s_compute_);
+      HIP_CHECK(hipStreamSynchronize(s_compute_));
+      for (size_t oi = 0; oi < plan_.ops.size(); ++oi) {
+        const PlanOp& op = plan_.ops[oi];
+        if (op.kind != PlanOp::CONV) continue;
+        kern::ConvArgs base = conv_args(op, B, 0);
+        base.ws = ws_;
+        const int nk = base.Kpad / 64;
+        float best = 1e30f;
+        Tune bt{kern::choose_tile(base.M, base.N, base.K), 1};
+        for (int tile = 0; tile < kern::NUM_TILES; ++tile) {
+          for (int sp = 1; sp <= 16; sp *= 2) {
+            if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
+            kern::ConvArgs a = base;
+            a.splits = sp;
+            if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;  // warm-up / validity
+            HIP_CHECK(hipEventRecord(e0, s_compute_));
+            for (int r = 0; r < 3; ++r) HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
+            HIP_CHECK(hipEventRecord(e1, s_compute_));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) {
+              best = ms;
+              bt = Tune{tile, sp};
+            }
+          }
+        }
+        tune_[bi][oi] = bt;
+        if (B == max_batch_) total_best_us += best / 3 * 1000.0;
+      }
+    }
+    tuned_conv_us_ = total_best_us;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   }
 
   // Encode one forward pass for `B` samples using slot `s`'s input/output buffers.
   void encode_forward(int B, int s, hipStream_t st) {
-    Slot& sl = slots_[s];
-    auto buf = [&](int id) -> void* {
-      if (id == -2) return sl.d_in;
-      if (id == -3) return sl.d_out;
-      if (id < 0) return nullptr;
-      return arena_ + plan_.bufs[id].offset;
-    };
-    auto prm = [&](size_t off) -> const float* {
-      return off == SIZE_MAX ? nullptr : reinterpret_cast<const float*>(params_ + off);
-    };
-    for (const PlanOp& op : plan_.ops) {
+    auto buf = [&](int id) -> void* { return buf_ptr(id, s); };
+    auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
+    for (size_t op_index = 0; op_index < plan_.ops.size(); ++op_index) {
+      const PlanOp& op = plan_.ops[op_index];
       hipError_t e = hipSuccess;
       switch (op.kind) {
         case PlanOp::INPUT_PREP:
@@ -255,20 +360,11 @@ class HipEngine : public Engine {
                                static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st);
           break;
         case PlanOp::CONV: {
-          kern::ConvArgs a = op.conv;
-          a.B = B;
-          a.M = B * a.Ho * a.Wo;
-          a.x = static_cast<const uint16_t*>(buf(op.in));
-          a.w = reinterpret_cast<const uint16_t*>(params_ + op.w_off);
-          a.bias = prm(op.bias_off);
-          a.res = static_cast<const uint16_t*>(buf(op.in2));
-          a.out = static_cast<uint16_t*>(buf(op.out));
-          a.out_f32 = static_cast<float*>(buf(op.out_f32));
-          a.scale2 = prm(op.s2_off);
-          a.shift2 = prm(op.b2_off);
-          a.out2 = static_cast<uint16_t*>(buf(op.out2));
-          const int tile = kern::choose_tile(a.M, a.N, a.K);
-          e = kern::conv_igemm(a, tile, st);
+          kern::ConvArgs a = conv_args(op, B, s);
+          const Tune t = tune_for(B, op_index);
+          a.splits = t.splits;
+          a.ws = ws_;
+          e = kern::conv_igemm(a, t.tile, st);
           break;
         }
         case PlanOp::POOL:
@@ -367,6 +463,10 @@ class HipEngine : public Engine {
   size_t in_numel_ = 0, out_numel_ = 0;
   uint8_t* params_ = nullptr;
   uint8_t* arena_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+  std::vector<std::vector<Tune>> tune_;  // [bucket][op]
+  double tuned_conv_us_ = 0;
   hipStream_t s_compute_{}, s_h2d_{}, s_d2h_{};
   std::vector<Slot> slots_;
   std::vector<int> buckets_;

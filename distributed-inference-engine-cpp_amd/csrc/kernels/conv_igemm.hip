@@ -5,18 +5,21 @@
 //  * NHWC bf16 activations, weights pre-packed as [Npad][Kpad] bf16 with k = (ky, kx, ci), so both
 //    MFMA operands are K-contiguous and a BK=64 K-step of the activation tile is a plain 128-byte
 //    row per output pixel (padding pixels -> zeros, predicated loads).
-//  * The GEMM is computed transposed (A = weights, B = pixels): the 16x16 accumulator then holds
-//    4 consecutive output channels of one pixel per lane, i.e. 8-byte contiguous NHWC stores and
-//    float4 bias/scale loads in the fused epilogue.
+//  * The GEMM is computed transposed (A = weights, B = pixels): each 16x16 accumulator holds
+//    4 consecutive output channels of one pixel per lane.
 //  * 256-thread blocks = 4 wave64s in a 2x2 grid; BMxBN in {128,64}^2; 64-wide K-steps double-
 //    buffered in LDS with the next tile's global loads issued before the MFMAs of the current one
 //    (async-STAGE split) and ONE barrier per K-step.
 //  * LDS rows are 128 B; the 16-byte chunk index is XOR-swizzled with (row>>1)&7, which makes the
 //    ds_read_b128 fragment reads of both operands bank-conflict-free for the gfx950 b128 lane
 //    groups ({0-3,12-15,20-27}, ...).
-//  * Fused epilogue: + bias (folded BatchNorm), + residual, ReLU, bf16 or f32 store, and an
-//    optional second output act(v*scale2+shift2) (the next pre-activation unit's BN+ReLU), which
-//    removes every standalone BatchNormalization / Relu / Add of ResNet-v2.
+//  * Epilogue staged through LDS (f32 tile, XOR-swizzled 16-B chunks), then every thread owns 8
+//    consecutive channels of one pixel: 16-byte coalesced residual loads and output stores (a wave
+//    writes whole 256-B row segments).  Fused: + bias (folded BatchNorm), + residual, ReLU, bf16
+//    and/or f32 store, and a second output act(v*scale2+shift2) (the next pre-activation unit's
+//    BN+ReLU), which removes every standalone BatchNormalization / Relu / Add of ResNet-v2.
+//  * Split-K for layers with few output tiles (late stages, the FC head): K slices write f32
+//    partials with the same coalesced path; splitk_epilogue sums them and applies the epilogue.
 #include "common.h"
 #include "kernels.h"
 
@@ -31,13 +34,55 @@ constexpr int BK = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
+__device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
+__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
+  const size_t o = static_cast<size_t>(m) * p.N + n;
+  if (p.bias) {
+    const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (p.res) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p.res + o);
+    float a, b;
+    unpack2(r.x, a, b); v[0] += a; v[1] += b;
+    unpack2(r.y, a, b); v[2] += a; v[3] += b;
+    unpack2(r.z, a, b); v[4] += a; v[5] += b;
+    unpack2(r.w, a, b); v[6] += a; v[7] += b;
+  }
+  if (p.relu) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+  }
+  if (p.out)
+    *reinterpret_cast<uint4*>(p.out + o) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+  if (p.out_f32) {
+    *reinterpret_cast<float4*>(p.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p.out_f32 + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  if (p.out2) {
+    const float4 s0 = ldf4(p.scale2 + n), s1 = ldf4(p.scale2 + n + 4);
+    const float4 h0 = ldf4(p.shift2 + n), h1 = ldf4(p.shift2 + n + 4);
+    float u[8] = {v[0] * s0.x + h0.x, v[1] * s0.y + h0.y, v[2] * s0.z + h0.z, v[3] * s0.w + h0.w,
+                  v[4] * s1.x + h1.x, v[5] * s1.y + h1.y, v[6] * s1.z + h1.z, v[7] * s1.w + h1.w};
+    if (p.relu2) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) u[t] = fmaxf(u[t], 0.f);
+    }
+    *reinterpret_cast<uint4*>(p.out2 + o) = make_uint4(pack2(u[0], u[1]), pack2(u[2], u[3]), pack2(u[4], u[5]), pack2(u[6], u[7]));
+  }
+}
+
 template <int BM, int BN, int MODE, int VEC>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p) {
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const int kt_per_split) {
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave pixels / channels
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, STAGE = A_ELEMS + B_ELEMS;
   constexpr int W_CH = BN / 32;                       // 16-B weight chunks per thread per stage
   constexpr int X_CH = VEC == 8 ? BM / 32 : BM / 16;  // activation units per thread per stage
+  static_assert(2 * STAGE * 2 >= BM * BN * 4, "epilogue staging must fit in the operand LDS");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE];
 
   const int tid = threadIdx.x;
@@ -48,6 +93,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p) {
   const int tile_n = blockIdx.x % ntn;
   const int tile_m = blockIdx.x / ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk_total = p.Kpad / BK;
+  const int kt_begin = blockIdx.y * kt_per_split;
+  const int kt_end = min(nk_total, kt_begin + kt_per_split);
 
   // ---- per-thread loader state ----
   const int wc = tid & 7;
@@ -141,14 +189,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.Kpad / BK;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
+  if (kt_begin < kt_end) {
+    load_stage(kt_begin * BK);
+    store_stage(0);
+    __syncthreads();
+  }
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_begin) & 1;
+    const bool more = kt + 1 < kt_end;
     if (more) load_stage((kt + 1) * BK);  // in flight under the MFMAs below
     const uint16_t* A = lds + cur * STAGE;
     const uint16_t* Bt = A + A_ELEMS;
@@ -172,82 +220,87 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p) {
     __syncthreads();
   }
 
-  // ---- fused epilogue ----
   const int lm = lane & 15;
   const int ln = (lane >> 4) * 4;
+  if ((p.N & 7) == 0) {
+    // ---- LDS-staged, coalesced epilogue ----
+    constexpr int CPR = BN / 4;  // 16-B chunks per staged row
+    float* st = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int row = wm * WM + j * 16 + lm;
+        const int c = (wn * WN + i * 16 + ln) >> 2;
+        *reinterpret_cast<f32x4*>(st + row * BN + ((c ^ (row & (CPR - 1))) << 2)) = acc[i][j];
+      }
+    __syncthreads();
+    constexpr int GPR = BN / 8;
+    const bool partial = p.splits > 1;
+    float* ws = partial ? p.ws + static_cast<size_t>(blockIdx.y) * p.M * p.N : nullptr;
+    for (int g = tid; g < BM * GPR; g += 256) {
+      const int row = g / GPR;
+      const int cg = g - row * GPR;
+      const int m = m0 + row;
+      const int n = n0 + cg * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float4 a = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg) ^ (row & (CPR - 1))) << 2));
+      const float4 b = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg + 1) ^ (row & (CPR - 1))) << 2));
+      if (partial) {
+        float* o = ws + static_cast<size_t>(m) * p.N + n;
+        *reinterpret_cast<float4*>(o) = a;
+        *reinterpret_cast<float4*>(o + 4) = b;
+      } else {
+        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        epilogue8(p, m, n, v);
+      }
+    }
+    return;
+  }
+  // ---- ragged N (e.g. a 10-class head): element-wise epilogue from registers ----
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int n = n0 + wn * WN + i * 16 + ln;
     if (n >= p.N) continue;
-    float4 bias = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 sc2 = make_float4(1.f, 1.f, 1.f, 1.f), sh2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.out2) {
-      sc2 = *reinterpret_cast<const float4*>(p.scale2 + n);
-      sh2 = *reinterpret_cast<const float4*>(p.shift2 + n);
-    }
-    if (p.N & 3) {  // ragged N (e.g. a 10-class head): element-wise path
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        const int m = m0 + wm * WM + j * 16 + lm;
-        if (m >= p.M) continue;
-        const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
-        const float s2[4] = {sc2.x, sc2.y, sc2.z, sc2.w};
-        const float h2[4] = {sh2.x, sh2.y, sh2.z, sh2.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (n + r >= p.N) break;
-          const size_t o = static_cast<size_t>(m) * p.N + n + r;
-          float v = acc[i][j][r] + bb[r];
-          if (p.res) v += bf2f(p.res[o]);
-          if (p.relu) v = fmaxf(v, 0.f);
-          if (p.out) p.out[o] = f2bf(v);
-          if (p.out_f32) p.out_f32[o] = v;
-          if (p.out2) {
-            float u = v * s2[r] + h2[r];
-            if (p.relu2) u = fmaxf(u, 0.f);
-            p.out2[o] = f2bf(u);
-          }
-        }
-      }
-      continue;
-    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm * WM + j * 16 + lm;
       if (m >= p.M) continue;
-      const size_t o = static_cast<size_t>(m) * p.N + n;
-      float v0 = acc[i][j][0] + bias.x, v1 = acc[i][j][1] + bias.y;
-      float v2 = acc[i][j][2] + bias.z, v3 = acc[i][j][3] + bias.w;
-      if (p.res) {
-        const uint2 r = *reinterpret_cast<const uint2*>(p.res + o);
-        float r0, r1, r2, r3;
-        unpack2(r.x, r0, r1);
-        unpack2(r.y, r2, r3);
-        v0 += r0;
-        v1 += r1;
-        v2 += r2;
-        v3 += r3;
-      }
-      if (p.relu) {
-        v0 = fmaxf(v0, 0.f);
-        v1 = fmaxf(v1, 0.f);
-        v2 = fmaxf(v2, 0.f);
-        v3 = fmaxf(v3, 0.f);
-      }
-      if (p.out) *reinterpret_cast<uint2*>(p.out + o) = make_uint2(pack2(v0, v1), pack2(v2, v3));
-      if (p.out_f32) *reinterpret_cast<float4*>(p.out_f32 + o) = make_float4(v0, v1, v2, v3);
-      if (p.out2) {
-        float u0 = v0 * sc2.x + sh2.x, u1 = v1 * sc2.y + sh2.y;
-        float u2 = v2 * sc2.z + sh2.z, u3 = v3 * sc2.w + sh2.w;
-        if (p.relu2) {
-          u0 = fmaxf(u0, 0.f);
-          u1 = fmaxf(u1, 0.f);
-          u2 = fmaxf(u2, 0.f);
-          u3 = fmaxf(u3, 0.f);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (n + r >= p.N) break;
+        const size_t o = static_cast<size_t>(m) * p.N + n + r;
+        float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
+        if (p.res) v += bf2f(p.res[o]);
+        if (p.relu) v = fmaxf(v, 0.f);
+        if (p.out) p.out[o] = f2bf(v);
+        if (p.out_f32) p.out_f32[o] = v;
+        if (p.out2) {
+          float u = v * p.scale2[n + r] + p.shift2[n + r];
+          if (p.relu2) u = fmaxf(u, 0.f);
+          p.out2[o] = f2bf(u);
         }
-        *reinterpret_cast<uint2*>(p.out2 + o) = make_uint2(pack2(u0, u1), pack2(u2, u3));
       }
     }
+  }
+}
+
+// Sum the split-K partials and apply the epilogue; one thread per 8 channels of one pixel.
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
+  const int GPR = p.N / 8;
+  const long long total = static_cast<long long>(p.M) * GPR;
+  const size_t slab = static_cast<size_t>(p.M) * p.N;
+  for (long long g = blockIdx.x * 256ll + threadIdx.x; g < total; g += static_cast<long long>(gridDim.x) * 256) {
+    const int m = static_cast<int>(g / GPR);
+    const int n = static_cast<int>(g - static_cast<long long>(m) * GPR) * 8;
+    const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < p.splits; ++s) {
+      const float4 a = ldf4(src + s * slab), b = ldf4(src + s * slab + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    epilogue8(p, m, n, v);
   }
 }
 
@@ -256,14 +309,26 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   const bool dense1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
                         a.W == a.Wo;
   const int vec = a.Cin % 8 == 0 ? 8 : 4;
-  const int grid = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int nk = a.Kpad / BK;
+  const int splits = std::max(1, std::min(a.splits, nk));
+  const int kt_per = (nk + splits - 1) / splits;
+  const int eff = (nk + kt_per - 1) / kt_per;  // no empty slices
+  ConvArgs b = a;
+  b.splits = eff;
+  dim3 grid(tiles, eff);
   if (dense1x1 && vec == 8) {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), grid, dim3(256), 0, s, b, kt_per);
   } else if (vec == 8) {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8>), grid, dim3(256), 0, s, b, kt_per);
   } else {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4>), grid, dim3(256), 0, s, b, kt_per);
   }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || eff == 1) return e;
+  const long long groups = static_cast<long long>(b.M) * (b.N / 8);
+  const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
@@ -288,13 +353,31 @@ int choose_tile(int M, int N, int K) {
   if (N <= 64) return blocks(TILE_128x64) >= 512 ? TILE_128x64 : TILE_64x64;
   if (blocks(TILE_128x128) >= 512) return TILE_128x128;
   if (blocks(TILE_64x128) >= 384) return TILE_64x128;
-  return TILE_64x64;
+  return TILE_128x128;  // few tiles: big tiles + split-K (choose_splits)
+}
+
+int choose_splits(int M, int N, int K, int cfg) {
+  if (N % 8) return 1;
+  int bm, bn;
+  tile_dims(cfg, bm, bn);
+  const long tiles = static_cast<long>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int nk = (K + BK - 1) / BK;
+  int s = 1;
+  while (tiles * s < 384 && s < 16 && nk / (2 * s) >= 4 &&
+         splitk_workspace_bytes(M, N, 2 * s) <= (64u << 20))
+    s *= 2;
+  return s;
+}
+
+size_t splitk_workspace_bytes(int M, int N, int splits) {
+  return splits > 1 ? static_cast<size_t>(splits) * M * N * sizeof(float) : 0;
 }
 
 hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (a.Cin % 4 != 0 || a.Kpad % BK != 0 || a.K > a.Kpad) return hipErrorInvalidValue;
   if (!a.out && !a.out_f32 && !a.out2) return hipErrorInvalidValue;
   if (a.out2 && (!a.scale2 || !a.shift2)) return hipErrorInvalidValue;
+  if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
   switch (cfg) {
     case TILE_128x128: return launch_cfg<128, 128>(a, s);
     case TILE_128x64: return launch_cfg<128, 64>(a, s);

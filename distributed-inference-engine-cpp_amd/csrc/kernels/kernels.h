@@ -31,15 +31,23 @@ struct ConvArgs {
   const float* shift2 = nullptr;
   int relu2 = 0;
   uint16_t* out2 = nullptr;
+  // split-K: `splits` slices of K write f32 partials to ws[split][M][N]; a second kernel sums them
+  // and applies the epilogue.  splits == 1 -> epilogue fused in the GEMM kernel.
+  int splits = 1;
+  float* ws = nullptr;
 };
 
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3 };
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
-// Heuristic tile choice for a problem shape.
+// Heuristic (tile, splits) choice for a problem shape (used when not autotuned).
 int choose_tile(int M, int N, int K);
-// Launch; `vec` = 8 (Cin % 8 == 0) or 4 (Cin % 4 == 0).  Returns hipSuccess or an error for an
-// unsupported configuration (checked on the host before launch).
+int choose_splits(int M, int N, int K, int tile_cfg);
+// Bytes of split-K workspace a launch needs.
+size_t splitk_workspace_bytes(int M, int N, int splits);
+// Launch (vectorisation picked from Cin: 8 channels per 16-B load when Cin % 8 == 0, else 4).
+// Returns hipSuccess or hipErrorInvalidValue for an unsupported configuration (checked on the host
+// before any launch).
 hipError_t conv_igemm(const ConvArgs& a, int tile_cfg, hipStream_t s);
 
 // fp32 NCHW -> (x * scale[c] + shift[c]) -> bf16 NHWC with Cp >= C channels (pad channels = 0).

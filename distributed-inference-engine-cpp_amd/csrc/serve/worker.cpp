@@ -139,8 +139,15 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   const size_t numel = eng.input_numel();
   sink.buf.capacity = std::min(sink.buf.capacity, numel);
   int seen = 0;
+  const auto t_parse = std::chrono::steady_clock::now();
   try {
     seen = parse_infer_body(req.body, sink);
+    parse_ns_.fetch_add(static_cast<int64_t>(
+                            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_parse)
+                                .count()),
+                        std::memory_order_relaxed);
+    parse_bytes_.fetch_add(static_cast<int64_t>(req.body.size()), std::memory_order_relaxed);
+    parsed_.fetch_add(1, std::memory_order_relaxed);
     if (!(seen & 1)) throw JsonError("key 'request_id' not found");
     if (!(seen & 2)) throw JsonError("key 'input_data' not found");
     if (sink.n > numel)
@@ -222,6 +229,10 @@ Json WorkerNode::getHealth() const {
   h["batch_processor"] = b;
   // extras (superset of the reference keys)
   h["errors"] = static_cast<long long>(errors_.load());
+  const int64_t np = parsed_.load();
+  h["parse_us_avg"] = np ? parse_ns_.load() / 1e3 / np : 0.0;
+  h["parse_gbps"] = parse_ns_.load() ? static_cast<double>(parse_bytes_.load()) / parse_ns_.load() : 0.0;
+  h["http_threads"] = opt_.http_threads;
   h["engine"] = engine_->stats();
   h["engine"]["name"] = engine_->name();
   Json ins = Json::array();

@@ -79,6 +79,7 @@ class WorkerNode {
   std::atomic<int64_t> total_requests_{0};
   std::atomic<int64_t> cache_hits_{0};
   std::atomic<int64_t> errors_{0};
+  std::atomic<int64_t> parse_ns_{0}, parse_bytes_{0}, parsed_{0};
   std::atomic<double> fault_fail_rate_{0.0};
   std::atomic<int> fault_latency_ms_{0};
   std::chrono::steady_clock::time_point started_;

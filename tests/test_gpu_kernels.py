@@ -35,6 +35,7 @@ CONV_SHAPES = [
     (4, 7, 512, 512, 3, 1, 1),
     (1, 9, 24, 40, 3, 1, 1),      # ragged: K not a multiple of 64, N not of 64
     (5, 1, 2048, 1000, 1, 1, 0),  # FC head as a 1x1 "conv"
+    (2, 8, 16, 12, 1, 1, 0),      # N % 8 != 0: register epilogue path
 ]
 
 
@@ -55,8 +56,8 @@ def test_conv_matches_torch(native, shape):
     assert rel_err(got, ref) < 2e-3, rel_err(got, ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
-def test_conv_all_tiles_and_epilogue(native, tile):
+@pytest.mark.parametrize("tile,splits", [(0, 1), (1, 1), (2, 1), (3, 1), (0, 3), (3, 4), (1, 9)])
+def test_conv_all_tiles_and_epilogue(native, tile, splits):
     torch = _t()
     from die_amd.ops import kernels as K
 
@@ -69,7 +70,7 @@ def test_conv_all_tiles_and_epilogue(native, tile):
     s2 = torch.rand(Cout, device="cuda", generator=g) + 0.5
     b2 = torch.randn(Cout, device="cuda", generator=g)
     out, out2 = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), w.float(), bias=bias, stride=1, pad=1, relu=True,
-                              res=res, scale2=s2, shift2=b2, relu2=True, tile=tile)
+                              res=res, scale2=s2, shift2=b2, relu2=True, tile=tile, splits=splits)
     torch.cuda.synchronize()
     v = torch.nn.functional.conv2d(x.float(), w.float(), bias, padding=1).permute(0, 2, 3, 1) + res.float()
     v = torch.relu(v)
