@@ -429,3 +429,24 @@ char* die_loadgen_run(const char* opts_json, char** err) {
 }
 
 }  // extern "C"
+
+extern "C" {
+// Parse `iters` times a ResNet-shaped body; returns average microseconds per parse.
+double die_parse_bench(const char* body, long n, int iters, int simd) {
+  struct S : InferBodySink {
+    std::vector<float> buf = std::vector<float>(1 << 20);
+    void on_request_id(std::string_view) override {}
+    float* input_buffer() override { return buf.data(); }
+    size_t input_capacity() const override { return buf.size(); }
+    void on_input_count(size_t) override {}
+  } s;
+  std::string b(body, static_cast<size_t>(n));
+  b.reserve(b.size() + 64);
+  set_json_simd(simd != 0);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters; ++i) parse_infer_body(b, s);
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+  set_json_simd(true);
+  return us;
+}
+}

@@ -20,6 +20,7 @@
 #include <unordered_map>
 
 #include "json.h"
+#include "sysinfo.h"
 
 namespace die {
 
@@ -230,7 +231,7 @@ int HttpServer::start(const std::string& host, int port, int threads) {
   port_ = ntohs(addr.sin_port);
   set_nonblock(listen_fd_);
 
-  if (threads <= 0) threads = static_cast<int>(std::min(32u, std::max(1u, std::thread::hardware_concurrency())));
+  if (threads <= 0) threads = std::min(32, available_cpus());
   running_ = true;
   for (int i = 0; i < threads; ++i) {
     auto r = std::make_unique<Reactor>();

@@ -5,7 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <emmintrin.h>
+#include <immintrin.h>
 
 namespace die {
 
@@ -493,9 +493,82 @@ inline bool fast_simple_float(const char*& p, const char* end, float& out) {
   return true;
 }
 
+// ---- SSE token converter ---------------------------------------------------------------------
+// For a token "d+" or "d+.d+" of length L <= 16 (sign already stripped): one pshufb removes the dot
+// and right-aligns the digits into 16 lanes, pmaddubsw/pmaddwd fold them into two 8-digit halves.
+// The shuffle masks depend only on (L, dot position) and are built once.
+struct ShufTable {
+  alignas(16) uint8_t m[17][17][16];  // [L][dot index or 16 = none][lane]
+  ShufTable() {
+    for (int L = 0; L <= 16; ++L)
+      for (int d = 0; d <= 16; ++d) {
+        // source positions of the digits, in order
+        int src[16], n = 0;
+        for (int i = 0; i < L && i < 16; ++i)
+          if (i != d) src[n++] = i;
+        for (int k = 0; k < 16; ++k) {
+          const int from_right = 15 - k;  // lane k holds the digit `from_right` places from the end
+          m[L][d][k] = from_right < n ? static_cast<uint8_t>(src[n - 1 - from_right]) : 0x80;  // 0x80 -> zero
+        }
+      }
+  }
+};
+const ShufTable kShuf;
+
+// Returns false (caller falls back) for anything but plain decimal digits with at most one dot.
+inline bool parse_token_sse(const char* b, long len, float& out, bool neg) {
+  const __m128i raw = _mm_loadu_si128(reinterpret_cast<const __m128i*>(b));
+  const __m128i dotm = _mm_cmpeq_epi8(raw, _mm_set1_epi8('.'));
+  const uint32_t lenmask = (1u << len) - 1u;
+  const uint32_t dots = static_cast<uint32_t>(_mm_movemask_epi8(dotm)) & lenmask;
+  const __m128i dig = _mm_sub_epi8(raw, _mm_set1_epi8('0'));
+  // digit lanes: (unsigned) dig <= 9
+  const __m128i isdig = _mm_cmpeq_epi8(_mm_min_epu8(dig, _mm_set1_epi8(9)), dig);
+  const uint32_t digs = static_cast<uint32_t>(_mm_movemask_epi8(isdig)) & lenmask;
+  if ((digs | dots) != lenmask || (dots & (dots - 1))) return false;  // bad char or >1 dot
+  const int d = dots ? __builtin_ctz(dots) : 16;
+  const int ndig = static_cast<int>(len) - (dots ? 1 : 0);
+  if (d == 0 || d == len - 1) return false;  // ".5" / "5." are not JSON
+  if (b[0] == '0' && (d == 16 ? len > 1 : d > 1)) return false;  // leading zero
+  const int frac = dots ? static_cast<int>(len) - 1 - d : 0;
+  if (ndig > 16 || frac > 10) return false;
+  const __m128i aligned = _mm_shuffle_epi8(dig, _mm_load_si128(reinterpret_cast<const __m128i*>(kShuf.m[len][d])));
+  // pairs -> 2-digit, quads -> 4-digit, octets -> 8-digit values
+  const __m128i t1 = _mm_maddubs_epi16(aligned, _mm_setr_epi8(10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1));
+  const __m128i t2 = _mm_madd_epi16(t1, _mm_setr_epi16(100, 1, 100, 1, 100, 1, 100, 1));
+  const __m128i t3 = _mm_packus_epi32(t2, t2);
+  const __m128i t4 = _mm_madd_epi16(t3, _mm_setr_epi16(10000, 1, 10000, 1, 10000, 1, 10000, 1));
+  const uint64_t hi = static_cast<uint32_t>(_mm_cvtsi128_si32(t4));
+  const uint64_t lo = static_cast<uint32_t>(_mm_extract_epi32(t4, 1));
+  const uint64_t mant = hi * 100000000ull + lo;
+  float v;
+  if (mant <= (1u << 24) && frac <= 10) {
+    v = static_cast<float>(static_cast<uint32_t>(mant)) / kPow10f[frac];
+  } else {
+    if (mant > (1ull << 53)) return false;
+    const double dv = static_cast<double>(mant) / kPow10[frac];
+    uint64_t bits;
+    std::memcpy(&bits, &dv, sizeof bits);
+    if ((bits & ((1ull << 29) - 1)) == (1ull << 28)) return false;
+    v = static_cast<float>(dv);
+  }
+  uint32_t vb;
+  std::memcpy(&vb, &v, 4);
+  vb |= static_cast<uint32_t>(neg) << 31;
+  std::memcpy(&out, &vb, 4);
+  return true;
+}
+
 // Parse one token [b, e) known to be delimited by separators (no whitespace inside).  Independent
 // of every other token, so consecutive calls overlap in the out-of-order core.
+bool g_token_simd = true;  // A/B switch for benchmarks (set_json_simd)
+
 inline bool parse_token(const char* b, const char* e, float& out) {
+  if (g_token_simd) {
+    const bool neg = *b == '-';
+    const long len = e - b - neg;
+    if (len > 0 && len <= 16 && parse_token_sse(b + neg, len, out, neg)) return true;
+  }
   const bool neg = *b == '-';
   b += neg;
   const long len = e - b;
@@ -855,4 +928,8 @@ bool find_top_level_string(std::string_view body, std::string_view key, std::str
   }
 }
 
+}  // namespace die
+
+namespace die {
+void set_json_simd(bool on) { g_token_simd = on; }
 }  // namespace die

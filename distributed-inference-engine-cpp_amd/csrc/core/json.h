@@ -125,4 +125,7 @@ int parse_infer_body(std::string_view body, InferBodySink& sink);
 // other members are skipped.  Returns false if the key is absent or not a string.
 bool find_top_level_string(std::string_view body, std::string_view key, std::string& out);
 
+// Benchmark switch: false disables the SSE token converter (scalar SWAR path only).
+void set_json_simd(bool on);
+
 }  // namespace die

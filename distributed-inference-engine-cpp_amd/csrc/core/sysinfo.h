@@ -1,0 +1,33 @@
+// CPU budget of this process: min(affinity mask size, cgroup v2 cpu.max quota).  GPU boxes expose
+// the whole machine in the affinity mask (hundreds of CPUs) but enforce a quota of ~16 CPUs per
+// GPU; sizing thread pools from hardware_concurrency() there oversubscribes the quota.
+#pragma once
+
+#include <sched.h>
+
+#include <cmath>
+#include <cstdio>
+#include <thread>
+
+namespace die {
+
+inline int available_cpus() {
+  static const int n = [] {
+    int cpus = static_cast<int>(std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = CPU_COUNT(&set);
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[64] = {0};
+      long period = 0;
+      if (std::fscanf(f, "%63s %ld", quota, &period) == 2 && period > 0 && quota[0] != 'm') {
+        const double q = std::atof(quota) / static_cast<double>(period);
+        if (q > 0) cpus = std::min(cpus, static_cast<int>(std::ceil(q)));
+      }
+      std::fclose(f);
+    }
+    return cpus < 1 ? 1 : cpus;
+  }();
+  return n;
+}
+
+}  // namespace die

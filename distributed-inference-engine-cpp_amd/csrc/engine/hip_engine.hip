@@ -85,6 +85,8 @@ class HipEngine : public Engine {
 
     ws_bytes_ = 64u << 20;  // split-K partials (choose_splits / autotune stay within it)
     HIP_CHECK(hipMalloc(&ws_, ws_bytes_));
+    HIP_CHECK(hipMalloc(&zeros_, 4096));
+    HIP_CHECK(hipMemset(zeros_, 0, 4096));
     // Validate every op eagerly at the largest bucket, tune, then capture one graph per
     // (bucket, slot).
     for (int s = 0; s < depth_; ++s) encode_forward(max_batch_, s, s_compute_);
@@ -134,6 +136,7 @@ class HipEngine : public Engine {
     (void)hipFree(params_);
     (void)hipFree(arena_);
     (void)hipFree(ws_);
+    (void)hipFree(zeros_);
     (void)hipStreamDestroy(s_compute_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -280,6 +283,7 @@ class HipEngine : public Engine {
     a.scale2 = prm_ptr(op.s2_off);
     a.shift2 = prm_ptr(op.b2_off);
     a.out2 = static_cast<uint16_t*>(buf_ptr(op.out2, s));
+    a.zeros = zeros_;
     return a;
   }
 
@@ -320,7 +324,7 @@ class HipEngine : public Engine {
         const int nk = base.Kpad / 64;
         float best = 1e30f;
         Tune bt{kern::choose_tile(base.M, base.N, base.K), 1};
-        for (int tile = 0; tile < kern::NUM_TILES; ++tile) {
+        for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
           for (int sp = 1; sp <= 16; sp *= 2) {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
             kern::ConvArgs a = base;
@@ -465,6 +469,7 @@ class HipEngine : public Engine {
   uint8_t* arena_ = nullptr;
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;
+  uint16_t* zeros_ = nullptr;
   std::vector<std::vector<Tune>> tune_;  // [bucket][op]
   double tuned_conv_us_ = 0;
   hipStream_t s_compute_{}, s_h2d_{}, s_d2h_{};

@@ -75,6 +75,10 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   }
 }
 
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
+                                              int m0, int n0, int wm, int wn, int lane, int tid);
+
 template <int BM, int BN, int MODE, int VEC>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const int kt_per_split) {
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave pixels / channels
@@ -219,7 +223,16 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     if (more) store_stage(cur ^ 1);
     __syncthreads();
   }
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid);
+}
 
+// Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
+// past their last operand read).
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
+                                              int m0, int n0, int wm, int wn, int lane, int tid) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
   const int lm = lane & 15;
   const int ln = (lane >> 4) * 4;
   if ((p.N & 7) == 0) {
@@ -304,8 +317,154 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// v3 main loop: operands stream global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging,
+// no ds_write), STAGES-deep ring with a counted `s_waitcnt vmcnt(N)` and a raw s_barrier per K-step,
+// so STAGES-1 K-steps stay in flight across the barrier.  The DMA writes 1 KiB per wave-instruction
+// lane-linearly (8 rows x 128 B), so the (row>>1)&7 chunk swizzle goes on the per-lane SOURCE
+// address.  Padding pixels and M tails read a zero page instead of being predicated.
+// MODE 0: dense rows (1x1/s1 conv, GEMM), K % 64 == 0.  MODE 2: implicit conv with Cin % 64 == 0
+// (one 64-channel K-step never straddles a filter tap, so the tap is wave-uniform per K-step).
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+__device__ __forceinline__ void glds16(const uint16_t* g, uint16_t* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int BM, int BN, int MODE, int STAGES>
+__global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, STAGE = A_ELEMS + B_ELEMS;
+  constexpr int GA = BN / 32, GB = BM / 32, G = GA + GB;  // DMA instructions per wave per stage
+  constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int tile_n = blockIdx.x % ntn;
+  const int tile_m = blockIdx.x / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk_total = p.Kpad / BK;
+  const int kt_begin = blockIdx.y * kt_per_split;
+  const int kt_end = min(nk_total, kt_begin + kt_per_split);
+  const int nk = kt_end - kt_begin;
+
+  // Per-lane DMA sources.  Wave `wave` fills rows [wave*R/4, (wave+1)*R/4) of each operand, 8 rows
+  // per instruction; lane L -> row (L>>3) of that group, physical chunk L&7.
+  const uint16_t* asrc[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
+  }
+  const uint16_t* bsrc[GB];  // MODE 0: row base; MODE 2: image base + channel chunk
+  int bih[GB], biw[GB];
+  bool bval[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int r = wave * (BM / 4) + i * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int m = m0 + r;
+    bval[i] = m < p.M;
+    const int mm = bval[i] ? m : 0;
+    if (MODE == 0) {
+      bsrc[i] = p.x + static_cast<size_t>(mm) * p.Cin + c * 8;
+      bih[i] = biw[i] = 0;
+    } else {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int rr = mm - b * hw;
+      const int oh = rr / p.Wo;
+      const int ow = rr - oh * p.Wo;
+      bih[i] = oh * p.stride - p.pad_h;
+      biw[i] = ow * p.stride - p.pad_w;
+      bsrc[i] = p.x + static_cast<size_t>(b) * p.H * p.W * p.Cin + c * 8;
+    }
+  }
+  const int cpt = p.Cin / BK;  // K-steps per filter tap (MODE 2)
+
+  auto issue = [&](int kt, int buf) {
+    uint16_t* A = lds + buf * STAGE;
+    uint16_t* Bt = A + A_ELEMS;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) glds16(asrc[i] + k0, A + (wave * (BN / 4) + i * 8) * BK);
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < GB; ++i) glds16(bval[i] ? bsrc[i] + k0 : p.zeros, Bt + (wave * (BM / 4) + i * 8) * BK);
+    } else {
+      const int tap = kt / cpt;
+      const int ci0 = (kt - tap * cpt) * BK;
+      const int ky = tap / p.KW;
+      const int kx = tap - ky * p.KW;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int ih = bih[i] + ky * p.dil;
+        const int iw = biw[i] + kx * p.dil;
+        const bool v = bval[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const uint16_t* src = v ? bsrc[i] + (static_cast<size_t>(ih) * p.W + iw) * p.Cin + ci0 : p.zeros;
+        glds16(src, Bt + (wave * (BM / 4) + i * 8) * BK);
+      }
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(kt_begin + s, s);
+
+  for (int t = 0; t < nk; ++t) {
+    // Stage t has landed for this wave once at most (STAGES-2) younger stages are outstanding.
+    if (STAGES == 3 && t + 1 < nk) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(kt_begin + t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    const uint16_t* A = lds + (t % STAGES) * STAGE;
+    const uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int chunk = s * 4 + (lane >> 4);
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * WN + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // all operand reads done before the epilogue reuses the LDS
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid);
+}
+
 template <int BM, int BN>
-hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
+hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   const bool dense1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
                         a.W == a.Wo;
   const int vec = a.Cin % 8 == 0 ? 8 : 4;
@@ -317,7 +476,18 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   ConvArgs b = a;
   b.splits = eff;
   dim3 grid(tiles, eff);
-  if (dense1x1 && vec == 8) {
+  if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
+    const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
+    const bool mode2 = !dense1x1 && a.Cin % BK == 0;
+    if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
+    if (variant == 1) {
+      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, 2>), grid, dim3(256), 0, s, b, kt_per);
+      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, 2>), grid, dim3(256), 0, s, b, kt_per);
+    } else {
+      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, 3>), grid, dim3(256), 0, s, b, kt_per);
+      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, 3>), grid, dim3(256), 0, s, b, kt_per);
+    }
+  } else if (dense1x1 && vec == 8) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), grid, dim3(256), 0, s, b, kt_per);
   } else if (vec == 8) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8>), grid, dim3(256), 0, s, b, kt_per);
@@ -335,7 +505,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
 }  // namespace
 
 void tile_dims(int cfg, int& bm, int& bn) {
-  switch (cfg) {
+  switch (cfg % NUM_TILES) {
     case TILE_128x128: bm = 128; bn = 128; break;
     case TILE_128x64: bm = 128; bn = 64; break;
     case TILE_64x128: bm = 64; bn = 128; break;
@@ -378,11 +548,13 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (!a.out && !a.out_f32 && !a.out2) return hipErrorInvalidValue;
   if (a.out2 && (!a.scale2 || !a.shift2)) return hipErrorInvalidValue;
   if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
-  switch (cfg) {
-    case TILE_128x128: return launch_cfg<128, 128>(a, s);
-    case TILE_128x64: return launch_cfg<128, 64>(a, s);
-    case TILE_64x128: return launch_cfg<64, 128>(a, s);
-    default: return launch_cfg<64, 64>(a, s);
+  if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
+  const int variant = cfg / NUM_TILES;
+  switch (cfg % NUM_TILES) {
+    case TILE_128x128: return launch_cfg<128, 128>(a, s, variant);
+    case TILE_128x64: return launch_cfg<128, 64>(a, s, variant);
+    case TILE_64x128: return launch_cfg<64, 128>(a, s, variant);
+    default: return launch_cfg<64, 64>(a, s, variant);
   }
 }
 

@@ -35,9 +35,14 @@ struct ConvArgs {
   // and applies the epilogue.  splits == 1 -> epilogue fused in the GEMM kernel.
   int splits = 1;
   float* ws = nullptr;
+  // >= 16 zero bytes (device): source of the LDS-DMA loads for padding pixels / M tails.
+  const uint16_t* zeros = nullptr;
 };
 
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4 };
+// A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),
+// 1 = LDS-DMA 2-stage ring, 2 = LDS-DMA 3-stage ring (variants 1/2: 1x1 with K % 64 == 0, or
+// Cin % 64 == 0; they return hipErrorInvalidValue otherwise so a tuner can skip them).
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 12 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

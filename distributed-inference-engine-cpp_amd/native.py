@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
         sig("die_gateway_stop", None, vp)
         sig("die_gateway_destroy", None, vp)
         sig("die_loadgen_run", vp, cp, errp)
+        sig("die_parse_bench", C.c_double, cp, C.c_long, C.c_int, C.c_int)
         _LIB = L
     return _LIB
 
@@ -139,6 +140,11 @@ def parse_infer(body: bytes, cap: int) -> Tuple[str, np.ndarray, int]:
     if n < 0:
         _raise_if(err, "parse_infer")
     return _take_str(idp.value), out[: min(n, cap)], n
+
+
+def parse_bench(body: bytes, iters: int = 20, simd: bool = True) -> float:
+    """Average microseconds to parse `body` as an /infer request (host parser benchmark)."""
+    return lib().die_parse_bench(body, len(body), iters, int(simd))
 
 
 def format_floats(v: np.ndarray) -> str:

@@ -79,6 +79,8 @@ def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=No
     out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
     geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad, pad_w=pad,
                 dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2), splits=int(splits))
+    zeros = torch.zeros(2048, dtype=torch.int16, device=dev)
+    geom["zeros"] = int(zeros.data_ptr())
     ws = None
     if splits > 1:
         ws = torch.empty(splits * B * Ho * Wo * cout, dtype=torch.float32, device=dev)
@@ -87,6 +89,8 @@ def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=No
     rc = L.die_kern_conv(json.dumps(geom).encode(), _ptr(x_nhwc.contiguous()), _ptr(wp), _ptr(bias_p),
                          _ptr(res.contiguous() if res is not None else None), 0 if out_f32 else _ptr(out),
                          _ptr(out) if out_f32 else 0, _ptr(s2_p), _ptr(b2_p), _ptr(out2), tile, _stream())
+    if rc != 0 and tile >= 0 and rc == 1:  # hipErrorInvalidValue: config not applicable to this shape
+        return None, None
     _check(rc, "conv_igemm")
     return out, out2
 

@@ -79,6 +79,41 @@ def test_conv_all_tiles_and_epilogue(native, tile, splits):
     assert rel_err(out2, u) < 5e-3
 
 
+@pytest.mark.parametrize("shape", [
+    (3, 28, 128, 256, 1, 1, 0),   # dense 1x1, M tail (3*784 = 2352 not a multiple of 128)
+    (2, 14, 256, 256, 3, 1, 1),   # implicit 3x3, padding
+    (2, 28, 128, 128, 3, 2, 1),   # implicit 3x3 stride 2
+    (2, 14, 512, 1024, 1, 2, 0),  # strided 1x1 (implicit path)
+])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_conv_every_variant(native, shape, splits):
+    """All 12 launch configs (4 tiles x {register-staged, LDS-DMA 2-stage, LDS-DMA 3-stage})."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B, H, Cin, Cout, k, s, p = shape
+    g = torch.Generator(device="cuda").manual_seed(11 + splits)
+    x = torch.randn(B, Cin, H, H, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, k, k, device="cuda", generator=g) / (Cin * k * k) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Cout, device="cuda", generator=g)
+    res = torch.randn(B, (H + 2 * p - k) // s + 1, (H + 2 * p - k) // s + 1, Cout, device="cuda",
+                      generator=g).to(torch.bfloat16)
+    ref = torch.relu(torch.nn.functional.conv2d(x.float(), w.float(), bias, stride=s, padding=p).permute(0, 2, 3, 1)
+                     + res.float())
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    ran = []
+    for cfg in range(12):
+        out, _ = K.conv2d_nhwc(xn, w.float(), bias=bias, stride=s, pad=p, relu=True, res=res, tile=cfg,
+                               splits=splits)
+        if out is None:
+            continue
+        torch.cuda.synchronize()
+        assert rel_err(out, ref) < 5e-3, (cfg, rel_err(out, ref))
+        ran.append(cfg)
+    assert any(c >= 4 for c in ran), "LDS-DMA variants must apply to these shapes"
+    assert any(c >= 8 for c in ran)
+
+
 def test_stem_conv_with_input_prep(native):
     torch = _t()
     from die_amd.ops import kernels as K

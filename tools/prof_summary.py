@@ -44,28 +44,39 @@ def main():
     starts = [i for i, r in enumerate(trace) if first in r["Kernel_Name"]]
     fw = None
     for s in reversed(starts):
-        if s + len(ops) <= len(trace):
-            fw = trace[s:s + len(ops)]
+        # group helper kernels (split-K reduce) with the op that launched them
+        grp, i = [], s
+        while i < len(trace) and len(grp) < len(ops):
+            g = [trace[i]]
+            i += 1
+            while i < len(trace) and "splitk_epilogue" in trace[i]["Kernel_Name"]:
+                g.append(trace[i])
+                i += 1
+            grp.append(g)
+        if len(grp) == len(ops):
+            fw = grp
             break
     if fw is None:
         return
-    t0 = int(fw[0]["Start_Timestamp"])
-    t1 = int(fw[-1]["End_Timestamp"])
-    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in fw)
+    t0 = int(fw[0][0]["Start_Timestamp"])
+    t1 = int(fw[-1][-1]["End_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for g in fw for r in g)
     print("## One forward (batch %d), op by op\n" % a.batch)
     print("Span %.1f us, kernel busy %.1f us (%.0f%%), %d kernels; %s\n" % ((t1 - t0) / 1e3, busy / 1e3,
                                                                           100 * busy / max(1, t1 - t0), len(fw),
                                                                           plan["summary"]))
     print("| # | op | kernel | us | GFLOP | TFLOP/s | N | K | KxK/s | epilogue |\n|---:|---|---|---:|---:|---:|---:|---:|---|---|")
-    for i, (r, op) in enumerate(zip(fw, ops)):
-        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    for i, (g, op) in enumerate(zip(fw, ops)):
+        r = g[0]
+        us = sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in g) / 1e3
         gf = op.get("gflop", 0.0) * a.batch
         epi = ""
         if op["kind"] == "conv":
             epi = "+".join(k for k in ("relu", "residual", "dual_store") if op.get(k))
-        print("| %d | %s | `%s` | %.1f | %.2f | %s | %s | %s | %s | %s |" % (
-            i, op["name"][:40], r["Kernel_Name"].split("(")[0][-40:], us, gf,
-            ("%.0f" % (gf / us * 1e-3 * 1e3)) if gf else "", op.get("N", ""), op.get("K", ""),
+        print("| %d | %s | `%s`%s | %.1f | %.2f | %s | %s | %s | %s | %s |" % (
+            i, op["name"][:40], r["Kernel_Name"].split("(")[0].replace("void ", "").replace("die::kern::(anonymous namespace)::", "")[-44:],
+            " +splitK" if len(g) > 1 else "", us, gf,
+            ("%.0f" % (gf / us * 1e3)) if gf else "", op.get("N", ""), op.get("K", ""),
             ("%sx%s/%s" % (op.get("KH"), op.get("KH"), op.get("stride"))) if op["kind"] == "conv" else "", epi))
 
 
