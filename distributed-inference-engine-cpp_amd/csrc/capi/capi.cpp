@@ -299,6 +299,31 @@ float* die_cpu_run(const char* model_path, const float* in, const int64_t* shape
   }
 }
 
+// Debug probe: run the CPU executor and return intermediate value `name` (f32; ints converted).
+float* die_cpu_run_value(const char* model_path, const float* in, const int64_t* shape, int rank, const char* name,
+                         int64_t* out_shape, int* out_rank, char** err) {
+  try {
+    CpuExecutor ex(onnx::load_onnx(model_path));
+    auto x = std::make_shared<CpuValue>();
+    x->shape.assign(shape, shape + rank);
+    x->f.assign(in, in + x->numel());
+    std::unordered_map<std::string, CpuValuePtr> trace;
+    ex.run(x, &trace);
+    auto it = trace.find(name);
+    if (it == trace.end()) throw std::runtime_error(std::string("no value named ") + name);
+    const CpuValue& v = *it->second;
+    *out_rank = static_cast<int>(v.shape.size());
+    for (size_t k = 0; k < v.shape.size(); ++k) out_shape[k] = v.shape[k];
+    const size_t n = static_cast<size_t>(v.numel());
+    float* o = static_cast<float*>(std::malloc(sizeof(float) * std::max<size_t>(n, 1)));
+    for (size_t k = 0; k < n; ++k) o[k] = v.is_int ? static_cast<float>(v.i[k]) : v.f[k];
+    return o;
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
 char* die_onnx_summary(const char* model_path, char** err) {
   try {
     auto m = onnx::load_onnx(model_path);

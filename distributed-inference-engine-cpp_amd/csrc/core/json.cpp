@@ -563,6 +563,58 @@ inline bool parse_token_sse(const char* b, long len, float& out, bool neg) {
 // of every other token, so consecutive calls overlap in the out-of-order core.
 bool g_token_simd = true;  // A/B switch for benchmarks (set_json_simd)
 
+// mantissa (<= 16 digits) and fraction digits -> float with the same rounding rules as above.
+inline bool finish_float(uint64_t mant, int frac, bool neg, float& out) {
+  float v;
+  if (mant <= (1u << 24)) {
+    v = static_cast<float>(static_cast<uint32_t>(mant)) / kPow10f[frac];
+  } else {
+    if (mant > (1ull << 53)) return false;
+    const double dv = static_cast<double>(mant) / kPow10[frac];
+    uint64_t bits;
+    std::memcpy(&bits, &dv, sizeof bits);
+    if ((bits & ((1ull << 29) - 1)) == (1ull << 28)) return false;
+    v = static_cast<float>(dv);
+  }
+  uint32_t vb;
+  std::memcpy(&vb, &v, 4);
+  vb |= static_cast<uint32_t>(neg) << 31;
+  std::memcpy(&out, &vb, 4);
+  return true;
+}
+
+// Two tokens per AVX2 pass: pshufb / maddubs / madd work within 128-bit lanes, so lane 0 converts
+// token a and lane 1 token b with the same instruction stream (the per-token work of
+// parse_token_sse at half the instructions).  Tokens are sign-stripped, 1..16 chars.
+inline bool parse_token_pair_avx2(const char* a, long la, bool na, const char* b, long lb, bool nb, float& oa,
+                                  float& ob) {
+  const __m256i raw = _mm256_loadu2_m128i(reinterpret_cast<const __m128i*>(b), reinterpret_cast<const __m128i*>(a));
+  const uint32_t lenmask = ((1u << la) - 1u) | (((1u << lb) - 1u) << 16);
+  const uint32_t dots = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(raw, _mm256_set1_epi8('.')))) & lenmask;
+  const __m256i dig = _mm256_sub_epi8(raw, _mm256_set1_epi8('0'));
+  const __m256i isdig = _mm256_cmpeq_epi8(_mm256_min_epu8(dig, _mm256_set1_epi8(9)), dig);
+  const uint32_t digs = static_cast<uint32_t>(_mm256_movemask_epi8(isdig)) & lenmask;
+  const uint32_t da = dots & 0xFFFFu, db = dots >> 16;
+  if ((digs | dots) != lenmask || (da & (da - 1)) || (db & (db - 1))) return false;
+  const int pa = da ? __builtin_ctz(da) : 16, pb = db ? __builtin_ctz(db) : 16;
+  if (pa == 0 || pb == 0 || (da && pa == la - 1) || (db && pb == lb - 1)) return false;
+  if ((a[0] == '0' && (da ? pa > 1 : la > 1)) || (b[0] == '0' && (db ? pb > 1 : lb > 1))) return false;
+  const int fa = da ? static_cast<int>(la) - 1 - pa : 0, fb = db ? static_cast<int>(lb) - 1 - pb : 0;
+  if (fa > 10 || fb > 10) return false;
+  const __m256i shuf = _mm256_loadu2_m128i(reinterpret_cast<const __m128i*>(kShuf.m[lb][pb]),
+                                           reinterpret_cast<const __m128i*>(kShuf.m[la][pa]));
+  const __m256i aligned = _mm256_shuffle_epi8(dig, shuf);
+  const __m256i t1 = _mm256_maddubs_epi16(aligned, _mm256_set1_epi16(0x010A));  // bytes (10, 1)
+  const __m256i t2 = _mm256_madd_epi16(t1, _mm256_set1_epi32(0x00010064));      // words (100, 1)
+  const __m256i t3 = _mm256_packus_epi32(t2, t2);
+  const __m256i t4 = _mm256_madd_epi16(t3, _mm256_set1_epi32(0x00012710));      // words (10000, 1)
+  const uint64_t ma = static_cast<uint64_t>(static_cast<uint32_t>(_mm256_extract_epi32(t4, 0))) * 100000000ull +
+                      static_cast<uint32_t>(_mm256_extract_epi32(t4, 1));
+  const uint64_t mb = static_cast<uint64_t>(static_cast<uint32_t>(_mm256_extract_epi32(t4, 4))) * 100000000ull +
+                      static_cast<uint32_t>(_mm256_extract_epi32(t4, 5));
+  return finish_float(ma, fa, na, oa) && finish_float(mb, fb, nb, ob);
+}
+
 inline bool parse_token(const char* b, const char* e, float& out) {
   if (g_token_simd) {
     const bool neg = *b == '-';
@@ -633,6 +685,29 @@ inline const char* bulk_float_array(const char* p, const char* end, float* dst, 
     sep_masks(base, comma, close);
     uint64_t m = comma | close;
     while (m) {
+      const uint64_t m2 = m & (m - 1);
+      if (m2 && g_token_simd && !((close >> __builtin_ctzll(m)) & 1)) {
+        // two complete tokens in this block: convert them together
+        const char* sep1 = base + __builtin_ctzll(m);
+        const char* sep2 = base + __builtin_ctzll(m2);
+        const char* t2 = sep1 + 1;
+        const bool n1 = *tok == '-', n2 = *t2 == '-';
+        const long l1 = sep1 - tok - n1, l2 = sep2 - t2 - n2;
+        float f1, f2;
+        if (l1 > 0 && l1 <= 16 && l2 > 0 && l2 <= 16 &&
+            parse_token_pair_avx2(tok + n1, l1, n1, t2 + n2, l2, n2, f1, f2)) {
+          if (n < cap) dst[n] = f1;
+          if (n + 1 < cap) dst[n + 1] = f2;
+          n += 2;
+          tok = sep2 + 1;
+          if ((close >> (sep2 - base)) & 1) {
+            done = true;
+            return tok;
+          }
+          m = m2 & (m2 - 1);
+          continue;
+        }
+      }
       const int s = __builtin_ctzll(m);
       const char* sep = base + s;
       float v;

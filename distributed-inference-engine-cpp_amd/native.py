@@ -319,6 +319,28 @@ def cpu_run(model_path: str, x: np.ndarray) -> np.ndarray:
     return arr.reshape(shp)
 
 
+def cpu_run_value(model_path: str, x: np.ndarray, name: str) -> np.ndarray:
+    """Intermediate value `name` of a CPU-executor run (debugging / per-op parity tests)."""
+    L = lib()
+    fn = L.die_cpu_run_value
+    fn.restype = C.c_void_p
+    fn.argtypes = [C.c_char_p, C.POINTER(C.c_float), C.POINTER(C.c_int64), C.c_int, C.c_char_p,
+                   C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_void_p)]
+    x = np.ascontiguousarray(x, np.float32)
+    shape = (C.c_int64 * x.ndim)(*x.shape)
+    out_shape = (C.c_int64 * 8)()
+    out_rank = C.c_int(0)
+    err = _err_box()
+    p = fn(model_path.encode(), _f32(x), shape, x.ndim, name.encode(), out_shape, C.byref(out_rank), C.byref(err))
+    if not p:
+        _raise_if(err, "cpu_run_value")
+    shp = tuple(out_shape[i] for i in range(out_rank.value))
+    n = int(np.prod(shp)) if shp else 1
+    arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n,)).copy()
+    L.die_free(p)
+    return arr.reshape(shp)
+
+
 def onnx_summary(model_path: str) -> Dict[str, Any]:
     err = _err_box()
     p = lib().die_onnx_summary(model_path.encode(), C.byref(err))

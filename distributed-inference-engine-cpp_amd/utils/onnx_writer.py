@@ -73,7 +73,7 @@ def f_packed_floats(field_no: int, vals: Iterable[float]) -> bytes:
 # ---- messages -------------------------------------------------------------------------------------
 
 def tensor_proto(name: str, arr: np.ndarray, use_raw: bool = True) -> bytes:
-    arr = np.ascontiguousarray(arr)
+    arr = np.asarray(arr, order="C")  # (ascontiguousarray would turn a 0-d scalar into shape (1,))
     dt = _NP2ONNX[arr.dtype]
     out = bytearray()
     for d in arr.shape:
@@ -166,7 +166,7 @@ class GraphBuilder:
 
     def init(self, name: str, arr: np.ndarray) -> str:
         assert name not in self.initializers, name
-        self.initializers[name] = np.ascontiguousarray(arr)
+        self.initializers[name] = np.asarray(arr, order="C")
         return name
 
     def const(self, arr, prefix: str = "const") -> str:
