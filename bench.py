@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--connections", type=int, default=50, help="client connections per GPU (reference: 50 threads)")
     ap.add_argument("--mode", choices=["http", "engine"], default="http")
-    ap.add_argument("--model", default="")
+    ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
+    ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
+                    help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=2)
     args = ap.parse_args()
 
@@ -56,14 +58,21 @@ def main():
 
     import die_amd  # noqa: F401
     from die_amd import native
-    from die_amd.models import resnet_v2 as r
+    if args.arch == "vit_b16":
+        from die_amd.models import vit as r
 
-    cfg = r.ResNetConfig()
+        cfg = r.ViTConfig()
+        model_name, fname = "ViT-B/16 (ONNX, generated)", "vit-b16.onnx"
+    else:
+        from die_amd.models import resnet_v2 as r
+
+        cfg = r.ResNetConfig()
+        model_name, fname = "ResNet50-v2-7 (ONNX, generated)", "resnet50-v2-7.onnx"
     model = args.model
     tmpdir = None
     if not model:
         tmpdir = tempfile.mkdtemp(prefix="die_bench_%d_" % rank)
-        model = os.path.join(tmpdir, "resnet50-v2-7.onnx")
+        model = os.path.join(tmpdir, fname)
         blob, _ = r.build_onnx(cfg)
         with open(model, "wb") as f:
             f.write(blob)
@@ -130,7 +139,8 @@ def main():
     value = ok / elapsed
     if rank == 0:
         out = {
-            "metric": "requests/sec + p50/p99 latency, ResNet50 ONNX /infer at 1/2/4/8 MI355X",
+            "metric": "requests/sec + p50/p99 latency, %s ONNX /infer at 1/2/4/8 MI355X"
+                      % ("ResNet50" if args.arch == "resnet50" else "ViT-B/16"),
             "value": value,
             "unit": "requests/s",
             "n_gpus": args.gpus,
@@ -139,10 +149,10 @@ def main():
             "ms_per_step": elapsed * 1000.0 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": value / BASELINE_RPS,
+            "vs_baseline": value / BASELINE_RPS if args.arch == "resnet50" else None,
             "dtype": "bf16",
-            "data": "synthetic: unique ResNet-shaped JSON payloads (3x224x224 floats, 4 decimals), random-init weights",
-            "config": {"model": "ResNet50-v2-7 (ONNX, generated)", "global_batch": B * args.gpus, "seq_len": 0,
+            "data": "synthetic: unique image-shaped JSON payloads (3x224x224 floats, 4 decimals), random-init weights",
+            "config": {"model": model_name, "global_batch": B * args.gpus, "seq_len": 0,
                        "parallelism": "dp%d" % args.gpus, "mode": args.mode, "max_batch_per_gpu": B,
                        "requests": int(ok + failed)},
         }

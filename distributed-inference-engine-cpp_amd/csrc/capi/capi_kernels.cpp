@@ -103,6 +103,27 @@ int die_kern_nhwc_to_nchw(uint64_t x, uint64_t y, int B, int H, int W, int C, ui
   return static_cast<int>(kern::nhwc_to_nchw_f32(P<const uint16_t>(x), P<float>(y), B, H, W, C, S(stream)));
 }
 
+int die_kern_layernorm(uint64_t x, uint64_t y, uint64_t gamma, uint64_t beta, float eps, long long rows, int C,
+                       uint64_t stream) {
+  return static_cast<int>(kern::layernorm_rows(P<const uint16_t>(x), P<uint16_t>(y), P<const float>(gamma),
+                                               P<const float>(beta), eps, rows, C, S(stream)));
+}
+
+int die_kern_tokens(uint64_t patches, uint64_t cls, uint64_t pos, uint64_t out, int B, int S0, int C, uint64_t stream) {
+  return static_cast<int>(kern::tokens_assemble(P<const uint16_t>(patches), P<const float>(cls), P<const float>(pos),
+                                                P<uint16_t>(out), B, S0, C, S(stream)));
+}
+
+int die_kern_gather_rows(uint64_t x, uint64_t y, int B, int Sq, int idx, int C, uint64_t stream) {
+  return static_cast<int>(kern::gather_rows(P<const uint16_t>(x), P<uint16_t>(y), B, Sq, idx, C, S(stream)));
+}
+
+int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,
+                       int ldv, int ldo, float scale, uint64_t stream) {
+  return static_cast<int>(kern::attention(P<const uint16_t>(q), P<const uint16_t>(k), P<const uint16_t>(v),
+                                          P<uint16_t>(out), B, Sq, H, D, ldq, ldk, ldv, ldo, scale, S(stream)));
+}
+
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
 char* die_plan_summary(const char* model_path, int max_batch, char** err) {
   try {
@@ -115,7 +136,7 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
     Json ops = Json::array();
     for (auto& o : p.ops) {
       Json e = Json::object();
-      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32"};
+      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention"};
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;
@@ -129,6 +150,8 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
         e["dual_store"] = o.out2 >= 0;
         e["store_main"] = o.out >= 0 || o.out_f32 != -1;
         e["relu2"] = o.conv.relu2;
+        e["act"] = o.conv.relu;
+        e["rows"] = o.conv.Ho * o.conv.Wo;
       }
       ops.push_back(e);
     }

@@ -14,9 +14,11 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <iostream>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
@@ -312,6 +314,7 @@ class HipEngine : public Engine {
     HIP_CHECK(hipEventCreate(&e1));
     tune_.assign(buckets_.size(), std::vector<Tune>(plan_.ops.size(), Tune{-1, 1}));
     double total_best_us = 0;
+    std::map<std::string, std::pair<Tune, double>> tuned_shapes;
     for (size_t bi = 0; bi < buckets_.size(); ++bi) {
       const int B = buckets_[bi];
       encode_forward(B, 0, s_compute_);
@@ -321,6 +324,17 @@ class HipEngine : public Engine {
         if (op.kind != PlanOp::CONV) continue;
         kern::ConvArgs base = conv_args(op, B, 0);
         base.ws = ws_;
+        // identical problems (repeated blocks) share one measurement
+        char key[256];
+        std::snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", base.M, base.N, base.K, base.Cin,
+                      base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
+                      base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
+        auto memo = tuned_shapes.find(key);
+        if (memo != tuned_shapes.end()) {
+          tune_[bi][oi] = memo->second.first;
+          if (B == max_batch_) total_best_us += memo->second.second;
+          continue;
+        }
         const int nk = base.Kpad / 64;
         float best = 1e30f;
         Tune bt{kern::choose_tile(base.M, base.N, base.K), 1};
@@ -343,6 +357,7 @@ class HipEngine : public Engine {
           }
         }
         tune_[bi][oi] = bt;
+        tuned_shapes[key] = {bt, best / 3 * 1000.0};
         if (B == max_batch_) total_best_us += best / 3 * 1000.0;
       }
     }
@@ -387,6 +402,24 @@ class HipEngine : public Engine {
         case PlanOp::TO_NCHW_F32:
           e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
                                      op.H, op.W, op.C, st);
+          break;
+        case PlanOp::LAYERNORM:
+          e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
+                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st);
+          break;
+        case PlanOp::TOKENS:
+          e = kern::tokens_assemble(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
+                                    static_cast<uint16_t*>(buf(op.out)), B, op.S, op.C, st);
+          break;
+        case PlanOp::GATHER_ROWS:
+          e = kern::gather_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.S,
+                                op.gidx, op.C, st);
+          break;
+        case PlanOp::ATTENTION:
+          e = kern::attention(static_cast<const uint16_t*>(buf(op.in)) + op.col[0],
+                              static_cast<const uint16_t*>(buf(op.in2)) + op.col[1],
+                              static_cast<const uint16_t*>(buf(op.in3)) + op.col[2], static_cast<uint16_t*>(buf(op.out)),
+                              B, op.S, op.nh, op.hd, op.ld[0], op.ld[1], op.ld[2], op.C, op.fscale, st);
           break;
         case PlanOp::BF16_TO_F32:
           e = kern::bf16_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),

@@ -1,6 +1,8 @@
 #include "hip_plan.h"
 
 #include <algorithm>
+#include <array>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <sstream>
@@ -27,12 +29,40 @@ uint16_t to_bf16(float f) {
 
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+constexpr int64_t kBatchDim = INT64_MIN;  // symbolic batch size inside SHAPE values
+
+// A planner value.  Besides materialised tensors (NHWC images, bf16/f32 rows) the planner keeps
+// lazy views that only become kernels when consumed in a supported way.
 struct Val {
-  enum Kind { GRAPH_IN, NHWC, ROWS_BF16, ROWS_F32 } kind = NHWC;
+  enum Kind {
+    GRAPH_IN,    // f32 NCHW graph input
+    NHWC,        // bf16 [B][H][W][C]
+    ROWS_BF16,   // bf16 rows: logical [B, H*W, C] (rank 3) or [B, C] (rank 2, H*W == 1)
+    ROWS_F32,    // f32 rows (graph output)
+    NCHW_FLAT,   // Reshape(NHWC, [0, C, -1]) : logical [B, C, H*W] over an NHWC buffer
+    HEADS,       // Reshape(rows, [0, 0, nh, hd]) (+ Transposes): base [B, S, nh, hd], logical = perm
+    ATTN,        // attention chain: stage 0 = Q K^T, 1 = softmax, 2 = (P V) with logical perm
+    SHAPE,       // int64 shape-computation value (ints known unless `known` is false)
+    BCAST_INIT,  // Expand(initializer, shape) -> [B, 1, C]
+    TOKCAT       // Concat([cls, patch rows], axis=1)
+  } kind = NHWC;
   int C = 0, H = 1, W = 1;
   int buf = -1;
+  int rank = 0;         // ROWS: 2 or 3
+  int ld = 0, col = 0;  // ROWS/HEADS: row pitch (0 -> C) and column offset, in elements
   bool has_affine = false;
   std::vector<float> asc, ash;
+  // HEADS / ATTN
+  int nh = 0, hd = 0;
+  std::array<int, 4> perm{{0, 1, 2, 3}};
+  int q = -1, k = -1, v = -1, stage = 0;
+  float scale = 1.f;
+  // SHAPE / BCAST_INIT / TOKCAT
+  std::vector<int64_t> ints;
+  bool known = true;
+  std::string init_name;
+  int patches = -1;
+  int pitch() const { return ld ? ld : C; }
 };
 
 class Planner {
@@ -136,16 +166,26 @@ class Planner {
   void lower(int idx) {
     const Node& n = m_.nodes[idx];
     const std::string& op = n.op_type;
+    if (lower_shape_op(idx)) return;
     if (op == "Conv") return lower_conv(idx);
     if (op == "Gemm" || (op == "MatMul" && is_init(n.in(1)))) return lower_gemm(idx);
+    if (op == "MatMul") return lower_attn_matmul(idx);
     if (op == "BatchNormalization") return lower_bn(idx);
     if (op == "Relu") return lower_relu(idx);
     if (op == "Add") return lower_add(idx);
     if (op == "MaxPool" || op == "AveragePool") return lower_pool(idx);
     if (op == "GlobalAveragePool") return lower_gap(idx);
-    if (op == "Flatten" || op == "Reshape" || op == "Squeeze") return lower_flatten(idx);
+    if (op == "Reshape") return lower_reshape(idx);
+    if (op == "Flatten" || op == "Squeeze") return lower_flatten(idx);
+    if (op == "Transpose") return lower_transpose(idx);
+    if (op == "Div" || op == "Mul") return lower_scale(idx);
+    if (op == "Softmax") return lower_softmax(idx);
+    if (op == "LayerNormalization") return lower_layernorm(idx);
+    if (op == "Gather") return lower_gather(idx);
+    if (op == "Concat") return lower_concat(idx);
     if (op == "Identity" || op == "Dropout") {
-      define(n.outputs[0], val(n.in(0), n));
+      Val v = val(n.in(0), n);
+      define(n.outputs[0], v);
       return;
     }
     throw std::runtime_error("HIP engine: unsupported op " + op + " (" + n.name + ")");
@@ -349,79 +389,585 @@ class Planner {
     add_op(std::move(p));
   }
 
+  // ---- GEMM over rows ---------------------------------------------------------------------------
+  bool scalar_is(const std::string& name, float want) const {
+    auto it = m_.initializers.find(name);
+    if (it == m_.initializers.end() || it->second.f.size() != 1) return false;
+    return std::fabs(it->second.f[0] - want) <= 1e-3f * std::fabs(want);
+  }
+  static const std::string& other_input(const Node& nd, const std::string& x) { return nd.in(0) == x ? nd.in(1) : nd.in(0); }
+
+  // erf-GELU as exported by torch: x/sqrt2 -> Erf -> +1 -> (x * .) -> (* 0.5), or 0.5x * (1 + erf).
+  bool match_gelu(const std::string& v, std::vector<int>& used, std::string& out) const {
+    if (graph_outputs_.count(v)) return false;
+    const auto cs = consumers(v);
+    if (cs.size() != 2) return false;
+    int dv = -1, mu = -1;
+    for (int c : cs) {
+      if (done_[c]) return false;
+      const Node& nd = m_.nodes[c];
+      if (nd.op_type == "Div" && nd.in(0) == v && scalar_is(nd.in(1), 1.41421356f)) dv = c;
+      else if (nd.op_type == "Mul" && scalar_is(other_input(nd, v), 0.70710678f)) dv = c;
+      else if (nd.op_type == "Mul") mu = c;
+      else return false;
+    }
+    if (dv < 0 || mu < 0) return false;
+    const int er = sole_consumer(m_.nodes[dv].outputs[0]);
+    if (er < 0 || m_.nodes[er].op_type != "Erf") return false;
+    const int ad = sole_consumer(m_.nodes[er].outputs[0]);
+    if (ad < 0 || m_.nodes[ad].op_type != "Add" || !scalar_is(other_input(m_.nodes[ad], m_.nodes[er].outputs[0]), 1.f))
+      return false;
+    const std::string& a = m_.nodes[ad].outputs[0];
+    const Node& M = m_.nodes[mu];
+    const std::string& mo = other_input(M, v);
+    if (mo == a) {
+      const int hf = sole_consumer(M.outputs[0]);
+      if (hf < 0 || m_.nodes[hf].op_type != "Mul" || !scalar_is(other_input(m_.nodes[hf], M.outputs[0]), 0.5f)) return false;
+      used = {dv, er, ad, mu, hf};
+      out = m_.nodes[hf].outputs[0];
+      return true;
+    }
+    if (scalar_is(mo, 0.5f)) {
+      const int fin = sole_consumer(a);
+      if (fin < 0 || fin != sole_consumer(M.outputs[0]) || m_.nodes[fin].op_type != "Mul") return false;
+      used = {dv, er, ad, mu, fin};
+      out = m_.nodes[fin].outputs[0];
+      return true;
+    }
+    return false;
+  }
+
+  struct GemmTail {
+    std::vector<float> bias;  // from a following Add(initializer), empty if none
+    int act = 0;              // 1 relu, 2 gelu
+    std::string res;          // residual operand (rows)
+    std::string out;
+    std::vector<int> used;
+  };
+  // Epilogue fusion lookahead for a MatMul/Gemm producing `N` columns over `rows` rows per sample.
+  GemmTail gemm_tail(const Node& n, int N, int rows, bool is_gemm) const {
+    GemmTail t;
+    t.out = n.outputs[0];
+    int c1 = sole_consumer(t.out);
+    if (!is_gemm && c1 >= 0 && m_.nodes[c1].op_type == "Add" && is_init(other_input(m_.nodes[c1], t.out))) {
+      const auto& c = m_.initializers.at(other_input(m_.nodes[c1], t.out)).f;
+      if (c.size() == static_cast<size_t>(N) || c.size() == 1) {
+        t.bias.resize(N);
+        for (int j = 0; j < N; ++j) t.bias[j] = c[c.size() == 1 ? 0 : j];
+        t.used.push_back(c1);
+        t.out = m_.nodes[c1].outputs[0];
+        c1 = sole_consumer(t.out);
+      }
+    }
+    std::vector<int> gu;
+    std::string g;
+    if (c1 >= 0 && m_.nodes[c1].op_type == "Relu") {
+      t.act = 1;
+      t.used.push_back(c1);
+      t.out = m_.nodes[c1].outputs[0];
+    } else if (match_gelu(t.out, gu, g)) {
+      t.act = 2;
+      t.used.insert(t.used.end(), gu.begin(), gu.end());
+      t.out = g;
+    } else if (c1 >= 0 && m_.nodes[c1].op_type == "Add") {
+      const Node& add = m_.nodes[c1];
+      const std::string& other = other_input(add, t.out);
+      auto it = vid_.find(other);
+      if (it != vid_.end() && add.in(0) != add.in(1)) {
+        const Val& r = vals_[it->second];
+        if (r.kind == Val::ROWS_BF16 && r.C == N && r.H * r.W == rows && r.pitch() == r.C && r.col == 0) {
+          t.res = other;
+          t.used.push_back(c1);
+          t.out = add.outputs[0];
+          const int c2 = sole_consumer(t.out);
+          if (c2 >= 0 && m_.nodes[c2].op_type == "Relu") {
+            t.act = 1;
+            t.used.push_back(c2);
+            t.out = m_.nodes[c2].outputs[0];
+          }
+        }
+      }
+    }
+    return t;
+  }
+
+  // Sibling MatMuls of one input that each only add a bias and feed a Reshape (Q/K/V projections)
+  // -> one GEMM with concatenated weights.  Returns the group (just {idx} when not applicable).
+  std::vector<int> qkv_group(int idx, const std::string& xname, int K) const {
+    std::vector<int> g;
+    bool self = false;
+    for (int c : consumers(xname)) {
+      if (c != idx && done_[c]) continue;
+      const Node& nd = m_.nodes[c];
+      if (nd.op_type != "MatMul" || nd.in(0) != xname || !is_init(nd.in(1))) continue;
+      const auto& w = m_.initializers.at(nd.in(1));
+      if (w.dims.size() != 2 || w.dims[0] != K || w.dims[1] % 8) continue;
+      const int a = sole_consumer(nd.outputs[0]);
+      if (a < 0 || m_.nodes[a].op_type != "Add" || !is_init(other_input(m_.nodes[a], nd.outputs[0]))) continue;
+      if (m_.initializers.at(other_input(m_.nodes[a], nd.outputs[0])).f.size() != static_cast<size_t>(w.dims[1])) continue;
+      const int r = sole_consumer(m_.nodes[a].outputs[0]);
+      if (r < 0 || m_.nodes[r].op_type != "Reshape") continue;
+      g.push_back(c);
+      self |= c == idx;
+    }
+    if (!self || g.size() < 2) return {idx};
+    return g;
+  }
+
   void lower_gemm(int idx) {
     const Node& n = m_.nodes[idx];
-    Val x = val(n.in(0), n);
-    if (!(x.kind == Val::ROWS_BF16 || (x.kind == Val::NHWC && x.H == 1 && x.W == 1)))
-      throw std::runtime_error(n.op_type + " " + n.name + ": input must be a [batch, features] matrix");
+    const Val x = val(n.in(0), n);
+    const bool gemm = n.op_type == "Gemm";
+    int rows = 1, rank = 2;
+    if (x.kind == Val::ROWS_BF16) {
+      rows = x.H * x.W;
+      rank = x.rank ? x.rank : (rows == 1 ? 2 : 3);
+    } else if (!(x.kind == Val::NHWC && x.H == 1 && x.W == 1)) {
+      throw std::runtime_error(n.op_type + " " + n.name + ": input must be a [batch, (tokens,) features] matrix");
+    }
+    if (x.pitch() != x.C || x.col) throw std::runtime_error(n.op_type + " " + n.name + ": strided input rows");
+    if (gemm && rank != 2) throw std::runtime_error("Gemm " + n.name + ": input must be 2-D");
     const auto& wt = init(n.in(1), n);
     if (wt.dims.size() != 2) throw std::runtime_error(n.op_type + " " + n.name + ": weight must be 2-D");
-    const bool gemm = n.op_type == "Gemm";
     if (gemm && n.get_int("transA", 0)) throw std::runtime_error("Gemm " + n.name + ": transA is not supported");
     const bool tb = gemm && n.get_int("transB", 0);
     const float alpha = gemm ? n.get_float("alpha", 1.f) : 1.f;
     const float beta = gemm ? n.get_float("beta", 1.f) : 1.f;
     const int K = static_cast<int>(tb ? wt.dims[1] : wt.dims[0]);
-    const int N = static_cast<int>(tb ? wt.dims[0] : wt.dims[1]);
     if (K != x.C) throw std::runtime_error(n.op_type + " " + n.name + ": inner dimension mismatch");
     if (K % 8) throw std::runtime_error(n.op_type + " " + n.name + ": K % 8 must be 0");
-    std::vector<float> bias(N, 0.f);
-    if (gemm && !n.in(2).empty()) {
-      const auto& c = init(n.in(2), n).f;
-      for (int j = 0; j < N; ++j) bias[j] = beta * c[c.size() == 1 ? 0 : j % c.size()];
-    }
-    std::string cur = n.outputs[0];
-    int relu = 0;
-    int c1 = sole_consumer(cur);
-    if (!gemm && c1 >= 0 && m_.nodes[c1].op_type == "Add" && is_init(m_.nodes[c1].in(0) == cur ? m_.nodes[c1].in(1) : m_.nodes[c1].in(0))) {
-      const Node& add = m_.nodes[c1];
-      const auto& c = init(add.in(0) == cur ? add.in(1) : add.in(0), add).f;
-      if (c.size() == static_cast<size_t>(N) || c.size() == 1) {
-        for (int j = 0; j < N; ++j) bias[j] += c[c.size() == 1 ? 0 : j];
-        done_[c1] = true;
-        cur = add.outputs[0];
-        c1 = sole_consumer(cur);
-      }
-    }
-    if (c1 >= 0 && m_.nodes[c1].op_type == "Relu") {
-      relu = 1;
-      done_[c1] = true;
-      cur = m_.nodes[c1].outputs[0];
+
+    const std::vector<int> group = gemm ? std::vector<int>{idx} : qkv_group(idx, n.in(0), K);
+    // columns of each member
+    std::vector<int> Ns, offs;
+    int Ntot = 0;
+    for (int gi : group) {
+      const auto& w = init(m_.nodes[gi].in(1), m_.nodes[gi]);
+      const int Nj = static_cast<int>(tb ? w.dims[0] : w.dims[1]);
+      offs.push_back(Ntot);
+      Ns.push_back(Nj);
+      Ntot += Nj;
     }
     const int Kpad = static_cast<int>(round_up(K, 64));
-    const int Npad = static_cast<int>(round_up(N, 128));
+    const int Npad = static_cast<int>(round_up(Ntot, 128));
     std::vector<uint16_t> wp(static_cast<size_t>(Npad) * Kpad, 0);
-    for (int j = 0; j < N; ++j)
-      for (int k = 0; k < K; ++k) {
-        const float w = tb ? wt.f[static_cast<size_t>(j) * K + k] : wt.f[static_cast<size_t>(k) * N + j];
-        wp[static_cast<size_t>(j) * Kpad + k] = to_bf16(alpha * w);
+    std::vector<float> bias(Ntot, 0.f);
+    for (size_t g = 0; g < group.size(); ++g) {
+      const Node& nd = m_.nodes[group[g]];
+      const auto& w = init(nd.in(1), nd);
+      const int Nj = Ns[g];
+      for (int j = 0; j < Nj; ++j)
+        for (int k = 0; k < K; ++k) {
+          const float v = tb ? w.f[static_cast<size_t>(j) * K + k] : w.f[static_cast<size_t>(k) * Nj + j];
+          wp[static_cast<size_t>(offs[g] + j) * Kpad + k] = to_bf16(alpha * v);
+        }
+      if (gemm && !nd.in(2).empty()) {
+        const auto& c = init(nd.in(2), nd).f;
+        for (int j = 0; j < Nj; ++j) bias[offs[g] + j] = beta * c[c.size() == 1 ? 0 : j % c.size()];
       }
+    }
     PlanOp p;
     p.kind = PlanOp::CONV;
-    p.name = n.name;
+    p.name = group.size() > 1 ? n.name + "+qkv" : n.name;
     p.in = x.buf;
     p.w_off = push_bf16(wp);
-    p.bias_off = push_f32(bias);
     auto& a = p.conv;
+    a.H = a.Ho = rows;
     a.Cin = K;
-    a.N = N;
+    a.N = Ntot;
     a.K = K;
     a.Kpad = Kpad;
-    a.relu = relu;
-    p.flops_per_sample = 2.0 * N * K;
-    p.tile_bmax = kern::choose_tile(max_batch_, N, K);
+    p.flops_per_sample = 2.0 * rows * Ntot * K;
+    p.tile_bmax = kern::choose_tile(max_batch_ * rows, Ntot, K);
+
+    if (group.size() > 1) {
+      // bias of each member's Add; outputs are column slices of one [rows][Ntot] buffer
+      p.out = new_buf(static_cast<size_t>(rows) * Ntot * 2);
+      for (size_t g = 0; g < group.size(); ++g) {
+        done_[group[g]] = true;
+        const Node& nd = m_.nodes[group[g]];
+        const int ad = sole_consumer(nd.outputs[0]);
+        const auto& c = m_.initializers.at(other_input(m_.nodes[ad], nd.outputs[0])).f;
+        for (int j = 0; j < Ns[g]; ++j) bias[offs[g] + j] += c[j];
+        done_[ad] = true;
+        Val o;
+        o.kind = Val::ROWS_BF16;
+        o.C = Ns[g];
+        o.H = rows;
+        o.rank = rank;
+        o.buf = p.out;
+        o.ld = Ntot;
+        o.col = offs[g];
+        define(m_.nodes[ad].outputs[0], o);
+      }
+      p.bias_off = push_f32(bias);
+      add_op(std::move(p));
+      return;
+    }
+
+    const GemmTail t = gemm_tail(n, Ntot, rows, gemm);
+    for (int u : t.used) done_[u] = true;
+    for (int j = 0; j < Ntot && !t.bias.empty(); ++j) bias[j] += t.bias[j];
+    p.bias_off = push_f32(bias);
+    a.relu = t.act;
+    if (!t.res.empty()) p.in2 = vals_[vid_.at(t.res)].buf;
     Val o;
-    o.C = N;
-    if (graph_outputs_.count(cur) && consumers(cur).empty()) {
+    o.C = Ntot;
+    o.H = rows;
+    o.rank = rank;
+    if (graph_outputs_.count(t.out) && consumers(t.out).empty()) {
       p.out_f32 = kBufGraphOut;
       o.kind = Val::ROWS_F32;
       o.buf = kBufGraphOut;
     } else {
-      p.out = new_buf(static_cast<size_t>(N) * 2);
+      p.out = new_buf(static_cast<size_t>(rows) * Ntot * 2);
       o.kind = Val::ROWS_BF16;
       o.buf = p.out;
     }
-    define(cur, o);
+    define(t.out, o);
+    add_op(std::move(p));
+  }
+
+  // ---- transformer views / ops --------------------------------------------------------------------
+  bool ints_of(const std::string& nm, std::vector<int64_t>& out) const {
+    auto it = vid_.find(nm);
+    if (it != vid_.end() && vals_[it->second].kind == Val::SHAPE) {
+      out = vals_[it->second].ints;
+      return vals_[it->second].known;
+    }
+    auto ii = m_.initializers.find(nm);
+    if (ii == m_.initializers.end()) return false;
+    if (!ii->second.i.empty()) out = ii->second.i;
+    else {
+      out.clear();
+      for (float f : ii->second.f) out.push_back(static_cast<int64_t>(f));
+    }
+    return true;
+  }
+
+  // Shape-computation subgraph (Shape/Gather/Concat/Unsqueeze/... on int64 shapes) and Expand.
+  bool lower_shape_op(int idx) {
+    const Node& n = m_.nodes[idx];
+    const std::string& op = n.op_type;
+    if (op == "Expand") {
+      if (!is_init(n.in(0))) throw std::runtime_error("Expand " + n.name + ": only initializers can be expanded");
+      const auto& t = m_.initializers.at(n.in(0));
+      const int C = static_cast<int>(t.dims.empty() ? 1 : t.dims.back());
+      if (static_cast<int64_t>(C) != t.numel()) throw std::runtime_error("Expand " + n.name + ": expects a [1, 1, C] token");
+      Val v;
+      v.kind = Val::BCAST_INIT;
+      v.C = C;
+      v.init_name = n.in(0);
+      define(n.outputs[0], v);
+      return true;
+    }
+    if (op == "Shape") {
+      const Val x = val(n.in(0), n);
+      Val s;
+      s.kind = Val::SHAPE;
+      if (x.kind == Val::GRAPH_IN || x.kind == Val::NHWC) s.ints = {kBatchDim, x.C, x.H, x.W};
+      else if (x.kind == Val::ROWS_BF16 && x.rank == 3) s.ints = {kBatchDim, x.H * x.W, x.C};
+      else if (x.kind == Val::ROWS_BF16) s.ints = {kBatchDim, x.C};
+      else s.known = false;
+      define(n.outputs[0], s);
+      return true;
+    }
+    bool any_shape = false;
+    for (auto& in : n.inputs) {
+      auto it = vid_.find(in);
+      if (it != vid_.end() && vals_[it->second].kind == Val::SHAPE) any_shape = true;
+    }
+    if (!any_shape || op == "Reshape") return false;
+    Val s;
+    s.kind = Val::SHAPE;
+    std::vector<int64_t> a, b;
+    if (op == "Gather" && n.get_int("axis", 0) == 0) {
+      s.known = ints_of(n.in(0), a) && ints_of(n.in(1), b);
+      for (int64_t i : b) {
+        if (!s.known) break;
+        if (i < 0) i += static_cast<int64_t>(a.size());
+        if (i < 0 || i >= static_cast<int64_t>(a.size())) s.known = false;
+        else s.ints.push_back(a[i]);
+      }
+    } else if (op == "Concat") {
+      for (auto& in : n.inputs) {
+        if (!ints_of(in, a)) s.known = false;
+        s.ints.insert(s.ints.end(), a.begin(), a.end());
+      }
+    } else if (op == "Unsqueeze" || op == "Squeeze" || op == "Cast" || op == "Identity") {
+      s.known = ints_of(n.in(0), s.ints);
+    } else {
+      s.known = false;
+    }
+    for (auto& o : n.outputs) define(o, s);
+    return true;
+  }
+
+  // Materialise an attention context (logical [B, S, nh, hd]) as rows [B, S, nh*hd].
+  int emit_attention(const Val& ctx, const std::string& name) {
+    const Val& q = vals_[ctx.q];
+    const Val& k = vals_[ctx.k];
+    const Val& v = vals_[ctx.v];
+    const int S = q.H, C = q.nh * q.hd;
+    if (q.hd != 64 || S > 256 || k.H != S || v.H != S)
+      throw std::runtime_error("attention " + name + ": needs head dim 64 and <= 256 tokens");
+    PlanOp p;
+    p.kind = PlanOp::ATTENTION;
+    p.name = name;
+    p.in = q.buf;
+    p.in2 = k.buf;
+    p.in3 = v.buf;
+    p.col[0] = q.col;
+    p.col[1] = k.col;
+    p.col[2] = v.col;
+    p.ld[0] = q.pitch();
+    p.ld[1] = k.pitch();
+    p.ld[2] = v.pitch();
+    p.S = S;
+    p.nh = q.nh;
+    p.hd = q.hd;
+    p.fscale = ctx.scale;
+    p.C = C;
+    p.flops_per_sample = 4.0 * S * S * q.hd * q.nh;
+    p.out = new_buf(static_cast<size_t>(S) * C * 2);
+    const int buf = p.out;
+    add_op(std::move(p));
+    return buf;
+  }
+
+  void lower_reshape(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    std::vector<int64_t> shp;
+    if (!ints_of(n.in(1), shp)) throw std::runtime_error("Reshape " + n.name + ": target shape must be static");
+    for (auto& d : shp)
+      if (d == kBatchDim) d = 0;
+    auto is_batch = [](int64_t d) { return d == 0 || d == -1; };
+    // NHWC map -> [B, C, H*W]
+    if (x.kind == Val::NHWC && shp.size() == 3 && is_batch(shp[0]) && shp[1] == x.C &&
+        (shp[2] == -1 || shp[2] == static_cast<int64_t>(x.H) * x.W) && x.H * x.W > 1) {
+      Val o = x;
+      o.kind = Val::NCHW_FLAT;
+      define(n.outputs[0], o);
+      return;
+    }
+    // rows [B, S, C] -> heads [B, S, nh, hd]
+    if (x.kind == Val::ROWS_BF16 && shp.size() == 4 && is_batch(shp[0]) &&
+        (shp[1] == 0 || shp[1] == -1 || shp[1] == x.H * x.W)) {
+      const int64_t nh = shp[2], hd = shp[3];
+      if (nh > 0 && hd > 0 && nh * hd == x.C) {
+        Val o = x;
+        o.kind = Val::HEADS;
+        o.H = x.H * x.W;
+        o.W = 1;
+        o.nh = static_cast<int>(nh);
+        o.hd = static_cast<int>(hd);
+        o.perm = {{0, 1, 2, 3}};
+        define(n.outputs[0], o);
+        return;
+      }
+    }
+    // attention context [B, S, nh, hd] -> rows [B, S, nh*hd]
+    if (x.kind == Val::ATTN && x.stage == 2 && x.perm == std::array<int, 4>{{0, 1, 2, 3}} && shp.size() == 3 &&
+        is_batch(shp[0])) {
+      const Val& q = vals_[x.q];
+      Val o;
+      o.kind = Val::ROWS_BF16;
+      o.C = q.nh * q.hd;
+      o.H = q.H;
+      o.rank = 3;
+      o.buf = emit_attention(x, n.name);
+      define(n.outputs[0], o);
+      return;
+    }
+    // rows with a single row per sample -> [B, C]
+    if ((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H * x.W == 1 && shp.size() == 2) {
+      Val o = x;
+      o.kind = Val::ROWS_BF16;
+      o.rank = 2;
+      define(n.outputs[0], o);
+      return;
+    }
+    throw std::runtime_error("Reshape " + n.name + ": unsupported reshape for the HIP engine");
+  }
+
+  void lower_transpose(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    const auto perm = n.get_ints("perm");
+    if (x.kind == Val::NCHW_FLAT && perm == std::vector<int64_t>{0, 2, 1}) {
+      Val o = x;  // [B, C, HW]^T = the NHWC buffer read as rows
+      o.kind = Val::ROWS_BF16;
+      o.H = x.H * x.W;
+      o.W = 1;
+      o.rank = 3;
+      define(n.outputs[0], o);
+      return;
+    }
+    if ((x.kind == Val::HEADS || (x.kind == Val::ATTN && x.stage == 2)) && perm.size() == 4) {
+      Val o = x;
+      for (int i = 0; i < 4; ++i) o.perm[i] = x.perm[static_cast<int>(perm[i])];
+      define(n.outputs[0], o);
+      return;
+    }
+    throw std::runtime_error("Transpose " + n.name + ": unsupported transpose for the HIP engine");
+  }
+
+  void lower_attn_matmul(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val a = val(n.in(0), n);
+    const Val b = val(n.in(1), n);
+    const std::array<int, 4> bhsd{{0, 2, 1, 3}}, bhds{{0, 2, 3, 1}};
+    if (a.kind == Val::HEADS && b.kind == Val::HEADS && a.perm == bhsd && b.perm == bhds && a.nh == b.nh &&
+        a.hd == b.hd) {
+      Val s;
+      s.kind = Val::ATTN;
+      s.stage = 0;
+      s.q = vid_.at(n.in(0));
+      s.k = vid_.at(n.in(1));
+      define(n.outputs[0], s);
+      return;
+    }
+    if (a.kind == Val::ATTN && a.stage == 1 && b.kind == Val::HEADS && b.perm == bhsd) {
+      Val c = a;
+      c.stage = 2;
+      c.v = vid_.at(n.in(1));
+      c.perm = bhsd;
+      define(n.outputs[0], c);
+      return;
+    }
+    throw std::runtime_error("MatMul " + n.name + ": activation x activation MatMul outside the attention pattern");
+  }
+
+  void lower_scale(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    auto it = m_.initializers.find(n.in(1));
+    if (x.kind == Val::ATTN && x.stage == 0 && it != m_.initializers.end() && it->second.f.size() == 1) {
+      Val o = x;
+      o.scale = n.op_type == "Div" ? x.scale / it->second.f[0] : x.scale * it->second.f[0];
+      define(n.outputs[0], o);
+      return;
+    }
+    throw std::runtime_error(n.op_type + " " + n.name + ": unsupported elementwise op for the HIP engine");
+  }
+
+  void lower_softmax(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    const int64_t axis = n.get_int("axis", -1);
+    if (x.kind == Val::ATTN && x.stage == 0 && (axis == -1 || axis == 3)) {
+      Val o = x;
+      o.stage = 1;
+      define(n.outputs[0], o);
+      return;
+    }
+    throw std::runtime_error("Softmax " + n.name + ": only attention-score softmax is supported");
+  }
+
+  void lower_layernorm(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    if (x.kind != Val::ROWS_BF16 || x.pitch() != x.C || x.col)
+      throw std::runtime_error("LayerNormalization " + n.name + ": input must be dense rows");
+    const int64_t axis = n.get_int("axis", -1);
+    if (!(axis == -1 || axis == (x.rank ? x.rank : 2) - 1)) throw std::runtime_error("LayerNormalization: axis must be last");
+    if (x.C % 8 || x.C > 2048) throw std::runtime_error("LayerNormalization: C % 8 == 0 and C <= 2048 required");
+    std::vector<float> g = init(n.in(1), n).f, b(x.C, 0.f);
+    if (n.inputs.size() > 2 && !n.in(2).empty()) b = init(n.in(2), n).f;
+    if (static_cast<int>(g.size()) != x.C || static_cast<int>(b.size()) != x.C)
+      throw std::runtime_error("LayerNormalization " + n.name + ": scale/bias size mismatch");
+    PlanOp p;
+    p.kind = PlanOp::LAYERNORM;
+    p.name = n.name;
+    p.in = x.buf;
+    p.scale_off = push_f32(g);
+    p.shift_off = push_f32(b);
+    p.eps = n.get_float("epsilon", 1e-5f);
+    p.C = x.C;
+    p.rows_per_sample = static_cast<long long>(x.H) * x.W;
+    p.out = new_buf(static_cast<size_t>(x.H) * x.W * x.C * 2);
+    Val o = x;
+    o.buf = p.out;
+    define(n.outputs[0], o);
+    add_op(std::move(p));
+  }
+
+  void lower_gather(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    std::vector<int64_t> ix;
+    const auto it = m_.initializers.find(n.in(1));
+    if (x.kind == Val::ROWS_BF16 && x.rank == 3 && n.get_int("axis", 0) == 1 && it != m_.initializers.end() &&
+        it->second.dims.empty() && ints_of(n.in(1), ix) && ix.size() == 1 && x.pitch() == x.C) {
+      const int S = x.H * x.W;
+      int64_t i = ix[0] < 0 ? ix[0] + S : ix[0];
+      if (i < 0 || i >= S) throw std::runtime_error("Gather " + n.name + ": index out of range");
+      PlanOp p;
+      p.kind = PlanOp::GATHER_ROWS;
+      p.name = n.name;
+      p.in = x.buf;
+      p.S = S;
+      p.gidx = static_cast<int>(i);
+      p.C = x.C;
+      p.out = new_buf(static_cast<size_t>(x.C) * 2);
+      Val o;
+      o.kind = Val::ROWS_BF16;
+      o.C = x.C;
+      o.rank = 2;
+      o.buf = p.out;
+      define(n.outputs[0], o);
+      add_op(std::move(p));
+      return;
+    }
+    throw std::runtime_error("Gather " + n.name + ": only selecting one token (axis 1, scalar index) is supported");
+  }
+
+  void lower_concat(int idx) {
+    const Node& n = m_.nodes[idx];
+    if (n.inputs.size() == 2 && n.get_int("axis", 0) == 1) {
+      const Val a = val(n.in(0), n);
+      const Val b = val(n.in(1), n);
+      if (a.kind == Val::BCAST_INIT && b.kind == Val::ROWS_BF16 && b.rank == 3 && a.C == b.C && b.pitch() == b.C) {
+        Val o;
+        o.kind = Val::TOKCAT;
+        o.C = b.C;
+        o.H = b.H * b.W + 1;
+        o.rank = 3;
+        o.init_name = a.init_name;
+        o.patches = vid_.at(n.in(1));
+        define(n.outputs[0], o);
+        return;
+      }
+    }
+    throw std::runtime_error("Concat " + n.name + ": only the [cls, patches] token concat is supported");
+  }
+
+  // TOKCAT (+ optional position embedding initializer) -> token assembly kernel.
+  void emit_tokens(const Node& n, const Val& cat, const std::string* pos_name, const std::string& out_name) {
+    const Val& pt = vals_[cat.patches];
+    const int S = cat.H, C = cat.C;
+    PlanOp p;
+    p.kind = PlanOp::TOKENS;
+    p.name = n.name;
+    p.in = pt.buf;
+    p.S = S - 1;
+    p.C = C;
+    p.scale_off = push_f32(m_.initializers.at(cat.init_name).f);
+    if (pos_name) {
+      const auto& pos = m_.initializers.at(*pos_name);
+      if (pos.numel() != static_cast<int64_t>(S) * C)
+        throw std::runtime_error("Add " + n.name + ": position embedding must be [1, S, C]");
+      p.shift_off = push_f32(pos.f);
+    }
+    p.out = new_buf(static_cast<size_t>(S) * C * 2);
+    Val o;
+    o.kind = Val::ROWS_BF16;
+    o.C = C;
+    o.H = S;
+    o.rank = 3;
+    o.buf = p.out;
+    define(out_name, o);
     add_op(std::move(p));
   }
 
@@ -456,8 +1002,18 @@ class Planner {
 
   void lower_add(int idx) {
     const Node& n = m_.nodes[idx];
-    Val& a = val(n.in(0), n);
-    Val& b = val(n.in(1), n);
+    // [cls, patches] + position embedding -> token assembly
+    for (int side = 0; side < 2; ++side) {
+      auto it = vid_.find(n.in(side));
+      if (it != vid_.end() && vals_[it->second].kind == Val::TOKCAT && is_init(n.in(1 - side))) {
+        const Val cat = vals_[it->second];
+        return emit_tokens(n, cat, &n.in(1 - side), n.outputs[0]);
+      }
+    }
+    const Val a = val(n.in(0), n);
+    const Val b = val(n.in(1), n);
+    if (a.pitch() != a.C || b.pitch() != b.C || a.col || b.col)
+      throw std::runtime_error("Add " + n.name + ": strided operands are not supported");
     if (a.kind != b.kind || a.C != b.C || a.H != b.H || a.W != b.W)
       throw std::runtime_error("Add " + n.name + ": broadcasting adds are not supported by the HIP engine");
     standalone_affine(n, a, nullptr, nullptr, &b);
@@ -561,11 +1117,11 @@ class Planner {
     const Node& n = m_.nodes[idx];
     Val x = val(n.in(0), n);
     if (n.op_type == "Flatten" && n.get_int("axis", 1) != 1) throw std::runtime_error("Flatten: axis must be 1");
-    if (!(x.kind == Val::ROWS_BF16 || (x.kind == Val::NHWC && x.H == 1 && x.W == 1)))
+    if (!((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H == 1 && x.W == 1))
       throw std::runtime_error(n.op_type + " " + n.name + ": only flattening of 1x1 feature maps is supported");
     Val o = x;
     o.kind = Val::ROWS_BF16;
-    o.H = o.W = 1;
+    o.rank = 2;
     define(n.outputs[0], o);
   }
 
@@ -574,18 +1130,25 @@ class Planner {
     auto it = vid_.find(name);
     if (it == vid_.end()) throw std::runtime_error("graph output " + name + " is not produced");
     Val v = vals_[it->second];
+    if (v.kind == Val::TOKCAT) {  // never materialised by a consumer
+      emit_tokens(m_.nodes[0], v, nullptr, name + "#tokens");
+      v = vals_[vid_.at(name + "#tokens")];
+    }
     if (v.kind == Val::ROWS_F32 && v.buf == kBufGraphOut) {
       plan_.output_shape = {1, v.C};
+      if (v.rank == 3) plan_.output_shape = {1, v.H, v.C};
     } else if (v.kind == Val::ROWS_BF16 || (v.kind == Val::NHWC && v.H == 1 && v.W == 1 &&
                                            m_.outputs[0].dims.size() == 2)) {
       PlanOp p;
       p.kind = PlanOp::BF16_TO_F32;
       p.name = "output_cast";
+      if (v.pitch() != v.C || v.col) throw std::runtime_error("graph output is a strided view");
       p.in = v.buf;
-      p.C = v.C;
+      p.C = v.C * v.H * v.W;
       p.out_f32 = kBufGraphOut;
       add_op(std::move(p));
       plan_.output_shape = {1, v.C};
+      if (v.kind == Val::ROWS_BF16 && v.rank == 3) plan_.output_shape = {1, v.H * v.W, v.C};
     } else if (v.kind == Val::NHWC) {
       PlanOp p;
       p.kind = PlanOp::TO_NCHW_F32;
@@ -610,7 +1173,7 @@ class Planner {
       const PlanOp& p = plan_.ops[i];
       for (int b : {p.out, p.out2})
         if (b >= 0 && plan_.bufs[b].first_use < 0) plan_.bufs[b].first_use = i;
-      for (int b : {p.in, p.in2, p.out, p.out2})
+      for (int b : {p.in, p.in2, p.in3, p.out, p.out2})
         if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, i);
     }
     struct Block {

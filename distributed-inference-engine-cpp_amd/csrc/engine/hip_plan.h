@@ -10,6 +10,12 @@
 //    -> the producing conv's second output (dual store), so ResNet-v2 has no standalone BN/ReLU/Add;
 //  * Gemm / MatMul(2-D initializer) -> the same MFMA kernel as a 1x1 conv over rows;
 //  * GlobalAveragePool / MaxPool / AveragePool -> NHWC kernels; Flatten of 1x1 maps -> view.
+//  * transformers (ViT): the patch Conv's Reshape/Transpose, the heads Reshape/Transpose, the
+//    MatMul -> Div -> Softmax -> MatMul chain and the shape-computation subgraph are all lazy views;
+//    the chain materialises as one fused attention kernel when the context is merged back into rows.
+//    Sibling Q/K/V MatMuls become one GEMM (N = 3*D); MatMul -> Add(bias) -> erf-GELU and
+//    MatMul -> Add(bias) -> Add(residual) fold into the GEMM epilogue; cls Expand/Concat + position
+//    Add -> one token-assembly kernel; LayerNormalization and Gather(token) -> row kernels.
 // Anything else falls back to standalone affine/add/relu kernels, or is rejected with a clear
 // error (the CPU executor still runs such models).
 #pragma once
@@ -30,10 +36,13 @@ struct PlanBuf {
 };
 
 struct PlanOp {
-  enum Kind { INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32 } kind;
+  enum Kind {
+    INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32,
+    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION
+  } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
-  int in = -1, in2 = -1, out = -1, out2 = -1, out_f32 = -1;
+  int in = -1, in2 = -1, in3 = -1, out = -1, out2 = -1, out_f32 = -1;
   // parameter offsets (bytes) into the device parameter blob
   size_t w_off = 0, bias_off = SIZE_MAX, s2_off = SIZE_MAX, b2_off = SIZE_MAX, scale_off = SIZE_MAX,
          shift_off = SIZE_MAX;
@@ -43,7 +52,11 @@ struct PlanOp {
   // generic geometry
   int C = 0, H = 0, W = 0, Ho = 0, Wo = 0, Cp = 0;
   int kh = 0, kw = 0, sh = 1, sw = 1, ph = 0, pw = 0, is_max = 0, cip = 0, act = 0;
-  long long rows_per_sample = 0;  // AFFINE: rows of C per sample
+  long long rows_per_sample = 0;  // AFFINE / LAYERNORM: rows of C per sample
+  // transformer ops: sequence length, heads, head dim, column offsets / pitches of in/in2/in3
+  int S = 0, nh = 0, hd = 0, gidx = 0;
+  int col[3] = {0, 0, 0}, ld[3] = {0, 0, 0};
+  float fscale = 1.f, eps = 0.f;
   double flops_per_sample = 0;
 };
 

@@ -34,6 +34,11 @@ constexpr int BK = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
+// Epilogue activation: 1 = ReLU, 2 = exact (erf) GELU.
+__device__ __forceinline__ float act_fn(float v, int act) {
+  return act == 1 ? fmaxf(v, 0.f) : 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+}
+
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
@@ -54,7 +59,7 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   }
   if (p.relu) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu);
   }
   if (p.out)
     *reinterpret_cast<uint4*>(p.out + o) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
@@ -285,7 +290,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         const size_t o = static_cast<size_t>(m) * p.N + n + r;
         float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
         if (p.res) v += bf2f(p.res[o]);
-        if (p.relu) v = fmaxf(v, 0.f);
+        if (p.relu) v = act_fn(v, p.relu);
         if (p.out) p.out[o] = f2bf(v);
         if (p.out_f32) p.out_f32[o] = v;
         if (p.out2) {

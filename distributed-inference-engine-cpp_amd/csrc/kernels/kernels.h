@@ -74,5 +74,19 @@ hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, in
 hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 
+// ---- transformer (transformer.hip) ----
+// LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.
+hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
+                          long long rows, int C, hipStream_t s);
+// out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
+hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
+                           int C, hipStream_t s);
+// y[b,:] = x[b, idx, :]   (x is [B][S][C])
+hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s);
+// Multi-head attention: out[b,s,h*D:(h+1)*D] = softmax(scale * Q_h K_h^T) V_h with Q/K/V rows
+// [B*S][ld*] (head h at columns h*D).  D == 64, S <= 256.
+hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
+                     int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s);
+
 }  // namespace kern
 }  // namespace die

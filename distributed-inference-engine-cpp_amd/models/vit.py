@@ -37,7 +37,8 @@ class ViTConfig:
 
 
 def tiny_vit_config(seed: int = 0) -> ViTConfig:
-    return ViTConfig(image=32, patch=8, dim=64, depth=2, heads=2, mlp=128, num_classes=16, seed=seed)
+    # head dim 64 (the fused attention kernel's tile), 16 patches + cls = 17 tokens
+    return ViTConfig(image=32, patch=8, dim=128, depth=2, heads=2, mlp=256, num_classes=16, seed=seed)
 
 
 def make_weights(cfg: ViTConfig) -> Dict[str, np.ndarray]:

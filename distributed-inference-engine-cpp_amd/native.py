@@ -436,6 +436,14 @@ def _sig_kernels():
     L.die_kern_affine.argtypes = [u64] * 4 + [i, u64, C.c_longlong, i, u64]
     L.die_kern_nhwc_to_nchw.restype = i
     L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64]
+    L.die_kern_layernorm.restype = i
+    L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64]
+    L.die_kern_tokens.restype = i
+    L.die_kern_tokens.argtypes = [u64] * 4 + [i] * 3 + [u64]
+    L.die_kern_gather_rows.restype = i
+    L.die_kern_gather_rows.argtypes = [u64, u64] + [i] * 4 + [u64]
+    L.die_kern_attention.restype = i
+    L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64]
     L._kern_sigs = True
     return L
 

@@ -142,3 +142,68 @@ def affine_act(x, scale=None, shift=None, z=None, relu=False):
                                           M, C, _stream())
     _check(rc, "affine_act")
     return y
+
+
+# ---- transformer kernels (csrc/kernels/transformer.hip) ---------------------------------------------
+
+def linear(x, w, bias=None, act=0, res=None, tile=-1, splits=1):
+    """Rows GEMM on the MFMA conv kernel: x [..., K] bf16, w [N, K] float -> act(x @ w^T + bias + res).
+    act: 0 none, 1 relu, 2 erf-GELU."""
+    K = x.shape[-1]
+    lead = x.shape[:-1]
+    M = x.numel() // K
+    N = w.shape[0]
+    r = None if res is None else res.reshape(M, 1, 1, N)
+    out, _ = conv2d_nhwc(x.reshape(M, 1, 1, K), w.reshape(N, K, 1, 1), bias=bias, relu=act, res=r, tile=tile,
+                         splits=splits)
+    return None if out is None else out.reshape(*lead, N)
+
+
+def layernorm(x, gamma, beta, eps=1e-5):
+    import torch
+
+    C = x.shape[-1]
+    y = torch.empty_like(x)
+    rc = native.kernels().die_kern_layernorm(_ptr(x.contiguous()), _ptr(y), _ptr(gamma.float().contiguous()),
+                                             _ptr(beta.float().contiguous()), float(eps), x.numel() // C, C, _stream())
+    _check(rc, "layernorm")
+    return y
+
+
+def tokens_assemble(patches, cls=None, pos=None):
+    """patches [B, S0, C] bf16, cls [C] f32, pos [S0+1, C] f32 -> [B, S0+1, C] bf16."""
+    import torch
+
+    B, S0, C = patches.shape
+    out = torch.empty((B, S0 + 1, C), dtype=torch.bfloat16, device=patches.device)
+    rc = native.kernels().die_kern_tokens(_ptr(patches.contiguous()), _ptr(cls), _ptr(pos), _ptr(out), B, S0, C,
+                                          _stream())
+    _check(rc, "tokens_assemble")
+    return out
+
+
+def gather_rows(x, idx):
+    import torch
+
+    B, S, C = x.shape
+    y = torch.empty((B, C), dtype=x.dtype, device=x.device)
+    rc = native.kernels().die_kern_gather_rows(_ptr(x.contiguous()), _ptr(y), B, S, int(idx), C, _stream())
+    _check(rc, "gather_rows")
+    return y
+
+
+def attention(q, k, v, heads, scale=None):
+    """q/k/v: [B, S, H*D] bf16 (may be column slices of a wider tensor, row stride = stride(1)).
+    Returns softmax(scale * Q K^T) V merged back to [B, S, H*D] bf16."""
+    import torch
+
+    B, S, C = q.shape
+    D = C // heads
+    for t in (q, k, v):
+        assert t.stride(2) == 1 and t.stride(0) == S * t.stride(1), "rows must be [B*S][ld] with unit column stride"
+    out = torch.empty((B, S, C), dtype=torch.bfloat16, device=q.device)
+    sc = float(scale if scale is not None else 1.0 / np.sqrt(D))
+    rc = native.kernels().die_kern_attention(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, S, heads, D, q.stride(1),
+                                             k.stride(1), v.stride(1), C, sc, _stream())
+    _check(rc, "attention")
+    return out

@@ -52,6 +52,20 @@ def models(tmp_path_factory):
         return out["rn50"]
 
     out["get_rn50"] = rn50
+
+    def vit(name):
+        from die_amd.models import vit as v
+
+        key = "vit_" + name
+        if key not in out:
+            c = v.tiny_vit_config() if name == "tiny" else v.ViTConfig()
+            b3, w3 = v.build_onnx(c)
+            p3 = str(d / (key + ".onnx"))
+            open(p3, "wb").write(b3)
+            out[key] = (p3, w3, c)
+        return out[key]
+
+    out["get_vit"] = vit
     return out
 
 

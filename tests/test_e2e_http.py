@@ -136,8 +136,12 @@ def test_failover_and_breaker_recovery(native, models):
         workers[0].stop()
         dead = "127.0.0.1:%d" % dead_port
         ok = 0
-        for i in range(40):
-            st, out = post(gw.url + "/infer", {"request_id": "fo_%d" % i, "input_data": [float(i)]})
+        # ring placement depends on the (random) ports: make sure >= failure_threshold ids hit the dead node
+        ring, keys = py_ring(names)
+        to_dead = [r for r in ("fo_%d" % i for i in range(2000)) if py_get(ring, keys, r) == dead][:10]
+        others = ["fo_%d" % i for i in range(30)]
+        for i, rid in enumerate(to_dead + others):
+            st, out = post(gw.url + "/infer", {"request_id": rid, "input_data": [float(i)]})
             ok += st == 200
             if st == 200:
                 assert out["node_id"] == "f1"

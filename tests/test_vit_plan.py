@@ -1,0 +1,52 @@
+"""ViT-B/16 (BASELINE config 5) on the CPU: generator vs torch through the C++ CPU executor, and the
+HIP planner's lowering of the transformer graph (runs without a GPU: planning is host code)."""
+import numpy as np
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12))
+
+
+def test_vit_tiny_cpu_executor_matches_torch(native, models):
+    import torch
+
+    from die_amd.models import vit
+
+    path, w, cfg = models["get_vit"]("tiny")
+    x = vit.synthetic_input(3, cfg)
+    got = native.cpu_run(path, x)
+    with torch.no_grad():
+        ref = vit.torch_forward(w, x, cfg).numpy()
+    assert got.shape == (3, cfg.num_classes)
+    assert rel_l2(got, ref) < 1e-4
+
+
+def test_vit_tiny_plan_fusions(native, models):
+    path, w, cfg = models["get_vit"]("tiny")
+    p = native.plan_summary(path, 8)
+    kinds = [o["kind"] for o in p["ops"]]
+    assert p["output_shape"] == [1, cfg.num_classes]
+    # per layer: LN, fused QKV GEMM, attention, proj(+residual), LN, fc1(+GELU), fc2(+residual)
+    assert kinds.count("attention") == cfg.depth
+    assert kinds.count("layernorm") == 2 * cfg.depth + 1
+    assert kinds.count("tokens") == 1 and kinds.count("gather_rows") == 1
+    gemms = [o for o in p["ops"] if o["kind"] == "conv"]
+    qkv = [o for o in gemms if o["name"].endswith("+qkv")]
+    assert len(qkv) == cfg.depth and all(o["N"] == 3 * cfg.dim for o in qkv)
+    assert sum(o["act"] == 2 for o in gemms) == cfg.depth  # GELU folded into fc1
+    assert sum(o["residual"] for o in gemms) == 2 * cfg.depth
+    S = (cfg.image // cfg.patch) ** 2 + 1
+    assert all(o["rows"] == S for o in gemms if "encoder" in o["name"])
+    # no standalone elementwise kernels are left
+    assert "affine" not in kinds
+
+
+def test_vit_base_plan(native, models):
+    path, w, cfg = models["get_vit"]("base")
+    p = native.plan_summary(path, 32)
+    kinds = [o["kind"] for o in p["ops"]]
+    assert kinds.count("attention") == 12
+    assert len(p["ops"]) == 90
+    # 86M parameters in bf16 (+ fp32 biases / LN params)
+    assert 160e6 < p["param_bytes"] < 190e6
+    assert abs(p["gflop_per_sample"] - 35.1) < 0.5
