@@ -25,6 +25,14 @@ sys.path.insert(0, REPO)
 BASELINE_RPS = 522.64  # BASELINE.md / README.md:282
 
 
+def _cpu_quota():
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -37,6 +45,8 @@ def main():
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--no-device-decode", action="store_true",
+                    help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
     args = ap.parse_args()
 
     import torch  # first: one HIP runtime per process (see native.lib)
@@ -84,7 +94,8 @@ def main():
     if args.mode == "http":
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
                            engine={"device": "hip", "device_id": local_rank, "max_batch": B,
-                                   "pipeline_depth": args.pipeline_depth})
+                                   "pipeline_depth": args.pipeline_depth,
+                                   "device_decode": not args.no_device_decode})
         lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
         native.loadgen(requests=args.warmup * B, warmup=0, id_prefix="warm%d_" % rank, **lg)
@@ -107,6 +118,8 @@ def main():
             "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
             "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
+            "cpu_quota": _cpu_quota(), "device_decode": e1.get("device_decode"),
+            "decode_fallbacks": h1.get("decode_fallbacks"),
         }
         wk.stop()
     else:

@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
   o.engine.precision = f.str("precision", "bf16");
   o.engine.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 2));
   o.engine.use_graphs = !f.b("no-graphs");
+  o.engine.device_decode = !f.b("no-device-decode");
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));

@@ -66,6 +66,7 @@ EngineOptions engine_opts(const Json& j) {
   e.pipeline_depth = jget<int>(j, "pipeline_depth", e.pipeline_depth);
   e.use_graphs = jget<bool>(j, "use_graphs", e.use_graphs);
   e.autotune = jget<bool>(j, "autotune", e.autotune);
+  e.device_decode = jget<bool>(j, "device_decode", e.device_decode);
   e.precision = jget<std::string>(j, "precision", e.precision);
   e.shard_id = jget<int>(j, "shard_id", e.shard_id);
   return e;

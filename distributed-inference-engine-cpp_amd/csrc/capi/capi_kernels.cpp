@@ -124,6 +124,17 @@ int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, 
                                           P<uint16_t>(out), B, Sq, H, D, ldq, ldk, ldv, ldo, scale, S(stream)));
 }
 
+long long die_decode_scratch_bytes(int max_batch, long long text_cap) {
+  return static_cast<long long>(kern::decode_scratch_bytes(max_batch, static_cast<size_t>(text_cap)));
+}
+
+int die_kern_decode(uint64_t text, long long text_cap, uint64_t lens, int B, uint64_t out, long long numel,
+                    uint64_t status, uint64_t ntok, uint64_t scratch, uint64_t stream) {
+  return static_cast<int>(kern::decode_json_numbers(P<const unsigned char>(text), static_cast<size_t>(text_cap),
+                                                    P<const long long>(lens), B, P<float>(out), numel, P<int>(status),
+                                                    P<int>(ntok), P<void>(scratch), S(stream)));
+}
+
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
 char* die_plan_summary(const char* model_path, int max_batch, char** err) {
   try {

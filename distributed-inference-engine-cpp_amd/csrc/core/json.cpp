@@ -887,6 +887,14 @@ int parse_infer_body(std::string_view body, InferBodySink& sink) {
         if (c.peek() != '[') throw JsonError("[json.exception.type_error.302] type must be array, but is " +
                                              std::string(c.peek() == '"' ? "string" : "other"));
         ++c.p;
+        if (sink.defer_input_text()) {
+          const char* q = static_cast<const char*>(std::memchr(c.p, ']', static_cast<size_t>(c.end - c.p)));
+          if (!q) c.fail("unexpected end of input; expected ']'");
+          sink.on_input_text(c.p, static_cast<size_t>(q - c.p));
+          c.p = q + 1;
+          seen |= 2 | 4;
+          goto next_member;
+        }
         float* dst = sink.input_buffer();
         const size_t cap = sink.input_capacity();
         size_t n = 0;
@@ -960,6 +968,7 @@ int parse_infer_body(std::string_view body, InferBodySink& sink) {
         Json v = parse_value(c, 1);
         sink.on_other_key(key, v);
       }
+    next_member:
       char n = c.peek();
       if (n == ',') {
         ++c.p;

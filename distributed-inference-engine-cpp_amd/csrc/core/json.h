@@ -114,11 +114,15 @@ struct InferBodySink {
   virtual size_t input_capacity() const = 0;
   virtual void on_input_count(size_t n) = 0;  // n may exceed capacity (values beyond are dropped)
   virtual void on_other_key(std::string_view key, const Json& value) { (void)key; (void)value; }
+  // Device decode: when true, input_data is not converted here; its raw text (between '[' and the
+  // first ']') goes to on_input_text and the engine converts it (malformed tokens are caught there).
+  virtual bool defer_input_text() const { return false; }
+  virtual void on_input_text(const char* b, size_t n) { (void)b; (void)n; }
 };
 
 // Parse a top-level object {"request_id": str, "input_data": [numbers...], ...}.  Throws JsonError
 // (message mirrors nlohmann's where it matters) on malformed JSON or wrong types.  Returns a bit
-// mask: 1 = request_id seen, 2 = input_data seen.
+// mask: 1 = request_id seen, 2 = input_data seen, 4 = input_data deferred as text.
 int parse_infer_body(std::string_view body, InferBodySink& sink);
 
 // Locate the top-level string member `key` without building a DOM (gateway routing).  Values of

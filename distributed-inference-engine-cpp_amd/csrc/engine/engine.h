@@ -51,6 +51,10 @@ class SamplePool {
 struct BatchItem {
   const float* input = nullptr;  // host pointer (usually a SampleBuffer)
   size_t len = 0;                // valid floats; engine zero-pads to input_numel
+  // Device decode (engines with text_capacity() > 0): the JSON number-list text of input_data
+  // (between '[' and ']') in engine-pinned memory; the engine converts it on the device.
+  const char* text = nullptr;
+  size_t text_len = 0;
 };
 
 struct BatchResult {
@@ -60,6 +64,11 @@ struct BatchResult {
   size_t output_numel = 0;
   double wall_us = 0;    // submit -> outputs on host
   double device_us = 0;  // forward time on the device (0 for CPU)
+  // Per item, for text items (valid during the callback only; null when the batch had none):
+  // status 0 = ok, bit 0 = needs the host parser (unusual token), 2 = more values than the model
+  // input; ntok = number of values found.
+  const int* status = nullptr;
+  const int* ntok = nullptr;
 };
 
 using BatchDone = std::function<void(BatchResult&)>;
@@ -89,6 +98,8 @@ class Engine {
 
   // Host staging allocation for request inputs.
   virtual SamplePool& sample_pool() = 0;
+  // Bytes of input_data text a SampleBuffer can carry for device decode (0 = not supported).
+  virtual size_t text_capacity() const { return 0; }
 
   // Synchronous helpers with the reference's padding rules: predict() pads or truncates to the
   // model input (src/inference_engine.cpp:100-103); batchPredict() pads short inputs and, unlike
@@ -109,6 +120,7 @@ struct EngineOptions {
   int pipeline_depth = 2;        // batches in flight (HIP)
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
+  bool device_decode = true;     // accept input_data text and convert it on the GPU (HIP)
   std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
   int cpu_threads = 0;
   int shard_id = 0;

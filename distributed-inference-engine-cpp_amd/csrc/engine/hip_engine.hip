@@ -61,8 +61,18 @@ class HipEngine : public Engine {
     HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+    if (opt.device_decode) text_cap_ = (in_numel_ * 16 + 4095) / 4096 * 4096;
     slots_.resize(depth_);
     for (auto& sl : slots_) {
+      if (text_cap_) {
+        HIP_CHECK(hipMalloc(&sl.d_text, text_cap_ * max_batch_));
+        HIP_CHECK(hipMalloc(&sl.d_scratch, kern::decode_scratch_bytes(max_batch_, text_cap_)));
+      }
+      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * max_batch_));
+      HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
+      HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * 2 * max_batch_));
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * max_batch_, hipHostMallocDefault));
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_status), sizeof(int) * 2 * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipMalloc(&sl.d_in, sizeof(float) * in_numel_ * max_batch_));
       HIP_CHECK(hipMalloc(&sl.d_out, sizeof(float) * out_numel_ * max_batch_));
       HIP_CHECK(hipMemset(sl.d_in, 0, sizeof(float) * in_numel_ * max_batch_));
@@ -77,7 +87,7 @@ class HipEngine : public Engine {
     buckets_.push_back(max_batch_);
 
     pool_ = std::make_unique<SamplePool>(
-        in_numel_,
+        std::max(in_numel_, text_cap_ / sizeof(float)),
         [](size_t bytes) -> void* {
           void* p = nullptr;
           if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
@@ -128,6 +138,12 @@ class HipEngine : public Engine {
     for (auto& sl : slots_) {
       (void)hipFree(sl.d_in);
       (void)hipFree(sl.d_out);
+      (void)hipFree(sl.d_text);
+      (void)hipFree(sl.d_scratch);
+      (void)hipFree(sl.d_lens);
+      (void)hipFree(sl.d_status);
+      (void)hipHostFree(sl.h_lens);
+      (void)hipHostFree(sl.h_status);
       (void)hipHostFree(sl.h_out);
       (void)hipEventDestroy(sl.ev_h2d);
       (void)hipEventDestroy(sl.ev_fwd0);
@@ -150,6 +166,7 @@ class HipEngine : public Engine {
   std::vector<int64_t> getOutputShape() const override { return plan_.output_shape; }
   int max_batch() const override { return max_batch_; }
   SamplePool& sample_pool() override { return *pool_; }
+  size_t text_capacity() const override { return text_cap_; }
 
   void wait_for_slot() override {
     std::unique_lock<std::mutex> lk(mu_);
@@ -194,12 +211,25 @@ class HipEngine : public Engine {
     try {
       HIP_CHECK(hipSetDevice(dev_));
       Slot& sl = slots_[slot];
+      bool any_text = false;
       for (int i = 0; i < B; ++i) {
+        if (items[i].text) {
+          if (!text_cap_ || items[i].text_len > text_cap_) throw std::runtime_error("input text exceeds device decode capacity");
+          HIP_CHECK(hipMemcpyAsync(sl.d_text + static_cast<size_t>(i) * text_cap_, items[i].text, items[i].text_len,
+                                   hipMemcpyHostToDevice, s_h2d_));
+          sl.h_lens[i] = static_cast<long long>(items[i].text_len);
+          any_text = true;
+          continue;
+        }
+        sl.h_lens[i] = -1;
         const size_t n = std::min(items[i].len, in_numel_);
         float* dst = sl.d_in + static_cast<size_t>(i) * in_numel_;
         if (n) HIP_CHECK(hipMemcpyAsync(dst, items[i].input, n * sizeof(float), hipMemcpyHostToDevice, s_h2d_));
         if (n < in_numel_) HIP_CHECK(hipMemsetAsync(dst + n, 0, (in_numel_ - n) * sizeof(float), s_h2d_));
       }
+      for (int i = B; i < max_batch_; ++i) sl.h_lens[i] = -1;
+      if (text_cap_) HIP_CHECK(hipMemcpyAsync(sl.d_lens, sl.h_lens, sizeof(long long) * max_batch_, hipMemcpyHostToDevice, s_h2d_));
+      job.has_text = any_text;
       HIP_CHECK(hipEventRecord(sl.ev_h2d, s_h2d_));
       HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_h2d, 0));
       HIP_CHECK(hipEventRecord(sl.ev_fwd0, s_compute_));
@@ -213,6 +243,8 @@ class HipEngine : public Engine {
       HIP_CHECK(hipEventRecord(sl.ev_fwd1, s_compute_));
       HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_fwd1, 0));
       HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_d2h_));
+      if (any_text)
+        HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_d2h_));
       HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
     } catch (const std::exception& e) {
       job.error = e.what();
@@ -242,6 +274,8 @@ class HipEngine : public Engine {
     j["gflop_per_image"] = plan_.flops_per_sample / 1e9;
     j["arena_mib"] = static_cast<double>(plan_.arena_bytes) / (1 << 20);
     j["pinned_samples"] = static_cast<long long>(pool_->allocated());
+    j["device_decode"] = text_cap_ > 0;
+    j["text_capacity"] = static_cast<long long>(text_cap_);
     j["autotuned"] = !tune_.empty();
     j["tuned_conv_us_at_max_batch"] = tuned_conv_us_;
     if (!tune_.empty()) {
@@ -370,6 +404,13 @@ class HipEngine : public Engine {
   void encode_forward(int B, int s, hipStream_t st) {
     auto buf = [&](int id) -> void* { return buf_ptr(id, s); };
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
+    if (text_cap_) {
+      Slot& sl = slots_[s];
+      const hipError_t e = kern::decode_json_numbers(sl.d_text, text_cap_, sl.d_lens, B, sl.d_in,
+                                                     static_cast<long long>(in_numel_), sl.d_status,
+                                                     sl.d_status + max_batch_, sl.d_scratch, st);
+      if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
+    }
     for (size_t op_index = 0; op_index < plan_.ops.size(); ++op_index) {
       const PlanOp& op = plan_.ops[op_index];
       hipError_t e = hipSuccess;
@@ -436,6 +477,12 @@ class HipEngine : public Engine {
     float* d_in = nullptr;
     float* d_out = nullptr;
     float* h_out = nullptr;
+    unsigned char* d_text = nullptr;  // max_batch x text_cap_ (device decode)
+    void* d_scratch = nullptr;
+    long long* d_lens = nullptr;
+    long long* h_lens = nullptr;      // pinned
+    int* d_status = nullptr;          // [status x max_batch][ntok x max_batch]
+    int* h_status = nullptr;          // pinned
     hipEvent_t ev_h2d{}, ev_fwd0{}, ev_fwd1{}, ev_d2h{};
   };
   struct Job {
@@ -444,6 +491,7 @@ class HipEngine : public Engine {
     BatchDone done;
     std::chrono::steady_clock::time_point t0;
     std::string error;
+    bool has_text = false;
   };
 
   void completion_loop() {
@@ -469,6 +517,10 @@ class HipEngine : public Engine {
           if (hipEventElapsedTime(&ms, sl.ev_fwd0, sl.ev_fwd1) == hipSuccess) r.device_us = ms * 1000.0;
           r.outputs = sl.h_out;
           r.output_numel = out_numel_;
+          if (job.has_text) {
+            r.status = sl.h_status;
+            r.ntok = sl.h_status + max_batch_;
+          }
           batches_++;
           images_ += job.B;
           device_ms_total_ = device_ms_total_.load() + ms;
@@ -498,6 +550,7 @@ class HipEngine : public Engine {
   int depth_ = 2;
   Plan plan_;
   size_t in_numel_ = 0, out_numel_ = 0;
+  size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
   uint8_t* params_ = nullptr;
   uint8_t* arena_ = nullptr;
   float* ws_ = nullptr;

@@ -1,0 +1,306 @@
+// Device-side decode of JSON number lists (the text between '[' and ']' of "input_data").
+//
+// The serving headline is bound by host CPU, and ~80% of a worker's CPU time went into converting
+// ~150k decimal strings per ResNet request.  MI355X has bandwidth to spare, so the worker copies the
+// raw text into pinned staging and the GPU converts it (inside the same hipGraph as the forward):
+//   1. dec_count : per 4 KiB chunk, count ',' separators and note non-blank bytes
+//   2. dec_scan  : per sample, exclusive prefix over the chunk counts -> token index of each chunk;
+//                  token count, "too many values" status, zero-fill of the padded tail
+//   3. dec_parse : every thread owns 16 bytes of a chunk staged in LDS (+ halo); each token that
+//                  starts in its bytes is converted and stored at out[sample][token index]
+// Conversion is bit-identical to the host parser: integers up to 2^24 scaled by an exact power of
+// ten in fp32 (one rounding), otherwise an exact-power double product/quotient checked for the
+// double-rounding hazard.  Anything unusual (exponent overflow, > 19 significant digits, subnormal,
+// malformed token, token > 64 bytes) sets status bit 1 and the worker re-parses that request on
+// the host with the strict parser, so accepted inputs and error messages match the host path.
+#include "common.h"
+#include "kernels.h"
+
+namespace die {
+namespace kern {
+
+namespace {
+
+constexpr int CHUNK = 4096;  // bytes per block: 256 threads x 16 B
+constexpr int HALO = 64;     // max token length converted on the device
+constexpr int PRE = 16;
+
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {  // 0x80 in each byte of v that is zero
+  const uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(t | v | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t v, uint32_t c4) { return zero_bytes(v ^ c4); }
+__device__ __forceinline__ bool is_ws(unsigned c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
+
+// 16 bytes at [off, off+16) of a sample's text, bytes >= len replaced by ' '.
+__device__ __forceinline__ uint4 load16(const unsigned char* t, long long off, long long len) {
+  uint4 q = *reinterpret_cast<const uint4*>(t + off);
+  if (off + 16 > len) {
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (off + i >= len) w[i >> 2] = (w[i >> 2] & ~(0xFFu << (8 * (i & 3)))) | (0x20u << (8 * (i & 3)));
+    q = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return q;
+}
+
+__device__ __forceinline__ int popc_commas(uint4 q) {
+  const uint32_t C = 0x2C2C2C2Cu;
+  return __popc(eq_bytes(q.x, C)) + __popc(eq_bytes(q.y, C)) + __popc(eq_bytes(q.z, C)) + __popc(eq_bytes(q.w, C));
+}
+
+__device__ __forceinline__ bool nonblank(uint4 q) {
+  uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t ws = eq_bytes(w[i], 0x20202020u) | eq_bytes(w[i], 0x0A0A0A0Au) | eq_bytes(w[i], 0x0D0D0D0Du) |
+                        eq_bytes(w[i], 0x09090909u);
+    any |= ws != 0x80808080u;
+  }
+  return any;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// exclusive block scan of one int per thread (256 threads)
+__device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) red[w] = x;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += red[i];
+  total = red[0] + red[1] + red[2] + red[3];
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict__ text, long long cap,
+                                                 const long long* __restrict__ lens, int* __restrict__ counts,
+                                                 int* __restrict__ blank, int max_chunks) {
+  __shared__ int red[4];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const long long len = lens[b];
+  if (len < 0 || static_cast<long long>(chunk) * CHUNK >= len) {
+    if (threadIdx.x == 0) {
+      counts[b * max_chunks + chunk] = 0;
+      blank[b * max_chunks + chunk] = 1;
+    }
+    return;
+  }
+  const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
+  int c = 0, nb = 0;
+  if (off < len) {
+    const uint4 q = load16(text + b * cap, off, len);
+    c = popc_commas(q);
+    nb = nonblank(q);
+  }
+  const int tc = block_sum(c, red);
+  const int tn = block_sum(nb, red);
+  if (threadIdx.x == 0) {
+    counts[b * max_chunks + chunk] = tc;
+    blank[b * max_chunks + chunk] = tn == 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void dec_scan(const long long* __restrict__ lens, int* __restrict__ counts,
+                                                const int* __restrict__ blank, int* __restrict__ status,
+                                                int* __restrict__ ntok, float* __restrict__ out, long long numel,
+                                                int max_chunks) {
+  __shared__ int red[4];
+  const int b = blockIdx.x;
+  const long long len = lens[b];
+  if (len < 0) {
+    if (threadIdx.x == 0) {
+      status[b] = 0;
+      ntok[b] = -1;
+    }
+    return;
+  }
+  const int nch = static_cast<int>((len + CHUNK - 1) / CHUNK);
+  int carry = 0, anynb = 0;
+  for (int c0 = 0; c0 < nch; c0 += 256) {
+    const int c = c0 + threadIdx.x;
+    const int v = c < nch ? counts[b * max_chunks + c] : 0;
+    anynb |= c < nch && !blank[b * max_chunks + c];
+    int tot;
+    const int ex = block_excl_scan(v, red, tot);
+    if (c < nch) counts[b * max_chunks + c] = carry + ex;  // in place: exclusive prefix
+    carry += tot;
+  }
+  const int nonblank_any = block_sum(anynb, red) > 0;
+  const long long n = nonblank_any ? static_cast<long long>(carry) + 1 : 0;
+  if (threadIdx.x == 0) {
+    status[b] = n > numel ? 2 : 0;
+    ntok[b] = static_cast<int>(n);
+  }
+  // zero-fill [n, numel)
+  float* o = out + b * numel;
+  for (long long i = n + threadIdx.x; i < numel; i += 256) o[i] = 0.f;
+}
+
+__constant__ float kP10f[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+__constant__ double kP10d[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Convert the token s[0..n) (separators excluded).  Returns false -> host fallback.
+__device__ bool convert_token(const unsigned char* s, int n, float& out) {
+  int i = 0;
+  while (i < n && is_ws(s[i])) ++i;
+  while (n > i && is_ws(s[n - 1])) --n;
+  if (i >= n) return false;
+  const bool neg = s[i] == '-';
+  i += neg;
+  if (i >= n || s[i] - '0' > 9u) return false;
+  uint64_t mant = 0;
+  int nd = 0, exp10 = 0;
+  if (s[i] == '0') {
+    ++i;
+    if (i < n && s[i] - '0' <= 9u) return false;  // leading zero
+  } else {
+    while (i < n && s[i] - '0' <= 9u) {
+      if (nd >= 19) return false;
+      mant = mant * 10 + (s[i] - '0');
+      ++nd;
+      ++i;
+    }
+  }
+  if (i < n && s[i] == '.') {
+    ++i;
+    if (i >= n || s[i] - '0' > 9u) return false;
+    while (i < n && s[i] - '0' <= 9u) {
+      const unsigned d = s[i] - '0';
+      if (mant != 0 || d != 0) {
+        if (nd >= 19) return false;
+        mant = mant * 10 + d;
+        ++nd;
+      }
+      --exp10;
+      ++i;
+    }
+  }
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    ++i;
+    int es = 1;
+    if (i < n && (s[i] == '+' || s[i] == '-')) {
+      es = s[i] == '-' ? -1 : 1;
+      ++i;
+    }
+    if (i >= n || s[i] - '0' > 9u) return false;
+    int e = 0;
+    while (i < n && s[i] - '0' <= 9u) {
+      e = e * 10 + (s[i] - '0');
+      if (e > 10000) e = 10000;
+      ++i;
+    }
+    exp10 += es * e;
+  }
+  if (i != n) return false;
+  float v;
+  if (mant == 0) {
+    v = 0.f;
+  } else if (mant <= (1u << 24) && exp10 >= -10 && exp10 <= 10) {
+    v = exp10 < 0 ? static_cast<float>(mant) / kP10f[-exp10] : static_cast<float>(mant) * kP10f[exp10];
+  } else if (exp10 >= -22 && exp10 <= 22) {
+    // <= 2 roundings in double (mantissa > 2^53, then the exact power): |d - x| < 2 ulp(d).  The
+    // float rounding of d equals that of x unless d is within 2 ulp of a float midpoint.
+    const double d = exp10 < 0 ? static_cast<double>(mant) / kP10d[-exp10] : static_cast<double>(mant) * kP10d[exp10];
+    const uint64_t bits = __double_as_longlong(d);
+    const long long low = static_cast<long long>(bits & ((1ull << 29) - 1)) - (1ll << 28);
+    if (low >= -2 && low <= 2) return false;  // double-rounding hazard
+    if (d > 3.4028234663852886e38 || d < 1.1754943508222875e-38) return false;  // overflow / subnormal
+    v = static_cast<float>(d);
+  } else {
+    return false;
+  }
+  out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
+  return true;
+}
+
+__global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
+                                                 const long long* __restrict__ lens, const int* __restrict__ prefix,
+                                                 int* __restrict__ status, float* __restrict__ out, long long numel,
+                                                 int max_chunks) {
+  __shared__ __attribute__((aligned(16))) unsigned char buf[PRE + CHUNK + HALO];
+  __shared__ int red[4];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const long long len = lens[b];
+  const long long c0 = static_cast<long long>(chunk) * CHUNK;
+  if (len < 0 || c0 >= len) return;
+  const unsigned char* t = text + b * cap;
+  // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
+  for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
+    const long long off = c0 - PRE + 16ll * i;
+    uint4 q;
+    if (off < 0) q = make_uint4(0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu);
+    else if (off >= len) q = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    else q = load16(t, off, len);
+    *reinterpret_cast<uint4*>(buf + 16 * i) = q;
+  }
+  __syncthreads();
+  const int lo = PRE + threadIdx.x * 16;
+  const uint4 mine = *reinterpret_cast<const uint4*>(buf + lo);
+  int tot;
+  const int ex = block_excl_scan(popc_commas(mine), red, tot);
+  if (c0 + threadIdx.x * 16 >= len) return;
+  long long idx = static_cast<long long>(prefix[b * max_chunks + chunk]) + ex;
+  const long long lim = len - c0 + PRE;  // first LDS index past the text
+  bool bad = false;
+  for (int j = 0; j < 16; ++j) {
+    const int p = lo + j;
+    if (p >= lim) break;
+    if (buf[p - 1] == ',') {  // a token starts here: it has index idx
+      int e = p;
+      while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
+      if (e == PRE + CHUNK + HALO && e < lim) {  // longer than the halo
+        bad = true;
+      } else if (idx < numel) {
+        float v;
+        if (convert_token(buf + p, e - p, v)) out[b * numel + idx] = v;
+        else bad = true;
+      }
+    }
+    if (buf[p] == ',') ++idx;
+  }
+  if (bad) atomicOr(status + b, 1);
+}
+
+}  // namespace
+
+size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
+  const size_t chunks = (text_cap + CHUNK - 1) / CHUNK;
+  return static_cast<size_t>(max_batch) * chunks * 2 * sizeof(int);
+}
+
+hipError_t decode_json_numbers(const unsigned char* text, size_t text_cap, const long long* lens, int B,
+                               float* out, long long numel, int* status, int* ntok, void* scratch,
+                               hipStream_t s) {
+  if (text_cap % CHUNK) return hipErrorInvalidValue;
+  const int max_chunks = static_cast<int>(text_cap / CHUNK);
+  int* counts = static_cast<int*>(scratch);
+  int* blank = counts + static_cast<size_t>(B) * max_chunks;
+  hipLaunchKernelGGL(dec_count, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), lens,
+                     counts, blank, max_chunks);
+  hipLaunchKernelGGL(dec_scan, dim3(B), dim3(256), 0, s, lens, counts, blank, status, ntok, out, numel, max_chunks);
+  hipLaunchKernelGGL(dec_parse, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), lens,
+                     counts, status, out, numel, max_chunks);
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace die

@@ -74,6 +74,15 @@ hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, in
 hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 
+// ---- device JSON decode (decode.hip) ----
+// Sample b's number-list text lives at text + b * text_cap (text_cap % 4096 == 0) with lens[b]
+// bytes (-1 = not a text sample: skipped).  Writes out[b][0..numel) (values, zero padded),
+// status[b] (0 ok, bit 0 = needs host parse, 2 = more than numel values) and ntok[b].
+size_t decode_scratch_bytes(int max_batch, size_t text_cap);
+hipError_t decode_json_numbers(const unsigned char* text, size_t text_cap, const long long* lens, int B,
+                               float* out, long long numel, int* status, int* ntok, void* scratch,
+                               hipStream_t s);
+
 // ---- transformer (transformer.hip) ----
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,

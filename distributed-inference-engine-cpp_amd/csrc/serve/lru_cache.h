@@ -99,24 +99,34 @@ struct InputKeyHash {
   size_t operator()(const InputKey& k) const { return static_cast<size_t>(k.h0 ^ (k.h1 * 0x9E3779B97F4A7C15ull)); }
 };
 
-// 128-bit hash over the bit patterns of n floats (two independent multiply-mix lanes).
-inline InputKey hash_floats(const float* v, size_t n) {
+// 128-bit hash of a byte string: four independent multiply-mix lanes over 64-byte blocks (the
+// lanes have no dependency on each other, so a 1 MB body hashes at memory speed), folded at the
+// end.  `tag` separates key domains (float bit patterns vs. raw input text).
+inline InputKey hash_bytes(const void* data, size_t bytes, uint64_t tag) {
   auto mum = [](uint64_t a, uint64_t b) {
     __uint128_t r = static_cast<__uint128_t>(a) * b;
     return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
   };
   const uint64_t k0 = 0xa0761d6478bd642full, k1 = 0xe7037ed1a0b428dbull, k2 = 0x8ebc6af09c88c6e3ull,
                  k3 = 0x589965cc75374cc3ull;
-  uint64_t a = 0x243F6A8885A308D3ull ^ n, b = 0x13198A2E03707344ull + n;
-  const unsigned char* p = reinterpret_cast<const unsigned char*>(v);
-  size_t bytes = n * sizeof(float);
+  uint64_t h[4] = {0x243F6A8885A308D3ull ^ bytes, 0x13198A2E03707344ull + bytes, 0xA4093822299F31D0ull ^ tag,
+                   0x082EFA98EC4E6C89ull + tag};
+  const unsigned char* p = static_cast<const unsigned char*>(data);
   size_t i = 0;
+  for (; i + 64 <= bytes; i += 64) {
+    uint64_t w[8];
+    std::memcpy(w, p + i, 64);
+    h[0] = mum(h[0] ^ w[0] ^ k0, w[1] ^ k1);
+    h[1] = mum(h[1] ^ w[2] ^ k2, w[3] ^ k3);
+    h[2] = mum(h[2] ^ w[4] ^ k1, w[5] ^ k2);
+    h[3] = mum(h[3] ^ w[6] ^ k3, w[7] ^ k0);
+  }
   for (; i + 16 <= bytes; i += 16) {
     uint64_t w0, w1;
     std::memcpy(&w0, p + i, 8);
     std::memcpy(&w1, p + i + 8, 8);
-    a = mum(a ^ w0 ^ k0, w1 ^ k1);
-    b = mum(b ^ w1 ^ k2, w0 ^ k3) + a;
+    h[0] = mum(h[0] ^ w0 ^ k0, w1 ^ k1);
+    h[1] = mum(h[1] ^ w1 ^ k2, w0 ^ k3) + h[0];
   }
   uint64_t t0 = 0, t1 = 0;
   if (i < bytes) {
@@ -125,13 +135,20 @@ inline InputKey hash_floats(const float* v, size_t n) {
     std::memcpy(&t0, tail, 8);
     std::memcpy(&t1, tail + 8, 8);
   }
-  a = mum(a ^ t0 ^ k1, t1 ^ k2 ^ bytes);
-  b = mum(b ^ t1 ^ k3, t0 ^ k0 ^ a);
+  uint64_t a = mum(h[0] ^ t0 ^ k1, h[2] ^ t1 ^ k2 ^ bytes);
+  uint64_t b = mum(h[1] ^ t1 ^ k3, h[3] ^ t0 ^ k0 ^ a);
   InputKey key;
-  key.len = n;
+  key.len = bytes ^ (tag << 56);
   key.h0 = mum(a, k3) ^ b;
   key.h1 = mum(b, k1) ^ a;
   return key;
 }
+
+// Key of a parsed input (bit patterns of n floats).
+inline InputKey hash_floats(const float* v, size_t n) { return hash_bytes(v, n * sizeof(float), 0); }
+// Key of an input still in text form (device decode): byte-exact text of input_data.  Two texts
+// of the same numbers spelled differently ("1" vs "1.0") are different keys: a cache miss, never
+// a wrong answer.
+inline InputKey hash_text(const char* s, size_t n) { return hash_bytes(s, n, 1); }
 
 }  // namespace die

@@ -1,6 +1,7 @@
 #include "worker.h"
 
 #include <algorithm>
+#include <cstring>
 #include <iostream>
 #include <random>
 #include <thread>
@@ -11,12 +12,21 @@ namespace {
 
 struct SampleSink : InferBodySink {
   SampleBuffer buf;
+  size_t float_cap = 0;
   std::string id;
   size_t n = 0;
+  bool defer = false;
+  const char* text = nullptr;
+  size_t text_n = 0;
   void on_request_id(std::string_view s) override { id.assign(s); }
   float* input_buffer() override { return buf.data; }
-  size_t input_capacity() const override { return buf.capacity; }
+  size_t input_capacity() const override { return float_cap; }
   void on_input_count(size_t k) override { n = k; }
+  bool defer_input_text() const override { return defer; }
+  void on_input_text(const char* b, size_t k) override {
+    text = b;
+    text_n = k;
+  }
 };
 
 thread_local std::mt19937_64 tl_rng{std::random_device{}()};
@@ -54,7 +64,16 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
                         std::function<void(std::vector<Result>&&, std::exception_ptr)> finish) {
     std::vector<BatchItem> items;
     items.reserve(reqs.size());
-    for (auto& r : reqs) items.push_back(BatchItem{r.buf.data, r.len});
+    for (auto& r : reqs) {
+      BatchItem it{r.buf.data, r.len};
+      if (r.text_len) {
+        it.input = nullptr;
+        it.len = 0;
+        it.text = reinterpret_cast<const char*>(r.buf.data);
+        it.text_len = r.text_len;
+      }
+      items.push_back(it);
+    }
     const size_t B = reqs.size();
     eng->submit(std::move(items), [B, finish](BatchResult& br) {
       if (!br.ok) {
@@ -64,8 +83,13 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       std::vector<Result> out(B);
       const int64_t per = B ? static_cast<int64_t>(br.wall_us) / static_cast<int64_t>(B) : 0;
       for (size_t i = 0; i < B; ++i) {
-        out[i].output.assign(br.outputs + i * br.output_numel, br.outputs + (i + 1) * br.output_numel);
         out[i].inference_time_us = per;
+        if (br.status && br.status[i]) {
+          out[i].decode_status = br.status[i];
+          out[i].ntok = br.ntok[i];
+          continue;
+        }
+        out[i].output.assign(br.outputs + i * br.output_numel, br.outputs + (i + 1) * br.output_numel);
       }
       finish(std::move(out), nullptr);
     });
@@ -137,22 +161,44 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   SampleSink sink;
   sink.buf = pool.acquire();
   const size_t numel = eng.input_numel();
-  sink.buf.capacity = std::min(sink.buf.capacity, numel);
+  sink.float_cap = std::min(sink.buf.capacity, numel);
+  const size_t text_cap = std::min(eng.text_capacity(), sink.buf.capacity * sizeof(float));
+  sink.defer = text_cap > 0;
   int seen = 0;
   const auto t_parse = std::chrono::steady_clock::now();
+  InputKey key;
+  size_t text_len = 0;
   try {
     seen = parse_infer_body(req.body, sink);
+    if ((seen & 4) && sink.text_n > text_cap) {  // too long for device decode: parse on the host
+      sink.defer = false;
+      sink.text = nullptr;
+      seen = parse_infer_body(req.body, sink);
+    }
+    if (!(seen & 1)) throw JsonError("key 'request_id' not found");
+    if (!(seen & 2)) throw JsonError("key 'input_data' not found");
+    if (seen & 4) {
+      std::memcpy(sink.buf.data, sink.text, sink.text_n);
+      text_len = sink.text_n;
+      key = hash_text(sink.text, sink.text_n);
+      // an empty list needs no conversion
+      if (text_len == 0) {
+        text_len = 0;
+        sink.n = 0;
+        key = hash_floats(sink.buf.data, 0);
+      }
+    } else {
+      if (sink.n > numel)
+        throw std::runtime_error("input_data has " + std::to_string(sink.n) + " values; model input holds " +
+                                 std::to_string(numel));
+      key = hash_floats(sink.buf.data, sink.n);
+    }
     parse_ns_.fetch_add(static_cast<int64_t>(
                             std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_parse)
                                 .count()),
                         std::memory_order_relaxed);
     parse_bytes_.fetch_add(static_cast<int64_t>(req.body.size()), std::memory_order_relaxed);
     parsed_.fetch_add(1, std::memory_order_relaxed);
-    if (!(seen & 1)) throw JsonError("key 'request_id' not found");
-    if (!(seen & 2)) throw JsonError("key 'input_data' not found");
-    if (sink.n > numel)
-      throw std::runtime_error("input_data has " + std::to_string(sink.n) + " values; model input holds " +
-                               std::to_string(numel));
   } catch (const std::exception& e) {
     pool.release(sink.buf);
     errors_++;
@@ -162,7 +208,6 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   // Free the request body now: at ResNet size it is ~1 MB we no longer need.
   std::string().swap(req.body);
 
-  const InputKey key = hash_floats(sink.buf.data, sink.n);
   if (auto hit = cache_.get(key)) {
     cache_hits_.fetch_add(1, std::memory_order_relaxed);
     pool.release(sink.buf);
@@ -176,17 +221,26 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     });
     return;
   }
+  if (text_len) device_decoded_.fetch_add(1, std::memory_order_relaxed);
 
   Pending p;
   p.request_id = std::move(sink.id);
   p.buf = sink.buf;
   p.len = sink.n;
+  p.text_len = text_len;
   p.key = key;
+  dispatch(std::move(p), std::move(res));
+}
+
+void WorkerNode::dispatch(Pending p, Responder res) {
+  const SampleBuffer buf = p.buf;
+  const size_t text_len = p.text_len;
+  const InputKey key = p.key;
   std::string id_copy = p.request_id;
-  batcher_->submit(std::move(p), [this, res, key, buf = sink.buf, id = std::move(id_copy)](
+  batcher_->submit(std::move(p), [this, res, key, buf, text_len, id = std::move(id_copy)](
                                      Result* r, std::exception_ptr err) mutable {
-    engine_->sample_pool().release(buf);
     if (err) {
+      engine_->sample_pool().release(buf);
       errors_++;
       std::string msg = "inference failed";
       try {
@@ -196,6 +250,17 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
       } catch (...) {
       }
       res.send(error_response(500, msg));
+      return;
+    }
+    if (r->decode_status & 1) {
+      host_fallback(buf, text_len, std::move(id), key, std::move(res));
+      return;
+    }
+    engine_->sample_pool().release(buf);
+    if (r->decode_status) {
+      errors_++;
+      res.send(error_response(500, "input_data has " + std::to_string(r->ntok) + " values; model input holds " +
+                                       std::to_string(engine_->input_numel())));
       return;
     }
     cache_.put(key, r->output);
@@ -208,6 +273,38 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
       return resp;
     });
   });
+}
+
+void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, std::string id, InputKey key, Responder res) {
+  decode_fallbacks_.fetch_add(1, std::memory_order_relaxed);
+  SamplePool& pool = engine_->sample_pool();
+  const size_t numel = engine_->input_numel();
+  std::string body;
+  body.reserve(text_len + 32);
+  body += "{\"request_id\":\"\",\"input_data\":[";
+  body.append(reinterpret_cast<const char*>(text_buf.data), text_len);
+  body += "]}";
+  pool.release(text_buf);
+  SampleSink sink;
+  sink.buf = pool.acquire();
+  sink.float_cap = std::min(sink.buf.capacity, numel);
+  try {
+    parse_infer_body(body, sink);
+    if (sink.n > numel)
+      throw std::runtime_error("input_data has " + std::to_string(sink.n) + " values; model input holds " +
+                               std::to_string(numel));
+  } catch (const std::exception& e) {
+    pool.release(sink.buf);
+    errors_++;
+    res.send(error_response(500, e.what()));
+    return;
+  }
+  Pending p;
+  p.request_id = std::move(id);
+  p.buf = sink.buf;
+  p.len = sink.n;
+  p.key = key;
+  dispatch(std::move(p), std::move(res));
 }
 
 Json WorkerNode::getHealth() const {
@@ -232,6 +329,8 @@ Json WorkerNode::getHealth() const {
   const int64_t np = parsed_.load();
   h["parse_us_avg"] = np ? parse_ns_.load() / 1e3 / np : 0.0;
   h["parse_gbps"] = parse_ns_.load() ? static_cast<double>(parse_bytes_.load()) / parse_ns_.load() : 0.0;
+  h["device_decoded"] = static_cast<long long>(device_decoded_.load());
+  h["decode_fallbacks"] = static_cast<long long>(decode_fallbacks_.load());
   h["http_threads"] = opt_.http_threads;
   h["engine"] = engine_->stats();
   h["engine"]["name"] = engine_->name();

@@ -3,7 +3,8 @@
 // Reference: WorkerNode (src/worker_node.cpp:27-143) and its main (:145-204).  Same routes, JSON
 // keys, status codes, cache-hit constants (`cached:true`, `inference_time_us:50`) and miss timing
 // (batch wall time / batch size).  Differences: async request handling (no HTTP thread blocked per
-// request), floats decoded straight into engine-owned (pinned) staging, full-input cache keys,
+// request), floats decoded straight into engine-owned (pinned) staging -- or, with a HIP engine,
+// the raw input_data text copied there and converted on the GPU (device decode) -- full-input cache keys,
 // oversized inputs rejected with 500 instead of corrupting the batch, optional fault
 // injection for resilience tests.
 #pragma once
@@ -58,17 +59,24 @@ class WorkerNode {
   struct Pending {
     std::string request_id;
     SampleBuffer buf;
-    size_t len = 0;
+    size_t len = 0;       // parsed floats in buf
+    size_t text_len = 0;  // > 0: buf holds input_data text for device decode instead
     InputKey key;
   };
   struct Result {
     std::vector<float> output;
     int64_t inference_time_us = 0;
+    int decode_status = 0;  // device decode: bit 0 = needs host parse, 2 = too many values
+    int ntok = 0;
   };
 
  private:
   void handle_infer(HttpRequest& req, Responder res);
   void handle_admin_fault(HttpRequest& req, Responder res);
+  // Queue a parsed (or text) request on the batcher and answer `res` when it completes.
+  void dispatch(Pending p, Responder res);
+  // Device decode flagged the text: convert it with the strict host parser and re-dispatch.
+  void host_fallback(SampleBuffer text_buf, size_t text_len, std::string id, InputKey key, Responder res);
   HttpResponse error_response(int status, const std::string& msg) const;
 
   WorkerOptions opt_;
@@ -80,6 +88,7 @@ class WorkerNode {
   std::atomic<int64_t> cache_hits_{0};
   std::atomic<int64_t> errors_{0};
   std::atomic<int64_t> parse_ns_{0}, parse_bytes_{0}, parsed_{0};
+  std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0};
   std::atomic<double> fault_fail_rate_{0.0};
   std::atomic<int> fault_latency_ms_{0};
   std::chrono::steady_clock::time_point started_;

@@ -444,6 +444,10 @@ def _sig_kernels():
     L.die_kern_gather_rows.argtypes = [u64, u64] + [i] * 4 + [u64]
     L.die_kern_attention.restype = i
     L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64]
+    L.die_decode_scratch_bytes.restype = C.c_longlong
+    L.die_decode_scratch_bytes.argtypes = [i, C.c_longlong]
+    L.die_kern_decode.restype = i
+    L.die_kern_decode.argtypes = [u64, C.c_longlong, u64, i, u64, C.c_longlong, u64, u64, u64, u64]
     L._kern_sigs = True
     return L
 

@@ -207,3 +207,35 @@ def attention(q, k, v, heads, scale=None):
                                              k.stride(1), v.stride(1), C, sc, _stream())
     _check(rc, "attention")
     return out
+
+
+# ---- device JSON decode (csrc/kernels/decode.hip) ---------------------------------------------------
+
+def decode_json_numbers(texts, numel, text_cap=None):
+    """Decode number-list texts (bytes, the inside of a JSON array; None = skipped sample) on the GPU.
+    Returns (values [B, numel] f32, status [B] int32, ntok [B] int32) as torch tensors."""
+    import torch
+
+    B = len(texts)
+    if text_cap is None:
+        text_cap = max(4096, max(len(t) for t in texts if t is not None) + 64)
+        text_cap = (text_cap + 4095) // 4096 * 4096
+    host = np.zeros(B * text_cap, np.uint8)
+    lens = np.full(B, -1, np.int64)
+    for i, t in enumerate(texts):
+        if t is None:
+            continue
+        assert len(t) <= text_cap
+        host[i * text_cap:i * text_cap + len(t)] = np.frombuffer(t, np.uint8)
+        lens[i] = len(t)
+    L = native.kernels()
+    d_text = torch.from_numpy(host).cuda()
+    d_lens = torch.from_numpy(lens).cuda()
+    out = torch.full((B, numel), float("nan"), dtype=torch.float32, device="cuda")
+    status = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+    ntok = torch.zeros(B, dtype=torch.int32, device="cuda")
+    scratch = torch.empty(int(L.die_decode_scratch_bytes(B, text_cap)), dtype=torch.uint8, device="cuda")
+    rc = L.die_kern_decode(_ptr(d_text), text_cap, _ptr(d_lens), B, _ptr(out), numel, _ptr(status), _ptr(ntok),
+                           _ptr(scratch), _stream())
+    _check(rc, "decode_json_numbers")
+    return out, status, ntok

@@ -1,0 +1,138 @@
+"""Device JSON decode (csrc/kernels/decode.hip): bit-exact parity with the host parser on every value
+it accepts, host fallback for everything unusual, and the worker's device-decode path end to end."""
+import json
+import urllib.error
+import urllib.request
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+
+def _host(native, text: bytes, cap):
+    body = b'{"request_id":"x","input_data":[' + text + b"]}"
+    _, vals, n = native.parse_infer(body, cap)
+    return vals, n
+
+
+def _texts():
+    rng = np.random.default_rng(0)
+    n = 5000
+    u = rng.random(n)
+    s = rng.standard_normal(n).astype(np.float32)
+    out = {
+        "4dec_unit": ",".join("%.4f" % x for x in u),
+        "7dec_signed": ",".join("%.7f" % x for x in (u * 6 - 3)),
+        "repr_f32": ",".join(repr(float(x)) for x in s),
+        "repr_f64": ",".join(repr(float(x)) for x in rng.random(n)),
+        "ints": ",".join(str(int(x)) for x in rng.integers(-100000, 100000, n)),
+        "exponents": ",".join("%.6e" % x for x in s * 10.0 ** rng.integers(-15, 15, n)),
+        "spaces": ", ".join("%.3f" % x for x in u[:2000]) + " ,\n\t" + "1.5 ",
+        "zeros": ",".join(["0", "-0", "0.0", "-0.000", "0e5"] * 10),
+        "g17": ",".join("%.17g" % x for x in rng.random(n) * 1e3),
+    }
+    return {k: v.encode() for k, v in out.items()}
+
+
+def test_decode_matches_host_bit_exact(native):
+    from die_amd.ops import kernels as K
+
+    texts = _texts()
+    names = list(texts)
+    numel = 6000
+    vals, status, ntok = K.decode_json_numbers([texts[k] for k in names], numel)
+    vals, status, ntok = vals.cpu().numpy(), status.cpu().numpy(), ntok.cpu().numpy()
+    for i, k in enumerate(names):
+        hv, hn = _host(native, texts[k], numel)
+        assert ntok[i] == hn, (k, ntok[i], hn)
+        if k in ("repr_f64", "g17"):
+            # 17 significant digits: many tokens go to the host fallback (> 16 digits / hazard)
+            assert status[i] in (0, 1)
+        else:
+            assert status[i] == 0, (k, status[i])
+        if status[i] == 0:
+            np.testing.assert_array_equal(vals[i, :hn].view(np.uint32), hv.view(np.uint32), err_msg=k)
+            assert np.all(vals[i, hn:] == 0)
+
+
+@pytest.mark.parametrize("bad", [b"1.", b".5", b"01", b"abc", b"1,,2", b"[1]", b'"1"', b"1e", b"+1", b"--1",
+                                 b"1" * 70, b"1e-50", b"3e39", b"nan", b"1 2"])
+def test_decode_flags_unusual_tokens(native, bad):
+    from die_amd.ops import kernels as K
+
+    text = b"0.5," + bad + b",0.25"
+    vals, status, ntok = K.decode_json_numbers([text], 16)
+    assert int(status[0]) & 1, bad
+
+
+def test_decode_counts_padding_and_overflow(native):
+    from die_amd.ops import kernels as K
+
+    texts = [b"1,2,3", b"", b" ", None, b",".join([b"0.5"] * 20)]
+    vals, status, ntok = K.decode_json_numbers(texts, 8)
+    st = status.cpu().numpy()
+    nt = ntok.cpu().numpy()
+    v = vals.cpu().numpy()
+    assert st[0] == 0 and nt[0] == 3 and list(v[0]) == [1, 2, 3, 0, 0, 0, 0, 0]
+    assert st[1] == 0 and nt[1] == 0 and np.all(v[1] == 0)
+    assert nt[2] == 0  # whitespace only: zero values (may route through the host fallback)
+    assert st[3] == 0 and nt[3] == -1 and np.all(np.isnan(v[3]))  # skipped sample untouched
+    assert st[4] == 2 and nt[4] == 20
+
+
+def test_decode_long_text_multi_chunk(native):
+    from die_amd.ops import kernels as K
+
+    rng = np.random.default_rng(3)
+    x = rng.random(150528)
+    text = ",".join("%.4f" % v for v in x).encode()  # ~1 MB, ~260 chunks, tokens straddle chunk edges
+    vals, status, ntok = K.decode_json_numbers([text, text], 150528)
+    hv, hn = _host(native, text, 150528)
+    assert int(status[0]) == 0 and int(ntok[0]) == 150528
+    got = vals.cpu().numpy()
+    np.testing.assert_array_equal(got[0].view(np.uint32), hv.view(np.uint32))
+    np.testing.assert_array_equal(got[1], got[0])
+
+
+def _post(url, body):
+    req = urllib.request.Request(url + "/infer", data=body, headers={"Content-Type": "application/json"})
+    try:
+        return 200, json.loads(urllib.request.urlopen(req, timeout=60).read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def test_worker_device_decode_matches_host_parse(native, models):
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["tiny"]
+    a = native.Worker(path, node_id="dev", engine={"device": "hip", "device_decode": True})
+    b = native.Worker(path, node_id="host", engine={"device": "hip", "device_decode": False})
+    try:
+        assert a.health()["engine"]["device_decode"] is True
+        assert b.health()["engine"]["device_decode"] is False
+        x = r.synthetic_input(3, cfg).reshape(3, -1)
+        bodies = [
+            json.dumps({"request_id": "q%d" % i, "input_data": [float(v) for v in x[i]]}).encode() for i in range(3)
+        ]
+        bodies.append(b'{"request_id":"exotic","input_data":[1e-50, 0.5, 12345678901234567890]}')  # host fallback
+        bodies.append(b'{"input_data":[1,2,3],"request_id":"order"}')
+        for body in bodies:
+            sa, oa = _post(a.url, body)
+            sb, ob = _post(b.url, body)
+            assert sa == sb == 200, (oa, ob)
+            assert oa["output_data"] == ob["output_data"]
+        ha = a.health()
+        assert ha["device_decoded"] >= 4 and ha["decode_fallbacks"] >= 1
+        for bad in [b'{"request_id":"e1","input_data":[1,abc]}', b'{"request_id":"e2","input_data":[1,2,]}',
+                    b'{"request_id":"e3","input_data":[' + b",".join([b"1"] * (3 * 64 * 64 + 1)) + b"]}"]:
+            sa, oa = _post(a.url, bad)
+            sb, ob = _post(b.url, bad)
+            assert sa == sb == 500
+            assert oa["error"] == ob["error"], (oa, ob)
+    finally:
+        a.stop()
+        b.stop()
