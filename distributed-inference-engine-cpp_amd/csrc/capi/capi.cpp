@@ -2,6 +2,7 @@
 // Options travel as JSON strings; returned strings are malloc'ed and released with die_free().
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <memory>
 #include <string>
 
@@ -273,6 +274,50 @@ int die_engine_run(void* p, const float* in, long B, long len, float* out, char*
     auto ys = e->batchPredict(xs);
     const size_t on = e->output_numel();
     for (long b = 0; b < B; ++b) std::memcpy(out + b * on, ys[b].data(), on * sizeof(float));
+    return 0;
+  } catch (const std::exception& ex) {
+    set_err(err, ex.what());
+    return -1;
+  }
+}
+
+// Device-decode path: B texts (concatenated, lens[b] bytes each) -> outputs [B][out] and status[b]
+// (0 ok, bit 0 = needs host parse, 2 = too many values; outputs of such samples are undefined).
+int die_engine_run_text(void* p, const char* texts, const long long* lens, long B, float* out, int* status,
+                        char** err) {
+  auto* e = static_cast<Engine*>(p);
+  try {
+    if (e->text_capacity() == 0) throw std::runtime_error("engine has no device decode");
+    SamplePool& pool = e->sample_pool();
+    std::vector<SampleBuffer> bufs;
+    std::vector<BatchItem> items;
+    size_t off = 0;
+    for (long b = 0; b < B; ++b) {
+      if (static_cast<size_t>(lens[b]) > e->text_capacity()) throw std::runtime_error("text too long");
+      SampleBuffer sb = pool.acquire();
+      std::memcpy(sb.data, texts + off, static_cast<size_t>(lens[b]));
+      off += static_cast<size_t>(lens[b]);
+      bufs.push_back(sb);
+      BatchItem it;
+      it.text = reinterpret_cast<const char*>(sb.data);
+      it.text_len = static_cast<size_t>(lens[b]);
+      items.push_back(it);
+    }
+    std::promise<std::string> done;
+    auto fut = done.get_future();
+    const size_t on = e->output_numel();
+    e->submit(std::move(items), [&](BatchResult& r) {
+      if (!r.ok) {
+        done.set_value(r.error.empty() ? "batch failed" : r.error);
+        return;
+      }
+      std::memcpy(out, r.outputs, sizeof(float) * on * static_cast<size_t>(B));
+      for (long b = 0; b < B; ++b) status[b] = r.status ? r.status[b] : 0;
+      done.set_value("");
+    });
+    const std::string msg = fut.get();
+    for (auto& sb : bufs) pool.release(sb);
+    if (!msg.empty()) throw std::runtime_error(msg);
     return 0;
   } catch (const std::exception& ex) {
     set_err(err, ex.what());

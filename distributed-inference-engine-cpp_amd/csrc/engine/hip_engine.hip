@@ -61,7 +61,7 @@ class HipEngine : public Engine {
     HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
-    if (opt.device_decode) text_cap_ = (in_numel_ * 16 + 4095) / 4096 * 4096;
+    if (opt.device_decode) text_cap_ = (in_numel_ * 24 + 4095) / 4096 * 4096;  // up to 23 chars + separator per value
     slots_.resize(depth_);
     for (auto& sl : slots_) {
       if (text_cap_) {

@@ -216,13 +216,20 @@ __device__ bool convert_token(const unsigned char* s, int n, float& out) {
     v = 0.f;
   } else if (mant <= (1u << 24) && exp10 >= -10 && exp10 <= 10) {
     v = exp10 < 0 ? static_cast<float>(mant) / kP10f[-exp10] : static_cast<float>(mant) * kP10f[exp10];
-  } else if (exp10 >= -22 && exp10 <= 22) {
-    // <= 2 roundings in double (mantissa > 2^53, then the exact power): |d - x| < 2 ulp(d).  The
-    // float rounding of d equals that of x unless d is within 2 ulp of a float midpoint.
-    const double d = exp10 < 0 ? static_cast<double>(mant) / kP10d[-exp10] : static_cast<double>(mant) * kP10d[exp10];
+  } else if (exp10 >= -66 && exp10 <= 66) {
+    // r <= 4 roundings in double (mantissa > 2^53, then up to three exact powers <= 1e22), so
+    // |d - x| < r ulp(d).  The float rounding of d equals that of x unless d lies within r+1 ulp of
+    // a float midpoint (low 29 mantissa bits near 0x10000000) -> host fallback in that case.
+    double d = static_cast<double>(mant);
+    int r = mant > (1ull << 53);
+    for (int e = exp10; e != 0; ++r) {
+      const int k = e > 0 ? (e > 22 ? 22 : e) : (e < -22 ? 22 : -e);
+      d = e > 0 ? d * kP10d[k] : d / kP10d[k];
+      e += e > 0 ? -k : k;
+    }
     const uint64_t bits = __double_as_longlong(d);
     const long long low = static_cast<long long>(bits & ((1ull << 29) - 1)) - (1ll << 28);
-    if (low >= -2 && low <= 2) return false;  // double-rounding hazard
+    if (low >= -(r + 1) && low <= r + 1) return false;  // double-rounding hazard
     if (d > 3.4028234663852886e38 || d < 1.1754943508222875e-38) return false;  // overflow / subnormal
     v = static_cast<float>(d);
   } else {
@@ -275,7 +282,10 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
         else bad = true;
       }
     }
-    if (buf[p] == ',') ++idx;
+    if (buf[p] == ',') {
+      ++idx;
+      bad |= p + 1 == lim;  // trailing comma: empty last token
+    }
   }
   if (bad) atomicOr(status + b, 1);
 }

@@ -167,7 +167,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   int seen = 0;
   const auto t_parse = std::chrono::steady_clock::now();
   InputKey key;
-  size_t text_len = 0;
+  size_t text_len = 0, text_off = 0;
   try {
     seen = parse_infer_body(req.body, sink);
     if ((seen & 4) && sink.text_n > text_cap) {  // too long for device decode: parse on the host
@@ -180,6 +180,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     if (seen & 4) {
       std::memcpy(sink.buf.data, sink.text, sink.text_n);
       text_len = sink.text_n;
+      text_off = static_cast<size_t>(sink.text - req.body.data());
       key = hash_text(sink.text, sink.text_n);
       // an empty list needs no conversion
       if (text_len == 0) {
@@ -228,16 +229,17 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   p.buf = sink.buf;
   p.len = sink.n;
   p.text_len = text_len;
+  p.text_off = text_off;
   p.key = key;
   dispatch(std::move(p), std::move(res));
 }
 
 void WorkerNode::dispatch(Pending p, Responder res) {
   const SampleBuffer buf = p.buf;
-  const size_t text_len = p.text_len;
+  const size_t text_len = p.text_len, text_off = p.text_off;
   const InputKey key = p.key;
   std::string id_copy = p.request_id;
-  batcher_->submit(std::move(p), [this, res, key, buf, text_len, id = std::move(id_copy)](
+  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, id = std::move(id_copy)](
                                      Result* r, std::exception_ptr err) mutable {
     if (err) {
       engine_->sample_pool().release(buf);
@@ -253,7 +255,7 @@ void WorkerNode::dispatch(Pending p, Responder res) {
       return;
     }
     if (r->decode_status & 1) {
-      host_fallback(buf, text_len, std::move(id), key, std::move(res));
+      host_fallback(buf, text_len, text_off, std::move(id), key, std::move(res));
       return;
     }
     engine_->sample_pool().release(buf);
@@ -275,13 +277,21 @@ void WorkerNode::dispatch(Pending p, Responder res) {
   });
 }
 
-void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, std::string id, InputKey key, Responder res) {
+void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, size_t text_off, std::string id, InputKey key,
+                               Responder res) {
   decode_fallbacks_.fetch_add(1, std::memory_order_relaxed);
   SamplePool& pool = engine_->sample_pool();
   const size_t numel = engine_->input_numel();
   std::string body;
-  body.reserve(text_len + 32);
-  body += "{\"request_id\":\"\",\"input_data\":[";
+  // Same byte offsets as the original body, so parse errors report the same position:
+  // '{' + blanks + "input_data": '[' with the '[' at text_off - 1.
+  static const char kKey[] = "\"input_data\":";
+  const size_t pad = text_off >= sizeof(kKey) + 1 ? text_off - sizeof(kKey) - 1 : 0;
+  body.reserve(text_len + pad + 32);
+  body += '{';
+  body.append(pad, ' ');
+  body += kKey;
+  body += '[';
   body.append(reinterpret_cast<const char*>(text_buf.data), text_len);
   body += "]}";
   pool.release(text_buf);

@@ -61,6 +61,7 @@ class WorkerNode {
     SampleBuffer buf;
     size_t len = 0;       // parsed floats in buf
     size_t text_len = 0;  // > 0: buf holds input_data text for device decode instead
+    size_t text_off = 0;  // offset of that text in the request body (host-fallback error offsets)
     InputKey key;
   };
   struct Result {
@@ -76,7 +77,8 @@ class WorkerNode {
   // Queue a parsed (or text) request on the batcher and answer `res` when it completes.
   void dispatch(Pending p, Responder res);
   // Device decode flagged the text: convert it with the strict host parser and re-dispatch.
-  void host_fallback(SampleBuffer text_buf, size_t text_len, std::string id, InputKey key, Responder res);
+  void host_fallback(SampleBuffer text_buf, size_t text_len, size_t text_off, std::string id, InputKey key,
+                     Responder res);
   HttpResponse error_response(int status, const std::string& msg) const;
 
   WorkerOptions opt_;

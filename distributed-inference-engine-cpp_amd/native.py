@@ -83,6 +83,7 @@ def lib() -> C.CDLL:
         sig("die_engine_destroy", None, vp)
         sig("die_engine_info", vp, vp)
         sig("die_engine_run", C.c_int, vp, f32p, C.c_long, C.c_long, f32p, errp)
+        sig("die_engine_run_text", C.c_int, vp, C.c_char_p, i64p, C.c_long, f32p, C.POINTER(C.c_int), errp)
         sig("die_cpu_run", vp, cp, f32p, i64p, C.c_int, i64p, C.POINTER(C.c_int), errp)
         sig("die_onnx_summary", vp, cp, errp)
         sig("die_worker_create", vp, cp, errp)
@@ -291,6 +292,22 @@ class Engine:
         if lib().die_engine_run(self.h, _f32(x), B, L, _f32(out), C.byref(err)) != 0:
             _raise_if(err, "engine run")
         return out
+
+    def run_text(self, texts):
+        """Device-decode path: `texts` are input_data number lists (bytes, without brackets).
+        Returns (outputs [B, output numel], status [B]); status 0 = ok, bit 0 = needs the host
+        parser, 2 = more values than the model input."""
+        B = len(texts)
+        blob = b"".join(texts)
+        lens = np.array([len(t) for t in texts], np.int64)
+        out = np.zeros((B, self.output_numel), np.float32)
+        status = np.zeros(B, np.int32)
+        err = _err_box()
+        rc = lib().die_engine_run_text(self.h, blob, lens.ctypes.data_as(C.POINTER(C.c_int64)), B, _f32(out),
+                                       status.ctypes.data_as(C.POINTER(C.c_int)), C.byref(err))
+        if rc != 0:
+            _raise_if(err, "engine run_text")
+        return out, status
 
     def close(self):
         if getattr(self, "h", None):

@@ -59,7 +59,7 @@ def test_decode_matches_host_bit_exact(native):
 
 
 @pytest.mark.parametrize("bad", [b"1.", b".5", b"01", b"abc", b"1,,2", b"[1]", b'"1"', b"1e", b"+1", b"--1",
-                                 b"1" * 70, b"1e-50", b"3e39", b"nan", b"1 2"])
+                                 b"1" * 70, b"1e-50", b"3e39", b"nan", b"1 2", b"1,"])
 def test_decode_flags_unusual_tokens(native, bad):
     from die_amd.ops import kernels as K
 
@@ -109,8 +109,8 @@ def test_worker_device_decode_matches_host_parse(native, models):
     from die_amd.models import resnet_v2 as r
 
     path, w, cfg = models["tiny"]
-    a = native.Worker(path, node_id="dev", engine={"device": "hip", "device_decode": True})
-    b = native.Worker(path, node_id="host", engine={"device": "hip", "device_decode": False})
+    a = native.Worker(path, node_id="dev", engine={"device": "hip", "device_decode": True, "autotune": False})
+    b = native.Worker(path, node_id="host", engine={"device": "hip", "device_decode": False, "autotune": False})
     try:
         assert a.health()["engine"]["device_decode"] is True
         assert b.health()["engine"]["device_decode"] is False
@@ -136,3 +136,58 @@ def test_worker_device_decode_matches_host_parse(native, models):
     finally:
         a.stop()
         b.stop()
+
+
+def _dumps_texts(n_samples, numel, seed=0):
+    rng = np.random.default_rng(seed)
+    x = (np.round(rng.random((n_samples, numel)), 4)).astype(np.float32)
+    texts = [json.dumps([float(v) for v in row])[1:-1].encode() for row in x]  # ", " separators, repr floats
+    return x, texts
+
+
+def test_decode_json_dumps_payloads(native):
+    from die_amd.ops import kernels as K
+
+    x, texts = _dumps_texts(3, 12288)
+    vals, status, ntok = K.decode_json_numbers(texts, 12288)
+    assert status.cpu().numpy().tolist() == [0, 0, 0]
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), x.view(np.uint32))
+
+
+def _identity_model(path, C=3, H=16, W=16):
+    from die_amd.utils.onnx_writer import GraphBuilder
+
+    g = GraphBuilder(name="probe")
+    w = np.zeros((8, C, 1, 1), np.float32)
+    for c in range(C):
+        w[c, c, 0, 0] = 1.0
+    g.init("w", w)
+    xin = g.input("x", ["N", C, H, W])
+    y = g.node("Conv", [xin, "w"], name="probe", kernel_shape=[1, 1])
+    g.output(y, ["N", 8, H, W])
+    g.save(path, opset=13)
+
+
+def test_engine_run_text_matches_floats(native, tmp_path):
+    p = str(tmp_path / "probe.onnx")
+    _identity_model(p)
+    e = native.Engine(p, device="hip", max_batch=4)
+    x, texts = _dumps_texts(4, 3 * 16 * 16, seed=1)
+    texts[2] = b"1,2,3"  # short -> zero padded
+    x[2] = 0
+    x[2, :3] = [1, 2, 3]
+    got, st = e.run_text(texts)
+    assert st.tolist() == [0, 0, 0, 0]
+    ref = e.run(x)
+    np.testing.assert_array_equal(got, ref)
+    e.close()
+
+
+def test_engine_run_text_resnet_tiny(native, models):
+    path, w, cfg = models["tiny"]
+    e = native.Engine(path, device="hip", max_batch=4)
+    x, texts = _dumps_texts(3, 3 * 64 * 64, seed=2)
+    got, st = e.run_text(texts)
+    assert st.tolist() == [0, 0, 0]
+    np.testing.assert_array_equal(got, e.run(x))
+    e.close()
