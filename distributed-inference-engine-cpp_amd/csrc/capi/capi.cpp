@@ -253,6 +253,7 @@ void* die_engine_create(const char* model_path, const char* opts_json, char** er
   }
 }
 void die_engine_destroy(void* e) { delete static_cast<Engine*>(e); }
+char* die_engine_profile(void* p, int B, int iters) { return dup(static_cast<Engine*>(p)->profile_ops(B, iters).dump()); }
 char* die_engine_info(void* p) {
   auto* e = static_cast<Engine*>(p);
   Json j = e->stats();

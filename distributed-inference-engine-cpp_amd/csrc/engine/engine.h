@@ -108,6 +108,12 @@ class Engine {
   std::vector<std::vector<float>> batchPredict(const std::vector<std::vector<float>>& inputs);
 
   virtual Json stats() const { return Json::object(); }
+  // Per-op device timing of one forward at batch B (engines that support it; else empty object).
+  virtual Json profile_ops(int B, int iters) {
+    (void)B;
+    (void)iters;
+    return Json::object();
+  }
 
  protected:
   int shard_id_ = 0;

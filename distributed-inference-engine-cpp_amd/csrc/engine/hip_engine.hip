@@ -401,7 +401,9 @@ class HipEngine : public Engine {
   }
 
   // Encode one forward pass for `B` samples using slot `s`'s input/output buffers.
-  void encode_forward(int B, int s, hipStream_t st) {
+  // op_events (profiling): if given, events[0] is recorded before the first op and events[i + 1]
+  // after op i.
+  void encode_forward(int B, int s, hipStream_t st, hipEvent_t* op_events = nullptr) {
     auto buf = [&](int id) -> void* { return buf_ptr(id, s); };
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
     if (text_cap_) {
@@ -411,6 +413,7 @@ class HipEngine : public Engine {
                                                      sl.d_status + max_batch_, sl.d_scratch, st);
       if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
     }
+    if (op_events) HIP_CHECK(hipEventRecord(op_events[0], st));
     for (size_t op_index = 0; op_index < plan_.ops.size(); ++op_index) {
       const PlanOp& op = plan_.ops[op_index];
       hipError_t e = hipSuccess;
@@ -469,7 +472,59 @@ class HipEngine : public Engine {
       }
       if (e != hipSuccess)
         throw std::runtime_error("launch of " + op.name + " failed: " + std::string(hipGetErrorString(e)));
+      if (op_events) HIP_CHECK(hipEventRecord(op_events[op_index + 1], st));
     }
+  }
+
+  // Per-op device time (eager launches bracketed by events), averaged over `iters` forwards.
+  Json profile_ops(int B, int iters) override {
+    std::lock_guard<std::mutex> submit_guard(submit_mu_);
+    synchronize();
+    B = std::max(1, std::min(B, max_batch_));
+    const size_t n = plan_.ops.size();
+    std::vector<hipEvent_t> ev(n + 1);
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    std::vector<double> us(n, 0.0);
+    size_t bi = 0;
+    while (buckets_[bi] < B) ++bi;
+    const int Bk = buckets_[bi];
+    encode_forward(Bk, 0, s_compute_);  // warm
+    for (int it = 0; it < iters; ++it) {
+      encode_forward(Bk, 0, s_compute_, ev.data());
+      HIP_CHECK(hipStreamSynchronize(s_compute_));
+      for (size_t i = 0; i < n; ++i) {
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        us[i] += ms * 1000.0 / iters;
+      }
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
+                                  "layernorm", "tokens", "gather_rows", "attention"};
+    Json out = Json::object();
+    Json ops = Json::array();
+    double total = 0;
+    for (size_t i = 0; i < n; ++i) {
+      const PlanOp& op = plan_.ops[i];
+      Json o = Json::object();
+      o["name"] = op.name;
+      o["kind"] = kinds[op.kind];
+      o["us"] = us[i];
+      o["gflop"] = op.flops_per_sample * Bk / 1e9;
+      o["tflops"] = us[i] > 0 ? op.flops_per_sample * Bk / (us[i] * 1e6) : 0.0;
+      if (op.kind == PlanOp::CONV) {
+        const Tune t = tune_for(Bk, i);
+        o["tile"] = t.tile;
+        o["splits"] = t.splits;
+      }
+      total += us[i];
+      ops.push_back(o);
+    }
+    out["batch"] = Bk;
+    out["total_us"] = total;
+    out["tflops"] = total > 0 ? plan_.flops_per_sample * Bk / (total * 1e6) : 0.0;
+    out["ops"] = ops;
+    return out;
   }
 
  private:

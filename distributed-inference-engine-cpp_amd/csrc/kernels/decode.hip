@@ -6,8 +6,9 @@
 //   1. dec_count : per 4 KiB chunk, count ',' separators and note non-blank bytes
 //   2. dec_scan  : per sample, exclusive prefix over the chunk counts -> token index of each chunk;
 //                  token count, "too many values" status, zero-fill of the padded tail
-//   3. dec_parse : every thread owns 16 bytes of a chunk staged in LDS (+ halo); each token that
-//                  starts in its bytes is converted and stored at out[sample][token index]
+//   3. dec_parse : a chunk is staged in LDS (+ halo); token starts are found per 16 bytes and
+//                  compacted with a block scan; each lane then converts whole tokens from registers
+//                  and stores them at out[sample][token index]
 // Conversion is bit-identical to the host parser: integers up to 2^24 scaled by an exact power of
 // ten in fp32 (one rounding), otherwise an exact-power double product/quotient checked for the
 // double-rounding hazard.  Anything unusual (exponent overflow, > 19 significant digits, subnormal,
@@ -239,11 +240,111 @@ __device__ bool convert_token(const unsigned char* s, int n, float& out) {
   return true;
 }
 
+// 4 bits (one per byte) from a 0x80-per-byte mask
+__device__ __forceinline__ uint32_t mask4(uint32_t m) { return (((m >> 7) & 0x01010101u) * 0x01020408u) >> 24; }
+__device__ __forceinline__ uint32_t mask16(uint4 q, uint32_t c4) {
+  return mask4(eq_bytes(q.x, c4)) | (mask4(eq_bytes(q.y, c4)) << 4) | (mask4(eq_bytes(q.z, c4)) << 8) |
+         (mask4(eq_bytes(q.w, c4)) << 12);
+}
+
+// Register fast path: the token is in r[] (32 bytes, byte i = r[i/4] >> 8*(i%4)), n in [1, 32], no
+// whitespace.  Fully unrolled, so r[] stays in VGPRs.
+__device__ __forceinline__ bool convert_token_regs(const uint32_t (&r)[8], int n, float& out) {
+  uint64_t mant = 0;
+  int nd = 0, exp10 = 0, phase = 0, ndig_int = 0, ndig_frac = 0, ndig_exp = 0, ev = 0, es = 1;
+  bool neg = false, lead0 = false, ok = true;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    if (i >= n) break;
+    const unsigned c = (r[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    const unsigned d = c - '0';
+    if (phase == 0) {  // sign or first integer digit
+      if (c == '-' && i == 0) {
+        neg = true;
+        continue;
+      }
+      phase = 1;
+    }
+    if (phase == 1) {
+      if (d <= 9u) {
+        if (ndig_int == 1 && lead0) ok = false;
+        lead0 |= ndig_int == 0 && d == 0;
+        ++ndig_int;
+        if (mant != 0 || d != 0) {
+          ok &= nd < 19;
+          mant = mant * 10 + d;
+          ++nd;
+        }
+      } else if (c == '.' && ndig_int > 0) {
+        phase = 2;
+      } else if ((c | 0x20u) == 'e' && ndig_int > 0) {
+        phase = 3;
+      } else {
+        ok = false;
+      }
+    } else if (phase == 2) {
+      if (d <= 9u) {
+        ++ndig_frac;
+        --exp10;
+        if (mant != 0 || d != 0) {
+          ok &= nd < 19;
+          mant = mant * 10 + d;
+          ++nd;
+        }
+      } else if ((c | 0x20u) == 'e' && ndig_frac > 0) {
+        phase = 3;
+      } else {
+        ok = false;
+      }
+    } else {  // exponent
+      if ((c == '-' || c == '+') && ndig_exp == 0 && es == 1) {
+        es = c == '-' ? -1 : 1;
+        if (c == '+') es = 2;  // seen '+': a further sign is invalid
+      } else if (d <= 9u) {
+        ++ndig_exp;
+        ev = ev * 10 + static_cast<int>(d);
+        if (ev > 10000) ev = 10000;
+      } else {
+        ok = false;
+      }
+    }
+  }
+  if (!ok || ndig_int == 0 || (phase == 2 && ndig_frac == 0) || (phase == 3 && ndig_exp == 0)) return false;
+  exp10 += (es == -1 ? -ev : ev);
+  float v;
+  if (mant == 0) {
+    v = 0.f;
+  } else if (mant <= (1u << 24) && exp10 >= -10 && exp10 <= 10) {
+    v = exp10 < 0 ? static_cast<float>(mant) / kP10f[-exp10] : static_cast<float>(mant) * kP10f[exp10];
+  } else if (exp10 >= -66 && exp10 <= 66) {
+    double dd = static_cast<double>(mant);
+    int rr = mant > (1ull << 53);
+    for (int e = exp10; e != 0; ++rr) {
+      const int k = e > 0 ? (e > 22 ? 22 : e) : (e < -22 ? 22 : -e);
+      dd = e > 0 ? dd * kP10d[k] : dd / kP10d[k];
+      e += e > 0 ? -k : k;
+    }
+    const uint64_t bits = __double_as_longlong(dd);
+    const long long low = static_cast<long long>(bits & ((1ull << 29) - 1)) - (1ll << 28);
+    if (low >= -(rr + 1) && low <= rr + 1) return false;
+    if (dd > 3.4028234663852886e38 || dd < 1.1754943508222875e-38) return false;
+    v = static_cast<float>(dd);
+  } else {
+    return false;
+  }
+  out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
+  return true;
+}
+
+// Token-parallel parse of one 4 KiB chunk: (1) every thread finds the token starts in its 16 bytes,
+// (2) a block scan compacts them into an LDS list, (3) each lane converts whole tokens, loading 32
+// bytes into registers with aligned LDS reads + alignbyte.
 __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ lens, const int* __restrict__ prefix,
                                                  int* __restrict__ status, float* __restrict__ out, long long numel,
                                                  int max_chunks) {
   __shared__ __attribute__((aligned(16))) unsigned char buf[PRE + CHUNK + HALO];
+  __shared__ unsigned short starts[CHUNK / 2 + 1];
   __shared__ int red[4];
   const int b = blockIdx.y, chunk = blockIdx.x;
   const long long len = lens[b];
@@ -260,32 +361,65 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
     *reinterpret_cast<uint4*>(buf + 16 * i) = q;
   }
   __syncthreads();
+  const int lim = static_cast<int>(len - c0 < CHUNK + HALO ? len - c0 : CHUNK + HALO) + PRE;  // LDS end of text
   const int lo = PRE + threadIdx.x * 16;
   const uint4 mine = *reinterpret_cast<const uint4*>(buf + lo);
-  int tot;
-  const int ex = block_excl_scan(popc_commas(mine), red, tot);
-  if (c0 + threadIdx.x * 16 >= len) return;
-  long long idx = static_cast<long long>(prefix[b * max_chunks + chunk]) + ex;
-  const long long lim = len - c0 + PRE;  // first LDS index past the text
-  bool bad = false;
-  for (int j = 0; j < 16; ++j) {
-    const int p = lo + j;
-    if (p >= lim) break;
-    if (buf[p - 1] == ',') {  // a token starts here: it has index idx
-      int e = p;
-      while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
-      if (e == PRE + CHUNK + HALO && e < lim) {  // longer than the halo
-        bad = true;
-      } else if (idx < numel) {
-        float v;
-        if (convert_token(buf + p, e - p, v)) out[b * numel + idx] = v;
-        else bad = true;
+  const uint32_t cm = mask16(mine, 0x2C2C2C2Cu);
+  uint32_t sm = ((cm << 1) | (buf[lo - 1] == ',' ? 1u : 0u)) & 0xFFFFu;  // token starts in my 16 bytes
+  if (lo + 16 > lim) sm &= lim > lo ? (1u << (lim - lo)) - 1u : 0u;
+  int total;
+  int k = block_excl_scan(__popc(sm), red, total);
+  while (sm) {
+    const int j = __builtin_ctz(sm);
+    sm &= sm - 1;
+    starts[k++] = static_cast<unsigned short>(lo + j);
+  }
+  __syncthreads();
+  const long long base = static_cast<long long>(prefix[b * max_chunks + chunk]) + (buf[PRE - 1] != ',' ? 1 : 0);
+  bool bad = threadIdx.x == 0 && c0 + CHUNK >= len && buf[lim - 1] == ',';  // trailing comma
+  for (int tk = threadIdx.x; tk < total; tk += 256) {
+    const long long idx = base + tk;  // idx >= numel: still validated, not stored (dec_scan sets status 2)
+    const int p = starts[tk];
+    const int a4 = p & ~3, sh = p & 3;
+    uint32_t x[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = *reinterpret_cast<const uint32_t*>(buf + a4 + 4 * i);
+    uint32_t r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
+    // first ',' and first whitespace in the 32-byte window
+    int n = 32;
+    bool ws = false;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      const uint32_t c = eq_bytes(r[i], 0x2C2C2C2Cu);
+      if (c) n = 4 * i + (__builtin_ctz(c) >> 3);
+    }
+    const int rem = lim - p;
+    if (rem < n) n = rem;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t w = eq_bytes(r[i], 0x20202020u) | eq_bytes(r[i], 0x0A0A0A0Au) | eq_bytes(r[i], 0x0D0D0D0Du) |
+                         eq_bytes(r[i], 0x09090909u);
+      const int lo_b = 4 * i;
+      if (w && lo_b < n) {
+        const int first = lo_b + (__builtin_ctz(w) >> 3);
+        ws |= first < n;
       }
     }
-    if (buf[p] == ',') {
-      ++idx;
-      bad |= p + 1 == lim;  // trailing comma: empty last token
+    float v;
+    bool good;
+    if (n == 32 && rem > 32) {  // longer than the register window: LDS path
+      int e = p;
+      while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
+      good = !(e == PRE + CHUNK + HALO && e < lim) && convert_token(buf + p, e - p, v);
+    } else if (ws) {
+      good = convert_token(buf + p, n, v);
+    } else {
+      good = n > 0 && convert_token_regs(r, n, v);
     }
+    if (good && idx < numel) out[b * numel + idx] = v;
+    bad |= !good;
   }
   if (bad) atomicOr(status + b, 1);
 }

@@ -84,6 +84,7 @@ def lib() -> C.CDLL:
         sig("die_engine_info", vp, vp)
         sig("die_engine_run", C.c_int, vp, f32p, C.c_long, C.c_long, f32p, errp)
         sig("die_engine_run_text", C.c_int, vp, C.c_char_p, i64p, C.c_long, f32p, C.POINTER(C.c_int), errp)
+        sig("die_engine_profile", vp, vp, C.c_int, C.c_int)
         sig("die_cpu_run", vp, cp, f32p, i64p, C.c_int, i64p, C.POINTER(C.c_int), errp)
         sig("die_onnx_summary", vp, cp, errp)
         sig("die_worker_create", vp, cp, errp)
@@ -292,6 +293,10 @@ class Engine:
         if lib().die_engine_run(self.h, _f32(x), B, L, _f32(out), C.byref(err)) != 0:
             _raise_if(err, "engine run")
         return out
+
+    def profile(self, batch: int = 32, iters: int = 10) -> Dict[str, Any]:
+        """Per-op device time (µs) of one forward at `batch` (HIP engine; {} for the CPU engine)."""
+        return json.loads(_take_str(lib().die_engine_profile(self.h, batch, iters)))
 
     def run_text(self, texts):
         """Device-decode path: `texts` are input_data number lists (bytes, without brackets).

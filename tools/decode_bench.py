@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Device JSON decode throughput: B ResNet-sized input_data texts (150528 values) per launch."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+
+def main():
+    import torch
+
+    import die_amd  # noqa: F401
+    from die_amd import native
+
+    L = native.kernels()
+    numel = 150528
+    rng = np.random.default_rng(0)
+    styles = {
+        "4dec": lambda: ",".join("%.4f" % v for v in rng.random(numel)).encode(),
+        "repr_f32": lambda: json.dumps([float(v) for v in rng.random(numel).astype(np.float32)])[1:-1].encode(),
+    }
+    res = {}
+    for name, gen in styles.items():
+        for B in (16, 32):
+            texts = [gen() for _ in range(4)] * (B // 4)
+            cap = (numel * 24 + 4095) // 4096 * 4096
+            host = np.zeros(B * cap, np.uint8)
+            lens = np.array([len(t) for t in texts], np.int64)
+            for i, t in enumerate(texts):
+                host[i * cap:i * cap + len(t)] = np.frombuffer(t, np.uint8)
+            d_text = torch.from_numpy(host).cuda()
+            d_lens = torch.from_numpy(lens).cuda()
+            out = torch.empty((B, numel), dtype=torch.float32, device="cuda")
+            st = torch.empty(2 * B, dtype=torch.int32, device="cuda")
+            scratch = torch.empty(int(L.die_decode_scratch_bytes(B, cap)), dtype=torch.uint8, device="cuda")
+            s = int(torch.cuda.current_stream().cuda_stream)
+
+            def run():
+                rc = L.die_kern_decode(d_text.data_ptr(), cap, d_lens.data_ptr(), B, out.data_ptr(), numel,
+                                       st.data_ptr(), st.data_ptr() + 4 * B, scratch.data_ptr(), s)
+                assert rc == 0
+
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1000 / 20
+            assert int(st[:B].abs().sum()) == 0
+            res["%s_B%d" % (name, B)] = {"us": round(us, 1), "MB": round(lens.sum() / 1e6, 1),
+                                         "GBps": round(lens.sum() / us / 1e3, 1), "us_per_sample": round(us / B, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-op device time of one forward on the HIP engine (events around eager launches of the tuned
+kernels), written as a markdown table + JSON.  Usage: op_profile.py --arch resnet50|vit_b16 --batch 32"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import torch  # noqa: F401  (one HIP runtime)
+
+    import die_amd  # noqa: F401
+    from die_amd import native
+
+    if a.arch == "vit_b16":
+        from die_amd.models import vit as m
+
+        cfg = m.ViTConfig()
+    else:
+        from die_amd.models import resnet_v2 as m
+
+        cfg = m.ResNetConfig()
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, a.arch + ".onnx")
+    open(path, "wb").write(m.build_onnx(cfg)[0])
+    e = native.Engine(path, device="hip", max_batch=a.batch)
+    p = e.profile(a.batch, a.iters)
+    e.close()
+    lines = ["# %s per-op device time, batch %d (MI355X, bf16, tuned kernels)" % (a.arch, p["batch"]), "",
+             "Total %.1f us per forward = %.1f TFLOP/s over the whole graph; %.0f images/s device-bound." % (
+                 p["total_us"], p["tflops"], p["batch"] / p["total_us"] * 1e6), "",
+             "| # | op | kind | us | GFLOP | TFLOP/s | tile/splits |", "|---:|---|---|---:|---:|---:|---|"]
+    for i, o in enumerate(p["ops"]):
+        ts = "%d/%d" % (o["tile"], o["splits"]) if "tile" in o else ""
+        lines.append("| %d | %s | %s | %.1f | %.2f | %.0f | %s |" % (i, o["name"][:48], o["kind"], o["us"], o["gflop"],
+                                                                    o["tflops"], ts))
+    kinds = {}
+    for o in p["ops"]:
+        kinds[o["kind"]] = kinds.get(o["kind"], 0) + o["us"]
+    lines += ["", "| kind | us | share |", "|---|---:|---:|"]
+    for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
+        lines.append("| %s | %.1f | %.1f%% |" % (k, v, 100 * v / p["total_us"]))
+    text = "\n".join(lines) + "\n"
+    print(text)
+    if a.out:
+        open(a.out + ".md", "w").write(text)
+        json.dump(p, open(a.out + ".json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
