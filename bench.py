@@ -40,7 +40,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--connections", type=int, default=50, help="client connections per GPU (reference: 50 threads)")
-    ap.add_argument("--mode", choices=["http", "engine"], default="http")
+    ap.add_argument("--mode", choices=["http", "dp", "engine"], default="http",
+                    help="http: one serving replica per GPU (worker + client per rank); dp: ONE worker whose "
+                         "batches are sharded over all ranks (RCCL); engine: forward-only")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
@@ -122,6 +124,44 @@ def main():
             "decode_fallbacks": h1.get("decode_fallbacks"),
         }
         wk.stop()
+    elif args.mode == "dp":
+        # BASELINE config 4: ONE worker whose batches (B per GPU x N GPUs) are sharded over all ranks;
+        # rank 0 serves HTTP and drives the load, ranks >= 1 are DP followers on their own GPU.
+        group = "die_bench_dp_%s" % os.environ.get("MASTER_PORT", str(os.getpid()))
+        Btot = B * world
+        eng_opts = {"device": "hip", "device_id": local_rank, "pipeline_depth": args.pipeline_depth,
+                    "device_decode": not args.no_device_decode, "dp_world": world, "dp_group": group}
+        res, fol = {"ok": 0, "failed": 0}, None
+        if rank == 0:
+            wk = native.Worker(model, node_id="dp", max_batch=Btot, engine=eng_opts)
+            lg = dict(port=wk.port, connections=args.connections * world, payload="full", input_numel=numel,
+                      decimals=4, seed=1000, timeout_ms=60000)
+            native.loadgen(requests=args.warmup * Btot, warmup=0, id_prefix="warm_", **lg)
+            h0 = wk.health()
+        else:
+            eng_opts.pop("dp_group")
+            eng_opts.pop("dp_world")
+            fol = native.DpFollower(model, group, rank, world, max_batch=Btot, **eng_opts)
+        barrier()
+        t0 = time.perf_counter()
+        if rank == 0:
+            res = native.loadgen(requests=args.steps * Btot, warmup=0, id_prefix="r_", **lg)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        ok, failed = res["ok"], res["failed"]
+        if rank == 0:
+            h1 = wk.health()
+            bp0, bp1 = h0["batch_processor"], h1["batch_processor"]
+            nb = bp1["total_batches"] - bp0["total_batches"]
+            extra = {"p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
+                     "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+                     "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
+                     "engine": h1["engine"].get("device"), "dp_backend": h1["engine"].get("dp_backend"),
+                     "device_ms_per_batch": h1["engine"].get("avg_device_ms"),
+                     "client_connections": args.connections * world}
+            wk.stop()  # stops the DP group: followers return
+        else:
+            fol.join()
     else:
         import numpy as np
 

@@ -1,15 +1,85 @@
 // worker_node <port> <node_id> [model_path] [--flags]
 // Same positional CLI and MODEL_PATH fallback as the reference (src/worker_node.cpp:145-168).
+// Data parallel: `--devices 0,1,...,7` makes this worker the DP leader on the first device and
+// spawns one follower process per further device (`worker_node --dp-follower ...`, started with
+// posix_spawn before this process touches the GPU).
 #include <pthread.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <csignal>
 #include <iostream>
+#include <sstream>
+#include <thread>
 
 #include "../core/flags.h"
 #include "../serve/worker.h"
 
-int main(int argc, char** argv) {
-  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs"});
+extern char** environ;
+
+namespace {
+
+std::vector<int> parse_devices(const std::string& s) {
+  std::vector<int> d;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ','))
+    if (!tok.empty()) d.push_back(std::stoi(tok));
+  return d;
+}
+
+// worker_node --dp-follower <model> --dp-group G --dp-rank R --dp-world N --device-id D [--max-batch M]
+int follower_main(die::Flags& f, sigset_t& sigs) {
   const auto& pos = f.positional();
+  if (pos.empty()) {
+    std::cerr << "--dp-follower needs the model path" << std::endl;
+    return 1;
+  }
+  die::EngineOptions eo;
+  eo.device = f.str("device", "hip");
+  eo.device_id = static_cast<int>(f.i("device-id", 0));
+  eo.max_batch = static_cast<int>(f.i("max-batch", 32));
+  eo.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 2));
+  eo.use_graphs = !f.b("no-graphs");
+  eo.device_decode = !f.b("no-device-decode");
+  eo.dp_group = f.str("dp-group", "");
+  eo.dp_rank = static_cast<int>(f.i("dp-rank", 1));
+  eo.dp_world = static_cast<int>(f.i("dp-world", 2));
+  std::atomic<bool> stop{false};
+  std::thread sig_thread([&] {
+    int sig = 0;
+    sigwait(&sigs, &sig);
+    stop = true;
+  });
+  long served = 0;
+  int rc = 0;
+  try {
+    served = die::run_dp_follower(pos[0], eo, &stop);
+  } catch (const std::exception& e) {
+    std::cerr << "dp follower " << eo.dp_rank << " failed: " << e.what() << std::endl;
+    rc = 1;
+  }
+  std::cout << "dp follower " << eo.dp_rank << " served " << served << " batches" << std::endl;
+  pthread_kill(sig_thread.native_handle(), SIGTERM);
+  sig_thread.join();
+  return rc;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower"});
+  const auto& pos = f.positional();
+  if (f.b("dp-follower")) {
+    sigset_t fs;
+    sigemptyset(&fs);
+    sigaddset(&fs, SIGINT);
+    sigaddset(&fs, SIGTERM);
+    pthread_sigmask(SIG_BLOCK, &fs, nullptr);
+    return follower_main(f, fs);
+  }
   if (pos.size() < 2) {
     std::cerr << "Usage: " << argv[0] << " <port> <node_id> [model_path] [options]\n"
               << "  Or set MODEL_PATH environment variable\n"
@@ -17,7 +87,8 @@ int main(int argc, char** argv) {
               << "  --cache-capacity N (1000)  --max-batch N (32)  --batch-timeout-ms N (20)\n"
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision bf16|fp32 (bf16)\n"
-              << "  --pipeline-depth N (2)  --no-graphs  --http-threads N  --host ADDR (0.0.0.0)\n"
+              << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --http-threads N  --host ADDR (0.0.0.0)\n"
+              << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch)\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose" << std::endl;
     return 1;
   }
@@ -62,12 +133,45 @@ int main(int argc, char** argv) {
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));
   o.verbose = f.b("verbose");
 
+  // data parallel: spawn the followers first (before this process initialises HIP)
+  std::vector<pid_t> followers;
+  const std::vector<int> devices = parse_devices(f.str("devices", ""));
+  if (devices.size() > 1) {
+    o.engine.dp_world = static_cast<int>(devices.size());
+    o.engine.dp_group = "die_dp_" + std::to_string(getpid());
+    o.engine.device_id = devices[0];
+    if (o.engine.device == "auto") o.engine.device = "hip";
+    for (size_t r = 1; r < devices.size(); ++r) {
+      std::vector<std::string> args = {argv[0], "--dp-follower", o.model_path, "--dp-group", o.engine.dp_group,
+                                        "--dp-rank", std::to_string(r), "--dp-world", std::to_string(devices.size()),
+                                        "--device-id", std::to_string(devices[r]), "--device", o.engine.device,
+                                        "--max-batch", std::to_string(o.max_batch), "--pipeline-depth",
+                                        std::to_string(o.engine.pipeline_depth)};
+      if (!o.engine.use_graphs) args.push_back("--no-graphs");
+      if (!o.engine.device_decode) args.push_back("--no-device-decode");
+      std::vector<char*> av;
+      for (auto& a : args) av.push_back(const_cast<char*>(a.c_str()));
+      av.push_back(nullptr);
+      pid_t pid = 0;
+      if (posix_spawn(&pid, "/proc/self/exe", nullptr, nullptr, av.data(), environ) != 0) {
+        std::cerr << "failed to spawn dp follower " << r << std::endl;
+        return 1;
+      }
+      followers.push_back(pid);
+    }
+  }
+
   std::cout << "Using model: " << o.model_path << std::endl;
   std::unique_ptr<die::WorkerNode> worker;
   try {
     worker = std::make_unique<die::WorkerNode>(o);
   } catch (const std::exception& e) {
     std::cerr << "Failed to start worker: " << e.what() << std::endl;
+    for (pid_t p : followers) {
+      kill(p, SIGTERM);
+      int st = 0;
+      waitpid(p, &st, 0);
+    }
     return 1;
   }
   auto& eng = worker->engine();
@@ -97,5 +201,10 @@ int main(int argc, char** argv) {
   sigwait(&sigs, &sig);
   std::cout << "signal " << sig << ": draining and shutting down" << std::endl;
   worker->stop();
+  worker.reset();  // a DP leader's engine stops the group here: followers drain and exit
+  for (pid_t p : followers) {
+    int st = 0;
+    waitpid(p, &st, 0);
+  }
   return 0;
 }

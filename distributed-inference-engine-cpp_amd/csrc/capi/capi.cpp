@@ -5,6 +5,9 @@
 #include <future>
 #include <memory>
 #include <string>
+#include <thread>
+#include <mutex>
+#include <atomic>
 
 #include "../core/json.h"
 #include "../engine/cpu_exec.h"
@@ -70,6 +73,10 @@ EngineOptions engine_opts(const Json& j) {
   e.device_decode = jget<bool>(j, "device_decode", e.device_decode);
   e.precision = jget<std::string>(j, "precision", e.precision);
   e.shard_id = jget<int>(j, "shard_id", e.shard_id);
+  e.dp_world = jget<int>(j, "dp_world", e.dp_world);
+  e.dp_rank = jget<int>(j, "dp_rank", e.dp_rank);
+  e.dp_group = jget<std::string>(j, "dp_group", e.dp_group);
+  e.dp_arena_mb = static_cast<size_t>(jget<long>(j, "dp_arena_mb", 0));
   return e;
 }
 
@@ -440,6 +447,56 @@ void* die_worker_create(const char* opts_json, char** err) {
   }
 }
 int die_worker_port(void* w) { return static_cast<WorkerNode*>(w)->port(); }
+
+// ---- data-parallel follower (rank >= 1): serves shards on a background thread ----
+struct DpFollowerHandle {
+  std::thread th;
+  std::atomic<bool> stop{false};
+  std::atomic<bool> running{true};
+  std::atomic<long> served{0};
+  std::mutex mu;
+  std::string error;
+};
+void* die_dp_follower_start(const char* opts_json, char** err) {
+  try {
+    Json j = Json::parse(opts_json);
+    const std::string model = jget<std::string>(j, "model_path", "");
+    EngineOptions eo = engine_opts(j.contains("engine") ? j.at("engine") : Json::object());
+    eo.max_batch = jget<int>(j, "max_batch", eo.max_batch);
+    auto* h = new DpFollowerHandle();
+    h->th = std::thread([h, model, eo] {
+      try {
+        h->served = run_dp_follower(model, eo, &h->stop);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(h->mu);
+        h->error = e.what();
+      }
+      h->running = false;
+    });
+    return h;
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+char* die_dp_follower_status(void* p) {
+  auto* h = static_cast<DpFollowerHandle*>(p);
+  Json j = Json::object();
+  j["running"] = h->running.load();
+  j["served"] = static_cast<long long>(h->served.load());
+  std::lock_guard<std::mutex> g(h->mu);
+  j["error"] = h->error;
+  return dup(j.dump());
+}
+// Stop (if still running) and join; returns batches served.
+long die_dp_follower_join(void* p, int stop) {
+  auto* h = static_cast<DpFollowerHandle*>(p);
+  if (stop) h->stop = true;
+  if (h->th.joinable()) h->th.join();
+  const long n = h->served.load();
+  delete h;
+  return n;
+}
 char* die_worker_health(void* w) { return dup(static_cast<WorkerNode*>(w)->getHealth().dump()); }
 void die_worker_stop(void* w) { static_cast<WorkerNode*>(w)->stop(); }
 void die_worker_destroy(void* w) { delete static_cast<WorkerNode*>(w); }

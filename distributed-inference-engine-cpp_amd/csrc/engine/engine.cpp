@@ -211,7 +211,7 @@ class CpuEngine : public Engine {
         x->f.assign(B * numel, 0.f);
         for (size_t i = 0; i < B; ++i) {
           const size_t n = std::min(job.items[i].len, numel);
-          std::memcpy(x->f.data() + i * numel, job.items[i].input, n * sizeof(float));
+          if (n) std::memcpy(x->f.data() + i * numel, job.items[i].input, n * sizeof(float));
         }
         auto y = exec_.run(x);
         outbuf = std::move(y->f);
@@ -254,6 +254,7 @@ std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const E
 }
 
 std::unique_ptr<Engine> create_engine(const std::string& model_path, const EngineOptions& opt) {
+  if (opt.dp_world >= 1 && !opt.dp_group.empty() && opt.dp_comm == nullptr) return create_dp_engine(model_path, opt);
   if (opt.device != "cpu") {
     std::string why;
     auto e = create_hip_engine(model_path, opt, &why);

@@ -20,6 +20,8 @@
 
 namespace die {
 
+class Communicator;
+
 // A per-sample host buffer of input_numel floats (pinned when the engine is a GPU engine).
 struct SampleBuffer {
   float* data = nullptr;
@@ -69,6 +71,11 @@ struct BatchResult {
   // input; ntok = number of values found.
   const int* status = nullptr;
   const int* ntok = nullptr;
+  // Data-parallel engines with a device all-gather: outputs/status hold `gathered` ranks' shards
+  // (rank r's rows at [r * B, (r + 1) * B), B = items submitted per rank); status/ntok stride
+  // between ranks is `status_stride`.
+  int gathered = 1;
+  int status_stride = 0;
 };
 
 using BatchDone = std::function<void(BatchResult&)>;
@@ -100,6 +107,13 @@ class Engine {
   virtual SamplePool& sample_pool() = 0;
   // Bytes of input_data text a SampleBuffer can carry for device decode (0 = not supported).
   virtual size_t text_capacity() const { return 0; }
+  // Make host memory DMA-able for this engine (HIP: hipHostRegister); no-op elsewhere.
+  virtual void register_host_memory(void* p, size_t bytes) {
+    (void)p;
+    (void)bytes;
+  }
+  // True when the engine all-gathers outputs across data-parallel ranks itself (RCCL).
+  virtual bool device_gather() const { return false; }
 
   // Synchronous helpers with the reference's padding rules: predict() pads or truncates to the
   // model input (src/inference_engine.cpp:100-103); batchPredict() pads short inputs and, unlike
@@ -130,6 +144,13 @@ struct EngineOptions {
   std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
   int cpu_threads = 0;
   int shard_id = 0;
+  // Data parallel (one process per GPU): dp_world ranks share the DpGroup segment
+  // `dp_group`; rank 0 is the leader that owns the worker, ranks >= 1 run run_dp_follower().
+  int dp_world = 0;
+  int dp_rank = 0;
+  std::string dp_group;
+  size_t dp_arena_mb = 0;          // input arena size (0 = sized from the model)
+  Communicator* dp_comm = nullptr;  // set internally: RCCL communicator handed to the HIP engine
 };
 
 // Factory: HIP engine when a GPU is visible and device != cpu, else the CPU executor (the
@@ -137,6 +158,12 @@ struct EngineOptions {
 std::unique_ptr<Engine> create_engine(const std::string& model_path, const EngineOptions& opt);
 
 std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const EngineOptions& opt);
+// Data-parallel leader (rank 0): creates the DpGroup, the communicator and the local engine, waits
+// for the followers, and shards every submitted batch over the ranks.
+std::unique_ptr<Engine> create_dp_engine(const std::string& model_path, const EngineOptions& opt);
+// Data-parallel follower (rank >= 1): attach, build the local engine on this process's GPU and
+// serve shards until the leader stops the group or *stop becomes true.  Returns batches served.
+long run_dp_follower(const std::string& model_path, const EngineOptions& opt, const std::atomic<bool>* stop);
 // Defined in the HIP translation unit; returns nullptr (with `why` set) when no GPU is usable.
 std::unique_ptr<Engine> create_hip_engine(const std::string& model_path, const EngineOptions& opt, std::string* why);
 

@@ -26,6 +26,7 @@
 #include "../kernels/kernels.h"
 #include "engine.h"
 #include "hip_plan.h"
+#include "../parallel/comm.h"
 
 namespace die {
 
@@ -55,12 +56,19 @@ class HipEngine : public Engine {
     in_numel_ = plan_.input_numel;
     out_numel_ = plan_.output_numel;
 
+    comm_ = opt.dp_comm;
+    dp_world_ = comm_ ? comm_->world() : 1;
     HIP_CHECK(hipMalloc(&params_, std::max<size_t>(plan_.params.size(), 256)));
-    HIP_CHECK(hipMemcpy(params_, plan_.params.data(), plan_.params.size(), hipMemcpyHostToDevice));
     HIP_CHECK(hipMalloc(&arena_, std::max<size_t>(plan_.arena_bytes, 256)));
     HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+    if (!comm_ || comm_->rank() == 0)
+      HIP_CHECK(hipMemcpy(params_, plan_.params.data(), plan_.params.size(), hipMemcpyHostToDevice));
+    if (comm_) {  // data parallel: every rank gets the packed weights from rank 0 over xGMI
+      comm_->broadcast(params_, plan_.params.size(), 0, s_compute_);
+      HIP_CHECK(hipStreamSynchronize(s_compute_));
+    }
     if (opt.device_decode) text_cap_ = (in_numel_ * 24 + 4095) / 4096 * 4096;  // up to 23 chars + separator per value
     slots_.resize(depth_);
     for (auto& sl : slots_) {
@@ -71,6 +79,16 @@ class HipEngine : public Engine {
       HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * max_batch_));
       HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
       HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * 2 * max_batch_));
+      HIP_CHECK(hipMemset(sl.d_status, 0, sizeof(int) * 2 * max_batch_));
+      if (comm_) {
+        HIP_CHECK(hipMalloc(&sl.d_gather, sizeof(float) * out_numel_ * max_batch_ * dp_world_));
+        HIP_CHECK(hipMalloc(&sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_));
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_gather), sizeof(float) * out_numel_ * max_batch_ * dp_world_,
+                                hipHostMallocDefault));
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_gstatus), sizeof(int) * 2 * max_batch_ * dp_world_,
+                                hipHostMallocDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&sl.ev_gather, hipEventDisableTiming));
+      }
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_status), sizeof(int) * 2 * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipMalloc(&sl.d_in, sizeof(float) * in_numel_ * max_batch_));
@@ -144,6 +162,13 @@ class HipEngine : public Engine {
       (void)hipFree(sl.d_status);
       (void)hipHostFree(sl.h_lens);
       (void)hipHostFree(sl.h_status);
+      if (comm_) {
+        (void)hipFree(sl.d_gather);
+        (void)hipFree(sl.d_gstatus);
+        (void)hipHostFree(sl.h_gather);
+        (void)hipHostFree(sl.h_gstatus);
+        (void)hipEventDestroy(sl.ev_gather);
+      }
       (void)hipHostFree(sl.h_out);
       (void)hipEventDestroy(sl.ev_h2d);
       (void)hipEventDestroy(sl.ev_fwd0);
@@ -151,6 +176,7 @@ class HipEngine : public Engine {
       (void)hipEventDestroy(sl.ev_d2h);
     }
     pool_.reset();
+    for (void* p : registered_) (void)hipHostUnregister(p);
     (void)hipFree(params_);
     (void)hipFree(arena_);
     (void)hipFree(ws_);
@@ -167,6 +193,12 @@ class HipEngine : public Engine {
   int max_batch() const override { return max_batch_; }
   SamplePool& sample_pool() override { return *pool_; }
   size_t text_capacity() const override { return text_cap_; }
+  bool device_gather() const override { return comm_ != nullptr; }
+  void register_host_memory(void* p, size_t bytes) override {
+    HIP_CHECK(hipSetDevice(dev_));
+    HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    registered_.push_back(p);
+  }
 
   void wait_for_slot() override {
     std::unique_lock<std::mutex> lk(mu_);
@@ -241,11 +273,30 @@ class HipEngine : public Engine {
         encode_forward(buckets_[bi], slot, s_compute_);
       }
       HIP_CHECK(hipEventRecord(sl.ev_fwd1, s_compute_));
-      HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_fwd1, 0));
-      HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_d2h_));
-      if (any_text)
-        HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_d2h_));
-      HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
+      if (comm_) {
+        // data parallel: every rank contributes its B rows (and decode status) to rank 0 over xGMI;
+        // the same collectives in the same order on every rank, whatever its shard holds.
+        comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, s_compute_);
+        comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, s_compute_);
+        HIP_CHECK(hipEventRecord(sl.ev_gather, s_compute_));
+        if (comm_->rank() == 0) {
+          HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_gather, 0));
+          HIP_CHECK(hipMemcpyAsync(sl.h_gather, sl.d_gather, sizeof(float) * out_numel_ * B * dp_world_,
+                                   hipMemcpyDeviceToHost, s_d2h_));
+          HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
+                                   hipMemcpyDeviceToHost, s_d2h_));
+          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
+        } else {
+          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
+        }
+        job.has_text = text_cap_ > 0;
+      } else {
+        HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_fwd1, 0));
+        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_d2h_));
+        if (any_text)
+          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_d2h_));
+        HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
+      }
     } catch (const std::exception& e) {
       job.error = e.what();
     }
@@ -275,6 +326,7 @@ class HipEngine : public Engine {
     j["arena_mib"] = static_cast<double>(plan_.arena_bytes) / (1 << 20);
     j["pinned_samples"] = static_cast<long long>(pool_->allocated());
     j["device_decode"] = text_cap_ > 0;
+    j["dp_rank"] = comm_ ? comm_->rank() : 0;
     j["text_capacity"] = static_cast<long long>(text_cap_);
     j["autotuned"] = !tune_.empty();
     j["tuned_conv_us_at_max_batch"] = tuned_conv_us_;
@@ -529,6 +581,11 @@ class HipEngine : public Engine {
 
  private:
   struct Slot {
+    float* d_gather = nullptr;  // data parallel: [world][max_batch][out_numel]
+    int* d_gstatus = nullptr;
+    float* h_gather = nullptr;
+    int* h_gstatus = nullptr;
+    hipEvent_t ev_gather{};
     float* d_in = nullptr;
     float* d_out = nullptr;
     float* h_out = nullptr;
@@ -576,6 +633,13 @@ class HipEngine : public Engine {
             r.status = sl.h_status;
             r.ntok = sl.h_status + max_batch_;
           }
+          if (comm_) {
+            r.gathered = dp_world_;
+            r.outputs = comm_->rank() == 0 ? sl.h_gather : nullptr;
+            r.status = comm_->rank() == 0 && job.has_text ? sl.h_gstatus : nullptr;
+            r.ntok = r.status ? sl.h_gstatus + max_batch_ : nullptr;
+            r.status_stride = 2 * max_batch_;
+          }
           batches_++;
           images_ += job.B;
           device_ms_total_ = device_ms_total_.load() + ms;
@@ -606,6 +670,9 @@ class HipEngine : public Engine {
   Plan plan_;
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
+  Communicator* comm_ = nullptr;  // data parallel (not owned)
+  int dp_world_ = 1;
+  std::vector<void*> registered_;
   uint8_t* params_ = nullptr;
   uint8_t* arena_ = nullptr;
   float* ws_ = nullptr;

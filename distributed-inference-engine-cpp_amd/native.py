@@ -85,6 +85,9 @@ def lib() -> C.CDLL:
         sig("die_engine_run", C.c_int, vp, f32p, C.c_long, C.c_long, f32p, errp)
         sig("die_engine_run_text", C.c_int, vp, C.c_char_p, i64p, C.c_long, f32p, C.POINTER(C.c_int), errp)
         sig("die_engine_profile", vp, vp, C.c_int, C.c_int)
+        sig("die_dp_follower_start", vp, cp, errp)
+        sig("die_dp_follower_status", vp, vp)
+        sig("die_dp_follower_join", C.c_long, vp, C.c_int)
         sig("die_cpu_run", vp, cp, f32p, i64p, C.c_int, i64p, C.POINTER(C.c_int), errp)
         sig("die_onnx_summary", vp, cp, errp)
         sig("die_worker_create", vp, cp, errp)
@@ -372,6 +375,32 @@ def onnx_summary(model_path: str) -> Dict[str, Any]:
 
 
 # ---- servers ------------------------------------------------------------------------------------------
+
+class DpFollower:
+    """Data-parallel follower rank (csrc/engine/dp_engine.cpp): attaches to the leader's DpGroup
+    `group`, builds its local engine (RCCL communicator for HIP, host communicator for CPU) and
+    serves its shard of every batch on a background native thread."""
+
+    def __init__(self, model_path: str, group: str, rank: int, world: int, max_batch: int = 32, **engine):
+        eng = dict(engine)
+        eng.update(dp_group=group, dp_rank=rank, dp_world=world)
+        o = dict(model_path=model_path, max_batch=max_batch, engine=eng)
+        err = _err_box()
+        self.h = lib().die_dp_follower_start(json.dumps(o).encode(), C.byref(err))
+        if not self.h:
+            _raise_if(err, "dp follower")
+
+    def status(self) -> Dict[str, Any]:
+        return json.loads(_take_str(lib().die_dp_follower_status(self.h)))
+
+    def join(self, stop: bool = False) -> int:
+        """Wait for the follower to finish (the leader stops the group), or stop it; returns batches served."""
+        if not self.h:
+            return 0
+        n = lib().die_dp_follower_join(self.h, int(stop))
+        self.h = None
+        return n
+
 
 class Worker:
     """In-process worker node (HTTP on 127.0.0.1:<port>, port 0 = ephemeral)."""
