@@ -25,6 +25,7 @@ bool CircuitBreaker::allowRequest() {
     if (now() - last_failure_ >= timeout_) {
       state_ = CircuitState::HALF_OPEN;
       success_count_ = 0;
+      ++half_opened_;
       return true;
     }
     return false;
@@ -38,6 +39,7 @@ void CircuitBreaker::recordSuccess() {
     if (++success_count_ >= success_threshold_) {
       state_ = CircuitState::CLOSED;
       failure_count_ = 0;
+      ++closed_;
     }
   } else {
     failure_count_ = 0;
@@ -48,7 +50,10 @@ void CircuitBreaker::recordFailure() {
   std::lock_guard<std::mutex> g(mutex_);
   ++failure_count_;
   last_failure_ = now();
-  if (failure_count_ >= failure_threshold_ || state_ == CircuitState::HALF_OPEN) state_ = CircuitState::OPEN;
+  if ((failure_count_ >= failure_threshold_ || state_ == CircuitState::HALF_OPEN) && state_ != CircuitState::OPEN) {
+    state_ = CircuitState::OPEN;
+    ++opened_;
+  }
 }
 
 std::string CircuitBreaker::getStateString() const { return circuit_state_name(getState()); }

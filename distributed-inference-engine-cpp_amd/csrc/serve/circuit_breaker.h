@@ -30,6 +30,11 @@ class CircuitBreaker {
   std::string getStateString() const;
   int getFailureCount() const;
   int getSuccessCount() const { return success_count_.load(); }
+  // Transition counters (observability superset; fault-injection drills assert on them because a
+  // HALF_OPEN window can be shorter than any polling interval).
+  long long opened() const { return opened_.load(); }
+  long long half_opened() const { return half_opened_.load(); }
+  long long closed() const { return closed_.load(); }
 
  private:
   std::chrono::steady_clock::time_point now() const { return clock_ ? clock_() : std::chrono::steady_clock::now(); }
@@ -42,6 +47,7 @@ class CircuitBreaker {
   Clock clock_;
   std::chrono::steady_clock::time_point last_failure_;
   mutable std::mutex mutex_;
+  std::atomic<long long> opened_{0}, half_opened_{0}, closed_{0};
 };
 
 const char* circuit_state_name(CircuitState s);

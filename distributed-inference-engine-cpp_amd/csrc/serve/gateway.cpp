@@ -148,6 +148,9 @@ Json Gateway::getStats() const {
     b["state"] = kv.second->getStateString();
     b["failures"] = kv.second->getFailureCount();
     b["successes"] = kv.second->getSuccessCount();
+    b["opened"] = kv.second->opened();
+    b["half_opened"] = kv.second->half_opened();
+    b["closed"] = kv.second->closed();
     arr.push_back(std::move(b));
   }
   s["circuit_breakers"] = arr;
