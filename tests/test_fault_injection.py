@@ -38,3 +38,14 @@ def test_fault_drill(cluster, fault):
     assert rep["gateway"]["failovers"] > 0
     states = [s for _, s in rep["timeline"]]
     assert "OPEN" in states
+
+
+def test_diagnostics_script(cluster):
+    import subprocess
+
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "diagnostics.sh")
+    r = subprocess.run(["bash", script, str(cluster.gw_port), " ".join(str(p) for p in cluster.ports)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=120)
+    out = r.stdout.decode()
+    assert r.returncode == 0, out
+    assert "0 failed" in out
