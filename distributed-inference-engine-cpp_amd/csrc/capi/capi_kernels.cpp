@@ -135,6 +135,12 @@ int die_kern_decode(uint64_t text, long long text_cap, uint64_t lens, int B, uin
                                                     P<int>(ntok), P<void>(scratch), S(stream)));
 }
 
+int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, int H, int W, int Ho, int Wo, int relu,
+                  uint64_t stream) {
+  return static_cast<int>(kern::conv_stem7x7(P<const uint16_t>(x), P<const uint16_t>(w), P<const float>(bias),
+                                             P<uint16_t>(out), B, H, W, Ho, Wo, relu, S(stream)));
+}
+
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
 char* die_plan_summary(const char* model_path, int max_batch, char** err) {
   try {
@@ -147,7 +153,7 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
     Json ops = Json::array();
     for (auto& o : p.ops) {
       Json e = Json::object();
-      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention"};
+      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention", "stem"};
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;

@@ -499,6 +499,12 @@ class HipEngine : public Engine {
           e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
                                      op.H, op.W, op.C, st);
           break;
+        case PlanOp::STEM:
+          e = kern::conv_stem7x7(static_cast<const uint16_t*>(buf(op.in)),
+                                 reinterpret_cast<const uint16_t*>(params_ + op.w_off), prm(op.bias_off),
+                                 static_cast<uint16_t*>(buf(op.out)), B, op.conv.H, op.conv.W, op.conv.Ho, op.conv.Wo,
+                                 op.conv.relu, st);
+          break;
         case PlanOp::LAYERNORM:
           e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
                                    prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st);
@@ -552,7 +558,7 @@ class HipEngine : public Engine {
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
-                                  "layernorm", "tokens", "gather_rows", "attention"};
+                                  "layernorm", "tokens", "gather_rows", "attention", "stem"};
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

@@ -346,6 +346,20 @@ class Planner {
     p.name = n.name;
     p.in = in_buf;
     p.in2 = res_buf;
+    // ResNet stem (7x7/2, pad 3, 4 stored input channels, 64 outputs, plain epilogue): LDS-patch kernel
+    const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && Cstore == 4 &&
+                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur);
+    if (stem) {
+      p.kind = PlanOp::STEM;
+      std::vector<uint16_t> ws(64 * 224, 0);
+      for (int co = 0; co < Cout; ++co)
+        for (int ci = 0; ci < Cin; ++ci)
+          for (int ky = 0; ky < 7; ++ky)
+            for (int kx = 0; kx < 7; ++kx)
+              ws[co * 224 + ky * 32 + kx * 4 + ci] =
+                  to_bf16(wt.f[((static_cast<size_t>(co) * Cin + ci) * KH + ky) * KW + kx] * scale[co]);
+      wp.swap(ws);
+    }
     p.w_off = push_bf16(wp);
     p.bias_off = push_f32(shift);
     auto& a = p.conv;
@@ -1227,7 +1241,7 @@ class Planner {
 std::string Plan::summary() const {
   std::ostringstream os;
   size_t convs = 0;
-  for (auto& o : ops) convs += o.kind == PlanOp::CONV;
+  for (auto& o : ops) convs += o.kind == PlanOp::CONV || o.kind == PlanOp::STEM;
   os << ops.size() << " device ops (" << convs << " MFMA conv/gemm), arena " << arena_bytes / (1 << 20) << " MiB, params "
      << params.size() / (1 << 20) << " MiB, " << flops_per_sample / 1e9 << " GFLOP/sample";
   return os.str();

@@ -38,7 +38,7 @@ struct PlanBuf {
 struct PlanOp {
   enum Kind {
     INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32,
-    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION
+    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION, STEM
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).

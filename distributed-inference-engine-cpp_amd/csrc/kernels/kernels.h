@@ -74,6 +74,11 @@ hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, in
 hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 
+// 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:
+// w = [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8), out = act(conv + bias) NHWC bf16.
+hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
+                        int Ho, int Wo, int relu, hipStream_t s);
+
 // ---- device JSON decode (decode.hip) ----
 // Sample b's number-list text lives at text + b * text_cap (text_cap % 4096 == 0) with lens[b]
 // bytes (-1 = not a text sample: skipped).  Writes out[b][0..numel) (values, zero padded),

@@ -1,0 +1,121 @@
+// 7x7 / stride 2 / pad 3 stem convolution (ResNet conv0) on MFMA, gfx950.
+//
+// The generic implicit-GEMM kernel runs this layer at ~75 TFLOP/s: with 4 input channels every
+// lane gathers 8-byte pieces of 16 different pixels per k-step.  Here a block owns an 8 x 16 tile of
+// output pixels and all 64 output channels:
+//   * the 21 x 38 x 4-channel input patch it needs (rows 2*8+5, cols 2*16+6) is staged in LDS once;
+//   * K is ordered (ky, kx, c) with kx padded 7 -> 8 (zero weights), so K = 7*8*4 = 224 = 7 MFMA
+//     k-steps and k-step s is exactly filter row ky = s.  Lane group j of v_mfma_f32_16x16x32_bf16
+//     reads taps (2j, 2j+1) of that row: 16 contiguous, 16-byte-aligned bytes of the patch, and the
+//     16 lanes of a group read 16 consecutive output pixels = 256 contiguous bytes (no bank
+//     conflicts);
+//   * weights [64][224] (BN folded) sit in LDS with a 232-element pitch (conflict-free A reads);
+//   * epilogue: + bias, optional ReLU, bf16, staged through LDS (XOR-swizzled) so each output pixel's
+//     128 bytes go out as 16-byte stores.
+#include "common.h"
+#include "kernels.h"
+
+namespace die {
+namespace kern {
+
+using namespace die::k;
+
+namespace {
+
+constexpr int TY = 8, TX = 16;               // output tile
+constexpr int PY = 2 * TY + 5, PX = 2 * TX + 6;  // patch (PX even: kx padded to 8)
+constexpr int KS = 224, WP = 232;            // K and weight LDS pitch (elements)
+constexpr int NCH = 64;
+
+__global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                      int H, int W, int Ho, int Wo, int relu, int tiles_x) {
+  __shared__ __attribute__((aligned(16))) uint16_t wl[NCH * WP];
+  __shared__ __attribute__((aligned(16))) uint16_t patch[PY * PX * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.y;
+  const int ty0 = (blockIdx.x / tiles_x) * TY, tx0 = (blockIdx.x % tiles_x) * TX;
+  // weights -> LDS (64 x 224 bf16 = 28 chunks of 16 B per row)
+  for (int i = tid; i < NCH * (KS / 8); i += 256) {
+    const int r = i / (KS / 8), c = i % (KS / 8);
+    *reinterpret_cast<uint4*>(wl + r * WP + c * 8) = *reinterpret_cast<const uint4*>(w + r * KS + c * 8);
+  }
+  // input patch -> LDS: pixel (iy, ix) = 4 bf16 = 8 bytes; outside the image -> 0
+  const int iy0 = 2 * ty0 - 3, ix0 = 2 * tx0 - 3;
+  const uint16_t* xb = x + static_cast<size_t>(b) * H * W * 4;
+  for (int i = tid; i < PY * PX; i += 256) {
+    const int py = i / PX, px = i % PX;
+    const int iy = iy0 + py, ix = ix0 + px;
+    uint2 v = make_uint2(0, 0);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = *reinterpret_cast<const uint2*>(xb + (static_cast<size_t>(iy) * W + ix) * 4);
+    *reinterpret_cast<uint2*>(patch + i * 4) = v;
+  }
+  __syncthreads();
+  // wave w: output rows 2w, 2w+1 of the tile (16 pixels each) x 64 channels
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int j = lane >> 4, px_l = lane & 15;
+#pragma unroll
+  for (int ky = 0; ky < 7; ++ky) {
+    bf16x8 bf[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int oy = 2 * wave + m;
+      const int py = 2 * oy + ky, px = 2 * px_l + 2 * j;
+      bf[m] = *reinterpret_cast<const bf16x8*>(patch + (py * PX + px) * 4);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[m], acc[n][m], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // weights -> output stage [128 px][64 ch] bf16, 16-B chunk c of pixel p at chunk c ^ (p & 7)
+  uint16_t* stage = wl;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int ch = n * 16 + 4 * j;  // this lane's 4 consecutive channels
+    const float4 bv = *reinterpret_cast<const float4*>(bias + ch);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int p = (2 * wave + m) * TX + px_l;
+      float v0 = acc[n][m][0] + bv.x, v1 = acc[n][m][1] + bv.y, v2 = acc[n][m][2] + bv.z, v3 = acc[n][m][3] + bv.w;
+      if (relu) {
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+        v2 = fmaxf(v2, 0.f);
+        v3 = fmaxf(v3, 0.f);
+      }
+      const int chunk = (ch >> 3) ^ (p & 7);
+      *reinterpret_cast<uint2*>(stage + p * NCH + chunk * 8 + (ch & 7)) = make_uint2(pack2(v0, v1), pack2(v2, v3));
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < TY * TX * (NCH / 8); i += 256) {
+    const int p = i >> 3, c = i & 7;
+    const int oy = ty0 + p / TX, ox = tx0 + p % TX;
+    if (oy >= Ho || ox >= Wo) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(stage + p * NCH + ((c ^ (p & 7)) << 3));
+    *reinterpret_cast<uint4*>(out + ((static_cast<size_t>(b) * Ho + oy) * Wo + ox) * NCH + c * 8) = v;
+  }
+}
+
+}  // namespace
+
+static_assert(TY * TX * NCH <= NCH * WP, "output stage must fit in the weight buffer");
+
+hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
+                        int Ho, int Wo, int relu, hipStream_t s) {
+  if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1) return hipErrorInvalidValue;
+  const int tiles_x = (Wo + TX - 1) / TX, tiles_y = (Ho + TY - 1) / TY;
+  hipLaunchKernelGGL(stem7x7_kernel, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho, Wo, relu,
+                     tiles_x);
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace die

@@ -239,3 +239,28 @@ def decode_json_numbers(texts, numel, text_cap=None):
                            _ptr(scratch), _stream())
     _check(rc, "decode_json_numbers")
     return out, status, ntok
+
+
+def pack_stem_weight(w):
+    """[64, C<=4, 7, 7] float -> [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8)."""
+    import torch
+
+    co, ci = w.shape[:2]
+    wp = torch.zeros((co, 7, 8, 4), dtype=torch.float32, device=w.device)
+    wp[:, :, :7, :ci] = w.float().permute(0, 2, 3, 1)
+    return wp.reshape(co, 224).to(torch.bfloat16).contiguous()
+
+
+def conv_stem7x7(x_nhwc4, w, bias, relu=True):
+    """ResNet stem on the LDS-patch kernel: x [B,H,W,4] bf16, w [64,C,7,7] -> [B,Ho,Wo,64] bf16."""
+    import torch
+
+    B, H, W, C = x_nhwc4.shape
+    assert C == 4 and w.shape[0] == 64
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty((B, Ho, Wo, 64), dtype=torch.bfloat16, device=x_nhwc4.device)
+    b = bias.float().contiguous()
+    rc = native.kernels().die_kern_stem(_ptr(x_nhwc4.contiguous()), _ptr(pack_stem_weight(w)), _ptr(b), _ptr(out), B, H,
+                                        W, Ho, Wo, int(relu), _stream())
+    _check(rc, "conv_stem7x7")
+    return out

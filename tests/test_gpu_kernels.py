@@ -135,6 +135,29 @@ def test_stem_conv_with_input_prep(native):
     assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-3
 
 
+@pytest.mark.parametrize("B,H,W,relu", [(2, 224, 224, True), (3, 64, 64, False), (1, 37, 45, True)])
+def test_stem_lds_kernel(native, B, H, W, relu):
+    """7x7/2 LDS-patch stem kernel vs torch fp32 (odd sizes exercise the tile tails)."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    g = torch.Generator(device="cuda").manual_seed(B * 100 + H)
+    x = torch.rand(B, 3, H, W, device="cuda", generator=g) * 2 - 1
+    xp = K.input_prep(x, torch.ones(3, device="cuda"), torch.zeros(3, device="cuda"), cp=4)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) / 12.0).to(torch.bfloat16).float()
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    out = K.conv_stem7x7(xp, w, bias, relu=relu)
+    ref = torch.nn.functional.conv2d(xp[..., :3].permute(0, 3, 1, 2).float(), w, bias, stride=2, padding=3)
+    if relu:
+        ref = torch.relu(ref)
+    torch.cuda.synchronize()
+    assert out.shape == (B, ref.shape[2], ref.shape[3], 64)
+    assert rel_err(out.permute(0, 3, 1, 2).float(), ref) < 5e-3
+    # bit-identical on repeat (race screen)
+    again = K.conv_stem7x7(xp, w, bias, relu=relu)
+    assert torch.equal(out, again)
+
+
 def test_conv_repeatable_bitwise(native):
     """Race screen: repeated launches at several shapes must agree bit for bit."""
     torch = _t()
