@@ -122,6 +122,7 @@ def main():
             "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
             "cpu_quota": _cpu_quota(), "device_decode": e1.get("device_decode"),
             "decode_fallbacks": h1.get("decode_fallbacks"),
+            "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
         wk.stop()
     elif args.mode == "dp":

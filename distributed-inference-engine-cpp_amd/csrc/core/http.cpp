@@ -430,6 +430,7 @@ void HttpServer::reactor_loop(Reactor* r) {
         }
         c->in.erase(0, he + 4);
         c->headers_done = true;
+        c->req.t_headers = std::chrono::steady_clock::now();
         if (!c->chunked) {
           c->req.body.reserve(c->body_len + 64);
           c->req.body.resize(c->body_len);

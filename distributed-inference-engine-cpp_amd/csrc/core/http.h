@@ -30,6 +30,7 @@ struct HttpRequest {
   std::vector<std::pair<std::string, std::string>> headers;  // names lower-cased
   std::string body;    // capacity always >= size + 64 (slack for SIMD parsers)
   bool keep_alive = true;
+  std::chrono::steady_clock::time_point t_headers{};  // when the request head was parsed
   std::string_view header(std::string_view name) const;  // name must be lower-case
 };
 

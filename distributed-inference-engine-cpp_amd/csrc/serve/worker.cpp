@@ -75,7 +75,9 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       items.push_back(it);
     }
     const size_t B = reqs.size();
-    eng->submit(std::move(items), [B, finish](BatchResult& br) {
+    const auto t_dispatch = std::chrono::steady_clock::now();
+    eng->submit(std::move(items), [B, finish, t_dispatch](BatchResult& br) {
+      const auto t_done = std::chrono::steady_clock::now();
       if (!br.ok) {
         finish({}, std::make_exception_ptr(std::runtime_error(br.error)));
         return;
@@ -84,6 +86,8 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       const int64_t per = B ? static_cast<int64_t>(br.wall_us) / static_cast<int64_t>(B) : 0;
       for (size_t i = 0; i < B; ++i) {
         out[i].inference_time_us = per;
+        out[i].t_dispatch = t_dispatch;
+        out[i].t_done = t_done;
         if (br.status && br.status[i]) {
           out[i].decode_status = br.status[i];
           out[i].ntok = br.ntok[i];
@@ -166,6 +170,8 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   sink.defer = text_cap > 0;
   int seen = 0;
   const auto t_parse = std::chrono::steady_clock::now();
+  const auto t_start = t_parse;
+  if (req.t_headers.time_since_epoch().count()) h_recv_.add(t_start - req.t_headers);
   InputKey key;
   size_t text_len = 0, text_off = 0;
   try {
@@ -223,8 +229,12 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     return;
   }
   if (text_len) device_decoded_.fetch_add(1, std::memory_order_relaxed);
+  const auto t_queued = std::chrono::steady_clock::now();
+  h_parse_.add(t_queued - t_start);
 
   Pending p;
+  p.t_start = t_start;
+  p.t_queued = t_queued;
   p.request_id = std::move(sink.id);
   p.buf = sink.buf;
   p.len = sink.n;
@@ -238,9 +248,10 @@ void WorkerNode::dispatch(Pending p, Responder res) {
   const SampleBuffer buf = p.buf;
   const size_t text_len = p.text_len, text_off = p.text_off;
   const InputKey key = p.key;
+  const auto t_start = p.t_start, t_queued = p.t_queued;
   std::string id_copy = p.request_id;
-  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, id = std::move(id_copy)](
-                                     Result* r, std::exception_ptr err) mutable {
+  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, t_start, t_queued,
+                                  id = std::move(id_copy)](Result* r, std::exception_ptr err) mutable {
     if (err) {
       engine_->sample_pool().release(buf);
       errors_++;
@@ -266,12 +277,18 @@ void WorkerNode::dispatch(Pending p, Responder res) {
       return;
     }
     cache_.put(key, r->output);
+    h_queue_.add(r->t_dispatch - t_queued);
+    h_engine_.add(r->t_done - r->t_dispatch);
     auto out = std::make_shared<std::vector<float>>(std::move(r->output));
     const int64_t us = r->inference_time_us;
     std::string node = opt_.node_id;
-    res.defer([out, id = std::move(id), node = std::move(node), us] {
+    const auto t_done = r->t_done;
+    res.defer([this, out, id = std::move(id), node = std::move(node), us, t_start, t_done] {
       HttpResponse resp;
       resp.body = build_response(id, out->data(), out->size(), node, false, us);
+      const auto now = std::chrono::steady_clock::now();
+      h_respond_.add(now - t_done);
+      h_total_.add(now - t_start);
       return resp;
     });
   });
@@ -314,6 +331,7 @@ void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, size_t te
   p.buf = sink.buf;
   p.len = sink.n;
   p.key = key;
+  p.t_start = p.t_queued = std::chrono::steady_clock::now();
   dispatch(std::move(p), std::move(res));
 }
 
@@ -341,6 +359,14 @@ Json WorkerNode::getHealth() const {
   h["parse_gbps"] = parse_ns_.load() ? static_cast<double>(parse_bytes_.load()) / parse_ns_.load() : 0.0;
   h["device_decoded"] = static_cast<long long>(device_decoded_.load());
   h["decode_fallbacks"] = static_cast<long long>(decode_fallbacks_.load());
+  Json st = Json::object();
+  st["recv"] = h_recv_.snapshot();
+  st["parse"] = h_parse_.snapshot();
+  st["queue"] = h_queue_.snapshot();
+  st["engine"] = h_engine_.snapshot();
+  st["respond"] = h_respond_.snapshot();
+  st["total"] = h_total_.snapshot();
+  h["stages_us"] = st;
   h["http_threads"] = opt_.http_threads;
   h["engine"] = engine_->stats();
   h["engine"]["name"] = engine_->name();

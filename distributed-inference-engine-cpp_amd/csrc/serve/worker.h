@@ -21,6 +21,7 @@
 #include "../engine/engine.h"
 #include "batcher.h"
 #include "lru_cache.h"
+#include "stage_stats.h"
 
 namespace die {
 
@@ -63,12 +64,14 @@ class WorkerNode {
     size_t text_len = 0;  // > 0: buf holds input_data text for device decode instead
     size_t text_off = 0;  // offset of that text in the request body (host-fallback error offsets)
     InputKey key;
+    std::chrono::steady_clock::time_point t_start{}, t_queued{};
   };
   struct Result {
     std::vector<float> output;
     int64_t inference_time_us = 0;
     int decode_status = 0;  // device decode: bit 0 = needs host parse, 2 = too many values
     int ntok = 0;
+    std::chrono::steady_clock::time_point t_dispatch{}, t_done{};
   };
 
  private:
@@ -91,6 +94,9 @@ class WorkerNode {
   std::atomic<int64_t> errors_{0};
   std::atomic<int64_t> parse_ns_{0}, parse_bytes_{0}, parsed_{0};
   std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0};
+  // request stages: parse (body -> staging), queue (batcher wait), engine (submit -> outputs on
+  // host), respond (outputs -> serialised response), total (handler entry -> response)
+  StageHist h_recv_, h_parse_, h_queue_, h_engine_, h_respond_, h_total_;  // recv: head parsed -> body complete
   std::atomic<double> fault_fail_rate_{0.0};
   std::atomic<int> fault_latency_ms_{0};
   std::chrono::steady_clock::time_point started_;
