@@ -68,6 +68,8 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     a.splits = geti(j, "splits", 1);
     if (auto* v = j.find("ws")) a.ws = P<float>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("counters")) a.counters = P<int>(static_cast<uint64_t>(v->as_int()));
+    a.counters_n = geti(j, "counters_n", 0);
     if (tile < 0) tile = kern::choose_tile(a.M, a.N, a.K);
     return static_cast<int>(kern::conv_igemm(a, tile, S(stream)));
   } catch (...) {

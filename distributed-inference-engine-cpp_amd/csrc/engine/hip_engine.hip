@@ -117,6 +117,8 @@ class HipEngine : public Engine {
     HIP_CHECK(hipMalloc(&ws_, ws_bytes_));
     HIP_CHECK(hipMalloc(&zeros_, 4096));
     HIP_CHECK(hipMemset(zeros_, 0, 4096));
+    HIP_CHECK(hipMalloc(&counters_, sizeof(int) * kCounters));  // fused split-K tile counters
+    HIP_CHECK(hipMemset(counters_, 0, sizeof(int) * kCounters));
     // Validate every op eagerly at the largest bucket, tune, then capture one graph per
     // (bucket, slot).
     for (int s = 0; s < depth_; ++s) encode_forward(max_batch_, s, s_compute_);
@@ -181,6 +183,7 @@ class HipEngine : public Engine {
     (void)hipFree(arena_);
     (void)hipFree(ws_);
     (void)hipFree(zeros_);
+    (void)hipFree(counters_);
     (void)hipStreamDestroy(s_compute_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -335,7 +338,7 @@ class HipEngine : public Engine {
       for (size_t oi = 0; oi < plan_.ops.size(); ++oi)
         if (plan_.ops[oi].kind == PlanOp::CONV) {
           const Tune& x = tune_.back()[oi];
-          t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits));
+          t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits) + (x.fused ? "f" : ""));
         }
       j["tile_split_at_max_batch"] = t;
     }
@@ -345,6 +348,7 @@ class HipEngine : public Engine {
   struct Tune {
     int tile = 0;
     int splits = 1;
+    bool fused = false;  // split-K reduced in-kernel by the last split block (else a second kernel)
   };
 
   void* buf_ptr(int id, int s) {
@@ -372,6 +376,8 @@ class HipEngine : public Engine {
     a.shift2 = prm_ptr(op.b2_off);
     a.out2 = static_cast<uint16_t*>(buf_ptr(op.out2, s));
     a.zeros = zeros_;
+    a.counters = counters_;
+    a.counters_n = kCounters;
     return a;
   }
 
@@ -427,18 +433,21 @@ class HipEngine : public Engine {
         for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
           for (int sp = 1; sp <= 16; sp *= 2) {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
-            kern::ConvArgs a = base;
-            a.splits = sp;
-            if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;  // warm-up / validity
-            HIP_CHECK(hipEventRecord(e0, s_compute_));
-            for (int r = 0; r < 3; ++r) HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
-            HIP_CHECK(hipEventRecord(e1, s_compute_));
-            HIP_CHECK(hipEventSynchronize(e1));
-            float ms = 0;
-            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-            if (ms < best) {
-              best = ms;
-              bt = Tune{tile, sp};
+            for (int fused = 0; fused < (sp > 1 ? 2 : 1); ++fused) {
+              kern::ConvArgs a = base;
+              a.splits = sp;
+              if (!fused) a.counters = nullptr;
+              if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;  // warm-up / validity
+              HIP_CHECK(hipEventRecord(e0, s_compute_));
+              for (int r = 0; r < 3; ++r) HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
+              HIP_CHECK(hipEventRecord(e1, s_compute_));
+              HIP_CHECK(hipEventSynchronize(e1));
+              float ms = 0;
+              HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+              if (ms < best) {
+                best = ms;
+                bt = Tune{tile, sp, fused != 0};
+              }
             }
           }
         }
@@ -479,6 +488,7 @@ class HipEngine : public Engine {
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
           a.ws = ws_;
+          if (!t.fused) a.counters = nullptr;
           e = kern::conv_igemm(a, t.tile, st);
           break;
         }
@@ -574,6 +584,7 @@ class HipEngine : public Engine {
         const Tune t = tune_for(Bk, i);
         o["tile"] = t.tile;
         o["splits"] = t.splits;
+        o["fused_splitk"] = t.fused;
       }
       total += us[i];
       ops.push_back(o);
@@ -676,6 +687,8 @@ class HipEngine : public Engine {
   Plan plan_;
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
+  static constexpr int kCounters = 1 << 16;
+  int* counters_ = nullptr;
   Communicator* comm_ = nullptr;  // data parallel (not owned)
   int dp_world_ = 1;
   std::vector<void*> registered_;

@@ -273,6 +273,46 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         epilogue8(p, m, n, v);
       }
     }
+    if (!partial || !p.counters) return;
+    // Fused split-K reduction: the last split block of this tile to arrive sums every split's
+    // partial and runs the epilogue (no second kernel).  Hand-off per the agent-scope recipe
+    // (cdna_hip_programming §6 G16): every wave drains its slab stores, block barrier, ONE lane
+    // releases at agent scope and takes a ticket; the reducer's lane acquires at agent scope (which
+    // invalidates this CU's L1) before the barrier that precedes the plain slab loads.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);  // staging tile is dead now: reuse it for the broadcast
+    if (tid == 0) {
+      int* ctr = p.counters + blockIdx.x;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == p.splits - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const size_t slab = static_cast<size_t>(p.M) * p.N;
+    for (int g = tid; g < BM * GPR; g += 256) {
+      const int row = g / GPR;
+      const int cg = g - row * GPR;
+      const int m = m0 + row;
+      const int n = n0 + cg * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int s = 0; s < p.splits; ++s) {
+        const float4 a = ldf4(src + s * slab), b = ldf4(src + s * slab + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      epilogue8(p, m, n, v);
+    }
     return;
   }
   // ---- ragged N (e.g. a 10-class head): element-wise epilogue from registers ----
@@ -480,6 +520,9 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   const int eff = (nk + kt_per - 1) / kt_per;  // no empty slices
   ConvArgs b = a;
   b.splits = eff;
+  // fused split-K reduction needs a zeroed counter per output tile
+  const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
+  if (!fused) b.counters = nullptr;
   dim3 grid(tiles, eff);
   if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
@@ -500,7 +543,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4>), grid, dim3(256), 0, s, b, kt_per);
   }
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || eff == 1) return e;
+  if (e != hipSuccess || eff == 1 || fused) return e;
   const long long groups = static_cast<long long>(b.M) * (b.N / 8);
   const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
   hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);

@@ -35,6 +35,10 @@ struct ConvArgs {
   // and applies the epilogue.  splits == 1 -> epilogue fused in the GEMM kernel.
   int splits = 1;
   float* ws = nullptr;
+  // optional: counters_n zero-initialised ints -> the last split block of each tile reduces the
+  // partials and runs the epilogue itself (no second kernel); they return to zero after use.
+  int* counters = nullptr;
+  int counters_n = 0;
   // >= 16 zero bytes (device): source of the LDS-DMA loads for padding pixels / M tails.
   const uint16_t* zeros = nullptr;
 };

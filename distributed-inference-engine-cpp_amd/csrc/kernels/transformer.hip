@@ -118,28 +118,37 @@ __global__ void gather_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __r
 }
 
 // ---- fused attention ------------------------------------------------------------------------------
-// One block = (64 query rows, head h, image b); 4 waves x 16 query rows.  K [S][64] (XOR-swizzled
-// 128-B rows), V^T [64][SK+8] and each wave's P [16][SK+8] live in LDS.  QK^T and PV run on
-// v_mfma_f32_16x16x32_bf16; softmax in fp32 registers (a row's 16 key columns of a 16x16 tile are
-// spread over 16 lanes: max/sum reduce with xor-shuffles 1,2,4,8).
+// FlashAttention-style, on v_mfma_f32_32x32x16_bf16, for head dim 64 and S <= 256 (ViT: 197 tokens).
+// A block = (image b, head h, 4 query tiles of 32); each wave owns one 32-query tile.  K and V of the
+// (b, h) pair are staged in LDS once per block (K with XOR-swizzled 16-B chunks, V in plain rows
+// padded to 96 elements so the transposed reads below are bank-conflict free).
+//  * S^T = K Q^T (A = K rows from LDS, B = this wave's Q fragments kept in registers): the result has
+//    the QUERY on the lane and 32 KEYS in the 16 accumulator registers x 2 lane halves, so the
+//    softmax over keys is in-lane plus one xor-32 shuffle (online softmax across key tiles, exp2).
+//  * O^T += V^T P^T takes P^T straight from the accumulator registers as the B operand (no LDS, no
+//    lane movement: register 8s+j of lane half h is key 16s + 8(j>>2) + 4h + (j&3)); the A operand
+//    V^T comes from the row-major V image through ds_read_b64_tr_b16 (hardware transpose), two
+//    4-key reads per k-step in exactly that key order.
 constexpr int AT_D = 64;
+constexpr int VP = 96;  // V row pitch (elements)
 
-template <int SK>
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s16x4 ds_read_tr16(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
+}
+
+template <int NKT>
 __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                                                         const uint16_t* __restrict__ v, uint16_t* __restrict__ out,
-                                                        int S, int ldq, int ldk, int ldv, int ldo, float scale) {
-  constexpr int NT = SK / 16;   // key tiles
-  constexpr int NKS = SK / 32;  // PV k-steps
-  constexpr int VP = SK + 8;    // padded pitch (conflict-free transposed reads)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[SK * AT_D + AT_D * VP + 64 * VP];
-  uint16_t* Ks = lds;
-  uint16_t* Vt = lds + SK * AT_D;
-  uint16_t* P = Vt + AT_D * VP;
-
+                                                        int S, int ldq, int ldk, int ldv, int ldo, float scale_log2) {
+  constexpr int SK = NKT * 32;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[SK * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[SK * VP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.y, b = blockIdx.z;
   const long long rowbase = static_cast<long long>(b) * S;
-  // K -> LDS (swizzled chunks), V -> LDS transposed; rows >= S are zero.
   for (int i = tid; i < SK * 8; i += 256) {
     const int s = i >> 3, c = i & 7;
     uint4 kq = make_uint4(0, 0, 0, 0), vq = make_uint4(0, 0, 0, 0);
@@ -148,95 +157,91 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
       vq = *reinterpret_cast<const uint4*>(v + (rowbase + s) * ldv + h * AT_D + c * 8);
     }
     *reinterpret_cast<uint4*>(Ks + s * AT_D + ((c ^ ((s >> 1) & 7)) << 3)) = kq;
-    const uint32_t w[4] = {vq.x, vq.y, vq.z, vq.w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      Vt[(c * 8 + 2 * t) * VP + s] = static_cast<uint16_t>(w[t] & 0xFFFF);
-      Vt[(c * 8 + 2 * t + 1) * VP + s] = static_cast<uint16_t>(w[t] >> 16);
-    }
+    *reinterpret_cast<uint4*>(Vs + s * VP + c * 8) = vq;
   }
   __syncthreads();
-
-  const int q0 = blockIdx.x * 64 + wave * 16;
-  if (q0 >= S) return;  // whole wave past the end (after the only block barrier)
-  // Q fragments (A operand): lane -> row q0 + (lane & 15), k-chunk (lane >> 4) + 4*kk
-  bf16x8 qf[2];
+  const int q0 = (blockIdx.x * 4 + wave) * 32;
+  if (q0 >= S) return;  // whole wave (EXEC stays full for the transposed reads)
+  const int r = lane & 31, hh = lane >> 5;
+  bf16x8 qf[4];
   {
-    const int qr = q0 + (lane & 15);
+    const int qr = q0 + r;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int ks = 0; ks < 4; ++ks) {
       uint4 t = make_uint4(0, 0, 0, 0);
-      if (qr < S) t = *reinterpret_cast<const uint4*>(q + (rowbase + qr) * ldq + h * AT_D + ((lane >> 4) + 4 * kk) * 8);
-      qf[kk] = __builtin_bit_cast(bf16x8, t);
+      if (qr < S) t = *reinterpret_cast<const uint4*>(q + (rowbase + qr) * ldq + h * AT_D + ks * 16 + hh * 8);
+      qf[ks] = __builtin_bit_cast(bf16x8, t);
     }
   }
-  f32x4 sc[NT];
+  f32x16 o0, o1;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int key = t * 16 + (lane & 15);
+  for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  // transposed-read addressing: lane 4q'+p of each 16-lane group supplies row q', columns 4p..4p+3
+  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  for (int kt = 0; kt < NKT; ++kt) {
+    f32x16 sc;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = (lane >> 4) + 4 * kk;
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * AT_D + ((c ^ ((key >> 1) & 7)) << 3));
-      sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[kk], kf, sc[t], 0, 0, 0);
+    for (int i = 0; i < 16; ++i) sc[i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int key = kt * 32 + r, chunk = 2 * ks + hh;
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * AT_D + ((chunk ^ ((key >> 1) & 7)) << 3));
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc, 0, 0, 0);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      const float x = key < S ? sc[i] * scale_log2 : -INFINITY;
+      sc[i] = x;
+      mt = fmaxf(mt, x);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o0[i] *= alpha;
+      o1[i] *= alpha;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = exp2f(sc[i] - mn);
+      sc[i] = p;
+      l += p;
+    }
+    m = mn;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = static_cast<__bf16>(sc[8 * st + j]);
+      const uint16_t* vrow = Vs + (kt * 32 + 16 * st + 4 * hh + qq) * VP + 16 * g + 4 * pp;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const s16x4 lo = ds_read_tr16(vrow + dt * 32);
+        const s16x4 hi = ds_read_tr16(vrow + 8 * VP + dt * 32);
+        const s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 af = __builtin_bit_cast(bf16x8, a8);
+        if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o0, 0, 0, 0);
+        else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o1, 0, 0, 0);
+      }
     }
   }
-  // softmax over keys for the 4 rows this lane holds (rows 4*(lane>>4)+r, key column lane&15)
-  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  l += __shfl_xor(l, 32, 64);
+  const int qr = q0 + r;
+  if (qr >= S) return;
+  const float inv = 1.f / l;
+  uint16_t* orow = out + (rowbase + qr) * ldo + h * AT_D;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const bool valid = t * 16 + (lane & 15) < S;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float x = valid ? sc[t][r] * scale : -INFINITY;
-      sc[t][r] = x;
-      mx[r] = fmaxf(mx[r], x);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o, 64));
-  float sm[4] = {0.f, 0.f, 0.f, 0.f};
-  uint16_t* Pw = P + wave * 16 * VP;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float e = __expf(sc[t][r] - mx[r]);
-      sm[r] += e;
-      Pw[(4 * (lane >> 4) + r) * VP + t * 16 + (lane & 15)] = f2bf(e);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) sm[r] += __shfl_xor(sm[r], o, 64);
-  // zero P columns [NT*16, SK) never exist (SK multiple of 16); P rows are written by this wave only
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes land before the reads below
-  // O = P V : A = P [16 q x 32 keys], B = V [32 keys x 16 d]
-  f32x4 o[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(Pw + (lane & 15) * VP + ks * 32 + (lane >> 4) * 8);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vt + (n * 16 + (lane & 15)) * VP + ks * 32 + (lane >> 4) * 8);
-      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[n], 0, 0, 0);
-    }
-  }
-  // normalise and store: lane holds rows 4*(lane>>4)+r, columns n*16 + (lane&15)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qr = q0 + 4 * (lane >> 4) + r;
-    if (qr >= S) continue;
-    const float inv = 1.f / sm[r];
-    uint16_t* orow = out + (rowbase + qr) * ldo + h * AT_D;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) orow[n * 16 + (lane & 15)] = f2bf(o[n][r] * inv);
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d = 8 * g4 + 4 * hh;
+    *reinterpret_cast<uint2*>(orow + d) =
+        make_uint2(pack2(o0[4 * g4] * inv, o0[4 * g4 + 1] * inv), pack2(o0[4 * g4 + 2] * inv, o0[4 * g4 + 3] * inv));
+    *reinterpret_cast<uint2*>(orow + 32 + d) =
+        make_uint2(pack2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
   }
 }
 
@@ -276,12 +281,14 @@ hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, in
 
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s) {
-  if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8) return hipErrorInvalidValue;
-  dim3 grid((S + 63) / 64, H, B);
-  if (S <= 64) hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, scale);
-  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<128>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, scale);
-  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<224>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, scale);
-  else hipLaunchKernelGGL(attention_kernel<256>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, scale);
+  if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
+  const int qtiles = (S + 31) / 32;
+  dim3 grid((qtiles + 3) / 4, H, B);
+  const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
+  if (S <= 64) hipLaunchKernelGGL(attention_kernel<2>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<7>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else hipLaunchKernelGGL(attention_kernel<8>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
   return hipGetLastError();
 }
 

@@ -54,7 +54,7 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128):
 
 
 def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
-                scale2=None, shift2=None, relu2=False, tile=-1, splits=1):
+                scale2=None, shift2=None, relu2=False, tile=-1, splits=1, fused_splitk=True):
     """Implicit-GEMM conv.  x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float.
     Returns (out, out2) in NHWC ([B,Ho,Wo,Cout]); out is f32 if out_f32 else bf16."""
     import torch
@@ -85,6 +85,10 @@ def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=No
     if splits > 1:
         ws = torch.empty(splits * B * Ho * Wo * cout, dtype=torch.float32, device=dev)
         geom["ws"] = int(ws.data_ptr())
+        if fused_splitk:  # last split block reduces in-kernel (counters must start at zero)
+            counters = torch.zeros(65536, dtype=torch.int32, device=dev)
+            geom["counters"] = int(counters.data_ptr())
+            geom["counters_n"] = 65536
     L = native.kernels()
     rc = L.die_kern_conv(json.dumps(geom).encode(), _ptr(x_nhwc.contiguous()), _ptr(wp), _ptr(bias_p),
                          _ptr(res.contiguous() if res is not None else None), 0 if out_f32 else _ptr(out),

@@ -56,8 +56,10 @@ def test_conv_matches_torch(native, shape):
     assert rel_err(got, ref) < 2e-3, rel_err(got, ref)
 
 
-@pytest.mark.parametrize("tile,splits", [(0, 1), (1, 1), (2, 1), (3, 1), (0, 3), (3, 4), (1, 9)])
-def test_conv_all_tiles_and_epilogue(native, tile, splits):
+@pytest.mark.parametrize("tile,splits,fused", [(0, 1, True), (1, 1, True), (2, 1, True), (3, 1, True), (0, 3, True),
+                                               (3, 4, True), (1, 9, True), (7, 4, True), (11, 3, True),
+                                               (0, 3, False), (7, 4, False)])
+def test_conv_all_tiles_and_epilogue(native, tile, splits, fused):
     torch = _t()
     from die_amd.ops import kernels as K
 
@@ -70,13 +72,20 @@ def test_conv_all_tiles_and_epilogue(native, tile, splits):
     s2 = torch.rand(Cout, device="cuda", generator=g) + 0.5
     b2 = torch.randn(Cout, device="cuda", generator=g)
     out, out2 = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), w.float(), bias=bias, stride=1, pad=1, relu=True,
-                              res=res, scale2=s2, shift2=b2, relu2=True, tile=tile, splits=splits)
+                              res=res, scale2=s2, shift2=b2, relu2=True, tile=tile, splits=splits,
+                              fused_splitk=fused)
     torch.cuda.synchronize()
+    assert out is not None, "config not applicable"
     v = torch.nn.functional.conv2d(x.float(), w.float(), bias, padding=1).permute(0, 2, 3, 1) + res.float()
     v = torch.relu(v)
     u = torch.relu(v * s2 + b2)
     assert rel_err(out, v) < 5e-3
     assert rel_err(out2, u) < 5e-3
+    if splits > 1:  # fused reduction is deterministic and leaves the counters reset (bitwise repeat)
+        again, _ = K.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous(), w.float(), bias=bias, stride=1, pad=1, relu=True,
+                                 res=res, scale2=s2, shift2=b2, relu2=True, tile=tile, splits=splits,
+                                 fused_splitk=fused)
+        assert torch.equal(again, out)
 
 
 @pytest.mark.parametrize("shape", [

@@ -41,7 +41,7 @@ def main():
                  p["total_us"], p["tflops"], p["batch"] / p["total_us"] * 1e6), "",
              "| # | op | kind | us | GFLOP | TFLOP/s | tile/splits |", "|---:|---|---|---:|---:|---:|---|"]
     for i, o in enumerate(p["ops"]):
-        ts = "%d/%d" % (o["tile"], o["splits"]) if "tile" in o else ""
+        ts = ("%d/%d" % (o["tile"], o["splits"]) + ("f" if o.get("fused_splitk") else "")) if "tile" in o else ""
         lines.append("| %d | %s | %s | %.1f | %.2f | %.0f | %s |" % (i, o["name"][:48], o["kind"], o["us"], o["gflop"],
                                                                     o["tflops"], ts))
     kinds = {}
