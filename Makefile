@@ -53,5 +53,18 @@ $(BINDIR)/worker_node: $(SRC)/apps/worker_main.cpp $(LIBDIR)/libdie.so
 clean:
 	rm -rf $(BUILD) $(LIBDIR) $(BINDIR)
 
-.PHONY: all clean
+# Host-runtime concurrency stress under sanitizers; no GPU code is linked.
+STRESS_SRCS := core/json.cpp core/http.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
+               serve/gateway.cpp tests/stress_main.cpp
+SANFLAGS := -std=c++17 -O1 -g -march=x86-64-v3 -fno-omit-frame-pointer -Wall -Wno-unused-parameter
+stress-tsan: $(BINDIR)/die_stress_tsan
+stress-asan: $(BINDIR)/die_stress_asan
+$(BINDIR)/die_stress_tsan: $(addprefix $(SRC)/,$(STRESS_SRCS)) $(wildcard $(SRC)/*/*.h)
+	@mkdir -p $(BINDIR)
+	$(CXX) $(SANFLAGS) -fsanitize=thread $(addprefix $(SRC)/,$(STRESS_SRCS)) -o $@ -lpthread
+$(BINDIR)/die_stress_asan: $(addprefix $(SRC)/,$(STRESS_SRCS)) $(wildcard $(SRC)/*/*.h)
+	@mkdir -p $(BINDIR)
+	$(CXX) $(SANFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined $(addprefix $(SRC)/,$(STRESS_SRCS)) -o $@ -lpthread
+
+.PHONY: all clean stress-tsan stress-asan
 -include $(HOST_OBJS:.o=.d)
