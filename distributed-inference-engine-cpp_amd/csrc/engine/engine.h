@@ -141,6 +141,9 @@ struct EngineOptions {
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
   bool device_decode = true;     // accept input_data text and convert it on the GPU (HIP)
+  // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
+  // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
+  std::string tune_cache = "auto";
   std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
   int cpu_threads = 0;
   int shard_id = 0;

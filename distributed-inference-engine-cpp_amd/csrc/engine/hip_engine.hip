@@ -14,7 +14,12 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <unistd.h>
+
 #include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
 #include <cstring>
 #include <deque>
 #include <iostream>
@@ -333,6 +338,7 @@ class HipEngine : public Engine {
     j["text_capacity"] = static_cast<long long>(text_cap_);
     j["autotuned"] = !tune_.empty();
     j["tuned_conv_us_at_max_batch"] = tuned_conv_us_;
+    j["tune_cache_entries_loaded"] = tune_cache_hits_;
     if (!tune_.empty()) {
       Json t = Json::array();
       for (size_t oi = 0; oi < plan_.ops.size(); ++oi)
@@ -350,6 +356,71 @@ class HipEngine : public Engine {
     int splits = 1;
     bool fused = false;  // split-K reduced in-kernel by the last split block (else a second kernel)
   };
+
+  // ---- autotune persistence (kernel configs cached in a tuning file) ----
+  std::string tune_cache_path() const {
+    std::string p = opt_.tune_cache;
+    if (p == "auto") {
+      if (const char* e = std::getenv("DIE_TUNE_CACHE")) p = e;
+      else if (const char* h = std::getenv("HOME")) p = std::string(h) + "/.cache/die_amd/tune.json";
+      else p.clear();
+    }
+    return p;
+  }
+  size_t load_tune_cache(const std::string& path, std::map<std::string, std::pair<Tune, double>>& out) const {
+    if (path.empty()) return 0;
+    std::ifstream f(path);
+    if (!f) return 0;
+    try {
+      std::stringstream ss;
+      ss << f.rdbuf();
+      const Json j = Json::parse(ss.str());
+      const Json* arch = j.find(arch_);
+      if (!arch) return 0;
+      for (const auto& kv : arch->as_object()) {
+        const auto& a = kv.second.as_array();
+        if (a.size() < 4) continue;
+        out[kv.first] = {Tune{static_cast<int>(a[0].as_int()), static_cast<int>(a[1].as_int()), a[2].as_bool()},
+                         a[3].as_double()};
+      }
+    } catch (const std::exception&) {
+      return 0;  // unreadable cache: retune
+    }
+    return out.size();
+  }
+  void save_tune_cache(const std::string& path, const std::map<std::string, std::pair<Tune, double>>& shapes) const {
+    if (path.empty()) return;
+    try {
+      Json root = Json::object();
+      {
+        std::ifstream f(path);
+        if (f) {
+          std::stringstream ss;
+          ss << f.rdbuf();
+          root = Json::parse(ss.str());
+        }
+      }
+      Json arch = root.find(arch_) ? *root.find(arch_) : Json::object();
+      for (const auto& kv : shapes) {
+        Json a = Json::array();
+        a.push_back(kv.second.first.tile);
+        a.push_back(kv.second.first.splits);
+        a.push_back(kv.second.first.fused);
+        a.push_back(kv.second.second);
+        arch[kv.first] = a;
+      }
+      root[arch_] = arch;
+      const auto slash = path.rfind('/');
+      if (slash != std::string::npos) std::system(("mkdir -p '" + path.substr(0, slash) + "'").c_str());
+      const std::string tmp = path + ".tmp" + std::to_string(getpid());
+      {
+        std::ofstream o(tmp);
+        o << root.dump();
+      }
+      std::rename(tmp.c_str(), path.c_str());
+    } catch (const std::exception&) {
+    }
+  }
 
   void* buf_ptr(int id, int s) {
     Slot& sl = slots_[s];
@@ -407,6 +478,8 @@ class HipEngine : public Engine {
     tune_.assign(buckets_.size(), std::vector<Tune>(plan_.ops.size(), Tune{-1, 1}));
     double total_best_us = 0;
     std::map<std::string, std::pair<Tune, double>> tuned_shapes;
+    const std::string cache_path = tune_cache_path();
+    const size_t loaded = load_tune_cache(cache_path, tuned_shapes);
     for (size_t bi = 0; bi < buckets_.size(); ++bi) {
       const int B = buckets_[bi];
       encode_forward(B, 0, s_compute_);
@@ -457,6 +530,8 @@ class HipEngine : public Engine {
       }
     }
     tuned_conv_us_ = total_best_us;
+    tune_cache_hits_ = static_cast<long long>(loaded);
+    if (tuned_shapes.size() > loaded) save_tune_cache(cache_path, tuned_shapes);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
   }
@@ -687,6 +762,7 @@ class HipEngine : public Engine {
   Plan plan_;
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
+  long long tune_cache_hits_ = 0;
   static constexpr int kCounters = 1 << 16;
   int* counters_ = nullptr;
   Communicator* comm_ = nullptr;  // data parallel (not owned)

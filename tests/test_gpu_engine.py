@@ -75,3 +75,28 @@ def test_worker_on_gpu_http(native, models):
         assert out2["output_data"] == out["output_data"]
     finally:
         wk.stop()
+
+
+def test_tune_cache_roundtrip(native, models, tmp_path):
+    """Autotune results persist in the tuning file and are reused by the next engine."""
+    import time
+
+    path, w, cfg = models["tiny"]
+    cache = str(tmp_path / "tune.json")
+    t0 = time.time()
+    e1 = native.Engine(path, device="hip", max_batch=8, tune_cache=cache)
+    t1 = time.time()
+    info1 = e1.refresh_info()
+    e1.close()
+    assert info1["tune_cache_entries_loaded"] == 0
+    data = json.load(open(cache))
+    assert any(k.startswith("gfx950") for k in data) and sum(len(v) for v in data.values()) > 0
+    e2 = native.Engine(path, device="hip", max_batch=8, tune_cache=cache)
+    t2 = time.time()
+    info2 = e2.refresh_info()
+    assert info2["tune_cache_entries_loaded"] > 0
+    assert info2["tile_split_at_max_batch"] == info1["tile_split_at_max_batch"]
+    x = np.random.default_rng(0).random((3, 3 * 64 * 64), dtype=np.float32)
+    assert np.isfinite(e2.run(x)).all()
+    e2.close()
+    print("engine init with tuning %.2fs, from cache %.2fs" % (t1 - t0, time.time() - t2 + (t2 - t1)))
