@@ -14,7 +14,7 @@ CXXFLAGS := -std=c++17 -O3 -march=x86-64-v3 -fPIC -fopenmp -g -Wall -Wextra -Wno
             -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 HIPFLAGS := -std=c++17 -O3 --offload-arch=$(ARCH) -fPIC -g -Wall -Wno-unused-parameter -Wno-unused-result \
             -munsafe-fp-atomics
-LDLIBS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread
+LDLIBS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lgomp -lpthread
 
 HOST_SRCS := core/json.cpp core/http.cpp parallel/dp_group.cpp parallel/comm.cpp engine/dp_engine.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
              serve/worker.cpp serve/gateway.cpp serve/loadgen.cpp onnx/onnx_model.cpp \

@@ -31,6 +31,7 @@
 #include "../kernels/kernels.h"
 #include "engine.h"
 #include "hip_plan.h"
+#include "../core/trace.h"
 #include "../parallel/comm.h"
 
 namespace die {
@@ -243,6 +244,7 @@ class HipEngine : public Engine {
       slot = next_slot_;
       next_slot_ = (next_slot_ + 1) % depth_;
     }
+    TraceRange tr_submit("engine.submit(h2d+graph)");
     Job job;
     job.slot = slot;
     job.B = B;
@@ -710,6 +712,7 @@ class HipEngine : public Engine {
         jobs_.pop_front();
       }
       Slot& sl = slots_[job.slot];
+      TraceRange tr_done("engine.completion(d2h wait+callback)");
       BatchResult r;
       if (job.error.empty()) {
         hipError_t e = hipEventSynchronize(sl.ev_d2h);

@@ -1,5 +1,7 @@
 #include "worker.h"
 
+#include "../core/trace.h"
+
 #include <algorithm>
 #include <cstring>
 #include <iostream>
@@ -75,6 +77,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       items.push_back(it);
     }
     const size_t B = reqs.size();
+    TraceRange tr_dispatch("worker.batch_dispatch");
     const auto t_dispatch = std::chrono::steady_clock::now();
     eng->submit(std::move(items), [B, finish, t_dispatch](BatchResult& br) {
       const auto t_done = std::chrono::steady_clock::now();
@@ -169,6 +172,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   const size_t text_cap = std::min(eng.text_capacity(), sink.buf.capacity * sizeof(float));
   sink.defer = text_cap > 0;
   int seen = 0;
+  TraceRange tr_parse("worker.parse");
   const auto t_parse = std::chrono::steady_clock::now();
   const auto t_start = t_parse;
   if (req.t_headers.time_since_epoch().count()) h_recv_.add(t_start - req.t_headers);
@@ -284,6 +288,7 @@ void WorkerNode::dispatch(Pending p, Responder res) {
     std::string node = opt_.node_id;
     const auto t_done = r->t_done;
     res.defer([this, out, id = std::move(id), node = std::move(node), us, t_start, t_done] {
+      TraceRange tr_resp("worker.respond");
       HttpResponse resp;
       resp.body = build_response(id, out->data(), out->size(), node, false, us);
       const auto now = std::chrono::steady_clock::now();
