@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--stage-slots", type=int, default=-1,
+                    help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
     ap.add_argument("--no-device-decode", action="store_true",
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
     args = ap.parse_args()
@@ -94,10 +96,12 @@ def main():
     extra = {}
 
     if args.mode == "http":
+        t_init = time.perf_counter()
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
                            engine={"device": "hip", "device_id": local_rank, "max_batch": B,
-                                   "pipeline_depth": args.pipeline_depth,
+                                   "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                                    "device_decode": not args.no_device_decode})
+        t_ready = time.perf_counter()
         lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
         native.loadgen(requests=args.warmup * B, warmup=0, id_prefix="warm%d_" % rank, **lg)
@@ -122,6 +126,9 @@ def main():
             "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
             "cpu_quota": _cpu_quota(), "device_decode": e1.get("device_decode"),
             "decode_fallbacks": h1.get("decode_fallbacks"),
+            "staged_uploads": e1.get("staged_uploads", 0) - e0.get("staged_uploads", 0),
+            "pipeline_depth": args.pipeline_depth, "worker_init_s": round(t_ready - t_init, 2),
+            "staging_diag": e1.get("staging_diag"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
         wk.stop()

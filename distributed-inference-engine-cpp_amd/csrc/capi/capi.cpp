@@ -71,6 +71,7 @@ EngineOptions engine_opts(const Json& j) {
   e.use_graphs = jget<bool>(j, "use_graphs", e.use_graphs);
   e.autotune = jget<bool>(j, "autotune", e.autotune);
   e.device_decode = jget<bool>(j, "device_decode", e.device_decode);
+  e.stage_slots = jget<int>(j, "stage_slots", e.stage_slots);
   e.tune_cache = jget<std::string>(j, "tune_cache", e.tune_cache);
   e.precision = jget<std::string>(j, "precision", e.precision);
   e.shard_id = jget<int>(j, "shard_id", e.shard_id);

@@ -130,11 +130,12 @@ long long die_decode_scratch_bytes(int max_batch, long long text_cap) {
   return static_cast<long long>(kern::decode_scratch_bytes(max_batch, static_cast<size_t>(text_cap)));
 }
 
-int die_kern_decode(uint64_t text, long long text_cap, uint64_t lens, int B, uint64_t out, long long numel,
-                    uint64_t status, uint64_t ntok, uint64_t scratch, uint64_t stream) {
-  return static_cast<int>(kern::decode_json_numbers(P<const unsigned char>(text), static_cast<size_t>(text_cap),
-                                                    P<const long long>(lens), B, P<float>(out), numel, P<int>(status),
-                                                    P<int>(ntok), P<void>(scratch), S(stream)));
+int die_kern_decode(uint64_t text, uint64_t offs, long long text_cap, uint64_t lens, int B, uint64_t out,
+                    long long numel, uint64_t status, uint64_t ntok, uint64_t scratch, uint64_t stream) {
+  return static_cast<int>(kern::decode_json_numbers(P<const unsigned char>(text), P<const long long>(offs),
+                                                    static_cast<size_t>(text_cap), P<const long long>(lens), B,
+                                                    P<float>(out), numel, P<int>(status), P<int>(ntok), P<void>(scratch),
+                                                    S(stream)));
 }
 
 int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, int H, int W, int Ho, int Wo, int relu,

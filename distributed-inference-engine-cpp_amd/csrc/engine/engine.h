@@ -57,6 +57,8 @@ struct BatchItem {
   // (between '[' and ']') in engine-pinned memory; the engine converts it on the device.
   const char* text = nullptr;
   size_t text_len = 0;
+  // Ticket from Engine::stage_text() when the text was already uploaded early (-1 = not staged).
+  long staged = -1;
 };
 
 struct BatchResult {
@@ -107,6 +109,22 @@ class Engine {
   virtual SamplePool& sample_pool() = 0;
   // Bytes of input_data text a SampleBuffer can carry for device decode (0 = not supported).
   virtual size_t text_capacity() const { return 0; }
+  // Early upload for device decode: start copying one request's input text (engine-pinned, from
+  // sample_pool()) into device staging now, on a copy stream, so the batch that later carries it
+  // does not wait for its H2D.  Returns a ticket for BatchItem::staged, or -1 when the engine does
+  // not stage (or staging is full: submit() then copies as usual).  The caller owns the ticket and
+  // hands it back with release_staged() after the batch that carried it completed (ran = true: the
+  // copy is known to be done), or with ran = false when the request failed or was dropped before
+  // its batch ran (the engine then waits for the copy); the pinned text must not change until then.
+  virtual long stage_text(const char* text, size_t len) {
+    (void)text;
+    (void)len;
+    return -1;
+  }
+  virtual void release_staged(long ticket, bool ran) {
+    (void)ticket;
+    (void)ran;
+  }
   // Make host memory DMA-able for this engine (HIP: hipHostRegister); no-op elsewhere.
   virtual void register_host_memory(void* p, size_t bytes) {
     (void)p;
@@ -141,6 +159,7 @@ struct EngineOptions {
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
   bool device_decode = true;     // accept input_data text and convert it on the GPU (HIP)
+  int stage_slots = -1;          // early-upload text slots in device memory (-1 = auto, 0 = off)
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

@@ -67,8 +67,13 @@ class HipEngine : public Engine {
     HIP_CHECK(hipMalloc(&params_, std::max<size_t>(plan_.params.size(), 256)));
     HIP_CHECK(hipMalloc(&arena_, std::max<size_t>(plan_.arena_bytes, 256)));
     HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+    // Streams = hardware queues: the compute stream (graphs + the small result D2H) and
+    // kStageStreams copy streams (early uploads, submit-time copies).  HIP gives a process
+    // GPU_MAX_HW_QUEUES (4) queues; more streams than that share queues (serialising copies behind
+    // kernels), and raising the limit lets the queue scheduler time-slice the compute queue (measured:
+    // forwards 1.8x longer), so the engine stays within three.
+    if (const char* e = std::getenv("DIE_COPY_STREAMS")) n_copy_streams_ = std::max(1, std::min(kStageStreams, std::atoi(e)));
+    for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
     if (!comm_ || comm_->rank() == 0)
       HIP_CHECK(hipMemcpy(params_, plan_.params.data(), plan_.params.size(), hipMemcpyHostToDevice));
     if (comm_) {  // data parallel: every rank gets the packed weights from rank 0 over xGMI
@@ -76,14 +81,29 @@ class HipEngine : public Engine {
       HIP_CHECK(hipStreamSynchronize(s_compute_));
     }
     if (opt.device_decode) text_cap_ = (in_numel_ * 24 + 4095) / 4096 * 4096;  // up to 23 chars + separator per value
+    if (text_cap_) {
+      // One device text arena: n_stage_ early-upload slots (stage_text) followed by max_batch
+      // fallback slots per pipeline slot (texts copied at submit).  Decode finds sample i at
+      // offs[i].  Data-parallel ranks get their shards through the DP arena instead.
+      n_stage_ = opt.stage_slots >= 0 ? opt.stage_slots : std::min(1024, std::max(256, 8 * max_batch_));
+      if (comm_) n_stage_ = 0;
+      HIP_CHECK(hipMalloc(&d_text_, text_cap_ * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
+      stage_ev_.resize(n_stage_);
+      stage_seq_.assign(n_stage_, 0);
+      stage_stream_.assign(n_stage_, 0);
+      stage_state_.assign(n_stage_, kIssued);
+      for (int t = 0; t < n_stage_; ++t) {
+        HIP_CHECK(hipEventCreateWithFlags(&stage_ev_[t], hipEventDisableTiming));
+        stage_free_.push_back(n_stage_ - 1 - t);
+      }
+    }
     slots_.resize(depth_);
     for (auto& sl : slots_) {
-      if (text_cap_) {
-        HIP_CHECK(hipMalloc(&sl.d_text, text_cap_ * max_batch_));
-        HIP_CHECK(hipMalloc(&sl.d_scratch, kern::decode_scratch_bytes(max_batch_, text_cap_)));
-      }
-      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * max_batch_));
+      if (text_cap_) HIP_CHECK(hipMalloc(&sl.d_scratch, kern::decode_scratch_bytes(max_batch_, text_cap_)));
+      // [lens x max_batch][text offsets x max_batch]
+      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * 2 * max_batch_));
       HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
+      HIP_CHECK(hipMemset(sl.d_lens + max_batch_, 0, sizeof(long long) * max_batch_));
       HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * 2 * max_batch_));
       HIP_CHECK(hipMemset(sl.d_status, 0, sizeof(int) * 2 * max_batch_));
       if (comm_) {
@@ -95,19 +115,31 @@ class HipEngine : public Engine {
                                 hipHostMallocDefault));
         HIP_CHECK(hipEventCreateWithFlags(&sl.ev_gather, hipEventDisableTiming));
       }
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * max_batch_, hipHostMallocDefault));
+      // host-coherent: the graph's first kernel reads it directly (see encode_forward)
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * 2 * max_batch_,
+                              hipHostMallocCoherent | hipHostMallocMapped));
+      HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.h_lens_dev), sl.h_lens, 0));
+      for (int i = 0; i < max_batch_; ++i) {  // no text samples until a submit says otherwise
+        sl.h_lens[i] = -1;
+        sl.h_lens[max_batch_ + i] = 0;
+      }
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_status), sizeof(int) * 2 * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipMalloc(&sl.d_in, sizeof(float) * in_numel_ * max_batch_));
       HIP_CHECK(hipMalloc(&sl.d_out, sizeof(float) * out_numel_ * max_batch_));
       HIP_CHECK(hipMemset(sl.d_in, 0, sizeof(float) * in_numel_ * max_batch_));
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_out), sizeof(float) * out_numel_ * max_batch_,
                               hipHostMallocDefault));
-      HIP_CHECK(hipEventCreateWithFlags(&sl.ev_h2d, hipEventDisableTiming));
+      for (auto& ev : sl.ev_h2d) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       HIP_CHECK(hipEventCreate(&sl.ev_fwd0));
       HIP_CHECK(hipEventCreate(&sl.ev_fwd1));
       HIP_CHECK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
     }
-    for (int b = 1; b < max_batch_; b *= 2) buckets_.push_back(b);
+    // Batch buckets ~sqrt(2) apart (1, 2, 4, 6, 8, 12, 16, 24, 32, ...): a batch runs the graph of
+    // the smallest bucket >= B, so padding waste stays under a third.
+    for (int b = 1; b < max_batch_; b *= 2) {
+      buckets_.push_back(b);
+      if (b >= 4 && b + b / 2 < max_batch_) buckets_.push_back(b + b / 2);
+    }
     buckets_.push_back(max_batch_);
 
     pool_ = std::make_unique<SamplePool>(
@@ -148,6 +180,7 @@ class HipEngine : public Engine {
       HIP_CHECK(hipStreamSynchronize(s_compute_));
     }
     completion_ = std::thread([this] { completion_loop(); });
+    if (n_stage_) stager_ = std::thread([this] { stager_loop(); });
   }
 
   ~HipEngine() override {
@@ -157,14 +190,23 @@ class HipEngine : public Engine {
     }
     cv_.notify_all();
     if (completion_.joinable()) completion_.join();
+    {
+      std::lock_guard<std::mutex> g(stage_mu_);
+      stage_stop_ = true;  // the stager drains its queue first (queued tickets still get issued)
+    }
+    stage_cv_.notify_all();
+    if (stager_.joinable()) stager_.join();
     (void)hipSetDevice(dev_);
     (void)hipDeviceSynchronize();
     for (auto ge : graphs_)
       if (ge) (void)hipGraphExecDestroy(ge);
+    for (auto ev : stage_ev_) (void)hipEventDestroy(ev);
+    for (auto st : s_stage_)
+      if (st) (void)hipStreamDestroy(st);
+    (void)hipFree(d_text_);
     for (auto& sl : slots_) {
       (void)hipFree(sl.d_in);
       (void)hipFree(sl.d_out);
-      (void)hipFree(sl.d_text);
       (void)hipFree(sl.d_scratch);
       (void)hipFree(sl.d_lens);
       (void)hipFree(sl.d_status);
@@ -178,7 +220,7 @@ class HipEngine : public Engine {
         (void)hipEventDestroy(sl.ev_gather);
       }
       (void)hipHostFree(sl.h_out);
-      (void)hipEventDestroy(sl.ev_h2d);
+      for (auto ev : sl.ev_h2d) (void)hipEventDestroy(ev);
       (void)hipEventDestroy(sl.ev_fwd0);
       (void)hipEventDestroy(sl.ev_fwd1);
       (void)hipEventDestroy(sl.ev_d2h);
@@ -191,8 +233,6 @@ class HipEngine : public Engine {
     (void)hipFree(zeros_);
     (void)hipFree(counters_);
     (void)hipStreamDestroy(s_compute_);
-    (void)hipStreamDestroy(s_h2d_);
-    (void)hipStreamDestroy(s_d2h_);
   }
 
   std::string name() const override { return "hip:" + arch_ + ":" + std::to_string(dev_); }
@@ -207,6 +247,37 @@ class HipEngine : public Engine {
     HIP_CHECK(hipSetDevice(dev_));
     HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterDefault));
     registered_.push_back(p);
+  }
+
+  // Early upload: reactor threads only queue the request; ONE stager thread issues every staged
+  // copy (no HIP API traffic from the HTTP threads competing with the batcher's graph launches and
+  // the completion thread's waits -- measured: issuing from 16 reactors cost ~15% throughput).
+  long stage_text(const char* text, size_t len) override {
+    if (!text_cap_ || n_stage_ == 0 || len == 0 || len > text_cap_) return -1;
+    int t;
+    {
+      std::lock_guard<std::mutex> g(stage_mu_);
+      if (stage_free_.empty() || stage_stop_) return -1;
+      t = stage_free_.back();
+      stage_free_.pop_back();
+      stage_state_[t] = kQueued;
+      stage_q_.push_back(StageReq{t, text, len});
+    }
+    stage_cv_.notify_one();
+    staged_total_.fetch_add(1, std::memory_order_relaxed);
+    return t;
+  }
+
+  void release_staged(long t, bool ran) override {
+    if (t < 0 || t >= n_stage_) return;
+    if (!ran) {  // the pinned source may be reused after this: wait for an unconsumed copy
+      if (wait_staged(static_cast<int>(t)) == kIssued) {
+        (void)hipSetDevice(dev_);
+        (void)hipEventSynchronize(stage_ev_[t]);
+      }
+    }
+    std::lock_guard<std::mutex> g(stage_mu_);
+    stage_free_.push_back(static_cast<int>(t));
   }
 
   void wait_for_slot() override {
@@ -254,11 +325,34 @@ class HipEngine : public Engine {
       HIP_CHECK(hipSetDevice(dev_));
       Slot& sl = slots_[slot];
       bool any_text = false;
+      long long* h_offs = sl.h_lens + max_batch_;
+      int wait_ticket[kStageStreams];  // per copy stream, the staged copy issued last covers the earlier ones
+      bool copied[kStageStreams] = {};  // submit-time copies issued on that stream
+      for (auto& w : wait_ticket) w = -1;
+      int rr = 0;
       for (int i = 0; i < B; ++i) {
+        h_offs[i] = 0;
         if (items[i].text) {
           if (!text_cap_ || items[i].text_len > text_cap_) throw std::runtime_error("input text exceeds device decode capacity");
-          HIP_CHECK(hipMemcpyAsync(sl.d_text + static_cast<size_t>(i) * text_cap_, items[i].text, items[i].text_len,
-                                   hipMemcpyHostToDevice, s_h2d_));
+          const long t = items[i].staged;
+          const auto tw0 = std::chrono::steady_clock::now();
+          const bool issued = t >= 0 && t < n_stage_ && wait_staged(static_cast<int>(t)) == kIssued;
+          if (t >= 0) {
+            diag_submit_wait_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0).count();
+            if (issued && hipEventQuery(stage_ev_[t]) != hipSuccess) diag_not_ready_++;
+          }
+          if (issued) {
+            h_offs[i] = static_cast<long long>(t) * static_cast<long long>(text_cap_);
+            int& w = wait_ticket[stage_stream_[t]];
+            if (w < 0 || stage_seq_[t] > stage_seq_[w]) w = static_cast<int>(t);
+          } else {
+            const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
+            h_offs[i] = static_cast<long long>(idx * text_cap_);
+            const int si = rr++ % n_copy_streams_;
+            HIP_CHECK(hipMemcpyAsync(d_text_ + idx * text_cap_, items[i].text, items[i].text_len, hipMemcpyHostToDevice,
+                                     s_stage_[si]));
+            copied[si] = true;
+          }
           sl.h_lens[i] = static_cast<long long>(items[i].text_len);
           any_text = true;
           continue;
@@ -266,14 +360,30 @@ class HipEngine : public Engine {
         sl.h_lens[i] = -1;
         const size_t n = std::min(items[i].len, in_numel_);
         float* dst = sl.d_in + static_cast<size_t>(i) * in_numel_;
-        if (n) HIP_CHECK(hipMemcpyAsync(dst, items[i].input, n * sizeof(float), hipMemcpyHostToDevice, s_h2d_));
-        if (n < in_numel_) HIP_CHECK(hipMemsetAsync(dst + n, 0, (in_numel_ - n) * sizeof(float), s_h2d_));
+        const int si = rr++ % n_copy_streams_;
+        if (n) HIP_CHECK(hipMemcpyAsync(dst, items[i].input, n * sizeof(float), hipMemcpyHostToDevice, s_stage_[si]));
+        if (n < in_numel_) HIP_CHECK(hipMemsetAsync(dst + n, 0, (in_numel_ - n) * sizeof(float), s_stage_[si]));
+        copied[si] = true;
       }
-      for (int i = B; i < max_batch_; ++i) sl.h_lens[i] = -1;
-      if (text_cap_) HIP_CHECK(hipMemcpyAsync(sl.d_lens, sl.h_lens, sizeof(long long) * max_batch_, hipMemcpyHostToDevice, s_h2d_));
+      for (int i = B; i < max_batch_; ++i) {
+        sl.h_lens[i] = -1;
+        h_offs[i] = 0;
+      }
+      // lens/offsets reach the device through the graph's first kernel (host-coherent read), so
+      // nothing of this batch queues behind the copy engines except its own fallback copies
+      bool used_staged = false;
+      for (int w : wait_ticket)
+        if (w >= 0) {
+          HIP_CHECK(hipStreamWaitEvent(s_compute_, stage_ev_[w], 0));
+          used_staged = true;
+        }
+      if (used_staged) staged_used_.fetch_add(1, std::memory_order_relaxed);
       job.has_text = any_text;
-      HIP_CHECK(hipEventRecord(sl.ev_h2d, s_h2d_));
-      HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_h2d, 0));
+      for (int si = 0; si < kStageStreams; ++si)
+        if (copied[si]) {
+          HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
+          HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_h2d[si], 0));
+        }
       HIP_CHECK(hipEventRecord(sl.ev_fwd0, s_compute_));
       size_t bi = 0;
       while (buckets_[bi] < B) ++bi;
@@ -290,36 +400,36 @@ class HipEngine : public Engine {
         comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, s_compute_);
         HIP_CHECK(hipEventRecord(sl.ev_gather, s_compute_));
         if (comm_->rank() == 0) {
-          HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_gather, 0));
           HIP_CHECK(hipMemcpyAsync(sl.h_gather, sl.d_gather, sizeof(float) * out_numel_ * B * dp_world_,
-                                   hipMemcpyDeviceToHost, s_d2h_));
+                                   hipMemcpyDeviceToHost, s_compute_));
           HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
-                                   hipMemcpyDeviceToHost, s_d2h_));
-          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
+                                   hipMemcpyDeviceToHost, s_compute_));
+          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
         } else {
           HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
         }
         job.has_text = text_cap_ > 0;
       } else {
-        HIP_CHECK(hipStreamWaitEvent(s_d2h_, sl.ev_fwd1, 0));
-        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_d2h_));
+        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_compute_));
         if (any_text)
-          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_d2h_));
-        HIP_CHECK(hipEventRecord(sl.ev_d2h, s_d2h_));
+          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_compute_));
+        HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
       }
     } catch (const std::exception& e) {
       job.error = e.what();
     }
+    diag_submit_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     {
       std::lock_guard<std::mutex> g(mu_);
       jobs_.push_back(std::move(job));
+      ++callbacks_running_;
     }
     cv_.notify_all();
   }
 
   void synchronize() override {
     std::unique_lock<std::mutex> lk(mu_);
-    slot_cv_.wait(lk, [&] { return inflight_ == 0; });
+    slot_cv_.wait(lk, [&] { return inflight_ == 0 && callbacks_running_ == 0; });
   }
 
   Json stats() const override {
@@ -338,6 +448,18 @@ class HipEngine : public Engine {
     j["device_decode"] = text_cap_ > 0;
     j["dp_rank"] = comm_ ? comm_->rank() : 0;
     j["text_capacity"] = static_cast<long long>(text_cap_);
+    j["stage_slots"] = n_stage_;
+    j["staged_uploads"] = staged_total_.load();
+    j["batches_with_staged"] = staged_used_.load();
+    {
+      const long long st = std::max<long long>(1, staged_total_.load());
+      Json d = Json::object();
+      d["stager_issue_us_avg"] = diag_issue_ns_.load() / 1e3 / st;
+      d["submit_wait_us_avg"] = diag_submit_wait_ns_.load() / 1e3 / st;
+      d["staged_not_ready_at_submit"] = diag_not_ready_.load();
+      d["submit_us_avg"] = diag_submit_ns_.load() / 1e3 / std::max<long long>(1, batches_.load());
+      j["staging_diag"] = d;
+    }
     j["autotuned"] = !tune_.empty();
     j["tuned_conv_us_at_max_batch"] = tuned_conv_us_;
     j["tune_cache_entries_loaded"] = tune_cache_hits_;
@@ -546,7 +668,9 @@ class HipEngine : public Engine {
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
     if (text_cap_) {
       Slot& sl = slots_[s];
-      const hipError_t e = kern::decode_json_numbers(sl.d_text, text_cap_, sl.d_lens, B, sl.d_in,
+      const hipError_t ec = kern::copy_i64(sl.h_lens_dev, sl.d_lens, 2 * max_batch_, st);
+      if (ec != hipSuccess) throw std::runtime_error("launch of decode table fetch failed: " + std::string(hipGetErrorString(ec)));
+      const hipError_t e = kern::decode_json_numbers(d_text_, sl.d_lens + max_batch_, text_cap_, sl.d_lens, B, sl.d_in,
                                                      static_cast<long long>(in_numel_), sl.d_status,
                                                      sl.d_status + max_batch_, sl.d_scratch, st);
       if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
@@ -674,6 +798,7 @@ class HipEngine : public Engine {
   }
 
  private:
+  static constexpr int kStageStreams = 2;
   struct Slot {
     float* d_gather = nullptr;  // data parallel: [world][max_batch][out_numel]
     int* d_gstatus = nullptr;
@@ -683,13 +808,14 @@ class HipEngine : public Engine {
     float* d_in = nullptr;
     float* d_out = nullptr;
     float* h_out = nullptr;
-    unsigned char* d_text = nullptr;  // max_batch x text_cap_ (device decode)
     void* d_scratch = nullptr;
-    long long* d_lens = nullptr;
-    long long* h_lens = nullptr;      // pinned
+    long long* d_lens = nullptr;      // [lens x max_batch][text offsets into d_text_ x max_batch]
+    long long* h_lens = nullptr;      // pinned host-coherent, same layout
+    long long* h_lens_dev = nullptr;  // its device-side address
     int* d_status = nullptr;          // [status x max_batch][ntok x max_batch]
     int* h_status = nullptr;          // pinned
-    hipEvent_t ev_h2d{}, ev_fwd0{}, ev_fwd1{}, ev_d2h{};
+    hipEvent_t ev_h2d[kStageStreams] = {};
+    hipEvent_t ev_fwd0{}, ev_fwd1{}, ev_d2h{};
   };
   struct Job {
     int slot = 0;
@@ -699,6 +825,50 @@ class HipEngine : public Engine {
     std::string error;
     bool has_text = false;
   };
+
+  struct StageReq {
+    int t;
+    const char* text;
+    size_t len;
+  };
+  static constexpr int kQueued = 0, kIssued = 1, kFailed = 2;
+
+  // Block until the stager has issued (or failed) ticket t's copy; returns its state.
+  int wait_staged(int t) {
+    std::unique_lock<std::mutex> lk(stage_mu_);
+    stage_done_cv_.wait(lk, [&] { return stage_state_[t] != kQueued; });
+    return stage_state_[t];
+  }
+
+  void stager_loop() {
+    (void)hipSetDevice(dev_);
+    unsigned long long rr = 0;
+    while (true) {
+      StageReq rq;
+      {
+        std::unique_lock<std::mutex> lk(stage_mu_);
+        stage_cv_.wait(lk, [&] { return stage_stop_ || !stage_q_.empty(); });
+        if (stage_q_.empty()) return;
+        rq = stage_q_.front();
+        stage_q_.pop_front();
+      }
+      // round-robin over kStageStreams copy streams (one reaches ~36 GB/s for 1 MiB pinned copies,
+      // two ~47 GB/s); per stream copies complete in issue order, which the sequence number records
+      const int si = static_cast<int>(rr++ % n_copy_streams_);
+      const auto ti0 = std::chrono::steady_clock::now();
+      const bool ok = hipMemcpyAsync(d_text_ + static_cast<size_t>(rq.t) * text_cap_, rq.text, rq.len,
+                                     hipMemcpyHostToDevice, s_stage_[si]) == hipSuccess &&
+                      hipEventRecord(stage_ev_[rq.t], s_stage_[si]) == hipSuccess;
+      diag_issue_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ti0).count();
+      {
+        std::lock_guard<std::mutex> g(stage_mu_);
+        stage_stream_[rq.t] = si;
+        stage_seq_[rq.t] = ++stage_counter_[si];
+        stage_state_[rq.t] = ok ? kIssued : kFailed;
+      }
+      stage_done_cv_.notify_all();
+    }
+  }
 
   void completion_loop() {
     (void)hipSetDevice(dev_);
@@ -744,13 +914,35 @@ class HipEngine : public Engine {
         r.error = job.error;
       }
       r.wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - job.t0).count();
+      // Take the results out of the slot's pinned buffers and free the slot BEFORE the callbacks
+      // (cache inserts, response hand-off for B requests): the batcher can dispatch the next batch
+      // into this slot while they run, so the GPU does not idle behind host bookkeeping.
+      if (r.ok) {
+        const size_t rows = static_cast<size_t>(job.B) * (comm_ ? dp_world_ : 1);
+        if (r.outputs) {
+          out_copy_.assign(r.outputs, r.outputs + rows * out_numel_);
+          r.outputs = out_copy_.data();
+        }
+        if (r.status) {
+          const size_t n = comm_ ? static_cast<size_t>(r.status_stride) * dp_world_ : 2 * static_cast<size_t>(max_batch_);
+          const int* base = r.status;
+          status_copy_.assign(base, base + n);
+          r.status = status_copy_.data();
+          r.ntok = status_copy_.data() + max_batch_;
+        }
+      }
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        --inflight_;
+      }
+      slot_cv_.notify_all();
       try {
         job.done(r);
       } catch (...) {
       }
       {
         std::lock_guard<std::mutex> g(mu_);
-        --inflight_;
+        --callbacks_running_;
       }
       slot_cv_.notify_all();
     }
@@ -765,6 +957,23 @@ class HipEngine : public Engine {
   Plan plan_;
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
+  unsigned char* d_text_ = nullptr;  // (n_stage_ + depth_ * max_batch_) x text_cap_
+  int n_stage_ = 0;                  // early-upload slots (stage_text)
+  hipStream_t s_stage_[kStageStreams] = {};
+  int n_copy_streams_ = kStageStreams;  // copy streams in use (DIE_COPY_STREAMS, 1..kStageStreams)
+  unsigned long long stage_counter_[kStageStreams] = {};
+  std::vector<hipEvent_t> stage_ev_;
+  std::vector<unsigned long long> stage_seq_;  // guarded by stage_mu_ (like the three below)
+  std::vector<int> stage_stream_;
+  std::vector<int> stage_state_;
+  std::vector<int> stage_free_;
+  std::deque<StageReq> stage_q_;
+  bool stage_stop_ = false;
+  std::mutex stage_mu_;
+  std::condition_variable stage_cv_, stage_done_cv_;
+  std::thread stager_;
+  std::atomic<long long> staged_total_{0}, staged_used_{0};
+  std::atomic<long long> diag_issue_ns_{0}, diag_submit_wait_ns_{0}, diag_not_ready_{0}, diag_submit_ns_{0};
   long long tune_cache_hits_ = 0;
   static constexpr int kCounters = 1 << 16;
   int* counters_ = nullptr;
@@ -778,7 +987,7 @@ class HipEngine : public Engine {
   uint16_t* zeros_ = nullptr;
   std::vector<std::vector<Tune>> tune_;  // [bucket][op]
   double tuned_conv_us_ = 0;
-  hipStream_t s_compute_{}, s_h2d_{}, s_d2h_{};
+  hipStream_t s_compute_{};
   std::vector<Slot> slots_;
   std::vector<int> buckets_;
   std::vector<hipGraphExec_t> graphs_;
@@ -788,6 +997,9 @@ class HipEngine : public Engine {
   std::condition_variable cv_, slot_cv_;
   std::deque<Job> jobs_;
   int inflight_ = 0;
+  int callbacks_running_ = 0;           // submitted batches whose callback has not returned yet
+  std::vector<float> out_copy_;         // completion thread: results of the batch being called back
+  std::vector<int> status_copy_;
   int next_slot_ = 0;
   bool stop_ = false;
   std::atomic<long long> batches_{0}, images_{0};

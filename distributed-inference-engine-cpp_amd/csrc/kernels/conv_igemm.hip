@@ -371,13 +371,23 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
 // MODE 0: dense rows (1x1/s1 conv, GEMM), K % 64 == 0.  MODE 2: implicit conv with Cin % 64 == 0
 // (one 64-channel K-step never straddles a filter tap, so the tap is wave-uniform per K-step).
 // ------------------------------------------------------------------------------------------------
+// s_waitcnt with only the vector-memory counter constrained (gfx9 simm16: vmcnt = bits 3:0 + 15:14,
+// expcnt 6:4 and lgkmcnt 11:8 left at their maxima).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N == 0, "unsupported vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Wait until at most j*G of this wave's DMA instructions are outstanding, j <= J (j wave-uniform).
+template <int G, int J>
+__device__ __forceinline__ void wait_stages(int j) {
+  if constexpr (J == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (j >= J) wait_vmcnt<G * J>();
+    else wait_stages<G, J - 1>(j);
+  }
 }
 
 __device__ __forceinline__ void glds16(const uint16_t* g, uint16_t* l) {
@@ -478,9 +488,9 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     if (s < nk) issue(kt_begin + s, s);
 
   for (int t = 0; t < nk; ++t) {
-    // Stage t has landed for this wave once at most (STAGES-2) younger stages are outstanding.
-    if (STAGES == 3 && t + 1 < nk) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
+    // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
+    // instructions each) are outstanding.
+    wait_stages<G, STAGES - 2>(nk - 1 - t);
     __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
     asm volatile("" ::: "memory");
     if (t + STAGES - 1 < nk) issue(kt_begin + t + STAGES - 1, (t + STAGES - 1) % STAGES);
@@ -508,6 +518,12 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid);
 }
 
+template <int BM, int BN, int STAGES>
+void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
+  if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+  else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+}
+
 template <int BM, int BN>
 hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   const bool dense1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
@@ -528,12 +544,15 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
     if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
-    if (variant == 1) {
-      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, 2>), grid, dim3(256), 0, s, b, kt_per);
-      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, 2>), grid, dim3(256), 0, s, b, kt_per);
-    } else {
-      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, 3>), grid, dim3(256), 0, s, b, kt_per);
-      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, 3>), grid, dim3(256), 0, s, b, kt_per);
+    // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS)
+    constexpr int kStageBytes = (BM + BN) * BK * 2;
+    switch (variant) {
+      case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
+      case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;
+      case 3: launch_glds<BM, BN, 4>(mode0, grid, s, b, kt_per); break;
+      default:
+        if constexpr (6 * kStageBytes <= 160 * 1024) launch_glds<BM, BN, 6>(mode0, grid, s, b, kt_per);
+        else return hipErrorInvalidValue;
     }
   } else if (dense1x1 && vec == 8) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), grid, dim3(256), 0, s, b, kt_per);

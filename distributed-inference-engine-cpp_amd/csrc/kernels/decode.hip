@@ -92,6 +92,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
 }
 
 __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict__ text, long long cap,
+                                                 const long long* __restrict__ offs,
                                                  const long long* __restrict__ lens, int* __restrict__ counts,
                                                  int* __restrict__ blank, int max_chunks) {
   __shared__ int red[4];
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict
   const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
   int c = 0, nb = 0;
   if (off < len) {
-    const uint4 q = load16(text + b * cap, off, len);
+    const uint4 q = load16(text + (offs ? offs[b] : b * cap), off, len);
     c = popc_commas(q);
     nb = nonblank(q);
   }
@@ -340,6 +341,7 @@ __device__ __forceinline__ bool convert_token_regs(const uint32_t (&r)[8], int n
 // (2) a block scan compacts them into an LDS list, (3) each lane converts whole tokens, loading 32
 // bytes into registers with aligned LDS reads + alignbyte.
 __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
+                                                 const long long* __restrict__ offs,
                                                  const long long* __restrict__ lens, const int* __restrict__ prefix,
                                                  int* __restrict__ status, float* __restrict__ out, long long numel,
                                                  int max_chunks) {
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
   const long long len = lens[b];
   const long long c0 = static_cast<long long>(chunk) * CHUNK;
   if (len < 0 || c0 >= len) return;
-  const unsigned char* t = text + b * cap;
+  const unsigned char* t = text + (offs ? offs[b] : b * cap);
   // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
   for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
     const long long off = c0 - PRE + 16ll * i;
@@ -431,18 +433,18 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
   return static_cast<size_t>(max_batch) * chunks * 2 * sizeof(int);
 }
 
-hipError_t decode_json_numbers(const unsigned char* text, size_t text_cap, const long long* lens, int B,
-                               float* out, long long numel, int* status, int* ntok, void* scratch,
-                               hipStream_t s) {
+hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
+                               const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
+                               void* scratch, hipStream_t s) {
   if (text_cap % CHUNK) return hipErrorInvalidValue;
   const int max_chunks = static_cast<int>(text_cap / CHUNK);
   int* counts = static_cast<int*>(scratch);
   int* blank = counts + static_cast<size_t>(B) * max_chunks;
-  hipLaunchKernelGGL(dec_count, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), lens,
-                     counts, blank, max_chunks);
+  hipLaunchKernelGGL(dec_count, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
+                     lens, counts, blank, max_chunks);
   hipLaunchKernelGGL(dec_scan, dim3(B), dim3(256), 0, s, lens, counts, blank, status, ntok, out, numel, max_chunks);
-  hipLaunchKernelGGL(dec_parse, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), lens,
-                     counts, status, out, numel, max_chunks);
+  hipLaunchKernelGGL(dec_parse, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
+                     lens, counts, status, out, numel, max_chunks);
   return hipGetLastError();
 }
 

@@ -44,9 +44,10 @@ struct ConvArgs {
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),
-// 1 = LDS-DMA 2-stage ring, 2 = LDS-DMA 3-stage ring (variants 1/2: 1x1 with K % 64 == 0, or
-// Cin % 64 == 0; they return hipErrorInvalidValue otherwise so a tuner can skip them).
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 12 };
+// 1..4 = LDS-DMA ring of 2, 3, 4, 6 stages (variants 1-4: 1x1 with K % 64 == 0, or Cin % 64 == 0;
+// 6 stages only where they fit the LDS; they return hipErrorInvalidValue otherwise so a tuner can
+// skip them).  The deep rings keep more K-steps in flight for the latency-bound small-M layers.
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 20 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).
@@ -83,14 +84,18 @@ hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
                         int Ho, int Wo, int relu, hipStream_t s);
 
+// dst[0..n) = src[0..n) in one small block (src may be host-coherent pinned memory).
+hipError_t copy_i64(const long long* src, long long* dst, int n, hipStream_t s);
+
 // ---- device JSON decode (decode.hip) ----
-// Sample b's number-list text lives at text + b * text_cap (text_cap % 4096 == 0) with lens[b]
-// bytes (-1 = not a text sample: skipped).  Writes out[b][0..numel) (values, zero padded),
-// status[b] (0 ok, bit 0 = needs host parse, 2 = more than numel values) and ntok[b].
+// Sample b's number-list text lives at text + offs[b] (offs == nullptr: text + b * text_cap;
+// text_cap % 4096 == 0) with lens[b] <= text_cap bytes (-1 = not a text sample: skipped).  Writes
+// out[b][0..numel) (values, zero padded), status[b] (0 ok, bit 0 = needs host parse, 2 = more than
+// numel values) and ntok[b].
 size_t decode_scratch_bytes(int max_batch, size_t text_cap);
-hipError_t decode_json_numbers(const unsigned char* text, size_t text_cap, const long long* lens, int B,
-                               float* out, long long numel, int* status, int* ntok, void* scratch,
-                               hipStream_t s);
+hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
+                               const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
+                               void* scratch, hipStream_t s);
 
 // ---- transformer (transformer.hip) ----
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.

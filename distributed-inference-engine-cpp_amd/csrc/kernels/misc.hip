@@ -246,6 +246,17 @@ hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s) 
   return hipGetLastError();
 }
 
+// Pull a small per-batch table written by the host into device memory from inside a captured graph
+// (src = host-coherent pinned memory): no SDMA copy that could queue behind bulk uploads.
+__global__ void copy_i64_kernel(const long long* __restrict__ src, long long* __restrict__ dst, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+hipError_t copy_i64(const long long* src, long long* dst, int n, hipStream_t s) {
+  hipLaunchKernelGGL(copy_i64_kernel, dim3(1), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+
 hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s) {
   hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
   return hipGetLastError();

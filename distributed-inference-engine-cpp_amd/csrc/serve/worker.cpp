@@ -73,6 +73,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
         it.len = 0;
         it.text = reinterpret_cast<const char*>(r.buf.data);
         it.text_len = r.text_len;
+        it.staged = r.staged;
       }
       items.push_back(it);
     }
@@ -232,7 +233,13 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     });
     return;
   }
-  if (text_len) device_decoded_.fetch_add(1, std::memory_order_relaxed);
+  long staged = -1;
+  if (text_len) {
+    device_decoded_.fetch_add(1, std::memory_order_relaxed);
+    // start the H2D of this request's text now: by the time its batch is dispatched the bytes are
+    // on the device and the batch waits only for the GPU
+    staged = eng.stage_text(reinterpret_cast<const char*>(sink.buf.data), text_len);
+  }
   const auto t_queued = std::chrono::steady_clock::now();
   h_parse_.add(t_queued - t_start);
 
@@ -244,6 +251,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   p.len = sink.n;
   p.text_len = text_len;
   p.text_off = text_off;
+  p.staged = staged;
   p.key = key;
   dispatch(std::move(p), std::move(res));
 }
@@ -251,11 +259,14 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
 void WorkerNode::dispatch(Pending p, Responder res) {
   const SampleBuffer buf = p.buf;
   const size_t text_len = p.text_len, text_off = p.text_off;
+  const long staged = p.staged;
   const InputKey key = p.key;
   const auto t_start = p.t_start, t_queued = p.t_queued;
   std::string id_copy = p.request_id;
-  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, t_start, t_queued,
+  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, staged, t_start, t_queued,
                                   id = std::move(id_copy)](Result* r, std::exception_ptr err) mutable {
+    // the batch is done (or the request never ran): its staged device copy is free again
+    engine_->release_staged(staged, !err);
     if (err) {
       engine_->sample_pool().release(buf);
       errors_++;

@@ -63,6 +63,7 @@ class WorkerNode {
     size_t len = 0;       // parsed floats in buf
     size_t text_len = 0;  // > 0: buf holds input_data text for device decode instead
     size_t text_off = 0;  // offset of that text in the request body (host-fallback error offsets)
+    long staged = -1;     // Engine::stage_text ticket (text already uploading to the device)
     InputKey key;
     std::chrono::steady_clock::time_point t_start{}, t_queued{};
   };

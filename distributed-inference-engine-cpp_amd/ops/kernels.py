@@ -53,50 +53,72 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128):
     return out, K, Kpad
 
 
+class ConvProblem:
+    """One implicit-GEMM conv problem with packed weights and preallocated outputs, re-launchable with
+    any (config, split-K, fused) choice -- used by conv2d_nhwc and by tools/conv_bench.py.
+    x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float."""
+
+    def __init__(self, x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
+                 scale2=None, shift2=None, relu2=False, max_splits=16):
+        import torch
+
+        B, H, W, Cs = x_nhwc.shape
+        cout, cin, kh, kw = w.shape
+        self.wp, K, Kpad = pack_conv_weight(w, Cs)
+        Ho = (H + 2 * pad - dil * (kh - 1) - 1) // stride + 1
+        Wo = (W + 2 * pad - dil * (kw - 1) - 1) // stride + 1
+        dev = x_nhwc.device
+
+        def padded(v):
+            if v is None:
+                return None
+            n = (v.numel() + 127) // 128 * 128
+            o = torch.zeros(n, dtype=torch.float32, device=dev)
+            o[: v.numel()] = v.float()
+            return o
+
+        self.x = x_nhwc.contiguous()
+        self.res = res.contiguous() if res is not None else None
+        self.bias_p, self.s2_p, self.b2_p = padded(bias), padded(scale2), padded(shift2)
+        self.out_f32 = out_f32
+        self.out = torch.empty((B, Ho, Wo, cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
+        self.out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
+        self.geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad,
+                         pad_w=pad, dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2))
+        self.zeros = torch.zeros(2048, dtype=torch.int16, device=dev)
+        self.geom["zeros"] = int(self.zeros.data_ptr())
+        self.ws = torch.empty(max(1, max_splits) * B * Ho * Wo * cout if max_splits > 1 else 1, dtype=torch.float32,
+                              device=dev)
+        # fused split-K: the last split block of a tile reduces in-kernel (counters start at zero and
+        # are reset by that block)
+        self.counters = torch.zeros(65536, dtype=torch.int32, device=dev)
+        self.flops = 2.0 * B * Ho * Wo * cout * cin * kh * kw
+        self._L = native.kernels()
+
+    def launch(self, tile=-1, splits=1, fused_splitk=True) -> int:
+        """Launch on torch's current stream; returns the hipError code (1 = config not applicable)."""
+        g = dict(self.geom, splits=int(splits))
+        if splits > 1:
+            g["ws"] = int(self.ws.data_ptr())
+            if fused_splitk:
+                g["counters"] = int(self.counters.data_ptr())
+                g["counters_n"] = int(self.counters.numel())
+        return self._L.die_kern_conv(json.dumps(g).encode(), _ptr(self.x), _ptr(self.wp), _ptr(self.bias_p),
+                                     _ptr(self.res), 0 if self.out_f32 else _ptr(self.out),
+                                     _ptr(self.out) if self.out_f32 else 0, _ptr(self.s2_p), _ptr(self.b2_p),
+                                     _ptr(self.out2), tile, _stream())
+
+
 def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
                 scale2=None, shift2=None, relu2=False, tile=-1, splits=1, fused_splitk=True):
     """Implicit-GEMM conv.  x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float.
     Returns (out, out2) in NHWC ([B,Ho,Wo,Cout]); out is f32 if out_f32 else bf16."""
-    import torch
-
-    B, H, W, Cs = x_nhwc.shape
-    cout, cin, kh, kw = w.shape
-    wp, K, Kpad = pack_conv_weight(w, Cs)
-    Ho = (H + 2 * pad - dil * (kh - 1) - 1) // stride + 1
-    Wo = (W + 2 * pad - dil * (kw - 1) - 1) // stride + 1
-    dev = x_nhwc.device
-
-    def padded(v):
-        if v is None:
-            return None
-        n = (v.numel() + 127) // 128 * 128
-        o = torch.zeros(n, dtype=torch.float32, device=dev)
-        o[: v.numel()] = v.float()
-        return o
-
-    bias_p, s2_p, b2_p = padded(bias), padded(scale2), padded(shift2)
-    out = torch.empty((B, Ho, Wo, cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
-    out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
-    geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad, pad_w=pad,
-                dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2), splits=int(splits))
-    zeros = torch.zeros(2048, dtype=torch.int16, device=dev)
-    geom["zeros"] = int(zeros.data_ptr())
-    ws = None
-    if splits > 1:
-        ws = torch.empty(splits * B * Ho * Wo * cout, dtype=torch.float32, device=dev)
-        geom["ws"] = int(ws.data_ptr())
-        if fused_splitk:  # last split block reduces in-kernel (counters must start at zero)
-            counters = torch.zeros(65536, dtype=torch.int32, device=dev)
-            geom["counters"] = int(counters.data_ptr())
-            geom["counters_n"] = 65536
-    L = native.kernels()
-    rc = L.die_kern_conv(json.dumps(geom).encode(), _ptr(x_nhwc.contiguous()), _ptr(wp), _ptr(bias_p),
-                         _ptr(res.contiguous() if res is not None else None), 0 if out_f32 else _ptr(out),
-                         _ptr(out) if out_f32 else 0, _ptr(s2_p), _ptr(b2_p), _ptr(out2), tile, _stream())
+    pr = ConvProblem(x_nhwc, w, bias, stride, pad, dil, relu, res, out_f32, scale2, shift2, relu2, max_splits=splits)
+    rc = pr.launch(tile, splits, fused_splitk)
     if rc != 0 and tile >= 0 and rc == 1:  # hipErrorInvalidValue: config not applicable to this shape
         return None, None
     _check(rc, "conv_igemm")
-    return out, out2
+    return pr.out, pr.out2
 
 
 def input_prep(x_nchw, scale=None, shift=None, cp=4):
@@ -215,8 +237,10 @@ def attention(q, k, v, heads, scale=None):
 
 # ---- device JSON decode (csrc/kernels/decode.hip) ---------------------------------------------------
 
-def decode_json_numbers(texts, numel, text_cap=None):
+def decode_json_numbers(texts, numel, text_cap=None, slot_order=None):
     """Decode number-list texts (bytes, the inside of a JSON array; None = skipped sample) on the GPU.
+    slot_order: optional permutation; sample i's text is then placed in arena slot slot_order[i]
+    and located through the per-sample offset table (the engine's staged-upload layout).
     Returns (values [B, numel] f32, status [B] int32, ntok [B] int32) as torch tensors."""
     import torch
 
@@ -224,23 +248,28 @@ def decode_json_numbers(texts, numel, text_cap=None):
     if text_cap is None:
         text_cap = max(4096, max(len(t) for t in texts if t is not None) + 64)
         text_cap = (text_cap + 4095) // 4096 * 4096
-    host = np.zeros(B * text_cap, np.uint8)
+    slots = list(range(B)) if slot_order is None else list(slot_order)
+    nslots = max(slots) + 1 if slots else 1
+    host = np.zeros(nslots * text_cap, np.uint8)
     lens = np.full(B, -1, np.int64)
+    offs = np.zeros(B, np.int64)
     for i, t in enumerate(texts):
+        offs[i] = slots[i] * text_cap
         if t is None:
             continue
         assert len(t) <= text_cap
-        host[i * text_cap:i * text_cap + len(t)] = np.frombuffer(t, np.uint8)
+        host[offs[i]:offs[i] + len(t)] = np.frombuffer(t, np.uint8)
         lens[i] = len(t)
     L = native.kernels()
     d_text = torch.from_numpy(host).cuda()
     d_lens = torch.from_numpy(lens).cuda()
+    d_offs = torch.from_numpy(offs).cuda() if slot_order is not None else None
     out = torch.full((B, numel), float("nan"), dtype=torch.float32, device="cuda")
     status = torch.full((B,), -7, dtype=torch.int32, device="cuda")
     ntok = torch.zeros(B, dtype=torch.int32, device="cuda")
     scratch = torch.empty(int(L.die_decode_scratch_bytes(B, text_cap)), dtype=torch.uint8, device="cuda")
-    rc = L.die_kern_decode(_ptr(d_text), text_cap, _ptr(d_lens), B, _ptr(out), numel, _ptr(status), _ptr(ntok),
-                           _ptr(scratch), _stream())
+    rc = L.die_kern_decode(_ptr(d_text), _ptr(d_offs), text_cap, _ptr(d_lens), B, _ptr(out), numel, _ptr(status),
+                           _ptr(ntok), _ptr(scratch), _stream())
     _check(rc, "decode_json_numbers")
     return out, status, ntok
 

@@ -58,6 +58,21 @@ def test_decode_matches_host_bit_exact(native):
             assert np.all(vals[i, hn:] == 0)
 
 
+def test_decode_offset_table_matches_contiguous(native):
+    """Staged-upload layout: samples at arbitrary arena slots located through the offset table give
+    the same bits as the contiguous layout."""
+    import torch
+    from die_amd.ops import kernels as K
+
+    texts = _texts()
+    lst = [texts[k] for k in texts] + [None]
+    a = K.decode_json_numbers(lst, 6000, text_cap=128 * 1024)
+    b = K.decode_json_numbers(lst, 6000, text_cap=128 * 1024, slot_order=[7, 3, 11, 0, 5, 9, 2, 12, 8, 1])
+    for x, y in zip(a, b):
+        assert torch.equal(x.cpu().view(torch.int32) if x.dtype == torch.float32 else x.cpu(),
+                           y.cpu().view(torch.int32) if y.dtype == torch.float32 else y.cpu())
+
+
 @pytest.mark.parametrize("bad", [b"1.", b".5", b"01", b"abc", b"1,,2", b"[1]", b'"1"', b"1e", b"+1", b"--1",
                                  b"1" * 70, b"1e-50", b"3e39", b"nan", b"1 2", b"1,"])
 def test_decode_flags_unusual_tokens(native, bad):

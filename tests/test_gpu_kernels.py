@@ -96,7 +96,7 @@ def test_conv_all_tiles_and_epilogue(native, tile, splits, fused):
 ])
 @pytest.mark.parametrize("splits", [1, 2])
 def test_conv_every_variant(native, shape, splits):
-    """All 12 launch configs (4 tiles x {register-staged, LDS-DMA 2-stage, LDS-DMA 3-stage})."""
+    """All 20 launch configs (4 tiles x {register-staged, LDS-DMA ring of 2, 3, 4, 6 stages})."""
     torch = _t()
     from die_amd.ops import kernels as K
 
@@ -111,7 +111,7 @@ def test_conv_every_variant(native, shape, splits):
                      + res.float())
     xn = x.permute(0, 2, 3, 1).contiguous()
     ran = []
-    for cfg in range(12):
+    for cfg in range(20):
         out, _ = K.conv2d_nhwc(xn, w.float(), bias=bias, stride=s, pad=p, relu=True, res=res, tile=cfg,
                                splits=splits)
         if out is None:
@@ -121,6 +121,8 @@ def test_conv_every_variant(native, shape, splits):
         ran.append(cfg)
     assert any(c >= 4 for c in ran), "LDS-DMA variants must apply to these shapes"
     assert any(c >= 8 for c in ran)
+    assert any(c >= 12 for c in ran), "4-stage ring"
+    assert any(c >= 16 for c in ran), "6-stage ring"
 
 
 def test_stem_conv_with_input_prep(native):
@@ -179,6 +181,18 @@ def test_conv_repeatable_bitwise(native):
         for _ in range(10):
             again, _ = K.conv2d_nhwc(x, w, pad=k // 2)
             assert torch.equal(first.view(torch.int16), again.view(torch.int16))
+        # every LDS-DMA ring depth (counted vmcnt per stage) and split-K, repeated
+        pr = K.ConvProblem(x, w, pad=k // 2, max_splits=4)
+        for cfg in range(4, 20):
+            for splits in (1, 4):
+                if pr.launch(cfg, splits) == 1:
+                    continue
+                ref = pr.out.clone()
+                for _ in range(5):
+                    assert pr.launch(cfg, splits) == 0
+                    assert torch.equal(ref.view(torch.int16), pr.out.view(torch.int16)), (cfg, splits)
+                if splits == 1:  # same K order per output element in every config: bit-identical
+                    assert torch.equal(ref.view(torch.int16), first.view(torch.int16)), cfg
 
 
 @pytest.mark.parametrize("cfg", [(2, 112, 64, 3, 2, 1, True), (2, 14, 128, 2, 2, 0, False), (3, 9, 16, 3, 1, 1, False)])
