@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=2)
-    ap.add_argument("--stage-slots", type=int, default=-1,
+    ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
     ap.add_argument("--no-device-decode", action="store_true",
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
@@ -129,6 +129,7 @@ def main():
             "staged_uploads": e1.get("staged_uploads", 0) - e0.get("staged_uploads", 0),
             "pipeline_depth": args.pipeline_depth, "worker_init_s": round(t_ready - t_init, 2),
             "staging_diag": e1.get("staging_diag"),
+            "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
         wk.stop()

@@ -159,7 +159,10 @@ struct EngineOptions {
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
   bool device_decode = true;     // accept input_data text and convert it on the GPU (HIP)
-  int stage_slots = -1;          // early-upload text slots in device memory (-1 = auto, 0 = off)
+  // Early-upload text slots in device memory (stage_text; -1 = auto-sized, 0 = off).  Off by
+  // default: at pipeline depth 2 the submit-time copies already overlap the previous batch and
+  // measured faster (15.9k vs 13.3k req/s, profiles/r1_staging_ab.md); early upload wins at depth 1.
+  int stage_slots = 0;
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

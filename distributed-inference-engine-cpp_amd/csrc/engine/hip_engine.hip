@@ -130,8 +130,6 @@ class HipEngine : public Engine {
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_out), sizeof(float) * out_numel_ * max_batch_,
                               hipHostMallocDefault));
       for (auto& ev : sl.ev_h2d) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreate(&sl.ev_fwd0));
-      HIP_CHECK(hipEventCreate(&sl.ev_fwd1));
       HIP_CHECK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
     }
     // Batch buckets ~sqrt(2) apart (1, 2, 4, 6, 8, 12, 16, 24, 32, ...): a batch runs the graph of
@@ -179,6 +177,7 @@ class HipEngine : public Engine {
       HIP_CHECK(hipGraphLaunch(graphs_.back(), s_compute_));
       HIP_CHECK(hipStreamSynchronize(s_compute_));
     }
+    for (auto& e : tev_) HIP_CHECK(hipEventCreate(&e));
     completion_ = std::thread([this] { completion_loop(); });
     if (n_stage_) stager_ = std::thread([this] { stager_loop(); });
   }
@@ -201,6 +200,8 @@ class HipEngine : public Engine {
     for (auto ge : graphs_)
       if (ge) (void)hipGraphExecDestroy(ge);
     for (auto ev : stage_ev_) (void)hipEventDestroy(ev);
+    for (auto ev : tev_)
+      if (ev) (void)hipEventDestroy(ev);
     for (auto st : s_stage_)
       if (st) (void)hipStreamDestroy(st);
     (void)hipFree(d_text_);
@@ -221,8 +222,6 @@ class HipEngine : public Engine {
       }
       (void)hipHostFree(sl.h_out);
       for (auto ev : sl.ev_h2d) (void)hipEventDestroy(ev);
-      (void)hipEventDestroy(sl.ev_fwd0);
-      (void)hipEventDestroy(sl.ev_fwd1);
       (void)hipEventDestroy(sl.ev_d2h);
     }
     pool_.reset();
@@ -371,6 +370,10 @@ class HipEngine : public Engine {
       }
       // lens/offsets reach the device through the graph's first kernel (host-coherent read), so
       // nothing of this batch queues behind the copy engines except its own fallback copies
+      // timing events from a ring (a job's events outlive its slot's reuse): pre = the compute stream
+      // is done with earlier work; fwd0/fwd1 = around this forward
+      job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * 3);
+      HIP_CHECK(hipEventRecord(tev_[job.ev], s_compute_));
       bool used_staged = false;
       for (int w : wait_ticket)
         if (w >= 0) {
@@ -384,7 +387,7 @@ class HipEngine : public Engine {
           HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
           HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_h2d[si], 0));
         }
-      HIP_CHECK(hipEventRecord(sl.ev_fwd0, s_compute_));
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 1], s_compute_));
       size_t bi = 0;
       while (buckets_[bi] < B) ++bi;
       if (!graphs_.empty()) {
@@ -392,7 +395,7 @@ class HipEngine : public Engine {
       } else {
         encode_forward(buckets_[bi], slot, s_compute_);
       }
-      HIP_CHECK(hipEventRecord(sl.ev_fwd1, s_compute_));
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 2], s_compute_));
       if (comm_) {
         // data parallel: every rank contributes its B rows (and decode status) to rank 0 over xGMI;
         // the same collectives in the same order on every rank, whatever its shard holds.
@@ -439,6 +442,9 @@ class HipEngine : public Engine {
     j["images"] = static_cast<long long>(images_.load());
     const long long nb = batches_.load();
     j["avg_device_ms"] = nb ? device_ms_total_.load() / nb : 0.0;
+    // per batch: compute stream stalled on its input copies / idle before the batch was submitted
+    j["avg_copy_wait_ms"] = nb ? copy_wait_ms_total_.load() / nb : 0.0;
+    j["avg_gpu_gap_ms"] = nb ? gpu_gap_ms_total_.load() / nb : 0.0;
     j["hip_graphs"] = !graphs_.empty();
     j["pipeline_depth"] = depth_;
     j["plan"] = plan_.summary();
@@ -815,7 +821,7 @@ class HipEngine : public Engine {
     int* d_status = nullptr;          // [status x max_batch][ntok x max_batch]
     int* h_status = nullptr;          // pinned
     hipEvent_t ev_h2d[kStageStreams] = {};
-    hipEvent_t ev_fwd0{}, ev_fwd1{}, ev_d2h{};
+    hipEvent_t ev_d2h{};
   };
   struct Job {
     int slot = 0;
@@ -824,6 +830,7 @@ class HipEngine : public Engine {
     std::chrono::steady_clock::time_point t0;
     std::string error;
     bool has_text = false;
+    int ev = 0;  // first of its three timing events in tev_
   };
 
   struct StageReq {
@@ -891,7 +898,12 @@ class HipEngine : public Engine {
           r.error = std::string("device error: ") + hipGetErrorString(e);
         } else {
           float ms = 0;
-          if (hipEventElapsedTime(&ms, sl.ev_fwd0, sl.ev_fwd1) == hipSuccess) r.device_us = ms * 1000.0;
+          if (hipEventElapsedTime(&ms, tev_[job.ev + 1], tev_[job.ev + 2]) == hipSuccess) r.device_us = ms * 1000.0;
+          float wait_ms = 0, gap_ms = 0;
+          if (hipEventElapsedTime(&wait_ms, tev_[job.ev], tev_[job.ev + 1]) == hipSuccess) copy_wait_ms_total_ = copy_wait_ms_total_.load() + wait_ms;
+          if (prev_ev_ >= 0 && hipEventElapsedTime(&gap_ms, tev_[prev_ev_ + 2], tev_[job.ev]) == hipSuccess && gap_ms > 0)
+            gpu_gap_ms_total_ = gpu_gap_ms_total_.load() + gap_ms;
+          prev_ev_ = job.ev;
           r.outputs = sl.h_out;
           r.output_numel = out_numel_;
           if (job.has_text) {
@@ -997,6 +1009,11 @@ class HipEngine : public Engine {
   std::condition_variable cv_, slot_cv_;
   std::deque<Job> jobs_;
   int inflight_ = 0;
+  static constexpr int kTimingJobs = 16;
+  hipEvent_t tev_[3 * kTimingJobs] = {};
+  unsigned long long job_seq_ = 0;  // guarded by submit_mu_
+  int prev_ev_ = -1;                // completion thread
+  std::atomic<double> copy_wait_ms_total_{0.0}, gpu_gap_ms_total_{0.0};
   int callbacks_running_ = 0;           // submitted batches whose callback has not returned yet
   std::vector<float> out_copy_;         // completion thread: results of the batch being called back
   std::vector<int> status_copy_;
