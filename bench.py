@@ -130,6 +130,7 @@ def main():
             "pipeline_depth": args.pipeline_depth, "worker_init_s": round(t_ready - t_init, 2),
             "staging_diag": e1.get("staging_diag"),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
+            "prep_ms_per_batch": e1.get("avg_prep_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
         wk.stop()

@@ -59,6 +59,10 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     onnx::Model model = onnx::load_onnx(path);
     plan_ = build_plan(model, max_batch_);
+    while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
+      prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
+      ++n_prep_ops_;
+    }
     in_numel_ = plan_.input_numel;
     out_numel_ = plan_.output_numel;
 
@@ -131,6 +135,12 @@ class HipEngine : public Engine {
                               hipHostMallocDefault));
       for (auto& ev : sl.ev_h2d) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
+      HIP_CHECK(hipEventCreateWithFlags(&sl.ev_prep, hipEventDisableTiming));
+      for (int id : prep_out_ids_) {
+        void* pbuf = nullptr;
+        HIP_CHECK(hipMalloc(&pbuf, std::max<size_t>(plan_.bufs[id].bytes_per_sample * max_batch_, 256)));
+        sl.d_prep.push_back(pbuf);
+      }
     }
     // Batch buckets ~sqrt(2) apart (1, 2, 4, 6, 8, 12, 16, 24, 32, ...): a batch runs the graph of
     // the smallest bucket >= B, so padding waste stays under a third.
@@ -162,17 +172,23 @@ class HipEngine : public Engine {
     if (opt.autotune) autotune();
     if (opt.use_graphs) {
       graphs_.assign(buckets_.size() * depth_, nullptr);
+      prep_graphs_.assign(buckets_.size() * depth_, nullptr);
+      auto capture = [&](int B, int s, Part part) {
+        hipGraph_t g;
+        HIP_CHECK(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
+        encode_forward(B, s, s_compute_, nullptr, part);
+        HIP_CHECK(hipStreamEndCapture(s_compute_, &g));
+        hipGraphExec_t ge;
+        HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphDestroy(g));
+        return ge;
+      };
       for (size_t bi = 0; bi < buckets_.size(); ++bi)
         for (int s = 0; s < depth_; ++s) {
-          hipGraph_t g;
-          HIP_CHECK(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
-          encode_forward(buckets_[bi], s, s_compute_);
-          HIP_CHECK(hipStreamEndCapture(s_compute_, &g));
-          hipGraphExec_t ge;
-          HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-          HIP_CHECK(hipGraphDestroy(g));
-          graphs_[bi * depth_ + s] = ge;
+          prep_graphs_[bi * depth_ + s] = capture(buckets_[bi], s, PREP);
+          graphs_[bi * depth_ + s] = capture(buckets_[bi], s, MAIN);
         }
+      HIP_CHECK(hipGraphLaunch(prep_graphs_.back(), s_compute_));
       // warm the graph path once
       HIP_CHECK(hipGraphLaunch(graphs_.back(), s_compute_));
       HIP_CHECK(hipStreamSynchronize(s_compute_));
@@ -199,6 +215,8 @@ class HipEngine : public Engine {
     (void)hipDeviceSynchronize();
     for (auto ge : graphs_)
       if (ge) (void)hipGraphExecDestroy(ge);
+    for (auto ge : prep_graphs_)
+      if (ge) (void)hipGraphExecDestroy(ge);
     for (auto ev : stage_ev_) (void)hipEventDestroy(ev);
     for (auto ev : tev_)
       if (ev) (void)hipEventDestroy(ev);
@@ -223,6 +241,8 @@ class HipEngine : public Engine {
       (void)hipHostFree(sl.h_out);
       for (auto ev : sl.ev_h2d) (void)hipEventDestroy(ev);
       (void)hipEventDestroy(sl.ev_d2h);
+      (void)hipEventDestroy(sl.ev_prep);
+      for (void* pbuf : sl.d_prep) (void)hipFree(pbuf);
     }
     pool_.reset();
     for (void* p : registered_) (void)hipHostUnregister(p);
@@ -368,32 +388,39 @@ class HipEngine : public Engine {
         sl.h_lens[i] = -1;
         h_offs[i] = 0;
       }
-      // lens/offsets reach the device through the graph's first kernel (host-coherent read), so
-      // nothing of this batch queues behind the copy engines except its own fallback copies
-      // timing events from a ring (a job's events outlive its slot's reuse): pre = the compute stream
-      // is done with earlier work; fwd0/fwd1 = around this forward
-      job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * 3);
-      HIP_CHECK(hipEventRecord(tev_[job.ev], s_compute_));
+      job.has_text = any_text;
+      size_t bi = 0;
+      while (buckets_[bi] < B) ++bi;
+      // PREP (decode-table fetch from host-coherent memory, device decode, input prep) runs on copy
+      // stream 0 behind this batch's copies, overlapping the previous batch's MAIN on the compute
+      // stream; MAIN waits for it.  Timing events come from a ring (a job's events outlive its slot's
+      // reuse): pre = compute stream done with earlier work, fwd0/fwd1 around MAIN, p0/p1 around PREP.
+      hipStream_t ps = s_stage_[0];
+      for (int si = 1; si < kStageStreams; ++si)
+        if (copied[si]) {
+          HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
+          HIP_CHECK(hipStreamWaitEvent(ps, sl.ev_h2d[si], 0));
+        }
       bool used_staged = false;
       for (int w : wait_ticket)
         if (w >= 0) {
-          HIP_CHECK(hipStreamWaitEvent(s_compute_, stage_ev_[w], 0));
+          HIP_CHECK(hipStreamWaitEvent(ps, stage_ev_[w], 0));
           used_staged = true;
         }
       if (used_staged) staged_used_.fetch_add(1, std::memory_order_relaxed);
-      job.has_text = any_text;
-      for (int si = 0; si < kStageStreams; ++si)
-        if (copied[si]) {
-          HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
-          HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_h2d[si], 0));
-        }
+      job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 3], ps));
+      if (!prep_graphs_.empty()) HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
+      else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 4], ps));
+      HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
+      HIP_CHECK(hipEventRecord(tev_[job.ev], s_compute_));
+      HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_prep, 0));
       HIP_CHECK(hipEventRecord(tev_[job.ev + 1], s_compute_));
-      size_t bi = 0;
-      while (buckets_[bi] < B) ++bi;
       if (!graphs_.empty()) {
         HIP_CHECK(hipGraphLaunch(graphs_[bi * depth_ + slot], s_compute_));
       } else {
-        encode_forward(buckets_[bi], slot, s_compute_);
+        encode_forward(buckets_[bi], slot, s_compute_, nullptr, MAIN);
       }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 2], s_compute_));
       if (comm_) {
@@ -442,9 +469,10 @@ class HipEngine : public Engine {
     j["images"] = static_cast<long long>(images_.load());
     const long long nb = batches_.load();
     j["avg_device_ms"] = nb ? device_ms_total_.load() / nb : 0.0;
-    // per batch: compute stream stalled on its input copies / idle before the batch was submitted
+    // per batch: compute stream waiting for the batch's PREP (copies + decode) / idle before it was submitted
     j["avg_copy_wait_ms"] = nb ? copy_wait_ms_total_.load() / nb : 0.0;
     j["avg_gpu_gap_ms"] = nb ? gpu_gap_ms_total_.load() / nb : 0.0;
+    j["avg_prep_ms"] = nb ? prep_ms_total_.load() / nb : 0.0;  // decode + input prep, on the copy stream
     j["hip_graphs"] = !graphs_.empty();
     j["pipeline_depth"] = depth_;
     j["plan"] = plan_.summary();
@@ -557,6 +585,8 @@ class HipEngine : public Engine {
     if (id == -2) return sl.d_in;
     if (id == -3) return sl.d_out;
     if (id < 0) return nullptr;
+    for (size_t k = 0; k < prep_out_ids_.size(); ++k)
+      if (prep_out_ids_[k] == id) return sl.d_prep[k];
     return arena_ + plan_.bufs[id].offset;
   }
   const float* prm_ptr(size_t off) const {
@@ -669,10 +699,16 @@ class HipEngine : public Engine {
   // Encode one forward pass for `B` samples using slot `s`'s input/output buffers.
   // op_events (profiling): if given, events[0] is recorded before the first op and events[i + 1]
   // after op i.
-  void encode_forward(int B, int s, hipStream_t st, hipEvent_t* op_events = nullptr) {
+  enum Part { ALL = 0, PREP = 1, MAIN = 2 };
+  // PREP = decode-table fetch + device decode + the leading input-prep ops (per-slot buffers only);
+  // MAIN = the rest.  submit() runs PREP on the copy stream so it overlaps the previous batch's
+  // MAIN on the compute stream.
+  void encode_forward(int B, int s, hipStream_t st, hipEvent_t* op_events = nullptr, Part part = ALL) {
     auto buf = [&](int id) -> void* { return buf_ptr(id, s); };
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
-    if (text_cap_) {
+    const size_t op_begin = part == MAIN ? n_prep_ops_ : 0;
+    const size_t op_end = part == PREP ? n_prep_ops_ : plan_.ops.size();
+    if (text_cap_ && part != MAIN) {
       Slot& sl = slots_[s];
       const hipError_t ec = kern::copy_i64(sl.h_lens_dev, sl.d_lens, 2 * max_batch_, st);
       if (ec != hipSuccess) throw std::runtime_error("launch of decode table fetch failed: " + std::string(hipGetErrorString(ec)));
@@ -682,7 +718,7 @@ class HipEngine : public Engine {
       if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
     }
     if (op_events) HIP_CHECK(hipEventRecord(op_events[0], st));
-    for (size_t op_index = 0; op_index < plan_.ops.size(); ++op_index) {
+    for (size_t op_index = op_begin; op_index < op_end; ++op_index) {
       const PlanOp& op = plan_.ops[op_index];
       hipError_t e = hipSuccess;
       switch (op.kind) {
@@ -822,6 +858,8 @@ class HipEngine : public Engine {
     int* h_status = nullptr;          // pinned
     hipEvent_t ev_h2d[kStageStreams] = {};
     hipEvent_t ev_d2h{};
+    hipEvent_t ev_prep{};
+    std::vector<void*> d_prep;  // per-slot outputs of the PREP part's input-prep ops
   };
   struct Job {
     int slot = 0;
@@ -830,7 +868,7 @@ class HipEngine : public Engine {
     std::chrono::steady_clock::time_point t0;
     std::string error;
     bool has_text = false;
-    int ev = 0;  // first of its three timing events in tev_
+    int ev = 0;  // first of its kEvPerJob timing events in tev_
   };
 
   struct StageReq {
@@ -904,6 +942,9 @@ class HipEngine : public Engine {
           if (prev_ev_ >= 0 && hipEventElapsedTime(&gap_ms, tev_[prev_ev_ + 2], tev_[job.ev]) == hipSuccess && gap_ms > 0)
             gpu_gap_ms_total_ = gpu_gap_ms_total_.load() + gap_ms;
           prev_ev_ = job.ev;
+          float prep_ms = 0;
+          if (hipEventElapsedTime(&prep_ms, tev_[job.ev + 3], tev_[job.ev + 4]) == hipSuccess)
+            prep_ms_total_ = prep_ms_total_.load() + prep_ms;
           r.outputs = sl.h_out;
           r.output_numel = out_numel_;
           if (job.has_text) {
@@ -1002,18 +1043,21 @@ class HipEngine : public Engine {
   hipStream_t s_compute_{};
   std::vector<Slot> slots_;
   std::vector<int> buckets_;
-  std::vector<hipGraphExec_t> graphs_;
+  std::vector<hipGraphExec_t> graphs_;       // MAIN part per (bucket, slot)
+  std::vector<hipGraphExec_t> prep_graphs_;  // PREP part per (bucket, slot)
+  size_t n_prep_ops_ = 0;                    // leading INPUT_PREP ops (PREP part)
+  std::vector<int> prep_out_ids_;            // their outputs live in per-slot buffers
   std::unique_ptr<SamplePool> pool_;
   std::thread completion_;
   std::mutex mu_, submit_mu_;
   std::condition_variable cv_, slot_cv_;
   std::deque<Job> jobs_;
   int inflight_ = 0;
-  static constexpr int kTimingJobs = 16;
-  hipEvent_t tev_[3 * kTimingJobs] = {};
+  static constexpr int kTimingJobs = 16, kEvPerJob = 5;
+  hipEvent_t tev_[kEvPerJob * kTimingJobs] = {};
   unsigned long long job_seq_ = 0;  // guarded by submit_mu_
   int prev_ev_ = -1;                // completion thread
-  std::atomic<double> copy_wait_ms_total_{0.0}, gpu_gap_ms_total_{0.0};
+  std::atomic<double> copy_wait_ms_total_{0.0}, gpu_gap_ms_total_{0.0}, prep_ms_total_{0.0};
   int callbacks_running_ = 0;           // submitted batches whose callback has not returned yet
   std::vector<float> out_copy_;         // completion thread: results of the batch being called back
   std::vector<int> status_copy_;
