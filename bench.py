@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
     ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
     ap.add_argument("--no-device-decode", action="store_true",
@@ -100,6 +101,7 @@ def main():
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
                            engine={"device": "hip", "device_id": local_rank, "max_batch": B,
                                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
+                                   "exec_streams": args.exec_streams,
                                    "device_decode": not args.no_device_decode})
         t_ready = time.perf_counter()
         lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
@@ -127,7 +129,8 @@ def main():
             "cpu_quota": _cpu_quota(), "device_decode": e1.get("device_decode"),
             "decode_fallbacks": h1.get("decode_fallbacks"),
             "staged_uploads": e1.get("staged_uploads", 0) - e0.get("staged_uploads", 0),
-            "pipeline_depth": args.pipeline_depth, "worker_init_s": round(t_ready - t_init, 2),
+            "pipeline_depth": args.pipeline_depth, "exec_streams": e1.get("executors"),
+            "worker_init_s": round(t_ready - t_init, 2),
             "staging_diag": e1.get("staging_diag"),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
             "prep_ms_per_batch": e1.get("avg_prep_ms"),

@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
               << "  --cache-capacity N (1000)  --max-batch N (32)  --batch-timeout-ms N (20)\n"
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision bf16|fp32 (bf16)\n"
-              << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)\n"
+              << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --http-threads N  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch)\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose" << std::endl;
@@ -130,6 +130,7 @@ int main(int argc, char** argv) {
   o.engine.use_graphs = !f.b("no-graphs");
   o.engine.device_decode = !f.b("no-device-decode");
   o.engine.stage_slots = static_cast<int>(f.i("stage-slots", 0));
+  o.engine.exec_streams = static_cast<int>(f.i("exec-streams", 1));
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));

@@ -72,6 +72,7 @@ EngineOptions engine_opts(const Json& j) {
   e.autotune = jget<bool>(j, "autotune", e.autotune);
   e.device_decode = jget<bool>(j, "device_decode", e.device_decode);
   e.stage_slots = jget<int>(j, "stage_slots", e.stage_slots);
+  e.exec_streams = jget<int>(j, "exec_streams", e.exec_streams);
   e.tune_cache = jget<std::string>(j, "tune_cache", e.tune_cache);
   e.precision = jget<std::string>(j, "precision", e.precision);
   e.shard_id = jget<int>(j, "shard_id", e.shard_id);

@@ -156,6 +156,7 @@ struct EngineOptions {
   int device_id = 0;             // HIP device ordinal
   int max_batch = 32;
   int pipeline_depth = 2;        // batches in flight (HIP)
+  int exec_streams = 1;          // of those, batches executing concurrently (HIP; 1 = serialised)
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)
   bool device_decode = true;     // accept input_data text and convert it on the GPU (HIP)

@@ -69,13 +69,23 @@ class HipEngine : public Engine {
     comm_ = opt.dp_comm;
     dp_world_ = comm_ ? comm_->world() : 1;
     HIP_CHECK(hipMalloc(&params_, std::max<size_t>(plan_.params.size(), 256)));
-    HIP_CHECK(hipMalloc(&arena_, std::max<size_t>(plan_.arena_bytes, 256)));
-    HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
-    // Streams = hardware queues: the compute stream (graphs + the small result D2H) and
-    // kStageStreams copy streams (early uploads, submit-time copies).  HIP gives a process
-    // GPU_MAX_HW_QUEUES (4) queues; more streams than that share queues (serialising copies behind
-    // kernels), and raising the limit lets the queue scheduler time-slice the compute queue (measured:
-    // forwards 1.8x longer), so the engine stays within three.
+    // Executors: n_exec_ compute streams, each with its own activation arena, split-K workspace and
+    // tile counters, so n_exec_ batches run on the GPU at once (slot s -> executor s % n_exec_).  At
+    // serving batch sizes (~16) every conv is latency-bound and leaves most CUs idle; a second
+    // batch in flight fills them.  Data-parallel ranks keep one (RCCL collectives in one order).
+    n_exec_ = comm_ ? 1 : std::max(1, std::min({opt.exec_streams, depth_, kMaxExec}));
+    arena_bytes_ = std::max<size_t>(plan_.arena_bytes, 256);
+    for (int e = 0; e < n_exec_; ++e) {
+      HIP_CHECK(hipMalloc(&arenas_[e], arena_bytes_));
+      HIP_CHECK(hipStreamCreateWithFlags(&s_exec_[e], hipStreamNonBlocking));
+    }
+    s_compute_ = s_exec_[0];
+    // Streams = hardware queues: the executor streams (graphs + the small result D2H) and copy
+    // streams (early uploads, submit-time copies, PREP).  HIP gives a process GPU_MAX_HW_QUEUES (4)
+    // queues; more streams than that share queues (serialising copies behind kernels), and raising
+    // the limit lets the queue scheduler time-slice the compute queues (measured: forwards 1.8x
+    // longer), so the engine stays within three: 1 executor + 2 copy streams, or 2 + 1.
+    n_copy_streams_ = n_exec_ > 1 ? 1 : kStageStreams;
     if (const char* e = std::getenv("DIE_COPY_STREAMS")) n_copy_streams_ = std::max(1, std::min(kStageStreams, std::atoi(e)));
     for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
     if (!comm_ || comm_->rank() == 0)
@@ -160,11 +170,14 @@ class HipEngine : public Engine {
         [](void* p) { (void)hipHostFree(p); }, 32);
 
     ws_bytes_ = 64u << 20;  // split-K partials (choose_splits / autotune stay within it)
-    HIP_CHECK(hipMalloc(&ws_, ws_bytes_));
     HIP_CHECK(hipMalloc(&zeros_, 4096));
     HIP_CHECK(hipMemset(zeros_, 0, 4096));
-    HIP_CHECK(hipMalloc(&counters_, sizeof(int) * kCounters));  // fused split-K tile counters
-    HIP_CHECK(hipMemset(counters_, 0, sizeof(int) * kCounters));
+    for (int e = 0; e < n_exec_; ++e) {
+      HIP_CHECK(hipMalloc(&wss_[e], ws_bytes_));
+      HIP_CHECK(hipMalloc(&counterss_[e], sizeof(int) * kCounters));  // fused split-K tile counters
+      HIP_CHECK(hipMemset(counterss_[e], 0, sizeof(int) * kCounters));
+    }
+    ws_ = wss_[0];
     // Validate every op eagerly at the largest bucket, tune, then capture one graph per
     // (bucket, slot).
     for (int s = 0; s < depth_; ++s) encode_forward(max_batch_, s, s_compute_);
@@ -247,11 +260,13 @@ class HipEngine : public Engine {
     pool_.reset();
     for (void* p : registered_) (void)hipHostUnregister(p);
     (void)hipFree(params_);
-    (void)hipFree(arena_);
-    (void)hipFree(ws_);
     (void)hipFree(zeros_);
-    (void)hipFree(counters_);
-    (void)hipStreamDestroy(s_compute_);
+    for (int e = 0; e < n_exec_; ++e) {
+      (void)hipFree(arenas_[e]);
+      (void)hipFree(wss_[e]);
+      (void)hipFree(counterss_[e]);
+      (void)hipStreamDestroy(s_exec_[e]);
+    }
   }
 
   std::string name() const override { return "hip:" + arch_ + ":" + std::to_string(dev_); }
@@ -396,6 +411,7 @@ class HipEngine : public Engine {
       // stream; MAIN waits for it.  Timing events come from a ring (a job's events outlive its slot's
       // reuse): pre = compute stream done with earlier work, fwd0/fwd1 around MAIN, p0/p1 around PREP.
       hipStream_t ps = s_stage_[0];
+      hipStream_t cs = s_exec_[slot % n_exec_];
       for (int si = 1; si < kStageStreams; ++si)
         if (copied[si]) {
           HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
@@ -414,36 +430,36 @@ class HipEngine : public Engine {
       else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
       HIP_CHECK(hipEventRecord(tev_[job.ev + 4], ps));
       HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
-      HIP_CHECK(hipEventRecord(tev_[job.ev], s_compute_));
-      HIP_CHECK(hipStreamWaitEvent(s_compute_, sl.ev_prep, 0));
-      HIP_CHECK(hipEventRecord(tev_[job.ev + 1], s_compute_));
+      HIP_CHECK(hipEventRecord(tev_[job.ev], cs));
+      HIP_CHECK(hipStreamWaitEvent(cs, sl.ev_prep, 0));
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 1], cs));
       if (!graphs_.empty()) {
-        HIP_CHECK(hipGraphLaunch(graphs_[bi * depth_ + slot], s_compute_));
+        HIP_CHECK(hipGraphLaunch(graphs_[bi * depth_ + slot], cs));
       } else {
-        encode_forward(buckets_[bi], slot, s_compute_, nullptr, MAIN);
+        encode_forward(buckets_[bi], slot, cs, nullptr, MAIN);
       }
-      HIP_CHECK(hipEventRecord(tev_[job.ev + 2], s_compute_));
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 2], cs));
       if (comm_) {
         // data parallel: every rank contributes its B rows (and decode status) to rank 0 over xGMI;
         // the same collectives in the same order on every rank, whatever its shard holds.
-        comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, s_compute_);
-        comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, s_compute_);
-        HIP_CHECK(hipEventRecord(sl.ev_gather, s_compute_));
+        comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
+        comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, cs);
+        HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
         if (comm_->rank() == 0) {
           HIP_CHECK(hipMemcpyAsync(sl.h_gather, sl.d_gather, sizeof(float) * out_numel_ * B * dp_world_,
-                                   hipMemcpyDeviceToHost, s_compute_));
+                                   hipMemcpyDeviceToHost, cs));
           HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
-                                   hipMemcpyDeviceToHost, s_compute_));
-          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
+                                   hipMemcpyDeviceToHost, cs));
+          HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
         } else {
-          HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
+          HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
         }
         job.has_text = text_cap_ > 0;
       } else {
-        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, s_compute_));
+        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, cs));
         if (any_text)
-          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, s_compute_));
-        HIP_CHECK(hipEventRecord(sl.ev_d2h, s_compute_));
+          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, cs));
+        HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
       }
     } catch (const std::exception& e) {
       job.error = e.what();
@@ -475,6 +491,8 @@ class HipEngine : public Engine {
     j["avg_prep_ms"] = nb ? prep_ms_total_.load() / nb : 0.0;  // decode + input prep, on the copy stream
     j["hip_graphs"] = !graphs_.empty();
     j["pipeline_depth"] = depth_;
+    j["executors"] = n_exec_;
+    j["copy_streams"] = n_copy_streams_;
     j["plan"] = plan_.summary();
     j["gflop_per_image"] = plan_.flops_per_sample / 1e9;
     j["arena_mib"] = static_cast<double>(plan_.arena_bytes) / (1 << 20);
@@ -587,7 +605,7 @@ class HipEngine : public Engine {
     if (id < 0) return nullptr;
     for (size_t k = 0; k < prep_out_ids_.size(); ++k)
       if (prep_out_ids_[k] == id) return sl.d_prep[k];
-    return arena_ + plan_.bufs[id].offset;
+    return arenas_[s % n_exec_] + plan_.bufs[id].offset;
   }
   const float* prm_ptr(size_t off) const {
     return off == SIZE_MAX ? nullptr : reinterpret_cast<const float*>(params_ + off);
@@ -607,7 +625,7 @@ class HipEngine : public Engine {
     a.shift2 = prm_ptr(op.b2_off);
     a.out2 = static_cast<uint16_t*>(buf_ptr(op.out2, s));
     a.zeros = zeros_;
-    a.counters = counters_;
+    a.counters = counterss_[s % n_exec_];
     a.counters_n = kCounters;
     return a;
   }
@@ -730,7 +748,7 @@ class HipEngine : public Engine {
           kern::ConvArgs a = conv_args(op, B, s);
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
-          a.ws = ws_;
+          a.ws = wss_[s % n_exec_];
           if (!t.fused) a.counters = nullptr;
           e = kern::conv_igemm(a, t.tile, st);
           break;
@@ -1029,13 +1047,18 @@ class HipEngine : public Engine {
   std::atomic<long long> diag_issue_ns_{0}, diag_submit_wait_ns_{0}, diag_not_ready_{0}, diag_submit_ns_{0};
   long long tune_cache_hits_ = 0;
   static constexpr int kCounters = 1 << 16;
-  int* counters_ = nullptr;
+  static constexpr int kMaxExec = 2;
+  int n_exec_ = 1;
+  hipStream_t s_exec_[kMaxExec] = {};
+  uint8_t* arenas_[kMaxExec] = {};
+  float* wss_[kMaxExec] = {};
+  int* counterss_[kMaxExec] = {};
+  size_t arena_bytes_ = 0;
   Communicator* comm_ = nullptr;  // data parallel (not owned)
   int dp_world_ = 1;
   std::vector<void*> registered_;
   uint8_t* params_ = nullptr;
-  uint8_t* arena_ = nullptr;
-  float* ws_ = nullptr;
+  float* ws_ = nullptr;  // executor 0's (autotune)
   size_t ws_bytes_ = 0;
   uint16_t* zeros_ = nullptr;
   std::vector<std::vector<Tune>> tune_;  // [bucket][op]
