@@ -170,8 +170,12 @@ class HipEngine : public Engine {
         [](void* p) { (void)hipHostFree(p); }, 32);
 
     ws_bytes_ = 64u << 20;  // split-K partials (choose_splits / autotune stay within it)
-    HIP_CHECK(hipMalloc(&zeros_, 4096));
-    HIP_CHECK(hipMemset(zeros_, 0, 4096));
+    // zero page for the LDS-DMA conv loads: padding pixels and M-tail rows (a whole K row)
+    size_t zeros_bytes = 4096;
+    for (const PlanOp& op : plan_.ops)
+      if (op.kind == PlanOp::CONV) zeros_bytes = std::max<size_t>(zeros_bytes, (static_cast<size_t>(op.conv.Kpad) + 64) * 2);
+    HIP_CHECK(hipMalloc(&zeros_, zeros_bytes));
+    HIP_CHECK(hipMemset(zeros_, 0, zeros_bytes));
     for (int e = 0; e < n_exec_; ++e) {
       HIP_CHECK(hipMalloc(&wss_[e], ws_bytes_));
       HIP_CHECK(hipMalloc(&counterss_[e], sizeof(int) * kCounters));  // fused split-K tile counters

@@ -426,7 +426,10 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
   }
-  const uint16_t* bsrc[GB];  // MODE 0: row base; MODE 2: image base + channel chunk
+  // MODE 0: each lane's row pointer, M-tail rows pointed into the zero page (which holds a whole
+  // K row), so a K-step is one pointer add.  MODE 2: image base + channel chunk and the output
+  // pixel's top-left input coordinate; taps advance incrementally (no divisions in the loop).
+  const uint16_t* bsrc[GB];
   int bih[GB], biw[GB];
   bool bval[GB];
 #pragma unroll
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     bval[i] = m < p.M;
     const int mm = bval[i] ? m : 0;
     if (MODE == 0) {
-      bsrc[i] = p.x + static_cast<size_t>(mm) * p.Cin + c * 8;
+      bsrc[i] = (bval[i] ? p.x + static_cast<size_t>(mm) * p.Cin : p.zeros) + c * 8;
       bih[i] = biw[i] = 0;
     } else {
       const int hw = p.Ho * p.Wo;
@@ -445,36 +448,51 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
       const int rr = mm - b * hw;
       const int oh = rr / p.Wo;
       const int ow = rr - oh * p.Wo;
-      bih[i] = oh * p.stride - p.pad_h;
+      bih[i] = bval[i] ? oh * p.stride - p.pad_h : -(1 << 20);  // tail rows never pass the bounds test
       biw[i] = ow * p.stride - p.pad_w;
       bsrc[i] = p.x + static_cast<size_t>(b) * p.H * p.W * p.Cin + c * 8;
     }
   }
-  const int cpt = p.Cin / BK;  // K-steps per filter tap (MODE 2)
+  // uniform state of the next K-step to issue (MODE 2: channel offset within the tap, tap x/y)
+  int nx_k0 = kt_begin * BK;
+  int nx_ci0 = 0, nx_kx = 0, nx_ky = 0;
+  if (MODE == 2) {
+    const int cpt = p.Cin / BK;  // K-steps per filter tap
+    const int tap = kt_begin / cpt;
+    nx_ci0 = (kt_begin - tap * cpt) * BK;
+    nx_ky = tap / p.KW;
+    nx_kx = tap - nx_ky * p.KW;
+  }
 
-  auto issue = [&](int kt, int buf) {
+  auto issue = [&](int buf) {
     uint16_t* A = lds + buf * STAGE;
     uint16_t* Bt = A + A_ELEMS;
-    const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) glds16(asrc[i] + k0, A + (wave * (BN / 4) + i * 8) * BK);
+    for (int i = 0; i < GA; ++i) glds16(asrc[i] + nx_k0, A + (wave * (BN / 4) + i * 8) * BK);
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < GB; ++i) glds16(bval[i] ? bsrc[i] + k0 : p.zeros, Bt + (wave * (BM / 4) + i * 8) * BK);
+      for (int i = 0; i < GB; ++i) glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * 8) * BK);
     } else {
-      const int tap = kt / cpt;
-      const int ci0 = (kt - tap * cpt) * BK;
-      const int ky = tap / p.KW;
-      const int kx = tap - ky * p.KW;
+      const int dy = nx_ky * p.dil, dx = nx_kx * p.dil;
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
-        const int ih = bih[i] + ky * p.dil;
-        const int iw = biw[i] + kx * p.dil;
-        const bool v = bval[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-        const uint16_t* src = v ? bsrc[i] + (static_cast<size_t>(ih) * p.W + iw) * p.Cin + ci0 : p.zeros;
+        const int ih = bih[i] + dy;
+        const int iw = biw[i] + dx;
+        const bool v = static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                       static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+        const uint16_t* src = v ? bsrc[i] + ((ih * p.W + iw) * p.Cin + nx_ci0) : p.zeros;
         glds16(src, Bt + (wave * (BM / 4) + i * 8) * BK);
       }
+      nx_ci0 += BK;
+      if (nx_ci0 == p.Cin) {
+        nx_ci0 = 0;
+        if (++nx_kx == p.KW) {
+          nx_kx = 0;
+          ++nx_ky;
+        }
+      }
     }
+    nx_k0 += BK;
   };
 
   f32x4 acc[TN][TM];
@@ -485,16 +503,19 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(kt_begin + s, s);
+    if (s < nk) issue(s);
 
+  int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
   for (int t = 0; t < nk; ++t) {
     // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
     // instructions each) are outstanding.
     wait_stages<G, STAGES - 2>(nk - 1 - t);
     __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
     asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(kt_begin + t + STAGES - 1, (t + STAGES - 1) % STAGES);
-    const uint16_t* A = lds + (t % STAGES) * STAGE;
+    if (t + STAGES - 1 < nk) issue(wr);
+    wr = wr + 1 == STAGES ? 0 : wr + 1;
+    const uint16_t* A = lds + rd * STAGE;
+    rd = rd + 1 == STAGES ? 0 : rd + 1;
     const uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {

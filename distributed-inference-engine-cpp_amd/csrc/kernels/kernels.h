@@ -39,7 +39,8 @@ struct ConvArgs {
   // partials and runs the epilogue itself (no second kernel); they return to zero after use.
   int* counters = nullptr;
   int counters_n = 0;
-  // >= 16 zero bytes (device): source of the LDS-DMA loads for padding pixels / M tails.
+  // Zero page (device), >= Kpad + 64 bf16 elements: source of the LDS-DMA loads for padding pixels
+  // and M-tail rows (a tail row reads a whole K row from it).
   const uint16_t* zeros = nullptr;
 };
 

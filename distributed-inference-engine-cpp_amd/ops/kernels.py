@@ -85,7 +85,7 @@ class ConvProblem:
         self.out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
         self.geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad,
                          pad_w=pad, dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2))
-        self.zeros = torch.zeros(2048, dtype=torch.int16, device=dev)
+        self.zeros = torch.zeros(Kpad + 64, dtype=torch.int16, device=dev)  # zero page >= Kpad + 64
         self.geom["zeros"] = int(self.zeros.data_ptr())
         self.ws = torch.empty(max(1, max_splits) * B * Ho * Wo * cout if max_splits > 1 else 1, dtype=torch.float32,
                               device=dev)
