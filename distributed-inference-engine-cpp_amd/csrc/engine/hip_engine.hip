@@ -18,6 +18,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <filesystem>
 #include <fstream>
 #include <sstream>
 #include <cstring>
@@ -591,7 +592,10 @@ class HipEngine : public Engine {
       }
       root[arch_] = arch;
       const auto slash = path.rfind('/');
-      if (slash != std::string::npos) std::system(("mkdir -p '" + path.substr(0, slash) + "'").c_str());
+      if (slash != std::string::npos) {  // no shell: this process owns a GPU context
+        std::error_code ec;
+        std::filesystem::create_directories(path.substr(0, slash), ec);
+      }
       const std::string tmp = path + ".tmp" + std::to_string(getpid());
       {
         std::ofstream o(tmp);
