@@ -167,7 +167,8 @@ struct EngineOptions {
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";
-  std::string precision = "bf16";  // bf16 | fp32 (HIP compute precision)
+  // bf16 = HIP kernels (bf16 operands, fp32 accumulation); fp32 = CPU executor (device auto/cpu).
+  std::string precision = "bf16";
   int cpu_threads = 0;
   int shard_id = 0;
   // Data parallel (one process per GPU): dp_world ranks share the DpGroup segment

@@ -153,6 +153,40 @@ def test_worker_device_decode_matches_host_parse(native, models):
         b.stop()
 
 
+@pytest.mark.parametrize("opts", [{"stage_slots": -1}, {"stage_slots": -1, "pipeline_depth": 1},
+                                  {"exec_streams": 2}, {"stage_slots": 16, "exec_streams": 2}])
+def test_worker_serving_modes_match(native, models, opts):
+    """Early upload (stage_text tickets), concurrent executors and pipeline depths give the same
+    answers as the default path, under concurrent load (loadgen) and for single requests."""
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["tiny"]
+    base = {"device": "hip", "autotune": False}
+    a = native.Worker(path, node_id="mode", max_batch=8, engine=dict(base, max_batch=8, **opts))
+    b = native.Worker(path, node_id="ref", max_batch=8, engine=dict(base, max_batch=8))
+    try:
+        he = a.health()["engine"]
+        if opts.get("stage_slots"):
+            assert he["stage_slots"] > 0
+        x = r.synthetic_input(4, cfg).reshape(4, -1)
+        for i in range(4):
+            body = json.dumps({"request_id": "s%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            sa, oa = _post(a.url, body)
+            sb, ob = _post(b.url, body)
+            assert sa == sb == 200
+            assert oa["output_data"] == ob["output_data"]
+        numel = int(np.prod(x.shape[1:]))
+        res = native.loadgen(port=a.port, connections=16, requests=400, payload="full", input_numel=numel,
+                             decimals=4, seed=7, timeout_ms=30000)
+        assert res["ok"] == 400 and res["failed"] == 0, res
+        h = a.health()
+        if opts.get("stage_slots"):
+            assert h["engine"]["staged_uploads"] >= 400
+    finally:
+        a.stop()
+        b.stop()
+
+
 def _dumps_texts(n_samples, numel, seed=0):
     rng = np.random.default_rng(seed)
     x = (np.round(rng.random((n_samples, numel)), 4)).astype(np.float32)
