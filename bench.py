@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
     ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
+    ap.add_argument("--no-pace", action="store_true",
+                    help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
+    ap.add_argument("--no-pack-text", action="store_true",
+                    help="upload input text as-is instead of 4-bit packed (device decode)")
     ap.add_argument("--no-device-decode", action="store_true",
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
     args = ap.parse_args()
@@ -101,7 +105,8 @@ def main():
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
                            engine={"device": "hip", "device_id": local_rank, "max_batch": B,
                                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
-                                   "exec_streams": args.exec_streams,
+                                   "exec_streams": args.exec_streams, "pace": not args.no_pace,
+                                   "pack_text": not args.no_pack_text,
                                    "device_decode": not args.no_device_decode})
         t_ready = time.perf_counter()
         lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
@@ -133,7 +138,8 @@ def main():
             "worker_init_s": round(t_ready - t_init, 2),
             "staging_diag": e1.get("staging_diag"),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
-            "prep_ms_per_batch": e1.get("avg_prep_ms"),
+            "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
+            "pace_lead_ms": e1.get("avg_pace_lead_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
         wk.stop()

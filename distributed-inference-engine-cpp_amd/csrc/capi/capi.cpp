@@ -10,6 +10,7 @@
 #include <atomic>
 
 #include "../core/json.h"
+#include "../core/textpack.h"
 #include "../engine/cpu_exec.h"
 #include "../engine/engine.h"
 #include "../serve/circuit_breaker.h"
@@ -72,6 +73,8 @@ EngineOptions engine_opts(const Json& j) {
   e.autotune = jget<bool>(j, "autotune", e.autotune);
   e.device_decode = jget<bool>(j, "device_decode", e.device_decode);
   e.stage_slots = jget<int>(j, "stage_slots", e.stage_slots);
+  e.pace = jget<bool>(j, "pace", e.pace);
+  e.pack_text = jget<bool>(j, "pack_text", e.pack_text);
   e.exec_streams = jget<int>(j, "exec_streams", e.exec_streams);
   e.tune_cache = jget<std::string>(j, "tune_cache", e.tune_cache);
   e.precision = jget<std::string>(j, "precision", e.precision);
@@ -292,9 +295,14 @@ int die_engine_run(void* p, const float* in, long B, long len, float* out, char*
   }
 }
 
+// 4-bit text packing (core/textpack.h): returns 1 if packed, 0 if a byte is outside the alphabet.
+int die_pack_nibbles(const char* src, long long n, unsigned char* dst) { return pack_nibbles(src, static_cast<size_t>(n), dst) ? 1 : 0; }
+void die_unpack_nibbles(const unsigned char* src, long long n, char* dst) { unpack_nibbles(src, static_cast<size_t>(n), dst); }
+int die_engine_text_packing(void* p) { return static_cast<Engine*>(p)->text_packing() ? 1 : 0; }
+
 // Device-decode path: B texts (concatenated, lens[b] bytes each) -> outputs [B][out] and status[b]
 // (0 ok, bit 0 = needs host parse, 2 = too many values; outputs of such samples are undefined).
-int die_engine_run_text(void* p, const char* texts, const long long* lens, long B, float* out, int* status,
+int die_engine_run_text(void* p, const char* texts, const long long* lens, long B, float* out, int* status, int pack,
                         char** err) {
   auto* e = static_cast<Engine*>(p);
   try {
@@ -306,12 +314,15 @@ int die_engine_run_text(void* p, const char* texts, const long long* lens, long 
     for (long b = 0; b < B; ++b) {
       if (static_cast<size_t>(lens[b]) > e->text_capacity()) throw std::runtime_error("text too long");
       SampleBuffer sb = pool.acquire();
-      std::memcpy(sb.data, texts + off, static_cast<size_t>(lens[b]));
-      off += static_cast<size_t>(lens[b]);
-      bufs.push_back(sb);
       BatchItem it;
+      const size_t n = static_cast<size_t>(lens[b]);
+      // pack = 1: 4-bit packed upload when the engine takes it and the text fits the alphabet
+      it.packed = pack && e->text_packing() && pack_nibbles(texts + off, n, reinterpret_cast<uint8_t*>(sb.data));
+      if (!it.packed) std::memcpy(sb.data, texts + off, n);
+      off += n;
+      bufs.push_back(sb);
       it.text = reinterpret_cast<const char*>(sb.data);
-      it.text_len = static_cast<size_t>(lens[b]);
+      it.text_len = n;
       items.push_back(it);
     }
     std::promise<std::string> done;

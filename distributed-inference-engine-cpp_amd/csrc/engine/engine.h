@@ -9,6 +9,7 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -57,6 +58,7 @@ struct BatchItem {
   // (between '[' and ']') in engine-pinned memory; the engine converts it on the device.
   const char* text = nullptr;
   size_t text_len = 0;
+  bool packed = false;  // text is 4-bit packed (core/textpack.h): (text_len + 1) / 2 bytes at `text`
   // Ticket from Engine::stage_text() when the text was already uploaded early (-1 = not staged).
   long staged = -1;
 };
@@ -102,6 +104,10 @@ class Engine {
   virtual void submit(std::vector<BatchItem> items, BatchDone done) = 0;
   // Block until a submit() would not block.
   virtual void wait_for_slot() {}
+  // Pacing for work-conserving batching: the earliest time the next batch should be dispatched.
+  // An engine that knows when the batch in flight will drain returns (drain - lead), where lead
+  // covers the next batch's copies; dispatching earlier only makes the next batch smaller.
+  virtual std::chrono::steady_clock::time_point dispatch_not_before() { return std::chrono::steady_clock::now(); }
   // Drain everything in flight.
   virtual void synchronize() = 0;
 
@@ -109,6 +115,8 @@ class Engine {
   virtual SamplePool& sample_pool() = 0;
   // Bytes of input_data text a SampleBuffer can carry for device decode (0 = not supported).
   virtual size_t text_capacity() const { return 0; }
+  // True when submit() accepts 4-bit packed text items (BatchItem::packed).
+  virtual bool text_packing() const { return false; }
   // Early upload for device decode: start copying one request's input text (engine-pinned, from
   // sample_pool()) into device staging now, on a copy stream, so the batch that later carries it
   // does not wait for its H2D.  Returns a ticket for BatchItem::staged, or -1 when the engine does
@@ -164,6 +172,11 @@ struct EngineOptions {
   // default: at pipeline depth 2 the submit-time copies already overlap the previous batch and
   // measured faster (15.9k vs 13.3k req/s, profiles/r1_staging_ab.md); early upload wins at depth 1.
   int stage_slots = 0;
+  // Just-in-time dispatch (HIP, GREEDY batching): hold the next batch until the batch on the GPU is
+  // about to drain (dispatch_not_before) instead of dispatching it as soon as a slot frees.
+  bool pace = true;
+  // 4-bit packed text upload (core/textpack.h) for device decode: half the H2D bytes per request.
+  bool pack_text = true;
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

@@ -103,6 +103,9 @@ class HipEngine : public Engine {
       n_stage_ = opt.stage_slots >= 0 ? opt.stage_slots : std::min(1024, std::max(256, 8 * max_batch_));
       if (comm_) n_stage_ = 0;
       HIP_CHECK(hipMalloc(&d_text_, text_cap_ * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
+      // 4-bit packed texts (BatchItem::packed) land here and are expanded into d_text_ by PREP
+      // (early upload, when asked for, stages raw text instead)
+      if (!comm_ && opt.pack_text && n_stage_ == 0) HIP_CHECK(hipMalloc(&d_packed_, text_cap_ / 2 * static_cast<size_t>(depth_) * max_batch_));
       stage_ev_.resize(n_stage_);
       stage_seq_.assign(n_stage_, 0);
       stage_stream_.assign(n_stage_, 0);
@@ -115,10 +118,11 @@ class HipEngine : public Engine {
     slots_.resize(depth_);
     for (auto& sl : slots_) {
       if (text_cap_) HIP_CHECK(hipMalloc(&sl.d_scratch, kern::decode_scratch_bytes(max_batch_, text_cap_)));
-      // [lens x max_batch][text offsets x max_batch]
-      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * 2 * max_batch_));
+      // [lens x max_batch][text offsets x max_batch][packed-text offsets x max_batch (-1 = raw)]
+      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * kTableRows * max_batch_));
       HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
       HIP_CHECK(hipMemset(sl.d_lens + max_batch_, 0, sizeof(long long) * max_batch_));
+      HIP_CHECK(hipMemset(sl.d_lens + 2 * max_batch_, 0xFF, sizeof(long long) * max_batch_));
       HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * 2 * max_batch_));
       HIP_CHECK(hipMemset(sl.d_status, 0, sizeof(int) * 2 * max_batch_));
       if (comm_) {
@@ -131,12 +135,13 @@ class HipEngine : public Engine {
         HIP_CHECK(hipEventCreateWithFlags(&sl.ev_gather, hipEventDisableTiming));
       }
       // host-coherent: the graph's first kernel reads it directly (see encode_forward)
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * 2 * max_batch_,
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * kTableRows * max_batch_,
                               hipHostMallocCoherent | hipHostMallocMapped));
       HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.h_lens_dev), sl.h_lens, 0));
       for (int i = 0; i < max_batch_; ++i) {  // no text samples until a submit says otherwise
         sl.h_lens[i] = -1;
         sl.h_lens[max_batch_ + i] = 0;
+        sl.h_lens[2 * max_batch_ + i] = -1;
       }
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_status), sizeof(int) * 2 * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipMalloc(&sl.d_in, sizeof(float) * in_numel_ * max_batch_));
@@ -160,6 +165,7 @@ class HipEngine : public Engine {
       if (b >= 4 && b + b / 2 < max_batch_) buckets_.push_back(b + b / 2);
     }
     buckets_.push_back(max_batch_);
+    est_ms_.assign(buckets_.size(), 0.0);
 
     pool_ = std::make_unique<SamplePool>(
         std::max(in_numel_, text_cap_ / sizeof(float)),
@@ -241,6 +247,7 @@ class HipEngine : public Engine {
     for (auto st : s_stage_)
       if (st) (void)hipStreamDestroy(st);
     (void)hipFree(d_text_);
+    (void)hipFree(d_packed_);
     for (auto& sl : slots_) {
       (void)hipFree(sl.d_in);
       (void)hipFree(sl.d_out);
@@ -281,6 +288,7 @@ class HipEngine : public Engine {
   int max_batch() const override { return max_batch_; }
   SamplePool& sample_pool() override { return *pool_; }
   size_t text_capacity() const override { return text_cap_; }
+  bool text_packing() const override { return d_packed_ != nullptr; }
   bool device_gather() const override { return comm_ != nullptr; }
   void register_host_memory(void* p, size_t bytes) override {
     HIP_CHECK(hipSetDevice(dev_));
@@ -355,6 +363,15 @@ class HipEngine : public Engine {
       next_slot_ = (next_slot_ + 1) % depth_;
     }
     TraceRange tr_submit("engine.submit(h2d+graph)");
+    {
+      // paced dispatch that arrives after the predicted drain of the batch in flight: the GPU idled
+      std::lock_guard<std::mutex> g(pace_mu_);
+      if (pace_armed_) {
+        pace_armed_ = false;
+        const double late = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pace_drain_).count();
+        if (late > 0.03) lead_ms_ = std::min(lead_ms_ + 0.5 * late, 4.0);
+      }
+    }
     Job job;
     job.slot = slot;
     job.B = B;
@@ -365,14 +382,30 @@ class HipEngine : public Engine {
       Slot& sl = slots_[slot];
       bool any_text = false;
       long long* h_offs = sl.h_lens + max_batch_;
+      long long* h_poffs = sl.h_lens + 2 * max_batch_;
       int wait_ticket[kStageStreams];  // per copy stream, the staged copy issued last covers the earlier ones
       bool copied[kStageStreams] = {};  // submit-time copies issued on that stream
       for (auto& w : wait_ticket) w = -1;
       int rr = 0;
       for (int i = 0; i < B; ++i) {
         h_offs[i] = 0;
+        h_poffs[i] = -1;
         if (items[i].text) {
           if (!text_cap_ || items[i].text_len > text_cap_) throw std::runtime_error("input text exceeds device decode capacity");
+          if (items[i].packed) {
+            if (!d_packed_) throw std::runtime_error("engine does not take packed text");
+            const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
+            const size_t pidx = static_cast<size_t>(slot) * max_batch_ + i;
+            h_offs[i] = static_cast<long long>(idx * text_cap_);
+            h_poffs[i] = static_cast<long long>(pidx * (text_cap_ / 2));
+            const int si = rr++ % n_copy_streams_;
+            HIP_CHECK(hipMemcpyAsync(d_packed_ + pidx * (text_cap_ / 2), items[i].text, (items[i].text_len + 1) / 2,
+                                     hipMemcpyHostToDevice, s_stage_[si]));
+            copied[si] = true;
+            sl.h_lens[i] = static_cast<long long>(items[i].text_len);
+            any_text = true;
+            continue;
+          }
           const long t = items[i].staged;
           const auto tw0 = std::chrono::steady_clock::now();
           const bool issued = t >= 0 && t < n_stage_ && wait_staged(static_cast<int>(t)) == kIssued;
@@ -407,6 +440,7 @@ class HipEngine : public Engine {
       for (int i = B; i < max_batch_; ++i) {
         sl.h_lens[i] = -1;
         h_offs[i] = 0;
+        h_poffs[i] = -1;
       }
       job.has_text = any_text;
       size_t bi = 0;
@@ -430,6 +464,7 @@ class HipEngine : public Engine {
         }
       if (used_staged) staged_used_.fetch_add(1, std::memory_order_relaxed);
       job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
+      job.bi = static_cast<int>(bi);
       HIP_CHECK(hipEventRecord(tev_[job.ev + 3], ps));
       if (!prep_graphs_.empty()) HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
       else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
@@ -472,10 +507,57 @@ class HipEngine : public Engine {
     diag_submit_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     {
       std::lock_guard<std::mutex> g(mu_);
+      if (job.error.empty()) {
+        last_ev_ = job.ev;
+        last_bi_ = job.bi;
+      }
       jobs_.push_back(std::move(job));
       ++callbacks_running_;
     }
     cv_.notify_all();
+  }
+
+  // Just-in-time dispatch.  With the GPU busy on batch k, dispatching batch k+1 as soon as a slot
+  // frees makes it carry only what queued during k's submit; holding it until k is about to drain
+  // lets it absorb the requests that arrive meanwhile (bigger batches, better MFMA occupancy).
+  // Estimate: k's MAIN start (observed through its event) + the EMA device time of k's bucket - lead,
+  // where lead (next batch's copies + prep) adapts to the GPU idle time measured before each MAIN.
+  std::chrono::steady_clock::time_point dispatch_not_before() override {
+    using clk = std::chrono::steady_clock;
+    const auto now = clk::now();
+    if (!opt_.pace || n_exec_ > 1 || comm_ || graphs_.empty()) return now;
+    int ev, bi;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (inflight_ == 0 || last_ev_ < 0) return now;
+      ev = last_ev_;
+      bi = last_bi_;
+    }
+    double est, lead;
+    {
+      std::lock_guard<std::mutex> g(pace_mu_);
+      est = est_ms_[bi];
+      lead = lead_ms_;
+    }
+    if (est <= 0.0 || est <= lead) return now;
+    (void)hipSetDevice(dev_);
+    const auto give_up = now + std::chrono::milliseconds(20);
+    hipError_t q;
+    while ((q = hipEventQuery(tev_[ev + 1])) == hipErrorNotReady) {  // k's MAIN has not started yet
+      if (clk::now() > give_up) return clk::now();
+      std::this_thread::sleep_for(std::chrono::microseconds(15));
+    }
+    if (q != hipSuccess || hipEventQuery(tev_[ev + 2]) != hipErrorNotReady) return clk::now();  // k drained
+    const auto t0 = clk::now();
+    const auto drain = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double, std::milli>(est));
+    const auto t = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double, std::milli>(est - lead));
+    {
+      std::lock_guard<std::mutex> g(pace_mu_);
+      pace_drain_ = drain;
+      pace_armed_ = true;
+    }
+    paced_batches_++;
+    return t;
   }
 
   void synchronize() override {
@@ -494,6 +576,13 @@ class HipEngine : public Engine {
     j["avg_copy_wait_ms"] = nb ? copy_wait_ms_total_.load() / nb : 0.0;
     j["avg_gpu_gap_ms"] = nb ? gpu_gap_ms_total_.load() / nb : 0.0;
     j["avg_prep_ms"] = nb ? prep_ms_total_.load() / nb : 0.0;  // decode + input prep, on the copy stream
+    j["pace"] = opt_.pace && n_exec_ == 1 && !comm_ && !graphs_.empty();
+    j["pack_text"] = d_packed_ != nullptr;
+    j["paced_batches"] = static_cast<long long>(paced_batches_.load());
+    {
+      std::lock_guard<std::mutex> g(pace_mu_);
+      j["avg_pace_lead_ms"] = nb ? lead_ms_total_ / nb : 0.0;
+    }
     j["hip_graphs"] = !graphs_.empty();
     j["pipeline_depth"] = depth_;
     j["executors"] = n_exec_;
@@ -736,7 +825,12 @@ class HipEngine : public Engine {
     const size_t op_end = part == PREP ? n_prep_ops_ : plan_.ops.size();
     if (text_cap_ && part != MAIN) {
       Slot& sl = slots_[s];
-      const hipError_t ec = kern::copy_i64(sl.h_lens_dev, sl.d_lens, 2 * max_batch_, st);
+      const hipError_t ec = kern::copy_i64(sl.h_lens_dev, sl.d_lens, kTableRows * max_batch_, st);
+      if (ec == hipSuccess && d_packed_) {
+        const hipError_t eu = kern::unpack_text_nibbles(d_packed_, sl.d_lens + 2 * max_batch_, d_text_,
+                                                        sl.d_lens + max_batch_, sl.d_lens, B, st);
+        if (eu != hipSuccess) throw std::runtime_error("launch of text unpack failed: " + std::string(hipGetErrorString(eu)));
+      }
       if (ec != hipSuccess) throw std::runtime_error("launch of decode table fetch failed: " + std::string(hipGetErrorString(ec)));
       const hipError_t e = kern::decode_json_numbers(d_text_, sl.d_lens + max_batch_, text_cap_, sl.d_lens, B, sl.d_in,
                                                      static_cast<long long>(in_numel_), sl.d_status,
@@ -877,7 +971,7 @@ class HipEngine : public Engine {
     float* d_out = nullptr;
     float* h_out = nullptr;
     void* d_scratch = nullptr;
-    long long* d_lens = nullptr;      // [lens x max_batch][text offsets into d_text_ x max_batch]
+    long long* d_lens = nullptr;      // [lens][text offsets into d_text_][packed offsets into d_packed_] x max_batch
     long long* h_lens = nullptr;      // pinned host-coherent, same layout
     long long* h_lens_dev = nullptr;  // its device-side address
     int* d_status = nullptr;          // [status x max_batch][ntok x max_batch]
@@ -895,6 +989,7 @@ class HipEngine : public Engine {
     std::string error;
     bool has_text = false;
     int ev = 0;  // first of its kEvPerJob timing events in tev_
+    int bi = 0;  // batch bucket
   };
 
   struct StageReq {
@@ -968,6 +1063,20 @@ class HipEngine : public Engine {
           if (prev_ev_ >= 0 && hipEventElapsedTime(&gap_ms, tev_[prev_ev_ + 2], tev_[job.ev]) == hipSuccess && gap_ms > 0)
             gpu_gap_ms_total_ = gpu_gap_ms_total_.load() + gap_ms;
           prev_ev_ = job.ev;
+          {
+            // pacing feedback: device-time EMA per bucket; lead grows fast on GPU idle before this
+            // MAIN (copies/prep late, or dispatched after the GPU drained) and shrinks slowly otherwise
+            std::lock_guard<std::mutex> g(pace_mu_);
+            double& e = est_ms_[job.bi];
+            e = e > 0.0 ? 0.8 * e + 0.2 * ms : ms;
+            // (wait_ms = compute stream idle behind this batch's copies/prep; the device-side gap
+            // before a late submit is not a reliable signal -- it includes the D2H tail -- so
+            // lateness against the predicted drain is measured on the host in submit())
+            const double idle = wait_ms;
+            if (idle > 0.03) lead_ms_ = std::min(lead_ms_ + 0.5 * idle, 4.0);
+            else lead_ms_ = std::max(lead_ms_ - 0.01, 0.05);
+            lead_ms_total_ += lead_ms_;
+          }
           float prep_ms = 0;
           if (hipEventElapsedTime(&prep_ms, tev_[job.ev + 3], tev_[job.ev + 4]) == hipSuccess)
             prep_ms_total_ = prep_ms_total_.load() + prep_ms;
@@ -1037,6 +1146,8 @@ class HipEngine : public Engine {
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
   unsigned char* d_text_ = nullptr;  // (n_stage_ + depth_ * max_batch_) x text_cap_
+  unsigned char* d_packed_ = nullptr;  // depth_ * max_batch_ x text_cap_ / 2 (packed texts, copied at submit)
+  static constexpr int kTableRows = 3;  // per-slot decode table: lens, text offsets, packed offsets
   int n_stage_ = 0;                  // early-upload slots (stage_text)
   hipStream_t s_stage_[kStageStreams] = {};
   int n_copy_streams_ = kStageStreams;  // copy streams in use (DIE_COPY_STREAMS, 1..kStageStreams)
@@ -1093,6 +1204,13 @@ class HipEngine : public Engine {
   std::vector<float> out_copy_;         // completion thread: results of the batch being called back
   std::vector<int> status_copy_;
   int next_slot_ = 0;
+  int last_ev_ = -1, last_bi_ = 0;  // most recent submitted job (guarded by mu_)
+  mutable std::mutex pace_mu_;
+  std::vector<double> est_ms_;      // EMA device ms per bucket (pace_mu_)
+  double lead_ms_ = 0.3, lead_ms_total_ = 0.0;
+  std::chrono::steady_clock::time_point pace_drain_{};  // predicted drain of the batch in flight
+  bool pace_armed_ = false;
+  std::atomic<long long> paced_batches_{0};
   bool stop_ = false;
   std::atomic<long long> batches_{0}, images_{0};
   std::atomic<double> device_ms_total_{0.0};

@@ -433,6 +433,41 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
   return static_cast<size_t>(max_batch) * chunks * 2 * sizeof(int);
 }
 
+// 4-bit packed text (core/textpack.h) -> bytes.  One thread expands 8 packed bytes into 16
+// characters (two 8-byte stores); a block covers 4 KiB of output and strides over the sample.
+__global__ void __launch_bounds__(256) unpack_text(const unsigned char* __restrict__ packed,
+                                                   const long long* __restrict__ poffs, unsigned char* __restrict__ text,
+                                                   const long long* __restrict__ offs, const long long* __restrict__ lens) {
+  const int b = blockIdx.y;
+  const long long po = poffs[b], len = lens[b];
+  if (po < 0 || len <= 0) return;
+  // nibble -> character: symbols 0-7 in lo, 8-15 in hi (one byte each)
+  constexpr unsigned long long lo = 0x3736353433323130ull;  // '0'..'7'
+  constexpr unsigned long long hi = 0x20652B2D2E2C3938ull;  // '8' '9' ',' '.' '-' '+' 'e' ' '
+  const unsigned char* src = packed + po;
+  unsigned char* dst = text + offs[b];
+  for (long long o = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 16; o < len;
+       o += static_cast<long long>(gridDim.x) * 256 * 16) {
+    const uint2 q = *reinterpret_cast<const uint2*>(src + (o >> 1));
+    unsigned long long w[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t byte = ((k < 8 ? q.x : q.y) >> (8 * ((k >> 1) & 3))) & 0xFF;
+      const uint32_t sym = (k & 1) ? (byte >> 4) : (byte & 15);
+      const unsigned long long c = ((sym < 8 ? lo : hi) >> (8 * (sym & 7))) & 0xFF;
+      w[k >> 3] |= c << (8 * (k & 7));
+    }
+    *reinterpret_cast<uint4*>(dst + o) = make_uint4(static_cast<uint32_t>(w[0]), static_cast<uint32_t>(w[0] >> 32),
+                                                    static_cast<uint32_t>(w[1]), static_cast<uint32_t>(w[1] >> 32));
+  }
+}
+
+hipError_t unpack_text_nibbles(const unsigned char* packed, const long long* poffs, unsigned char* text,
+                               const long long* offs, const long long* lens, int B, hipStream_t s) {
+  hipLaunchKernelGGL(unpack_text, dim3(64, B), dim3(256), 0, s, packed, poffs, text, offs, lens);
+  return hipGetLastError();
+}
+
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
                                void* scratch, hipStream_t s) {

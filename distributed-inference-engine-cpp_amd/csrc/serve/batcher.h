@@ -41,6 +41,9 @@ class BatchProcessor {
       std::function<void(std::vector<Request>&&, std::function<void(std::vector<Response>&&, std::exception_ptr)>)>;
   // Called (on the batcher thread) before each dispatch; blocks while downstream is saturated.
   using ReadyFn = std::function<void()>;
+  // Optional pacing (GREEDY): after ReadyFn, requests keep accumulating until the returned time or
+  // until a full batch is queued, whichever comes first.
+  using PaceFn = std::function<std::chrono::steady_clock::time_point()>;
 
   struct Metrics {
     int64_t total_requests = 0;
@@ -67,12 +70,13 @@ class BatchProcessor {
   }
 
   BatchProcessor(size_t max_batch_size, std::chrono::milliseconds timeout, AsyncBatchFn fn, ReadyFn ready,
-                 BatchPolicy policy = BatchPolicy::GREEDY)
+                 BatchPolicy policy = BatchPolicy::GREEDY, PaceFn pace = nullptr)
       : max_batch_(max_batch_size ? max_batch_size : 1),
         timeout_(timeout),
         policy_(policy),
         async_(std::move(fn)),
-        ready_(std::move(ready)) {}
+        ready_(std::move(ready)),
+        pace_(std::move(pace)) {}
 
   ~BatchProcessor() { stop(); }
   BatchProcessor(const BatchProcessor&) = delete;
@@ -139,6 +143,9 @@ class BatchProcessor {
     return m;
   }
 
+  // Total time the batcher held dispatches back for pacing.
+  double paced_ms() const { return paced_ns_.load() / 1e6; }
+
   size_t queue_depth() const {
     std::lock_guard<std::mutex> g(mu_);
     return queue_.size();
@@ -166,6 +173,20 @@ class BatchProcessor {
         }
       }
       if (ready_) ready_();  // downstream saturated -> requests keep accumulating meanwhile
+      bool full;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        full = queue_.size() >= max_batch_;
+      }
+      if (pace_ && policy_ == BatchPolicy::GREEDY && !full) {
+        const auto t = pace_();  // may block (e.g. until the batch in flight starts); not under mu_
+        const auto w0 = std::chrono::steady_clock::now();
+        if (t > w0) {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait_until(lk, t, [&] { return queue_.size() >= max_batch_ || !running_; });
+          paced_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+        }
+      }
       {
         std::lock_guard<std::mutex> g(mu_);
         if (!running_) return;
@@ -219,6 +240,8 @@ class BatchProcessor {
   BatchPolicy policy_;
   AsyncBatchFn async_;
   ReadyFn ready_;
+  PaceFn pace_;
+  std::atomic<long long> paced_ns_{0};
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Item> queue_;

@@ -1,5 +1,6 @@
 #include "worker.h"
 
+#include "../core/textpack.h"
 #include "../core/trace.h"
 
 #include <algorithm>
@@ -73,6 +74,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
         it.len = 0;
         it.text = reinterpret_cast<const char*>(r.buf.data);
         it.text_len = r.text_len;
+        it.packed = r.packed;
         it.staged = r.staged;
       }
       items.push_back(it);
@@ -104,7 +106,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
   };
   batcher_ = std::make_unique<BatchProcessor<Pending, Result>>(
       static_cast<size_t>(std::max(1, std::min(opt_.max_batch, engine_->max_batch()))), opt_.batch_timeout, batch_fn,
-      [eng] { eng->wait_for_slot(); }, opt_.policy);
+      [eng] { eng->wait_for_slot(); }, opt_.policy, [eng] { return eng->dispatch_not_before(); });
   batcher_->start();
 
   server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) { handle_infer(req, res); });
@@ -179,6 +181,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   if (req.t_headers.time_since_epoch().count()) h_recv_.add(t_start - req.t_headers);
   InputKey key;
   size_t text_len = 0, text_off = 0;
+  bool packed = false;
   try {
     seen = parse_infer_body(req.body, sink);
     if ((seen & 4) && sink.text_n > text_cap) {  // too long for device decode: parse on the host
@@ -189,10 +192,16 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     if (!(seen & 1)) throw JsonError("key 'request_id' not found");
     if (!(seen & 2)) throw JsonError("key 'input_data' not found");
     if (seen & 4) {
-      std::memcpy(sink.buf.data, sink.text, sink.text_n);
       text_len = sink.text_n;
       text_off = static_cast<size_t>(sink.text - req.body.data());
-      key = hash_text(sink.text, sink.text_n);
+      auto* dst = reinterpret_cast<uint8_t*>(sink.buf.data);
+      if (eng.text_packing() && pack_nibbles(sink.text, sink.text_n, dst)) {
+        packed = true;  // half the bytes to copy to the device
+        key = hash_bytes(dst, (text_len + 1) / 2, 2);
+      } else {
+        std::memcpy(dst, sink.text, sink.text_n);
+        key = hash_text(sink.text, sink.text_n);
+      }
       // an empty list needs no conversion
       if (text_len == 0) {
         text_len = 0;
@@ -238,7 +247,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     device_decoded_.fetch_add(1, std::memory_order_relaxed);
     // start the H2D of this request's text now: by the time its batch is dispatched the bytes are
     // on the device and the batch waits only for the GPU
-    staged = eng.stage_text(reinterpret_cast<const char*>(sink.buf.data), text_len);
+    if (!packed) staged = eng.stage_text(reinterpret_cast<const char*>(sink.buf.data), text_len);
   }
   const auto t_queued = std::chrono::steady_clock::now();
   h_parse_.add(t_queued - t_start);
@@ -251,6 +260,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   p.len = sink.n;
   p.text_len = text_len;
   p.text_off = text_off;
+  p.packed = packed;
   p.staged = staged;
   p.key = key;
   dispatch(std::move(p), std::move(res));
@@ -259,11 +269,12 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
 void WorkerNode::dispatch(Pending p, Responder res) {
   const SampleBuffer buf = p.buf;
   const size_t text_len = p.text_len, text_off = p.text_off;
+  const bool packed = p.packed;
   const long staged = p.staged;
   const InputKey key = p.key;
   const auto t_start = p.t_start, t_queued = p.t_queued;
   std::string id_copy = p.request_id;
-  batcher_->submit(std::move(p), [this, res, key, buf, text_len, text_off, staged, t_start, t_queued,
+  batcher_->submit(std::move(p), [this, res, key, buf, text_len, packed, text_off, staged, t_start, t_queued,
                                   id = std::move(id_copy)](Result* r, std::exception_ptr err) mutable {
     // the batch is done (or the request never ran): its staged device copy is free again
     engine_->release_staged(staged, !err);
@@ -281,7 +292,7 @@ void WorkerNode::dispatch(Pending p, Responder res) {
       return;
     }
     if (r->decode_status & 1) {
-      host_fallback(buf, text_len, text_off, std::move(id), key, std::move(res));
+      host_fallback(buf, text_len, packed, text_off, std::move(id), key, std::move(res));
       return;
     }
     engine_->sample_pool().release(buf);
@@ -310,7 +321,7 @@ void WorkerNode::dispatch(Pending p, Responder res) {
   });
 }
 
-void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, size_t text_off, std::string id, InputKey key,
+void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, bool packed, size_t text_off, std::string id, InputKey key,
                                Responder res) {
   decode_fallbacks_.fetch_add(1, std::memory_order_relaxed);
   SamplePool& pool = engine_->sample_pool();
@@ -325,7 +336,13 @@ void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, size_t te
   body.append(pad, ' ');
   body += kKey;
   body += '[';
-  body.append(reinterpret_cast<const char*>(text_buf.data), text_len);
+  if (packed) {
+    const size_t at = body.size();
+    body.resize(at + text_len);
+    unpack_nibbles(reinterpret_cast<const uint8_t*>(text_buf.data), text_len, &body[at]);
+  } else {
+    body.append(reinterpret_cast<const char*>(text_buf.data), text_len);
+  }
   body += "]}";
   pool.release(text_buf);
   SampleSink sink;

@@ -63,6 +63,7 @@ class WorkerNode {
     size_t len = 0;       // parsed floats in buf
     size_t text_len = 0;  // > 0: buf holds input_data text for device decode instead
     size_t text_off = 0;  // offset of that text in the request body (host-fallback error offsets)
+    bool packed = false;  // the text is 4-bit packed (core/textpack.h): (text_len + 1) / 2 bytes
     long staged = -1;     // Engine::stage_text ticket (text already uploading to the device)
     InputKey key;
     std::chrono::steady_clock::time_point t_start{}, t_queued{};
@@ -81,7 +82,7 @@ class WorkerNode {
   // Queue a parsed (or text) request on the batcher and answer `res` when it completes.
   void dispatch(Pending p, Responder res);
   // Device decode flagged the text: convert it with the strict host parser and re-dispatch.
-  void host_fallback(SampleBuffer text_buf, size_t text_len, size_t text_off, std::string id, InputKey key,
+  void host_fallback(SampleBuffer text_buf, size_t text_len, bool packed, size_t text_off, std::string id, InputKey key,
                      Responder res);
   HttpResponse error_response(int status, const std::string& msg) const;
 

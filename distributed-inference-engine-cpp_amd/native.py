@@ -83,7 +83,10 @@ def lib() -> C.CDLL:
         sig("die_engine_destroy", None, vp)
         sig("die_engine_info", vp, vp)
         sig("die_engine_run", C.c_int, vp, f32p, C.c_long, C.c_long, f32p, errp)
-        sig("die_engine_run_text", C.c_int, vp, C.c_char_p, i64p, C.c_long, f32p, C.POINTER(C.c_int), errp)
+        sig("die_engine_run_text", C.c_int, vp, C.c_char_p, i64p, C.c_long, f32p, C.POINTER(C.c_int), C.c_int, errp)
+        sig("die_pack_nibbles", C.c_int, C.c_char_p, C.c_longlong, C.c_char_p)
+        sig("die_unpack_nibbles", None, C.c_char_p, C.c_longlong, C.c_char_p)
+        sig("die_engine_text_packing", C.c_int, vp)
         sig("die_engine_profile", vp, vp, C.c_int, C.c_int)
         sig("die_dp_follower_start", vp, cp, errp)
         sig("die_dp_follower_status", vp, vp)
@@ -158,6 +161,20 @@ def format_floats(v: np.ndarray) -> str:
 
 
 # ---- control plane ------------------------------------------------------------------------------
+
+def pack_nibbles(text: bytes) -> Optional[bytes]:
+    """4-bit packing of number-list text (core/textpack.h); None if a byte is outside the alphabet."""
+    dst = C.create_string_buffer((len(text) + 1) // 2 + 1)
+    if not lib().die_pack_nibbles(text, len(text), dst):
+        return None
+    return dst.raw[: (len(text) + 1) // 2]
+
+
+def unpack_nibbles(packed: bytes, n: int) -> bytes:
+    dst = C.create_string_buffer(n + 1)
+    lib().die_unpack_nibbles(packed, n, dst)
+    return dst.raw[:n]
+
 
 def fnv1a(s: str) -> int:
     return lib().die_fnv1a(s.encode())
@@ -301,8 +318,14 @@ class Engine:
         """Per-op device time (µs) of one forward at `batch` (HIP engine; {} for the CPU engine)."""
         return json.loads(_take_str(lib().die_engine_profile(self.h, batch, iters)))
 
-    def run_text(self, texts):
+    @property
+    def text_packing(self) -> bool:
+        """True when the engine takes 4-bit packed input text (half the H2D bytes)."""
+        return bool(lib().die_engine_text_packing(self.h))
+
+    def run_text(self, texts, pack: bool = False):
         """Device-decode path: `texts` are input_data number lists (bytes, without brackets).
+        pack=True uploads them 4-bit packed (as the worker does) when the engine supports it.
         Returns (outputs [B, output numel], status [B]); status 0 = ok, bit 0 = needs the host
         parser, 2 = more values than the model input."""
         B = len(texts)
@@ -312,7 +335,7 @@ class Engine:
         status = np.zeros(B, np.int32)
         err = _err_box()
         rc = lib().die_engine_run_text(self.h, blob, lens.ctypes.data_as(C.POINTER(C.c_int64)), B, _f32(out),
-                                       status.ctypes.data_as(C.POINTER(C.c_int)), C.byref(err))
+                                       status.ctypes.data_as(C.POINTER(C.c_int)), int(pack), C.byref(err))
         if rc != 0:
             _raise_if(err, "engine run_text")
         return out, status

@@ -242,3 +242,39 @@ def test_batcher_exception_propagates_and_stop_fails_fast(native):
     b.stop()
     with pytest.raises(native.NativeError, match="stopped"):
         b.process(1)
+
+
+# ---- 4-bit text packing for the H2D copy (core/textpack.h) ----
+
+_NIB = b"0123456789,.-+e "
+
+
+def _pack_ref(t: bytes) -> bytes:
+    sym = [_NIB.index(c) for c in t] + ([15] if len(t) % 2 else [])
+    return bytes(a | (b << 4) for a, b in zip(sym[0::2], sym[1::2]))
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 31, 63, 64, 65, 127, 128, 4095, 4096, 4097, 10001])
+def test_pack_nibbles_matches_reference(native, n):
+    rng = np.random.default_rng(n)
+    t = bytes(rng.choice(list(_NIB), size=n).tolist())
+    p = native.pack_nibbles(t)
+    assert p == _pack_ref(t)
+    assert native.unpack_nibbles(p, n) == t
+
+
+@pytest.mark.parametrize("bad", [b"E", b"\n", b"\t", b"\r", b"a", b"]", b"\x00", b"\xff", b"/", b":", b"!"])
+@pytest.mark.parametrize("pos", [0, 31, 63, 64, 5000, -1])
+def test_pack_nibbles_rejects_other_bytes(native, bad, pos):
+    t = bytearray(b"0.1234," * 1000)
+    t[pos] = bad[0]
+    assert native.pack_nibbles(bytes(t)) is None
+
+
+def test_pack_nibbles_json_dumps_payload(native):
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(20000).astype(np.float32)
+    t = json.dumps([float(v) for v in x])[1:-1].encode()  # ", " separators, e-notation, negatives
+    p = native.pack_nibbles(t)
+    assert p is not None and len(p) == (len(t) + 1) // 2
+    assert native.unpack_nibbles(p, len(t)) == t

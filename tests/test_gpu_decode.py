@@ -240,3 +240,29 @@ def test_engine_run_text_resnet_tiny(native, models):
     assert st.tolist() == [0, 0, 0]
     np.testing.assert_array_equal(got, e.run(x))
     e.close()
+
+
+@pytest.mark.gpu
+def test_engine_run_text_packed_matches_raw(native, tmp_path):
+    """4-bit packed upload (device unpack -> decode) is bit-identical to the raw-text path; a batch
+    may mix packed and raw (non-packable) samples, with odd and even text lengths."""
+    p = str(tmp_path / "probe.onnx")
+    _identity_model(p)
+    e = native.Engine(p, device="hip", max_batch=8)
+    assert e.text_packing
+    x, texts = _dumps_texts(6, 3 * 16 * 16, seed=7)
+    texts[1] = texts[1] + b" "  # odd/even length flip
+    texts[3] = texts[3].replace(b", ", b",\n", 5)  # newline: not packable -> raw upload
+    texts[4] = b"1,2,3"
+    x[4] = 0
+    x[4, :3] = [1, 2, 3]
+    texts[5] = texts[5].replace(b"0.", b"0.0e0", 0) + b",1E0"  # 'E' -> raw; one extra value
+    assert native.pack_nibbles(texts[3]) is None and native.pack_nibbles(texts[5]) is None
+    raw, st_raw = e.run_text(texts, pack=False)
+    packed, st_packed = e.run_text(texts, pack=True)
+    assert st_packed.tolist() == st_raw.tolist()
+    assert st_raw[:5].tolist() == [0, 0, 0, 0, 0]
+    np.testing.assert_array_equal(packed, raw)
+    ref = e.run(x[:5])
+    np.testing.assert_array_equal(packed[:5], ref)
+    e.close()
