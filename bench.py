@@ -50,8 +50,11 @@ def main():
     ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
     ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
+    ap.add_argument("--no-numa", action="store_true", help="keep the inherited CPU affinity (no NUMA binding)")
     ap.add_argument("--no-pace", action="store_true",
                     help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
+    ap.add_argument("--branch-streams", action="store_true",
+                    help="run the projection-shortcut convs on a side stream (measured slower; off by default)")
     ap.add_argument("--no-pack-text", action="store_true",
                     help="upload input text as-is instead of 4-bit packed (device decode)")
     ap.add_argument("--no-device-decode", action="store_true",
@@ -96,6 +99,10 @@ def main():
         with open(model, "wb") as f:
             f.write(blob)
     torch.cuda.set_device(local_rank)
+    numa = {"bound": False}
+    if not args.no_numa:
+        # one process per GPU: this rank's threads and host buffers on its GPU's socket
+        numa = native.bind_local_cpus(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     B = args.batch
     numel = cfg.in_ch * cfg.image * cfg.image
     extra = {}
@@ -106,7 +113,7 @@ def main():
                            engine={"device": "hip", "device_id": local_rank, "max_batch": B,
                                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
-                                   "pack_text": not args.no_pack_text,
+                                   "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                                    "device_decode": not args.no_device_decode})
         t_ready = time.perf_counter()
         lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
@@ -139,6 +146,7 @@ def main():
             "staging_diag": e1.get("staging_diag"),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
             "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
+            "branch_streams": e1.get("branch_streams"),
             "pace_lead_ms": e1.get("avg_pace_lead_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
@@ -185,7 +193,7 @@ def main():
         import numpy as np
 
         eng = native.Engine(model, device="hip", device_id=local_rank, max_batch=B,
-                            pipeline_depth=args.pipeline_depth)
+                            pipeline_depth=args.pipeline_depth, branch_streams=args.branch_streams)
         x = r.synthetic_input(B, cfg, seed=rank).reshape(B, -1)
         for _ in range(args.warmup):
             eng.run(x)
@@ -228,6 +236,7 @@ def main():
                        "parallelism": "dp%d" % args.gpus, "mode": args.mode, "max_batch_per_gpu": B,
                        "requests": int(ok + failed)},
         }
+        extra["numa"] = numa
         out.update({k: v for k, v in extra.items() if v is not None})
         print(json.dumps(out), flush=True)
     if dist is not None:

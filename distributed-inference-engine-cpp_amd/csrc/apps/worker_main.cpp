@@ -132,6 +132,7 @@ int main(int argc, char** argv) {
   o.engine.stage_slots = static_cast<int>(f.i("stage-slots", 0));
   o.engine.pace = !f.b("no-pace");
   o.engine.pack_text = !f.b("no-pack-text");
+  o.engine.branch_streams = f.b("branch-streams");
   o.engine.exec_streams = static_cast<int>(f.i("exec-streams", 1));
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);

@@ -160,6 +160,19 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;
+      e["join"] = o.join;
+      // arena ranges [offset, offset + bytes) at max_batch of the op's buffers, by role
+      Json bufs = Json::object();
+      const char* roles[] = {"in", "in2", "in3", "out", "out2"};
+      const int ids[] = {o.in, o.in2, o.in3, o.out, o.out2};
+      for (int r = 0; r < 5; ++r)
+        if (ids[r] >= 0) {
+          Json range = Json::array();
+          range.push_back(static_cast<long long>(p.bufs[ids[r]].offset));
+          range.push_back(static_cast<long long>(p.bufs[ids[r]].offset + p.bufs[ids[r]].bytes_per_sample * max_batch));
+          bufs[roles[r]] = range;
+        }
+      e["bufs"] = bufs;
       if (o.kind == PlanOp::CONV) {
         e["N"] = o.conv.N;
         e["K"] = o.conv.K;

@@ -1,12 +1,15 @@
 // CPU budget of this process: min(affinity mask size, cgroup v2 cpu.max quota).  GPU boxes expose
 // the whole machine in the affinity mask (hundreds of CPUs) but enforce a quota of ~16 CPUs per
-// GPU; sizing thread pools from hardware_concurrency() there oversubscribes the quota.
+// GPU; sizing thread pools from hardware_concurrency() there oversubscribes the quota.  When
+// several ranks share one node (one process per GPU), the launcher sets DIE_CPUS to this
+// process's share (native.bind_local_cpus).
 #pragma once
 
 #include <sched.h>
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 
 namespace die {
@@ -24,6 +27,10 @@ inline int available_cpus() {
         if (q > 0) cpus = std::min(cpus, static_cast<int>(std::ceil(q)));
       }
       std::fclose(f);
+    }
+    if (const char* e = std::getenv("DIE_CPUS")) {
+      const int share = std::atoi(e);
+      if (share > 0) cpus = std::min(cpus, share);
     }
     return cpus < 1 ? 1 : cpus;
   }();

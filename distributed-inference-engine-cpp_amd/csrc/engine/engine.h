@@ -177,6 +177,10 @@ struct EngineOptions {
   bool pace = true;
   // 4-bit packed text upload (core/textpack.h) for device decode: half the H2D bytes per request.
   bool pack_text = true;
+  // Run independent plan branches (ResNet projection shortcuts) on a second stream (HIP).  Off by
+  // default: measured slower (ResNet50 forward 0.79 vs 0.75 ms at batch 16, and the serving
+  // headline -15%: the branch's queue competes with the copy streams), profiles/r1_branches_ab.md.
+  bool branch_streams = false;
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

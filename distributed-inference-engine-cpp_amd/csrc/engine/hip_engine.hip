@@ -89,6 +89,13 @@ class HipEngine : public Engine {
     n_copy_streams_ = n_exec_ > 1 ? 1 : kStageStreams;
     if (const char* e = std::getenv("DIE_COPY_STREAMS")) n_copy_streams_ = std::max(1, std::min(kStageStreams, std::atoi(e)));
     for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
+    // side-branch stream (plan ops with join >= 0): the fourth and last queue; only with one executor
+    branches_ = opt.branch_streams && n_exec_ == 1;
+    if (branches_) {
+      HIP_CHECK(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    }
     if (!comm_ || comm_->rank() == 0)
       HIP_CHECK(hipMemcpy(params_, plan_.params.data(), plan_.params.size(), hipMemcpyHostToDevice));
     if (comm_) {  // data parallel: every rank gets the packed weights from rank 0 over xGMI
@@ -188,6 +195,11 @@ class HipEngine : public Engine {
       HIP_CHECK(hipMalloc(&counterss_[e], sizeof(int) * kCounters));  // fused split-K tile counters
       HIP_CHECK(hipMemset(counterss_[e], 0, sizeof(int) * kCounters));
     }
+    if (branches_) {  // a branch running beside the main chain needs its own split-K scratch
+      HIP_CHECK(hipMalloc(&ws_side_, ws_bytes_));
+      HIP_CHECK(hipMalloc(&counters_side_, sizeof(int) * kCounters));
+      HIP_CHECK(hipMemset(counters_side_, 0, sizeof(int) * kCounters));
+    }
     ws_ = wss_[0];
     // Validate every op eagerly at the largest bucket, tune, then capture one graph per
     // (bucket, slot).
@@ -279,6 +291,13 @@ class HipEngine : public Engine {
       (void)hipFree(counterss_[e]);
       (void)hipStreamDestroy(s_exec_[e]);
     }
+    if (branches_) {
+      (void)hipFree(ws_side_);
+      (void)hipFree(counters_side_);
+      (void)hipEventDestroy(ev_fork_);
+      (void)hipEventDestroy(ev_join_);
+      (void)hipStreamDestroy(s_side_);
+    }
   }
 
   std::string name() const override { return "hip:" + arch_ + ":" + std::to_string(dev_); }
@@ -369,7 +388,7 @@ class HipEngine : public Engine {
       if (pace_armed_) {
         pace_armed_ = false;
         const double late = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pace_drain_).count();
-        if (late > 0.03) lead_ms_ = std::min(lead_ms_ + 0.5 * late, 4.0);
+        if (late > 0.03) margin_ms_ = std::min(margin_ms_ + 0.5 * late, 1.0);
       }
     }
     Job job;
@@ -380,6 +399,9 @@ class HipEngine : public Engine {
     try {
       HIP_CHECK(hipSetDevice(dev_));
       Slot& sl = slots_[slot];
+      job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
+      job.bi = static_cast<int>(bucket_index(B));
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 5], s_stage_[0]));  // input upload starts (pacing model)
       bool any_text = false;
       long long* h_offs = sl.h_lens + max_batch_;
       long long* h_poffs = sl.h_lens + 2 * max_batch_;
@@ -463,8 +485,6 @@ class HipEngine : public Engine {
           used_staged = true;
         }
       if (used_staged) staged_used_.fetch_add(1, std::memory_order_relaxed);
-      job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
-      job.bi = static_cast<int>(bi);
       HIP_CHECK(hipEventRecord(tev_[job.ev + 3], ps));
       if (!prep_graphs_.empty()) HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
       else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
@@ -578,10 +598,13 @@ class HipEngine : public Engine {
     j["avg_prep_ms"] = nb ? prep_ms_total_.load() / nb : 0.0;  // decode + input prep, on the copy stream
     j["pace"] = opt_.pace && n_exec_ == 1 && !comm_ && !graphs_.empty();
     j["pack_text"] = d_packed_ != nullptr;
+    j["branch_streams"] = branches_;
     j["paced_batches"] = static_cast<long long>(paced_batches_.load());
     {
       std::lock_guard<std::mutex> g(pace_mu_);
       j["avg_pace_lead_ms"] = nb ? lead_ms_total_ / nb : 0.0;
+      j["pace_input_ms"] = input_ms_;
+      j["pace_margin_ms"] = margin_ms_;
     }
     j["hip_graphs"] = !graphs_.empty();
     j["pipeline_depth"] = depth_;
@@ -838,9 +861,23 @@ class HipEngine : public Engine {
       if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
     }
     if (op_events) HIP_CHECK(hipEventRecord(op_events[0], st));
+    const hipStream_t main_st = st;
+    int pending_join = -1;  // open side branch: the op that waits for it
     for (size_t op_index = op_begin; op_index < op_end; ++op_index) {
       const PlanOp& op = plan_.ops[op_index];
       hipError_t e = hipSuccess;
+      if (static_cast<int>(op_index) == pending_join) {
+        HIP_CHECK(hipStreamWaitEvent(main_st, ev_join_, 0));
+        pending_join = -1;
+      }
+      // per-op profiling times ops one after another: no branches then
+      const bool side = branches_ && !op_events && op.join >= 0 && pending_join < 0;
+      st = main_st;
+      if (side) {
+        HIP_CHECK(hipEventRecord(ev_fork_, main_st));
+        HIP_CHECK(hipStreamWaitEvent(s_side_, ev_fork_, 0));
+        st = s_side_;
+      }
       switch (op.kind) {
         case PlanOp::INPUT_PREP:
           e = kern::input_prep(static_cast<const float*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
@@ -850,7 +887,8 @@ class HipEngine : public Engine {
           kern::ConvArgs a = conv_args(op, B, s);
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
-          a.ws = wss_[s % n_exec_];
+          a.ws = side ? ws_side_ : wss_[s % n_exec_];
+          if (side) a.counters = counters_side_;
           if (!t.fused) a.counters = nullptr;
           e = kern::conv_igemm(a, t.tile, st);
           break;
@@ -903,8 +941,13 @@ class HipEngine : public Engine {
       }
       if (e != hipSuccess)
         throw std::runtime_error("launch of " + op.name + " failed: " + std::string(hipGetErrorString(e)));
+      if (side) {
+        HIP_CHECK(hipEventRecord(ev_join_, s_side_));
+        pending_join = op.join;
+      }
       if (op_events) HIP_CHECK(hipEventRecord(op_events[op_index + 1], st));
     }
+    if (pending_join >= 0) HIP_CHECK(hipStreamWaitEvent(main_st, ev_join_, 0));  // part ended before the join
   }
 
   // Per-op device time (eager launches bracketed by events), averaged over `iters` forwards.
@@ -1064,17 +1107,19 @@ class HipEngine : public Engine {
             gpu_gap_ms_total_ = gpu_gap_ms_total_.load() + gap_ms;
           prev_ev_ = job.ev;
           {
-            // pacing feedback: device-time EMA per bucket; lead grows fast on GPU idle before this
-            // MAIN (copies/prep late, or dispatched after the GPU drained) and shrinks slowly otherwise
+            // pacing model: device-time EMA per bucket, and lead = EMA of this batch's input path
+            // (first copy issued -> PREP done, on the device) + a margin for the dispatch itself
+            // that grows when MAIN had to wait for its input anyway (wait_ms: compute stream idle
+            // behind the copies/prep) and shrinks slowly otherwise
+            float in_ms = 0;
+            const bool have_in = hipEventElapsedTime(&in_ms, tev_[job.ev + 5], tev_[job.ev + 4]) == hipSuccess;
             std::lock_guard<std::mutex> g(pace_mu_);
             double& e = est_ms_[job.bi];
             e = e > 0.0 ? 0.8 * e + 0.2 * ms : ms;
-            // (wait_ms = compute stream idle behind this batch's copies/prep; the device-side gap
-            // before a late submit is not a reliable signal -- it includes the D2H tail -- so
-            // lateness against the predicted drain is measured on the host in submit())
-            const double idle = wait_ms;
-            if (idle > 0.03) lead_ms_ = std::min(lead_ms_ + 0.5 * idle, 4.0);
-            else lead_ms_ = std::max(lead_ms_ - 0.01, 0.05);
+            if (have_in) input_ms_ = input_ms_ > 0.0 ? 0.8 * input_ms_ + 0.2 * in_ms : in_ms;
+            if (wait_ms > 0.02) margin_ms_ = std::min(margin_ms_ + 0.02, 1.0);
+            else margin_ms_ = std::max(margin_ms_ - 0.004, 0.03);
+            lead_ms_ = input_ms_ + margin_ms_;
             lead_ms_total_ += lead_ms_;
           }
           float prep_ms = 0;
@@ -1168,6 +1213,11 @@ class HipEngine : public Engine {
   static constexpr int kCounters = 1 << 16;
   static constexpr int kMaxExec = 2;
   int n_exec_ = 1;
+  bool branches_ = false;  // side-branch stream in use (PlanOp::join)
+  hipStream_t s_side_{};
+  hipEvent_t ev_fork_{}, ev_join_{};
+  float* ws_side_ = nullptr;
+  int* counters_side_ = nullptr;
   hipStream_t s_exec_[kMaxExec] = {};
   uint8_t* arenas_[kMaxExec] = {};
   float* wss_[kMaxExec] = {};
@@ -1195,7 +1245,9 @@ class HipEngine : public Engine {
   std::condition_variable cv_, slot_cv_;
   std::deque<Job> jobs_;
   int inflight_ = 0;
-  static constexpr int kTimingJobs = 16, kEvPerJob = 5;
+  // per job: [0] compute stream reaches the job, [1] MAIN start, [2] MAIN end, [3] PREP start,
+  // [4] PREP end, [5] first input copy issued
+  static constexpr int kTimingJobs = 16, kEvPerJob = 6;
   hipEvent_t tev_[kEvPerJob * kTimingJobs] = {};
   unsigned long long job_seq_ = 0;  // guarded by submit_mu_
   int prev_ev_ = -1;                // completion thread
@@ -1207,7 +1259,7 @@ class HipEngine : public Engine {
   int last_ev_ = -1, last_bi_ = 0;  // most recent submitted job (guarded by mu_)
   mutable std::mutex pace_mu_;
   std::vector<double> est_ms_;      // EMA device ms per bucket (pace_mu_)
-  double lead_ms_ = 0.3, lead_ms_total_ = 0.0;
+  double lead_ms_ = 0.3, lead_ms_total_ = 0.0, input_ms_ = 0.0, margin_ms_ = 0.08;
   std::chrono::steady_clock::time_point pace_drain_{};  // predicted drain of the batch in flight
   bool pace_armed_ = false;
   std::atomic<long long> paced_batches_{0};

@@ -95,6 +95,7 @@ class Planner {
       lower(static_cast<int>(i));
     }
     finalize_output();
+    mark_side_branches();
     assign_arena();
     return std::move(plan_);
   }
@@ -1181,6 +1182,29 @@ class Planner {
     for (auto dim : plan_.output_shape) plan_.output_numel *= static_cast<size_t>(dim);
   }
 
+  // Branch concurrency: a conv whose output is first consumed two or more ops later (ResNet's
+  // projection shortcut: consumed as the residual of the unit's expand conv, after the reduce and
+  // 3x3 convs) is independent of the ops in between.  At serving batch sizes every one of those
+  // convs is latency-bound and leaves CUs idle, so the engine runs the branch on a second stream
+  // and joins it at its consumer.  One branch open at a time.
+  void mark_side_branches() {
+    const int nops = static_cast<int>(plan_.ops.size());
+    int open_until = -1;
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (i <= open_until || p.kind != PlanOp::CONV || p.out < 0 || p.out_f32 >= 0) continue;
+      int j = -1;
+      for (int k = i + 1; k < nops && j < 0; ++k) {
+        const PlanOp& q = plan_.ops[k];
+        for (int b : {q.in, q.in2, q.in3})
+          if (b >= 0 && (b == p.out || b == p.out2)) j = k;
+      }
+      if (j < i + 2) continue;
+      p.join = j;
+      open_until = j;
+    }
+  }
+
   void assign_arena() {
     const int nops = static_cast<int>(plan_.ops.size());
     for (int i = 0; i < nops; ++i) {
@@ -1189,6 +1213,10 @@ class Planner {
         if (b >= 0 && plan_.bufs[b].first_use < 0) plan_.bufs[b].first_use = i;
       for (int b : {p.in, p.in2, p.in3, p.out, p.out2})
         if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, i);
+      // a side branch may still be reading its inputs until its join
+      if (p.join >= 0)
+        for (int b : {p.in, p.in2, p.in3})
+          if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, p.join);
     }
     struct Block {
       size_t off, size;

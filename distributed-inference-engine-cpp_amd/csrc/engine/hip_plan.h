@@ -58,6 +58,9 @@ struct PlanOp {
   int col[3] = {0, 0, 0}, ld[3] = {0, 0, 0};
   float fscale = 1.f, eps = 0.f;
   double flops_per_sample = 0;
+  // Side branch: this op may run on a second stream, concurrently with the ops after it, until
+  // op `join` (its first consumer) waits for it.  The arena keeps its inputs live until `join`.
+  int join = -1;
 };
 
 struct Plan {

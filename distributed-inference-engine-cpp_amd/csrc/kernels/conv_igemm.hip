@@ -82,7 +82,34 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
 
 template <int BM, int BN>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid);
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split);
+
+// XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
+// id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
+// tile = blockIdx.x spreads the N-tiles of one M-tile (same activation rows) or the M-tiles of
+// one N-tile (same weight rows) over 8 L2s.  The bijective remap gives every XCD a contiguous range
+// of logical ids; a tile's split-K slices are adjacent (same XCD for the fused reducer), and tiles
+// are ordered so the operand with more bytes is the one shared within an XCD: N-fastest (an
+// M-tile's activations read once per XCD, every XCD reads all weights) when weights are the
+// smaller operand (N <= M), M-fastest otherwise (stage-4 / FC shapes with M < N).
+__device__ __forceinline__ void block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
+                                             int& tile) {
+  const int nwg = gridDim.x * gridDim.y;
+  const int b = blockIdx.x + blockIdx.y * gridDim.x;
+  const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  const int S = gridDim.y;  // split-K slices
+  tile = id / S;
+  split = id - tile * S;
+  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  if (p.N <= p.M) {
+    tile_m = tile / ntn;
+    tile_n = tile - tile_m * ntn;
+  } else {
+    tile_n = tile / ntm;
+    tile_m = tile - tile_n * ntm;
+  }
+}
 
 template <int BM, int BN, int MODE, int VEC>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const int kt_per_split) {
@@ -98,12 +125,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int ntn = (p.N + BN - 1) / BN;
-  const int tile_n = blockIdx.x % ntn;
-  const int tile_m = blockIdx.x / ntn;
+  int tile_m, tile_n, split, tile;
+  block_coords(p, BM, BN, tile_m, tile_n, split, tile);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BK;
-  const int kt_begin = blockIdx.y * kt_per_split;
+  const int kt_begin = split * kt_per_split;
   const int kt_end = min(nk_total, kt_begin + kt_per_split);
 
   // ---- per-thread loader state ----
@@ -228,14 +254,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     if (more) store_stage(cur ^ 1);
     __syncthreads();
   }
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
 }
 
 // Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
 // past their last operand read).
 template <int BM, int BN>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid) {
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   const int lm = lane & 15;
@@ -255,7 +281,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     __syncthreads();
     constexpr int GPR = BN / 8;
     const bool partial = p.splits > 1;
-    float* ws = partial ? p.ws + static_cast<size_t>(blockIdx.y) * p.M * p.N : nullptr;
+    float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
     for (int g = tid; g < BM * GPR; g += 256) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
@@ -283,7 +309,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     __syncthreads();
     int* flag = reinterpret_cast<int*>(lds);  // staging tile is dead now: reuse it for the broadcast
     if (tid == 0) {
-      int* ctr = p.counters + blockIdx.x;
+      int* ctr = p.counters + tile;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -408,12 +434,11 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int ntn = (p.N + BN - 1) / BN;
-  const int tile_n = blockIdx.x % ntn;
-  const int tile_m = blockIdx.x / ntn;
+  int tile_m, tile_n, split, tile;
+  block_coords(p, BM, BN, tile_m, tile_n, split, tile);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BK;
-  const int kt_begin = blockIdx.y * kt_per_split;
+  const int kt_begin = split * kt_per_split;
   const int kt_end = min(nk_total, kt_begin + kt_per_split);
   const int nk = kt_end - kt_begin;
 
@@ -536,7 +561,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
 }
 
 template <int BM, int BN, int STAGES>

@@ -13,6 +13,8 @@
 //  * stop() fails queued requests with an error instead of destroying their promises.
 #pragma once
 
+#include <sys/prctl.h>
+
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -84,7 +86,10 @@ class BatchProcessor {
 
   void start() {
     if (running_.exchange(true)) return;
-    thread_ = std::thread([this] { loop(); });
+    thread_ = std::thread([this] {
+      prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // paced dispatch: wake within ~1 us, not 50 us
+      loop();
+    });
   }
 
   void stop() {

@@ -162,6 +162,56 @@ def format_floats(v: np.ndarray) -> str:
 
 # ---- control plane ------------------------------------------------------------------------------
 
+def _cpulist(text: str) -> List[int]:
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _cgroup_quota() -> Optional[float]:
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        return None
+
+
+def bind_local_cpus(device: int = 0, ranks_per_node: int = 1) -> Dict[str, Any]:
+    """NUMA placement for one-process-per-GPU serving: restrict this process (and every thread it
+    creates afterwards: HTTP reactors, batcher, completion, client) to the CPUs local to its GPU's
+    PCIe root (sysfs local_cpulist), so request bodies, pinned staging and DMA stay on the GPU's
+    socket, and set DIE_CPUS to this rank's share of the node's CPU budget for thread-pool sizing.
+    Needs torch (device -> PCI address); a no-op where sysfs does not say."""
+    info: Dict[str, Any] = {"bound": False}
+    cur = sorted(os.sched_getaffinity(0))
+    quota = _cgroup_quota()
+    budget = min(len(cur), int(quota)) if quota else len(cur)
+    share = max(4, budget // max(1, ranks_per_node))
+    os.environ["DIE_CPUS"] = str(share)
+    info["cpu_share"] = share
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device)
+        bdf = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        local = _cpulist(open("/sys/bus/pci/devices/%s/local_cpulist" % bdf).read())
+    except Exception as e:  # no torch/sysfs: keep the inherited mask
+        info["reason"] = str(e)
+        return info
+    cpus = sorted(set(local) & set(cur))
+    info["pci"] = bdf
+    if len(cpus) < 8 or len(cpus) == len(cur):
+        info["reason"] = "local set %d of %d CPUs" % (len(cpus), len(cur))
+        return info
+    os.sched_setaffinity(0, cpus)
+    info.update(bound=True, cpus=len(cpus))
+    return info
+
+
 def pack_nibbles(text: bytes) -> Optional[bytes]:
     """4-bit packing of number-list text (core/textpack.h); None if a byte is outside the alphabet."""
     dst = C.create_string_buffer((len(text) + 1) // 2 + 1)

@@ -100,3 +100,25 @@ def test_tune_cache_roundtrip(native, models, tmp_path):
     assert np.isfinite(e2.run(x)).all()
     e2.close()
     print("engine init with tuning %.2fs, from cache %.2fs" % (t1 - t0, time.time() - t2 + (t2 - t1)))
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_branch_streams_bit_identical(native, models, graphs):
+    """Projection shortcuts on the side stream (hipGraph branches, or eager fork/join events) give
+    exactly the outputs of the in-line schedule (same heuristic kernel configs, no autotune), at
+    several buckets and across repeated runs (race screen)."""
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["get_rn50"]()
+    base = dict(device="hip", max_batch=32, use_graphs=graphs, autotune=False, tune_cache="")
+    a = native.Engine(path, branch_streams=True, **base)
+    b = native.Engine(path, branch_streams=False, **base)
+    assert a.refresh_info()["branch_streams"] is True and b.refresh_info()["branch_streams"] is False
+    for B in (1, 7, 24, 32):
+        x = r.synthetic_input(B, cfg, seed=B).reshape(B, -1)
+        ya = a.run(x)
+        for _ in range(3):
+            np.testing.assert_array_equal(ya, a.run(x))
+        np.testing.assert_array_equal(ya, b.run(x))
+    a.close()
+    b.close()
