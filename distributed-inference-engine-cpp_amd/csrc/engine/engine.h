@@ -181,6 +181,9 @@ struct EngineOptions {
   // default: measured slower (ResNet50 forward 0.79 vs 0.75 ms at batch 16, and the serving
   // headline -15%: the branch's queue competes with the copy streams), profiles/r1_branches_ab.md.
   bool branch_streams = false;
+  // Run the PREP part (decode-table fetch, device decode, input prep) on the compute stream right
+  // before MAIN instead of on the copy stream beside the previous batch's MAIN.
+  bool prep_on_compute = false;
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

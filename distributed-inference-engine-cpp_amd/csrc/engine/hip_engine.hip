@@ -91,6 +91,8 @@ class HipEngine : public Engine {
     for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
     // side-branch stream (plan ops with join >= 0): the fourth and last queue; only with one executor
     branches_ = opt.branch_streams && n_exec_ == 1;
+    prep_on_compute_ = opt.prep_on_compute;
+    if (const char* e = std::getenv("DIE_PREP_ON_COMPUTE")) prep_on_compute_ = std::atoi(e) != 0;
     if (branches_) {
       HIP_CHECK(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -485,13 +487,23 @@ class HipEngine : public Engine {
           used_staged = true;
         }
       if (used_staged) staged_used_.fetch_add(1, std::memory_order_relaxed);
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 6], ps));  // all input copies landed
+      if (prep_on_compute_) {
+        // PREP in line on the compute stream, after the previous MAIN: only the copies need lead
+        HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
+        HIP_CHECK(hipEventRecord(tev_[job.ev], cs));
+        HIP_CHECK(hipStreamWaitEvent(cs, sl.ev_prep, 0));
+        ps = cs;
+      }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 3], ps));
       if (!prep_graphs_.empty()) HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
       else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
       HIP_CHECK(hipEventRecord(tev_[job.ev + 4], ps));
-      HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
-      HIP_CHECK(hipEventRecord(tev_[job.ev], cs));
-      HIP_CHECK(hipStreamWaitEvent(cs, sl.ev_prep, 0));
+      if (!prep_on_compute_) {
+        HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
+        HIP_CHECK(hipEventRecord(tev_[job.ev], cs));
+        HIP_CHECK(hipStreamWaitEvent(cs, sl.ev_prep, 0));
+      }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 1], cs));
       if (!graphs_.empty()) {
         HIP_CHECK(hipGraphLaunch(graphs_[bi * depth_ + slot], cs));
@@ -599,6 +611,7 @@ class HipEngine : public Engine {
     j["pace"] = opt_.pace && n_exec_ == 1 && !comm_ && !graphs_.empty();
     j["pack_text"] = d_packed_ != nullptr;
     j["branch_streams"] = branches_;
+    j["prep_on_compute"] = prep_on_compute_;
     j["paced_batches"] = static_cast<long long>(paced_batches_.load());
     {
       std::lock_guard<std::mutex> g(pace_mu_);
@@ -1102,7 +1115,7 @@ class HipEngine : public Engine {
           float ms = 0;
           if (hipEventElapsedTime(&ms, tev_[job.ev + 1], tev_[job.ev + 2]) == hipSuccess) r.device_us = ms * 1000.0;
           float wait_ms = 0, gap_ms = 0;
-          if (hipEventElapsedTime(&wait_ms, tev_[job.ev], tev_[job.ev + 1]) == hipSuccess) copy_wait_ms_total_ = copy_wait_ms_total_.load() + wait_ms;
+          if (hipEventElapsedTime(&wait_ms, tev_[job.ev], tev_[job.ev + (prep_on_compute_ ? 3 : 1)]) == hipSuccess) copy_wait_ms_total_ = copy_wait_ms_total_.load() + wait_ms;
           if (prev_ev_ >= 0 && hipEventElapsedTime(&gap_ms, tev_[prev_ev_ + 2], tev_[job.ev]) == hipSuccess && gap_ms > 0)
             gpu_gap_ms_total_ = gpu_gap_ms_total_.load() + gap_ms;
           prev_ev_ = job.ev;
@@ -1112,7 +1125,9 @@ class HipEngine : public Engine {
             // that grows when MAIN had to wait for its input anyway (wait_ms: compute stream idle
             // behind the copies/prep) and shrinks slowly otherwise
             float in_ms = 0;
-            const bool have_in = hipEventElapsedTime(&in_ms, tev_[job.ev + 5], tev_[job.ev + 4]) == hipSuccess;
+            // (PREP in line on the compute stream: the lead covers the copies only)
+            const bool have_in =
+                hipEventElapsedTime(&in_ms, tev_[job.ev + 5], tev_[job.ev + (prep_on_compute_ ? 6 : 4)]) == hipSuccess;
             std::lock_guard<std::mutex> g(pace_mu_);
             double& e = est_ms_[job.bi];
             e = e > 0.0 ? 0.8 * e + 0.2 * ms : ms;
@@ -1214,6 +1229,7 @@ class HipEngine : public Engine {
   static constexpr int kMaxExec = 2;
   int n_exec_ = 1;
   bool branches_ = false;  // side-branch stream in use (PlanOp::join)
+  bool prep_on_compute_ = false;  // PREP runs on the compute stream before MAIN (EngineOptions)
   hipStream_t s_side_{};
   hipEvent_t ev_fork_{}, ev_join_{};
   float* ws_side_ = nullptr;
@@ -1246,8 +1262,8 @@ class HipEngine : public Engine {
   std::deque<Job> jobs_;
   int inflight_ = 0;
   // per job: [0] compute stream reaches the job, [1] MAIN start, [2] MAIN end, [3] PREP start,
-  // [4] PREP end, [5] first input copy issued
-  static constexpr int kTimingJobs = 16, kEvPerJob = 6;
+  // [4] PREP end, [5] first input copy issued, [6] input copies done
+  static constexpr int kTimingJobs = 16, kEvPerJob = 7;
   hipEvent_t tev_[kEvPerJob * kTimingJobs] = {};
   unsigned long long job_seq_ = 0;  // guarded by submit_mu_
   int prev_ev_ = -1;                // completion thread
