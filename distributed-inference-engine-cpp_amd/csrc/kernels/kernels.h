@@ -85,6 +85,10 @@ hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
                         int Ho, int Wo, int relu, hipStream_t s);
 
+// Evict the L2s: stream-read `bytes` (> 8 x 4 MiB) of a scratch buffer (autotuning in the cache
+// state a layer sees inside a forward: L2 cold, Infinity Cache warm).
+hipError_t l2_scrub(const void* buf, size_t bytes, float* sink, hipStream_t s);
+
 // dst[0..n) = src[0..n) in one small block (src may be host-coherent pinned memory).
 hipError_t copy_i64(const long long* src, long long* dst, int n, hipStream_t s);
 
