@@ -77,6 +77,7 @@ EngineOptions engine_opts(const Json& j) {
   e.pack_text = jget<bool>(j, "pack_text", e.pack_text);
   e.branch_streams = jget<bool>(j, "branch_streams", e.branch_streams);
   e.prep_on_compute = jget<bool>(j, "prep_on_compute", e.prep_on_compute);
+  e.live_batch = jget<bool>(j, "live_batch", e.live_batch);
   e.exec_streams = jget<int>(j, "exec_streams", e.exec_streams);
   e.tune_cache = jget<std::string>(j, "tune_cache", e.tune_cache);
   e.precision = jget<std::string>(j, "precision", e.precision);

@@ -124,9 +124,10 @@ class Engine {
   // hands it back with release_staged() after the batch that carried it completed (ran = true: the
   // copy is known to be done), or with ran = false when the request failed or was dropped before
   // its batch ran (the engine then waits for the copy); the pinned text must not change until then.
-  virtual long stage_text(const char* text, size_t len) {
+  virtual long stage_text(const char* text, size_t len, bool packed = false) {
     (void)text;
     (void)len;
+    (void)packed;
     return -1;
   }
   virtual void release_staged(long ticket, bool ran) {
@@ -184,6 +185,9 @@ struct EngineOptions {
   // Run the PREP part (decode-table fetch, device decode, input prep) on the compute stream right
   // before MAIN instead of on the copy stream beside the previous batch's MAIN.
   bool prep_on_compute = false;
+  // A batch runs the hipGraph of the smallest bucket >= B; with live_batch the kernels read B from
+  // the slot's table and skip the work of the bucket's padding samples.
+  bool live_batch = true;
   // Autotune results persist here across restarts (keyed by GPU arch + problem shape); "" = off,
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";

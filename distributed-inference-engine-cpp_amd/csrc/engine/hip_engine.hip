@@ -91,7 +91,12 @@ class HipEngine : public Engine {
     for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
     // side-branch stream (plan ops with join >= 0): the fourth and last queue; only with one executor
     branches_ = opt.branch_streams && n_exec_ == 1;
+    // the fourth queue: side branches, or a dedicated PREP stream when texts are uploaded early
+    if (!branches_ && n_exec_ == 1 && opt.device_decode && opt.stage_slots != 0 && !comm_)
+      HIP_CHECK(hipStreamCreateWithFlags(&s_prep_, hipStreamNonBlocking));
     prep_on_compute_ = opt.prep_on_compute;
+    use_live_ = opt.live_batch;
+    if (const char* e = std::getenv("DIE_LIVE_BATCH")) use_live_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("DIE_PREP_ON_COMPUTE")) prep_on_compute_ = std::atoi(e) != 0;
     if (branches_) {
       HIP_CHECK(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
@@ -112,11 +117,13 @@ class HipEngine : public Engine {
       n_stage_ = opt.stage_slots >= 0 ? opt.stage_slots : std::min(1024, std::max(256, 8 * max_batch_));
       if (comm_) n_stage_ = 0;
       HIP_CHECK(hipMalloc(&d_text_, text_cap_ * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
-      // 4-bit packed texts (BatchItem::packed) land here and are expanded into d_text_ by PREP
-      // (early upload, when asked for, stages raw text instead)
-      if (!comm_ && opt.pack_text && n_stage_ == 0) HIP_CHECK(hipMalloc(&d_packed_, text_cap_ / 2 * static_cast<size_t>(depth_) * max_batch_));
+      // 4-bit packed texts (BatchItem::packed; early-uploaded or copied at submit) land here, slot
+      // for slot like d_text_, and PREP expands them into d_text_
+      if (!comm_ && opt.pack_text)
+        HIP_CHECK(hipMalloc(&d_packed_, text_cap_ / 2 * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
       stage_ev_.resize(n_stage_);
       stage_seq_.assign(n_stage_, 0);
+      stage_packed_.assign(n_stage_, 0);
       stage_stream_.assign(n_stage_, 0);
       stage_state_.assign(n_stage_, kIssued);
       for (int t = 0; t < n_stage_; ++t) {
@@ -128,7 +135,7 @@ class HipEngine : public Engine {
     for (auto& sl : slots_) {
       if (text_cap_) HIP_CHECK(hipMalloc(&sl.d_scratch, kern::decode_scratch_bytes(max_batch_, text_cap_)));
       // [lens x max_batch][text offsets x max_batch][packed-text offsets x max_batch (-1 = raw)]
-      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * kTableRows * max_batch_));
+      HIP_CHECK(hipMalloc(&sl.d_lens, sizeof(long long) * table_len()));
       HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
       HIP_CHECK(hipMemset(sl.d_lens + max_batch_, 0, sizeof(long long) * max_batch_));
       HIP_CHECK(hipMemset(sl.d_lens + 2 * max_batch_, 0xFF, sizeof(long long) * max_batch_));
@@ -144,7 +151,7 @@ class HipEngine : public Engine {
         HIP_CHECK(hipEventCreateWithFlags(&sl.ev_gather, hipEventDisableTiming));
       }
       // host-coherent: the graph's first kernel reads it directly (see encode_forward)
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * kTableRows * max_batch_,
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_lens), sizeof(long long) * table_len(),
                               hipHostMallocCoherent | hipHostMallocMapped));
       HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.h_lens_dev), sl.h_lens, 0));
       for (int i = 0; i < max_batch_; ++i) {  // no text samples until a submit says otherwise
@@ -152,6 +159,8 @@ class HipEngine : public Engine {
         sl.h_lens[max_batch_ + i] = 0;
         sl.h_lens[2 * max_batch_ + i] = -1;
       }
+      sl.h_lens[live_index()] = max_batch_;  // live batch: every sample of the bucket until a submit
+      HIP_CHECK(hipMemcpy(sl.d_lens + live_index(), sl.h_lens + live_index(), sizeof(long long), hipMemcpyHostToDevice));
       HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_status), sizeof(int) * 2 * max_batch_, hipHostMallocDefault));
       HIP_CHECK(hipMalloc(&sl.d_in, sizeof(float) * in_numel_ * max_batch_));
       HIP_CHECK(hipMalloc(&sl.d_out, sizeof(float) * out_numel_ * max_batch_));
@@ -293,6 +302,7 @@ class HipEngine : public Engine {
       (void)hipFree(counterss_[e]);
       (void)hipStreamDestroy(s_exec_[e]);
     }
+    if (s_prep_) (void)hipStreamDestroy(s_prep_);
     if (branches_) {
       (void)hipFree(ws_side_);
       (void)hipFree(counters_side_);
@@ -320,8 +330,8 @@ class HipEngine : public Engine {
   // Early upload: reactor threads only queue the request; ONE stager thread issues every staged
   // copy (no HIP API traffic from the HTTP threads competing with the batcher's graph launches and
   // the completion thread's waits -- measured: issuing from 16 reactors cost ~15% throughput).
-  long stage_text(const char* text, size_t len) override {
-    if (!text_cap_ || n_stage_ == 0 || len == 0 || len > text_cap_) return -1;
+  long stage_text(const char* text, size_t len, bool packed) override {
+    if (!text_cap_ || n_stage_ == 0 || len == 0 || len > text_cap_ || (packed && !d_packed_)) return -1;
     int t;
     {
       std::lock_guard<std::mutex> g(stage_mu_);
@@ -329,7 +339,8 @@ class HipEngine : public Engine {
       t = stage_free_.back();
       stage_free_.pop_back();
       stage_state_[t] = kQueued;
-      stage_q_.push_back(StageReq{t, text, len});
+      stage_packed_[t] = packed;
+      stage_q_.push_back(StageReq{t, text, len, packed});
     }
     stage_cv_.notify_one();
     staged_total_.fetch_add(1, std::memory_order_relaxed);
@@ -403,7 +414,7 @@ class HipEngine : public Engine {
       Slot& sl = slots_[slot];
       job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
       job.bi = static_cast<int>(bucket_index(B));
-      HIP_CHECK(hipEventRecord(tev_[job.ev + 5], s_stage_[0]));  // input upload starts (pacing model)
+      HIP_CHECK(hipEventRecord(tev_[job.ev + 5], s_prep_ ? s_prep_ : s_stage_[0]));  // input path starts (pacing model)
       bool any_text = false;
       long long* h_offs = sl.h_lens + max_batch_;
       long long* h_poffs = sl.h_lens + 2 * max_batch_;
@@ -416,20 +427,7 @@ class HipEngine : public Engine {
         h_poffs[i] = -1;
         if (items[i].text) {
           if (!text_cap_ || items[i].text_len > text_cap_) throw std::runtime_error("input text exceeds device decode capacity");
-          if (items[i].packed) {
-            if (!d_packed_) throw std::runtime_error("engine does not take packed text");
-            const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
-            const size_t pidx = static_cast<size_t>(slot) * max_batch_ + i;
-            h_offs[i] = static_cast<long long>(idx * text_cap_);
-            h_poffs[i] = static_cast<long long>(pidx * (text_cap_ / 2));
-            const int si = rr++ % n_copy_streams_;
-            HIP_CHECK(hipMemcpyAsync(d_packed_ + pidx * (text_cap_ / 2), items[i].text, (items[i].text_len + 1) / 2,
-                                     hipMemcpyHostToDevice, s_stage_[si]));
-            copied[si] = true;
-            sl.h_lens[i] = static_cast<long long>(items[i].text_len);
-            any_text = true;
-            continue;
-          }
+          if (items[i].packed && !d_packed_) throw std::runtime_error("engine does not take packed text");
           const long t = items[i].staged;
           const auto tw0 = std::chrono::steady_clock::now();
           const bool issued = t >= 0 && t < n_stage_ && wait_staged(static_cast<int>(t)) == kIssued;
@@ -437,10 +435,19 @@ class HipEngine : public Engine {
             diag_submit_wait_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0).count();
             if (issued && hipEventQuery(stage_ev_[t]) != hipSuccess) diag_not_ready_++;
           }
-          if (issued) {
+          if (issued) {  // already uploaded (raw, or packed: PREP expands it into the stage slot)
             h_offs[i] = static_cast<long long>(t) * static_cast<long long>(text_cap_);
+            if (stage_packed_[t]) h_poffs[i] = static_cast<long long>(t) * static_cast<long long>(text_cap_ / 2);
             int& w = wait_ticket[stage_stream_[t]];
             if (w < 0 || stage_seq_[t] > stage_seq_[w]) w = static_cast<int>(t);
+          } else if (items[i].packed) {
+            const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
+            h_offs[i] = static_cast<long long>(idx * text_cap_);
+            h_poffs[i] = static_cast<long long>(idx * (text_cap_ / 2));
+            const int si = rr++ % n_copy_streams_;
+            HIP_CHECK(hipMemcpyAsync(d_packed_ + idx * (text_cap_ / 2), items[i].text, (items[i].text_len + 1) / 2,
+                                     hipMemcpyHostToDevice, s_stage_[si]));
+            copied[si] = true;
           } else {
             const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
             h_offs[i] = static_cast<long long>(idx * text_cap_);
@@ -461,6 +468,7 @@ class HipEngine : public Engine {
         if (n < in_numel_) HIP_CHECK(hipMemsetAsync(dst + n, 0, (in_numel_ - n) * sizeof(float), s_stage_[si]));
         copied[si] = true;
       }
+      sl.h_lens[live_index()] = use_live_ ? B : max_batch_;
       for (int i = B; i < max_batch_; ++i) {
         sl.h_lens[i] = -1;
         h_offs[i] = 0;
@@ -473,9 +481,11 @@ class HipEngine : public Engine {
       // stream 0 behind this batch's copies, overlapping the previous batch's MAIN on the compute
       // stream; MAIN waits for it.  Timing events come from a ring (a job's events outlive its slot's
       // reuse): pre = compute stream done with earlier work, fwd0/fwd1 around MAIN, p0/p1 around PREP.
-      hipStream_t ps = s_stage_[0];
+      // PREP runs on its own stream when there is one (early upload: the stager's copies for later
+      // batches must not queue behind this batch's decode on a copy stream), else on copy stream 0
+      hipStream_t ps = s_prep_ ? s_prep_ : s_stage_[0];
       hipStream_t cs = s_exec_[slot % n_exec_];
-      for (int si = 1; si < kStageStreams; ++si)
+      for (int si = s_prep_ ? 0 : 1; si < kStageStreams; ++si)
         if (copied[si]) {
           HIP_CHECK(hipEventRecord(sl.ev_h2d[si], s_stage_[si]));
           HIP_CHECK(hipStreamWaitEvent(ps, sl.ev_h2d[si], 0));
@@ -612,6 +622,7 @@ class HipEngine : public Engine {
     j["pack_text"] = d_packed_ != nullptr;
     j["branch_streams"] = branches_;
     j["prep_on_compute"] = prep_on_compute_;
+    j["live_batch"] = use_live_;
     j["paced_batches"] = static_cast<long long>(paced_batches_.load());
     {
       std::lock_guard<std::mutex> g(pace_mu_);
@@ -760,6 +771,7 @@ class HipEngine : public Engine {
     a.zeros = zeros_;
     a.counters = counterss_[s % n_exec_];
     a.counters_n = kCounters;
+    a.live = slots_[s].d_lens + live_index();
     return a;
   }
 
@@ -815,6 +827,7 @@ class HipEngine : public Engine {
         if (op.kind != PlanOp::CONV) continue;
         kern::ConvArgs base = conv_args(op, B, 0);
         base.ws = ws_;
+        base.live = nullptr;  // tune the whole bucket
         // identical problems (repeated blocks) share one measurement
         char key[256];
         std::snprintf(key, sizeof(key), "%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", base.M, base.N, base.K, base.Cin,
@@ -889,10 +902,14 @@ class HipEngine : public Engine {
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
     const size_t op_begin = part == MAIN ? n_prep_ops_ : 0;
     const size_t op_end = part == PREP ? n_prep_ops_ : plan_.ops.size();
+    if (part != MAIN) {  // the slot's table (live batch; decode lens/offsets) from host-coherent memory
+      const hipError_t ec = kern::copy_i64(slots_[s].h_lens_dev, slots_[s].d_lens, static_cast<int>(table_len()), st);
+      if (ec != hipSuccess) throw std::runtime_error("launch of table fetch failed: " + std::string(hipGetErrorString(ec)));
+    }
     if (text_cap_ && part != MAIN) {
       Slot& sl = slots_[s];
-      const hipError_t ec = kern::copy_i64(sl.h_lens_dev, sl.d_lens, kTableRows * max_batch_, st);
-      if (ec == hipSuccess && d_packed_) {
+      const hipError_t ec = hipSuccess;
+      if (d_packed_) {
         const hipError_t eu = kern::unpack_text_nibbles(d_packed_, sl.d_lens + 2 * max_batch_, d_text_,
                                                         sl.d_lens + max_batch_, sl.d_lens, B, st);
         if (eu != hipSuccess) throw std::runtime_error("launch of text unpack failed: " + std::string(hipGetErrorString(eu)));
@@ -905,6 +922,7 @@ class HipEngine : public Engine {
     }
     if (op_events) HIP_CHECK(hipEventRecord(op_events[0], st));
     const hipStream_t main_st = st;
+    const long long* live = use_live_ ? slots_[s].d_lens + live_index() : nullptr;
     int pending_join = -1;  // open side branch: the op that waits for it
     for (size_t op_index = op_begin; op_index < op_end; ++op_index) {
       const PlanOp& op = plan_.ops[op_index];
@@ -928,6 +946,7 @@ class HipEngine : public Engine {
           break;
         case PlanOp::CONV: {
           kern::ConvArgs a = conv_args(op, B, s);
+          if (!use_live_) a.live = nullptr;
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
           a.ws = side ? ws_side_ : wss_[s % n_exec_];
@@ -938,16 +957,16 @@ class HipEngine : public Engine {
         }
         case PlanOp::POOL:
           e = kern::pool2d(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
-                           op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st);
+                           op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st, live);
           break;
         case PlanOp::GAP:
           e = kern::global_avgpool(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st);
+                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live);
           break;
         case PlanOp::AFFINE:
           e = kern::affine_act(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
                                prm(op.scale_off), prm(op.shift_off), op.act, static_cast<uint16_t*>(buf(op.out)),
-                               op.rows_per_sample * B, op.C, st);
+                               op.rows_per_sample * B, op.C, st, live, op.rows_per_sample);
           break;
         case PlanOp::TO_NCHW_F32:
           e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
@@ -957,7 +976,7 @@ class HipEngine : public Engine {
           e = kern::conv_stem7x7(static_cast<const uint16_t*>(buf(op.in)),
                                  reinterpret_cast<const uint16_t*>(params_ + op.w_off), prm(op.bias_off),
                                  static_cast<uint16_t*>(buf(op.out)), B, op.conv.H, op.conv.W, op.conv.Ho, op.conv.Wo,
-                                 op.conv.relu, st);
+                                 op.conv.relu, st, live);
           break;
         case PlanOp::LAYERNORM:
           e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
@@ -1005,6 +1024,7 @@ class HipEngine : public Engine {
     size_t bi = 0;
     while (buckets_[bi] < B) ++bi;
     const int Bk = buckets_[bi];
+    slots_[0].h_lens[live_index()] = Bk;  // profile the whole bucket
     encode_forward(Bk, 0, s_compute_);  // warm
     for (int it = 0; it < iters; ++it) {
       encode_forward(Bk, 0, s_compute_, ev.data());
@@ -1082,6 +1102,7 @@ class HipEngine : public Engine {
     int t;
     const char* text;
     size_t len;
+    bool packed;  // 4-bit packed: (len + 1) / 2 bytes to d_packed_
   };
   static constexpr int kQueued = 0, kIssued = 1, kFailed = 2;
 
@@ -1108,8 +1129,10 @@ class HipEngine : public Engine {
       // two ~47 GB/s); per stream copies complete in issue order, which the sequence number records
       const int si = static_cast<int>(rr++ % n_copy_streams_);
       const auto ti0 = std::chrono::steady_clock::now();
-      const bool ok = hipMemcpyAsync(d_text_ + static_cast<size_t>(rq.t) * text_cap_, rq.text, rq.len,
-                                     hipMemcpyHostToDevice, s_stage_[si]) == hipSuccess &&
+      const bool ok = (rq.packed ? hipMemcpyAsync(d_packed_ + static_cast<size_t>(rq.t) * (text_cap_ / 2), rq.text,
+                                                  (rq.len + 1) / 2, hipMemcpyHostToDevice, s_stage_[si])
+                                 : hipMemcpyAsync(d_text_ + static_cast<size_t>(rq.t) * text_cap_, rq.text, rq.len,
+                                                  hipMemcpyHostToDevice, s_stage_[si])) == hipSuccess &&
                       hipEventRecord(stage_ev_[rq.t], s_stage_[si]) == hipSuccess;
       diag_issue_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ti0).count();
       {
@@ -1238,6 +1261,9 @@ class HipEngine : public Engine {
   unsigned char* d_text_ = nullptr;  // (n_stage_ + depth_ * max_batch_) x text_cap_
   unsigned char* d_packed_ = nullptr;  // depth_ * max_batch_ x text_cap_ / 2 (packed texts, copied at submit)
   static constexpr int kTableRows = 3;  // per-slot decode table: lens, text offsets, packed offsets
+  // ... followed by one element: the live batch (samples of the bucket that are real)
+  size_t table_len() const { return static_cast<size_t>(kTableRows) * max_batch_ + 1; }
+  size_t live_index() const { return static_cast<size_t>(kTableRows) * max_batch_; }
   int n_stage_ = 0;                  // early-upload slots (stage_text)
   hipStream_t s_stage_[kStageStreams] = {};
   int n_copy_streams_ = kStageStreams;  // copy streams in use (DIE_COPY_STREAMS, 1..kStageStreams)
@@ -1245,6 +1271,7 @@ class HipEngine : public Engine {
   std::vector<hipEvent_t> stage_ev_;
   std::vector<unsigned long long> stage_seq_;  // guarded by stage_mu_ (like the three below)
   std::vector<int> stage_stream_;
+  std::vector<char> stage_packed_;  // the ticket's text is 4-bit packed
   std::vector<int> stage_state_;
   std::vector<int> stage_free_;
   std::deque<StageReq> stage_q_;
@@ -1260,7 +1287,9 @@ class HipEngine : public Engine {
   int n_exec_ = 1;
   bool branches_ = false;  // side-branch stream in use (PlanOp::join)
   bool prep_on_compute_ = false;  // PREP runs on the compute stream before MAIN (EngineOptions)
+  bool use_live_ = true;          // skip the bucket's padding samples (EngineOptions::live_batch)
   hipStream_t s_side_{};
+  hipStream_t s_prep_{};  // PREP stream (early upload), else PREP shares copy stream 0
   hipEvent_t ev_fork_{}, ev_join_{};
   float* ws_side_ = nullptr;
   int* counters_side_ = nullptr;

@@ -92,16 +92,22 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
 // are ordered so the operand with more bytes is the one shared within an XCD: N-fastest (an
 // M-tile's activations read once per XCD, every XCD reads all weights) when weights are the
 // smaller operand (N <= M), M-fastest otherwise (stage-4 / FC shapes with M < N).
-__device__ __forceinline__ void block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
+// With a live batch (ConvArgs::live) only the tiles holding real samples get work: the first
+// live_tiles * S blocks (spread evenly over the XCDs) are remapped over them and the rest exit.
+// Returns false for a block without work.
+__device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
                                              int& tile) {
-  const int nwg = gridDim.x * gridDim.y;
+  const int S = gridDim.y;  // split-K slices
+  const int ntn = (p.N + BN - 1) / BN;
+  const int Ml = p.live ? min(p.M, static_cast<int>(*p.live) * p.Ho * p.Wo) : p.M;
+  const int ntm = (Ml + BM - 1) / BM;
+  const int nwg = min(static_cast<int>(gridDim.x * gridDim.y), ntm * ntn * S);
   const int b = blockIdx.x + blockIdx.y * gridDim.x;
+  if (b >= nwg) return false;
   const int q = nwg >> 3, r = nwg & 7, x = b & 7;
   const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-  const int S = gridDim.y;  // split-K slices
   tile = id / S;
   split = id - tile * S;
-  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   if (p.N <= p.M) {
     tile_m = tile / ntn;
     tile_n = tile - tile_m * ntn;
@@ -109,6 +115,7 @@ __device__ __forceinline__ void block_coords(const ConvArgs& p, int BM, int BN, 
     tile_n = tile / ntm;
     tile_m = tile - tile_n * ntm;
   }
+  return true;
 }
 
 template <int BM, int BN, int MODE, int VEC>
@@ -126,7 +133,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
   const int wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   int tile_m, tile_n, split, tile;
-  block_coords(p, BM, BN, tile_m, tile_n, split, tile);
+  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BK;
   const int kt_begin = split * kt_per_split;
@@ -435,7 +442,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const int wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   int tile_m, tile_n, split, tile;
-  block_coords(p, BM, BN, tile_m, tile_n, split, tile);
+  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BK;
   const int kt_begin = split * kt_per_split;

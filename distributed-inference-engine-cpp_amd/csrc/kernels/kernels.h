@@ -42,6 +42,10 @@ struct ConvArgs {
   // Zero page (device), >= Kpad + 64 bf16 elements: source of the LDS-DMA loads for padding pixels
   // and M-tail rows (a tail row reads a whole K row from it).
   const uint16_t* zeros = nullptr;
+  // Live batch (device scalar, nullable): a hipGraph captured for a batch bucket runs the batches
+  // that round up to it; only the first *live samples are real, so output tiles that hold padding
+  // samples only are skipped (their rows stay undefined; every op is per-sample).
+  const long long* live = nullptr;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),
@@ -64,16 +68,20 @@ hipError_t conv_igemm(const ConvArgs& a, int tile_cfg, hipStream_t s);
 // fp32 NCHW -> (x * scale[c] + shift[c]) -> bf16 NHWC with Cp >= C channels (pad channels = 0).
 hipError_t input_prep(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
                       int W, int Cp, hipStream_t s);
+// `live` (nullable device scalar, kernels below and ConvArgs::live): only the first *live of the B
+// samples are computed; the rest of the outputs are left as they are.
 // NHWC bf16 max / average pooling (C % 8 == 0).
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
-                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s);
+                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s,
+                  const long long* live = nullptr);
 // [B, HW, C] bf16 -> [B, C] (mean over HW), optional y = relu(x*scale+shift) before averaging;
 // writes bf16 `out` and/or f32 `out_f32`.
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
-                          int relu, int B, int HW, int C, hipStream_t s);
+                          int relu, int B, int HW, int C, hipStream_t s, const long long* live = nullptr);
 // Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional)
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
-                      uint16_t* y, long long M, int C, hipStream_t s);
+                      uint16_t* y, long long M, int C, hipStream_t s, const long long* live = nullptr,
+                      long long rows_per_sample = 0);
 // bf16 NHWC [B,H,W,C] -> f32 NCHW [B,C,H,W]
 hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s);
 // f32 -> bf16 / bf16 -> f32 copies
@@ -83,7 +91,7 @@ hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
 // 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:
 // w = [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8), out = act(conv + bias) NHWC bf16.
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
-                        int Ho, int Wo, int relu, hipStream_t s);
+                        int Ho, int Wo, int relu, hipStream_t s, const long long* live = nullptr);
 
 // Evict the L2s: stream-read `bytes` (> 8 x 4 MiB) of a scratch buffer (autotuning in the cache
 // state a layer sees inside a forward: L2 cold, Infinity Cache warm).

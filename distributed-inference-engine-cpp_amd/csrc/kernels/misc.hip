@@ -58,7 +58,9 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
 
 // One thread per (output pixel, 8-channel group).
 __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
-                              int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int cip) {
+                              int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int cip,
+                              const long long* __restrict__ live) {
+  if (live) B = min(B, static_cast<int>(*live));
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * Ho * Wo * CG;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
@@ -99,9 +101,11 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
 
 // Grid: (C/8 groups / 64, B) blocks of 256 threads = 64 channel groups x 4 row-slices.
 __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
-                           const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C) {
+                           const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
+                           const long long* __restrict__ live) {
   __shared__ float part[4][64][8];
   const int b = blockIdx.y;
+  if (live && b >= *live) return;  // whole block: before any barrier
   const int g = blockIdx.x * 64 + (threadIdx.x & 63);
   const int slice = threadIdx.x >> 6;
   const int CG = C / 8;
@@ -145,7 +149,9 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
 // act: 0 none, 1 relu.  One thread per 8 elements of a row of C (C % 8 == 0).
 __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ z,
                                   const float* __restrict__ scale, const float* __restrict__ shift, int act,
-                                  uint16_t* __restrict__ y, long long M, int C) {
+                                  uint16_t* __restrict__ y, long long M, int C, const long long* __restrict__ live,
+                                  long long rows_per_sample) {
+  if (live) M = min(M, *live * rows_per_sample);
   const int CG = C / 8;
   const long long total = M * CG;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
@@ -210,28 +216,29 @@ hipError_t input_prep(const float* x, const float* scale, const float* shift, ui
 }
 
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
-                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s) {
+                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s, const long long* live) {
   if (C % 8) return hipErrorInvalidValue;
   const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(pool2d_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, kh, kw, sh, sw,
-                     ph, pw, is_max, count_include_pad);
+                     ph, pw, is_max, count_include_pad, live);
   return hipGetLastError();
 }
 
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
-                          int relu, int B, int HW, int C, hipStream_t s) {
+                          int relu, int B, int HW, int C, hipStream_t s, const long long* live) {
   if (C % 8) return hipErrorInvalidValue;
   const int CG = C / 8;
   dim3 grid((CG + 63) / 64, B);
-  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C);
+  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live);
   return hipGetLastError();
 }
 
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
-                      uint16_t* y, long long M, int C, hipStream_t s) {
+                      uint16_t* y, long long M, int C, hipStream_t s, const long long* live, long long rows_per_sample) {
   if (C % 8) return hipErrorInvalidValue;
+  if (live && rows_per_sample <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(M * (C / 8))), dim3(256), 0, s, x, z, scale, shift, act, y, M,
-                     C);
+                     C, live, rows_per_sample);
   return hipGetLastError();
 }
 

@@ -29,11 +29,13 @@ constexpr int NCH = 64;
 
 __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
-                                                      int H, int W, int Ho, int Wo, int relu, int tiles_x) {
+                                                      int H, int W, int Ho, int Wo, int relu, int tiles_x,
+                                                      const long long* __restrict__ live) {
   __shared__ __attribute__((aligned(16))) uint16_t wl[NCH * WP];
   __shared__ __attribute__((aligned(16))) uint16_t patch[PY * PX * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.y;
+  if (live && b >= *live) return;  // padding sample of the bucket: whole block, before any barrier
   const int ty0 = (blockIdx.x / tiles_x) * TY, tx0 = (blockIdx.x % tiles_x) * TX;
   // weights -> LDS (64 x 224 bf16 = 28 chunks of 16 B per row)
   for (int i = tid; i < NCH * (KS / 8); i += 256) {
@@ -109,11 +111,11 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
 static_assert(TY * TX * NCH <= NCH * WP, "output stage must fit in the weight buffer");
 
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
-                        int Ho, int Wo, int relu, hipStream_t s) {
+                        int Ho, int Wo, int relu, hipStream_t s, const long long* live) {
   if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1) return hipErrorInvalidValue;
   const int tiles_x = (Wo + TX - 1) / TX, tiles_y = (Ho + TY - 1) / TY;
   hipLaunchKernelGGL(stem7x7_kernel, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho, Wo, relu,
-                     tiles_x);
+                     tiles_x, live);
   return hipGetLastError();
 }
 

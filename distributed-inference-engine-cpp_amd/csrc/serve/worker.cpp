@@ -247,7 +247,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     device_decoded_.fetch_add(1, std::memory_order_relaxed);
     // start the H2D of this request's text now: by the time its batch is dispatched the bytes are
     // on the device and the batch waits only for the GPU
-    if (!packed) staged = eng.stage_text(reinterpret_cast<const char*>(sink.buf.data), text_len);
+    staged = eng.stage_text(reinterpret_cast<const char*>(sink.buf.data), text_len, packed);
   }
   const auto t_queued = std::chrono::steady_clock::now();
   h_parse_.add(t_queued - t_start);

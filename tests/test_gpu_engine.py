@@ -122,3 +122,28 @@ def test_branch_streams_bit_identical(native, models, graphs):
         np.testing.assert_array_equal(ya, b.run(x))
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("arch", ["resnet", "vit"])
+def test_live_batch_skips_padding_exactly(native, models, arch):
+    """A batch runs its bucket's graph; with live_batch the kernels skip the padding samples.  The
+    real rows must be bit-identical to computing the whole bucket (same kernel configs)."""
+    if arch == "resnet":
+        from die_amd.models import resnet_v2 as r
+
+        path, w, cfg = models["get_rn50"]()
+    else:
+        from die_amd.models import vit as r
+
+        path, w, cfg = models["get_vit"]("tiny")
+    base = dict(device="hip", max_batch=32, autotune=False, tune_cache="")
+    a = native.Engine(path, live_batch=True, **base)
+    b = native.Engine(path, live_batch=False, **base)
+    assert a.refresh_info()["live_batch"] is True and b.refresh_info()["live_batch"] is False
+    for B in (3, 5, 13, 17, 23, 29, 32):
+        x = r.synthetic_input(B, cfg, seed=100 + B).reshape(B, -1)
+        ya = a.run(x)
+        np.testing.assert_array_equal(ya, b.run(x))
+        assert np.isfinite(ya).all()
+    a.close()
+    b.close()
