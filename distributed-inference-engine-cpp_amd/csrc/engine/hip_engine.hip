@@ -96,6 +96,7 @@ class HipEngine : public Engine {
       HIP_CHECK(hipStreamCreateWithFlags(&s_prep_, hipStreamNonBlocking));
     prep_on_compute_ = opt.prep_on_compute;
     use_live_ = opt.live_batch;
+    if (const char* e = std::getenv("DIE_PACE_LEAD_SCALE")) lead_scale_ = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("DIE_LIVE_BATCH")) use_live_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("DIE_PREP_ON_COMPUTE")) prep_on_compute_ = std::atoi(e) != 0;
     if (branches_) {
@@ -575,11 +576,12 @@ class HipEngine : public Engine {
       ev = last_ev_;
       bi = last_bi_;
     }
-    double est, lead;
+    double est, lead, in_ms;
     {
       std::lock_guard<std::mutex> g(pace_mu_);
       est = est_ms_[bi];
       lead = lead_ms_;
+      in_ms = input_ms_;
     }
     if (est <= 0.0 || est <= lead) return now;
     (void)hipSetDevice(dev_);
@@ -592,7 +594,7 @@ class HipEngine : public Engine {
     if (q != hipSuccess || hipEventQuery(tev_[ev + 2]) != hipErrorNotReady) return clk::now();  // k drained
     const auto t0 = clk::now();
     const auto drain = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double, std::milli>(est));
-    const auto t = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double, std::milli>(est - lead));
+    const auto t = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double, std::milli>(est - (lead_scale_ == 1.0 ? lead : in_ms * lead_scale_)));
     {
       std::lock_guard<std::mutex> g(pace_mu_);
       pace_drain_ = drain;
@@ -957,7 +959,8 @@ class HipEngine : public Engine {
         }
         case PlanOp::POOL:
           e = kern::pool2d(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
-                           op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st, live);
+                           op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st, live,
+                           prm(op.scale_off), prm(op.shift_off), op.act);
           break;
         case PlanOp::GAP:
           e = kern::global_avgpool(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
@@ -1288,6 +1291,7 @@ class HipEngine : public Engine {
   bool branches_ = false;  // side-branch stream in use (PlanOp::join)
   bool prep_on_compute_ = false;  // PREP runs on the compute stream before MAIN (EngineOptions)
   bool use_live_ = true;          // skip the bucket's padding samples (EngineOptions::live_batch)
+  double lead_scale_ = 1.0;       // DIE_PACE_LEAD_SCALE (< 1: dispatch later, trading GPU idle for batch size)
   hipStream_t s_side_{};
   hipStream_t s_prep_{};  // PREP stream (early upload), else PREP shares copy stream 0
   hipEvent_t ev_fork_{}, ev_join_{};

@@ -95,6 +95,7 @@ class Planner {
       lower(static_cast<int>(i));
     }
     finalize_output();
+    fuse_pool_affine();
     mark_side_branches();
     assign_arena();
     return std::move(plan_);
@@ -1180,6 +1181,34 @@ class Planner {
     }
     plan_.output_numel = 1;
     for (auto dim : plan_.output_shape) plan_.output_numel *= static_cast<size_t>(dim);
+  }
+
+  // Pool -> BN(+ReLU) where the pooled value has no other reader (ResNet-v2: the stem's max pool
+  // feeds only stage 1's pre-activation BN, the first unit having a projection shortcut): the pool
+  // kernel applies the per-channel affine and activation before its single store.
+  void fuse_pool_affine() {
+    std::vector<int> readers(plan_.bufs.size(), 0);
+    for (const PlanOp& p : plan_.ops)
+      for (int b : {p.in, p.in2, p.in3})
+        if (b >= 0) readers[b]++;
+    std::vector<PlanOp> out;
+    out.reserve(plan_.ops.size());
+    for (size_t i = 0; i < plan_.ops.size(); ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind == PlanOp::AFFINE && p.in2 < 0 && p.in >= 0 && readers[p.in] == 1 && !out.empty() &&
+          out.back().kind == PlanOp::POOL && out.back().out == p.in && out.back().scale_off == SIZE_MAX &&
+          out.back().act == 0 && p.rows_per_sample == static_cast<long long>(out.back().Ho) * out.back().Wo) {
+        PlanOp& pool = out.back();
+        pool.scale_off = p.scale_off;
+        pool.shift_off = p.shift_off;
+        pool.act = p.act;
+        pool.out = p.out;
+        pool.name += "+" + p.name;
+        continue;
+      }
+      out.push_back(std::move(p));
+    }
+    plan_.ops = std::move(out);
   }
 
   // Branch concurrency: a conv whose output is first consumed two or more ops later (ResNet's

@@ -73,7 +73,8 @@ hipError_t input_prep(const float* x, const float* scale, const float* shift, ui
 // NHWC bf16 max / average pooling (C % 8 == 0).
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
                   int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s,
-                  const long long* live = nullptr);
+                  const long long* live = nullptr, const float* scale = nullptr, const float* shift = nullptr,
+                  int act = 0);
 // [B, HW, C] bf16 -> [B, C] (mean over HW), optional y = relu(x*scale+shift) before averaging;
 // writes bf16 `out` and/or f32 `out_f32`.
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,

@@ -59,7 +59,8 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
 // One thread per (output pixel, 8-channel group).
 __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
                               int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int cip,
-                              const long long* __restrict__ live) {
+                              const long long* __restrict__ live, const float* __restrict__ scale,
+                              const float* __restrict__ shift, int act) {
   if (live) B = min(B, static_cast<int>(*live));
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * Ho * Wo * CG;
@@ -94,6 +95,18 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
       const float inv = cnt ? 1.f / cnt : 0.f;
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] *= inv;
+    }
+    if (scale) {  // fused per-channel affine (+ ReLU) on the pooled value
+      const float4 s0 = *reinterpret_cast<const float4*>(scale + cg * 8), s1 = *reinterpret_cast<const float4*>(scale + cg * 8 + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(shift + cg * 8), h1 = *reinterpret_cast<const float4*>(shift + cg * 8 + 4);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = acc[t] * sc[t] + sf[t];
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = fmaxf(acc[t], 0.f);
     }
     store8(y + i * 8, acc);
   }
@@ -216,11 +229,12 @@ hipError_t input_prep(const float* x, const float* scale, const float* shift, ui
 }
 
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
-                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s, const long long* live) {
+                  int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s, const long long* live,
+                  const float* scale, const float* shift, int act) {
   if (C % 8) return hipErrorInvalidValue;
   const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(pool2d_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, kh, kw, sh, sw,
-                     ph, pw, is_max, count_include_pad, live);
+                     ph, pw, is_max, count_include_pad, live, scale, shift, act);
   return hipGetLastError();
 }
 
