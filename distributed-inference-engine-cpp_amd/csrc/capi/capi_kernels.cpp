@@ -145,9 +145,9 @@ int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, in
 }
 
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
-char* die_plan_summary(const char* model_path, int max_batch, char** err) {
+char* die_plan_summary(const char* model_path, int max_batch, int side_branches, char** err) {
   try {
-    Plan p = build_plan(onnx::load_onnx(model_path), max_batch);
+    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -181,6 +181,7 @@ char* die_plan_summary(const char* model_path, int max_batch, char** err) {
         e["relu"] = o.conv.relu;
         e["residual"] = o.in2 >= 0;
         e["dual_store"] = o.out2 >= 0;
+        e["preact_on_load"] = o.in_scale_off != SIZE_MAX;
         e["store_main"] = o.out >= 0 || o.out_f32 != -1;
         e["relu2"] = o.conv.relu2;
         e["act"] = o.conv.relu;

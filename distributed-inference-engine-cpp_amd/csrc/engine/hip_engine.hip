@@ -59,7 +59,7 @@ class HipEngine : public Engine {
     max_batch_ = std::max(1, opt.max_batch);
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     onnx::Model model = onnx::load_onnx(path);
-    plan_ = build_plan(model, max_batch_);
+    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1);
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
       ++n_prep_ops_;
@@ -774,6 +774,9 @@ class HipEngine : public Engine {
     a.counters = counterss_[s % n_exec_];
     a.counters_n = kCounters;
     a.live = slots_[s].d_lens + live_index();
+    a.in_scale = prm_ptr(op.in_scale_off);
+    a.in_shift = prm_ptr(op.in_shift_off);
+    a.in_relu = op.in_relu;
     return a;
   }
 

@@ -67,7 +67,8 @@ struct Val {
 
 class Planner {
  public:
-  Planner(const onnx::Model& m, int max_batch) : m_(m), max_batch_(max_batch) {}
+  Planner(const onnx::Model& m, int max_batch, bool side_branches)
+      : m_(m), max_batch_(max_batch), side_branches_(side_branches) {}
 
   Plan run() {
     if (m_.inputs.empty() || m_.outputs.empty()) throw std::runtime_error("model needs an input and an output");
@@ -96,7 +97,8 @@ class Planner {
     }
     finalize_output();
     fuse_pool_affine();
-    mark_side_branches();
+    if (std::getenv("DIE_BN_ON_LOAD")) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
+    if (side_branches_) mark_side_branches();
     assign_arena();
     return std::move(plan_);
   }
@@ -1211,6 +1213,42 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
+  // Pre-activation on load (opt-in, DIE_BN_ON_LOAD=1).  A dual-store conv writes x (the raw sum: next residual) AND
+  // a = act(bn(x)) (the next unit's input).  When every reader of `a` is a 1x1 conv the LDS-DMA
+  // loop can run (K = Cin <= 2048, Cin % 64 == 0), those convs read x and apply bn+act to their
+  // operand fragments instead, and the producer stores x only: one activation-sized write and
+  // read fewer per unit (ResNet-v2 expand convs are store-bound).
+  void preact_on_load() {
+    const int nops = static_cast<int>(plan_.ops.size());
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind != PlanOp::CONV || p.out < 0 || p.out2 < 0 || p.s2_off == SIZE_MAX) continue;
+      std::vector<int> readers;
+      bool ok = true;
+      for (int k = 0; k < nops && ok; ++k) {
+        if (k == i) continue;
+        const PlanOp& q = plan_.ops[k];
+        if (q.in2 == p.out2 || q.in3 == p.out2 || q.out == p.out2 || q.out2 == p.out2) ok = false;
+        if (q.in != p.out2) continue;
+        const kern::ConvArgs& c = q.conv;
+        ok = q.kind == PlanOp::CONV && c.KH == 1 && c.KW == 1 && c.pad_h == 0 && c.pad_w == 0 && c.K == c.Cin &&
+             c.Cin % 64 == 0 && c.K <= 2048 && q.in_scale_off == SIZE_MAX;
+        readers.push_back(k);
+      }
+      if (!ok || readers.empty()) continue;
+      for (int k : readers) {
+        PlanOp& q = plan_.ops[k];
+        q.in = p.out;
+        q.in_scale_off = p.s2_off;
+        q.in_shift_off = p.b2_off;
+        q.in_relu = p.conv.relu2;
+      }
+      p.out2 = -1;
+      p.s2_off = p.b2_off = SIZE_MAX;
+      p.conv.relu2 = 0;
+    }
+  }
+
   // Branch concurrency: a conv whose output is first consumed two or more ops later (ResNet's
   // projection shortcut: consumed as the residual of the unit's expand conv, after the reduce and
   // 3x3 convs) is independent of the ops in between.  At serving batch sizes every one of those
@@ -1247,33 +1285,37 @@ class Planner {
         for (int b : {p.in, p.in2, p.in3})
           if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, p.join);
     }
-    struct Block {
+    // Offsets: greedy by size (largest first, each at the lowest offset that does not overlap an
+    // already placed buffer whose lifetime intersects its own) -- for ResNet50 this packs the
+    // arena ~1.5x tighter than first-fit in program order, which keeps activations + weights inside
+    // the 256 MiB Infinity Cache.
+    std::vector<int> order;
+    for (size_t i = 0; i < plan_.bufs.size(); ++i)
+      if (plan_.bufs[i].first_use >= 0 || plan_.bufs[i].last_use >= 0) order.push_back(static_cast<int>(i));
+    auto bytes_of = [&](int bi) { return round_up(plan_.bufs[bi].bytes_per_sample * max_batch_, 256); };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bytes_of(a) > bytes_of(b); });
+    struct Placed {
       size_t off, size;
-      int last;
+      int first, last;
     };
-    std::vector<Block> live;
+    std::vector<Placed> placed;
     size_t top = 0;
-    std::vector<int> order(plan_.bufs.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<int>(i);
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return plan_.bufs[a].first_use < plan_.bufs[b].first_use; });
     for (int bi : order) {
       PlanBuf& b = plan_.bufs[bi];
-      const size_t size = round_up(b.bytes_per_sample * max_batch_, 256);
-      live.erase(std::remove_if(live.begin(), live.end(), [&](const Block& k) { return k.last < b.first_use; }),
-                 live.end());
-      std::sort(live.begin(), live.end(), [](const Block& a, const Block& c) { return a.off < c.off; });
+      const size_t size = bytes_of(bi);
+      const int first = b.first_use < 0 ? 0 : b.first_use;
+      const int last = std::max(b.last_use, first);
+      std::vector<std::pair<size_t, size_t>> busy;  // ranges of lifetime-overlapping buffers
+      for (const Placed& q : placed)
+        if (q.first <= last && first <= q.last) busy.emplace_back(q.off, q.off + q.size);
+      std::sort(busy.begin(), busy.end());
       size_t cand = 0;
-      bool placed = false;
-      for (const Block& k : live) {
-        if (k.off >= cand + size) {
-          placed = true;
-          break;
-        }
-        cand = std::max(cand, k.off + k.size);
+      for (const auto& r : busy) {
+        if (r.first >= cand + size) break;
+        cand = std::max(cand, r.second);
       }
-      (void)placed;
       b.offset = cand;
-      live.push_back(Block{cand, size, b.last_use});
+      placed.push_back(Placed{cand, size, first, last});
       top = std::max(top, cand + size);
     }
     plan_.arena_bytes = top;
@@ -1284,6 +1326,7 @@ class Planner {
 
   const onnx::Model& m_;
   int max_batch_;
+  bool side_branches_ = false;
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -1304,6 +1347,8 @@ std::string Plan::summary() const {
   return os.str();
 }
 
-Plan build_plan(const onnx::Model& m, int max_batch) { return Planner(m, max_batch).run(); }
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches) {
+  return Planner(m, max_batch, side_branches).run();
+}
 
 }  // namespace die

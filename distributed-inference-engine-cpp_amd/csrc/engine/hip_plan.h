@@ -61,6 +61,9 @@ struct PlanOp {
   // Side branch: this op may run on a second stream, concurrently with the ops after it, until
   // op `join` (its first consumer) waits for it.  The arena keeps its inputs live until `join`.
   int join = -1;
+  // CONV: pre-activation on load (ConvArgs::in_scale/in_shift/in_relu), parameter offsets
+  size_t in_scale_off = SIZE_MAX, in_shift_off = SIZE_MAX;
+  int in_relu = 0;
 };
 
 struct Plan {
@@ -76,7 +79,8 @@ struct Plan {
   std::string summary() const;
 };
 
-// Build the plan for batches up to max_batch.  Throws on unsupported graphs.
-Plan build_plan(const onnx::Model& m, int max_batch);
+// Build the plan for batches up to max_batch.  Throws on unsupported graphs.  side_branches: mark
+// independent convs to run on a second stream (PlanOp::join; extends their inputs' lifetimes).
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false);
 
 }  // namespace die

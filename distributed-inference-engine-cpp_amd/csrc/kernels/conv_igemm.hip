@@ -428,7 +428,27 @@ __device__ __forceinline__ void glds16(const uint16_t* g, uint16_t* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <int BM, int BN, int MODE, int STAGES>
+// 8 bf16 (one MFMA operand fragment, 8 consecutive channels) -> act(v * s + h), re-rounded to bf16.
+__device__ __forceinline__ bf16x8 bn_act8(bf16x8 f, float4 s0, float4 s1, float4 h0, float4 h1, int relu) {
+  const uint4 q = __builtin_bit_cast(uint4, f);
+  float v[8];
+  unpack2(q.x, v[0], v[1]);
+  unpack2(q.y, v[2], v[3]);
+  unpack2(q.z, v[4], v[5]);
+  unpack2(q.w, v[6], v[7]);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    v[t] = fmaf(v[t], sc[t], sh[t]);
+    if (relu) v[t] = fmaxf(v[t], 0.f);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])));
+}
+
+constexpr int kBnlMaxK = 2048;  // pre-activation on load: channels staged in LDS
+
+template <int BM, int BN, int MODE, int STAGES, bool BNL = false>
 __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -448,6 +468,15 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const int kt_begin = split * kt_per_split;
   const int kt_end = min(nk_total, kt_begin + kt_per_split);
   const int nk = kt_end - kt_begin;
+  // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
+  __shared__ __attribute__((aligned(16))) float bnl[BNL ? 2 * kBnlMaxK : 4];
+  if constexpr (BNL) {
+    for (int i = tid; i < nk * BK; i += 256) {
+      bnl[i] = p.in_scale[kt_begin * BK + i];
+      bnl[kBnlMaxK + i] = p.in_shift[kt_begin * BK + i];
+    }
+    // visible to every wave after the main loop's first barrier
+  }
 
   // Per-lane DMA sources.  Wave `wave` fills rows [wave*R/4, (wave+1)*R/4) of each operand, 8 rows
   // per instruction; lane L -> row (L>>3) of that group, physical chunk L&7.
@@ -559,6 +588,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 #pragma unroll
       for (int j = 0; j < TM; ++j)
         bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+      if constexpr (BNL) {
+        const float* sc = bnl + t * BK + chunk * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sc + kBnlMaxK);
+        const float4 h1 = *reinterpret_cast<const float4*>(sc + kBnlMaxK + 4);
+#pragma unroll
+        for (int j = 0; j < TM; ++j) bfr[j] = bn_act8(bfr[j], s0, s1, h0, h1, p.in_relu);
+      }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -573,8 +610,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 
 template <int BM, int BN, int STAGES>
 void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
-  if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES>), grid, dim3(256), 0, s, b, kt_per);
-  else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+  if (b.in_scale) {
+    if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
+  } else if (mode0) {
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+  } else {
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+  }
 }
 
 template <int BM, int BN>
@@ -593,12 +636,18 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
   if (!fused) b.counters = nullptr;
   dim3 grid(tiles, eff);
+  if (a.in_scale) {  // pre-activation on load: 1x1 convs in the LDS-DMA loop only
+    if (a.KH != 1 || a.KW != 1 || a.pad_h || a.pad_w || a.K != a.Cin || a.K > kBnlMaxK || a.Cin % BK || !a.in_shift)
+      return hipErrorInvalidValue;
+    if (variant == 0) variant = 1;  // the register-staged loop has no pre-activation: 2-stage ring
+  }
   if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
     if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
     // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS)
     constexpr int kStageBytes = (BM + BN) * BK * 2;
+    if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
     switch (variant) {
       case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
       case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;

@@ -46,6 +46,12 @@ struct ConvArgs {
   // that round up to it; only the first *live samples are real, so output tiles that hold padding
   // samples only are skipped (their rows stay undefined; every op is per-sample).
   const long long* live = nullptr;
+  // Pre-activation on load (1x1 convs, K = Cin <= 2048, LDS-DMA loop): the input operand is
+  // act(x * in_scale[c] + in_shift[c]) of the stored x (ResNet-v2's BN+ReLU of the unit input is
+  // applied here instead of being stored a second time by the producing conv).
+  const float* in_scale = nullptr;
+  const float* in_shift = nullptr;
+  int in_relu = 0;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),

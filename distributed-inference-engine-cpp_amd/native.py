@@ -547,7 +547,7 @@ def _sig_kernels():
         return L
     u64, i = C.c_uint64, C.c_int
     L.die_plan_summary.restype = C.c_void_p
-    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.die_kern_conv.restype = i
     L.die_kern_conv.argtypes = [C.c_char_p] + [u64] * 9 + [i, u64]
     L.die_kern_input_prep.restype = i
@@ -578,10 +578,10 @@ def _sig_kernels():
     return L
 
 
-def plan_summary(model_path: str, max_batch: int = 32) -> Dict[str, Any]:
+def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False) -> Dict[str, Any]:
     L = _sig_kernels()
     err = _err_box()
-    p = L.die_plan_summary(model_path.encode(), max_batch, C.byref(err))
+    p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), C.byref(err))
     if not p:
         _raise_if(err, "plan")
     return json.loads(_take_str(p))

@@ -29,7 +29,7 @@ def _check_branches(plan):
 
 def test_resnet50_projection_shortcuts_are_branches(native, models):
     path, _, _ = models["get_rn50"]()
-    plan = native.plan_summary(path, 32)
+    plan = native.plan_summary(path, 32, side_branches=True)
     branches = _check_branches(plan)
     names = [plan["ops"][i]["name"] for i, _ in branches]
     assert len(branches) == 4, names  # one projection conv per stage
@@ -40,9 +40,14 @@ def test_resnet50_projection_shortcuts_are_branches(native, models):
 @pytest.mark.parametrize("B", [1, 8])
 def test_tiny_resnet_branches_safe(native, models, B):
     path, _, _ = models["tiny"]
-    _check_branches(native.plan_summary(path, B))
+    _check_branches(native.plan_summary(path, B, side_branches=True))
 
 
 def test_vit_plan_branches_safe(native, models):
     path, _, _ = models["get_vit"]("tiny")
-    _check_branches(native.plan_summary(path, 4))
+    _check_branches(native.plan_summary(path, 4, side_branches=True))
+
+
+def test_no_branches_unless_asked(native, models):
+    path, _, _ = models["get_rn50"]()
+    assert all(o["join"] < 0 for o in native.plan_summary(path, 32)["ops"])
