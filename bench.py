@@ -59,7 +59,15 @@ def main():
                     help="upload input text as-is instead of 4-bit packed (device decode)")
     ap.add_argument("--no-device-decode", action="store_true",
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
+    ap.add_argument("--device", choices=["hip", "cpu"], default="hip",
+                    help="cpu: rehearse the multi-rank contract on the host executor (tests; no GPU)")
     args = ap.parse_args()
+
+    # rank 0's stdout carries exactly ONE JSON line: library chatter written to fd 1 while the
+    # job runs (RCCL's version banner at communicator init, ROCm runtime notes) goes to stderr.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch  # first: one HIP runtime per process (see native.lib)
 
@@ -73,10 +81,13 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
+    hip = args.device == "hip"
+
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        if hip:
+            torch.cuda.synchronize()
 
     import die_amd  # noqa: F401
     from die_amd import native
@@ -98,11 +109,15 @@ def main():
         blob, _ = r.build_onnx(cfg)
         with open(model, "wb") as f:
             f.write(blob)
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; ranks wrap onto the visible GPUs (a 1-GPU box can rehearse N=2 in
+    # http mode: two independent replicas on one card; RCCL dp mode needs distinct GPUs)
+    dev = local_rank % max(1, torch.cuda.device_count()) if hip else 0
+    if hip:
+        torch.cuda.set_device(dev)
     numa = {"bound": False}
-    if not args.no_numa:
-        # one process per GPU: this rank's threads and host buffers on its GPU's socket
-        numa = native.bind_local_cpus(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    if hip and not args.no_numa:
+        # this rank's threads and host buffers on its GPU's socket
+        numa = native.bind_local_cpus(dev, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     B = args.batch
     numel = cfg.in_ch * cfg.image * cfg.image
     extra = {}
@@ -110,7 +125,7 @@ def main():
     if args.mode == "http":
         t_init = time.perf_counter()
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
-                           engine={"device": "hip", "device_id": local_rank, "max_batch": B,
+                           engine={"device": args.device, "device_id": dev, "max_batch": B,
                                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
@@ -156,7 +171,7 @@ def main():
         # rank 0 serves HTTP and drives the load, ranks >= 1 are DP followers on their own GPU.
         group = "die_bench_dp_%s" % os.environ.get("MASTER_PORT", str(os.getpid()))
         Btot = B * world
-        eng_opts = {"device": "hip", "device_id": local_rank, "pipeline_depth": args.pipeline_depth,
+        eng_opts = {"device": args.device, "device_id": dev, "pipeline_depth": args.pipeline_depth,
                     "device_decode": not args.no_device_decode, "dp_world": world, "dp_group": group}
         res, fol = {"ok": 0, "failed": 0}, None
         if rank == 0:
@@ -192,7 +207,7 @@ def main():
     else:
         import numpy as np
 
-        eng = native.Engine(model, device="hip", device_id=local_rank, max_batch=B,
+        eng = native.Engine(model, device=args.device, device_id=dev, max_batch=B,
                             pipeline_depth=args.pipeline_depth, branch_streams=args.branch_streams)
         x = r.synthetic_input(B, cfg, seed=rank).reshape(B, -1)
         for _ in range(args.warmup):
@@ -230,7 +245,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": value / BASELINE_RPS if args.arch == "resnet50" else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if hip else "fp32",
             "data": "synthetic: unique image-shaped JSON payloads (3x224x224 floats, 4 decimals), random-init weights",
             "config": {"model": model_name, "global_batch": B * args.gpus, "seq_len": 0,
                        "parallelism": "dp%d" % args.gpus, "mode": args.mode, "max_batch_per_gpu": B,
@@ -238,7 +253,7 @@ def main():
         }
         extra["numa"] = numa
         out.update({k: v for k, v in extra.items() if v is not None})
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1,0 +1,56 @@
+"""bench.py driver contract rehearsed on the CPU: one JSON line on rank 0's stdout, whole-job
+aggregate over ranks, N>1 through torch.distributed.run (gloo barriers, 127.0.0.1 rendezvous) --
+the same launch line the driver uses for the 8-GPU scaling run, on the host executor."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd, timeout=300):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout  # exactly one JSON line, nothing else on stdout
+    return json.loads(lines[0])
+
+
+def _check(out, n, steps, warmup, mode):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["higher_is_better"] is True and out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == "dp%d" % n and out["config"]["mode"] == mode
+    assert out["failed"] == 0 and out["value"] > 0
+    # whole-job aggregate: every rank's requests are counted
+    assert out["config"]["requests"] == steps * out["config"]["global_batch"]
+
+
+@pytest.mark.parametrize("mode", ["http", "dp"])
+def test_bench_single_rank_cpu(mode):
+    out = _run([sys.executable, "bench.py", "--device", "cpu", "--mode", mode, "--batch", "2", "--steps", "2",
+                "--warmup", "1", "--connections", "4"])
+    _check(out, 1, 2, 1, mode)
+
+
+@pytest.mark.parametrize("mode", ["http", "dp"])
+def test_bench_two_ranks_torchrun_cpu(mode):
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                "--device", "cpu", "--mode", mode, "--batch", "2", "--steps", "2", "--warmup", "1",
+                "--connections", "4"])
+    _check(out, 2, 2, 1, mode)
+    assert out["config"]["global_batch"] == 4
