@@ -138,6 +138,16 @@ int die_kern_decode(uint64_t text, uint64_t offs, long long text_cap, uint64_t l
                                                     S(stream)));
 }
 
+// packed: 4-bit packed samples at packed + poffs[b] (poffs[b] < 0: raw text at text + offs[b])
+int die_kern_decode_packed(uint64_t text, uint64_t offs, uint64_t packed, uint64_t poffs, long long text_cap,
+                           uint64_t lens, int B, uint64_t out, long long numel, uint64_t status, uint64_t ntok,
+                           uint64_t scratch, uint64_t stream) {
+  return static_cast<int>(kern::decode_json_numbers(P<const unsigned char>(text), P<const long long>(offs),
+                                                    static_cast<size_t>(text_cap), P<const long long>(lens), B,
+                                                    P<float>(out), numel, P<int>(status), P<int>(ntok), P<void>(scratch),
+                                                    S(stream), P<const unsigned char>(packed), P<const long long>(poffs)));
+}
+
 int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, int H, int W, int Ho, int Wo, int relu,
                   uint64_t stream) {
   return static_cast<int>(kern::conv_stem7x7(P<const uint16_t>(x), P<const uint16_t>(w), P<const float>(bias),

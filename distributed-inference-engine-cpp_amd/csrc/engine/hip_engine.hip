@@ -119,7 +119,7 @@ class HipEngine : public Engine {
       if (comm_) n_stage_ = 0;
       HIP_CHECK(hipMalloc(&d_text_, text_cap_ * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
       // 4-bit packed texts (BatchItem::packed; early-uploaded or copied at submit) land here, slot
-      // for slot like d_text_, and PREP expands them into d_text_
+      // for slot like d_text_; the decode kernels expand them in registers (no character copy in HBM)
       if (!comm_ && opt.pack_text)
         HIP_CHECK(hipMalloc(&d_packed_, text_cap_ / 2 * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
       stage_ev_.resize(n_stage_);
@@ -436,7 +436,7 @@ class HipEngine : public Engine {
             diag_submit_wait_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0).count();
             if (issued && hipEventQuery(stage_ev_[t]) != hipSuccess) diag_not_ready_++;
           }
-          if (issued) {  // already uploaded (raw, or packed: PREP expands it into the stage slot)
+          if (issued) {  // already uploaded (raw, or packed: decoded straight from its packed slot)
             h_offs[i] = static_cast<long long>(t) * static_cast<long long>(text_cap_);
             if (stage_packed_[t]) h_poffs[i] = static_cast<long long>(t) * static_cast<long long>(text_cap_ / 2);
             int& w = wait_ticket[stage_stream_[t]];
@@ -913,16 +913,11 @@ class HipEngine : public Engine {
     }
     if (text_cap_ && part != MAIN) {
       Slot& sl = slots_[s];
-      const hipError_t ec = hipSuccess;
-      if (d_packed_) {
-        const hipError_t eu = kern::unpack_text_nibbles(d_packed_, sl.d_lens + 2 * max_batch_, d_text_,
-                                                        sl.d_lens + max_batch_, sl.d_lens, B, st);
-        if (eu != hipSuccess) throw std::runtime_error("launch of text unpack failed: " + std::string(hipGetErrorString(eu)));
-      }
-      if (ec != hipSuccess) throw std::runtime_error("launch of decode table fetch failed: " + std::string(hipGetErrorString(ec)));
+      // packed samples (d_lens row 2 >= 0) are expanded in registers by the decode kernels
       const hipError_t e = kern::decode_json_numbers(d_text_, sl.d_lens + max_batch_, text_cap_, sl.d_lens, B, sl.d_in,
                                                      static_cast<long long>(in_numel_), sl.d_status,
-                                                     sl.d_status + max_batch_, sl.d_scratch, st);
+                                                     sl.d_status + max_batch_, sl.d_scratch, st, d_packed_,
+                                                     d_packed_ ? sl.d_lens + 2 * max_batch_ : nullptr);
       if (e != hipSuccess) throw std::runtime_error("launch of device decode failed: " + std::string(hipGetErrorString(e)));
     }
     if (op_events) HIP_CHECK(hipEventRecord(op_events[0], st));

@@ -3,6 +3,7 @@
 // The serving headline is bound by host CPU, and ~80% of a worker's CPU time went into converting
 // ~150k decimal strings per ResNet request.  MI355X has bandwidth to spare, so the worker copies the
 // raw text into pinned staging and the GPU converts it (inside the same hipGraph as the forward):
+//   (samples uploaded 4-bit packed are expanded to characters in registers as each kernel loads them)
 //   1. dec_count : per 4 KiB chunk, count ',' separators and note non-blank bytes
 //   2. dec_scan  : per sample, exclusive prefix over the chunk counts -> token index of each chunk;
 //                  token count, "too many values" status, zero-fill of the padded tail
@@ -33,9 +34,8 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {  // 0x80 in each by
 __device__ __forceinline__ uint32_t eq_bytes(uint32_t v, uint32_t c4) { return zero_bytes(v ^ c4); }
 __device__ __forceinline__ bool is_ws(unsigned c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
 
-// 16 bytes at [off, off+16) of a sample's text, bytes >= len replaced by ' '.
-__device__ __forceinline__ uint4 load16(const unsigned char* t, long long off, long long len) {
-  uint4 q = *reinterpret_cast<const uint4*>(t + off);
+// bytes of q at or beyond len (q holds [off, off+16)) replaced by ' '
+__device__ __forceinline__ uint4 blank_tail(uint4 q, long long off, long long len) {
   if (off + 16 > len) {
     uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -44,6 +44,34 @@ __device__ __forceinline__ uint4 load16(const unsigned char* t, long long off, l
     q = make_uint4(w[0], w[1], w[2], w[3]);
   }
   return q;
+}
+
+// 4 characters from 2 packed bytes (core/textpack.h: low nibble first).  Symbols 0-7 map through
+// one v_perm_b32 table ('0'..'7'), 8-15 through another ('8' '9' ',' '.' '-' '+' 'e' ' '); bit 3 of
+// each nibble picks the table.
+__device__ __forceinline__ uint32_t nib4(uint32_t p16) {
+  const uint32_t t = (p16 & 0xFFu) | ((p16 & 0xFF00u) << 8);
+  const uint32_t x = (t & 0x000F000Fu) | ((t & 0x00F000F0u) << 4);  // one nibble per byte
+  const uint32_t sel = x & 0x07070707u;
+  const uint32_t m = ((x >> 3) & 0x01010101u) * 0xFFu;
+  const uint32_t lo = __builtin_amdgcn_perm(0x37363534u, 0x33323130u, sel);
+  const uint32_t hi = __builtin_amdgcn_perm(0x20652B2Du, 0x2E2C3938u, sel);
+  return (hi & m) | (lo & ~m);
+}
+
+// 16 bytes at [off, off+16) of a sample's text (off % 16 == 0), bytes >= len replaced by ' '.  A
+// sample uploaded 4-bit packed (pk != nullptr) is expanded from its 8 packed bytes in registers, so
+// the character text is never materialised in HBM.  The packed slot is text_cap / 2 bytes and
+// off + 16 <= text_cap, so the 8-byte read stays inside it.
+__device__ __forceinline__ uint4 load16(const unsigned char* t, const unsigned char* pk, long long off, long long len) {
+  uint4 q;
+  if (pk) {
+    const uint2 p = *reinterpret_cast<const uint2*>(pk + (off >> 1));
+    q = make_uint4(nib4(p.x & 0xFFFFu), nib4(p.x >> 16), nib4(p.y & 0xFFFFu), nib4(p.y >> 16));
+  } else {
+    q = *reinterpret_cast<const uint4*>(t + off);
+  }
+  return blank_tail(q, off, len);
 }
 
 __device__ __forceinline__ int popc_commas(uint4 q) {
@@ -93,6 +121,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
 
 __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
+                                                 const unsigned char* __restrict__ packed,
+                                                 const long long* __restrict__ poffs,
                                                  const long long* __restrict__ lens, int* __restrict__ counts,
                                                  int* __restrict__ blank, int max_chunks) {
   __shared__ int red[4];
@@ -108,7 +138,8 @@ __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict
   const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
   int c = 0, nb = 0;
   if (off < len) {
-    const uint4 q = load16(text + (offs ? offs[b] : b * cap), off, len);
+    const long long po = poffs ? poffs[b] : -1;
+    const uint4 q = load16(text + (offs ? offs[b] : b * cap), po >= 0 ? packed + po : nullptr, off, len);
     c = popc_commas(q);
     nb = nonblank(q);
   }
@@ -337,11 +368,52 @@ __device__ __forceinline__ bool convert_token_regs(const uint32_t (&r)[8], int n
   return true;
 }
 
+// Common-case fast path: [-](0|[1-9][0-9]*)[.[0-9]+] with at most 8 digits and no exponent, the
+// shape every serializer emits for image-like data ("0.1234", "-12.5").  32-bit accumulation over
+// at most 10 bytes instead of convert_token_regs' 32-step state machine; the value is computed by
+// the same single fp32 rounding (mant <= 2^24, |exp10| <= 8), so it is bit-identical.  Anything
+// else (exponent, > 8 digits, malformed) returns false and the caller runs the full converter,
+// which decides acceptance and error status exactly as before.
+__device__ __forceinline__ bool convert_token_fast(const uint32_t (&r)[8], int n, float& out) {
+  if (n > 10) return false;
+  const bool neg = (r[0] & 0xFFu) == '-';
+  uint32_t mant = 0;
+  int nd = 0, frac = -1;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    if (i < n && i >= static_cast<int>(neg)) {
+      const uint32_t c = (r[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      const uint32_t d = c - '0';
+      if (c == '.') {
+        ok &= frac < 0 && nd > 0;
+        frac = 0;
+      } else {
+        ok &= d <= 9u;
+        mant = mant * 10 + d;
+        ++nd;
+        frac += frac >= 0;
+      }
+    }
+  }
+  // a leading '0' must be the whole integer part
+  const int f = neg ? 1 : 0;
+  const uint32_t c0 = (r[0] >> (8 * f)) & 0xFFu, c1 = (r[0] >> (8 * (f + 1))) & 0xFFu;
+  ok &= !(c0 == '0' && n > f + 1 && c1 != '.');
+  ok &= nd > 0 && nd <= 8 && frac != 0 && mant <= (1u << 24);
+  if (!ok) return false;
+  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / kP10f[frac] : static_cast<float>(mant) * kP10f[0]);
+  out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
+  return true;
+}
+
 // Token-parallel parse of one 4 KiB chunk: (1) every thread finds the token starts in its 16 bytes,
 // (2) a block scan compacts them into an LDS list, (3) each lane converts whole tokens, loading 32
 // bytes into registers with aligned LDS reads + alignbyte.
 __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
+                                                 const unsigned char* __restrict__ packed,
+                                                 const long long* __restrict__ poffs,
                                                  const long long* __restrict__ lens, const int* __restrict__ prefix,
                                                  int* __restrict__ status, float* __restrict__ out, long long numel,
                                                  int max_chunks) {
@@ -353,13 +425,15 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
   const long long c0 = static_cast<long long>(chunk) * CHUNK;
   if (len < 0 || c0 >= len) return;
   const unsigned char* t = text + (offs ? offs[b] : b * cap);
+  const long long po = poffs ? poffs[b] : -1;
+  const unsigned char* pk = po >= 0 ? packed + po : nullptr;
   // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
   for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
     const long long off = c0 - PRE + 16ll * i;
     uint4 q;
     if (off < 0) q = make_uint4(0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu);
     else if (off >= len) q = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    else q = load16(t, off, len);
+    else q = load16(t, pk, off, len);
     *reinterpret_cast<uint4*>(buf + 16 * i) = q;
   }
   __syncthreads();
@@ -418,7 +492,7 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
     } else if (ws) {
       good = convert_token(buf + p, n, v);
     } else {
-      good = n > 0 && convert_token_regs(r, n, v);
+      good = n > 0 && (convert_token_fast(r, n, v) || convert_token_regs(r, n, v));
     }
     if (good && idx < numel) out[b * numel + idx] = v;
     bad |= !good;
@@ -433,53 +507,18 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
   return static_cast<size_t>(max_batch) * chunks * 2 * sizeof(int);
 }
 
-// 4-bit packed text (core/textpack.h) -> bytes.  One thread expands 8 packed bytes into 16
-// characters (two 8-byte stores); a block covers 4 KiB of output and strides over the sample.
-__global__ void __launch_bounds__(256) unpack_text(const unsigned char* __restrict__ packed,
-                                                   const long long* __restrict__ poffs, unsigned char* __restrict__ text,
-                                                   const long long* __restrict__ offs, const long long* __restrict__ lens) {
-  const int b = blockIdx.y;
-  const long long po = poffs[b], len = lens[b];
-  if (po < 0 || len <= 0) return;
-  // nibble -> character: symbols 0-7 in lo, 8-15 in hi (one byte each)
-  constexpr unsigned long long lo = 0x3736353433323130ull;  // '0'..'7'
-  constexpr unsigned long long hi = 0x20652B2D2E2C3938ull;  // '8' '9' ',' '.' '-' '+' 'e' ' '
-  const unsigned char* src = packed + po;
-  unsigned char* dst = text + offs[b];
-  for (long long o = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 16; o < len;
-       o += static_cast<long long>(gridDim.x) * 256 * 16) {
-    const uint2 q = *reinterpret_cast<const uint2*>(src + (o >> 1));
-    unsigned long long w[2] = {0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t byte = ((k < 8 ? q.x : q.y) >> (8 * ((k >> 1) & 3))) & 0xFF;
-      const uint32_t sym = (k & 1) ? (byte >> 4) : (byte & 15);
-      const unsigned long long c = ((sym < 8 ? lo : hi) >> (8 * (sym & 7))) & 0xFF;
-      w[k >> 3] |= c << (8 * (k & 7));
-    }
-    *reinterpret_cast<uint4*>(dst + o) = make_uint4(static_cast<uint32_t>(w[0]), static_cast<uint32_t>(w[0] >> 32),
-                                                    static_cast<uint32_t>(w[1]), static_cast<uint32_t>(w[1] >> 32));
-  }
-}
-
-hipError_t unpack_text_nibbles(const unsigned char* packed, const long long* poffs, unsigned char* text,
-                               const long long* offs, const long long* lens, int B, hipStream_t s) {
-  hipLaunchKernelGGL(unpack_text, dim3(64, B), dim3(256), 0, s, packed, poffs, text, offs, lens);
-  return hipGetLastError();
-}
-
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
-                               void* scratch, hipStream_t s) {
+                               void* scratch, hipStream_t s, const unsigned char* packed, const long long* poffs) {
   if (text_cap % CHUNK) return hipErrorInvalidValue;
   const int max_chunks = static_cast<int>(text_cap / CHUNK);
   int* counts = static_cast<int*>(scratch);
   int* blank = counts + static_cast<size_t>(B) * max_chunks;
   hipLaunchKernelGGL(dec_count, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
-                     lens, counts, blank, max_chunks);
+                     packed, poffs, lens, counts, blank, max_chunks);
   hipLaunchKernelGGL(dec_scan, dim3(B), dim3(256), 0, s, lens, counts, blank, status, ntok, out, numel, max_chunks);
   hipLaunchKernelGGL(dec_parse, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
-                     lens, counts, status, out, numel, max_chunks);
+                     packed, poffs, lens, counts, status, out, numel, max_chunks);
   return hipGetLastError();
 }
 

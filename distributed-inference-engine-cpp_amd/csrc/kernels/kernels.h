@@ -113,14 +113,13 @@ hipError_t copy_i64(const long long* src, long long* dst, int n, hipStream_t s);
 // out[b][0..numel) (values, zero padded), status[b] (0 ok, bit 0 = needs host parse, 2 = more than
 // numel values) and ntok[b].
 size_t decode_scratch_bytes(int max_batch, size_t text_cap);
-// 4-bit packed text (core/textpack.h): sample b's lens[b] characters, packed at packed + poffs[b]
-// (poffs[b] < 0: not packed, skipped; 8-byte aligned), are expanded to text + offs[b] (16-byte
-// aligned; up to 15 bytes past lens[b] may be written).
-hipError_t unpack_text_nibbles(const unsigned char* packed, const long long* poffs, unsigned char* text,
-                               const long long* offs, const long long* lens, int B, hipStream_t s);
+// packed/poffs (optional): sample b's lens[b] characters are 4-bit packed (core/textpack.h) at
+// packed + poffs[b] (8-byte aligned, in a slot of text_cap / 2 bytes) and expanded in registers as
+// the decode kernels load them; poffs[b] < 0 (or packed == nullptr) reads raw text at text + offs[b].
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
-                               void* scratch, hipStream_t s);
+                               void* scratch, hipStream_t s, const unsigned char* packed = nullptr,
+                               const long long* poffs = nullptr);
 
 // ---- transformer (transformer.hip) ----
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.

@@ -112,27 +112,32 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
   }
 }
 
-// Grid: (C/8 groups / 64, B) blocks of 256 threads = 64 channel groups x 4 row-slices.
+// Grid: (C/8 groups / 16, B) blocks of 256 threads = 16 channel groups x 16 row-slices.  ResNet50's
+// head (B~20, 7x7x2048) gets 16x more blocks than one-block-per-64-groups and each thread issues
+// its ~3 16-byte loads back to back, so the 4 MB read is not latency-bound on ~80 blocks.
 __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
                            const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
                            const long long* __restrict__ live) {
-  __shared__ float part[4][64][8];
+  constexpr int G = 16, S = 16;
+  __shared__ float part[S][G][9];  // +1 pad: the reduction reads 16 slices of one group
   const int b = blockIdx.y;
   if (live && b >= *live) return;  // whole block: before any barrier
-  const int g = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int slice = threadIdx.x >> 6;
+  const int gl = threadIdx.x % G, slice = threadIdx.x / G;
+  const int g = blockIdx.x * G + gl;
   const int CG = C / 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float sc[8], sf[8];
   if (g < CG) {
+    float sc[8], sf[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       sc[t] = scale ? scale[g * 8 + t] : 1.f;
       sf[t] = scale ? shift[g * 8 + t] : 0.f;
     }
-    for (int p = slice; p < HW; p += 4) {
+    const uint16_t* src = x + static_cast<long long>(b) * HW * C + g * 8;
+#pragma unroll 4
+    for (int p = slice; p < HW; p += S) {
       float v[8];
-      load8(x + (static_cast<long long>(b) * HW + p) * C + g * 8, v);
+      load8(src + static_cast<long long>(p) * C, v);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         float u = v[t] * sc[t] + sf[t];
@@ -142,14 +147,18 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
     }
   }
 #pragma unroll
-  for (int t = 0; t < 8; ++t) part[slice][threadIdx.x & 63][t] = acc[t];
+  for (int t = 0; t < 8; ++t) part[slice][gl][t] = acc[t];
   __syncthreads();
   if (slice == 0 && g < CG) {
     const float inv = 1.f / HW;
     float r[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-      r[t] = (part[0][threadIdx.x][t] + part[1][threadIdx.x][t] + part[2][threadIdx.x][t] + part[3][threadIdx.x][t]) * inv;
+    for (int t = 0; t < 8; ++t) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) sum += part[k][gl][t];
+      r[t] = sum * inv;
+    }
     if (out) store8(out + static_cast<long long>(b) * C + g * 8, r);
     if (out_f32) {
       float4* o = reinterpret_cast<float4*>(out_f32 + static_cast<long long>(b) * C + g * 8);
@@ -242,7 +251,7 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
                           int relu, int B, int HW, int C, hipStream_t s, const long long* live) {
   if (C % 8) return hipErrorInvalidValue;
   const int CG = C / 8;
-  dim3 grid((CG + 63) / 64, B);
+  dim3 grid((CG + 15) / 16, B);
   hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live);
   return hipGetLastError();
 }

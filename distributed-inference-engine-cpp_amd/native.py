@@ -574,6 +574,8 @@ def _sig_kernels():
     L.die_decode_scratch_bytes.argtypes = [i, C.c_longlong]
     L.die_kern_decode.restype = i
     L.die_kern_decode.argtypes = [u64, u64, C.c_longlong, u64, i, u64, C.c_longlong, u64, u64, u64, u64]
+    L.die_kern_decode_packed.restype = i
+    L.die_kern_decode_packed.argtypes = [u64, u64, u64, u64, C.c_longlong, u64, i, u64, C.c_longlong, u64, u64, u64, u64]
     L._kern_sigs = True
     return L
 
