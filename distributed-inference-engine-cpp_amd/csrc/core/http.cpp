@@ -74,8 +74,9 @@ void parse_headers(std::string_view block, std::vector<std::pair<std::string, st
 }
 
 // Decode a complete chunked body starting at `data`; returns bytes consumed, 0 if incomplete,
-// -1 if malformed.
-long dechunk(std::string_view data, std::string& out) {
+// -1 if malformed, -2 if the decoded body would exceed `max_out` bytes.  Chunk sizes are checked
+// without overflow (a size near 2^64 must not wrap the bounds test).
+long dechunk(std::string_view data, std::string& out, size_t max_out) {
   size_t pos = 0;
   while (true) {
     size_t eol = data.find("\r\n", pos);
@@ -85,8 +86,9 @@ long dechunk(std::string_view data, std::string& out) {
     if (semi != std::string_view::npos) szs = szs.substr(0, semi);
     char* endp = nullptr;
     std::string tmp(trim(szs));
-    unsigned long sz = std::strtoul(tmp.c_str(), &endp, 16);
-    if (tmp.empty() || (endp && *endp)) return -1;
+    if (tmp.empty() || tmp.size() > 16) return -1;
+    unsigned long long sz = std::strtoull(tmp.c_str(), &endp, 16);
+    if (endp && *endp) return -1;
     pos = eol + 2;
     if (sz == 0) {
       // trailers until blank line
@@ -98,8 +100,9 @@ long dechunk(std::string_view data, std::string& out) {
         if (blank) return static_cast<long>(pos);
       }
     }
-    if (data.size() < pos + sz + 2) return 0;
-    out.append(data.data() + pos, sz);
+    if (sz > max_out || out.size() > max_out - sz) return -2;
+    if (pos > data.size() || data.size() - pos < 2 || sz > data.size() - pos - 2) return 0;
+    out.append(data.data() + pos, static_cast<size_t>(sz));
     pos += sz + 2;
   }
 }
@@ -442,8 +445,10 @@ void HttpServer::reactor_loop(Reactor* r) {
       }
       if (c->chunked) {
         std::string decoded;
-        long used = dechunk(c->in, decoded);
+        long used = dechunk(c->in, decoded, max_body_bytes);
+        if (used == -2) return respond_now(c, 413, "payload too large");
         if (used < 0) return respond_now(c, 400, "bad chunked body");
+        if (used == 0 && c->in.size() > max_body_bytes + (64u << 10)) return respond_now(c, 413, "payload too large");
         if (used == 0) {
           if (c->peer_eof) {
             close_conn(c);
@@ -565,7 +570,14 @@ void HttpServer::reactor_loop(Reactor* r) {
         if (ev & EPOLLOUT) {
           if (!flush(c)) continue;
         }
-        if (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) on_readable(c);
+        if (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+          // A malformed or hostile request must cost its connection, never the process.
+          try {
+            on_readable(c);
+          } catch (const std::exception&) {
+            if (r->conns.count(tag)) close_conn(c);
+          }
+        }
       }
     }
   }
@@ -826,7 +838,7 @@ std::optional<HttpResponse> HttpClient::request(const std::string& method, const
         }
         if (chunked) {
           std::string decoded;
-          long used = dechunk(std::string_view(buf).substr(body_start), decoded);
+          long used = dechunk(std::string_view(buf).substr(body_start), decoded, size_t{1} << 31);
           if (used < 0) {
             fail = "bad chunked response";
             break;

@@ -201,3 +201,58 @@ def test_binaries_cli(native, models, tmp_path):
         assert g.wait(timeout=20) == 0
     usage = subprocess.run([os.path.join(BIN_DIR, "worker_node")], capture_output=True, text=True)
     assert usage.returncode == 1 and "Usage" in usage.stderr
+
+
+def _raw_http(port, payload, timeout=5):
+    import socket
+
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    try:
+        s.sendall(payload)
+        data = b""
+        while True:
+            try:
+                chunk = s.recv(65536)
+            except socket.timeout:
+                break
+            if not chunk:
+                break
+            data += chunk
+            if b"\r\n\r\n" in data:
+                head, _, body = data.partition(b"\r\n\r\n")
+                for line in head.split(b"\r\n"):
+                    if line.lower().startswith(b"content-length:") and len(body) >= int(line.split(b":")[1]):
+                        return data
+        return data
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("chunk", [b"ffffffffffffffff\r\nXY", b"fffffffffffffffff0\r\nXY", b"7fffffff\r\nXY"])
+def test_hostile_chunk_sizes_do_not_kill_server(cluster, chunk):
+    """A chunk size near 2^64 used to wrap the bounds check and abort the process."""
+    port = int(cluster["gw"].url.rsplit(":", 1)[1])
+    req = (b"POST /infer HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" + chunk)
+    out = _raw_http(port, req, timeout=2)
+    assert out == b"" or out.startswith(b"HTTP/1.1 4")
+    # the server is still alive and serving
+    st, s = get(cluster["gw"].url + "/stats")
+    assert st == 200 and s["total_workers"] == 3
+
+
+def test_chunked_body_over_limit_is_413(cluster):
+    port = int(cluster["gw"].url.rsplit(":", 1)[1])
+    big = 600 << 20  # above the default 512 MiB body limit
+    req = b"POST /infer HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" + (b"%x\r\n" % big) + b"abc"
+    out = _raw_http(port, req)
+    assert out.startswith(b"HTTP/1.1 413"), out[:80]
+
+
+def test_chunked_request_still_works(cluster):
+    port = int(cluster["gw"].url.rsplit(":", 1)[1])
+    body = json.dumps({"request_id": "chunky", "input_data": [1.0, 2.0]}).encode()
+    half = len(body) // 2
+    req = (b"POST /infer HTTP/1.1\r\nHost: x\r\nConnection: close\r\nTransfer-Encoding: chunked\r\n\r\n"
+           + b"%x\r\n" % half + body[:half] + b"\r\n" + b"%x\r\n" % (len(body) - half) + body[half:] + b"\r\n0\r\n\r\n")
+    out = _raw_http(port, req)
+    assert out.startswith(b"HTTP/1.1 200"), out[:200]
