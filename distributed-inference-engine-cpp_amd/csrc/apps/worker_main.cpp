@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
               << "Options (defaults = reference constants):\n"
               << "  --cache-capacity N (1000)  --max-batch N (32)  --batch-timeout-ms N (20)\n"
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
-              << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision bf16|fp32 (bf16)\n"
+              << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --http-threads N  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch)\n"
@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.engine.device = f.str("device", "auto");
   o.engine.device_id = static_cast<int>(f.i("device-id", 0));
-  o.engine.precision = f.str("precision", "bf16");
+  o.engine.precision = f.str("precision", "fp32");
   o.engine.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 2));
   o.engine.use_graphs = !f.b("no-graphs");
   o.engine.device_decode = !f.b("no-device-decode");

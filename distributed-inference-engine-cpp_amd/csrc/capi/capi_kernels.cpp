@@ -70,6 +70,8 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("counters")) a.counters = P<int>(static_cast<uint64_t>(v->as_int()));
     a.counters_n = geti(j, "counters_n", 0);
+    a.split = geti(j, "split", 0);
+    if (auto* v = j.find("wplane")) a.wplane = v->as_int();
     if (tile < 0) tile = kern::choose_tile(a.M, a.N, a.K);
     return static_cast<int>(kern::conv_igemm(a, tile, S(stream)));
   } catch (...) {
@@ -78,52 +80,55 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
 }
 
 int die_kern_input_prep(uint64_t x, uint64_t scale, uint64_t shift, uint64_t out, int B, int C, int H, int W, int Cp,
-                        uint64_t stream) {
-  return static_cast<int>(
-      kern::input_prep(P<const float>(x), P<const float>(scale), P<const float>(shift), P<uint16_t>(out), B, C, H, W, Cp, S(stream)));
+                        uint64_t stream, int split) {
+  return static_cast<int>(kern::input_prep(P<const float>(x), P<const float>(scale), P<const float>(shift),
+                                           P<uint16_t>(out), B, C, H, W, Cp, S(stream), split));
 }
 
 int die_kern_pool2d(uint64_t x, uint64_t y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
-                    int ph, int pw, int is_max, int cip, uint64_t stream) {
+                    int ph, int pw, int is_max, int cip, uint64_t stream, int split) {
   return static_cast<int>(kern::pool2d(P<const uint16_t>(x), P<uint16_t>(y), B, H, W, C, Ho, Wo, kh, kw, sh, sw, ph,
-                                       pw, is_max, cip, S(stream)));
+                                       pw, is_max, cip, S(stream), nullptr, nullptr, nullptr, 0, split));
 }
 
 int die_kern_gap(uint64_t x, uint64_t out, uint64_t out_f32, uint64_t scale, uint64_t shift, int relu, int B, int HW,
-                 int C, uint64_t stream) {
+                 int C, uint64_t stream, int split) {
   return static_cast<int>(kern::global_avgpool(P<const uint16_t>(x), P<uint16_t>(out), P<float>(out_f32),
-                                               P<const float>(scale), P<const float>(shift), relu, B, HW, C, S(stream)));
+                                               P<const float>(scale), P<const float>(shift), relu, B, HW, C, S(stream),
+                                               nullptr, split));
 }
 
 int die_kern_affine(uint64_t x, uint64_t z, uint64_t scale, uint64_t shift, int act, uint64_t y, long long M, int C,
-                    uint64_t stream) {
+                    uint64_t stream, int split) {
   return static_cast<int>(kern::affine_act(P<const uint16_t>(x), P<const uint16_t>(z), P<const float>(scale),
-                                           P<const float>(shift), act, P<uint16_t>(y), M, C, S(stream)));
+                                           P<const float>(shift), act, P<uint16_t>(y), M, C, S(stream), nullptr, 0,
+                                           split));
 }
 
-int die_kern_nhwc_to_nchw(uint64_t x, uint64_t y, int B, int H, int W, int C, uint64_t stream) {
-  return static_cast<int>(kern::nhwc_to_nchw_f32(P<const uint16_t>(x), P<float>(y), B, H, W, C, S(stream)));
+int die_kern_nhwc_to_nchw(uint64_t x, uint64_t y, int B, int H, int W, int C, uint64_t stream, int split) {
+  return static_cast<int>(kern::nhwc_to_nchw_f32(P<const uint16_t>(x), P<float>(y), B, H, W, C, S(stream), split));
 }
 
 int die_kern_layernorm(uint64_t x, uint64_t y, uint64_t gamma, uint64_t beta, float eps, long long rows, int C,
-                       uint64_t stream) {
+                       uint64_t stream, int split) {
   return static_cast<int>(kern::layernorm_rows(P<const uint16_t>(x), P<uint16_t>(y), P<const float>(gamma),
-                                               P<const float>(beta), eps, rows, C, S(stream)));
+                                               P<const float>(beta), eps, rows, C, S(stream), split));
 }
 
-int die_kern_tokens(uint64_t patches, uint64_t cls, uint64_t pos, uint64_t out, int B, int S0, int C, uint64_t stream) {
+int die_kern_tokens(uint64_t patches, uint64_t cls, uint64_t pos, uint64_t out, int B, int S0, int C, uint64_t stream,
+                    int split) {
   return static_cast<int>(kern::tokens_assemble(P<const uint16_t>(patches), P<const float>(cls), P<const float>(pos),
-                                                P<uint16_t>(out), B, S0, C, S(stream)));
+                                                P<uint16_t>(out), B, S0, C, S(stream), split));
 }
 
-int die_kern_gather_rows(uint64_t x, uint64_t y, int B, int Sq, int idx, int C, uint64_t stream) {
-  return static_cast<int>(kern::gather_rows(P<const uint16_t>(x), P<uint16_t>(y), B, Sq, idx, C, S(stream)));
+int die_kern_gather_rows(uint64_t x, uint64_t y, int B, int Sq, int idx, int C, uint64_t stream, int split) {
+  return static_cast<int>(kern::gather_rows(P<const uint16_t>(x), P<uint16_t>(y), B, Sq, idx, C, S(stream), split));
 }
 
 int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,
-                       int ldv, int ldo, float scale, uint64_t stream) {
+                       int ldv, int ldo, float scale, uint64_t stream, int split) {
   return static_cast<int>(kern::attention(P<const uint16_t>(q), P<const uint16_t>(k), P<const uint16_t>(v),
-                                          P<uint16_t>(out), B, Sq, H, D, ldq, ldk, ldv, ldo, scale, S(stream)));
+                                          P<uint16_t>(out), B, Sq, H, D, ldq, ldk, ldv, ldo, scale, S(stream), split));
 }
 
 long long die_decode_scratch_bytes(int max_batch, long long text_cap) {
@@ -155,14 +160,15 @@ int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, in
 }
 
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
-char* die_plan_summary(const char* model_path, int max_batch, int side_branches, char** err) {
+char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, char** err) {
   try {
-    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0);
+    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
     j["param_bytes"] = static_cast<long long>(p.params.size());
     j["gflop_per_sample"] = p.flops_per_sample / 1e9;
+    j["precision"] = p.split ? "fp32" : "bf16";
     Json ops = Json::array();
     for (auto& o : p.ops) {
       Json e = Json::object();

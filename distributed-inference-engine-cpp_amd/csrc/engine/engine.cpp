@@ -256,13 +256,8 @@ std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const E
 std::unique_ptr<Engine> create_engine(const std::string& model_path, const EngineOptions& opt) {
   if (opt.precision != "bf16" && opt.precision != "fp32")
     throw std::runtime_error("unknown precision '" + opt.precision + "' (bf16 | fp32)");
-  // The HIP kernels compute in bf16 with fp32 accumulation; fp32 end to end is the CPU executor's
-  // (the reference's ORT CPU-EP numerics).  Never silently run bf16 when fp32 was asked for.
-  if (opt.precision == "fp32") {
-    if (opt.device == "hip") throw std::runtime_error("precision fp32 is served by --device cpu; the HIP engine computes in bf16");
-    if (opt.dp_world >= 1 && !opt.dp_group.empty()) throw std::runtime_error("data parallel serving is bf16 (HIP) only");
-    return create_cpu_engine(model_path, opt);
-  }
+  // fp32 (default, the reference's ORT numerics): on the HIP engine every GEMM runs on split hi/lo
+  // bf16 operands with fp32 accumulation (kernels/common.h); bf16 is the opt-in fast mode.
   if (opt.dp_world >= 1 && !opt.dp_group.empty() && opt.dp_comm == nullptr) return create_dp_engine(model_path, opt);
   if (opt.device != "cpu") {
     std::string why;

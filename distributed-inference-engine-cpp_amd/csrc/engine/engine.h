@@ -192,7 +192,7 @@ struct EngineOptions {
   // "auto" = $DIE_TUNE_CACHE or ~/.cache/die_amd/tune.json.
   std::string tune_cache = "auto";
   // bf16 = HIP kernels (bf16 operands, fp32 accumulation); fp32 = CPU executor (device auto/cpu).
-  std::string precision = "bf16";
+  std::string precision = "fp32";  // fp32 (reference parity; split bf16 MFMA on HIP) | bf16 (fast)
   int cpu_threads = 0;
   int shard_id = 0;
   // Data parallel (one process per GPU): dp_world ranks share the DpGroup segment

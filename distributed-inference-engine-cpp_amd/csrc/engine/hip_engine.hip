@@ -59,7 +59,9 @@ class HipEngine : public Engine {
     max_batch_ = std::max(1, opt.max_batch);
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     onnx::Model model = onnx::load_onnx(path);
-    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1);
+    // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
+    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32");
+    sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
       ++n_prep_ops_;
@@ -637,6 +639,7 @@ class HipEngine : public Engine {
     j["executors"] = n_exec_;
     j["copy_streams"] = n_copy_streams_;
     j["plan"] = plan_.summary();
+    j["precision"] = sp_ ? "fp32" : "bf16";
     j["gflop_per_image"] = plan_.flops_per_sample / 1e9;
     j["arena_mib"] = static_cast<double>(plan_.arena_bytes) / (1 << 20);
     j["pinned_samples"] = static_cast<long long>(pool_->allocated());
@@ -835,7 +838,7 @@ class HipEngine : public Engine {
         base.live = nullptr;  // tune the whole bucket
         // identical problems (repeated blocks) share one measurement
         char key[256];
-        std::snprintf(key, sizeof(key), "%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", base.M, base.N, base.K, base.Cin,
+        std::snprintf(key, sizeof(key), "%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
         auto memo = tuned_shapes.find(key);
@@ -942,7 +945,7 @@ class HipEngine : public Engine {
       switch (op.kind) {
         case PlanOp::INPUT_PREP:
           e = kern::input_prep(static_cast<const float*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
-                               static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st);
+                               static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st, sp_);
           break;
         case PlanOp::CONV: {
           kern::ConvArgs a = conv_args(op, B, s);
@@ -958,20 +961,20 @@ class HipEngine : public Engine {
         case PlanOp::POOL:
           e = kern::pool2d(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
                            op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st, live,
-                           prm(op.scale_off), prm(op.shift_off), op.act);
+                           prm(op.scale_off), prm(op.shift_off), op.act, sp_);
           break;
         case PlanOp::GAP:
           e = kern::global_avgpool(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live);
+                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live, sp_);
           break;
         case PlanOp::AFFINE:
           e = kern::affine_act(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
                                prm(op.scale_off), prm(op.shift_off), op.act, static_cast<uint16_t*>(buf(op.out)),
-                               op.rows_per_sample * B, op.C, st, live, op.rows_per_sample);
+                               op.rows_per_sample * B, op.C, st, live, op.rows_per_sample, sp_);
           break;
         case PlanOp::TO_NCHW_F32:
           e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
-                                     op.H, op.W, op.C, st);
+                                     op.H, op.W, op.C, st, sp_);
           break;
         case PlanOp::STEM:
           e = kern::conv_stem7x7(static_cast<const uint16_t*>(buf(op.in)),
@@ -981,25 +984,25 @@ class HipEngine : public Engine {
           break;
         case PlanOp::LAYERNORM:
           e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st);
+                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_);
           break;
         case PlanOp::TOKENS:
           e = kern::tokens_assemble(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
-                                    static_cast<uint16_t*>(buf(op.out)), B, op.S, op.C, st);
+                                    static_cast<uint16_t*>(buf(op.out)), B, op.S, op.C, st, sp_);
           break;
         case PlanOp::GATHER_ROWS:
           e = kern::gather_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.S,
-                                op.gidx, op.C, st);
+                                op.gidx, op.C, st, sp_);
           break;
         case PlanOp::ATTENTION:
           e = kern::attention(static_cast<const uint16_t*>(buf(op.in)) + op.col[0],
                               static_cast<const uint16_t*>(buf(op.in2)) + op.col[1],
                               static_cast<const uint16_t*>(buf(op.in3)) + op.col[2], static_cast<uint16_t*>(buf(op.out)),
-                              B, op.S, op.nh, op.hd, op.ld[0], op.ld[1], op.ld[2], op.C, op.fscale, st);
+                              B, op.S, op.nh, op.hd, op.ld[0], op.ld[1], op.ld[2], op.C, op.fscale, st, sp_);
           break;
         case PlanOp::BF16_TO_F32:
           e = kern::bf16_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
-                                static_cast<long long>(B) * op.C, st);
+                                static_cast<long long>(B) * op.C, st, sp_);
           break;
       }
       if (e != hipSuccess)
@@ -1257,6 +1260,7 @@ class HipEngine : public Engine {
   int max_batch_ = 32;
   int depth_ = 2;
   Plan plan_;
+  int sp_ = 0;  // fp32 mode (split kernels)
   size_t in_numel_ = 0, out_numel_ = 0;
   size_t text_cap_ = 0;  // bytes of input text per sample for device decode (0 = off)
   unsigned char* d_text_ = nullptr;  // (n_stage_ + depth_ * max_batch_) x text_cap_

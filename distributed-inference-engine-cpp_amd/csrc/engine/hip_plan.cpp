@@ -67,8 +67,8 @@ struct Val {
 
 class Planner {
  public:
-  Planner(const onnx::Model& m, int max_batch, bool side_branches)
-      : m_(m), max_batch_(max_batch), side_branches_(side_branches) {}
+  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split)
+      : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split) {}
 
   Plan run() {
     if (m_.inputs.empty() || m_.outputs.empty()) throw std::runtime_error("model needs an input and an output");
@@ -87,6 +87,7 @@ class Planner {
     if (in.C <= 0 || in.H <= 0 || in.W <= 0) throw std::runtime_error("input dims must be static except the batch");
     define(vi.name, in);
     plan_.input_shape = {1, in.C, in.H, in.W};
+    plan_.split = split_;
     plan_.input_numel = static_cast<size_t>(in.C) * in.H * in.W;
 
     done_.assign(m_.nodes.size(), false);
@@ -97,7 +98,7 @@ class Planner {
     }
     finalize_output();
     fuse_pool_affine();
-    if (std::getenv("DIE_BN_ON_LOAD")) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
+    if (std::getenv("DIE_BN_ON_LOAD") && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
     return std::move(plan_);
@@ -131,9 +132,10 @@ class Planner {
     auto it = consumers_.find(name);
     return it == consumers_.end() ? std::vector<int>{} : it->second;
   }
+  // An activation buffer of `bytes_per_sample` bf16 bytes (fp32 mode: hi and lo planes, twice that).
   int new_buf(size_t bytes_per_sample) {
     PlanBuf b;
-    b.bytes_per_sample = bytes_per_sample;
+    b.bytes_per_sample = bytes_per_sample * (split_ ? 2 : 1);
     plan_.bufs.push_back(b);
     return static_cast<int>(plan_.bufs.size()) - 1;
   }
@@ -148,6 +150,22 @@ class Planner {
     plan_.params.resize(off + v.size() * 2);
     std::memcpy(plan_.params.data() + off, v.data(), v.size() * 2);
     return off;
+  }
+  // GEMM weights given in fp32: bf16, or (fp32 mode) the hi plane followed by the lo plane
+  // (lo = bf16(w - hi)); `wplane` receives the plane distance in elements (0 when not split).
+  size_t push_weights(const std::vector<float>& w, long long& wplane) {
+    std::vector<uint16_t> q(w.size() * (split_ ? 2 : 1));
+    for (size_t i = 0; i < w.size(); ++i) {
+      q[i] = to_bf16(w[i]);
+      if (split_) {
+        uint32_t u = static_cast<uint32_t>(q[i]) << 16;
+        float hi;
+        std::memcpy(&hi, &u, 4);
+        q[w.size() + i] = to_bf16(w[i] - hi);
+      }
+    }
+    wplane = split_ ? static_cast<long long>(w.size()) : 0;
+    return push_bf16(q);
   }
   void add_op(PlanOp op) { plan_.ops.push_back(std::move(op)); }
 
@@ -336,13 +354,13 @@ class Planner {
     const int K = KH * KW * Cstore;
     const int Kpad = static_cast<int>(round_up(K, 64));
     const int Npad = static_cast<int>(round_up(Cout, 128));
-    std::vector<uint16_t> wp(static_cast<size_t>(Npad) * Kpad, 0);
+    std::vector<float> wp(static_cast<size_t>(Npad) * Kpad, 0.f);
     for (int co = 0; co < Cout; ++co)
       for (int ci = 0; ci < Cin; ++ci)
         for (int ky = 0; ky < KH; ++ky)
           for (int kx = 0; kx < KW; ++kx) {
             const float w = wt.f[((static_cast<size_t>(co) * Cin + ci) * KH + ky) * KW + kx] * scale[co];
-            wp[static_cast<size_t>(co) * Kpad + (ky * KW + kx) * Cstore + ci] = to_bf16(w);
+            wp[static_cast<size_t>(co) * Kpad + (ky * KW + kx) * Cstore + ci] = w;
           }
 
     PlanOp p;
@@ -351,20 +369,21 @@ class Planner {
     p.in = in_buf;
     p.in2 = res_buf;
     // ResNet stem (7x7/2, pad 3, 4 stored input channels, 64 outputs, plain epilogue): LDS-patch kernel
+    // (bf16 only: in fp32 mode the stem runs as a generic split conv)
     const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && Cstore == 4 &&
-                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur);
+                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur) && !split_;
     if (stem) {
       p.kind = PlanOp::STEM;
-      std::vector<uint16_t> ws(64 * 224, 0);
+      std::vector<float> ws(64 * 224, 0.f);
       for (int co = 0; co < Cout; ++co)
         for (int ci = 0; ci < Cin; ++ci)
           for (int ky = 0; ky < 7; ++ky)
             for (int kx = 0; kx < 7; ++kx)
-              ws[co * 224 + ky * 32 + kx * 4 + ci] =
-                  to_bf16(wt.f[((static_cast<size_t>(co) * Cin + ci) * KH + ky) * KW + kx] * scale[co]);
+              ws[co * 224 + ky * 32 + kx * 4 + ci] = wt.f[((static_cast<size_t>(co) * Cin + ci) * KH + ky) * KW + kx] * scale[co];
       wp.swap(ws);
     }
-    p.w_off = push_bf16(wp);
+    p.w_off = push_weights(wp, p.conv.wplane);
+    p.conv.split = split_;
     p.bias_off = push_f32(shift);
     auto& a = p.conv;
     a.H = x.H;
@@ -568,7 +587,7 @@ class Planner {
     }
     const int Kpad = static_cast<int>(round_up(K, 64));
     const int Npad = static_cast<int>(round_up(Ntot, 128));
-    std::vector<uint16_t> wp(static_cast<size_t>(Npad) * Kpad, 0);
+    std::vector<float> wp(static_cast<size_t>(Npad) * Kpad, 0.f);
     std::vector<float> bias(Ntot, 0.f);
     for (size_t g = 0; g < group.size(); ++g) {
       const Node& nd = m_.nodes[group[g]];
@@ -577,7 +596,7 @@ class Planner {
       for (int j = 0; j < Nj; ++j)
         for (int k = 0; k < K; ++k) {
           const float v = tb ? w.f[static_cast<size_t>(j) * K + k] : w.f[static_cast<size_t>(k) * Nj + j];
-          wp[static_cast<size_t>(offs[g] + j) * Kpad + k] = to_bf16(alpha * v);
+          wp[static_cast<size_t>(offs[g] + j) * Kpad + k] = alpha * v;
         }
       if (gemm && !nd.in(2).empty()) {
         const auto& c = init(nd.in(2), nd).f;
@@ -588,7 +607,8 @@ class Planner {
     p.kind = PlanOp::CONV;
     p.name = group.size() > 1 ? n.name + "+qkv" : n.name;
     p.in = x.buf;
-    p.w_off = push_bf16(wp);
+    p.w_off = push_weights(wp, p.conv.wplane);
+    p.conv.split = split_;
     auto& a = p.conv;
     a.H = a.Ho = rows;
     a.Cin = K;
@@ -1327,6 +1347,7 @@ class Planner {
   const onnx::Model& m_;
   int max_batch_;
   bool side_branches_ = false;
+  bool split_ = false;  // fp32 mode: split (hi, lo) activations and weights
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -1347,8 +1368,8 @@ std::string Plan::summary() const {
   return os.str();
 }
 
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches) {
-  return Planner(m, max_batch, side_branches).run();
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split) {
+  return Planner(m, max_batch, side_branches, split).run();
 }
 
 }  // namespace die

@@ -76,11 +76,15 @@ struct Plan {
   std::vector<int64_t> output_shape;  // [1, ...]
   size_t input_numel = 0, output_numel = 0;
   double flops_per_sample = 0;
+  // fp32 mode: every activation buffer holds split (hi, lo) bf16 planes (kernels/common.h), GEMM
+  // weights are packed as hi + lo planes, and every kernel runs its split variant.
+  bool split = false;
   std::string summary() const;
 };
 
 // Build the plan for batches up to max_batch.  Throws on unsupported graphs.  side_branches: mark
 // independent convs to run on a second stream (PlanOp::join; extends their inputs' lifetimes).
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false);
+// split: fp32 mode (Plan::split).
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false);
 
 }  // namespace die

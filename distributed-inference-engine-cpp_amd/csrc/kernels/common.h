@@ -29,5 +29,72 @@ __device__ __forceinline__ void unpack2(uint32_t v, float& a, float& b) {
   b = __uint_as_float(v & 0xFFFF0000u);
 }
 
+// ---- fp32 mode: split (hi, lo) bf16 planes -------------------------------------------------------
+// A "split" tensor stores each fp32 value v as hi = bf16(v) in a hi plane and lo = bf16(v - hi) in a
+// lo plane `plane` elements after it (same indexing in both).  hi + lo carries ~16 significant bits
+// (relative representation error <= 2^-17), and a GEMM over split operands takes three bf16 MFMAs
+// per fragment pair (hi*hi + lo*hi + hi*lo; the lo*lo term is below fp32 accumulation noise), so
+// the matrix cores keep their bf16 rate (3x the work, ~5x the v_mfma_f32_*_f32 throughput).
+__device__ __forceinline__ void split1(float v, uint16_t& hi, uint16_t& lo) {
+  hi = f2bf(v);
+  lo = f2bf(v - bf2f(hi));
+}
+
+// 8 values -> hi/lo 16-byte vectors.
+__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
+  uint16_t h[8], l[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) split1(v[t], h[t], l[t]);
+  hi = make_uint4(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16), h[4] | (uint32_t(h[5]) << 16),
+                  h[6] | (uint32_t(h[7]) << 16));
+  lo = make_uint4(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16), l[4] | (uint32_t(l[5]) << 16),
+                  l[6] | (uint32_t(l[7]) << 16));
+}
+
+__device__ __forceinline__ void unpack8(const uint4 q, float* v) {
+  unpack2(q.x, v[0], v[1]);
+  unpack2(q.y, v[2], v[3]);
+  unpack2(q.z, v[4], v[5]);
+  unpack2(q.w, v[6], v[7]);
+}
+
+// Load 8 consecutive values (16-B aligned) of a bf16 tensor, or of a split tensor (hi + lo).
+__device__ __forceinline__ void load8v(const uint16_t* p, long long plane, bool split, float* v) {
+  unpack8(*reinterpret_cast<const uint4*>(p), v);
+  if (split) {
+    float w[8];
+    unpack8(*reinterpret_cast<const uint4*>(p + plane), w);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] += w[t];
+  }
+}
+
+// Store 8 consecutive values as bf16, or split into the hi/lo planes.
+__device__ __forceinline__ void store8v(uint16_t* p, long long plane, bool split, const float* v) {
+  if (split) {
+    uint4 hi, lo;
+    split8(v, hi, lo);
+    *reinterpret_cast<uint4*>(p) = hi;
+    *reinterpret_cast<uint4*>(p + plane) = lo;
+  } else {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+  }
+}
+
+__device__ __forceinline__ float load1v(const uint16_t* p, long long plane, bool split) {
+  return split ? bf2f(p[0]) + bf2f(p[plane]) : bf2f(p[0]);
+}
+
+__device__ __forceinline__ void store1v(uint16_t* p, long long plane, bool split, float v) {
+  if (split) {
+    uint16_t h, l;
+    split1(v, h, l);
+    p[0] = h;
+    p[plane] = l;
+  } else {
+    p[0] = f2bf(v);
+  }
+}
+
 }  // namespace k
 }  // namespace die

@@ -42,27 +42,26 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
+// fp32 mode (p.split): the residual is read as hi + lo and out/out2 are stored as split planes.
 __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
   const size_t o = static_cast<size_t>(m) * p.N + n;
+  const bool split = p.split != 0;
   if (p.bias) {
     const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
     v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
     v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
   }
   if (p.res) {
-    const uint4 r = *reinterpret_cast<const uint4*>(p.res + o);
-    float a, b;
-    unpack2(r.x, a, b); v[0] += a; v[1] += b;
-    unpack2(r.y, a, b); v[2] += a; v[3] += b;
-    unpack2(r.z, a, b); v[4] += a; v[5] += b;
-    unpack2(r.w, a, b); v[6] += a; v[7] += b;
+    float r[8];
+    load8v(p.res + o, p.oplane, split, r);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] += r[t];
   }
   if (p.relu) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu);
   }
-  if (p.out)
-    *reinterpret_cast<uint4*>(p.out + o) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+  if (p.out) store8v(p.out + o, p.oplane, split, v);
   if (p.out_f32) {
     *reinterpret_cast<float4*>(p.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(p.out_f32 + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -76,7 +75,7 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
 #pragma unroll
       for (int t = 0; t < 8; ++t) u[t] = fmaxf(u[t], 0.f);
     }
-    *reinterpret_cast<uint4*>(p.out2 + o) = make_uint4(pack2(u[0], u[1]), pack2(u[2], u[3]), pack2(u[4], u[5]), pack2(u[6], u[7]));
+    store8v(p.out2 + o, p.oplane, split, u);
   }
 }
 
@@ -118,15 +117,18 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   return true;
 }
 
-template <int BM, int BN, int MODE, int VEC>
+// Register-staged main loop (any shape).  SPLIT (fp32 mode): both operands come as hi/lo planes, a
+// stage holds four tiles [A_hi][B_hi][A_lo][B_lo] and every fragment pair takes three MFMAs.
+template <int BM, int BN, int MODE, int VEC, bool SPLIT = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const int kt_per_split) {
+  constexpr int NP = SPLIT ? 2 : 1;                   // operand planes
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave pixels / channels
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, STAGE = A_ELEMS + B_ELEMS;
   constexpr int W_CH = BN / 32;                       // 16-B weight chunks per thread per stage
   constexpr int X_CH = VEC == 8 ? BM / 32 : BM / 16;  // activation units per thread per stage
-  static_assert(2 * STAGE * 2 >= BM * BN * 4, "epilogue staging must fit in the operand LDS");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE];
+  static_assert(2 * STAGE * NP * 2 >= BM * BN * 4, "epilogue staging must fit in the operand LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE * NP];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -171,14 +173,16 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     }
   }
 
-  uint4 wreg[W_CH];
-  uint4 xreg8[VEC == 8 ? X_CH : 1];
-  uint2 xreg4[VEC == 4 ? X_CH : 1];
+  uint4 wreg[NP][W_CH];
+  uint4 xreg8[NP][VEC == 8 ? X_CH : 1];
+  uint2 xreg4[NP][VEC == 4 ? X_CH : 1];
 
   auto load_stage = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < W_CH; ++i)
-      wreg[i] = *reinterpret_cast<const uint4*>(wsrc + static_cast<size_t>(32 * i) * p.Kpad + k0);
+    for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i)
+        wreg[pl][i] = *reinterpret_cast<const uint4*>(wsrc + pl * p.wplane + static_cast<size_t>(32 * i) * p.Kpad + k0);
     const int kk = k0 + xc * VEC;
     bool kvalid = kk < p.K;
     int off = 0, ky = 0, kx = 0;
@@ -201,26 +205,33 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
         v = v && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         addr += (static_cast<size_t>(ih) * p.W + iw) * p.Cin;
       }
-      if (VEC == 8) {
-        xreg8[i] = v ? *reinterpret_cast<const uint4*>(p.x + addr) : make_uint4(0, 0, 0, 0);
-      } else {
-        xreg4[i] = v ? *reinterpret_cast<const uint2*>(p.x + addr) : make_uint2(0, 0);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        const uint16_t* src = p.x + addr + pl * p.xplane;
+        if (VEC == 8) {
+          xreg8[pl][i] = v ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        } else {
+          xreg4[pl][i] = v ? *reinterpret_cast<const uint2*>(src) : make_uint2(0, 0);
+        }
       }
     }
   };
 
   auto store_stage = [&](int buf) {
-    uint16_t* A = lds + buf * STAGE;
-    uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
-    for (int i = 0; i < W_CH; ++i) *reinterpret_cast<uint4*>(A + swz(wr + 32 * i, wc)) = wreg[i];
+    for (int pl = 0; pl < NP; ++pl) {
+      uint16_t* A = lds + (buf * NP + pl) * STAGE;
+      uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
-    for (int i = 0; i < X_CH; ++i) {
-      const int row = xr + XR_STEP * i;
-      if (VEC == 8) {
-        *reinterpret_cast<uint4*>(Bt + swz(row, xc)) = xreg8[i];
-      } else {
-        *reinterpret_cast<uint2*>(Bt + swz(row, xc >> 1) + 4 * (xc & 1)) = xreg4[i];
+      for (int i = 0; i < W_CH; ++i) *reinterpret_cast<uint4*>(A + swz(wr + 32 * i, wc)) = wreg[pl][i];
+#pragma unroll
+      for (int i = 0; i < X_CH; ++i) {
+        const int row = xr + XR_STEP * i;
+        if (VEC == 8) {
+          *reinterpret_cast<uint4*>(Bt + swz(row, xc)) = xreg8[pl][i];
+        } else {
+          *reinterpret_cast<uint2*>(Bt + swz(row, xc >> 1) + 4 * (xc & 1)) = xreg4[pl][i];
+        }
       }
     }
   };
@@ -240,23 +251,31 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     const int cur = (kt - kt_begin) & 1;
     const bool more = kt + 1 < kt_end;
     if (more) load_stage((kt + 1) * BK);  // in flight under the MFMAs below
-    const uint16_t* A = lds + cur * STAGE;
-    const uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int chunk = s * 4 + (lane >> 4);
-      bf16x8 af[TN], bfr[TM];
+      bf16x8 af[NP][TN], bfr[NP][TM];
 #pragma unroll
-      for (int i = 0; i < TN; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * WN + i * 16 + (lane & 15), chunk));
+      for (int pl = 0; pl < NP; ++pl) {
+        const uint16_t* A = lds + (cur * NP + pl) * STAGE;
+        const uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
-      for (int j = 0; j < TM; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
+        for (int i = 0; i < TN; ++i)
+          af[pl][i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * WN + i * 16 + (lane & 15), chunk));
 #pragma unroll
         for (int j = 0; j < TM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[pl][j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          if constexpr (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[1][j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+        }
     }
     if (more) store_stage(cur ^ 1);
     __syncthreads();
@@ -362,14 +381,14 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         if (n + r >= p.N) break;
         const size_t o = static_cast<size_t>(m) * p.N + n + r;
         float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
-        if (p.res) v += bf2f(p.res[o]);
+        if (p.res) v += load1v(p.res + o, p.oplane, p.split);
         if (p.relu) v = act_fn(v, p.relu);
-        if (p.out) p.out[o] = f2bf(v);
+        if (p.out) store1v(p.out + o, p.oplane, p.split, v);
         if (p.out_f32) p.out_f32[o] = v;
         if (p.out2) {
           float u = v * p.scale2[n + r] + p.shift2[n + r];
           if (p.relu2) u = fmaxf(u, 0.f);
-          p.out2[o] = f2bf(u);
+          store1v(p.out2 + o, p.oplane, p.split, u);
         }
       }
     }
@@ -448,12 +467,16 @@ __device__ __forceinline__ bf16x8 bn_act8(bf16x8 f, float4 s0, float4 s1, float4
 
 constexpr int kBnlMaxK = 2048;  // pre-activation on load: channels staged in LDS
 
-template <int BM, int BN, int MODE, int STAGES, bool BNL = false>
+// SPLIT (fp32 mode): each stage holds [A_hi][B_hi][A_lo][B_lo]; the lo tiles are DMA'd from the
+// planes wplane / xplane elements after the hi ones (zero-page rows stay zero-page), and every
+// fragment pair takes three MFMAs (hi*hi + lo*hi + hi*lo).
+template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
+  constexpr int NP = SPLIT ? 2 : 1;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, STAGE = A_ELEMS + B_ELEMS;
-  constexpr int GA = BN / 32, GB = BM / 32, G = GA + GB;  // DMA instructions per wave per stage
+  constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
+  constexpr int GA = BN / 32, GB = BM / 32, G = NP * (GA + GB);  // DMA instructions per wave per stage
   constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
@@ -493,12 +516,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const uint16_t* bsrc[GB];
   int bih[GB], biw[GB];
   bool bval[GB];
+  long long bdel[GB];  // SPLIT, MODE 0: distance to the lo plane (0 for zero-page tail rows)
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
     const int r = wave * (BM / 4) + i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = m0 + r;
     bval[i] = m < p.M;
+    bdel[i] = bval[i] ? p.xplane : 0;
     const int mm = bval[i] ? m : 0;
     if (MODE == 0) {
       bsrc[i] = (bval[i] ? p.x + static_cast<size_t>(mm) * p.Cin : p.zeros) + c * 8;
@@ -530,9 +555,16 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
     for (int i = 0; i < GA; ++i) glds16(asrc[i] + nx_k0, A + (wave * (BN / 4) + i * 8) * BK);
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < GA; ++i) glds16(asrc[i] + p.wplane + nx_k0, A + PLANE + (wave * (BN / 4) + i * 8) * BK);
+    }
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < GB; ++i) glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * 8) * BK);
+      for (int i = 0; i < GB; ++i) {
+        glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * 8) * BK);
+        if constexpr (SPLIT) glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 4) + i * 8) * BK);
+      }
     } else {
       const int dy = nx_ky * p.dil, dx = nx_kx * p.dil;
 #pragma unroll
@@ -543,6 +575,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
                        static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
         const uint16_t* src = v ? bsrc[i] + ((ih * p.W + iw) * p.Cin + nx_ci0) : p.zeros;
         glds16(src, Bt + (wave * (BM / 4) + i * 8) * BK);
+        if constexpr (SPLIT) glds16(v ? src + p.xplane : p.zeros, Bt + PLANE + (wave * (BM / 4) + i * 8) * BK);
       }
       nx_ci0 += BK;
       if (nx_ci0 == p.Cin) {
@@ -588,6 +621,22 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 #pragma unroll
       for (int j = 0; j < TM; ++j)
         bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+      if constexpr (SPLIT) {
+        bf16x8 afl[TN], bfl[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          afl[i] = *reinterpret_cast<const bf16x8*>(A + PLANE + swz(wn * WN + i * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          bfl[j] = *reinterpret_cast<const bf16x8*>(Bt + PLANE + swz(wm * WM + j * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+          }
+      }
       if constexpr (BNL) {
         const float* sc = bnl + t * BK + chunk * 8;
         const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
@@ -610,7 +659,12 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 
 template <int BM, int BN, int STAGES>
 void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
-  if (b.in_scale) {
+  if (b.split) {  // only ring depths whose doubled stages fit the LDS are instantiated
+    if constexpr (STAGES * (BM + BN) * BK * 4 <= 160 * 1024) {
+      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true>), grid, dim3(256), 0, s, b, kt_per);
+      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, true>), grid, dim3(256), 0, s, b, kt_per);
+    }
+  } else if (b.in_scale) {
     if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
     else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
   } else if (mode0) {
@@ -632,6 +686,13 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   const int eff = (nk + kt_per - 1) / kt_per;  // no empty slices
   ConvArgs b = a;
   b.splits = eff;
+  if (a.split) {  // plane distances of the split activations (weights: set by the planner)
+    b.xplane = static_cast<long long>(a.B) * a.H * a.W * a.Cin;
+    b.oplane = static_cast<long long>(a.M) * a.N;
+    if (a.wplane <= 0 || a.in_scale) return hipErrorInvalidValue;
+  } else {
+    b.xplane = b.oplane = 0;
+  }
   // fused split-K reduction needs a zeroed counter per output tile
   const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
   if (!fused) b.counters = nullptr;
@@ -648,6 +709,10 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS)
     constexpr int kStageBytes = (BM + BN) * BK * 2;
     if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
+    // split stages are twice as large: 128x128 fits 2 stages, 64-wide tiles 3-4 (160 KiB LDS)
+    const int np = a.split ? 2 : 1;
+    const int stages = variant == 1 ? 2 : variant == 2 ? 3 : variant == 3 ? 4 : 6;
+    if (stages * kStageBytes * np > 160 * 1024) return hipErrorInvalidValue;
     switch (variant) {
       case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
       case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;
@@ -656,6 +721,10 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
         if constexpr (6 * kStageBytes <= 160 * 1024) launch_glds<BM, BN, 6>(mode0, grid, s, b, kt_per);
         else return hipErrorInvalidValue;
     }
+  } else if (a.split) {
+    if (dense1x1 && vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8, true>), grid, dim3(256), 0, s, b, kt_per);
+    else if (vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8, true>), grid, dim3(256), 0, s, b, kt_per);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4, true>), grid, dim3(256), 0, s, b, kt_per);
   } else if (dense1x1 && vec == 8) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), grid, dim3(256), 0, s, b, kt_per);
   } else if (vec == 8) {

@@ -52,6 +52,13 @@ struct ConvArgs {
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
   int in_relu = 0;
+  // fp32 mode (common.h "split" tensors): x, res, out and out2 are split (hi, lo) bf16 planes and w
+  // holds the weights' hi plane followed by their lo plane `wplane` elements later.  The planes of
+  // the activations follow from the shapes (x: B*H*W*Cin, res/out/out2: M*N; the launcher fills
+  // xplane/oplane).  out_f32 and the split-K workspace stay plain fp32.
+  int split = 0;
+  long long wplane = 0;
+  long long xplane = 0, oplane = 0;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),
@@ -71,29 +78,32 @@ size_t splitk_workspace_bytes(int M, int N, int splits);
 // before any launch).
 hipError_t conv_igemm(const ConvArgs& a, int tile_cfg, hipStream_t s);
 
+// `split` (launchers below): every bf16 tensor argument is a split tensor (common.h) whose lo plane
+// follows its hi plane by the tensor's element count at batch B (views: rows * pitch).
 // fp32 NCHW -> (x * scale[c] + shift[c]) -> bf16 NHWC with Cp >= C channels (pad channels = 0).
 hipError_t input_prep(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
-                      int W, int Cp, hipStream_t s);
+                      int W, int Cp, hipStream_t s, int split = 0);
 // `live` (nullable device scalar, kernels below and ConvArgs::live): only the first *live of the B
 // samples are computed; the rest of the outputs are left as they are.
 // NHWC bf16 max / average pooling (C % 8 == 0).
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
                   int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s,
                   const long long* live = nullptr, const float* scale = nullptr, const float* shift = nullptr,
-                  int act = 0);
+                  int act = 0, int split = 0);
 // [B, HW, C] bf16 -> [B, C] (mean over HW), optional y = relu(x*scale+shift) before averaging;
 // writes bf16 `out` and/or f32 `out_f32`.
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
-                          int relu, int B, int HW, int C, hipStream_t s, const long long* live = nullptr);
+                          int relu, int B, int HW, int C, hipStream_t s, const long long* live = nullptr,
+                          int split = 0);
 // Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional)
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
                       uint16_t* y, long long M, int C, hipStream_t s, const long long* live = nullptr,
-                      long long rows_per_sample = 0);
+                      long long rows_per_sample = 0, int split = 0);
 // bf16 NHWC [B,H,W,C] -> f32 NCHW [B,C,H,W]
-hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s);
+hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s, int split = 0);
 // f32 -> bf16 / bf16 -> f32 copies
 hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
-hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s);
+hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s, int split = 0);
 
 // 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:
 // w = [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8), out = act(conv + bias) NHWC bf16.
@@ -124,16 +134,17 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // ---- transformer (transformer.hip) ----
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s);
+                          long long rows, int C, hipStream_t s, int split = 0);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
-                           int C, hipStream_t s);
+                           int C, hipStream_t s, int split = 0);
 // y[b,:] = x[b, idx, :]   (x is [B][S][C])
-hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s);
+hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s, int split = 0);
 // Multi-head attention: out[b,s,h*D:(h+1)*D] = softmax(scale * Q_h K_h^T) V_h with Q/K/V rows
-// [B*S][ld*] (head h at columns h*D).  D == 64, S <= 256.
+// [B*S][ld*] (head h at columns h*D).  D == 64, S <= 256 (split: S <= 224; q/k/v/out planes are
+// B*S*ld of their pitch).
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
-                     int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s);
+                     int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split = 0);
 
 }  // namespace kern
 }  // namespace die

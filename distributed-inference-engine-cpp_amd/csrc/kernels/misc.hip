@@ -20,8 +20,10 @@ inline int grid_for(long long work, int block = 256, int cap = 4096) {
 // fp32 NCHW -> affine -> bf16 NHWC (Cp channels; Cp in {4, 8}), one thread per pixel.
 template <int CP>
 __global__ void input_prep_kernel(const float* __restrict__ x, const float* __restrict__ scale,
-                                  const float* __restrict__ shift, uint16_t* __restrict__ out, int B, int C, int HW) {
+                                  const float* __restrict__ shift, uint16_t* __restrict__ out, int B, int C, int HW,
+                                  int split) {
   const long long total = static_cast<long long>(B) * HW;
+  const long long plane = total * CP;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
        i += static_cast<long long>(gridDim.x) * blockDim.x) {
     const long long b = i / HW;
@@ -37,30 +39,26 @@ __global__ void input_prep_kernel(const float* __restrict__ x, const float* __re
       }
     }
     if (CP == 4) {
-      *reinterpret_cast<uint2*>(out + i * 4) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) split1(v[c], h[c], l[c]);
+      *reinterpret_cast<uint2*>(out + i * 4) = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+      if (split)
+        *reinterpret_cast<uint2*>(out + plane + i * 4) =
+            make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
     } else {
-      *reinterpret_cast<uint4*>(out + i * 8) =
-          make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      store8v(out + i * 8, plane, split != 0, v);
     }
   }
 }
 
-__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
-  const uint4 q = *reinterpret_cast<const uint4*>(p);
-  unpack2(q.x, v[0], v[1]);
-  unpack2(q.y, v[2], v[3]);
-  unpack2(q.z, v[4], v[5]);
-  unpack2(q.w, v[6], v[7]);
-}
-__device__ __forceinline__ void store8(uint16_t* p, const float* v) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
-}
 
 // One thread per (output pixel, 8-channel group).
 __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
                               int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int cip,
                               const long long* __restrict__ live, const float* __restrict__ scale,
-                              const float* __restrict__ shift, int act) {
+                              const float* __restrict__ shift, int act, int split) {
+  const long long xplane = static_cast<long long>(B) * H * W * C, yplane = static_cast<long long>(B) * Ho * Wo * C;
   if (live) B = min(B, static_cast<int>(*live));
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * Ho * Wo * CG;
@@ -85,7 +83,7 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
           continue;
         }
         float v[8];
-        load8(x + ((static_cast<long long>(b) * H + ih) * W + iw) * C + cg * 8, v);
+        load8v(x + ((static_cast<long long>(b) * H + ih) * W + iw) * C + cg * 8, xplane, split != 0, v);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = is_max ? fmaxf(acc[t], v[t]) : acc[t] + v[t];
         ++cnt;
@@ -108,7 +106,7 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = fmaxf(acc[t], 0.f);
     }
-    store8(y + i * 8, acc);
+    store8v(y + i * 8, yplane, split != 0, acc);
   }
 }
 
@@ -117,7 +115,8 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
 // its ~3 16-byte loads back to back, so the 4 MB read is not latency-bound on ~80 blocks.
 __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
                            const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
-                           const long long* __restrict__ live) {
+                           const long long* __restrict__ live, int split) {
+  const long long xplane = static_cast<long long>(gridDim.y) * HW * C, oplane = static_cast<long long>(gridDim.y) * C;
   constexpr int G = 16, S = 16;
   __shared__ float part[S][G][9];  // +1 pad: the reduction reads 16 slices of one group
   const int b = blockIdx.y;
@@ -137,7 +136,7 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
 #pragma unroll 4
     for (int p = slice; p < HW; p += S) {
       float v[8];
-      load8(src + static_cast<long long>(p) * C, v);
+      load8v(src + static_cast<long long>(p) * C, xplane, split != 0, v);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         float u = v[t] * sc[t] + sf[t];
@@ -159,7 +158,7 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
       for (int k = 0; k < S; ++k) sum += part[k][gl][t];
       r[t] = sum * inv;
     }
-    if (out) store8(out + static_cast<long long>(b) * C + g * 8, r);
+    if (out) store8v(out + static_cast<long long>(b) * C + g * 8, oplane, split != 0, r);
     if (out_f32) {
       float4* o = reinterpret_cast<float4*>(out_f32 + static_cast<long long>(b) * C + g * 8);
       o[0] = make_float4(r[0], r[1], r[2], r[3]);
@@ -172,7 +171,8 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
 __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ z,
                                   const float* __restrict__ scale, const float* __restrict__ shift, int act,
                                   uint16_t* __restrict__ y, long long M, int C, const long long* __restrict__ live,
-                                  long long rows_per_sample) {
+                                  long long rows_per_sample, int split) {
+  const long long plane = M * C;
   if (live) M = min(M, *live * rows_per_sample);
   const int CG = C / 8;
   const long long total = M * CG;
@@ -180,14 +180,14 @@ __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t
        i += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int c0 = static_cast<int>(i % CG) * 8;
     float v[8];
-    load8(x + i * 8, v);
+    load8v(x + i * 8, plane, split != 0, v);
     if (scale) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = v[t] * scale[c0 + t] + shift[c0 + t];
     }
     if (z) {
       float w[8];
-      load8(z + i * 8, w);
+      load8v(z + i * 8, plane, split != 0, w);
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += w[t];
     }
@@ -195,11 +195,12 @@ __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
     }
-    store8(y + i * 8, v);
+    store8v(y + i * 8, plane, split != 0, v);
   }
 }
 
-__global__ void nhwc_to_nchw_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int B, int HW, int C) {
+__global__ void nhwc_to_nchw_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int B, int HW, int C,
+                                        int split) {
   const long long total = static_cast<long long>(B) * HW * C;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
        i += static_cast<long long>(gridDim.x) * blockDim.x) {
@@ -208,7 +209,7 @@ __global__ void nhwc_to_nchw_f32_kernel(const uint16_t* __restrict__ x, float* _
     long long r = i / HW;
     const long long c = r % C;
     const long long b = r / C;
-    y[i] = bf2f(x[(b * HW + p) * C + c]);
+    y[i] = load1v(x + (b * HW + p) * C + c, total, split != 0);
   }
 }
 
@@ -218,56 +219,57 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __rest
     y[i] = f2bf(x[i]);
 }
 
-__global__ void bf16_to_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, long long n) {
+__global__ void bf16_to_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, long long n, int split) {
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<long long>(gridDim.x) * blockDim.x)
-    y[i] = bf2f(x[i]);
+    y[i] = load1v(x + i, n, split != 0);
 }
 
 }  // namespace
 
 hipError_t input_prep(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
-                      int W, int Cp, hipStream_t s) {
+                      int W, int Cp, hipStream_t s, int split) {
   if (C > Cp || (Cp != 4 && Cp != 8)) return hipErrorInvalidValue;
   const long long work = static_cast<long long>(B) * H * W;
   if (Cp == 4)
-    hipLaunchKernelGGL(input_prep_kernel<4>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W);
+    hipLaunchKernelGGL(input_prep_kernel<4>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W, split);
   else
-    hipLaunchKernelGGL(input_prep_kernel<8>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W);
+    hipLaunchKernelGGL(input_prep_kernel<8>, dim3(grid_for(work)), dim3(256), 0, s, x, scale, shift, out, B, C, H * W, split);
   return hipGetLastError();
 }
 
 hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
                   int sw, int ph, int pw, int is_max, int count_include_pad, hipStream_t s, const long long* live,
-                  const float* scale, const float* shift, int act) {
+                  const float* scale, const float* shift, int act, int split) {
   if (C % 8) return hipErrorInvalidValue;
   const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(pool2d_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, kh, kw, sh, sw,
-                     ph, pw, is_max, count_include_pad, live, scale, shift, act);
+                     ph, pw, is_max, count_include_pad, live, scale, shift, act, split);
   return hipGetLastError();
 }
 
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
-                          int relu, int B, int HW, int C, hipStream_t s, const long long* live) {
+                          int relu, int B, int HW, int C, hipStream_t s, const long long* live, int split) {
   if (C % 8) return hipErrorInvalidValue;
   const int CG = C / 8;
   dim3 grid((CG + 15) / 16, B);
-  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live);
+  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split);
   return hipGetLastError();
 }
 
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
-                      uint16_t* y, long long M, int C, hipStream_t s, const long long* live, long long rows_per_sample) {
+                      uint16_t* y, long long M, int C, hipStream_t s, const long long* live, long long rows_per_sample,
+                      int split) {
   if (C % 8) return hipErrorInvalidValue;
   if (live && rows_per_sample <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(M * (C / 8))), dim3(256), 0, s, x, z, scale, shift, act, y, M,
-                     C, live, rows_per_sample);
+                     C, live, rows_per_sample, split);
   return hipGetLastError();
 }
 
-hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s) {
+hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s, int split) {
   const long long work = static_cast<long long>(B) * H * W * C;
-  hipLaunchKernelGGL(nhwc_to_nchw_f32_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H * W, C);
+  hipLaunchKernelGGL(nhwc_to_nchw_f32_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H * W, C, split);
   return hipGetLastError();
 }
 
@@ -303,8 +305,8 @@ hipError_t copy_i64(const long long* src, long long* dst, int n, hipStream_t s) 
   return hipGetLastError();
 }
 
-hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s, int split) {
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n, split);
   return hipGetLastError();
 }
 

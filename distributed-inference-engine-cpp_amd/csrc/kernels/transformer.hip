@@ -26,10 +26,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <int CPL>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         const float* __restrict__ g, const float* __restrict__ b,
-                                                        float eps, long long rows, int C) {
+                                                        float eps, long long rows, int C, int split) {
   const int lane = threadIdx.x & 63;
   const long long row = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
+  const long long plane = rows * C;
   const int nch = C / 8;
   const uint16_t* xr = x + row * C;
   float v[CPL][8];
@@ -38,11 +39,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
-      const uint4 q = *reinterpret_cast<const uint4*>(xr + c * 8);
-      unpack2(q.x, v[i][0], v[i][1]);
-      unpack2(q.y, v[i][2], v[i][3]);
-      unpack2(q.z, v[i][4], v[i][5]);
-      unpack2(q.w, v[i][6], v[i][7]);
+      load8v(xr + c * 8, plane, split != 0, v[i]);
 #pragma unroll
       for (int t = 0; t < 8; ++t) s += v[i][t];
     } else {
@@ -69,17 +66,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
     float o[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) o[t] = (v[i][t] - mean) * inv * g[c * 8 + t] + b[c * 8 + t];
-    *reinterpret_cast<uint4*>(y + row * C + c * 8) =
-        make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+    store8v(y + row * C + c * 8, plane, split != 0, o);
   }
 }
 
 // out[b, 0, :] = cls + pos[0];  out[b, 1 + s, :] = patches[b, s, :] + pos[1 + s]
 __global__ void tokens_kernel(const uint16_t* __restrict__ patches, const float* __restrict__ cls,
-                              const float* __restrict__ pos, uint16_t* __restrict__ out, int B, int S0, int C) {
+                              const float* __restrict__ pos, uint16_t* __restrict__ out, int B, int S0, int C,
+                              int split) {
   const int S = S0 + 1;
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * S * CG;
+  const long long pplane = static_cast<long long>(B) * S0 * C, oplane = static_cast<long long>(B) * S * C;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
     const int cg = static_cast<int>(i % CG);
     const long long r = i / CG;
@@ -90,30 +88,27 @@ __global__ void tokens_kernel(const uint16_t* __restrict__ patches, const float*
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = cls ? cls[cg * 8 + t] : 0.f;
     } else {
-      const uint4 q = *reinterpret_cast<const uint4*>(patches + ((b * S0 + s - 1) * C + cg * 8));
-      unpack2(q.x, v[0], v[1]);
-      unpack2(q.y, v[2], v[3]);
-      unpack2(q.z, v[4], v[5]);
-      unpack2(q.w, v[6], v[7]);
+      load8v(patches + ((b * S0 + s - 1) * C + cg * 8), pplane, split != 0, v);
     }
     if (pos) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += pos[static_cast<long long>(s) * C + cg * 8 + t];
     }
-    *reinterpret_cast<uint4*>(out + i * 8) =
-        make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    store8v(out + i * 8, oplane, split != 0, v);
   }
 }
 
 __global__ void gather_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int S, int idx,
-                                   int C) {
+                                   int C, int split) {
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * CG;
+  const long long xplane = static_cast<long long>(B) * S * C, yplane = static_cast<long long>(B) * C;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
     const long long b = i / CG;
     const int cg = static_cast<int>(i % CG);
-    *reinterpret_cast<uint4*>(y + i * 8) =
-        *reinterpret_cast<const uint4*>(x + ((b * S + idx) * C + cg * 8));
+    const uint16_t* src = x + ((b * S + idx) * C + cg * 8);
+    *reinterpret_cast<uint4*>(y + i * 8) = *reinterpret_cast<const uint4*>(src);
+    if (split) *reinterpret_cast<uint4*>(y + yplane + i * 8) = *reinterpret_cast<const uint4*>(src + xplane);
   }
 }
 
@@ -139,39 +134,52 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const uint16_t* p) {
       (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
 }
 
-template <int NKT>
+// SPLIT (fp32 mode): Q, K, V and the output are hi/lo planes; K and V stage both planes in LDS,
+// S = K_hi Q_hi + K_lo Q_hi + K_hi Q_lo and O += V_hi P_hi + V_lo P_hi + V_hi P_lo with P split in
+// registers (p_hi = bf16(p), p_lo = bf16(p - p_hi)).  LDS: 2 x (SK x 64 + SK x 96) bf16 -> SK <= 224.
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) { return make_uint2(pack2(a, b), pack2(c, d)); }
+
+template <int NKT, bool SPLIT = false>
 __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                                                         const uint16_t* __restrict__ v, uint16_t* __restrict__ out,
                                                         int S, int ldq, int ldk, int ldv, int ldo, float scale_log2) {
+  constexpr int NP = SPLIT ? 2 : 1;
   constexpr int SK = NKT * 32;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[SK * AT_D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[SK * VP];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NP][SK * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[NP][SK * VP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.y, b = blockIdx.z;
   const long long rowbase = static_cast<long long>(b) * S;
+  const long long rows = static_cast<long long>(gridDim.z) * S;  // plane distances: rows x pitch
   for (int i = tid; i < SK * 8; i += 256) {
     const int s = i >> 3, c = i & 7;
-    uint4 kq = make_uint4(0, 0, 0, 0), vq = make_uint4(0, 0, 0, 0);
-    if (s < S) {
-      kq = *reinterpret_cast<const uint4*>(k + (rowbase + s) * ldk + h * AT_D + c * 8);
-      vq = *reinterpret_cast<const uint4*>(v + (rowbase + s) * ldv + h * AT_D + c * 8);
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      uint4 kq = make_uint4(0, 0, 0, 0), vq = make_uint4(0, 0, 0, 0);
+      if (s < S) {
+        kq = *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * AT_D + c * 8);
+        vq = *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * AT_D + c * 8);
+      }
+      *reinterpret_cast<uint4*>(Ks[pl] + s * AT_D + ((c ^ ((s >> 1) & 7)) << 3)) = kq;
+      *reinterpret_cast<uint4*>(Vs[pl] + s * VP + c * 8) = vq;
     }
-    *reinterpret_cast<uint4*>(Ks + s * AT_D + ((c ^ ((s >> 1) & 7)) << 3)) = kq;
-    *reinterpret_cast<uint4*>(Vs + s * VP + c * 8) = vq;
   }
   __syncthreads();
   const int q0 = (blockIdx.x * 4 + wave) * 32;
   if (q0 >= S) return;  // whole wave (EXEC stays full for the transposed reads)
   const int r = lane & 31, hh = lane >> 5;
-  bf16x8 qf[4];
+  bf16x8 qf[NP][4];
   {
     const int qr = q0 + r;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      uint4 t = make_uint4(0, 0, 0, 0);
-      if (qr < S) t = *reinterpret_cast<const uint4*>(q + (rowbase + qr) * ldq + h * AT_D + ks * 16 + hh * 8);
-      qf[ks] = __builtin_bit_cast(bf16x8, t);
-    }
+    for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        uint4 t = make_uint4(0, 0, 0, 0);
+        if (qr < S)
+          t = *reinterpret_cast<const uint4*>(q + pl * rows * ldq + (rowbase + qr) * ldq + h * AT_D + ks * 16 + hh * 8);
+        qf[pl][ks] = __builtin_bit_cast(bf16x8, t);
+      }
   }
   f32x16 o0, o1;
 #pragma unroll
@@ -186,8 +194,14 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int key = kt * 32 + r, chunk = 2 * ks + hh;
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + key * AT_D + ((chunk ^ ((key >> 1) & 7)) << 3));
-      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc, 0, 0, 0);
+      const int ko = key * AT_D + ((chunk ^ ((key >> 1) & 7)) << 3);
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks[0] + ko);
+      if constexpr (SPLIT) {
+        const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Ks[1] + ko);
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[0][ks], sc, 0, 0, 0);
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[NP - 1][ks], sc, 0, 0, 0);
+      }
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][ks], sc, 0, 0, 0);
     }
     float mt = -INFINITY;
 #pragma unroll
@@ -215,18 +229,28 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
     m = mn;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      bf16x8 pf;
+      bf16x8 pf, pfl;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pf[j] = static_cast<__bf16>(sc[8 * st + j]);
-      const uint16_t* vrow = Vs + (kt * 32 + 16 * st + 4 * hh + qq) * VP + 16 * g + 4 * pp;
+      for (int j = 0; j < 8; ++j) {
+        pf[j] = static_cast<__bf16>(sc[8 * st + j]);
+        if constexpr (SPLIT) pfl[j] = static_cast<__bf16>(sc[8 * st + j] - static_cast<float>(pf[j]));
+      }
+      const int vo = (kt * 32 + 16 * st + 4 * hh + qq) * VP + 16 * g + 4 * pp;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const s16x4 lo = ds_read_tr16(vrow + dt * 32);
-        const s16x4 hi = ds_read_tr16(vrow + 8 * VP + dt * 32);
-        const s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 af = __builtin_bit_cast(bf16x8, a8);
-        if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o0, 0, 0, 0);
-        else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o1, 0, 0, 0);
+        const s16x4 lo = ds_read_tr16(Vs[0] + vo + dt * 32);
+        const s16x4 hi = ds_read_tr16(Vs[0] + vo + 8 * VP + dt * 32);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        f32x16& o = dt == 0 ? o0 : o1;
+        if constexpr (SPLIT) {
+          const s16x4 lo2 = ds_read_tr16(Vs[NP - 1] + vo + dt * 32);
+          const s16x4 hi2 = ds_read_tr16(Vs[NP - 1] + vo + 8 * VP + dt * 32);
+          const bf16x8 al =
+              __builtin_bit_cast(bf16x8, s16x8{lo2[0], lo2[1], lo2[2], lo2[3], hi2[0], hi2[1], hi2[2], hi2[3]});
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, pf, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pfl, o, 0, 0, 0);
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o, 0, 0, 0);
       }
     }
   }
@@ -235,13 +259,26 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
   if (qr >= S) return;
   const float inv = 1.f / l;
   uint16_t* orow = out + (rowbase + qr) * ldo + h * AT_D;
+  const long long oplane = rows * ldo;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
     const int d = 8 * g4 + 4 * hh;
-    *reinterpret_cast<uint2*>(orow + d) =
-        make_uint2(pack2(o0[4 * g4] * inv, o0[4 * g4 + 1] * inv), pack2(o0[4 * g4 + 2] * inv, o0[4 * g4 + 3] * inv));
-    *reinterpret_cast<uint2*>(orow + 32 + d) =
-        make_uint2(pack2(o1[4 * g4] * inv, o1[4 * g4 + 1] * inv), pack2(o1[4 * g4 + 2] * inv, o1[4 * g4 + 3] * inv));
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const f32x16& o = half ? o1 : o0;
+      float w[4] = {o[4 * g4] * inv, o[4 * g4 + 1] * inv, o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv};
+      uint16_t* dst = orow + 32 * half + d;
+      if constexpr (SPLIT) {
+        uint16_t hv[4], lv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) split1(w[t], hv[t], lv[t]);
+        *reinterpret_cast<uint2*>(dst) = make_uint2(hv[0] | (uint32_t(hv[1]) << 16), hv[2] | (uint32_t(hv[3]) << 16));
+        *reinterpret_cast<uint2*>(dst + oplane) =
+            make_uint2(lv[0] | (uint32_t(lv[1]) << 16), lv[2] | (uint32_t(lv[3]) << 16));
+      } else {
+        *reinterpret_cast<uint2*>(dst) = pack4(w[0], w[1], w[2], w[3]);
+      }
+    }
   }
 }
 
@@ -254,37 +291,44 @@ inline int grid_for(long long work, int cap = 4096) {
 }  // namespace
 
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s) {
+                          long long rows, int C, hipStream_t s, int split) {
   if (C % 8) return hipErrorInvalidValue;
   const int blocks = static_cast<int>((rows + 3) / 4);
-  if (C <= 64 * 8) hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C);
-  else if (C <= 128 * 8) hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C);
-  else if (C <= 256 * 8) hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C);
+  if (C <= 64 * 8) hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
+  else if (C <= 128 * 8) hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
+  else if (C <= 256 * 8) hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
-                           int C, hipStream_t s) {
+                           int C, hipStream_t s, int split) {
   if (C % 8) return hipErrorInvalidValue;
   hipLaunchKernelGGL(tokens_kernel, dim3(grid_for(static_cast<long long>(B) * (S0 + 1) * (C / 8))), dim3(256), 0, s,
-                     patches, cls, pos, out, B, S0, C);
+                     patches, cls, pos, out, B, S0, C, split);
   return hipGetLastError();
 }
 
-hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s) {
+hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s, int split) {
   if (C % 8 || idx < 0 || idx >= S) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(static_cast<long long>(B) * (C / 8))), dim3(256), 0, s, x, y, B,
-                     S, idx, C);
+                     S, idx, C, split);
   return hipGetLastError();
 }
 
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
-                     int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s) {
+                     int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
   if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
   const int qtiles = (S + 31) / 32;
   dim3 grid((qtiles + 3) / 4, H, B);
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
+  if (split) {
+    if (S <= 64) hipLaunchKernelGGL((attention_kernel<2, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (S <= 128) hipLaunchKernelGGL((attention_kernel<4, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (S <= 224) hipLaunchKernelGGL((attention_kernel<7, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (S <= 64) hipLaunchKernelGGL(attention_kernel<2>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
   else if (S <= 128) hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
   else if (S <= 224) hipLaunchKernelGGL(attention_kernel<7>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);

@@ -547,29 +547,29 @@ def _sig_kernels():
         return L
     u64, i = C.c_uint64, C.c_int
     L.die_plan_summary.restype = C.c_void_p
-    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.die_kern_conv.restype = i
     L.die_kern_conv.argtypes = [C.c_char_p] + [u64] * 9 + [i, u64]
     L.die_kern_input_prep.restype = i
-    L.die_kern_input_prep.argtypes = [u64] * 4 + [i] * 5 + [u64]
+    L.die_kern_input_prep.argtypes = [u64] * 4 + [i] * 5 + [u64, i]
     L.die_kern_pool2d.restype = i
-    L.die_kern_pool2d.argtypes = [u64, u64] + [i] * 14 + [u64]
+    L.die_kern_pool2d.argtypes = [u64, u64] + [i] * 14 + [u64, i]
     L.die_kern_gap.restype = i
-    L.die_kern_gap.argtypes = [u64] * 5 + [i] * 4 + [u64]
+    L.die_kern_gap.argtypes = [u64] * 5 + [i] * 4 + [u64, i]
     L.die_kern_affine.restype = i
-    L.die_kern_affine.argtypes = [u64] * 4 + [i, u64, C.c_longlong, i, u64]
+    L.die_kern_affine.argtypes = [u64] * 4 + [i, u64, C.c_longlong, i, u64, i]
     L.die_kern_nhwc_to_nchw.restype = i
-    L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64]
+    L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64, i]
     L.die_kern_stem.restype = i
     L.die_kern_stem.argtypes = [u64] * 4 + [i] * 6 + [u64]
     L.die_kern_layernorm.restype = i
-    L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64]
+    L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64, i]
     L.die_kern_tokens.restype = i
-    L.die_kern_tokens.argtypes = [u64] * 4 + [i] * 3 + [u64]
+    L.die_kern_tokens.argtypes = [u64] * 4 + [i] * 3 + [u64, i]
     L.die_kern_gather_rows.restype = i
-    L.die_kern_gather_rows.argtypes = [u64, u64] + [i] * 4 + [u64]
+    L.die_kern_gather_rows.argtypes = [u64, u64] + [i] * 4 + [u64, i]
     L.die_kern_attention.restype = i
-    L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64]
+    L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64, i]
     L.die_decode_scratch_bytes.restype = C.c_longlong
     L.die_decode_scratch_bytes.argtypes = [i, C.c_longlong]
     L.die_kern_decode.restype = i
@@ -580,10 +580,12 @@ def _sig_kernels():
     return L
 
 
-def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False) -> Dict[str, Any]:
+def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False,
+                 precision: str = "bf16") -> Dict[str, Any]:
+    """precision "fp32" plans the split (hi, lo) kernels of the HIP engine's default mode."""
     L = _sig_kernels()
     err = _err_box()
-    p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), C.byref(err))
+    p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), int(precision == "fp32"), C.byref(err))
     if not p:
         _raise_if(err, "plan")
     return json.loads(_take_str(p))

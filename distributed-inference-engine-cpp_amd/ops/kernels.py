@@ -36,8 +36,25 @@ def bf16_bits(t):
     return t.contiguous().view(torch.int16)
 
 
-def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128):
-    """[Cout, Cin, KH, KW] float -> [Npad][Kpad] bf16 with k = (ky*KW + kx)*Cin_store + ci."""
+def split_planes(t):
+    """fp32 tensor -> its split form (csrc/kernels/common.h): [2, *shape] bf16, plane 0 = hi = bf16(t),
+    plane 1 = lo = bf16(t - hi) (both round to nearest even, like the device)."""
+    import torch
+
+    t = t.float()
+    hi = t.to(torch.bfloat16)
+    lo = (t - hi.float()).to(torch.bfloat16)
+    return torch.stack([hi, lo]).contiguous()
+
+
+def join_planes(p):
+    """[2, ...] split planes -> fp32 (hi + lo)."""
+    return p[0].float() + p[1].float()
+
+
+def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split: bool = False):
+    """[Cout, Cin, KH, KW] float -> [Npad][Kpad] bf16 with k = (ky*KW + kx)*Cin_store + ci.
+    split: [2][Npad][Kpad] (hi plane, then lo plane)."""
     import torch
 
     cout, cin, kh, kw = w.shape
@@ -48,23 +65,26 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128):
     wp = torch.zeros((Np, kh, kw, cs), dtype=torch.float32, device=w.device)
     wp[:cout, :, :, :cin] = w.permute(0, 2, 3, 1).float()
     wp = wp.reshape(Np, K)
-    out = torch.zeros((Np, Kpad), dtype=torch.bfloat16, device=w.device)
-    out[:, :K] = wp.to(torch.bfloat16)
+    full = torch.zeros((Np, Kpad), dtype=torch.float32, device=w.device)
+    full[:, :K] = wp
+    out = split_planes(full) if split else full.to(torch.bfloat16)
     return out, K, Kpad
 
 
 class ConvProblem:
     """One implicit-GEMM conv problem with packed weights and preallocated outputs, re-launchable with
     any (config, split-K, fused) choice -- used by conv2d_nhwc and by tools/conv_bench.py.
-    x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float."""
+    x_nhwc: [B,H,W,Cin] bf16 (split: any float dtype, converted to hi/lo planes), w: [Cout,Cin,KH,KW]
+    float.  split = fp32 mode: x/res/out/out2 are split planes and the weights are packed hi + lo."""
 
     def __init__(self, x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
-                 scale2=None, shift2=None, relu2=False, max_splits=16):
+                 scale2=None, shift2=None, relu2=False, max_splits=16, split=False):
         import torch
 
         B, H, W, Cs = x_nhwc.shape
         cout, cin, kh, kw = w.shape
-        self.wp, K, Kpad = pack_conv_weight(w, Cs)
+        self.split = split
+        self.wp, K, Kpad = pack_conv_weight(w, Cs, split=split)
         Ho = (H + 2 * pad - dil * (kh - 1) - 1) // stride + 1
         Wo = (W + 2 * pad - dil * (kw - 1) - 1) // stride + 1
         dev = x_nhwc.device
@@ -77,14 +97,19 @@ class ConvProblem:
             o[: v.numel()] = v.float()
             return o
 
-        self.x = x_nhwc.contiguous()
-        self.res = res.contiguous() if res is not None else None
+        np_ = (2,) if split else ()
+        self.x = split_planes(x_nhwc) if split else x_nhwc.contiguous()
+        self.res = None if res is None else (split_planes(res.reshape(B, Ho, Wo, cout)) if split else res.contiguous())
         self.bias_p, self.s2_p, self.b2_p = padded(bias), padded(scale2), padded(shift2)
         self.out_f32 = out_f32
-        self.out = torch.empty((B, Ho, Wo, cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
-        self.out2 = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev) if scale2 is not None else None
+        self.out = (torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=dev) if out_f32 else
+                    torch.empty(np_ + (B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev))
+        self.out2 = (torch.empty(np_ + (B, Ho, Wo, cout), dtype=torch.bfloat16, device=dev)
+                     if scale2 is not None else None)
         self.geom = dict(B=B, H=H, W=W, Cin=Cs, Ho=Ho, Wo=Wo, N=cout, KH=kh, KW=kw, stride=stride, pad_h=pad,
                          pad_w=pad, dil=dil, K=K, Kpad=Kpad, relu=int(relu), relu2=int(relu2))
+        if split:
+            self.geom.update(split=1, wplane=int(self.wp[0].numel()))
         self.zeros = torch.zeros(Kpad + 64, dtype=torch.int16, device=dev)  # zero page >= Kpad + 64
         self.geom["zeros"] = int(self.zeros.data_ptr())
         self.ws = torch.empty(max(1, max_splits) * B * Ho * Wo * cout if max_splits > 1 else 1, dtype=torch.float32,
@@ -108,114 +133,133 @@ class ConvProblem:
                                      _ptr(self.out) if self.out_f32 else 0, _ptr(self.s2_p), _ptr(self.b2_p),
                                      _ptr(self.out2), tile, _stream())
 
+    def results(self):
+        """(out, out2); split planes joined to fp32."""
+        if not self.split:
+            return self.out, self.out2
+        out = self.out if self.out_f32 else join_planes(self.out)
+        return out, None if self.out2 is None else join_planes(self.out2)
+
 
 def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=None, out_f32=False,
-                scale2=None, shift2=None, relu2=False, tile=-1, splits=1, fused_splitk=True):
+                scale2=None, shift2=None, relu2=False, tile=-1, splits=1, fused_splitk=True, split=False):
     """Implicit-GEMM conv.  x_nhwc: [B,H,W,Cin] bf16, w: [Cout,Cin,KH,KW] float.
-    Returns (out, out2) in NHWC ([B,Ho,Wo,Cout]); out is f32 if out_f32 else bf16."""
-    pr = ConvProblem(x_nhwc, w, bias, stride, pad, dil, relu, res, out_f32, scale2, shift2, relu2, max_splits=splits)
+    Returns (out, out2) in NHWC ([B,Ho,Wo,Cout]); out is f32 if out_f32 else bf16.
+    split (fp32 mode): x/res any float dtype; outputs are the fp32 values of the split planes."""
+    pr = ConvProblem(x_nhwc, w, bias, stride, pad, dil, relu, res, out_f32, scale2, shift2, relu2, max_splits=splits,
+                     split=split)
     rc = pr.launch(tile, splits, fused_splitk)
     if rc != 0 and tile >= 0 and rc == 1:  # hipErrorInvalidValue: config not applicable to this shape
         return None, None
     _check(rc, "conv_igemm")
-    return pr.out, pr.out2
+    return pr.results()
 
 
-def input_prep(x_nchw, scale=None, shift=None, cp=4):
+def _in(x, split):
+    return split_planes(x) if split else x.contiguous()
+
+
+def _out(y, split):
+    return join_planes(y) if split else y
+
+
+def input_prep(x_nchw, scale=None, shift=None, cp=4, split=False):
     import torch
 
     B, C, H, W = x_nchw.shape
-    out = torch.empty((B, H, W, cp), dtype=torch.bfloat16, device=x_nchw.device)
+    out = torch.empty(((2,) if split else ()) + (B, H, W, cp), dtype=torch.bfloat16, device=x_nchw.device)
     L = native.kernels()
     rc = L.die_kern_input_prep(_ptr(x_nchw.contiguous().float()), _ptr(scale), _ptr(shift), _ptr(out), B, C, H, W, cp,
-                               _stream())
+                               _stream(), int(split))
     _check(rc, "input_prep")
-    return out
+    return _out(out, split)
 
 
-def pool2d_nhwc(x, k, stride, pad, is_max=True, count_include_pad=False):
+def pool2d_nhwc(x, k, stride, pad, is_max=True, count_include_pad=False, split=False):
     import torch
 
     B, H, W, C = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
-    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
-    rc = native.kernels().die_kern_pool2d(_ptr(x.contiguous()), _ptr(y), B, H, W, C, Ho, Wo, k, k, stride, stride, pad,
-                                          pad, int(is_max), int(count_include_pad), _stream())
+    y = torch.empty(((2,) if split else ()) + (B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    rc = native.kernels().die_kern_pool2d(_ptr(_in(x, split)), _ptr(y), B, H, W, C, Ho, Wo, k, k, stride, stride, pad,
+                                          pad, int(is_max), int(count_include_pad), _stream(), int(split))
     _check(rc, "pool2d")
-    return y
+    return _out(y, split)
 
 
-def global_avgpool_nhwc(x, scale=None, shift=None, relu=False):
+def global_avgpool_nhwc(x, scale=None, shift=None, relu=False, split=False):
     import torch
 
     B, H, W, C = x.shape
-    out = torch.empty((B, C), dtype=torch.bfloat16, device=x.device)
+    out = torch.empty(((2,) if split else ()) + (B, C), dtype=torch.bfloat16, device=x.device)
     out32 = torch.empty((B, C), dtype=torch.float32, device=x.device)
-    rc = native.kernels().die_kern_gap(_ptr(x.contiguous()), _ptr(out), _ptr(out32), _ptr(scale), _ptr(shift),
-                                       int(relu), B, H * W, C, _stream())
+    rc = native.kernels().die_kern_gap(_ptr(_in(x, split)), _ptr(out), _ptr(out32), _ptr(scale), _ptr(shift),
+                                       int(relu), B, H * W, C, _stream(), int(split))
     _check(rc, "global_avgpool")
-    return out, out32
+    return _out(out, split), out32
 
 
-def affine_act(x, scale=None, shift=None, z=None, relu=False):
+def affine_act(x, scale=None, shift=None, z=None, relu=False, split=False):
     import torch
 
     C = x.shape[-1]
     M = x.numel() // C
-    y = torch.empty_like(x)
-    rc = native.kernels().die_kern_affine(_ptr(x.contiguous()), _ptr(z), _ptr(scale), _ptr(shift), int(relu), _ptr(y),
-                                          M, C, _stream())
+    y = torch.empty(((2,) if split else ()) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+    zz = None if z is None else _in(z, split)
+    rc = native.kernels().die_kern_affine(_ptr(_in(x, split)), _ptr(zz), _ptr(scale), _ptr(shift), int(relu), _ptr(y),
+                                          M, C, _stream(), int(split))
     _check(rc, "affine_act")
-    return y
+    return _out(y, split)
 
 
 # ---- transformer kernels (csrc/kernels/transformer.hip) ---------------------------------------------
 
-def linear(x, w, bias=None, act=0, res=None, tile=-1, splits=1):
+def linear(x, w, bias=None, act=0, res=None, tile=-1, splits=1, split=False):
     """Rows GEMM on the MFMA conv kernel: x [..., K] bf16, w [N, K] float -> act(x @ w^T + bias + res).
-    act: 0 none, 1 relu, 2 erf-GELU."""
+    act: 0 none, 1 relu, 2 erf-GELU.  split: fp32 mode (fp32 result)."""
     K = x.shape[-1]
     lead = x.shape[:-1]
     M = x.numel() // K
     N = w.shape[0]
     r = None if res is None else res.reshape(M, 1, 1, N)
     out, _ = conv2d_nhwc(x.reshape(M, 1, 1, K), w.reshape(N, K, 1, 1), bias=bias, relu=act, res=r, tile=tile,
-                         splits=splits)
+                         splits=splits, split=split)
     return None if out is None else out.reshape(*lead, N)
 
 
-def layernorm(x, gamma, beta, eps=1e-5):
+def layernorm(x, gamma, beta, eps=1e-5, split=False):
     import torch
 
     C = x.shape[-1]
-    y = torch.empty_like(x)
-    rc = native.kernels().die_kern_layernorm(_ptr(x.contiguous()), _ptr(y), _ptr(gamma.float().contiguous()),
-                                             _ptr(beta.float().contiguous()), float(eps), x.numel() // C, C, _stream())
+    y = torch.empty(((2,) if split else ()) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+    rc = native.kernels().die_kern_layernorm(_ptr(_in(x, split)), _ptr(y), _ptr(gamma.float().contiguous()),
+                                             _ptr(beta.float().contiguous()), float(eps), x.numel() // C, C, _stream(),
+                                             int(split))
     _check(rc, "layernorm")
-    return y
+    return _out(y, split)
 
 
-def tokens_assemble(patches, cls=None, pos=None):
+def tokens_assemble(patches, cls=None, pos=None, split=False):
     """patches [B, S0, C] bf16, cls [C] f32, pos [S0+1, C] f32 -> [B, S0+1, C] bf16."""
     import torch
 
     B, S0, C = patches.shape
-    out = torch.empty((B, S0 + 1, C), dtype=torch.bfloat16, device=patches.device)
-    rc = native.kernels().die_kern_tokens(_ptr(patches.contiguous()), _ptr(cls), _ptr(pos), _ptr(out), B, S0, C,
-                                          _stream())
+    out = torch.empty(((2,) if split else ()) + (B, S0 + 1, C), dtype=torch.bfloat16, device=patches.device)
+    rc = native.kernels().die_kern_tokens(_ptr(_in(patches, split)), _ptr(cls), _ptr(pos), _ptr(out), B, S0, C,
+                                          _stream(), int(split))
     _check(rc, "tokens_assemble")
-    return out
+    return _out(out, split)
 
 
-def gather_rows(x, idx):
+def gather_rows(x, idx, split=False):
     import torch
 
     B, S, C = x.shape
-    y = torch.empty((B, C), dtype=x.dtype, device=x.device)
-    rc = native.kernels().die_kern_gather_rows(_ptr(x.contiguous()), _ptr(y), B, S, int(idx), C, _stream())
+    y = torch.empty(((2,) if split else ()) + (B, C), dtype=torch.bfloat16 if split else x.dtype, device=x.device)
+    rc = native.kernels().die_kern_gather_rows(_ptr(_in(x, split)), _ptr(y), B, S, int(idx), C, _stream(), int(split))
     _check(rc, "gather_rows")
-    return y
+    return _out(y, split)
 
 
 def attention(q, k, v, heads, scale=None):
@@ -230,9 +274,27 @@ def attention(q, k, v, heads, scale=None):
     out = torch.empty((B, S, C), dtype=torch.bfloat16, device=q.device)
     sc = float(scale if scale is not None else 1.0 / np.sqrt(D))
     rc = native.kernels().die_kern_attention(_ptr(q), _ptr(k), _ptr(v), _ptr(out), B, S, heads, D, q.stride(1),
-                                             k.stride(1), v.stride(1), C, sc, _stream())
+                                             k.stride(1), v.stride(1), C, sc, _stream(), 0)
     _check(rc, "attention")
     return out
+
+
+def attention_qkv_split(qkv, heads, scale=None):
+    """fp32 mode: qkv [B, S, 3*C] float (Q | K | V columns) -> fp32 [B, S, C] through the split kernel
+    (planes of the packed QKV rows, like the engine's fused QKV GEMM output)."""
+    import torch
+
+    B, S, C3 = qkv.shape
+    C = C3 // 3
+    D = C // heads
+    planes = split_planes(qkv)  # [2, B, S, 3C]
+    out = torch.empty((2, B, S, C), dtype=torch.bfloat16, device=qkv.device)
+    sc = float(scale if scale is not None else 1.0 / np.sqrt(D))
+    base = _ptr(planes)
+    rc = native.kernels().die_kern_attention(base, base + 2 * C, base + 4 * C, _ptr(out), B, S, heads, D, C3, C3, C3,
+                                             C, sc, _stream(), 1)
+    _check(rc, "attention (split)")
+    return join_planes(out)
 
 
 # ---- device JSON decode (csrc/kernels/decode.hip) ---------------------------------------------------

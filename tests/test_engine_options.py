@@ -1,12 +1,12 @@
-"""Engine option semantics that hold on any host: precision routing (fp32 never silently runs on
-the bf16 HIP kernels) and option validation."""
+"""Engine option semantics that hold on any host: precision selection (fp32 is the default, bf16
+the opt-in fast mode) and option validation."""
 import numpy as np
 import pytest
 
 
-def test_fp32_precision_routes_to_cpu_executor(native, models):
+def test_fp32_precision_on_cpu_executor(native, models):
     path, _, _ = models["tiny"]
-    e = native.Engine(path, device="auto", precision="fp32", max_batch=2)
+    e = native.Engine(path, device="cpu", precision="fp32", max_batch=2)
     try:
         assert e.info["device"].startswith("cpu"), e.info["device"]
         x = np.random.default_rng(0).random((2, e.input_numel), dtype=np.float32)
@@ -16,9 +16,13 @@ def test_fp32_precision_routes_to_cpu_executor(native, models):
         e.close()
 
 
-def test_fp32_on_hip_is_rejected(native, models):
+def test_hip_without_gpu_fails_loudly(native, models):
+    from conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("a GPU is visible")
     path, _, _ = models["tiny"]
-    with pytest.raises(Exception, match="fp32"):
+    with pytest.raises(Exception, match="HIP engine unavailable"):
         native.Engine(path, device="hip", precision="fp32")
 
 
