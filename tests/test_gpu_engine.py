@@ -24,11 +24,13 @@ def test_hip_engine_tiny_vs_cpu(native, models):
     x = r.synthetic_input(5, cfg)
     got = e.run(x.reshape(5, -1))
     ref = native.cpu_run(path, x)
-    assert rel_l2(got, ref) < 2e-2, rel_l2(got, ref)
-    assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.8
-    # padding invariance: sample 0 alone (bucket 1) == sample 0 inside a batch of 5 (bucket 8)
+    assert e.info["precision"] == "fp32"  # the default, like the reference's ORT session
+    assert rel_l2(got, ref) < 1e-4, rel_l2(got, ref)
+    assert (got.argmax(1) == ref.argmax(1)).all()
+    # padding invariance: sample 0 alone (bucket 1) == sample 0 inside a batch of 5 (bucket 8); the
+    # buckets may use different tuned split-K orders, so equal up to fp32 re-association
     one = e.run(x[:1].reshape(1, -1))
-    np.testing.assert_allclose(one[0], got[0], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(one[0], got[0], rtol=1e-4, atol=1e-5)
     e.close()
 
 
@@ -46,8 +48,8 @@ def test_hip_engine_resnet50_vs_torch(native, models):
     with torch.no_grad():
         ref = r.torch_forward(w, x, cfg, device="cuda").cpu().numpy()
     err = rel_l2(got, ref)
-    assert err < 3e-2, err
-    assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.75
+    assert err < 1e-4, err
+    assert (got.argmax(1) == ref.argmax(1)).all()
     # short input -> zero padded (reference semantics)
     short = e.run(np.array([[1.0, 2.0, 3.0]], np.float32))
     full = np.zeros((1, 3 * 224 * 224), np.float32)

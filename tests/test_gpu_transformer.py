@@ -140,9 +140,10 @@ def test_vit_tiny_engine_vs_torch(native, models):
     with torch.no_grad():
         ref = vit.torch_forward(w, x, cfg).numpy()
     err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
-    assert err < 3e-2, err
+    assert err < 1e-4, err  # fp32 engine (default precision)
+    assert (got.argmax(1) == ref.argmax(1)).all()
     one = e.run(x[:1].reshape(1, -1))
-    np.testing.assert_allclose(one[0], got[0], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(one[0], got[0], rtol=1e-4, atol=1e-5)
     e.close()
 
 
@@ -160,6 +161,6 @@ def test_vit_base_engine_vs_torch(native, models):
     with torch.no_grad():
         ref = vit.torch_forward(w, x, cfg, device="cuda").cpu().numpy()
     err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
-    assert err < 5e-2, err
-    assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.75
+    assert err < 1e-4, err  # fp32 engine (default precision)
+    assert (got.argmax(1) == ref.argmax(1)).all()
     e.close()
