@@ -1,16 +1,22 @@
 """Headline benchmark: requests/sec (+ p50/p99 latency) of ResNet50-v2 `/infer` on MI355X.
 
 Reference headline (README.md:276-289): 522.64 req/s, p50 84.6 ms at 10k requests /
-50 client threads through HTTP/JSON.  Here every rank runs the full serving path on its own GPU:
-an in-process worker node (C++ epoll HTTP server, JSON decode straight into pinned staging, LRU
-cache, dynamic batcher at max batch 32, HIP engine with hipGraph-captured forward) driven by a
-C++ closed-loop client with 50 keep-alive connections per GPU.  Payloads are ResNet-shaped
-(3x224x224 floats, 4 decimals, ~1.1 MB of JSON) and unique per request, so every request is a real
-inference (no cache hits).  Weights are random-init (no checkpoint offline).
+50 client threads through the gateway (benchmark.py:26-30 -> src/gateway.cpp:176-198 -> worker).
+Same topology here (default --mode gateway): every rank runs a worker node on its own GPU (C++
+epoll HTTP server, JSON text decoded on the GPU, LRU cache, dynamic batcher at max batch 32, HIP
+engine with hipGraph-captured forward passes, fp32 numerics like the reference's ORT session) and
+a gateway (consistent-hash routing on request_id over ALL ranks' workers, circuit breakers,
+event-driven keep-alive forwarding), driven by a C++ closed-loop client with 50 keep-alive
+connections per GPU into that gateway.  Payloads are ResNet-shaped (3x224x224 floats, 4 decimals,
+~1.1 MB of JSON) and unique per request, so every request is a real inference (no cache hits).
+Weights are random-init (no checkpoint offline).
 
-A "step" = one batch worth (32) of requests per GPU.  W warmup steps, then exactly K timed steps
-bracketed by barrier + torch.cuda.synchronize(); the max wall time over ranks is the job time and
-`value` = total successful requests / that time (whole job, all GPUs).
+A "step" = --step-requests (500) requests per GPU, so the driver's `--steps 20` times 10,000
+requests per GPU: the reference's run length.  W warmup steps (after engine autotune and graph
+capture), then exactly K timed steps bracketed by barrier + torch.cuda.synchronize(); the max wall
+time over ranks is the job time and `value` = total successful requests / that time (whole job,
+all GPUs).  The same count of requests sent straight to the worker (no gateway hop) is reported as
+the extra key `direct_worker`.
 """
 import argparse
 import json
@@ -36,13 +42,19 @@ def _cpu_quota():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--step-requests", type=int, default=500,
+                    help="requests per GPU per step (20 steps = the reference's 10k requests)")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--connections", type=int, default=50, help="client connections per GPU (reference: 50 threads)")
-    ap.add_argument("--mode", choices=["http", "dp", "engine"], default="http",
-                    help="http: one serving replica per GPU (worker + client per rank); dp: ONE worker whose "
-                         "batches are sharded over all ranks (RCCL); engine: forward-only")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32 = the reference's numerics (split bf16 MFMA); bf16 = fast mode")
+    ap.add_argument("--mode", choices=["gateway", "http", "dp", "engine"], default="gateway",
+                    help="gateway: client -> gateway -> worker per GPU (reference topology); http: client -> "
+                         "worker; dp: ONE worker whose batches are sharded over all ranks (RCCL); engine: "
+                         "forward-only (a step = one batch)")
+    ap.add_argument("--no-direct", action="store_true", help="skip the extra direct-to-worker measurement")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
@@ -62,6 +74,9 @@ def main():
     ap.add_argument("--device", choices=["hip", "cpu"], default="hip",
                     help="cpu: rehearse the multi-rank contract on the host executor (tests; no GPU)")
     args = ap.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        # n_gpus and global_batch come from --gpus: a torchrun launch must say how many ranks it has
+        ap.error("--gpus %d does not match WORLD_SIZE %s" % (args.gpus, os.environ.get("WORLD_SIZE", "1")))
 
     # rank 0's stdout carries exactly ONE JSON line: library chatter written to fd 1 while the
     # job runs (RCCL's version banner at communicator init, ROCm runtime notes) goes to stderr.
@@ -122,25 +137,38 @@ def main():
     numel = cfg.in_ch * cfg.image * cfg.image
     extra = {}
 
-    if args.mode == "http":
+    SR = args.step_requests
+    engine_opts = {"device": args.device, "device_id": dev, "max_batch": B, "precision": args.precision,
+                   "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
+                   "exec_streams": args.exec_streams, "pace": not args.no_pace,
+                   "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
+                   "device_decode": not args.no_device_decode}
+    if args.mode in ("gateway", "http"):
         t_init = time.perf_counter()
-        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B,
-                           engine={"device": args.device, "device_id": dev, "max_batch": B,
-                                   "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
-                                   "exec_streams": args.exec_streams, "pace": not args.no_pace,
-                                   "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
-                                   "device_decode": not args.no_device_decode})
+        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts)
         t_ready = time.perf_counter()
-        lg = dict(port=wk.port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
+        gw = None
+        target_port = wk.port
+        if args.mode == "gateway":
+            # every rank's gateway routes over every rank's worker (ring on request_id)
+            ports = [wk.port]
+            if dist is not None:
+                ports = [None] * world
+                dist.all_gather_object(ports, wk.port)
+            gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports])
+            target_port = gw.port
+        lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
-        native.loadgen(requests=args.warmup * B, warmup=0, id_prefix="warm%d_" % rank, **lg)
+        native.loadgen(port=target_port, requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, **lg)
         h0 = wk.health()
+        g0 = gw.stats() if gw else {}
         barrier()
         t0 = time.perf_counter()
-        res = native.loadgen(requests=args.steps * B, warmup=0, id_prefix="r%d_" % rank, **lg)
+        res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, **lg)
         barrier()
         elapsed = time.perf_counter() - t0
         h1 = wk.health()
+        g1 = gw.stats() if gw else {}
         ok = res["ok"]
         failed = res["failed"]
         bp0, bp1 = h0["batch_processor"], h1["batch_processor"]
@@ -151,20 +179,33 @@ def main():
             "mean_ms": res["latency_ms"]["mean"], "failed": failed,
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
             "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
+            "precision": e1.get("precision"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
             "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
             "cpu_quota": _cpu_quota(), "device_decode": e1.get("device_decode"),
             "decode_fallbacks": h1.get("decode_fallbacks"),
-            "staged_uploads": e1.get("staged_uploads", 0) - e0.get("staged_uploads", 0),
             "pipeline_depth": args.pipeline_depth, "exec_streams": e1.get("executors"),
             "worker_init_s": round(t_ready - t_init, 2),
-            "staging_diag": e1.get("staging_diag"),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
             "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
-            "branch_streams": e1.get("branch_streams"),
             "pace_lead_ms": e1.get("avg_pace_lead_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
         }
+        if gw:
+            extra["gateway"] = {"failovers": g1["failovers"] - g0["failovers"], "failed": g1["failed"] - g0["failed"],
+                                "upstream_connections": g1.get("upstream_connections_opened"),
+                                "breakers": [b["state"] for b in g1["circuit_breakers"]]}
+        if gw and not args.no_direct:
+            # informative: the same request count straight to this rank's worker (no gateway hop)
+            barrier()
+            td = time.perf_counter()
+            rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank, **lg)
+            barrier()
+            el = time.perf_counter() - td
+            extra["direct_worker"] = {"rps_this_rank": rd["ok"] / el, "p50_ms": rd["latency_ms"]["p50"],
+                                      "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"]}
+        if gw:
+            gw.stop()
         wk.stop()
     elif args.mode == "dp":
         # BASELINE config 4: ONE worker whose batches (B per GPU x N GPUs) are sharded over all ranks;
@@ -172,13 +213,14 @@ def main():
         group = "die_bench_dp_%s" % os.environ.get("MASTER_PORT", str(os.getpid()))
         Btot = B * world
         eng_opts = {"device": args.device, "device_id": dev, "pipeline_depth": args.pipeline_depth,
-                    "device_decode": not args.no_device_decode, "dp_world": world, "dp_group": group}
+                    "precision": args.precision, "device_decode": not args.no_device_decode, "dp_world": world,
+                    "dp_group": group}
         res, fol = {"ok": 0, "failed": 0}, None
         if rank == 0:
             wk = native.Worker(model, node_id="dp", max_batch=Btot, engine=eng_opts)
             lg = dict(port=wk.port, connections=args.connections * world, payload="full", input_numel=numel,
                       decimals=4, seed=1000, timeout_ms=60000)
-            native.loadgen(requests=args.warmup * Btot, warmup=0, id_prefix="warm_", **lg)
+            native.loadgen(requests=args.warmup * SR * world, warmup=0, id_prefix="warm_", **lg)
             h0 = wk.health()
         else:
             eng_opts.pop("dp_group")
@@ -187,7 +229,7 @@ def main():
         barrier()
         t0 = time.perf_counter()
         if rank == 0:
-            res = native.loadgen(requests=args.steps * Btot, warmup=0, id_prefix="r_", **lg)
+            res = native.loadgen(requests=args.steps * SR * world, warmup=0, id_prefix="r_", **lg)
         barrier()
         elapsed = time.perf_counter() - t0
         ok, failed = res["ok"], res["failed"]
@@ -207,7 +249,7 @@ def main():
     else:
         import numpy as np
 
-        eng = native.Engine(model, device=args.device, device_id=dev, max_batch=B,
+        eng = native.Engine(model, device=args.device, device_id=dev, max_batch=B, precision=args.precision,
                             pipeline_depth=args.pipeline_depth, branch_streams=args.branch_streams)
         x = r.synthetic_input(B, cfg, seed=rank).reshape(B, -1)
         for _ in range(args.warmup):
@@ -245,11 +287,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": value / BASELINE_RPS if args.arch == "resnet50" else None,
-            "dtype": "bf16" if hip else "fp32",
+            "dtype": args.precision if hip else "fp32",
             "data": "synthetic: unique image-shaped JSON payloads (3x224x224 floats, 4 decimals), random-init weights",
             "config": {"model": model_name, "global_batch": B * args.gpus, "seq_len": 0,
-                       "parallelism": "dp%d" % args.gpus, "mode": args.mode, "max_batch_per_gpu": B,
-                       "requests": int(ok + failed)},
+                       "parallelism": "dp%d" % args.gpus,
+                       "mode": {"gateway": "gateway+worker", "http": "worker"}.get(args.mode, args.mode),
+                       "max_batch_per_gpu": B, "requests": int(ok + failed), "connections_per_gpu": args.connections},
         }
         extra["numa"] = numa
         out.update({k: v for k, v in extra.items() if v is not None})

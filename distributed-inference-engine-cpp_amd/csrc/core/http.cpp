@@ -15,16 +15,18 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <deque>
 #include <unordered_map>
 
+#include "http_util.h"
 #include "json.h"
 #include "sysinfo.h"
 
 namespace die {
 
-namespace {
+namespace http_detail {
 
 struct IgnoreSigpipe {
   IgnoreSigpipe() { signal(SIGPIPE, SIG_IGN); }
@@ -107,7 +109,9 @@ long dechunk(std::string_view data, std::string& out, size_t max_out) {
   }
 }
 
-}  // namespace
+}  // namespace http_detail
+
+using namespace http_detail;
 
 std::string_view HttpRequest::header(std::string_view name) const {
   for (auto& kv : headers)
@@ -144,6 +148,7 @@ struct Mailbox {
   std::vector<Item> items;
   int efd = -1;
   bool open = true;
+  std::atomic<bool> pending{false};  // items waiting: the reactor also checks between events
 
   void post(Item it) {
     {
@@ -151,6 +156,7 @@ struct Mailbox {
       if (!open) return;
       items.push_back(std::move(it));
     }
+    pending.store(true, std::memory_order_release);
     uint64_t one = 1;
     ssize_t r = ::write(efd, &one, sizeof one);
     (void)r;
@@ -375,6 +381,12 @@ void HttpServer::reactor_loop(Reactor* r) {
     h += resp.content_type.empty() ? "text/plain" : resp.content_type;
     h += "\r\nContent-Length: ";
     h += std::to_string(resp.body.size());
+    for (auto& kv : resp.headers) {
+      h += "\r\n";
+      h += kv.first;
+      h += ": ";
+      h += kv.second;
+    }
     h += c->close_after ? "\r\nConnection: close\r\n\r\n" : "\r\nConnection: keep-alive\r\n\r\n";
     c->out_body = std::move(resp.body);
     c->out_off = 0;
@@ -512,6 +524,34 @@ void HttpServer::reactor_loop(Reactor* r) {
     if (c->peer_eof && !c->busy && r->conns.count(c->id)) close_conn(c);
   };
 
+  auto drain_mailbox = [&] {
+    {
+      std::lock_guard<std::mutex> g(r->box->mu);
+      r->box->pending.store(false, std::memory_order_relaxed);
+      drained.swap(r->box->items);
+    }
+    for (auto& it : drained) {
+      auto f = r->conns.find(it.conn_id);
+      if (f == r->conns.end()) continue;
+      HttpResponse resp;
+      if (it.build) {
+        try {
+          resp = it.build();
+        } catch (const std::exception& e) {
+          resp = HttpResponse{};
+          resp.status = 500;
+          Json j = Json::object();
+          j["error"] = e.what();
+          resp.body = j.dump();
+        }
+      } else {
+        resp = std::move(it.resp);
+      }
+      queue_response(f->second.get(), std::move(resp), it.keep_alive);
+    }
+    drained.clear();
+  };
+
   while (running_.load(std::memory_order_relaxed)) {
     int n = epoll_wait(r->ep, events.data(), static_cast<int>(events.size()), 200);
     if (n < 0) {
@@ -538,30 +578,7 @@ void HttpServer::reactor_loop(Reactor* r) {
         uint64_t v;
         ssize_t rd = ::read(r->box->efd, &v, sizeof v);
         (void)rd;
-        {
-          std::lock_guard<std::mutex> g(r->box->mu);
-          drained.swap(r->box->items);
-        }
-        for (auto& it : drained) {
-          auto f = r->conns.find(it.conn_id);
-          if (f == r->conns.end()) continue;
-          HttpResponse resp;
-          if (it.build) {
-            try {
-              resp = it.build();
-            } catch (const std::exception& e) {
-              resp = HttpResponse{};
-              resp.status = 500;
-              Json j = Json::object();
-              j["error"] = e.what();
-              resp.body = j.dump();
-            }
-          } else {
-            resp = std::move(it.resp);
-          }
-          queue_response(f->second.get(), std::move(resp), it.keep_alive);
-        }
-        drained.clear();
+        drain_mailbox();
       } else {
         auto f = r->conns.find(tag);
         if (f == r->conns.end()) continue;
@@ -578,6 +595,10 @@ void HttpServer::reactor_loop(Reactor* r) {
             if (r->conns.count(tag)) close_conn(c);
           }
         }
+        // Completed responses are written between connection events, not after the whole batch of
+        // events: a reactor busy receiving ~1 MB request bodies must not hold finished answers back
+        // (head-of-line blocking of the respond stage).
+        if (r->box->pending.load(std::memory_order_acquire)) drain_mailbox();
       }
     }
   }
@@ -827,6 +848,7 @@ std::optional<HttpResponse> HttpClient::request(const std::string& method, const
               resp.content_type = kv.second;
             }
           }
+          resp.headers = headers;
           if (has_len) buf.reserve(header_end + 4 + content_len + 64);
         }
       }

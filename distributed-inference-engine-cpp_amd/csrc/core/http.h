@@ -39,6 +39,13 @@ struct HttpResponse {
   std::string content_type = "application/json";
   std::string body;
   bool close = false;
+  // extra headers (server: written as given; clients: every received header, names lower-cased)
+  std::vector<std::pair<std::string, std::string>> headers;
+  std::string_view header(std::string_view lower_name) const {
+    for (auto& kv : headers)
+      if (kv.first == lower_name) return kv.second;
+    return {};
+  }
 };
 
 const char* http_status_text(int status);

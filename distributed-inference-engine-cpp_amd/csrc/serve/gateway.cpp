@@ -4,40 +4,6 @@
 
 namespace die {
 
-ThreadPool::ThreadPool(size_t n) {
-  for (size_t i = 0; i < n; ++i)
-    threads_.emplace_back([this] {
-      while (true) {
-        std::function<void()> fn;
-        {
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-          if (q_.empty()) return;
-          fn = std::move(q_.front());
-          q_.pop_front();
-        }
-        fn();
-      }
-    });
-}
-
-ThreadPool::~ThreadPool() {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    stop_ = true;
-  }
-  cv_.notify_all();
-  for (auto& t : threads_) t.join();
-}
-
-void ThreadPool::post(std::function<void()> fn) {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(std::move(fn));
-  }
-  cv_.notify_one();
-}
-
 namespace {
 
 std::string error_body(const std::string& msg) {
@@ -46,27 +12,42 @@ std::string error_body(const std::string& msg) {
   return j.dump();
 }
 
+HttpResponse error_response(const std::string& msg) {
+  HttpResponse r;
+  r.status = 500;
+  r.body = error_body(msg);
+  return r;
+}
+
 }  // namespace
 
+// One request's failover walk: the primary, then the other nodes in ring order
+// (src/gateway.cpp:46-59).
+struct Gateway::Route {
+  std::shared_ptr<const std::string> body;
+  std::function<void(HttpResponse&&)> done;
+  std::string target;
+  std::vector<std::string> order;
+  size_t next = 0;
+};
+
 Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) {
+  AsyncHttpClient::Options co;
+  co.threads = std::max(1, opt_.client_threads);
+  co.connect_timeout = opt_.connect_timeout;
+  co.read_timeout = opt_.read_timeout;
+  client_ = std::make_unique<AsyncHttpClient>(co);
   for (const auto& w : opt_.workers) {
     ring_.addNode(w);
     breakers_[w] = std::make_unique<CircuitBreaker>(opt_.failure_threshold, opt_.success_threshold,
                                                     opt_.breaker_timeout);
     auto hp = parse_host_port(w);
-    clients_[w] = std::make_unique<HttpClient>(hp.first, hp.second, opt_.connect_timeout, opt_.read_timeout);
+    upstream_[w] = client_->add_upstream(hp.first, hp.second);
     if (opt_.verbose) std::cout << "Parsed URL: " << w << " -> host=" << hp.first << " port=" << hp.second << std::endl;
   }
-  pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opt_.forward_threads)));
   server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
-    auto body = std::make_shared<std::string>(std::move(req.body));
-    pool_->post([this, body, res] {
-      auto r = routeRequest(*body);
-      HttpResponse resp;
-      resp.status = r.first;
-      resp.body = std::move(r.second);
-      res.send(std::move(resp));
-    });
+    auto body = std::make_shared<const std::string>(std::move(req.body));
+    routeRequest(std::move(body), [res](HttpResponse&& r) { res.send(std::move(r)); });
   });
   server_.route("GET", "/stats", [this](HttpRequest&, Responder res) {
     HttpResponse r;
@@ -79,63 +60,80 @@ Gateway::~Gateway() { stop(); }
 
 int Gateway::start() { return server_.start(opt_.host, opt_.port, opt_.http_threads); }
 void Gateway::wait() { server_.wait(); }
-void Gateway::stop() { server_.stop(); }
-
-std::optional<std::string> Gateway::tryNode(const std::string& node, const std::string& body) {
-  auto b = breakers_.find(node);
-  if (b == breakers_.end()) return std::nullopt;
-  CircuitBreaker& breaker = *b->second;
-  if (!breaker.allowRequest()) {
-    if (opt_.verbose) std::cout << "Circuit breaker OPEN for " << node << ", skipping" << std::endl;
-    return std::nullopt;
-  }
-  auto c = clients_.find(node);
-  if (c == clients_.end()) {
-    breaker.recordFailure();
-    return std::nullopt;
-  }
-  std::string err;
-  auto resp = c->second->post("/infer", body, "application/json", &err);
-  if (resp && resp->status == 200) {
-    breaker.recordSuccess();
-    return std::move(resp->body);
-  }
-  if (opt_.verbose) {
-    if (resp) std::cerr << "Request to " << node << " failed with status: " << resp->status << std::endl;
-    else std::cerr << "Request to " << node << " failed: " << err << std::endl;
-  }
-  breaker.recordFailure();
-  return std::nullopt;
+void Gateway::stop() {
+  server_.stop();
+  if (client_) client_->stop();
 }
 
-std::pair<int, std::string> Gateway::routeRequest(const std::string& body) {
+void Gateway::routeRequest(std::shared_ptr<const std::string> body, std::function<void(HttpResponse&&)> done) {
   routed_++;
   std::string request_id;
-  if (!find_top_level_string(body, "request_id", request_id)) {
+  if (!find_top_level_string(*body, "request_id", request_id)) {
     // Slow path only to produce the same kind of error the reference returns.
     try {
-      Json j = Json::parse(body);
+      Json j = Json::parse(*body);
       request_id = j.at("request_id").as_string();
     } catch (const std::exception& e) {
       failed_++;
-      return {500, error_body(e.what())};
+      done(error_response(e.what()));
+      return;
     }
   }
-  const std::string target = ring_.getNode(request_id);
-  if (target.empty()) {
+  auto r = std::make_shared<Route>();
+  r->body = std::move(body);
+  r->done = std::move(done);
+  r->target = ring_.getNode(request_id);
+  if (r->target.empty()) {
     failed_++;
-    return {500, error_body("No workers available")};
+    r->done(error_response("No workers available"));
+    return;
   }
-  if (auto r = tryNode(target, body)) return {200, std::move(*r)};
-  for (const auto& node : ring_.getAllNodes()) {
-    if (node == target) continue;
-    if (auto r = tryNode(node, body)) {
-      failovers_++;
-      return {200, std::move(*r)};
+  r->order.push_back(r->target);
+  for (const auto& node : ring_.getAllNodes())
+    if (node != r->target) r->order.push_back(node);
+  try_next(std::move(r));
+}
+
+void Gateway::try_next(std::shared_ptr<Route> r) {
+  while (r->next < r->order.size()) {
+    const std::string node = r->order[r->next++];
+    CircuitBreaker& breaker = *breakers_.at(node);
+    if (!breaker.allowRequest()) {
+      if (opt_.verbose) std::cout << "Circuit breaker OPEN for " << node << ", skipping" << std::endl;
+      continue;
     }
+    client_->post(upstream_.at(node), "/infer", r->body, "application/json",
+                  [this, r, node](std::optional<HttpResponse> resp, const std::string& err) {
+                    CircuitBreaker& br = *breakers_.at(node);
+                    if (resp && resp->status == 200) {
+                      br.recordSuccess();
+                      if (node != r->target) failovers_++;
+                      HttpResponse out;
+                      out.body = std::move(resp->body);
+                      r->done(std::move(out));
+                      return;
+                    }
+                    if (resp && resp->header("x-die-error") == "client") {
+                      // the worker is healthy; the request is bad: same answer from any node
+                      br.recordSuccess();
+                      client_errors_++;
+                      HttpResponse out;
+                      out.status = resp->status;
+                      out.body = std::move(resp->body);
+                      r->done(std::move(out));
+                      return;
+                    }
+                    if (opt_.verbose) {
+                      if (resp) std::cerr << "Request to " << node << " failed with status: " << resp->status << std::endl;
+                      else std::cerr << "Request to " << node << " failed: " << err << std::endl;
+                    }
+                    br.recordFailure();
+                    try_next(r);
+                  });
+    return;
   }
   failed_++;
-  return {500, error_body("All workers failed or circuit breakers open")};
+  r->done(error_response("All workers failed or circuit breakers open"));
 }
 
 Json Gateway::getStats() const {
@@ -157,6 +155,9 @@ Json Gateway::getStats() const {
   s["routed"] = static_cast<long long>(routed_.load());
   s["failovers"] = static_cast<long long>(failovers_.load());
   s["failed"] = static_cast<long long>(failed_.load());
+  s["client_errors"] = static_cast<long long>(client_errors_.load());
+  s["in_flight"] = client_->in_flight();
+  s["upstream_connections_opened"] = client_->connections_opened();
   return s;
 }
 

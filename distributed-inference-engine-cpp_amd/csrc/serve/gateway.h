@@ -3,9 +3,13 @@
 // Reference: Gateway (src/gateway.cpp:12-159) and main (:161-200).  Same routing key, ring,
 // breaker thresholds, failover order (primary, then every other node in ring order), /stats
 // document and error bodies.  Differences: the request body is forwarded verbatim (only
-// `request_id` is extracted, no re-parse/re-dump), gateway->worker traffic uses a keep-alive
-// connection pool per worker (the reference's single httplib::Client per worker serialises all
-// forwards to that worker: SURVEY Q4), and per-request logging is off unless --verbose (Q11).
+// `request_id` is extracted, no re-parse/re-dump), gateway->worker traffic is event-driven over
+// keep-alive connections (core/http_async.h: any number of forwards in flight per worker, no thread
+// per request; the reference's single httplib::Client per worker serialises all forwards to that
+// worker: SURVEY Q4), per-request logging is off unless --verbose (Q11), and a worker's answer
+// marked as a client error (X-Die-Error: client, e.g. malformed JSON) is passed through without
+// failover and without counting against the worker's breaker -- in the reference any non-200 is a
+// breaker failure, so five malformed requests open every breaker (src/gateway.cpp:104-122).
 #pragma once
 
 #include <atomic>
@@ -22,25 +26,12 @@
 #include <vector>
 
 #include "../core/http.h"
+#include "../core/http_async.h"
 #include "../core/json.h"
 #include "circuit_breaker.h"
 #include "consistent_hash.h"
 
 namespace die {
-
-class ThreadPool {
- public:
-  explicit ThreadPool(size_t n);
-  ~ThreadPool();
-  void post(std::function<void()> fn);
-
- private:
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-  std::vector<std::thread> threads_;
-  bool stop_ = false;
-};
 
 struct GatewayOptions {
   std::vector<std::string> workers;
@@ -53,7 +44,7 @@ struct GatewayOptions {
   std::chrono::milliseconds connect_timeout{5000};  // :32
   std::chrono::milliseconds read_timeout{5000};     // :33
   int http_threads = 0;
-  int forward_threads = 256;
+  int client_threads = 2;  // event loops of the worker-side client
   bool verbose = false;
 };
 
@@ -67,20 +58,23 @@ class Gateway {
   int port() const { return server_.port(); }
 
   Json getStats() const;
-  // Synchronous routing (tests / reuse): returns (status, body).
-  std::pair<int, std::string> routeRequest(const std::string& body);
+  // Route one /infer body (reference Gateway::routeRequest, src/gateway.cpp:38-61): primary by
+  // request_id, then every other node in ring order; `done(status, response)` runs once, on a
+  // client loop thread (or inline for requests that never reach a worker).
+  void routeRequest(std::shared_ptr<const std::string> body, std::function<void(HttpResponse&&)> done);
   const ConsistentHash& ring() const { return ring_; }
 
  private:
-  std::optional<std::string> tryNode(const std::string& node, const std::string& body);
+  struct Route;
+  void try_next(std::shared_ptr<Route> r);
 
   GatewayOptions opt_;
   ConsistentHash ring_;
   std::map<std::string, std::unique_ptr<CircuitBreaker>> breakers_;
-  std::map<std::string, std::unique_ptr<HttpClient>> clients_;
-  std::unique_ptr<ThreadPool> pool_;
+  std::map<std::string, int> upstream_;  // node -> AsyncHttpClient upstream id
+  std::unique_ptr<AsyncHttpClient> client_;
   HttpServer server_;
-  std::atomic<int64_t> routed_{0}, failovers_{0}, failed_{0};
+  std::atomic<int64_t> routed_{0}, failovers_{0}, failed_{0}, client_errors_{0};
 };
 
 }  // namespace die

@@ -130,9 +130,12 @@ void WorkerNode::stop() {
   if (engine_) engine_->synchronize();
 }
 
-HttpResponse WorkerNode::error_response(int status, const std::string& msg) const {
+HttpResponse WorkerNode::error_response(int status, const std::string& msg, bool client_error) const {
   HttpResponse r;
   r.status = status;
+  // Same status and {"error": ...} body as the reference (500); the extra header tells the gateway
+  // that the request, not this worker, is at fault (no failover, no breaker failure).
+  if (client_error) r.headers.emplace_back("X-Die-Error", "client");
   Json j = Json::object();
   j["error"] = msg;
   r.body = j.dump();
@@ -223,7 +226,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   } catch (const std::exception& e) {
     pool.release(sink.buf);
     errors_++;
-    res.send(error_response(500, e.what()));
+    res.send(error_response(500, e.what(), true));
     return;
   }
   // Free the request body now: at ResNet size it is ~1 MB we no longer need.
@@ -299,7 +302,7 @@ void WorkerNode::dispatch(Pending p, Responder res) {
     if (r->decode_status) {
       errors_++;
       res.send(error_response(500, "input_data has " + std::to_string(r->ntok) + " values; model input holds " +
-                                       std::to_string(engine_->input_numel())));
+                                       std::to_string(engine_->input_numel()), true));
       return;
     }
     cache_.put(key, r->output);
@@ -356,7 +359,7 @@ void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, bool pack
   } catch (const std::exception& e) {
     pool.release(sink.buf);
     errors_++;
-    res.send(error_response(500, e.what()));
+    res.send(error_response(500, e.what(), true));
     return;
   }
   Pending p;

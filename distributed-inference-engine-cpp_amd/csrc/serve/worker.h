@@ -84,7 +84,7 @@ class WorkerNode {
   // Device decode flagged the text: convert it with the strict host parser and re-dispatch.
   void host_fallback(SampleBuffer text_buf, size_t text_len, bool packed, size_t text_off, std::string id, InputKey key,
                      Responder res);
-  HttpResponse error_response(int status, const std::string& msg) const;
+  HttpResponse error_response(int status, const std::string& msg, bool client_error = false) const;
 
   WorkerOptions opt_;
   std::unique_ptr<Engine> engine_;

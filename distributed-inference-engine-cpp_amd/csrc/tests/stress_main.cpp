@@ -163,7 +163,7 @@ static void stress_http_gateway(double secs) {
   go.host = "127.0.0.1";
   go.port = 0;
   go.breaker_timeout = std::chrono::milliseconds(50);
-  go.forward_threads = 16;
+  go.client_threads = 2;
   go.http_threads = 2;
   Gateway gw(go);
   const int gport = gw.start();

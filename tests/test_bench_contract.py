@@ -33,24 +33,40 @@ def _check(out, n, steps, warmup, mode):
         assert k in out, k
     assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
     assert out["higher_is_better"] is True and out["scaling"] == "weak"
-    assert out["config"]["parallelism"] == "dp%d" % n and out["config"]["mode"] == mode
+    names = {"gateway": "gateway+worker", "http": "worker"}
+    assert out["config"]["parallelism"] == "dp%d" % n and out["config"]["mode"] == names.get(mode, mode)
     assert out["failed"] == 0 and out["value"] > 0
-    # whole-job aggregate: every rank's requests are counted
-    assert out["config"]["requests"] == steps * out["config"]["global_batch"]
+    # whole-job aggregate: every rank's requests are counted; a step is STEP_REQ requests per GPU
+    assert out["config"]["requests"] == steps * STEP_REQ * n
+    if mode == "gateway":
+        assert out["gateway"]["failed"] == 0 and set(out["gateway"]["breakers"]) == {"CLOSED"}
+        assert out["direct_worker"]["failed"] == 0
 
 
-@pytest.mark.parametrize("mode", ["http", "dp"])
+STEP_REQ = 4
+ARGS = ["--device", "cpu", "--batch", "2", "--steps", "2", "--warmup", "1", "--connections", "4",
+        "--step-requests", str(STEP_REQ)]
+
+
+@pytest.mark.parametrize("mode", ["gateway", "http", "dp"])
 def test_bench_single_rank_cpu(mode):
-    out = _run([sys.executable, "bench.py", "--device", "cpu", "--mode", mode, "--batch", "2", "--steps", "2",
-                "--warmup", "1", "--connections", "4"])
+    out = _run([sys.executable, "bench.py", "--mode", mode] + ARGS)
     _check(out, 1, 2, 1, mode)
+    assert out["dtype"] == "fp32"
 
 
-@pytest.mark.parametrize("mode", ["http", "dp"])
+@pytest.mark.parametrize("mode", ["gateway", "dp"])
 def test_bench_two_ranks_torchrun_cpu(mode):
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-                "--device", "cpu", "--mode", mode, "--batch", "2", "--steps", "2", "--warmup", "1",
-                "--connections", "4"])
+                "--mode", mode] + ARGS)
     _check(out, 2, 2, 1, mode)
     assert out["config"]["global_batch"] == 4
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+                        "--mode", "http"] + ARGS, cwd=REPO, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert p.returncode != 0 and "does not match WORLD_SIZE" in p.stderr

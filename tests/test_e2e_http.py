@@ -256,3 +256,22 @@ def test_chunked_request_still_works(cluster):
            + b"%x\r\n" % half + body[:half] + b"\r\n" + b"%x\r\n" % (len(body) - half) + body[half:] + b"\r\n0\r\n\r\n")
     out = _raw_http(port, req)
     assert out.startswith(b"HTTP/1.1 200"), out[:200]
+
+
+def test_malformed_bodies_leave_breakers_closed(cluster):
+    """a malformed body that still names a request_id reached every worker and each 500
+    counted against its breaker, so five of them opened every breaker.  Workers now mark request
+    errors (X-Die-Error: client); the gateway passes them through without failover or failure."""
+    gw = cluster["gw"]
+    _, before = get(gw.url + "/stats")
+    for i in range(12):
+        st, out = post(gw.url + "/infer", raw=b'{"request_id": "bad_%d", "input_data": [1.0, oops]}' % i)
+        assert st == 500 and "error" in out
+        st, out = post(gw.url + "/infer", raw=b'{"request_id": "bad2_%d"}' % i)
+        assert st == 500 and "input_data" in out["error"]
+    _, s = get(gw.url + "/stats")
+    assert all(b["state"] == "CLOSED" for b in s["circuit_breakers"]), s
+    assert s["client_errors"] - before.get("client_errors", 0) == 24
+    assert s["failovers"] == before["failovers"]
+    st, out = post(gw.url + "/infer", {"request_id": "good_after_bad", "input_data": [1.0]})
+    assert st == 200
