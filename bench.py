@@ -21,6 +21,7 @@ the extra key `direct_worker`.
 import argparse
 import json
 import os
+import resource
 import sys
 import tempfile
 import time
@@ -55,6 +56,7 @@ def main():
                          "worker; dp: ONE worker whose batches are sharded over all ranks (RCCL); engine: "
                          "forward-only (a step = one batch)")
     ap.add_argument("--no-direct", action="store_true", help="skip the extra direct-to-worker measurement")
+    ap.add_argument("--gw-client-threads", type=int, default=0, help="gateway forwarding loops (0 = auto)")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
@@ -155,7 +157,7 @@ def main():
             if dist is not None:
                 ports = [None] * world
                 dist.all_gather_object(ports, wk.port)
-            gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports])
+            gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads)
             target_port = gw.port
         lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
@@ -163,10 +165,12 @@ def main():
         h0 = wk.health()
         g0 = gw.stats() if gw else {}
         barrier()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, **lg)
         barrier()
         elapsed = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
         h1 = wk.health()
         g1 = gw.stats() if gw else {}
         ok = res["ok"]
@@ -190,6 +194,9 @@ def main():
             "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
             "pace_lead_ms": e1.get("avg_pace_lead_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
+            # host CPU spent per request by this process (client + gateway + worker threads together)
+            "cpu_us_per_request": {"user": round((ru1.ru_utime - ru0.ru_utime) * 1e6 / max(1, res["ok"]), 1),
+                                   "sys": round((ru1.ru_stime - ru0.ru_stime) * 1e6 / max(1, res["ok"]), 1)},
         }
         if gw:
             extra["gateway"] = {"failovers": g1["failovers"] - g0["failovers"], "failed": g1["failed"] - g0["failed"],
@@ -198,12 +205,17 @@ def main():
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()
+            rd0 = resource.getrusage(resource.RUSAGE_SELF)
             td = time.perf_counter()
             rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank, **lg)
             barrier()
             el = time.perf_counter() - td
+            rd1 = resource.getrusage(resource.RUSAGE_SELF)
+            n_ok = max(1, rd["ok"])
             extra["direct_worker"] = {"rps_this_rank": rd["ok"] / el, "p50_ms": rd["latency_ms"]["p50"],
-                                      "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"]}
+                                      "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"],
+                                      "cpu_us_per_request": {"user": round((rd1.ru_utime - rd0.ru_utime) * 1e6 / n_ok, 1),
+                                                             "sys": round((rd1.ru_stime - rd0.ru_stime) * 1e6 / n_ok, 1)}}
         if gw:
             gw.stop()
         wk.stop()

@@ -16,7 +16,7 @@ int main(int argc, char** argv) {
               << "Options (defaults = reference constants):\n"
               << "  --port N (8000)  --failure-threshold N (5)  --success-threshold N (2)\n"
               << "  --breaker-timeout-s S (30)  --vnodes N (150)  --connect-timeout-ms N (5000)\n"
-              << "  --read-timeout-ms N (5000)  --client-threads N (2)  --http-threads N  --verbose"
+              << "  --read-timeout-ms N (5000)  --client-threads N (CPUs/2)  --http-threads N  --verbose"
               << std::endl;
     return 1;
   }
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
   o.vnodes = static_cast<int>(f.i("vnodes", 150));
   o.connect_timeout = std::chrono::milliseconds(f.i("connect-timeout-ms", 5000));
   o.read_timeout = std::chrono::milliseconds(f.i("read-timeout-ms", 5000));
-  o.client_threads = static_cast<int>(f.i("client-threads", 2));
+  o.client_threads = static_cast<int>(f.i("client-threads", 0));
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.verbose = f.b("verbose");
   die::Gateway gw(o);

@@ -531,7 +531,7 @@ void* die_gateway_create(const char* opts_json, char** err) {
     o.vnodes = jget<int>(j, "vnodes", 150);
     o.connect_timeout = std::chrono::milliseconds(jget<long>(j, "connect_timeout_ms", 5000));
     o.read_timeout = std::chrono::milliseconds(jget<long>(j, "read_timeout_ms", 5000));
-    o.client_threads = jget<int>(j, "client_threads", 2);
+    o.client_threads = jget<int>(j, "client_threads", 0);
     o.http_threads = jget<int>(j, "http_threads", 0);
     auto* g = new Gateway(o);
     if (g->start() < 0) {

@@ -154,9 +154,9 @@ int die_kern_decode_packed(uint64_t text, uint64_t offs, uint64_t packed, uint64
 }
 
 int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, int H, int W, int Ho, int Wo, int relu,
-                  uint64_t stream) {
+                  uint64_t stream, int split) {
   return static_cast<int>(kern::conv_stem7x7(P<const uint16_t>(x), P<const uint16_t>(w), P<const float>(bias),
-                                             P<uint16_t>(out), B, H, W, Ho, Wo, relu, S(stream)));
+                                             P<uint16_t>(out), B, H, W, Ho, Wo, relu, S(stream), nullptr, split));
 }
 
 // Plan summary of a model (op list with fused epilogues), for tests and docs.

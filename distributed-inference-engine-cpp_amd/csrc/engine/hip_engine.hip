@@ -980,7 +980,7 @@ class HipEngine : public Engine {
           e = kern::conv_stem7x7(static_cast<const uint16_t*>(buf(op.in)),
                                  reinterpret_cast<const uint16_t*>(params_ + op.w_off), prm(op.bias_off),
                                  static_cast<uint16_t*>(buf(op.out)), B, op.conv.H, op.conv.W, op.conv.Ho, op.conv.Wo,
-                                 op.conv.relu, st, live);
+                                 op.conv.relu, st, live, sp_);
           break;
         case PlanOp::LAYERNORM:
           e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),

@@ -369,9 +369,8 @@ class Planner {
     p.in = in_buf;
     p.in2 = res_buf;
     // ResNet stem (7x7/2, pad 3, 4 stored input channels, 64 outputs, plain epilogue): LDS-patch kernel
-    // (bf16 only: in fp32 mode the stem runs as a generic split conv)
     const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && Cstore == 4 &&
-                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur) && !split_;
+                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur);
     if (stem) {
       p.kind = PlanOp::STEM;
       std::vector<float> ws(64 * 224, 0.f);

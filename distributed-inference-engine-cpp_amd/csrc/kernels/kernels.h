@@ -107,8 +107,9 @@ hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s, 
 
 // 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:
 // w = [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8), out = act(conv + bias) NHWC bf16.
+// split: x/out are split tensors and w holds the hi plane [64][224] followed by the lo plane.
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
-                        int Ho, int Wo, int relu, hipStream_t s, const long long* live = nullptr);
+                        int Ho, int Wo, int relu, hipStream_t s, const long long* live = nullptr, int split = 0);
 
 // Evict the L2s: stream-read `bytes` (> 8 x 4 MiB) of a scratch buffer (autotuning in the cache
 // state a layer sees inside a forward: L2 cold, Infinity Cache warm).

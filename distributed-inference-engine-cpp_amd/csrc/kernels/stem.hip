@@ -12,6 +12,8 @@
 //   * weights [64][224] (BN folded) sit in LDS with a 232-element pitch (conflict-free A reads);
 //   * epilogue: + bias, optional ReLU, bf16, staged through LDS (XOR-swizzled) so each output pixel's
 //     128 bytes go out as 16-byte stores.
+//   * SPLIT (fp32 mode, common.h): input, weights and output are hi/lo planes; both planes of the
+//     patch and the weights sit in LDS and each fragment pair takes three MFMAs.
 #include "common.h"
 #include "kernels.h"
 
@@ -27,30 +29,38 @@ constexpr int PY = 2 * TY + 5, PX = 2 * TX + 6;  // patch (PX even: kx padded to
 constexpr int KS = 224, WP = 232;            // K and weight LDS pitch (elements)
 constexpr int NCH = 64;
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                       int H, int W, int Ho, int Wo, int relu, int tiles_x,
                                                       const long long* __restrict__ live) {
-  __shared__ __attribute__((aligned(16))) uint16_t wl[NCH * WP];
-  __shared__ __attribute__((aligned(16))) uint16_t patch[PY * PX * 4];
+  constexpr int NP = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t wl[NP * NCH * WP];
+  __shared__ __attribute__((aligned(16))) uint16_t patch[NP * PY * PX * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.y;
+  const long long xplane = static_cast<long long>(gridDim.y) * H * W * 4;
+  const long long oplane = static_cast<long long>(gridDim.y) * Ho * Wo * NCH;
   if (live && b >= *live) return;  // padding sample of the bucket: whole block, before any barrier
   const int ty0 = (blockIdx.x / tiles_x) * TY, tx0 = (blockIdx.x % tiles_x) * TX;
-  // weights -> LDS (64 x 224 bf16 = 28 chunks of 16 B per row)
-  for (int i = tid; i < NCH * (KS / 8); i += 256) {
-    const int r = i / (KS / 8), c = i % (KS / 8);
-    *reinterpret_cast<uint4*>(wl + r * WP + c * 8) = *reinterpret_cast<const uint4*>(w + r * KS + c * 8);
+  // weights -> LDS (64 x 224 bf16 = 28 chunks of 16 B per row; SPLIT: the lo plane follows)
+  for (int i = tid; i < NP * NCH * (KS / 8); i += 256) {
+    const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
+    const int r = q / (KS / 8), c = q % (KS / 8);
+    *reinterpret_cast<uint4*>(wl + pl * NCH * WP + r * WP + c * 8) =
+        *reinterpret_cast<const uint4*>(w + pl * NCH * KS + r * KS + c * 8);
   }
   // input patch -> LDS: pixel (iy, ix) = 4 bf16 = 8 bytes; outside the image -> 0
   const int iy0 = 2 * ty0 - 3, ix0 = 2 * tx0 - 3;
   const uint16_t* xb = x + static_cast<size_t>(b) * H * W * 4;
-  for (int i = tid; i < PY * PX; i += 256) {
-    const int py = i / PX, px = i % PX;
+  for (int i = tid; i < NP * PY * PX; i += 256) {
+    const int pl = i / (PY * PX), q = i % (PY * PX);
+    const int py = q / PX, px = q % PX;
     const int iy = iy0 + py, ix = ix0 + px;
     uint2 v = make_uint2(0, 0);
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = *reinterpret_cast<const uint2*>(xb + (static_cast<size_t>(iy) * W + ix) * 4);
-    *reinterpret_cast<uint2*>(patch + i * 4) = v;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = *reinterpret_cast<const uint2*>(xb + pl * xplane + (static_cast<size_t>(iy) * W + ix) * 4);
+    *reinterpret_cast<uint2*>(patch + pl * PY * PX * 4 + q * 4) = v;
   }
   __syncthreads();
   // wave w: output rows 2w, 2w+1 of the tile (16 pixels each) x 64 channels
@@ -62,18 +72,29 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
   const int j = lane >> 4, px_l = lane & 15;
 #pragma unroll
   for (int ky = 0; ky < 7; ++ky) {
-    bf16x8 bf[2];
+    bf16x8 bf[NP][2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int oy = 2 * wave + m;
-      const int py = 2 * oy + ky, px = 2 * px_l + 2 * j;
-      bf[m] = *reinterpret_cast<const bf16x8*>(patch + (py * PX + px) * 4);
-    }
+    for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int oy = 2 * wave + m;
+        const int py = 2 * oy + ky, px = 2 * px_l + 2 * j;
+        bf[pl][m] = *reinterpret_cast<const bf16x8*>(patch + pl * PY * PX * 4 + (py * PX + px) * 4);
+      }
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8);
+      const int wo = (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8;
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + wo);
+      if constexpr (SPLIT) {
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(wl + NCH * WP + wo);
 #pragma unroll
-      for (int m = 0; m < 2; ++m) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[m], acc[n][m], 0, 0, 0);
+        for (int m = 0; m < 2; ++m) {
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf[0][m], acc[n][m], 0, 0, 0);
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[NP - 1][m], acc[n][m], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[0][m], acc[n][m], 0, 0, 0);
     }
   }
   __syncthreads();  // weights -> output stage [128 px][64 ch] bf16, 16-B chunk c of pixel p at chunk c ^ (p & 7)
@@ -93,16 +114,28 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
         v3 = fmaxf(v3, 0.f);
       }
       const int chunk = (ch >> 3) ^ (p & 7);
-      *reinterpret_cast<uint2*>(stage + p * NCH + chunk * 8 + (ch & 7)) = make_uint2(pack2(v0, v1), pack2(v2, v3));
+      uint16_t* dst = stage + p * NCH + chunk * 8 + (ch & 7);
+      if constexpr (SPLIT) {
+        const float vv[4] = {v0, v1, v2, v3};
+        uint16_t h[4], l[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) split1(vv[t], h[t], l[t]);
+        *reinterpret_cast<uint2*>(dst) = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+        *reinterpret_cast<uint2*>(dst + TY * TX * NCH) =
+            make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
+      } else {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(v0, v1), pack2(v2, v3));
+      }
     }
   }
   __syncthreads();
-  for (int i = tid; i < TY * TX * (NCH / 8); i += 256) {
-    const int p = i >> 3, c = i & 7;
+  for (int i = tid; i < NP * TY * TX * (NCH / 8); i += 256) {
+    const int pl = i / (TY * TX * (NCH / 8)), q = i % (TY * TX * (NCH / 8));
+    const int p = q >> 3, c = q & 7;
     const int oy = ty0 + p / TX, ox = tx0 + p % TX;
     if (oy >= Ho || ox >= Wo) continue;
-    const uint4 v = *reinterpret_cast<const uint4*>(stage + p * NCH + ((c ^ (p & 7)) << 3));
-    *reinterpret_cast<uint4*>(out + ((static_cast<size_t>(b) * Ho + oy) * Wo + ox) * NCH + c * 8) = v;
+    const uint4 v = *reinterpret_cast<const uint4*>(stage + pl * TY * TX * NCH + p * NCH + ((c ^ (p & 7)) << 3));
+    *reinterpret_cast<uint4*>(out + pl * oplane + ((static_cast<size_t>(b) * Ho + oy) * Wo + ox) * NCH + c * 8) = v;
   }
 }
 
@@ -111,11 +144,15 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
 static_assert(TY * TX * NCH <= NCH * WP, "output stage must fit in the weight buffer");
 
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
-                        int Ho, int Wo, int relu, hipStream_t s, const long long* live) {
+                        int Ho, int Wo, int relu, hipStream_t s, const long long* live, int split) {
   if (Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1) return hipErrorInvalidValue;
   const int tiles_x = (Wo + TX - 1) / TX, tiles_y = (Ho + TY - 1) / TY;
-  hipLaunchKernelGGL(stem7x7_kernel, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho, Wo, relu,
-                     tiles_x, live);
+  if (split)
+    hipLaunchKernelGGL(stem7x7_kernel<true>, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho,
+                       Wo, relu, tiles_x, live);
+  else
+    hipLaunchKernelGGL(stem7x7_kernel<false>, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho,
+                       Wo, relu, tiles_x, live);
   return hipGetLastError();
 }
 

@@ -2,6 +2,8 @@
 
 #include <iostream>
 
+#include "../core/sysinfo.h"
+
 namespace die {
 
 namespace {
@@ -33,7 +35,9 @@ struct Gateway::Route {
 
 Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) {
   AsyncHttpClient::Options co;
-  co.threads = std::max(1, opt_.client_threads);
+  // Forwarding a ~1 MB body is a ~100 us kernel copy: with 2 loops the gateway capped at ~10.8k
+  // req/s on a 16-CPU share (profiles/r2_gateway_threads.md), so it scales with the CPUs.
+  co.threads = opt_.client_threads > 0 ? opt_.client_threads : std::max(2, available_cpus() / 2);
   co.connect_timeout = opt_.connect_timeout;
   co.read_timeout = opt_.read_timeout;
   client_ = std::make_unique<AsyncHttpClient>(co);

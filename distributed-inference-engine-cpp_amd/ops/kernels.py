@@ -336,26 +336,29 @@ def decode_json_numbers(texts, numel, text_cap=None, slot_order=None):
     return out, status, ntok
 
 
-def pack_stem_weight(w):
-    """[64, C<=4, 7, 7] float -> [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8)."""
+def pack_stem_weight(w, split=False):
+    """[64, C<=4, 7, 7] float -> [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8)
+    (split: [2][64][224] hi, lo planes)."""
     import torch
 
     co, ci = w.shape[:2]
     wp = torch.zeros((co, 7, 8, 4), dtype=torch.float32, device=w.device)
     wp[:, :, :7, :ci] = w.float().permute(0, 2, 3, 1)
-    return wp.reshape(co, 224).to(torch.bfloat16).contiguous()
+    wp = wp.reshape(co, 224)
+    return split_planes(wp) if split else wp.to(torch.bfloat16).contiguous()
 
 
-def conv_stem7x7(x_nhwc4, w, bias, relu=True):
-    """ResNet stem on the LDS-patch kernel: x [B,H,W,4] bf16, w [64,C,7,7] -> [B,Ho,Wo,64] bf16."""
+def conv_stem7x7(x_nhwc4, w, bias, relu=True, split=False):
+    """ResNet stem on the LDS-patch kernel: x [B,H,W,4] bf16, w [64,C,7,7] -> [B,Ho,Wo,64] bf16.
+    split (fp32 mode): x any float dtype, fp32 result."""
     import torch
 
     B, H, W, C = x_nhwc4.shape
     assert C == 4 and w.shape[0] == 64
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-    out = torch.empty((B, Ho, Wo, 64), dtype=torch.bfloat16, device=x_nhwc4.device)
+    out = torch.empty(((2,) if split else ()) + (B, Ho, Wo, 64), dtype=torch.bfloat16, device=x_nhwc4.device)
     b = bias.float().contiguous()
-    rc = native.kernels().die_kern_stem(_ptr(x_nhwc4.contiguous()), _ptr(pack_stem_weight(w)), _ptr(b), _ptr(out), B, H,
-                                        W, Ho, Wo, int(relu), _stream())
+    rc = native.kernels().die_kern_stem(_ptr(_in(x_nhwc4, split)), _ptr(pack_stem_weight(w, split)), _ptr(b), _ptr(out),
+                                        B, H, W, Ho, Wo, int(relu), _stream(), int(split))
     _check(rc, "conv_stem7x7")
-    return out
+    return _out(out, split)

@@ -248,3 +248,22 @@ def test_engine_fp32_matches_torch(native, models, arch):
     finally:
         e32.close()
         e16.close()
+
+
+@pytest.mark.parametrize("B,H,W,relu", [(2, 224, 224, True), (1, 37, 45, False)])
+def test_split_stem_kernel(native, B, H, W, relu):
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    g = torch.Generator(device="cuda").manual_seed(B * 7 + H)
+    x = torch.zeros(B, H, W, 4, device="cuda")
+    x[..., :3] = torch.rand(B, H, W, 3, device="cuda", generator=g) * 2 - 1
+    w = torch.randn(64, 3, 7, 7, device="cuda", generator=g) / 12.0
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    got = K.conv_stem7x7(x, w, bias, relu=relu, split=True)
+    ref = torch.nn.functional.conv2d(x[..., :3].permute(0, 3, 1, 2).double(), w.double(), bias.double(), stride=2,
+                                     padding=3)
+    if relu:
+        ref = torch.relu(ref)
+    torch.cuda.synchronize()
+    assert rel_err(got.permute(0, 3, 1, 2), ref) < TOL, rel_err(got.permute(0, 3, 1, 2), ref)

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
 
@@ -33,10 +34,10 @@ def main():
     d = tempfile.mkdtemp()
     path = os.path.join(d, a.arch + ".onnx")
     open(path, "wb").write(m.build_onnx(cfg)[0])
-    e = native.Engine(path, device="hip", max_batch=a.batch)
+    e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision)
     p = e.profile(a.batch, a.iters)
     e.close()
-    lines = ["# %s per-op device time, batch %d (MI355X, bf16, tuned kernels)" % (a.arch, p["batch"]), "",
+    lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
              "Total %.1f us per forward = %.1f TFLOP/s over the whole graph; %.0f images/s device-bound." % (
                  p["total_us"], p["tflops"], p["batch"] / p["total_us"] * 1e6), "",
              "| # | op | kind | us | GFLOP | TFLOP/s | tile/splits |", "|---:|---|---|---:|---:|---:|---|"]
