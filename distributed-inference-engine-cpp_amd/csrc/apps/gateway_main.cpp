@@ -5,6 +5,7 @@
 #include <iostream>
 
 #include "../core/flags.h"
+#include "../core/log.h"
 #include "../serve/gateway.h"
 
 int main(int argc, char** argv) {
@@ -16,7 +17,8 @@ int main(int argc, char** argv) {
               << "Options (defaults = reference constants):\n"
               << "  --port N (8000)  --failure-threshold N (5)  --success-threshold N (2)\n"
               << "  --breaker-timeout-s S (30)  --vnodes N (150)  --connect-timeout-ms N (5000)\n"
-              << "  --read-timeout-ms N (5000)  --client-threads N (CPUs/2)  --http-threads N  --verbose"
+              << "  --read-timeout-ms N (5000)  --client-threads N (CPUs/2)  --http-threads N  --verbose\n"
+              << "  --log-level trace|debug|info|warn|error|off (info; env DIE_LOG_LEVEL)"
               << std::endl;
     return 1;
   }
@@ -38,6 +40,9 @@ int main(int argc, char** argv) {
   o.client_threads = static_cast<int>(f.i("client-threads", 0));
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.verbose = f.b("verbose");
+  if (o.verbose) die::set_log_level(die::LogLevel::DEBUG);
+  die::LogLevel lv;
+  if (die::parse_log_level(f.str("log-level", ""), &lv)) die::set_log_level(lv);
   die::Gateway gw(o);
   if (gw.start() < 0) {
     std::cerr << "Failed to bind port " << o.port << std::endl;

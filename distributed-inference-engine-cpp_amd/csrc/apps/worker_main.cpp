@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "../core/flags.h"
+#include "../core/log.h"
 #include "../serve/worker.h"
 
 extern char** environ;
@@ -90,7 +91,8 @@ int main(int argc, char** argv) {
               << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --http-threads N  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch)\n"
-              << "  --fault-fail-rate P  --fault-latency-ms N  --verbose" << std::endl;
+              << "  --fault-fail-rate P  --fault-latency-ms N  --verbose\n"
+              << "  --log-level trace|debug|info|warn|error|off (info; env DIE_LOG_LEVEL)" << std::endl;
     return 1;
   }
   // Block SIGINT/SIGTERM in every thread; the main thread waits for them with sigwait() and then
@@ -138,6 +140,9 @@ int main(int argc, char** argv) {
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));
   o.verbose = f.b("verbose");
+  if (o.verbose) die::set_log_level(die::LogLevel::DEBUG);
+  die::LogLevel lv;
+  if (die::parse_log_level(f.str("log-level", ""), &lv)) die::set_log_level(lv);
 
   // data parallel: spawn the followers first (before this process initialises HIP)
   std::vector<pid_t> followers;

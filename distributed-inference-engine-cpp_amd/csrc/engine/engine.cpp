@@ -1,5 +1,7 @@
 #include "engine.h"
 
+#include "../core/log.h"
+
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -264,7 +266,7 @@ std::unique_ptr<Engine> create_engine(const std::string& model_path, const Engin
     auto e = create_hip_engine(model_path, opt, &why);
     if (e) return e;
     if (opt.device == "hip") throw std::runtime_error("HIP engine unavailable: " + why);
-    std::cerr << "HIP engine unavailable (" << why << "); falling back to the CPU executor" << std::endl;
+    DIE_LOG(WARN, "HIP engine unavailable (" << why << "); falling back to the CPU executor");
   }
   return create_cpu_engine(model_path, opt);
 }

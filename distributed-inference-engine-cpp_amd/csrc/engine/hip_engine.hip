@@ -450,6 +450,7 @@ class HipEngine : public Engine {
             const int si = rr++ % n_copy_streams_;
             HIP_CHECK(hipMemcpyAsync(d_packed_ + idx * (text_cap_ / 2), items[i].text, (items[i].text_len + 1) / 2,
                                      hipMemcpyHostToDevice, s_stage_[si]));
+            h2d_bytes_.fetch_add(static_cast<long long>((items[i].text_len + 1) / 2), std::memory_order_relaxed);
             copied[si] = true;
           } else {
             const size_t idx = static_cast<size_t>(n_stage_) + static_cast<size_t>(slot) * max_batch_ + i;
@@ -457,6 +458,7 @@ class HipEngine : public Engine {
             const int si = rr++ % n_copy_streams_;
             HIP_CHECK(hipMemcpyAsync(d_text_ + idx * text_cap_, items[i].text, items[i].text_len, hipMemcpyHostToDevice,
                                      s_stage_[si]));
+            h2d_bytes_.fetch_add(static_cast<long long>(items[i].text_len), std::memory_order_relaxed);
             copied[si] = true;
           }
           sl.h_lens[i] = static_cast<long long>(items[i].text_len);
@@ -468,6 +470,7 @@ class HipEngine : public Engine {
         float* dst = sl.d_in + static_cast<size_t>(i) * in_numel_;
         const int si = rr++ % n_copy_streams_;
         if (n) HIP_CHECK(hipMemcpyAsync(dst, items[i].input, n * sizeof(float), hipMemcpyHostToDevice, s_stage_[si]));
+        h2d_bytes_.fetch_add(static_cast<long long>(n * sizeof(float)), std::memory_order_relaxed);
         if (n < in_numel_) HIP_CHECK(hipMemsetAsync(dst + n, 0, (in_numel_ - n) * sizeof(float), s_stage_[si]));
         copied[si] = true;
       }
@@ -509,8 +512,12 @@ class HipEngine : public Engine {
         ps = cs;
       }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 3], ps));
-      if (!prep_graphs_.empty()) HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
-      else encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
+      if (!prep_graphs_.empty()) {
+        HIP_CHECK(hipGraphLaunch(prep_graphs_[bi * depth_ + slot], ps));
+        graph_replays_.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        encode_forward(buckets_[bi], slot, ps, nullptr, PREP);
+      }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 4], ps));
       if (!prep_on_compute_) {
         HIP_CHECK(hipEventRecord(sl.ev_prep, ps));
@@ -520,6 +527,7 @@ class HipEngine : public Engine {
       HIP_CHECK(hipEventRecord(tev_[job.ev + 1], cs));
       if (!graphs_.empty()) {
         HIP_CHECK(hipGraphLaunch(graphs_[bi * depth_ + slot], cs));
+        graph_replays_.fetch_add(1, std::memory_order_relaxed);
       } else {
         encode_forward(buckets_[bi], slot, cs, nullptr, MAIN);
       }
@@ -535,6 +543,9 @@ class HipEngine : public Engine {
                                    hipMemcpyDeviceToHost, cs));
           HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
                                    hipMemcpyDeviceToHost, cs));
+          d2h_bytes_.fetch_add(static_cast<long long>((sizeof(float) * out_numel_ * B + sizeof(int) * 2 * max_batch_) *
+                                                      dp_world_),
+                               std::memory_order_relaxed);
           HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
         } else {
           HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
@@ -542,8 +553,11 @@ class HipEngine : public Engine {
         job.has_text = text_cap_ > 0;
       } else {
         HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, cs));
-        if (any_text)
+        d2h_bytes_.fetch_add(static_cast<long long>(sizeof(float) * out_numel_ * B), std::memory_order_relaxed);
+        if (any_text) {
           HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, cs));
+          d2h_bytes_.fetch_add(static_cast<long long>(sizeof(int) * 2 * max_batch_), std::memory_order_relaxed);
+        }
         HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
       }
     } catch (const std::exception& e) {
@@ -618,6 +632,12 @@ class HipEngine : public Engine {
     j["images"] = static_cast<long long>(images_.load());
     const long long nb = batches_.load();
     j["avg_device_ms"] = nb ? device_ms_total_.load() / nb : 0.0;
+    // per-GPU I/O and activity counters
+    j["device_id"] = dev_;
+    j["h2d_bytes"] = h2d_bytes_.load();
+    j["d2h_bytes"] = d2h_bytes_.load();
+    j["graph_replays"] = graph_replays_.load();
+    j["device_busy_ms"] = device_ms_total_.load();
     // per batch: compute stream waiting for the batch's PREP (copies + decode) / idle before it was submitted
     j["avg_copy_wait_ms"] = nb ? copy_wait_ms_total_.load() / nb : 0.0;
     j["avg_gpu_gap_ms"] = nb ? gpu_gap_ms_total_.load() / nb : 0.0;
@@ -1139,6 +1159,7 @@ class HipEngine : public Engine {
                                                   hipMemcpyHostToDevice, s_stage_[si])) == hipSuccess &&
                       hipEventRecord(stage_ev_[rq.t], s_stage_[si]) == hipSuccess;
       diag_issue_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ti0).count();
+      if (ok) h2d_bytes_.fetch_add(static_cast<long long>(rq.packed ? (rq.len + 1) / 2 : rq.len), std::memory_order_relaxed);
       {
         std::lock_guard<std::mutex> g(stage_mu_);
         stage_stream_[rq.t] = si;
@@ -1346,6 +1367,7 @@ class HipEngine : public Engine {
   std::atomic<long long> paced_batches_{0};
   bool stop_ = false;
   std::atomic<long long> batches_{0}, images_{0};
+  std::atomic<long long> h2d_bytes_{0}, d2h_bytes_{0}, graph_replays_{0};
   std::atomic<double> device_ms_total_{0.0};
 };
 

@@ -2,6 +2,7 @@
 
 #include <iostream>
 
+#include "../core/log.h"
 #include "../core/sysinfo.h"
 
 namespace die {
@@ -47,7 +48,7 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
                                                     opt_.breaker_timeout);
     auto hp = parse_host_port(w);
     upstream_[w] = client_->add_upstream(hp.first, hp.second);
-    if (opt_.verbose) std::cout << "Parsed URL: " << w << " -> host=" << hp.first << " port=" << hp.second << std::endl;
+    DIE_LOG(DEBUG, "Parsed URL: " << w << " -> host=" << hp.first << " port=" << hp.second);
   }
   server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
     auto body = std::make_shared<const std::string>(std::move(req.body));
@@ -103,7 +104,7 @@ void Gateway::try_next(std::shared_ptr<Route> r) {
     const std::string node = r->order[r->next++];
     CircuitBreaker& breaker = *breakers_.at(node);
     if (!breaker.allowRequest()) {
-      if (opt_.verbose) std::cout << "Circuit breaker OPEN for " << node << ", skipping" << std::endl;
+      DIE_LOG_EVERY_MS(DEBUG, 1000, "Circuit breaker OPEN for " << node << ", skipping");
       continue;
     }
     client_->post(upstream_.at(node), "/infer", r->body, "application/json",
@@ -127,10 +128,10 @@ void Gateway::try_next(std::shared_ptr<Route> r) {
                       r->done(std::move(out));
                       return;
                     }
-                    if (opt_.verbose) {
-                      if (resp) std::cerr << "Request to " << node << " failed with status: " << resp->status << std::endl;
-                      else std::cerr << "Request to " << node << " failed: " << err << std::endl;
-                    }
+                    // the reference logs every failure (src/gateway.cpp:110-118); here at most one line
+                    // per second per site, with a count of the ones it held back
+                    if (resp) DIE_LOG_EVERY_MS(WARN, 1000, "Request to " << node << " failed with status: " << resp->status);
+                    else DIE_LOG_EVERY_MS(WARN, 1000, "Request to " << node << " failed: " << err);
                     br.recordFailure();
                     try_next(r);
                   });
@@ -162,6 +163,8 @@ Json Gateway::getStats() const {
   s["client_errors"] = static_cast<long long>(client_errors_.load());
   s["in_flight"] = client_->in_flight();
   s["upstream_connections_opened"] = client_->connections_opened();
+  s["log_lines"] = static_cast<long long>(log_lines_emitted());
+  s["log_lines_suppressed"] = static_cast<long long>(log_lines_suppressed());
   return s;
 }
 

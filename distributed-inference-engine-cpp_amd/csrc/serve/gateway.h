@@ -45,7 +45,7 @@ struct GatewayOptions {
   std::chrono::milliseconds read_timeout{5000};     // :33
   int http_threads = 0;
   int client_threads = 0;  // event loops of the worker-side client (0 = half the usable CPUs, >= 2)
-  bool verbose = false;
+  bool verbose = false;  // --verbose = log level debug (core/log.h)
 };
 
 class Gateway {

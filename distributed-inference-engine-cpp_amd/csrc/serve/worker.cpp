@@ -1,5 +1,6 @@
 #include "worker.h"
 
+#include "../core/log.h"
 #include "../core/textpack.h"
 #include "../core/trace.h"
 
@@ -406,6 +407,23 @@ Json WorkerNode::getHealth() const {
   h["http_threads"] = opt_.http_threads;
   h["engine"] = engine_->stats();
   h["engine"]["name"] = engine_->name();
+  // per-GPU I/O counters, one schema for every engine (zeros where not applicable)
+  Json io = Json::object();
+  const Json& es = h["engine"];
+  for (const char* k : {"h2d_bytes", "d2h_bytes", "graph_replays", "batches", "images"}) {
+    const Json* v = es.find(k);
+    io[k] = v ? v->as_int() : 0LL;
+  }
+  const Json* busy = es.find("device_busy_ms");
+  io["device_busy_ms"] = busy ? busy->as_double() : 0.0;
+  const Json* dev = es.find("device_id");
+  io["device_id"] = dev ? dev->as_int() : -1LL;
+  h["io"] = io;
+  Json lg = Json::object();
+  lg["level"] = static_cast<long long>(log_level());
+  lg["lines"] = static_cast<long long>(log_lines_emitted());
+  lg["suppressed"] = static_cast<long long>(log_lines_suppressed());
+  h["log"] = lg;
   Json ins = Json::array();
   for (auto d : engine_->getInputShape()) ins.push_back(static_cast<long long>(d));
   Json outs = Json::array();

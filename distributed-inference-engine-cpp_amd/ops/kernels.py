@@ -169,7 +169,8 @@ def input_prep(x_nchw, scale=None, shift=None, cp=4, split=False):
     B, C, H, W = x_nchw.shape
     out = torch.empty(((2,) if split else ()) + (B, H, W, cp), dtype=torch.bfloat16, device=x_nchw.device)
     L = native.kernels()
-    rc = L.die_kern_input_prep(_ptr(x_nchw.contiguous().float()), _ptr(scale), _ptr(shift), _ptr(out), B, C, H, W, cp,
+    xin = x_nchw.contiguous().float()  # locals keep every launched-on buffer alive through the launch
+    rc = L.die_kern_input_prep(_ptr(xin), _ptr(scale), _ptr(shift), _ptr(out), B, C, H, W, cp,
                                _stream(), int(split))
     _check(rc, "input_prep")
     return _out(out, split)
@@ -182,7 +183,8 @@ def pool2d_nhwc(x, k, stride, pad, is_max=True, count_include_pad=False, split=F
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty(((2,) if split else ()) + (B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
-    rc = native.kernels().die_kern_pool2d(_ptr(_in(x, split)), _ptr(y), B, H, W, C, Ho, Wo, k, k, stride, stride, pad,
+    xin = _in(x, split)
+    rc = native.kernels().die_kern_pool2d(_ptr(xin), _ptr(y), B, H, W, C, Ho, Wo, k, k, stride, stride, pad,
                                           pad, int(is_max), int(count_include_pad), _stream(), int(split))
     _check(rc, "pool2d")
     return _out(y, split)
@@ -194,7 +196,8 @@ def global_avgpool_nhwc(x, scale=None, shift=None, relu=False, split=False):
     B, H, W, C = x.shape
     out = torch.empty(((2,) if split else ()) + (B, C), dtype=torch.bfloat16, device=x.device)
     out32 = torch.empty((B, C), dtype=torch.float32, device=x.device)
-    rc = native.kernels().die_kern_gap(_ptr(_in(x, split)), _ptr(out), _ptr(out32), _ptr(scale), _ptr(shift),
+    xin = _in(x, split)
+    rc = native.kernels().die_kern_gap(_ptr(xin), _ptr(out), _ptr(out32), _ptr(scale), _ptr(shift),
                                        int(relu), B, H * W, C, _stream(), int(split))
     _check(rc, "global_avgpool")
     return _out(out, split), out32
@@ -207,7 +210,8 @@ def affine_act(x, scale=None, shift=None, z=None, relu=False, split=False):
     M = x.numel() // C
     y = torch.empty(((2,) if split else ()) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
     zz = None if z is None else _in(z, split)
-    rc = native.kernels().die_kern_affine(_ptr(_in(x, split)), _ptr(zz), _ptr(scale), _ptr(shift), int(relu), _ptr(y),
+    xin = _in(x, split)
+    rc = native.kernels().die_kern_affine(_ptr(xin), _ptr(zz), _ptr(scale), _ptr(shift), int(relu), _ptr(y),
                                           M, C, _stream(), int(split))
     _check(rc, "affine_act")
     return _out(y, split)
@@ -233,8 +237,8 @@ def layernorm(x, gamma, beta, eps=1e-5, split=False):
 
     C = x.shape[-1]
     y = torch.empty(((2,) if split else ()) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
-    rc = native.kernels().die_kern_layernorm(_ptr(_in(x, split)), _ptr(y), _ptr(gamma.float().contiguous()),
-                                             _ptr(beta.float().contiguous()), float(eps), x.numel() // C, C, _stream(),
+    xin, gm, bt = _in(x, split), gamma.float().contiguous(), beta.float().contiguous()
+    rc = native.kernels().die_kern_layernorm(_ptr(xin), _ptr(y), _ptr(gm), _ptr(bt), float(eps), x.numel() // C, C, _stream(),
                                              int(split))
     _check(rc, "layernorm")
     return _out(y, split)
@@ -246,7 +250,8 @@ def tokens_assemble(patches, cls=None, pos=None, split=False):
 
     B, S0, C = patches.shape
     out = torch.empty(((2,) if split else ()) + (B, S0 + 1, C), dtype=torch.bfloat16, device=patches.device)
-    rc = native.kernels().die_kern_tokens(_ptr(_in(patches, split)), _ptr(cls), _ptr(pos), _ptr(out), B, S0, C,
+    pin = _in(patches, split)
+    rc = native.kernels().die_kern_tokens(_ptr(pin), _ptr(cls), _ptr(pos), _ptr(out), B, S0, C,
                                           _stream(), int(split))
     _check(rc, "tokens_assemble")
     return _out(out, split)
@@ -257,7 +262,8 @@ def gather_rows(x, idx, split=False):
 
     B, S, C = x.shape
     y = torch.empty(((2,) if split else ()) + (B, C), dtype=torch.bfloat16 if split else x.dtype, device=x.device)
-    rc = native.kernels().die_kern_gather_rows(_ptr(_in(x, split)), _ptr(y), B, S, int(idx), C, _stream(), int(split))
+    xin = _in(x, split)
+    rc = native.kernels().die_kern_gather_rows(_ptr(xin), _ptr(y), B, S, int(idx), C, _stream(), int(split))
     _check(rc, "gather_rows")
     return _out(y, split)
 
@@ -358,7 +364,8 @@ def conv_stem7x7(x_nhwc4, w, bias, relu=True, split=False):
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     out = torch.empty(((2,) if split else ()) + (B, Ho, Wo, 64), dtype=torch.bfloat16, device=x_nhwc4.device)
     b = bias.float().contiguous()
-    rc = native.kernels().die_kern_stem(_ptr(_in(x_nhwc4, split)), _ptr(pack_stem_weight(w, split)), _ptr(b), _ptr(out),
+    xin, wp = _in(x_nhwc4, split), pack_stem_weight(w, split)
+    rc = native.kernels().die_kern_stem(_ptr(xin), _ptr(wp), _ptr(b), _ptr(out),
                                         B, H, W, Ho, Wo, int(relu), _stream(), int(split))
     _check(rc, "conv_stem7x7")
     return _out(out, split)

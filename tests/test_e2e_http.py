@@ -275,3 +275,49 @@ def test_malformed_bodies_leave_breakers_closed(cluster):
     assert s["failovers"] == before["failovers"]
     st, out = post(gw.url + "/infer", {"request_id": "good_after_bad", "input_data": [1.0]})
     assert st == 200
+
+
+def test_health_io_and_log_counters(cluster):
+    """SURVEY §5.5 observability: /health carries per-device I/O counters and logger statistics with
+    one schema for every engine; the counters move with traffic."""
+    w = cluster["workers"][1]
+    _, h0 = get(w.url + "/health")
+    for k in ("device_id", "h2d_bytes", "d2h_bytes", "graph_replays", "device_busy_ms", "batches", "images"):
+        assert k in h0["io"], k
+    for k in ("level", "lines", "suppressed"):
+        assert k in h0["log"], k
+    for i in range(5):
+        st, _ = post(w.url + "/infer", {"request_id": "io_%d" % i, "input_data": [float(i), 2.0, 3.0, 4.5]})
+        assert st == 200
+    _, h1 = get(w.url + "/health")
+    assert h1["io"]["batches"] > h0["io"]["batches"] and h1["io"]["images"] >= h0["io"]["images"] + 5
+    assert h1["engine"]["name"].startswith("cpu")
+    _, s = get(cluster["gw"].url + "/stats")
+    assert "log_lines" in s and "log_lines_suppressed" in s
+
+
+def test_gateway_failure_logging_is_rate_limited(native, models):
+    """A dead worker produces one WARN line per second per call site, not one per request (the
+    reference flushes two lines per request: SURVEY Q11)."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    dead = s.getsockname()[1]
+    s.close()
+    path = models["tiny"][0]
+    live = native.Worker(path, node_id="live", engine={"device": "cpu"})
+    gw = native.GatewayServer(["127.0.0.1:%d" % dead, "127.0.0.1:%d" % live.port], failure_threshold=1000)
+    try:
+        _, s0 = get(gw.url + "/stats")
+        for i in range(60):
+            st, _ = post(gw.url + "/infer", {"request_id": "rl_%d" % i, "input_data": [1.0]})
+            assert st == 200
+        _, s1 = get(gw.url + "/stats")
+        emitted = s1["log_lines"] - s0["log_lines"]
+        suppressed = s1["log_lines_suppressed"] - s0["log_lines_suppressed"]
+        assert s1["failovers"] - s0["failovers"] > 10
+        assert emitted <= 5 and suppressed > 5, (emitted, suppressed)
+    finally:
+        gw.stop()
+        live.stop()

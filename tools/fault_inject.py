@@ -45,7 +45,8 @@ def _wait_http(url, timeout_s=60.0):
 
 class Cluster:
     def __init__(self, model, n_workers=3, device="cpu", base_port=0, breaker_timeout_s=1.0, failure_threshold=5,
-                 success_threshold=2, read_timeout_ms=2000, connect_timeout_ms=500, log_dir=None, worker_threads=0):
+                 success_threshold=2, read_timeout_ms=2000, connect_timeout_ms=500, log_dir=None, worker_threads=0,
+                 stagger=False, worker_args=()):
         import socket
 
         def free_port():
@@ -62,11 +63,16 @@ class Cluster:
         self.env = dict(os.environ)
         if worker_threads:  # CPU workers share the host: cap each one's OpenMP pool
             self.env["OMP_NUM_THREADS"] = str(worker_threads)
+        self.worker_args = list(worker_args)
         self.workers = [None] * n_workers
+        # stagger: GPU workers start one at a time (the first fills the autotune cache the others load;
+        # HIP workers sharing GPU 0 is the reference's own topology)
         for i in range(n_workers):
             self.start_worker(i)
+            if stagger:
+                _wait_http("http://127.0.0.1:%d/health" % self.ports[i], 300.0)
         for p in self.ports:
-            _wait_http("http://127.0.0.1:%d/health" % p)
+            _wait_http("http://127.0.0.1:%d/health" % p, 300.0)
         args = [os.path.join(BIN, "gateway")] + ["127.0.0.1:%d" % p for p in self.ports] + [
             "--port", str(self.gw_port), "--host", "127.0.0.1", "--breaker-timeout-s", str(breaker_timeout_s),
             "--failure-threshold", str(failure_threshold), "--success-threshold", str(success_threshold),
@@ -90,17 +96,18 @@ class Cluster:
 
     def start_worker(self, i):
         args = [os.path.join(BIN, "worker_node"), str(self.ports[i]), "w%d" % i, self.model, "--host", "127.0.0.1",
-                "--device", self.device]
+                "--device", self.device] + self.worker_args
         self.workers[i] = subprocess.Popen(args, stdout=self._log("worker%d" % i), stderr=subprocess.STDOUT,
                                            start_new_session=True, env=self.env)
 
     def signal(self, i, sig):
         self.workers[i].send_signal(sig)
 
-    def restart(self, i):
+    def restart(self, i, wait=True):
         self.workers[i].wait(timeout=10)
         self.start_worker(i)
-        _wait_http("http://127.0.0.1:%d/health" % self.ports[i])
+        if wait:
+            _wait_http("http://127.0.0.1:%d/health" % self.ports[i], 300.0)
 
     def stats(self):
         return _get(self.url + "/stats")
