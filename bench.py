@@ -57,6 +57,8 @@ def main():
                          "forward-only (a step = one batch)")
     ap.add_argument("--no-direct", action="store_true", help="skip the extra direct-to-worker measurement")
     ap.add_argument("--gw-client-threads", type=int, default=0, help="gateway forwarding loops (0 = auto)")
+    ap.add_argument("--no-local-shm", action="store_true",
+                    help="gateway sends co-located workers the body bytes instead of a shared-memory descriptor")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
@@ -157,7 +159,8 @@ def main():
             if dist is not None:
                 ports = [None] * world
                 dist.all_gather_object(ports, wk.port)
-            gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads)
+            gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
+                                      local_shm=not args.no_local_shm)
             target_port = gw.port
         lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
@@ -201,6 +204,8 @@ def main():
         if gw:
             extra["gateway"] = {"failovers": g1["failovers"] - g0["failovers"], "failed": g1["failed"] - g0["failed"],
                                 "upstream_connections": g1.get("upstream_connections_opened"),
+                                "shm_forwards": g1.get("shm_forwards", 0) - g0.get("shm_forwards", 0),
+                                "byte_forwards": g1.get("byte_forwards", 0) - g0.get("byte_forwards", 0),
                                 "breakers": [b["state"] for b in g1["circuit_breakers"]]}
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)

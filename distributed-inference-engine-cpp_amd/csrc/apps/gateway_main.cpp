@@ -9,7 +9,7 @@
 #include "../serve/gateway.h"
 
 int main(int argc, char** argv) {
-  die::Flags f(argc, argv, {"verbose"});
+  die::Flags f(argc, argv, {"verbose", "no-local-shm"});
   const auto& pos = f.positional();
   if (pos.empty()) {
     std::cerr << "Usage: " << argv[0] << " <worker1:port> [worker2:port] ... [options]\n"
@@ -18,7 +18,9 @@ int main(int argc, char** argv) {
               << "  --port N (8000)  --failure-threshold N (5)  --success-threshold N (2)\n"
               << "  --breaker-timeout-s S (30)  --vnodes N (150)  --connect-timeout-ms N (5000)\n"
               << "  --read-timeout-ms N (5000)  --client-threads N (CPUs/2)  --http-threads N  --verbose\n"
-              << "  --log-level trace|debug|info|warn|error|off (info; env DIE_LOG_LEVEL)"
+              << "  --log-level trace|debug|info|warn|error|off (info; env DIE_LOG_LEVEL)\n"
+              << "  --no-local-shm (send co-located workers the body bytes, not a shared-memory descriptor)"
+              << "  --shm-mb N (512)"
               << std::endl;
     return 1;
   }
@@ -38,6 +40,8 @@ int main(int argc, char** argv) {
   o.connect_timeout = std::chrono::milliseconds(f.i("connect-timeout-ms", 5000));
   o.read_timeout = std::chrono::milliseconds(f.i("read-timeout-ms", 5000));
   o.client_threads = static_cast<int>(f.i("client-threads", 0));
+  o.local_shm = !f.b("no-local-shm");
+  o.shm_mb = static_cast<size_t>(f.i("shm-mb", 512));
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.verbose = f.b("verbose");
   if (o.verbose) die::set_log_level(die::LogLevel::DEBUG);

@@ -71,7 +71,7 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower"});
+  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower", "no-shm"});
   const auto& pos = f.positional();
   if (f.b("dp-follower")) {
     sigset_t fs;
@@ -140,6 +140,7 @@ int main(int argc, char** argv) {
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));
   o.verbose = f.b("verbose");
+  o.accept_shm = !f.b("no-shm");
   if (o.verbose) die::set_log_level(die::LogLevel::DEBUG);
   die::LogLevel lv;
   if (die::parse_log_level(f.str("log-level", ""), &lv)) die::set_log_level(lv);

@@ -451,6 +451,7 @@ void* die_worker_create(const char* opts_json, char** err) {
     o.engine = engine_opts(j.contains("engine") ? j.at("engine") : Json::object());
     o.fault_fail_rate = jget<double>(j, "fault_fail_rate", 0.0);
     o.fault_latency_ms = jget<int>(j, "fault_latency_ms", 0);
+    o.accept_shm = jget<bool>(j, "accept_shm", true);
     auto* w = new WorkerNode(o);
     if (w->start() < 0) {
       delete w;
@@ -533,6 +534,8 @@ void* die_gateway_create(const char* opts_json, char** err) {
     o.read_timeout = std::chrono::milliseconds(jget<long>(j, "read_timeout_ms", 5000));
     o.client_threads = jget<int>(j, "client_threads", 0);
     o.http_threads = jget<int>(j, "http_threads", 0);
+    o.local_shm = jget<bool>(j, "local_shm", true);
+    o.shm_mb = static_cast<size_t>(jget<long>(j, "shm_mb", 512));
     auto* g = new Gateway(o);
     if (g->start() < 0) {
       delete g;

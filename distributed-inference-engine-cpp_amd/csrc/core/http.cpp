@@ -188,6 +188,8 @@ struct HttpServer::Conn {
   bool chunked = false;
   size_t body_len = 0;     // content-length
   size_t body_have = 0;
+  BodyBuffer ext;          // allocator memory the current body is received into (if any)
+  char* body_dst() { return ext.data ? ext.data : &req.body[0]; }
   HttpRequest req;
   bool busy = false;       // a request is being handled
   bool peer_eof = false;
@@ -446,11 +448,18 @@ void HttpServer::reactor_loop(Reactor* r) {
         c->in.erase(0, he + 4);
         c->headers_done = true;
         c->req.t_headers = std::chrono::steady_clock::now();
+        c->ext = BodyBuffer{};
+        if (!c->chunked && body_alloc_ && c->body_len >= body_alloc_min_ && c->body_len > 0) {
+          c->ext = body_alloc_(c->body_len + 64);
+          if (c->ext.data && c->ext.capacity < c->body_len + 64) c->ext = BodyBuffer{};
+        }
         if (!c->chunked) {
-          c->req.body.reserve(c->body_len + 64);
-          c->req.body.resize(c->body_len);
+          if (!c->ext.data) {
+            c->req.body.reserve(c->body_len + 64);
+            c->req.body.resize(c->body_len);
+          }
           size_t take = std::min(c->body_len, c->in.size());
-          std::memcpy(&c->req.body[0], c->in.data(), take);
+          if (take) std::memcpy(c->body_dst(), c->in.data(), take);
           c->in.erase(0, take);
           c->body_have = take;
         }
@@ -479,6 +488,13 @@ void HttpServer::reactor_loop(Reactor* r) {
         return true;
       }
       // complete request
+      if (c->ext.data) {
+        std::memset(c->ext.data + c->body_len, 0, 64);  // parser slack
+        c->req.ext_body = c->ext.data;
+        c->req.ext_len = c->body_len;
+        c->req.ext_owner = std::move(c->ext.owner);
+        c->ext = BodyBuffer{};
+      }
       c->headers_done = false;
       c->busy = true;
       dispatch(r, c);
@@ -492,7 +508,7 @@ void HttpServer::reactor_loop(Reactor* r) {
     while (true) {
       ssize_t n;
       if (c->headers_done && !c->chunked && c->body_have < c->body_len) {
-        n = ::recv(c->fd, &c->req.body[c->body_have], c->body_len - c->body_have, 0);
+        n = ::recv(c->fd, c->body_dst() + c->body_have, c->body_len - c->body_have, 0);
         if (n > 0) {
           c->body_have += static_cast<size_t>(n);
           continue;

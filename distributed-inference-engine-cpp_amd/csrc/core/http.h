@@ -23,15 +23,29 @@
 
 namespace die {
 
+// Memory a request body may be received into instead of HttpRequest::body (see
+// HttpServer::set_body_allocator); `owner` releases it.
+struct BodyBuffer {
+  char* data = nullptr;
+  size_t capacity = 0;
+  std::shared_ptr<void> owner;
+};
+
 struct HttpRequest {
   std::string method;
   std::string path;    // without query string
   std::string query;   // raw query string (after '?'), may be empty
   std::vector<std::pair<std::string, std::string>> headers;  // names lower-cased
   std::string body;    // capacity always >= size + 64 (slack for SIMD parsers)
+  // Body received into allocator memory (then `body` is empty): ext_len bytes at ext_body, followed by
+  // 64 zero bytes of slack; ext_owner keeps the memory alive.
+  char* ext_body = nullptr;
+  size_t ext_len = 0;
+  std::shared_ptr<void> ext_owner;
   bool keep_alive = true;
   std::chrono::steady_clock::time_point t_headers{};  // when the request head was parsed
   std::string_view header(std::string_view name) const;  // name must be lower-case
+  std::string_view body_view() const { return ext_body ? std::string_view(ext_body, ext_len) : std::string_view(body); }
 };
 
 struct HttpResponse {
@@ -79,6 +93,12 @@ class HttpServer {
   HttpServer& operator=(const HttpServer&) = delete;
 
   void route(const std::string& method, const std::string& path, Handler h);
+  // Receive Content-Length bodies of >= min_bytes straight into memory from `alloc(len + 64)`
+  // (e.g. a shared-memory arena the next hop reads in place); an empty BodyBuffer declines.
+  void set_body_allocator(std::function<BodyBuffer(size_t)> alloc, size_t min_bytes) {
+    body_alloc_ = std::move(alloc);
+    body_alloc_min_ = min_bytes;
+  }
   // Bind and start `threads` reactor threads (0 = hardware concurrency, capped at 32).
   // port 0 picks an ephemeral port; returns the bound port, or -1 on failure.
   int start(const std::string& host, int port, int threads = 0);
@@ -98,6 +118,8 @@ class HttpServer {
   void dispatch(Reactor* r, Conn* c);
 
   std::vector<std::pair<std::pair<std::string, std::string>, Handler>> routes_;
+  std::function<BodyBuffer(size_t)> body_alloc_;
+  size_t body_alloc_min_ = 0;
   std::vector<std::unique_ptr<Reactor>> reactors_;
   std::vector<std::thread> threads_;
   int listen_fd_ = -1;

@@ -25,7 +25,7 @@ using Clock = std::chrono::steady_clock;
 struct AsyncHttpClient::Job {
   int upstream = 0;
   std::string head;  // request line + headers
-  std::shared_ptr<const std::string> body;
+  BodyRef body;
   Callback cb;
   bool retried = false;  // already re-sent once after a stale keep-alive connection
 };
@@ -87,8 +87,8 @@ int AsyncHttpClient::add_upstream(const std::string& host, int port) {
   return static_cast<int>(ups_.size()) - 1;
 }
 
-void AsyncHttpClient::post(int upstream, const std::string& path, std::shared_ptr<const std::string> body,
-                           const std::string& content_type, Callback cb) {
+void AsyncHttpClient::post(int upstream, const std::string& path, BodyRef body, const std::string& content_type,
+                           const std::string& extra_headers, Callback cb) {
   if (upstream < 0 || upstream >= static_cast<int>(ups_.size()) || !running_.load()) {
     cb(std::nullopt, "client stopped or unknown upstream");
     return;
@@ -104,8 +104,10 @@ void AsyncHttpClient::post(int upstream, const std::string& path, std::shared_pt
   j->head += "\r\nContent-Type: ";
   j->head += content_type;
   j->head += "\r\nContent-Length: ";
-  j->head += std::to_string(body ? body->size() : 0);
-  j->head += "\r\nConnection: keep-alive\r\n\r\n";
+  j->head += std::to_string(body.size);
+  j->head += "\r\n";
+  j->head += extra_headers;
+  j->head += "Connection: keep-alive\r\n\r\n";
   j->body = std::move(body);
   j->cb = std::move(cb);
   in_flight_.fetch_add(1, std::memory_order_relaxed);
@@ -197,16 +199,16 @@ void AsyncHttpClient::run(Loop* L) {
   // Write as much of the request as the socket takes; returns false if the connection failed.
   auto pump_write = [&](Conn* c) -> bool {
     const std::string& h = c->job->head;
-    const std::string* b = c->job->body.get();
-    const size_t bs = b ? b->size() : 0, total = h.size() + bs;
+    const char* bd = c->job->body.data;
+    const size_t bs = bd ? c->job->body.size : 0, total = h.size() + bs;
     while (c->out_off < total) {
       iovec iov[2];
       int n = 0;
       if (c->out_off < h.size()) {
         iov[n++] = {const_cast<char*>(h.data()) + c->out_off, h.size() - c->out_off};
-        if (bs) iov[n++] = {const_cast<char*>(b->data()), bs};
+        if (bs) iov[n++] = {const_cast<char*>(bd), bs};
       } else {
-        iov[n++] = {const_cast<char*>(b->data()) + (c->out_off - h.size()), total - c->out_off};
+        iov[n++] = {const_cast<char*>(bd) + (c->out_off - h.size()), total - c->out_off};
       }
       msghdr mh{};
       mh.msg_iov = iov;

@@ -39,10 +39,21 @@ class AsyncHttpClient {
 
   // Register an upstream before the first request; returns its id.
   int add_upstream(const std::string& host, int port);
-  // Thread-safe; `cb` runs exactly once, on a loop thread.  `body` must stay alive until then (the
-  // shared_ptr keeps it).
+  // Request body bytes that stay valid while `owner` is held (no copy is made).
+  struct BodyRef {
+    const char* data = nullptr;
+    size_t size = 0;
+    std::shared_ptr<const void> owner;
+  };
+  // Thread-safe; `cb` runs exactly once, on a loop thread.  `extra_headers` ("Name: value\r\n"
+  // lines) are sent as given.
+  void post(int upstream, const std::string& path, BodyRef body, const std::string& content_type,
+            const std::string& extra_headers, Callback cb);
   void post(int upstream, const std::string& path, std::shared_ptr<const std::string> body,
-            const std::string& content_type, Callback cb);
+            const std::string& content_type, Callback cb) {
+    BodyRef b{body ? body->data() : nullptr, body ? body->size() : 0, body};
+    post(upstream, path, std::move(b), content_type, std::string(), std::move(cb));
+  }
   void stop();
 
   long long in_flight() const { return in_flight_.load(); }

@@ -1,5 +1,7 @@
 #include "gateway.h"
 
+#include <unistd.h>
+
 #include <iostream>
 
 #include "../core/log.h"
@@ -27,7 +29,8 @@ HttpResponse error_response(const std::string& msg) {
 // One request's failover walk: the primary, then the other nodes in ring order
 // (src/gateway.cpp:46-59).
 struct Gateway::Route {
-  std::shared_ptr<const std::string> body;
+  AsyncHttpClient::BodyRef body;
+  long long shm_off = -1;
   std::function<void(HttpResponse&&)> done;
   std::string target;
   std::vector<std::string> order;
@@ -48,11 +51,48 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
                                                     opt_.breaker_timeout);
     auto hp = parse_host_port(w);
     upstream_[w] = client_->add_upstream(hp.first, hp.second);
+    node_shm_[w] = std::make_unique<NodeShm>();
+    node_shm_[w]->local = hp.first == "127.0.0.1" || hp.first == "localhost";
     DIE_LOG(DEBUG, "Parsed URL: " << w << " -> host=" << hp.first << " port=" << hp.second);
   }
+  bool any_local = false;
+  for (auto& kv : node_shm_) any_local |= kv.second->local;
+  if (opt_.local_shm && any_local) {
+    static std::atomic<int> instance{0};
+    std::string err;
+    shm_ = ShmArena::create("/die_gw_" + std::to_string(getpid()) + "_" + std::to_string(instance++),
+                            opt_.shm_mb << 20, &err);
+    if (!shm_) DIE_LOG(WARN, "gateway: no shared-memory body arena (" << err << "); forwarding bytes");
+  }
+  if (shm_) {
+    // large bodies are received straight into the arena (the client's bytes are copied once, by the
+    // kernel, into memory the co-located worker reads in place)
+    std::weak_ptr<ShmArena> wa = shm_;
+    server_.set_body_allocator(
+        [wa](size_t n) -> BodyBuffer {
+          auto a = wa.lock();
+          if (!a) return {};
+          const long long off = a->alloc(n);
+          if (off < 0) return {};
+          BodyBuffer b;
+          b.data = a->base() + off;
+          b.capacity = n;
+          b.owner = std::shared_ptr<void>(b.data, [a, off](void*) { a->free(off); });
+          return b;
+        },
+        64 << 10);
+  }
   server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
-    auto body = std::make_shared<const std::string>(std::move(req.body));
-    routeRequest(std::move(body), [res](HttpResponse&& r) { res.send(std::move(r)); });
+    AsyncHttpClient::BodyRef b;
+    long long off = -1;
+    if (req.ext_body) {
+      b = AsyncHttpClient::BodyRef{req.ext_body, req.ext_len, req.ext_owner};
+      off = req.ext_body - shm_->base();
+    } else {
+      auto body = std::make_shared<const std::string>(std::move(req.body));
+      b = AsyncHttpClient::BodyRef{body->data(), body->size(), body};
+    }
+    routeRequest(std::move(b), off, [res](HttpResponse&& r) { res.send(std::move(r)); });
   });
   server_.route("GET", "/stats", [this](HttpRequest&, Responder res) {
     HttpResponse r;
@@ -70,13 +110,14 @@ void Gateway::stop() {
   if (client_) client_->stop();
 }
 
-void Gateway::routeRequest(std::shared_ptr<const std::string> body, std::function<void(HttpResponse&&)> done) {
+void Gateway::routeRequest(AsyncHttpClient::BodyRef body, long long shm_off, std::function<void(HttpResponse&&)> done) {
   routed_++;
   std::string request_id;
-  if (!find_top_level_string(*body, "request_id", request_id)) {
+  const std::string_view view(body.data ? body.data : "", body.size);
+  if (!find_top_level_string(view, "request_id", request_id)) {
     // Slow path only to produce the same kind of error the reference returns.
     try {
-      Json j = Json::parse(*body);
+      Json j = Json::parse(view);
       request_id = j.at("request_id").as_string();
     } catch (const std::exception& e) {
       failed_++;
@@ -86,6 +127,7 @@ void Gateway::routeRequest(std::shared_ptr<const std::string> body, std::functio
   }
   auto r = std::make_shared<Route>();
   r->body = std::move(body);
+  r->shm_off = shm_off;
   r->done = std::move(done);
   r->target = ring_.getNode(request_id);
   if (r->target.empty()) {
@@ -107,9 +149,29 @@ void Gateway::try_next(std::shared_ptr<Route> r) {
       DIE_LOG_EVERY_MS(DEBUG, 1000, "Circuit breaker OPEN for " << node << ", skipping");
       continue;
     }
-    client_->post(upstream_.at(node), "/infer", r->body, "application/json",
-                  [this, r, node](std::optional<HttpResponse> resp, const std::string& err) {
+    NodeShm& ns = *node_shm_.at(node);
+    const bool via_shm = r->shm_off >= 0 && shm_ && ns.local && ns.ok.load(std::memory_order_relaxed);
+    AsyncHttpClient::BodyRef send = r->body;
+    std::string extra;
+    if (via_shm) {  // descriptor only: the worker parses the body where it lies
+      extra = "X-Die-Shm: " + shm_->name() + ":" + std::to_string(r->shm_off) + ":" + std::to_string(r->body.size) + "\r\n";
+      send = AsyncHttpClient::BodyRef{nullptr, 0, r->body.owner};
+      shm_forwards_++;
+    } else {
+      byte_forwards_++;
+    }
+    client_->post(upstream_.at(node), "/infer", std::move(send), "application/json", extra,
+                  [this, r, node, via_shm](std::optional<HttpResponse> resp, const std::string& err) {
                     CircuitBreaker& br = *breakers_.at(node);
+                    if (via_shm && resp && resp->header("x-die-error") == "shm") {
+                      // this worker cannot map the arena (other host / namespace): send it bytes
+                      node_shm_.at(node)->ok.store(false);
+                      DIE_LOG(WARN, "worker " << node << " cannot read the shared-memory arena (" << resp->body
+                                              << "); forwarding bodies as bytes");
+                      --r->next;
+                      try_next(r);
+                      return;
+                    }
                     if (resp && resp->status == 200) {
                       br.recordSuccess();
                       if (node != r->target) failovers_++;
@@ -163,6 +225,9 @@ Json Gateway::getStats() const {
   s["client_errors"] = static_cast<long long>(client_errors_.load());
   s["in_flight"] = client_->in_flight();
   s["upstream_connections_opened"] = client_->connections_opened();
+  s["shm_forwards"] = static_cast<long long>(shm_forwards_.load());
+  s["byte_forwards"] = static_cast<long long>(byte_forwards_.load());
+  s["shm_arena_mib"] = shm_ ? static_cast<double>(shm_->size()) / (1 << 20) : 0.0;
   s["log_lines"] = static_cast<long long>(log_lines_emitted());
   s["log_lines_suppressed"] = static_cast<long long>(log_lines_suppressed());
   return s;

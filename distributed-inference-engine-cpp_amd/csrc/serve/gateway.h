@@ -28,6 +28,7 @@
 #include "../core/http.h"
 #include "../core/http_async.h"
 #include "../core/json.h"
+#include "../core/shm_arena.h"
 #include "circuit_breaker.h"
 #include "consistent_hash.h"
 
@@ -46,6 +47,11 @@ struct GatewayOptions {
   int http_threads = 0;
   int client_threads = 0;  // event loops of the worker-side client (0 = half the usable CPUs, >= 2)
   bool verbose = false;  // --verbose = log level debug (core/log.h)
+  // Co-located workers (loopback upstreams) get large bodies as a shared-memory descriptor instead
+  // of the bytes (core/shm_arena.h); a worker that cannot map the arena answers X-Die-Error: shm
+  // and is sent the bytes from then on.
+  bool local_shm = true;
+  size_t shm_mb = 512;
 };
 
 class Gateway {
@@ -61,7 +67,8 @@ class Gateway {
   // Route one /infer body (reference Gateway::routeRequest, src/gateway.cpp:38-61): primary by
   // request_id, then every other node in ring order; `done(status, response)` runs once, on a
   // client loop thread (or inline for requests that never reach a worker).
-  void routeRequest(std::shared_ptr<const std::string> body, std::function<void(HttpResponse&&)> done);
+  // shm_off >= 0: the body lies in this gateway's arena at that offset.
+  void routeRequest(AsyncHttpClient::BodyRef body, long long shm_off, std::function<void(HttpResponse&&)> done);
   const ConsistentHash& ring() const { return ring_; }
 
  private:
@@ -72,6 +79,13 @@ class Gateway {
   ConsistentHash ring_;
   std::map<std::string, std::unique_ptr<CircuitBreaker>> breakers_;
   std::map<std::string, int> upstream_;  // node -> AsyncHttpClient upstream id
+  std::shared_ptr<ShmArena> shm_;
+  struct NodeShm {
+    bool local = false;
+    std::atomic<bool> ok{true};
+  };
+  std::map<std::string, std::unique_ptr<NodeShm>> node_shm_;
+  std::atomic<int64_t> shm_forwards_{0}, byte_forwards_{0};
   std::unique_ptr<AsyncHttpClient> client_;
   HttpServer server_;
   std::atomic<int64_t> routed_{0}, failovers_{0}, failed_{0}, client_errors_{0};

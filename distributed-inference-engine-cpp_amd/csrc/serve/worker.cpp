@@ -186,18 +186,34 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   InputKey key;
   size_t text_len = 0, text_off = 0;
   bool packed = false;
+  std::string_view body = req.body_view();
+  if (const std::string_view desc = req.header("x-die-shm"); !desc.empty()) {
+    // co-located gateway: the body lies in its shared-memory arena (core/shm_arena.h)
+    const char* p = nullptr;
+    size_t n = 0;
+    std::string err;
+    if (!opt_.accept_shm || !shm_reader_.resolve(desc, &p, &n, &err)) {
+      pool.release(sink.buf);
+      HttpResponse r = error_response(500, opt_.accept_shm ? err : "shared-memory bodies disabled");
+      r.headers.emplace_back("X-Die-Error", "shm");
+      res.send(std::move(r));
+      return;
+    }
+    body = std::string_view(p, n);
+    shm_bodies_.fetch_add(1, std::memory_order_relaxed);
+  }
   try {
-    seen = parse_infer_body(req.body, sink);
+    seen = parse_infer_body(body, sink);
     if ((seen & 4) && sink.text_n > text_cap) {  // too long for device decode: parse on the host
       sink.defer = false;
       sink.text = nullptr;
-      seen = parse_infer_body(req.body, sink);
+      seen = parse_infer_body(body, sink);
     }
     if (!(seen & 1)) throw JsonError("key 'request_id' not found");
     if (!(seen & 2)) throw JsonError("key 'input_data' not found");
     if (seen & 4) {
       text_len = sink.text_n;
-      text_off = static_cast<size_t>(sink.text - req.body.data());
+      text_off = static_cast<size_t>(sink.text - body.data());
       auto* dst = reinterpret_cast<uint8_t*>(sink.buf.data);
       if (eng.text_packing() && pack_nibbles(sink.text, sink.text_n, dst)) {
         packed = true;  // half the bytes to copy to the device
@@ -222,7 +238,7 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
                             std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_parse)
                                 .count()),
                         std::memory_order_relaxed);
-    parse_bytes_.fetch_add(static_cast<int64_t>(req.body.size()), std::memory_order_relaxed);
+    parse_bytes_.fetch_add(static_cast<int64_t>(body.size()), std::memory_order_relaxed);
     parsed_.fetch_add(1, std::memory_order_relaxed);
   } catch (const std::exception& e) {
     pool.release(sink.buf);
@@ -395,6 +411,7 @@ Json WorkerNode::getHealth() const {
   h["parse_us_avg"] = np ? parse_ns_.load() / 1e3 / np : 0.0;
   h["parse_gbps"] = parse_ns_.load() ? static_cast<double>(parse_bytes_.load()) / parse_ns_.load() : 0.0;
   h["device_decoded"] = static_cast<long long>(device_decoded_.load());
+  h["shm_bodies"] = static_cast<long long>(shm_bodies_.load());
   h["decode_fallbacks"] = static_cast<long long>(decode_fallbacks_.load());
   Json st = Json::object();
   st["recv"] = h_recv_.snapshot();

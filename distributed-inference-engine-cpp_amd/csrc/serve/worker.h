@@ -18,6 +18,7 @@
 
 #include "../core/http.h"
 #include "../core/json.h"
+#include "../core/shm_arena.h"
 #include "../engine/engine.h"
 #include "batcher.h"
 #include "lru_cache.h"
@@ -40,6 +41,8 @@ struct WorkerOptions {
   double fault_fail_rate = 0.0;
   int fault_latency_ms = 0;
   bool verbose = false;
+  // Accept X-Die-Shm body descriptors from a co-located gateway (core/shm_arena.h).
+  bool accept_shm = true;
 };
 
 class WorkerNode {
@@ -95,7 +98,8 @@ class WorkerNode {
   std::atomic<int64_t> cache_hits_{0};
   std::atomic<int64_t> errors_{0};
   std::atomic<int64_t> parse_ns_{0}, parse_bytes_{0}, parsed_{0};
-  std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0};
+  std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0}, shm_bodies_{0};
+  ShmReader shm_reader_;
   // request stages: parse (body -> staging), queue (batcher wait), engine (submit -> outputs on
   // host), respond (outputs -> serialised response), total (handler entry -> response)
   StageHist h_recv_, h_parse_, h_queue_, h_engine_, h_respond_, h_total_;  // recv: head parsed -> body complete

@@ -310,7 +310,7 @@ def test_gateway_failure_logging_is_rate_limited(native, models):
     gw = native.GatewayServer(["127.0.0.1:%d" % dead, "127.0.0.1:%d" % live.port], failure_threshold=1000)
     try:
         _, s0 = get(gw.url + "/stats")
-        for i in range(60):
+        for i in range(200):
             st, _ = post(gw.url + "/infer", {"request_id": "rl_%d" % i, "input_data": [1.0]})
             assert st == 200
         _, s1 = get(gw.url + "/stats")
@@ -321,3 +321,33 @@ def test_gateway_failure_logging_is_rate_limited(native, models):
     finally:
         gw.stop()
         live.stop()
+
+
+def test_large_bodies_cross_shared_memory(native, models):
+    """Bodies >= 64 KiB reach a co-located worker as an X-Die-Shm descriptor (the gateway received
+    them into its shared-memory arena); the answer equals the direct one.  A worker that refuses
+    descriptors gets the bytes instead, without a breaker failure."""
+    import numpy as np
+
+    path = models["tiny"][0]
+    a = native.Worker(path, node_id="shm_a", engine={"device": "cpu"})
+    b = native.Worker(path, node_id="shm_b", engine={"device": "cpu"}, accept_shm=False)
+    gw = native.GatewayServer(["127.0.0.1:%d" % a.port, "127.0.0.1:%d" % b.port])
+    try:
+        rng = np.random.default_rng(3)
+        for i in range(16):
+            vals = np.round(rng.random(3 * 64 * 64), 4).tolist()
+            body = {"request_id": "big_%d" % i, "input_data": vals}
+            st, out = post(gw.url + "/infer", body)
+            assert st == 200, out
+            direct = a if out["node_id"] == "shm_a" else b
+            st2, ref = post(direct.url + "/infer", dict(body, request_id="d_%d" % i))
+            assert st2 == 200 and ref["output_data"] == out["output_data"]
+        _, s = get(gw.url + "/stats")
+        assert s["shm_arena_mib"] > 0 and s["shm_forwards"] > 0 and s["byte_forwards"] > 0, s
+        assert all(x["state"] == "CLOSED" and x["failures"] == 0 for x in s["circuit_breakers"]), s
+        assert a.health()["shm_bodies"] > 0 and b.health()["shm_bodies"] == 0
+    finally:
+        gw.stop()
+        a.stop()
+        b.stop()
