@@ -131,6 +131,43 @@ int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, 
                                           P<uint16_t>(out), B, Sq, H, D, ldq, ldk, ldv, ldo, scale, S(stream), split));
 }
 
+// geometry JSON: B,H,W,Cin,Ho,Wo,Cout,groups,KH,KW,stride,pad_h,pad_w,dil,act,clip_lo,clip_hi,split
+int die_kern_gconv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint64_t out, uint64_t stream) {
+  try {
+    Json j = Json::parse(geom);
+    kern::GConvArgs a;
+    a.B = geti(j, "B", 1);
+    a.H = geti(j, "H", 1);
+    a.W = geti(j, "W", 1);
+    a.Cin = geti(j, "Cin", 8);
+    a.Ho = geti(j, "Ho", 1);
+    a.Wo = geti(j, "Wo", 1);
+    a.Cout = geti(j, "Cout", 8);
+    a.groups = geti(j, "groups", 1);
+    a.KH = geti(j, "KH", 1);
+    a.KW = geti(j, "KW", 1);
+    a.stride = geti(j, "stride", 1);
+    a.pad_h = geti(j, "pad_h", 0);
+    a.pad_w = geti(j, "pad_w", 0);
+    a.dil = geti(j, "dil", 1);
+    a.act = geti(j, "act", 0);
+    if (auto* v = j.find("clip_lo")) a.clip_lo = static_cast<float>(v->as_double());
+    if (auto* v = j.find("clip_hi")) a.clip_hi = static_cast<float>(v->as_double());
+    a.split = geti(j, "split", 0);
+    a.x = P<const uint16_t>(x);
+    a.w = P<const float>(w);
+    a.bias = P<const float>(bias);
+    a.out = P<uint16_t>(out);
+    return static_cast<int>(kern::grouped_conv(a, S(stream)));
+  } catch (...) {
+    return -1;
+  }
+}
+
+int die_kern_softmax(uint64_t x, uint64_t y, uint64_t yf, long long rows, int C, uint64_t stream, int split) {
+  return static_cast<int>(kern::softmax_rows(P<const uint16_t>(x), P<uint16_t>(y), P<float>(yf), rows, C, S(stream), split));
+}
+
 long long die_decode_scratch_bytes(int max_batch, long long text_cap) {
   return static_cast<long long>(kern::decode_scratch_bytes(max_batch, static_cast<size_t>(text_cap)));
 }
@@ -172,7 +209,7 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
     Json ops = Json::array();
     for (auto& o : p.ops) {
       Json e = Json::object();
-      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention", "stem"};
+      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax"};
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;

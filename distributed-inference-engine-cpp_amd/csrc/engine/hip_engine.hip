@@ -990,7 +990,7 @@ class HipEngine : public Engine {
         case PlanOp::AFFINE:
           e = kern::affine_act(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
                                prm(op.scale_off), prm(op.shift_off), op.act, static_cast<uint16_t*>(buf(op.out)),
-                               op.rows_per_sample * B, op.C, st, live, op.rows_per_sample, sp_);
+                               op.rows_per_sample * B, op.C, st, live, op.rows_per_sample, sp_, op.clip_lo, op.clip_hi);
           break;
         case PlanOp::TO_NCHW_F32:
           e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
@@ -1019,6 +1019,39 @@ class HipEngine : public Engine {
                               static_cast<const uint16_t*>(buf(op.in2)) + op.col[1],
                               static_cast<const uint16_t*>(buf(op.in3)) + op.col[2], static_cast<uint16_t*>(buf(op.out)),
                               B, op.S, op.nh, op.hd, op.ld[0], op.ld[1], op.ld[2], op.C, op.fscale, st, sp_);
+          break;
+        case PlanOp::GCONV: {
+          kern::GConvArgs g;
+          g.x = static_cast<const uint16_t*>(buf(op.in));
+          g.w = prm(op.w_off);
+          g.bias = prm(op.bias_off);
+          g.res = static_cast<const uint16_t*>(buf(op.in2));
+          g.out = static_cast<uint16_t*>(buf(op.out));
+          g.B = B;
+          g.H = op.H;
+          g.W = op.W;
+          g.Cin = op.C;
+          g.Ho = op.Ho;
+          g.Wo = op.Wo;
+          g.Cout = op.Cp;
+          g.groups = op.groups;
+          g.KH = op.kh;
+          g.KW = op.kw;
+          g.stride = op.sh;
+          g.dil = op.sw;
+          g.pad_h = op.ph;
+          g.pad_w = op.pw;
+          g.act = op.act;
+          g.clip_lo = op.clip_lo;
+          g.clip_hi = op.clip_hi;
+          g.split = sp_;
+          g.live = live;
+          e = kern::grouped_conv(g, st);
+          break;
+        }
+        case PlanOp::SOFTMAX:
+          e = kern::softmax_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
+                                 static_cast<float*>(buf(op.out_f32)), op.rows_per_sample * B, op.C, st, sp_);
           break;
         case PlanOp::BF16_TO_F32:
           e = kern::bf16_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
@@ -1061,7 +1094,7 @@ class HipEngine : public Engine {
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
-                                  "layernorm", "tokens", "gather_rows", "attention", "stem"};
+                                  "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax"};
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

@@ -189,7 +189,7 @@ class Planner {
     const Node& n = m_.nodes[idx];
     const std::string& op = n.op_type;
     if (lower_shape_op(idx)) return;
-    if (op == "Conv") return lower_conv(idx);
+    if (op == "Conv") return n.get_int("group", 1) != 1 ? lower_gconv(idx) : lower_conv(idx);
     if (op == "Gemm" || (op == "MatMul" && is_init(n.in(1)))) return lower_gemm(idx);
     if (op == "MatMul") return lower_attn_matmul(idx);
     if (op == "BatchNormalization") return lower_bn(idx);
@@ -200,8 +200,11 @@ class Planner {
     if (op == "Reshape") return lower_reshape(idx);
     if (op == "Flatten" || op == "Squeeze") return lower_flatten(idx);
     if (op == "Transpose") return lower_transpose(idx);
-    if (op == "Div" || op == "Mul") return lower_scale(idx);
+    if (op == "Div" || op == "Mul" || op == "Sub") return lower_scale(idx);
     if (op == "Softmax") return lower_softmax(idx);
+    if (op == "Clip") return lower_clip(idx);
+    if (op == "ReduceMean") return lower_reduce_mean(idx);
+    if (op == "Slice") return lower_slice(idx);
     if (op == "LayerNormalization") return lower_layernorm(idx);
     if (op == "Gather") return lower_gather(idx);
     if (op == "Concat") return lower_concat(idx);
@@ -274,11 +277,11 @@ class Planner {
     } else if (ap == "VALID") {
       pads = {0, 0, 0, 0};
     }
-    if (pads[0] != pads[2] || pads[1] != pads[3])
-      throw std::runtime_error("Conv " + n.name + ": asymmetric padding is not supported");
+    // pads = [top, left, bottom, right]: the kernels offset by top/left and bound-check the input,
+    // so asymmetric padding (TF-style SAME exports) only changes the output size
     const int s = static_cast<int>(st[0]), d = static_cast<int>(dl[0]);
-    const int Ho = (x.H + 2 * static_cast<int>(pads[0]) - d * (KH - 1) - 1) / s + 1;
-    const int Wo = (x.W + 2 * static_cast<int>(pads[1]) - d * (KW - 1) - 1) / s + 1;
+    const int Ho = (x.H + static_cast<int>(pads[0] + pads[2]) - d * (KH - 1) - 1) / s + 1;
+    const int Wo = (x.W + static_cast<int>(pads[1] + pads[3]) - d * (KW - 1) - 1) / s + 1;
     if (Cout % 8) throw std::runtime_error("Conv " + n.name + ": output channels must be a multiple of 8");
 
     // --- fusion lookahead ---
@@ -300,10 +303,15 @@ class Planner {
       cur = m_.nodes[c1].outputs[0];
     }
     int relu = 0, res_buf = -1;
+    float clip_lo = 0.f, clip_hi = 0.f;
     std::string res_name;
     c1 = sole_consumer(cur);
     if (c1 >= 0 && m_.nodes[c1].op_type == "Relu") {
       relu = 1;
+      done_[c1] = true;
+      cur = m_.nodes[c1].outputs[0];
+    } else if (c1 >= 0 && m_.nodes[c1].op_type == "Clip" && clip_bounds(m_.nodes[c1], clip_lo, clip_hi)) {
+      relu = 3;  // Clip epilogue (ReLU6)
       done_[c1] = true;
       cur = m_.nodes[c1].outputs[0];
     } else if (c1 >= 0 && m_.nodes[c1].op_type == "Add") {
@@ -369,8 +377,9 @@ class Planner {
     p.in = in_buf;
     p.in2 = res_buf;
     // ResNet stem (7x7/2, pad 3, 4 stored input channels, 64 outputs, plain epilogue): LDS-patch kernel
-    const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && Cstore == 4 &&
-                      Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 && !graph_outputs_.count(cur);
+    const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && pads[2] == 3 &&
+                      pads[3] == 3 && Cstore == 4 && Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 &&
+                      relu != 3 && !graph_outputs_.count(cur);
     if (stem) {
       p.kind = PlanOp::STEM;
       std::vector<float> ws(64 * 224, 0.f);
@@ -401,6 +410,8 @@ class Planner {
     a.Kpad = Kpad;
     a.relu = relu;
     a.relu2 = relu2;
+    a.clip_lo = clip_lo;
+    a.clip_hi = clip_hi;
     p.flops_per_sample = 2.0 * Ho * Wo * Cout * (KH * KW * Cin);
     p.tile_bmax = kern::choose_tile(max_batch_ * Ho * Wo, Cout, K);
     const size_t out_bytes = static_cast<size_t>(Ho) * Wo * Cout * 2;
@@ -878,13 +889,43 @@ class Planner {
 
   void lower_scale(int idx) {
     const Node& n = m_.nodes[idx];
-    const Val x = val(n.in(0), n);
     auto it = m_.initializers.find(n.in(1));
-    if (x.kind == Val::ATTN && x.stage == 0 && it != m_.initializers.end() && it->second.f.size() == 1) {
-      Val o = x;
-      o.scale = n.op_type == "Div" ? x.scale / it->second.f[0] : x.scale * it->second.f[0];
-      define(n.outputs[0], o);
-      return;
+    if (n.op_type != "Sub" && vid_.count(n.in(0))) {
+      const Val& x = vals_[vid_.at(n.in(0))];
+      if (x.kind == Val::ATTN && x.stage == 0 && it != m_.initializers.end() && it->second.f.size() == 1) {
+        Val o = x;
+        o.scale = n.op_type == "Div" ? x.scale / it->second.f[0] : x.scale * it->second.f[0];
+        define(n.outputs[0], o);
+        return;
+      }
+    }
+    // activation (op) per-channel / scalar constant  ->  affine
+    for (int side = 0; side < 2; ++side) {
+      const std::string& an = n.in(side);
+      const std::string& cn = n.in(1 - side);
+      if (!vid_.count(an) || !is_init(cn)) continue;
+      const Val& x = vals_[vid_.at(an)];
+      const auto& c = m_.initializers.at(cn).f;
+      if (c.size() != 1 && static_cast<int>(c.size()) != x.C) continue;
+      std::vector<float> sc(x.C, 1.f), sh(x.C, 0.f);
+      for (int k = 0; k < x.C; ++k) {
+        const float v = c[c.size() == 1 ? 0 : k];
+        if (n.op_type == "Mul") sc[k] = v;
+        else if (n.op_type == "Div" && side == 0) sc[k] = 1.f / v;
+        else if (n.op_type == "Sub" && side == 0) sh[k] = -v;          // x - c
+        else if (n.op_type == "Sub") { sc[k] = -1.f; sh[k] = v; }      // c - x
+        else throw std::runtime_error(n.op_type + " " + n.name + ": constant / activation is not supported");
+      }
+      return standalone_affine(n, x, &sc, &sh, nullptr);
+    }
+    // Sub of two activations: a - b = (-1) * b + a
+    if (n.op_type == "Sub" && vid_.count(n.in(0)) && vid_.count(n.in(1))) {
+      const Val a = vals_[vid_.at(n.in(0))];
+      const Val b = vals_[vid_.at(n.in(1))];
+      if (a.kind == b.kind && a.C == b.C && a.H == b.H && a.W == b.W && a.pitch() == a.C && b.pitch() == b.C && !a.col && !b.col) {
+        std::vector<float> sc(b.C, -1.f), sh(b.C, 0.f);
+        return standalone_affine(n, b, &sc, &sh, &a);
+      }
     }
     throw std::runtime_error(n.op_type + " " + n.name + ": unsupported elementwise op for the HIP engine");
   }
@@ -899,7 +940,31 @@ class Planner {
       define(n.outputs[0], o);
       return;
     }
-    throw std::runtime_error("Softmax " + n.name + ": only attention-score softmax is supported");
+    const int rank = x.rank ? x.rank : 2;
+    if ((x.kind == Val::ROWS_BF16 || (x.kind == Val::NHWC && x.H * x.W == 1)) && x.pitch() == x.C && !x.col &&
+        (axis == -1 || axis == rank - 1)) {
+      PlanOp p;
+      p.kind = PlanOp::SOFTMAX;
+      p.name = n.name;
+      p.in = x.buf;
+      p.C = x.C;
+      p.rows_per_sample = static_cast<long long>(x.H) * x.W;
+      Val o = x;
+      o.kind = Val::ROWS_BF16;
+      o.rank = rank;
+      if (graph_outputs_.count(n.outputs[0]) && consumers(n.outputs[0]).empty()) {
+        p.out_f32 = kBufGraphOut;  // probabilities straight to the f32 output
+        o.kind = Val::ROWS_F32;
+        o.buf = kBufGraphOut;
+      } else {
+        p.out = new_buf(static_cast<size_t>(p.rows_per_sample) * x.C * 2);
+        o.buf = p.out;
+      }
+      define(n.outputs[0], o);
+      add_op(std::move(p));
+      return;
+    }
+    throw std::runtime_error("Softmax " + n.name + ": only attention scores or the last axis of rows are supported");
   }
 
   void lower_layernorm(int idx) {
@@ -1008,6 +1073,258 @@ class Planner {
     add_op(std::move(p));
   }
 
+  // ---- Clip / grouped conv / decomposed LayerNorm / row softmax / constant binary ops ------------
+  // Clip bounds from attributes (opset < 11) or the optional min/max initializer inputs.
+  bool clip_bounds(const Node& n, float& lo, float& hi) const {
+    lo = -3.4e38f;
+    hi = 3.4e38f;
+    if (n.has("min") || n.has("max")) {
+      lo = n.get_float("min", lo);
+      hi = n.get_float("max", hi);
+      return true;
+    }
+    for (int k = 1; k <= 2; ++k) {
+      if (n.inputs.size() <= static_cast<size_t>(k) || n.in(k).empty()) continue;
+      auto it = m_.initializers.find(n.in(k));
+      if (it == m_.initializers.end() || it->second.f.size() != 1) return false;
+      (k == 1 ? lo : hi) = it->second.f[0];
+    }
+    return true;
+  }
+
+  // Activation consumer of `cur` (Relu / Clip): folds it into the producing op.
+  int take_act(std::string& cur, float& lo, float& hi) {
+    const int c = sole_consumer(cur);
+    if (c < 0) return 0;
+    const Node& a = m_.nodes[c];
+    int act = 0;
+    if (a.op_type == "Relu") act = 1;
+    else if (a.op_type == "Clip" && clip_bounds(a, lo, hi)) act = 3;
+    if (!act) return 0;
+    done_[c] = true;
+    cur = a.outputs[0];
+    return act;
+  }
+
+  // Grouped / depthwise Conv (group > 1): direct NHWC kernel, BN folded, ReLU/Clip epilogue.
+  void lower_gconv(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    if (x.kind != Val::NHWC) throw std::runtime_error("Conv " + n.name + ": grouped conv input must be an image tensor");
+    const auto& wt = init(n.in(1), n);
+    const int G = static_cast<int>(n.get_int("group", 1));
+    const int Cout = static_cast<int>(wt.dims[0]), cpg = static_cast<int>(wt.dims[1]);
+    const int KH = static_cast<int>(wt.dims[2]), KW = static_cast<int>(wt.dims[3]);
+    if (cpg * G != x.C || Cout % G || Cout % 8 || x.C % 8)
+      throw std::runtime_error("Conv " + n.name + ": grouped conv needs Cin = group * Cin/group and channels % 8 == 0");
+    auto st = n.get_ints("strides", {1, 1});
+    auto dl = n.get_ints("dilations", {1, 1});
+    auto pads = n.get_ints("pads", {0, 0, 0, 0});
+    if (st[0] != st[1] || dl[0] != dl[1]) throw std::runtime_error("Conv " + n.name + ": anisotropic stride/dilation");
+    const std::string ap = n.get_string("auto_pad", "NOTSET");
+    if (ap == "SAME_UPPER" || ap == "SAME_LOWER") {
+      for (int d = 0; d < 2; ++d) {
+        const int in = d ? x.W : x.H, k = d ? KW : KH;
+        const int out = (in + static_cast<int>(st[0]) - 1) / static_cast<int>(st[0]);
+        const int total = std::max(0, (out - 1) * static_cast<int>(st[0]) + (k - 1) * static_cast<int>(dl[0]) + 1 - in);
+        const int lo = ap == "SAME_UPPER" ? total / 2 : total - total / 2;
+        pads[d] = lo;
+        pads[d + 2] = total - lo;
+      }
+    } else if (ap == "VALID") {
+      pads = {0, 0, 0, 0};
+    }
+    const int s = static_cast<int>(st[0]), d = static_cast<int>(dl[0]);
+    const int Ho = (x.H + static_cast<int>(pads[0] + pads[2]) - d * (KH - 1) - 1) / s + 1;
+    const int Wo = (x.W + static_cast<int>(pads[1] + pads[3]) - d * (KW - 1) - 1) / s + 1;
+    std::vector<float> scale(Cout, 1.f), shift(Cout, 0.f);
+    if (!n.in(2).empty()) shift = init(n.in(2), n).f;
+    std::string cur = n.outputs[0];
+    int c1 = sole_consumer(cur);
+    if (c1 >= 0 && m_.nodes[c1].op_type == "BatchNormalization") {
+      std::vector<float> sc, sh;
+      bn_affine(m_.nodes[c1], sc, sh);
+      for (int c = 0; c < Cout; ++c) {
+        scale[c] = sc[c];
+        shift[c] = shift[c] * sc[c] + sh[c];
+      }
+      done_[c1] = true;
+      cur = m_.nodes[c1].outputs[0];
+    }
+    PlanOp p;
+    p.kind = PlanOp::GCONV;
+    p.name = n.name;
+    p.in = x.buf;
+    p.act = take_act(cur, p.clip_lo, p.clip_hi);
+    // fp32 weights [Cout][KH][KW][cpg] with the BN scale folded
+    std::vector<float> w(static_cast<size_t>(Cout) * KH * KW * cpg);
+    for (int co = 0; co < Cout; ++co)
+      for (int ci = 0; ci < cpg; ++ci)
+        for (int ky = 0; ky < KH; ++ky)
+          for (int kx = 0; kx < KW; ++kx)
+            w[((static_cast<size_t>(co) * KH + ky) * KW + kx) * cpg + ci] =
+                wt.f[((static_cast<size_t>(co) * cpg + ci) * KH + ky) * KW + kx] * scale[co];
+    p.w_off = push_f32(w);
+    p.bias_off = push_f32(shift);
+    p.groups = G;
+    p.C = x.C;
+    p.H = x.H;
+    p.W = x.W;
+    p.Ho = Ho;
+    p.Wo = Wo;
+    p.Cp = Cout;
+    p.kh = KH;
+    p.kw = KW;
+    p.sh = s;
+    p.sw = d;  // dilation
+    p.ph = static_cast<int>(pads[0]);
+    p.pw = static_cast<int>(pads[1]);
+    p.flops_per_sample = 2.0 * Ho * Wo * Cout * KH * KW * cpg;
+    p.out = new_buf(static_cast<size_t>(Ho) * Wo * Cout * 2);
+    Val o;
+    o.kind = Val::NHWC;
+    o.C = Cout;
+    o.H = Ho;
+    o.W = Wo;
+    o.buf = p.out;
+    define(cur, o);
+    add_op(std::move(p));
+  }
+
+  void lower_clip(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    float lo, hi;
+    if (!clip_bounds(n, lo, hi)) throw std::runtime_error("Clip " + n.name + ": bounds must be constants");
+    standalone_affine(n, x, nullptr, nullptr, nullptr, 3, lo, hi);
+  }
+
+  static int64_t last_axis_of(const Node& n, const onnx::Model& m, bool& ok) {
+    std::vector<int64_t> ax = n.get_ints("axes");
+    if (ax.empty() && n.inputs.size() > 1 && !n.in(1).empty()) {
+      auto it = m.initializers.find(n.in(1));
+      if (it != m.initializers.end()) ax = it->second.i;
+    }
+    ok = ax.size() == 1 && n.get_int("keepdims", 1) == 1;
+    return ok ? ax[0] : 0;
+  }
+
+  // torch's LayerNorm export below opset 17: ReduceMean -> Sub -> Pow(2) -> ReduceMean -> Add(eps)
+  // -> Sqrt -> Div [-> Mul(gamma)] [-> Add(beta)]  ==> one LAYERNORM op.
+  void lower_reduce_mean(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    auto fail = [&](const std::string& why) {
+      throw std::runtime_error("ReduceMean " + n.name + ": only the decomposed LayerNormalization pattern is supported (" +
+                               why + ")");
+    };
+    bool ok;
+    const int64_t axis = last_axis_of(n, m_, ok);
+    const int rank = x.rank ? x.rank : 2;
+    if (!ok || !(axis == -1 || axis == rank - 1)) fail("reduction over the last axis with keepdims");
+    if (x.kind != Val::ROWS_BF16 || x.pitch() != x.C || x.col) fail("input must be dense rows");
+    const std::string& xn = n.in(0);
+    const std::string& mu = n.outputs[0];
+    int sub = -1;
+    for (int c : consumers(mu))
+      if (m_.nodes[c].op_type == "Sub" && m_.nodes[c].in(0) == xn && m_.nodes[c].in(1) == mu) sub = c;
+    if (sub < 0) fail("no x - mean");
+    const std::string& d = m_.nodes[sub].outputs[0];
+    int sq = -1, div = -1;
+    for (int c : consumers(d)) {
+      const Node& q = m_.nodes[c];
+      if ((q.op_type == "Pow" && q.in(0) == d && scalar_is(q.in(1), 2.f)) || (q.op_type == "Mul" && q.in(0) == d && q.in(1) == d))
+        sq = c;
+      else if (q.op_type == "Div" && q.in(0) == d)
+        div = c;
+    }
+    if (sq < 0 || div < 0) fail("no variance / normalisation");
+    const int rm2 = sole_consumer(m_.nodes[sq].outputs[0]);
+    if (rm2 < 0 || m_.nodes[rm2].op_type != "ReduceMean") fail("no variance mean");
+    const int add = sole_consumer(m_.nodes[rm2].outputs[0]);
+    if (add < 0 || m_.nodes[add].op_type != "Add") fail("no variance + eps");
+    const std::string eps_name = other_input(m_.nodes[add], m_.nodes[rm2].outputs[0]);
+    auto ei = m_.initializers.find(eps_name);
+    if (ei == m_.initializers.end() || ei->second.f.size() != 1) fail("eps must be a scalar constant");
+    const int sq_rt = sole_consumer(m_.nodes[add].outputs[0]);
+    if (sq_rt < 0 || m_.nodes[sq_rt].op_type != "Sqrt" || m_.nodes[div].in(1) != m_.nodes[sq_rt].outputs[0])
+      fail("no sqrt feeding the division");
+    std::vector<float> g(x.C, 1.f), b(x.C, 0.f);
+    std::string cur = m_.nodes[div].outputs[0];
+    std::vector<int> used = {sub, sq, rm2, add, sq_rt, div};
+    int c = sole_consumer(cur);
+    if (c >= 0 && m_.nodes[c].op_type == "Mul" && is_init(other_input(m_.nodes[c], cur)) &&
+        static_cast<int>(m_.initializers.at(other_input(m_.nodes[c], cur)).f.size()) == x.C) {
+      g = m_.initializers.at(other_input(m_.nodes[c], cur)).f;
+      used.push_back(c);
+      cur = m_.nodes[c].outputs[0];
+      c = sole_consumer(cur);
+    }
+    if (c >= 0 && m_.nodes[c].op_type == "Add" && is_init(other_input(m_.nodes[c], cur)) &&
+        static_cast<int>(m_.initializers.at(other_input(m_.nodes[c], cur)).f.size()) == x.C) {
+      b = m_.initializers.at(other_input(m_.nodes[c], cur)).f;
+      used.push_back(c);
+      cur = m_.nodes[c].outputs[0];
+    }
+    if (x.C % 8 || x.C > 2048) fail("C % 8 == 0 and C <= 2048");
+    for (int u : used) done_[u] = true;
+    PlanOp p;
+    p.kind = PlanOp::LAYERNORM;
+    p.name = n.name + "+decomposed_layernorm";
+    p.in = x.buf;
+    p.scale_off = push_f32(g);
+    p.shift_off = push_f32(b);
+    p.eps = ei->second.f[0];
+    p.C = x.C;
+    p.rows_per_sample = static_cast<long long>(x.H) * x.W;
+    p.out = new_buf(static_cast<size_t>(x.H) * x.W * x.C * 2);
+    Val o = x;
+    o.buf = p.out;
+    define(cur, o);
+    add_op(std::move(p));
+  }
+
+  // Slice of one token along axis 1 of [B, S, C] rows (e.g. the cls token) -> row gather.
+  void lower_slice(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    std::vector<int64_t> starts = n.get_ints("starts"), ends = n.get_ints("ends"), axes = n.get_ints("axes"), steps;
+    if (starts.empty() && n.inputs.size() >= 3) {  // opset >= 10: inputs
+      ints_of(n.in(1), starts);
+      ints_of(n.in(2), ends);
+      if (n.inputs.size() > 3 && !n.in(3).empty()) ints_of(n.in(3), axes);
+      if (n.inputs.size() > 4 && !n.in(4).empty()) ints_of(n.in(4), steps);
+    }
+    if (axes.empty())
+      for (size_t i = 0; i < starts.size(); ++i) axes.push_back(static_cast<int64_t>(i));
+    const int S = x.H * x.W;
+    if (x.kind == Val::ROWS_BF16 && x.rank == 3 && x.pitch() == x.C && starts.size() == 1 && ends.size() == 1 &&
+        axes.size() == 1 && axes[0] == 1 && (steps.empty() || steps[0] == 1)) {
+      int64_t s0 = starts[0] < 0 ? starts[0] + S : starts[0];
+      int64_t e0 = ends[0] < 0 ? ends[0] + S : std::min<int64_t>(ends[0], S);
+      if (s0 >= 0 && e0 == s0 + 1) {
+        PlanOp p;
+        p.kind = PlanOp::GATHER_ROWS;
+        p.name = n.name;
+        p.in = x.buf;
+        p.S = S;
+        p.gidx = static_cast<int>(s0);
+        p.C = x.C;
+        p.out = new_buf(static_cast<size_t>(x.C) * 2);
+        Val o;
+        o.kind = Val::ROWS_BF16;
+        o.C = x.C;
+        o.H = 1;
+        o.rank = 3;
+        o.buf = p.out;
+        define(n.outputs[0], o);
+        add_op(std::move(p));
+        return;
+      }
+    }
+    throw std::runtime_error("Slice " + n.name + ": only a single token along axis 1 of [B, S, C] rows is supported");
+  }
+
   void lower_bn(int idx) {
     const Node& n = m_.nodes[idx];
     Val& x = val(n.in(0), n);
@@ -1047,6 +1364,15 @@ class Planner {
         return emit_tokens(n, cat, &n.in(1 - side), n.outputs[0]);
       }
     }
+    for (int side = 0; side < 2; ++side) {  // activation + per-channel / scalar constant
+      if (!vid_.count(n.in(side)) || !is_init(n.in(1 - side))) continue;
+      const Val& x = vals_[vid_.at(n.in(side))];
+      const auto& c = m_.initializers.at(n.in(1 - side)).f;
+      if (c.size() != 1 && static_cast<int>(c.size()) != x.C) continue;
+      std::vector<float> sc(x.C, 1.f), sh(x.C);
+      for (int k = 0; k < x.C; ++k) sh[k] = c[c.size() == 1 ? 0 : k];
+      return standalone_affine(n, x, &sc, &sh, nullptr);
+    }
     const Val a = val(n.in(0), n);
     const Val b = val(n.in(1), n);
     if (a.pitch() != a.C || b.pitch() != b.C || a.col || b.col)
@@ -1057,21 +1383,18 @@ class Planner {
   }
 
   void standalone_affine(const Node& n, const Val& x, const std::vector<float>* sc, const std::vector<float>* sh,
-                         const Val* z) {
+                         const Val* z, int own_act = 0, float own_lo = 0.f, float own_hi = 0.f) {
     if (x.kind != Val::NHWC && x.kind != Val::ROWS_BF16)
       throw std::runtime_error(n.op_type + " " + n.name + ": unsupported input layout");
     if (x.C % 8) throw std::runtime_error(n.op_type + " " + n.name + ": channels must be a multiple of 8");
+    if (x.pitch() != x.C || x.col) throw std::runtime_error(n.op_type + " " + n.name + ": strided operand");
     std::string cur = n.outputs[0];
-    int act = n.op_type == "Relu" ? 1 : 0;
-    if (!act) {
-      const int c1 = sole_consumer(cur);
-      if (c1 >= 0 && m_.nodes[c1].op_type == "Relu") {
-        act = 1;
-        done_[c1] = true;
-        cur = m_.nodes[c1].outputs[0];
-      }
-    }
+    int act = n.op_type == "Relu" ? 1 : own_act;
+    float lo = own_lo, hi = own_hi;
+    if (!act) act = take_act(cur, lo, hi);
     PlanOp p;
+    p.clip_lo = lo;
+    p.clip_hi = hi;
     p.kind = PlanOp::AFFINE;
     p.name = n.name;
     p.in = x.buf;
@@ -1098,10 +1421,12 @@ class Planner {
     auto k = n.get_ints("kernel_shape");
     auto st = n.get_ints("strides", {1, 1});
     auto pads = n.get_ints("pads", {0, 0, 0, 0});
-    if (pads[0] != pads[2] || pads[1] != pads[3]) throw std::runtime_error(n.op_type + ": asymmetric pads");
+    const bool cip_avg = n.op_type == "AveragePool" && n.get_int("count_include_pad", 0);
+    if ((pads[0] != pads[2] || pads[1] != pads[3]) && cip_avg)
+      throw std::runtime_error(n.op_type + " " + n.name + ": count_include_pad with asymmetric pads is not supported");
     const bool ceil_mode = n.get_int("ceil_mode", 0) != 0;
     auto od = [&](int in, int d) {
-      double v = static_cast<double>(in + 2 * pads[d] - k[d]) / st[d];
+      double v = static_cast<double>(in + pads[d] + pads[d + 2] - k[d]) / st[d];
       return static_cast<int>(ceil_mode ? std::ceil(v) : std::floor(v)) + 1;
     };
     PlanOp p;

@@ -38,7 +38,7 @@ struct PlanBuf {
 struct PlanOp {
   enum Kind {
     INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32,
-    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION, STEM
+    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION, STEM, GCONV, SOFTMAX
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
@@ -52,6 +52,8 @@ struct PlanOp {
   // generic geometry
   int C = 0, H = 0, W = 0, Ho = 0, Wo = 0, Cp = 0;
   int kh = 0, kw = 0, sh = 1, sw = 1, ph = 0, pw = 0, is_max = 0, cip = 0, act = 0;
+  int groups = 1;                      // GCONV
+  float clip_lo = 0.f, clip_hi = 0.f;  // act == 3 (Clip) of AFFINE / GCONV
   long long rows_per_sample = 0;  // AFFINE / LAYERNORM: rows of C per sample
   // transformer ops: sequence length, heads, head dim, column offsets / pitches of in/in2/in3
   int S = 0, nh = 0, hd = 0, gidx = 0;

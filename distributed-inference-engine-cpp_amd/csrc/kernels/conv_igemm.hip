@@ -34,8 +34,9 @@ constexpr int BK = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
-// Epilogue activation: 1 = ReLU, 2 = exact (erf) GELU.
-__device__ __forceinline__ float act_fn(float v, int act) {
+// Epilogue activation: 1 = ReLU, 2 = exact (erf) GELU, 3 = Clip(lo, hi).
+__device__ __forceinline__ float act_fn(float v, int act, float lo = 0.f, float hi = 0.f) {
+  if (act == 3) return fminf(fmaxf(v, lo), hi);
   return act == 1 ? fmaxf(v, 0.f) : 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
 }
 
@@ -59,7 +60,7 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   }
   if (p.relu) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu);
+    for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu, p.clip_lo, p.clip_hi);
   }
   if (p.out) store8v(p.out + o, p.oplane, split, v);
   if (p.out_f32) {
@@ -382,7 +383,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         const size_t o = static_cast<size_t>(m) * p.N + n + r;
         float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
         if (p.res) v += load1v(p.res + o, p.oplane, p.split);
-        if (p.relu) v = act_fn(v, p.relu);
+        if (p.relu) v = act_fn(v, p.relu, p.clip_lo, p.clip_hi);
         if (p.out) store1v(p.out + o, p.oplane, p.split, v);
         if (p.out_f32) p.out_f32[o] = v;
         if (p.out2) {

@@ -52,6 +52,8 @@ struct ConvArgs {
   const float* in_scale = nullptr;
   const float* in_shift = nullptr;
   int in_relu = 0;
+  // relu == 3: Clip(clip_lo, clip_hi) (ReLU6 = Clip(0, 6)) instead of ReLU / GELU
+  float clip_lo = 0.f, clip_hi = 0.f;
   // fp32 mode (common.h "split" tensors): x, res, out and out2 are split (hi, lo) bf16 planes and w
   // holds the weights' hi plane followed by their lo plane `wplane` elements later.  The planes of
   // the activations follow from the shapes (x: B*H*W*Cin, res/out/out2: M*N; the launcher fills
@@ -95,10 +97,33 @@ hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, in
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
                           int relu, int B, int HW, int C, hipStream_t s, const long long* live = nullptr,
                           int split = 0);
-// Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional)
+// Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional;
+// act 1 = ReLU, 3 = Clip(clip_lo, clip_hi))
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
                       uint16_t* y, long long M, int C, hipStream_t s, const long long* live = nullptr,
-                      long long rows_per_sample = 0, int split = 0);
+                      long long rows_per_sample = 0, int split = 0, float clip_lo = 0.f, float clip_hi = 0.f);
+
+// Grouped / depthwise convolution, NHWC, fp32 weights [Cout][KH][KW][Cin/groups] (gconv.hip).
+struct GConvArgs {
+  const uint16_t* x = nullptr;
+  const float* w = nullptr;
+  const float* bias = nullptr;
+  const uint16_t* res = nullptr;  // added after the activation (inverted-residual blocks)
+  uint16_t* out = nullptr;
+  float* out_f32 = nullptr;
+  int B = 1, H = 1, W = 1, Cin = 1, Ho = 1, Wo = 1, Cout = 8, groups = 1;
+  int KH = 1, KW = 1, stride = 1, pad_h = 0, pad_w = 0, dil = 1;
+  int act = 0;  // 0 none, 1 ReLU, 3 Clip(clip_lo, clip_hi)
+  float clip_lo = 0.f, clip_hi = 0.f;
+  int split = 0;
+  const long long* live = nullptr;
+};
+hipError_t grouped_conv(const GConvArgs& a, hipStream_t s);
+
+// Softmax over the last axis of [rows][C] (one wave per row, fp32 math); writes bf16/split `y`
+// and/or f32 `y_f32`.
+hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long rows, int C, hipStream_t s,
+                        int split = 0);
 // bf16 NHWC [B,H,W,C] -> f32 NCHW [B,C,H,W]
 hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s, int split = 0);
 // f32 -> bf16 / bf16 -> f32 copies

@@ -171,7 +171,7 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
 __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ z,
                                   const float* __restrict__ scale, const float* __restrict__ shift, int act,
                                   uint16_t* __restrict__ y, long long M, int C, const long long* __restrict__ live,
-                                  long long rows_per_sample, int split) {
+                                  long long rows_per_sample, int split, float clip_lo, float clip_hi) {
   const long long plane = M * C;
   if (live) M = min(M, *live * rows_per_sample);
   const int CG = C / 8;
@@ -194,6 +194,9 @@ __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t
     if (act == 1) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], 0.f);
+    } else if (act == 3) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = fminf(fmaxf(v[t], clip_lo), clip_hi);
     }
     store8v(y + i * 8, plane, split != 0, v);
   }
@@ -259,11 +262,11 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
 
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,
                       uint16_t* y, long long M, int C, hipStream_t s, const long long* live, long long rows_per_sample,
-                      int split) {
+                      int split, float clip_lo, float clip_hi) {
   if (C % 8) return hipErrorInvalidValue;
   if (live && rows_per_sample <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(M * (C / 8))), dim3(256), 0, s, x, z, scale, shift, act, y, M,
-                     C, live, rows_per_sample, split);
+                     C, live, rows_per_sample, split, clip_lo, clip_hi);
   return hipGetLastError();
 }
 

@@ -282,6 +282,31 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
   }
 }
 
+// Softmax over rows (one wave per row, fp32 max / sum with exp2): classifier heads and any softmax
+// outside the fused attention.
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                           float* __restrict__ yf, long long rows, int C, int split) {
+  const int lane = threadIdx.x & 63;
+  const long long row = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long plane = rows * C;
+  const uint16_t* xr = x + row * C;
+  const bool sp = split != 0;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, load1v(xr + c, plane, sp));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  constexpr float kLog2e = 1.4426950408889634f;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += exp2f((load1v(xr + c, plane, sp) - m) * kLog2e);
+  const float inv = 1.f / wave_sum(s);
+  for (int c = lane; c < C; c += 64) {
+    const float p = exp2f((load1v(xr + c, plane, sp) - m) * kLog2e) * inv;
+    if (y) store1v(y + row * C + c, plane, sp, p);
+    if (yf) yf[row * C + c] = p;
+  }
+}
+
 inline int grid_for(long long work, int cap = 4096) {
   long long g = (work + 255) / 256;
   if (g < 1) g = 1;
@@ -313,6 +338,14 @@ hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, in
   if (C % 8 || idx < 0 || idx >= S) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(static_cast<long long>(B) * (C / 8))), dim3(256), 0, s, x, y, B,
                      S, idx, C, split);
+  return hipGetLastError();
+}
+
+hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long rows, int C, hipStream_t s,
+                        int split) {
+  if (C <= 0 || rows <= 0 || (!y && !y_f32)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(static_cast<unsigned>((rows + 3) / 4)), dim3(256), 0, s, x, y, y_f32,
+                     rows, C, split);
   return hipGetLastError();
 }
 

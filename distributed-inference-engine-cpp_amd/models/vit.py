@@ -10,6 +10,11 @@ Graph layout follows a HuggingFace `ViTForImageClassification` export at opset 1
   -> LayerNormalization -> Gather(token 0) -> Gemm (classifier).
 The batch dimension is dynamic (the cls-token Expand takes its shape from Shape(input)).  Weights
 are random (no checkpoint offline); `torch_forward` is the fp32 oracle for both executors.
+
+Export variants (op coverage of the HIP engine): `decomposed_ln` writes every LayerNormalization the
+way torch exports it below opset 17 (ReduceMean, Sub, Pow, ReduceMean, Add, Sqrt, Div, Mul, Add),
+`cls_slice` selects the cls token with Slice + Reshape instead of Gather, `softmax_head` appends a
+Softmax to the logits.
 """
 from __future__ import annotations
 
@@ -34,6 +39,9 @@ class ViTConfig:
     num_classes: int = 1000
     eps: float = 1e-12
     seed: int = 0
+    decomposed_ln: bool = False
+    cls_slice: bool = False
+    softmax_head: bool = False
 
 
 def tiny_vit_config(seed: int = 0) -> ViTConfig:
@@ -101,10 +109,25 @@ def build_onnx(cfg: ViTConfig = ViTConfig(), opset: int = 17) -> Tuple[bytes, Di
         y = g.node("MatMul", [inp, name + ".weight"], name=name + "/MatMul")
         return g.node("Add", [y, name + ".bias"], name=name + "/Add")
 
+    two = g.const(np.array(2.0, np.float32), "two")
+    eps_c = g.const(np.array(cfg.eps, np.float32), "ln_eps")
+
+    def layer_norm(inp, wname, name):
+        if not cfg.decomposed_ln:
+            return g.node("LayerNormalization", [inp, wname + ".weight", wname + ".bias"], name=name, axis=-1,
+                          epsilon=cfg.eps)
+        mu = g.node("ReduceMean", [inp], name=name + "/mean", axes=[-1], keepdims=1)
+        d = g.node("Sub", [inp, mu], name=name + "/sub")
+        var = g.node("ReduceMean", [g.node("Pow", [d, two], name=name + "/pow")], name=name + "/var", axes=[-1],
+                     keepdims=1)
+        sd = g.node("Sqrt", [g.node("Add", [var, eps_c], name=name + "/add_eps")], name=name + "/sqrt")
+        y = g.node("Div", [d, sd], name=name + "/div")
+        y = g.node("Mul", [y, wname + ".weight"], name=name + "/scale")
+        return g.node("Add", [y, wname + ".bias"], name=name + "/shift")
+
     for i in range(cfg.depth):
         p = "encoder.layer.%d." % i
-        a = g.node("LayerNormalization", [h, p + "layernorm_before.weight", p + "layernorm_before.bias"],
-                   name=p + "layernorm_before", axis=-1, epsilon=cfg.eps)
+        a = layer_norm(h, p + "layernorm_before", p + "layernorm_before")
         q = linear(a, p + "attention.query")
         k = linear(a, p + "attention.key")
         v = linear(a, p + "attention.value")
@@ -122,8 +145,7 @@ def build_onnx(cfg: ViTConfig = ViTConfig(), opset: int = 17) -> Tuple[bytes, Di
         c = g.node("Reshape", [c, merge_shape], name=p + "ctx_merge")
         o = linear(c, p + "attention.output")
         h = g.node("Add", [o, h], name=p + "residual1")
-        a = g.node("LayerNormalization", [h, p + "layernorm_after.weight", p + "layernorm_after.bias"],
-                   name=p + "layernorm_after", axis=-1, epsilon=cfg.eps)
+        a = layer_norm(h, p + "layernorm_after", p + "layernorm_after")
         m = linear(a, p + "intermediate")
         t = g.node("Div", [m, sqrt2], name=p + "gelu/div")
         t = g.node("Erf", [t], name=p + "gelu/erf")
@@ -132,10 +154,16 @@ def build_onnx(cfg: ViTConfig = ViTConfig(), opset: int = 17) -> Tuple[bytes, Di
         t = g.node("Mul", [t, half], name=p + "gelu/half")
         o = linear(t, p + "output")
         h = g.node("Add", [o, h], name=p + "residual2")
-    h = g.node("LayerNormalization", [h, "layernorm.weight", "layernorm.bias"], name="layernorm", axis=-1,
-               epsilon=cfg.eps)
-    h = g.node("Gather", [h, g.const(np.array(0, np.int64), "cls_index")], name="cls_select", axis=1)
+    h = layer_norm(h, "layernorm", "layernorm")
+    if cfg.cls_slice:
+        h = g.node("Slice", [h, g.const(np.array([0], np.int64), "s0"), g.const(np.array([1], np.int64), "s1"),
+                             g.const(np.array([1], np.int64), "s_axis")], name="cls_slice")
+        h = g.node("Reshape", [h, g.const(np.array([0, D], np.int64), "cls_shape2")], name="cls_flat")
+    else:
+        h = g.node("Gather", [h, g.const(np.array(0, np.int64), "cls_index")], name="cls_select", axis=1)
     y = g.node("Gemm", [h, "classifier.weight", "classifier.bias"], name="logits", transB=1)
+    if cfg.softmax_head:
+        y = g.node("Softmax", [y], name="prob", axis=-1)
     g.output(y, ["batch", cfg.num_classes])
     return g.model_proto(opset=opset, ir_version=8), w
 
@@ -173,7 +201,8 @@ def torch_forward(w, x, cfg: ViTConfig = ViTConfig(), device="cpu"):
         m = 0.5 * m * (1.0 + torch.erf(m / 1.4142135381698608))
         h = lin(m, p + "output") + h
     h = F.layer_norm(h, (D,), t["layernorm.weight"], t["layernorm.bias"], cfg.eps)
-    return F.linear(h[:, 0], t["classifier.weight"], t["classifier.bias"])
+    y = F.linear(h[:, 0], t["classifier.weight"], t["classifier.bias"])
+    return torch.softmax(y, -1) if cfg.softmax_head else y
 
 
 def synthetic_input(batch: int, cfg: ViTConfig = ViTConfig(), seed: int = 1) -> np.ndarray:

@@ -562,6 +562,10 @@ def _sig_kernels():
     L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64, i]
     L.die_kern_stem.restype = i
     L.die_kern_stem.argtypes = [u64] * 4 + [i] * 6 + [u64, i]
+    L.die_kern_gconv.restype = i
+    L.die_kern_gconv.argtypes = [C.c_char_p] + [u64] * 5
+    L.die_kern_softmax.restype = i
+    L.die_kern_softmax.argtypes = [u64, u64, u64, C.c_longlong, i, u64, i]
     L.die_kern_layernorm.restype = i
     L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64, i]
     L.die_kern_tokens.restype = i

@@ -369,3 +369,40 @@ def conv_stem7x7(x_nhwc4, w, bias, relu=True, split=False):
                                         B, H, W, Ho, Wo, int(relu), _stream(), int(split))
     _check(rc, "conv_stem7x7")
     return _out(out, split)
+
+
+# ---- grouped conv / row softmax (csrc/kernels/gconv.hip, transformer.hip) ---------------------------
+
+def grouped_conv(x_nhwc, w, bias=None, stride=1, pads=(0, 0, 0, 0), groups=1, clip=None, relu=False, split=False):
+    """x [B,H,W,Cin] (bf16, or any float dtype with split), w [Cout, Cin/groups, k, k] float,
+    pads [top, left, bottom, right] -> [B,Ho,Wo,Cout] (fp32 values of the split planes when split)."""
+    import torch
+
+    B, H, W, Cin = x_nhwc.shape
+    Cout, cpg, KH, KW = w.shape
+    Ho = (H + pads[0] + pads[2] - KH) // stride + 1
+    Wo = (W + pads[1] + pads[3] - KW) // stride + 1
+    xin = _in(x_nhwc, split)
+    wp = w.float().permute(0, 2, 3, 1).contiguous()
+    bp = None if bias is None else bias.float().contiguous()
+    out = torch.empty(((2,) if split else ()) + (B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x_nhwc.device)
+    act = 3 if clip is not None else (1 if relu else 0)
+    lo, hi = clip if clip is not None else (0.0, 0.0)
+    geom = dict(B=B, H=H, W=W, Cin=Cin, Ho=Ho, Wo=Wo, Cout=Cout, groups=groups, KH=KH, KW=KW, stride=stride,
+                pad_h=pads[0], pad_w=pads[1], act=act, clip_lo=float(lo), clip_hi=float(hi), split=int(split))
+    rc = native.kernels().die_kern_gconv(json.dumps(geom).encode(), _ptr(xin), _ptr(wp), _ptr(bp), _ptr(out), _stream())
+    _check(rc, "grouped_conv")
+    return _out(out, split)
+
+
+def softmax_rows(x, split=False):
+    """x [rows, C] float -> (softmax stored bf16/split -> fp32 values, softmax fp32)."""
+    import torch
+
+    rows, C = x.shape
+    xin = _in(x, split) if split else x.to(torch.bfloat16).contiguous()
+    y = torch.empty(((2,) if split else ()) + (rows, C), dtype=torch.bfloat16, device=x.device)
+    yf = torch.empty((rows, C), dtype=torch.float32, device=x.device)
+    rc = native.kernels().die_kern_softmax(_ptr(xin), _ptr(y), _ptr(yf), rows, C, _stream(), int(split))
+    _check(rc, "softmax_rows")
+    return (join_planes(y) if split else y.float()), yf

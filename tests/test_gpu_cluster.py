@@ -25,7 +25,8 @@ def hip_cluster(models, tmp_path_factory):
 
     path = models["get_rn50"]()[0]
     logs = tmp_path_factory.mktemp("gpu_cluster_logs")
-    c = fault_inject.Cluster(path, n_workers=3, device="hip", breaker_timeout_s=1.0, read_timeout_ms=5000,
+    # read timeout 2 s: a hung (SIGSTOPped) worker must fail requests well inside the drill window
+    c = fault_inject.Cluster(path, n_workers=3, device="hip", breaker_timeout_s=1.0, read_timeout_ms=2000,
                              log_dir=str(logs), stagger=True)
     yield c
     c.close()
@@ -51,8 +52,8 @@ def test_fault_drill_hip_workers(hip_cluster, fault):
     import fault_inject
 
     before = hip_cluster.breaker(0)
-    rep = fault_inject.drill(hip_cluster, fault, target=0, down_s=3.0, requests=24000, connections=24,
-                             input_numel=NUMEL)
+    rep = fault_inject.drill(hip_cluster, fault, target=0, down_s=4.0 if fault == "hang" else 3.0, requests=24000,
+                             connections=24, input_numel=NUMEL)
     print("CONFIG3_DRILL " + json.dumps({k: rep[k] for k in ("fault", "timeline", "heal_to_closed_s", "client",
                                                                 "gateway")}))
     client = rep["client"]
