@@ -225,44 +225,52 @@ def main():
             gw.stop()
         wk.stop()
     elif args.mode == "dp":
-        # BASELINE config 4: ONE worker whose batches (B per GPU x N GPUs) are sharded over all ranks;
-        # rank 0 serves HTTP and drives the load, ranks >= 1 are DP followers on their own GPU.
+        # BASELINE config 4: ONE data-parallel worker over all ranks.  Every rank serves HTTP on the
+        # same port (SO_REUSEPORT) and parses its own connections' requests; the leader merges the
+        # ranks' queued sub-batches into DP batches sharded over the GPUs (RCCL all-gather of logits),
+        # and every rank answers its own requests.  Each rank drives its own 50-connection client.
         group = "die_bench_dp_%s" % os.environ.get("MASTER_PORT", str(os.getpid()))
         Btot = B * world
-        eng_opts = {"device": args.device, "device_id": dev, "pipeline_depth": args.pipeline_depth,
-                    "precision": args.precision, "device_decode": not args.no_device_decode, "dp_world": world,
-                    "dp_group": group}
-        res, fol = {"ok": 0, "failed": 0}, None
+        port = 0
         if rank == 0:
-            wk = native.Worker(model, node_id="dp", max_batch=Btot, engine=eng_opts)
-            lg = dict(port=wk.port, connections=args.connections * world, payload="full", input_numel=numel,
-                      decimals=4, seed=1000, timeout_ms=60000)
-            native.loadgen(requests=args.warmup * SR * world, warmup=0, id_prefix="warm_", **lg)
-            h0 = wk.health()
-        else:
-            eng_opts.pop("dp_group")
-            eng_opts.pop("dp_world")
-            fol = native.DpFollower(model, group, rank, world, max_batch=Btot, **eng_opts)
+            import socket
+
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+            sk.close()
+        if dist is not None:
+            obj = [port]
+            dist.broadcast_object_list(obj, src=0)
+            port = obj[0]
+        eng_opts = dict(engine_opts, dp_world=world, dp_group=group, dp_rank=rank)
+        wk = native.Worker(model, node_id="dp-r%d" % rank, port=port, reuse_port=True, max_batch=Btot,
+                           engine=eng_opts)
+        lg = dict(port=port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
+                  seed=1000 + rank, timeout_ms=60000)
+        native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, **lg)
+        h0 = wk.health()
         barrier()
         t0 = time.perf_counter()
-        if rank == 0:
-            res = native.loadgen(requests=args.steps * SR * world, warmup=0, id_prefix="r_", **lg)
+        res = native.loadgen(requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, **lg)
         barrier()
         elapsed = time.perf_counter() - t0
         ok, failed = res["ok"], res["failed"]
-        if rank == 0:
-            h1 = wk.health()
-            bp0, bp1 = h0["batch_processor"], h1["batch_processor"]
-            nb = bp1["total_batches"] - bp0["total_batches"]
-            extra = {"p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
-                     "mean_ms": res["latency_ms"]["mean"], "failed": failed,
-                     "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
-                     "engine": h1["engine"].get("device"), "dp_backend": h1["engine"].get("dp_backend"),
-                     "device_ms_per_batch": h1["engine"].get("avg_device_ms"),
-                     "client_connections": args.connections * world}
-            wk.stop()  # stops the DP group: followers return
-        else:
-            fol.join()
+        h1 = wk.health()
+        e1 = h1["engine"]
+        extra = {"p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
+                 "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+                 "engine": e1.get("device"), "dp_backend": e1.get("dp_backend"), "precision": e1.get("precision"),
+                 "device_ms_per_batch": e1.get("avg_device_ms"),
+                 "dp_batches_rank0": e1.get("dp_batches", 0) - h0["engine"].get("dp_batches", 0),
+                 "requests_parsed_this_rank": h1["total_requests"] - h0["total_requests"],
+                 "client_connections_per_gpu": args.connections}
+        barrier()  # every rank done with traffic before the leader stops the group
+        if rank != 0:
+            barrier()
+        wk.stop()
+        if rank == 0 and dist is not None:
+            barrier()
     else:
         import numpy as np
 

@@ -48,6 +48,7 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
   eo.dp_group = f.str("dp-group", "");
   eo.dp_rank = static_cast<int>(f.i("dp-rank", 1));
   eo.dp_world = static_cast<int>(f.i("dp-world", 2));
+  eo.precision = f.str("precision", "fp32");
   std::atomic<bool> stop{false};
   std::thread sig_thread([&] {
     int sig = 0;
@@ -71,7 +72,8 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower", "no-shm"});
+  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower", "no-shm",
+                            "reuse-port", "dp-no-ingest", "no-pace", "no-pack-text", "branch-streams"});
   const auto& pos = f.positional();
   if (f.b("dp-follower")) {
     sigset_t fs;
@@ -90,7 +92,8 @@ int main(int argc, char** argv) {
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --http-threads N  --host ADDR (0.0.0.0)\n"
-              << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch)\n"
+              << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
+              << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose\n"
               << "  --log-level trace|debug|info|warn|error|off (info; env DIE_LOG_LEVEL)" << std::endl;
     return 1;
@@ -141,6 +144,12 @@ int main(int argc, char** argv) {
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));
   o.verbose = f.b("verbose");
   o.accept_shm = !f.b("no-shm");
+  o.reuse_port = f.b("reuse-port");
+  if (f.i("dp-rank", 0) > 0) {  // an ingesting rank of a data-parallel worker (spawned by rank 0)
+    o.engine.dp_rank = static_cast<int>(f.i("dp-rank", 0));
+    o.engine.dp_world = static_cast<int>(f.i("dp-world", 2));
+    o.engine.dp_group = f.str("dp-group", "");
+  }
   if (o.verbose) die::set_log_level(die::LogLevel::DEBUG);
   die::LogLevel lv;
   if (die::parse_log_level(f.str("log-level", ""), &lv)) die::set_log_level(lv);
@@ -153,12 +162,23 @@ int main(int argc, char** argv) {
     o.engine.dp_group = "die_dp_" + std::to_string(getpid());
     o.engine.device_id = devices[0];
     if (o.engine.device == "auto") o.engine.device = "hip";
+    // ingest on every rank: all ranks listen on the same port (needs a fixed port)
+    const bool ingest = !f.b("dp-no-ingest") && o.port > 0;
+    o.reuse_port = o.reuse_port || ingest;
     for (size_t r = 1; r < devices.size(); ++r) {
-      std::vector<std::string> args = {argv[0], "--dp-follower", o.model_path, "--dp-group", o.engine.dp_group,
-                                        "--dp-rank", std::to_string(r), "--dp-world", std::to_string(devices.size()),
-                                        "--device-id", std::to_string(devices[r]), "--device", o.engine.device,
-                                        "--max-batch", std::to_string(o.max_batch), "--pipeline-depth",
-                                        std::to_string(o.engine.pipeline_depth)};
+      std::vector<std::string> args;
+      if (ingest) {
+        args = {argv[0], std::to_string(o.port), o.node_id + "-r" + std::to_string(r), o.model_path, "--reuse-port",
+                "--host", o.host, "--precision", o.engine.precision};
+      } else {
+        args = {argv[0], "--dp-follower", o.model_path};
+      }
+      for (const std::string& a : {std::string("--dp-group"), o.engine.dp_group, std::string("--dp-rank"),
+                                   std::to_string(r), std::string("--dp-world"), std::to_string(devices.size()),
+                                   std::string("--device-id"), std::to_string(devices[r]), std::string("--device"),
+                                   o.engine.device, std::string("--max-batch"), std::to_string(o.max_batch),
+                                   std::string("--pipeline-depth"), std::to_string(o.engine.pipeline_depth)})
+        args.push_back(a);
       if (!o.engine.use_graphs) args.push_back("--no-graphs");
       if (!o.engine.device_decode) args.push_back("--no-device-decode");
       std::vector<char*> av;

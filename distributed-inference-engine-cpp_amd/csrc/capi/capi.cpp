@@ -452,6 +452,7 @@ void* die_worker_create(const char* opts_json, char** err) {
     o.fault_fail_rate = jget<double>(j, "fault_fail_rate", 0.0);
     o.fault_latency_ms = jget<int>(j, "fault_latency_ms", 0);
     o.accept_shm = jget<bool>(j, "accept_shm", true);
+    o.reuse_port = jget<bool>(j, "reuse_port", false);
     auto* w = new WorkerNode(o);
     if (w->start() < 0) {
       delete w;

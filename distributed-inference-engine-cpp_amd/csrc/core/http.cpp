@@ -215,11 +215,12 @@ void HttpServer::route(const std::string& method, const std::string& path, Handl
   routes_.push_back({{method, path}, std::move(h)});
 }
 
-int HttpServer::start(const std::string& host, int port, int threads) {
+int HttpServer::start(const std::string& host, int port, int threads, bool reuse_port) {
   listen_fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (listen_fd_ < 0) return -1;
   int one = 1;
   setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (reuse_port) setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
   sockaddr_in addr{};
   addr.sin_family = AF_INET;
   addr.sin_port = htons(static_cast<uint16_t>(port));

@@ -101,7 +101,9 @@ class HttpServer {
   }
   // Bind and start `threads` reactor threads (0 = hardware concurrency, capped at 32).
   // port 0 picks an ephemeral port; returns the bound port, or -1 on failure.
-  int start(const std::string& host, int port, int threads = 0);
+  // reuse_port: SO_REUSEPORT, so several processes (the ranks of a data-parallel worker) can listen
+  // on the same port and the kernel spreads incoming connections over them.
+  int start(const std::string& host, int port, int threads = 0, bool reuse_port = false);
   // Block until stop() is called.
   void wait();
   void stop();

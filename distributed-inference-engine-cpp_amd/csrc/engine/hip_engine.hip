@@ -538,7 +538,7 @@ class HipEngine : public Engine {
         comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
         comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, cs);
         HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
-        if (comm_->rank() == 0) {
+        {  // every rank answers the sub-batches it ingested: all rows come back to every host
           HIP_CHECK(hipMemcpyAsync(sl.h_gather, sl.d_gather, sizeof(float) * out_numel_ * B * dp_world_,
                                    hipMemcpyDeviceToHost, cs));
           HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
@@ -546,8 +546,6 @@ class HipEngine : public Engine {
           d2h_bytes_.fetch_add(static_cast<long long>((sizeof(float) * out_numel_ * B + sizeof(int) * 2 * max_batch_) *
                                                       dp_world_),
                                std::memory_order_relaxed);
-          HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
-        } else {
           HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
         }
         job.has_text = text_cap_ > 0;
@@ -1259,8 +1257,8 @@ class HipEngine : public Engine {
           }
           if (comm_) {
             r.gathered = dp_world_;
-            r.outputs = comm_->rank() == 0 ? sl.h_gather : nullptr;
-            r.status = comm_->rank() == 0 && job.has_text ? sl.h_gstatus : nullptr;
+            r.outputs = sl.h_gather;
+            r.status = job.has_text ? sl.h_gstatus : nullptr;
             r.ntok = r.status ? sl.h_gstatus + max_batch_ : nullptr;
             r.status_stride = 2 * max_batch_;
           }

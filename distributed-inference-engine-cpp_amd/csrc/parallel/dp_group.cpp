@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <climits>
+#include <cstdint>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -50,6 +51,13 @@ struct DpGroup::Control {
   std::atomic<uint32_t> done_seq[kDpMaxRanks];
   std::atomic<uint32_t> done_any;
   std::atomic<uint32_t> bar_count, bar_gen;
+  std::atomic<int32_t> port;
+  std::atomic<uint64_t> gseq;
+  std::atomic<uint32_t> subs_posted, subs_taken;
+  struct SubRing {
+    std::atomic<uint32_t> head, tail;  // head: next slot to fill (producer), tail: next to take (leader)
+    DpSub slots[kDpSubRing];
+  } subq[kDpMaxRanks];
   DpBatch ring[kDpRing];
 };
 
@@ -100,6 +108,14 @@ std::unique_ptr<DpGroup> DpGroup::create(const std::string& name, int world, siz
   c->done_any = 0;
   c->bar_count = 0;
   c->bar_gen = 0;
+  c->port = 0;
+  c->gseq = 0;
+  c->subs_posted = 0;
+  c->subs_taken = 0;
+  for (auto& q : c->subq) {
+    q.head = 0;
+    q.tail = 0;
+  }
   g->arena_ = g->base_ + c->arena_off;
   g->arena_bytes_ = arena_bytes;
   g->gather_ = g->base_ + c->gather_off;
@@ -208,6 +224,8 @@ uint64_t DpGroup::post(const DpBatch& b) {
   slot.seq = seq;
   slot.B = b.B;
   slot.per = b.per;
+  slot.nsub = b.nsub;
+  std::memcpy(slot.subs, b.subs, sizeof(DpSubRef) * static_cast<size_t>(b.nsub));
   std::memcpy(slot.items, b.items, sizeof(DpItem) * static_cast<size_t>(b.B));
   ctl_->head.store(seq, std::memory_order_release);
   futex_wake(&ctl_->head);
@@ -225,6 +243,8 @@ bool DpGroup::next(uint64_t seq, DpBatch& out, const std::atomic<bool>* ext_stop
   out.seq = slot.seq;
   out.B = slot.B;
   out.per = slot.per;
+  out.nsub = slot.nsub;
+  std::memcpy(out.subs, slot.subs, sizeof(DpSubRef) * static_cast<size_t>(slot.nsub));
   std::memcpy(out.items, slot.items, sizeof(DpItem) * static_cast<size_t>(slot.B));
   return true;
 }
@@ -235,12 +255,103 @@ void DpGroup::done(uint64_t seq) {
   futex_wake(&ctl_->done_any);
 }
 
+bool DpGroup::push_sub(const DpSub& s) {
+  if (s.n < 0 || s.n > kDpSubMax) throw std::runtime_error("dp sub-batch too large");
+  auto& q = ctl_->subq[rank_];
+  while (true) {  // single producer per rank (the caller serialises its own pushes)
+    const uint32_t taken = ctl_->subs_taken.load(std::memory_order_acquire);
+    if (q.head.load(std::memory_order_relaxed) - q.tail.load(std::memory_order_acquire) < kDpSubRing) break;
+    if (ctl_->stop.load()) return false;
+    futex_wait(&ctl_->subs_taken, taken, 50);
+  }
+  const uint32_t h = q.head.load(std::memory_order_relaxed);
+  DpSub& slot = q.slots[h % kDpSubRing];
+  slot.gseq = ctl_->gseq.fetch_add(1) + 1;
+  slot.sub_id = s.sub_id;
+  slot.n = s.n;
+  std::memcpy(slot.items, s.items, sizeof(DpItem) * static_cast<size_t>(s.n));
+  q.head.store(h + 1, std::memory_order_release);
+  ctl_->subs_posted.fetch_add(1, std::memory_order_release);
+  futex_wake(&ctl_->subs_posted);
+  return !ctl_->stop.load();
+}
+
+int DpGroup::peek_sub_items() const {
+  int best = -1;
+  uint64_t best_seq = UINT64_MAX;
+  for (int r = 0; r < world_; ++r) {
+    auto& q = ctl_->subq[r];
+    const uint32_t t = q.tail.load(std::memory_order_relaxed);
+    if (q.head.load(std::memory_order_acquire) == t) continue;
+    const DpSub& s = q.slots[t % kDpSubRing];
+    if (s.gseq < best_seq) {
+      best_seq = s.gseq;
+      best = s.n;
+    }
+  }
+  return best;
+}
+
+bool DpGroup::pop_sub(DpSub& out, int& rank, int timeout_ms) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (true) {
+    const uint32_t posted = ctl_->subs_posted.load(std::memory_order_acquire);
+    int best = -1;
+    uint64_t best_seq = UINT64_MAX;
+    for (int r = 0; r < world_; ++r) {
+      auto& q = ctl_->subq[r];
+      const uint32_t t = q.tail.load(std::memory_order_relaxed);
+      if (q.head.load(std::memory_order_acquire) == t) continue;
+      const uint64_t gs = q.slots[t % kDpSubRing].gseq;
+      if (gs < best_seq) {
+        best_seq = gs;
+        best = r;
+      }
+    }
+    if (best >= 0) {
+      auto& q = ctl_->subq[best];
+      const uint32_t t = q.tail.load(std::memory_order_relaxed);
+      const DpSub& s = q.slots[t % kDpSubRing];
+      out.gseq = s.gseq;
+      out.sub_id = s.sub_id;
+      out.n = s.n;
+      std::memcpy(out.items, s.items, sizeof(DpItem) * static_cast<size_t>(s.n));
+      q.tail.store(t + 1, std::memory_order_release);
+      ctl_->subs_taken.fetch_add(1, std::memory_order_release);
+      futex_wake(&ctl_->subs_taken);
+      rank = best;
+      return true;
+    }
+    if (ctl_->stop.load()) return false;
+    const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    if (left.count() <= 0) return false;
+    futex_wait(&ctl_->subs_posted, posted, static_cast<int>(std::min<long long>(left.count(), 50)));
+  }
+}
+
+void DpGroup::publish_port(int port) {
+  ctl_->port.store(port, std::memory_order_release);
+  futex_wake(reinterpret_cast<std::atomic<uint32_t>*>(&ctl_->port));
+}
+
+int DpGroup::wait_port(int timeout_ms) const {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (true) {
+    const int p = ctl_->port.load(std::memory_order_acquire);
+    if (p > 0) return p;
+    if (ctl_->stop.load() || std::chrono::steady_clock::now() > deadline) return -1;
+    futex_wait(reinterpret_cast<std::atomic<uint32_t>*>(&ctl_->port), 0, 50);
+  }
+}
+
 void DpGroup::stop() {
   ctl_->stop.store(1);
   futex_wake(&ctl_->head);
   futex_wake(&ctl_->done_any);
   futex_wake(&ctl_->id_ready);
   futex_wake(&ctl_->bar_gen);
+  futex_wake(&ctl_->subs_posted);
+  futex_wake(&ctl_->subs_taken);
 }
 
 bool DpGroup::stopping() const { return ctl_->stop.load() != 0; }

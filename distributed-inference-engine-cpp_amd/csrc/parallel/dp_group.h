@@ -8,7 +8,11 @@
 //     follower reads its shard's inputs from the very pages the HTTP thread wrote (each process
 //     hipHostRegister()s the arena, and every GPU pulls its shard over its own PCIe link -- no
 //     routing through GPU 0);
-//   * gather slots for the host communicator (CPU engines / tests).
+//   * gather slots for the host communicator (CPU engines / tests);
+//   * per-rank sub-batch rings: EVERY rank's worker ingests HTTP (the ranks share one listening port
+//     through SO_REUSEPORT), parses into the arena and queues its requests as a sub-batch; the
+//     leader's dispatcher merges queued sub-batches (oldest first) into one DP batch, so no single
+//     process's ingest caps an N-GPU worker.
 // Reference: none (the reference has no intra-worker parallelism); this implements
 // the north-star DP mode (BASELINE.json config 4).
 #pragma once
@@ -25,19 +29,40 @@ namespace die {
 constexpr int kDpMaxRanks = 16;
 constexpr int kDpMaxItems = 2048;  // requests per DP batch
 constexpr int kDpRing = 4;         // batch descriptors in flight
+constexpr int kDpSubMax = 256;     // requests per sub-batch (one rank's local batch)
+constexpr int kDpSubRing = 8;      // sub-batches queued per rank
+constexpr int kDpMaxSubs = 64;     // sub-batches merged into one DP batch
 
 struct DpItem {
   uint64_t off = 0;  // byte offset of the item's buffer in the arena
   uint64_t len = 0;  // floats, or text bytes when is_text
-  uint32_t is_text = 0;
+  uint32_t is_text = 0;  // 1 = raw JSON number text, 2 = 4-bit packed text (core/textpack.h)
   uint32_t pad = 0;
+};
+
+// Where a rank's sub-batch sits inside a DP batch: items [start, start + n).
+struct DpSubRef {
+  int32_t rank = 0;
+  uint32_t sub_id = 0;
+  int32_t start = 0;
+  int32_t n = 0;
 };
 
 struct DpBatch {
   uint64_t seq = 0;
   int32_t B = 0;    // items in the whole batch
-  int32_t per = 0;  // items per rank (ceil(B / world)); rank r owns [r*per, min(B, (r+1)*per))
+  int32_t per = 0;  // items per rank (ceil(B / world)); rank r computes [r*per, min(B, (r+1)*per))
+  int32_t nsub = 0;
+  int32_t pad = 0;
+  DpSubRef subs[kDpMaxSubs];
   DpItem items[kDpMaxItems];
+};
+
+struct DpSub {
+  uint64_t gseq = 0;  // group-wide queue order (the dispatcher takes the oldest first)
+  uint32_t sub_id = 0;
+  int32_t n = 0;
+  DpItem items[kDpSubMax];
 };
 
 class DpGroup {
@@ -59,7 +84,7 @@ class DpGroup {
   // ---- input arena (leader allocates; offsets are valid in every process) ----
   uint8_t* arena() const { return arena_; }
   size_t arena_bytes() const { return arena_bytes_; }
-  void* arena_alloc(size_t bytes);  // leader only; 4 KiB aligned bump allocation, nullptr when full
+  void* arena_alloc(size_t bytes);  // any rank (atomic bump in the segment); 4 KiB aligned, nullptr when full
   uint64_t offset_of(const void* p) const { return static_cast<uint64_t>(static_cast<const uint8_t*>(p) - arena_); }
   void* at(uint64_t off) const { return arena_ + off; }
 
@@ -77,6 +102,18 @@ class DpGroup {
   bool next(uint64_t seq, DpBatch& out, const std::atomic<bool>* ext_stop = nullptr);
   // Follower: batch `seq` fully processed (its ring slot may be reused).
   void done(uint64_t seq);
+
+  // ---- sub-batch queues (every rank produces, the leader consumes) ----
+  // Queue a sub-batch of this rank (blocks while its ring is full); false when stopping.
+  bool push_sub(const DpSub& s);
+  // Leader: take the oldest queued sub-batch of any rank; waits up to timeout_ms (false if none).
+  bool pop_sub(DpSub& out, int& rank, int timeout_ms);
+  // Leader: oldest queued sub-batch's item count without taking it (-1 when none).
+  int peek_sub_items() const;
+
+  // ---- shared listening port (SO_REUSEPORT ingest on every rank) ----
+  void publish_port(int port);
+  int wait_port(int timeout_ms) const;
   void stop();
   bool stopping() const;
 

@@ -122,7 +122,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
 
 WorkerNode::~WorkerNode() { stop(); }
 
-int WorkerNode::start() { return server_.start(opt_.host, opt_.port, opt_.http_threads); }
+int WorkerNode::start() { return server_.start(opt_.host, opt_.port, opt_.http_threads, opt_.reuse_port); }
 void WorkerNode::wait() { server_.wait(); }
 
 void WorkerNode::stop() {

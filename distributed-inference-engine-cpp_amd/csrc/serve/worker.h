@@ -43,6 +43,8 @@ struct WorkerOptions {
   bool verbose = false;
   // Accept X-Die-Shm body descriptors from a co-located gateway (core/shm_arena.h).
   bool accept_shm = true;
+  // Share the listening port with other processes (the ranks of a data-parallel worker).
+  bool reuse_port = false;
 };
 
 class WorkerNode {

@@ -382,7 +382,7 @@ def grouped_conv(x_nhwc, w, bias=None, stride=1, pads=(0, 0, 0, 0), groups=1, cl
     Cout, cpg, KH, KW = w.shape
     Ho = (H + pads[0] + pads[2] - KH) // stride + 1
     Wo = (W + pads[1] + pads[3] - KW) // stride + 1
-    xin = _in(x_nhwc, split)
+    xin = _in(x_nhwc, split) if split else x_nhwc.to(torch.bfloat16).contiguous()
     wp = w.float().permute(0, 2, 3, 1).contiguous()
     bp = None if bias is None else bias.float().contiguous()
     out = torch.empty(((2,) if split else ()) + (B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x_nhwc.device)

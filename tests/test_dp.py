@@ -109,3 +109,74 @@ def test_dp_follower_reports_missing_group(native, models):
     time.sleep(0.2)
     assert f.status()["running"] is True
     assert f.join(stop=True) == 0
+
+
+INGEST_RANK = """
+import sys, os, json
+sys.path.insert(0, {repo!r}); os.environ['DIE_NO_TORCH'] = '1'
+import die_amd
+from die_amd import native
+w = native.Worker({model!r}, node_id='dp-r{rank}', port={port}, reuse_port=True, max_batch={mb},
+                  engine=dict(device='cpu', dp_world={world}, dp_group={group!r}, dp_rank={rank}))
+print('READY', flush=True)
+sys.stdin.readline()
+print('HEALTH ' + json.dumps(w.health()), flush=True)
+w.stop()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_every_rank_ingests(native, models, world):
+    """the DP leader owned all HTTP ingest.  Now every rank listens on the same port
+    (SO_REUSEPORT), parses its own connections' requests into the shared arena and queues them as
+    sub-batches; the leader merges the queues into DP batches and every rank answers its own."""
+    import socket
+
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["tiny"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    group = "die_dp_i%d_%d" % (os.getpid(), world)
+    env = dict(os.environ, DIE_NO_TORCH="1")
+    ps = [subprocess.Popen([sys.executable, "-c", INGEST_RANK.format(repo=REPO, model=path, rank=k, port=port,
+                                                                     mb=8, world=world, group=group)],
+                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+          for k in range(1, world)]
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=8,
+                           engine={"device": "cpu", "dp_world": world, "dp_group": group})
+        for p in ps:
+            line = p.stdout.readline().decode()
+            assert "READY" in line, line + p.stdout.read().decode()
+        res = native.loadgen(port=port, connections=24, requests=240, payload="full", input_numel=3 * 64 * 64)
+        assert res["ok"] == 240 and res["failed"] == 0, res
+        x = r.synthetic_input(3, cfg).reshape(3, -1)
+        for i in range(3):  # answers are right whichever rank took the connection
+            body = json.dumps({"request_id": "ing%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            out = json.loads(urllib.request.urlopen(urllib.request.Request("http://127.0.0.1:%d/infer" % port,
+                                                                           data=body), timeout=30).read())
+            ref = native.cpu_run(path, x[i:i + 1].reshape(1, 3, 64, 64))[0]
+            np.testing.assert_allclose(np.array(out["output_data"], np.float32), ref, rtol=1e-5, atol=1e-5)
+        h0 = wk.health()
+        assert h0["engine"]["dp_rank"] == 0 and h0["engine"]["dp_batches"] >= 1
+    finally:
+        if wk is not None:
+            wk.stop()
+        healths = []
+        for p in ps:
+            try:
+                out, _ = p.communicate(b"stop\n", timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                out, _ = p.communicate()
+            healths += [json.loads(l[len("HEALTH "):]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
+    assert len(healths) == world - 1
+    parsed = [h0["total_requests"]] + [h["total_requests"] for h in healths]
+    assert sum(parsed) >= 243 and all(n > 0 for n in parsed), parsed  # every rank ingested
+    merged = h0["engine"]["dp_subbatches_merged"]
+    sent = h0["engine"]["dp_subbatches_sent"] + sum(h["engine"]["dp_subbatches_sent"] for h in healths)
+    assert merged == sent and merged > h0["engine"]["dp_batches"] / 2

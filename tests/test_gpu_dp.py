@@ -55,3 +55,68 @@ def test_dp_worker_rccl_world1_http(native, models):
     finally:
         wk.stop()
         ref_eng.close()
+
+
+RANK1 = """
+import sys, os, json
+sys.path.insert(0, {repo!r})
+import torch
+import die_amd
+from die_amd import native
+w = native.Worker({model!r}, node_id='dp-r1', port={port}, reuse_port=True, max_batch=16,
+                  engine=dict(device='hip', device_id=1, dp_world=2, dp_group={group!r}, dp_rank=1, autotune=False))
+print('READY', flush=True)
+sys.stdin.readline()
+print('HEALTH ' + json.dumps(w.health()), flush=True)
+w.stop()
+"""
+
+
+def test_dp_rccl_two_ranks(native, models):
+    """Two RCCL ranks on two GPUs (skipped on a 1-GPU box: RCCL refuses two ranks on one device):
+    the follower's weights arrive by ncclBroadcast, per-sample-identifiable inputs come back in item
+    order through ncclAllGather, and both ranks ingest HTTP on the shared port."""
+    import socket
+    import subprocess
+    import sys
+
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    from die_amd.models import resnet_v2 as r
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path, w, cfg = models["tiny"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    group = "die_gpu_dp2_%d" % os.getpid()
+    p = subprocess.Popen([sys.executable, "-c", RANK1.format(repo=repo, model=path, port=port, group=group)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    wk = None
+    plain = native.Engine(path, device="hip", max_batch=16, autotune=False)
+    try:
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=16,
+                           engine={"device": "hip", "dp_world": 2, "dp_group": group, "autotune": False})
+        line = p.stdout.readline().decode()
+        assert "READY" in line, line
+        res = native.loadgen(port=port, connections=16, requests=256, payload="full", input_numel=3 * 64 * 64)
+        assert res["ok"] == 256 and res["failed"] == 0, res
+        x = r.synthetic_input(12, cfg, seed=5).reshape(12, -1)
+        ref = plain.run(x)
+        for i in range(12):  # distinct inputs: a shard/gather order mix-up would swap rows
+            body = json.dumps({"request_id": "two%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            out = json.loads(urllib.request.urlopen(urllib.request.Request("http://127.0.0.1:%d/infer" % port,
+                                                                           data=body), timeout=60).read())
+            np.testing.assert_allclose(np.array(out["output_data"], np.float32), ref[i], rtol=1e-4, atol=1e-5)
+        h0 = wk.health()
+        assert h0["engine"]["dp_backend"] == "rccl" and h0["engine"]["dp_world"] == 2
+    finally:
+        if wk is not None:
+            wk.stop()
+        out, _ = p.communicate(b"stop\n", timeout=120)
+        plain.close()
+    h1 = [json.loads(l[7:]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
+    assert h1 and h1[0]["total_requests"] > 0 and h0["total_requests"] > 0
