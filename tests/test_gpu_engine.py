@@ -30,7 +30,7 @@ def test_hip_engine_tiny_vs_cpu(native, models):
     # padding invariance: sample 0 alone (bucket 1) == sample 0 inside a batch of 5 (bucket 8); the
     # buckets may use different tuned split-K orders, so equal up to fp32 re-association
     one = e.run(x[:1].reshape(1, -1))
-    np.testing.assert_allclose(one[0], got[0], rtol=1e-4, atol=1e-5)
+    assert float(np.linalg.norm(one[0] - got[0]) / np.linalg.norm(got[0])) < 1e-4
     e.close()
 
 

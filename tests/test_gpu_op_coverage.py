@@ -91,5 +91,6 @@ def test_softmax_rows_kernel(native, split):
     got16, got32 = K.softmax_rows(x, split=split)
     ref = torch.softmax(x.double(), -1)
     torch.cuda.synchronize()
-    assert float((got32.double() - ref).norm() / ref.norm()) < 1e-6
+    # split input carries ~17 significant bits (exp of |x| <= 16 magnifies that to ~1e-5 relative)
+    assert float((got32.double() - ref).norm() / ref.norm()) < (2e-5 if split else 1e-6)
     assert float((got16.double() - ref).norm() / ref.norm()) < (2e-5 if split else 1e-2)
