@@ -582,7 +582,7 @@ class HipEngine : public Engine {
   std::chrono::steady_clock::time_point dispatch_not_before() override {
     using clk = std::chrono::steady_clock;
     const auto now = clk::now();
-    if (!opt_.pace || n_exec_ > 1 || comm_ || graphs_.empty()) return now;
+    if (!opt_.pace || n_exec_ > 1 || graphs_.empty()) return now;
     int ev, bi;
     {
       std::lock_guard<std::mutex> g(mu_);

@@ -12,6 +12,9 @@ Derived metrics (gfx950: 256 CUs, 1024 SIMDs; formulas from `rocprofv3 -L`):
                 of wide coalesced reads on gfx950 -> doubled; an estimate, Infinity-Cache hits included)
   L2 hit %    = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   LDS conf    = SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS (conflict cycles per LDS instruction)
+  park/stall/issue % = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over their sum (wave parked
+                on s_waitcnt or a barrier / issue-stalled / issuing; disjoint, ~= SQ_WAVE_CYCLES)
+  LDS-issue % = SQ_WAIT_INST_LDS over the same sum (a sub-bucket of the stall share)
 usage: pmc_summary.py gpurun_out/r10/resnet50 [--title T]
 """
 import argparse
@@ -47,14 +50,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--title", default="")
+    ap.add_argument("--note", default="heuristic kernel configs, no graphs")
     a = ap.parse_args()
     passes = [load(os.path.join(a.dir, p)) for p in ("p1", "p2", "p3", "p4") if os.path.isdir(os.path.join(a.dir, p))]
     n = min(len(p) for p in passes)
     lines = ["# rocprofv3 PMC counters: %s" % (a.title or os.path.basename(a.dir.rstrip("/"))), "",
-             "One eager forward at batch 32 (heuristic kernel configs, no graphs), counters from 4 separate",
+             "One eager forward at batch 32 (%s), counters from 4 separate" % a.note,
              "`rocprofv3 --kernel-trace --pmc` passes joined by dispatch order. Derived formulas: see tools/pmc_summary.py.",
-             "", "| # | kernel | grid | VGPR/AGPR | LDS B | us | MfmaUtil % | Occ % | HBM GB/s (est) | L2 hit % | LDS conf/instr |",
-             "|---:|---|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
+             "", "| # | kernel | grid | VGPR/AGPR | LDS B | us | MfmaUtil % | Occ % | HBM GB/s (est) | L2 hit % | LDS conf/instr | park/stall/issue % | LDS-issue % |",
+             "|---:|---|---:|---|---:|---:|---:|---:|---:|---:|---:|---|---:|"]
     tot = defaultdict(float)
     for i in range(n):
         k = {}
@@ -73,8 +77,11 @@ def main():
         hit, miss = k.get("TCC_HIT_sum", 0), k.get("TCC_MISS_sum", 0)
         l2 = 100 * hit / (hit + miss) if hit + miss else 0
         ldsc = k.get("SQ_LDS_BANK_CONFLICT", 0) / max(k.get("SQ_INSTS_LDS", 0), 1)
-        lines.append("| %d | `%s` | %d | %d/%d | %d | %.1f | %.1f | %.0f | %.0f | %.0f | %.2f |" % (
-            i, short(d["name"]), d["grid"], d["vgpr"], d["agpr"], d["lds"], us, mfma, occ, gbs, l2, ldsc))
+        wa, wi, ac = k.get("SQ_WAIT_ANY", 0), k.get("SQ_WAIT_INST_ANY", 0), k.get("SQ_ACTIVE_INST_ANY", 0)
+        ws = max(wa + wi + ac, 1)
+        lines.append("| %d | `%s` | %d | %d/%d | %d | %.1f | %.1f | %.0f | %.0f | %.0f | %.2f | %.0f/%.0f/%.0f | %.0f |" % (
+            i, short(d["name"]), d["grid"], d["vgpr"], d["agpr"], d["lds"], us, mfma, occ, gbs, l2, ldsc,
+            100 * wa / ws, 100 * wi / ws, 100 * ac / ws, 100 * k.get("SQ_WAIT_INST_LDS", 0) / ws))
         tot["us"] += us
         tot["mfma_cyc"] += k.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
         tot["gui"] += gui
