@@ -90,26 +90,18 @@ def main():
 
     import torch  # first: one HIP runtime per process (see native.lib)
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+    import die_amd  # noqa: F401
+    from die_amd import native
+    from die_amd.parallel.launch import HostGroup
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
+    hg = HostGroup()  # gloo: host-side barriers and reductions over the ranks
+    rank, world, local_rank = hg.rank, hg.world, hg.info.local_rank
     hip = args.device == "hip"
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        hg.barrier()
         if hip:
             torch.cuda.synchronize()
-
-    import die_amd  # noqa: F401
-    from die_amd import native
     if args.arch == "vit_b16":
         from die_amd.models import vit as r
 
@@ -155,10 +147,7 @@ def main():
         target_port = wk.port
         if args.mode == "gateway":
             # every rank's gateway routes over every rank's worker (ring on request_id)
-            ports = [wk.port]
-            if dist is not None:
-                ports = [None] * world
-                dist.all_gather_object(ports, wk.port)
+            ports = hg.all_gather_object(wk.port)
             gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
                                       local_shm=not args.no_local_shm)
             target_port = gw.port
@@ -239,10 +228,7 @@ def main():
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
             sk.close()
-        if dist is not None:
-            obj = [port]
-            dist.broadcast_object_list(obj, src=0)
-            port = obj[0]
+        port = hg.broadcast_object(port, src=0)
         eng_opts = dict(engine_opts, dp_world=world, dp_group=group, dp_rank=rank)
         wk = native.Worker(model, node_id="dp-r%d" % rank, port=port, reuse_port=True, max_batch=Btot,
                            engine=eng_opts)
@@ -269,7 +255,7 @@ def main():
         if rank != 0:
             barrier()
         wk.stop()
-        if rank == 0 and dist is not None:
+        if rank == 0 and world > 1:
             barrier()
     else:
         import numpy as np
@@ -289,15 +275,10 @@ def main():
         extra = {"engine": eng.refresh_info()["name"], "device_ms_per_batch": eng.info.get("avg_device_ms")}
         eng.close()
 
-    if dist is not None:
-        t = torch.tensor([elapsed, float(ok), float(failed)], dtype=torch.float64)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, ok, failed = mx[0].item(), t[1].item(), t[2].item()
-        lat = torch.tensor([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], dtype=torch.float64)
-        dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-        extra["p50_ms"], extra["p99_ms"] = lat[0].item(), lat[1].item()
+    if world > 1:
+        elapsed = hg.reduce([elapsed], "max")[0]
+        ok, failed = hg.reduce([ok, failed], "sum")
+        extra["p50_ms"], extra["p99_ms"] = hg.reduce([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], "max")
     value = ok / elapsed
     if rank == 0:
         out = {
@@ -322,8 +303,7 @@ def main():
         extra["numa"] = numa
         out.update({k: v for k, v in extra.items() if v is not None})
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    if dist is not None:
-        dist.destroy_process_group()
+    hg.close()
 
 
 if __name__ == "__main__":

@@ -596,21 +596,8 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s);
-
-  int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
-  for (int t = 0; t < nk; ++t) {
-    // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
-    // instructions each) are outstanding.
-    wait_stages<G, STAGES - 2>(nk - 1 - t);
-    __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
-    asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(wr);
-    wr = wr + 1 == STAGES ? 0 : wr + 1;
-    const uint16_t* A = lds + rd * STAGE;
-    rd = rd + 1 == STAGES ? 0 : rd + 1;
+  // One K-step's MFMAs on the stage at A (K-step t of this slice, for the BNL channel table).
+  auto compute = [&](const uint16_t* A, int t) {
     const uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -651,6 +638,36 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
 #pragma unroll
         for (int j = 0; j < TM; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (STAGES == 1) {
+    // No ring: load, wait, compute, once per K-step.  Meant for nk == 1 (K <= 64: the expand /
+    // reduce convs of stage 1), where a ring buys nothing and a 1-stage LDS footprint lets 2-4x
+    // more blocks share a CU to hide the load and epilogue latency.
+    for (int t = 0; t < nk; ++t) {
+      if (t) __syncthreads();  // everyone done reading the previous K-step
+      issue(0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(lds, t);
+    }
+  } else {
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nk) issue(s);
+    int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
+    for (int t = 0; t < nk; ++t) {
+      // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
+      // instructions each) are outstanding.
+      wait_stages<G, STAGES - 2>(nk - 1 - t);
+      __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
+      asm volatile("" ::: "memory");
+      if (t + STAGES - 1 < nk) issue(wr);
+      wr = wr + 1 == STAGES ? 0 : wr + 1;
+      const uint16_t* A = lds + rd * STAGE;
+      rd = rd + 1 == STAGES ? 0 : rd + 1;
+      compute(A, t);
     }
   }
   wait_vmcnt<0>();
@@ -707,17 +724,19 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
     if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
-    // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS)
+    // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS); variant 5 =
+    // one stage, no ring
     constexpr int kStageBytes = (BM + BN) * BK * 2;
     if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
     // split stages are twice as large: 128x128 fits 2 stages, 64-wide tiles 3-4 (160 KiB LDS)
     const int np = a.split ? 2 : 1;
-    const int stages = variant == 1 ? 2 : variant == 2 ? 3 : variant == 3 ? 4 : 6;
+    const int stages = variant == 1 ? 2 : variant == 2 ? 3 : variant == 3 ? 4 : variant == 4 ? 6 : 1;
     if (stages * kStageBytes * np > 160 * 1024) return hipErrorInvalidValue;
     switch (variant) {
       case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
       case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;
       case 3: launch_glds<BM, BN, 4>(mode0, grid, s, b, kt_per); break;
+      case 5: launch_glds<BM, BN, 1>(mode0, grid, s, b, kt_per); break;
       default:
         if constexpr (6 * kStageBytes <= 160 * 1024) launch_glds<BM, BN, 6>(mode0, grid, s, b, kt_per);
         else return hipErrorInvalidValue;

@@ -67,7 +67,9 @@ struct ConvArgs {
 // 1..4 = LDS-DMA ring of 2, 3, 4, 6 stages (variants 1-4: 1x1 with K % 64 == 0, or Cin % 64 == 0;
 // 6 stages only where they fit the LDS; they return hipErrorInvalidValue otherwise so a tuner can
 // skip them).  The deep rings keep more K-steps in flight for the latency-bound small-M layers.
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 20 };
+// Variant 5 = the LDS-DMA loop with ONE stage (no ring): for K <= 64 layers, where the smaller LDS
+// footprint fits more blocks per CU.
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 24 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

@@ -9,12 +9,14 @@
 // same key, and two different inputs collide with probability ~2^-128.
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <list>
 #include <mutex>
 #include <optional>
+#include <random>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -99,16 +101,30 @@ struct InputKeyHash {
   size_t operator()(const InputKey& k) const { return static_cast<size_t>(k.h0 ^ (k.h1 * 0x9E3779B97F4A7C15ull)); }
 };
 
-// 128-bit hash of a byte string: four independent multiply-mix lanes over 64-byte blocks (the
+// Per-process random secret of the input hash: which inputs collide cannot be worked out from the
+// source (the reference compares whole keys; this cache keeps 128 bits of a keyed hash instead).
+inline const uint64_t* cache_hash_secret() {
+  static const std::array<uint64_t, 4> s = [] {
+    std::random_device rd;
+    std::array<uint64_t, 4> v{};
+    for (auto& x : v) x = (static_cast<uint64_t>(rd()) << 32 | rd()) | 1ull;  // odd: never a zero multiplier
+    return v;
+  }();
+  return s.data();
+}
+
+// 128-bit keyed hash of a byte string: four independent multiply-mix lanes over 64-byte blocks (the
 // lanes have no dependency on each other, so a 1 MB body hashes at memory speed), folded at the
-// end.  `tag` separates key domains (float bit patterns vs. raw input text).
+// end.  `tag` separates key domains (float bit patterns vs. raw input text).  The mix is the
+// "protected" form: a lane keeps its multiplicands XORed in, so a zero product (one operand equal
+// to its secret word) does not wipe the lane's history.
 inline InputKey hash_bytes(const void* data, size_t bytes, uint64_t tag) {
   auto mum = [](uint64_t a, uint64_t b) {
     __uint128_t r = static_cast<__uint128_t>(a) * b;
-    return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
+    return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64) ^ a ^ b;
   };
-  const uint64_t k0 = 0xa0761d6478bd642full, k1 = 0xe7037ed1a0b428dbull, k2 = 0x8ebc6af09c88c6e3ull,
-                 k3 = 0x589965cc75374cc3ull;
+  const uint64_t* sec = cache_hash_secret();
+  const uint64_t k0 = sec[0], k1 = sec[1], k2 = sec[2], k3 = sec[3];
   uint64_t h[4] = {0x243F6A8885A308D3ull ^ bytes, 0x13198A2E03707344ull + bytes, 0xA4093822299F31D0ull ^ tag,
                    0x082EFA98EC4E6C89ull + tag};
   const unsigned char* p = static_cast<const unsigned char*>(data);

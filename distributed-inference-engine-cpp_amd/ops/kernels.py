@@ -71,6 +71,10 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split:
     return out, K, Kpad
 
 
+# launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg)
+NUM_CFGS = 24
+
+
 class ConvProblem:
     """One implicit-GEMM conv problem with packed weights and preallocated outputs, re-launchable with
     any (config, split-K, fused) choice -- used by conv2d_nhwc and by tools/conv_bench.py.

@@ -142,6 +142,21 @@ def test_lru_cache(native):
     assert c.get(np.array([0.0, 1.0], np.float32)) is None
 
 
+def test_lru_cache_hash_is_keyed(native):
+    """Inputs built to zero a lane of an unkeyed multiply-mix hash (a 64-bit word equal to the mix
+    constant) must not collide: the hash is keyed with a per-process secret and the mix keeps its
+    multiplicands (lru_cache.h hash_bytes)."""
+    c = native.Cache(8)
+    words = np.zeros(8, np.uint64)
+    words[1] = np.uint64(0xE7037ED1A0B428DB)  # the former fixed k1 of lane 0
+    a, b = words.copy(), words.copy()
+    a[0], b[0] = 1, 2
+    ka, kb = a.view(np.float32), b.view(np.float32)
+    c.put(ka, np.array([1], np.float32))
+    assert c.get(kb) is None
+    assert c.get(ka.copy())[0] == 1
+
+
 def test_json_roundtrip(native):
     doc = '{"a":[1,2.5,-3e2,"x\\u00e9\\n"],"b":{"c":null,"d":true,"e":false},"f":-0.0,"g":1e-7}'
     out = json.loads(native.json_roundtrip(doc))

@@ -89,7 +89,7 @@ def test_split_conv_every_variant_and_epilogue(native, shape, splits, fused):
     pr = K.ConvProblem(x.permute(0, 2, 3, 1).contiguous(), w, bias=bias, stride=s, pad=p, relu=True, res=res,
                        scale2=s2, shift2=b2, relu2=True, max_splits=splits, split=True)
     ran = []
-    for cfg in range(20):
+    for cfg in range(K.NUM_CFGS):
         rc = pr.launch(cfg, splits, fused)
         if rc == 1:
             continue
@@ -109,7 +109,7 @@ def test_split_conv_repeatable_bitwise(native):
     x = torch.randn(4, 28, 28, 128, device="cuda")
     w = torch.randn(128, 128, 3, 3, device="cuda") * 0.05
     pr = K.ConvProblem(x, w, pad=1, max_splits=4, split=True)
-    for cfg in range(20):
+    for cfg in range(K.NUM_CFGS):
         for splits in (1, 4):
             if pr.launch(cfg, splits) == 1:
                 continue

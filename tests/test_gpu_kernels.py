@@ -111,7 +111,7 @@ def test_conv_every_variant(native, shape, splits):
                      + res.float())
     xn = x.permute(0, 2, 3, 1).contiguous()
     ran = []
-    for cfg in range(20):
+    for cfg in range(K.NUM_CFGS):
         out, _ = K.conv2d_nhwc(xn, w.float(), bias=bias, stride=s, pad=p, relu=True, res=res, tile=cfg,
                                splits=splits)
         if out is None:
@@ -183,7 +183,7 @@ def test_conv_repeatable_bitwise(native):
             assert torch.equal(first.view(torch.int16), again.view(torch.int16))
         # every LDS-DMA ring depth (counted vmcnt per stage) and split-K, repeated
         pr = K.ConvProblem(x, w, pad=k // 2, max_splits=4)
-        for cfg in range(4, 20):
+        for cfg in range(4, K.NUM_CFGS):
             for splits in (1, 4):
                 if pr.launch(cfg, splits) == 1:
                     continue

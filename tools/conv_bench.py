@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--only", default="", help="substring filter on the shape name")
     ap.add_argument("--ref", action="store_true", help="also time torch.matmul (hipBLASLt) on the GEMM view "
                     "and F.conv2d (MIOpen, channels_last) for calibration")
+    ap.add_argument("--split", action="store_true", help="fp32 mode: split (hi, lo) planes, 3 MFMAs per pair")
     ap.add_argument("--json", default="")
     ap.add_argument("--md", default="")
     a = ap.parse_args()
@@ -78,10 +79,10 @@ def main():
                       relu2=True)
         elif epi == "f32":
             kw["out_f32"] = True
-        pr = K.ConvProblem(x, w, max_splits=16, **kw)
+        pr = K.ConvProblem(x, w, max_splits=16, split=a.split, **kw)
         nk = (cin * k * k + 63) // 64
         cands = []
-        for cfg in range(20):
+        for cfg in range(K.NUM_CFGS):
             for sp in (1, 2, 4, 8, 16):
                 if sp > nk or (sp > 1 and cout % 8):
                     continue
@@ -165,13 +166,14 @@ def main():
             json.dump(dict(batch=a.batch, total_us=total, shapes=results), f, indent=1)
     if a.md:
         lines = ["# conv kernel sweep, ResNet50-v2 shapes, batch %d (MI355X)" % a.batch, "",
-                 "Best of 20 configs x split-K {1..16} x {separate, fused} reduction; hipGraph of %d launches, "
-                 "median of %d replays. Weighted total %.1f us." % (a.reps, a.trials, total), "",
-                 "| shape | x | M | N | K | best us | TFLOP/s | cfg/split | v0 | v1 (2st) | v2 (3st) | v3 (4st) | v4 (6st) |",
-                 "|---|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|---:|---:|"]
+                 ("fp32 split mode. " if a.split else "") +
+                 "Best of %d configs x split-K {1..16} x {separate, fused} reduction; hipGraph of %d launches, "
+                 "median of %d replays. Weighted total %.1f us." % (K.NUM_CFGS, a.reps, a.trials, total), "",
+                 "| shape | x | M | N | K | best us | TFLOP/s | cfg/split | v0 | v1 (2st) | v2 (3st) | v3 (4st) | v4 (6st) | v5 (1st) |",
+                 "|---|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|"]
         for r in results:
             pv = r["best_per_variant"]
-            cells = ["%.1f" % pv[str(v)]["us"] if str(v) in pv else "-" for v in range(5)]
+            cells = ["%.1f" % pv[str(v)]["us"] if str(v) in pv else "-" for v in range(6)]
             lines.append("| %s | %d | %d | %d | %d | %.1f | %.0f | %d/%d%s | %s |" % (
                 r["name"], r["count"], r["M"], r["N"], r["K"], r["us"], r["tflops"], r["cfg"], r["splits"],
                 "f" if r["fused"] else "", " | ".join(cells)))
