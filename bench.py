@@ -250,7 +250,13 @@ def main():
                  "device_ms_per_batch": e1.get("avg_device_ms"),
                  "dp_batches_rank0": e1.get("dp_batches", 0) - h0["engine"].get("dp_batches", 0),
                  "requests_parsed_this_rank": h1["total_requests"] - h0["total_requests"],
-                 "client_connections_per_gpu": args.connections}
+                 "client_connections_per_gpu": args.connections,
+                 "subbatches_sent_this_rank": e1.get("dp_subbatches_sent", 0) - h0["engine"].get("dp_subbatches_sent", 0),
+                 "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"), "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"),
+                 "pace_lead_ms": e1.get("avg_pace_lead_ms"),
+                 "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()}}
+        if extra["dp_batches_rank0"]:
+            extra["avg_dp_batch"] = world * SR * args.steps / extra["dp_batches_rank0"] if rank == 0 else None
         barrier()  # every rank done with traffic before the leader stops the group
         if rank != 0:
             barrier()

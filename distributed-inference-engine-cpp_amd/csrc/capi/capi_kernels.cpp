@@ -196,6 +196,13 @@ int die_kern_stem(uint64_t x, uint64_t w, uint64_t bias, uint64_t out, int B, in
                                              P<uint16_t>(out), B, H, W, Ho, Wo, relu, S(stream), nullptr, split));
 }
 
+int die_kern_stem_nchw(uint64_t x, int C, uint64_t scale, uint64_t shift, uint64_t w, uint64_t bias, uint64_t out, int B,
+                       int H, int W, int Ho, int Wo, int relu, uint64_t stream, int split, int max_blocks) {
+  return static_cast<int>(kern::conv_stem7x7_nchw(P<const float>(x), C, P<const float>(scale), P<const float>(shift),
+                                                  P<const uint16_t>(w), P<const float>(bias), P<uint16_t>(out), B, H, W,
+                                                  Ho, Wo, relu, S(stream), nullptr, split, max_blocks));
+}
+
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, char** err) {
   try {

@@ -995,6 +995,13 @@ class HipEngine : public Engine {
                                      op.H, op.W, op.C, st, sp_);
           break;
         case PlanOp::STEM:
+          if (op.in == -2) {  // graph input, input prep fused
+            e = kern::conv_stem7x7_nchw(static_cast<const float*>(buf(op.in)), op.C, prm(op.scale_off),
+                                        prm(op.shift_off), reinterpret_cast<const uint16_t*>(params_ + op.w_off),
+                                        prm(op.bias_off), static_cast<uint16_t*>(buf(op.out)), B, op.conv.H,
+                                        op.conv.W, op.conv.Ho, op.conv.Wo, op.conv.relu, st, live, sp_);
+            break;
+          }
           e = kern::conv_stem7x7(static_cast<const uint16_t*>(buf(op.in)),
                                  reinterpret_cast<const uint16_t*>(params_ + op.w_off), prm(op.bias_off),
                                  static_cast<uint16_t*>(buf(op.out)), B, op.conv.H, op.conv.W, op.conv.Ho, op.conv.Wo,

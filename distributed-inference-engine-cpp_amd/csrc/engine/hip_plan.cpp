@@ -255,8 +255,12 @@ class Planner {
     const std::string ap = n.get_string("auto_pad", "NOTSET");
     int in_buf;
     int Cstore;
+    // A ResNet-style stem on the graph input reads the fp32 NCHW input itself (input_prep fused into
+    // its patch loader); the prep pass is only planned if this conv turns out not to be that stem.
+    bool deferred_prep = false;
     if (x.kind == Val::GRAPH_IN) {
-      in_buf = ensure_nhwc_input(x, n.in(0));
+      deferred_prep = KH == 7 && KW == 7 && x.C <= 4;
+      in_buf = deferred_prep ? -2 : ensure_nhwc_input(x, n.in(0));
       Cstore = x.C <= 4 ? 4 : 8;
     } else if (x.kind == Val::NHWC) {
       in_buf = x.buf;
@@ -380,8 +384,19 @@ class Planner {
     const bool stem = KH == 7 && KW == 7 && s == 2 && d == 1 && pads[0] == 3 && pads[1] == 3 && pads[2] == 3 &&
                       pads[3] == 3 && Cstore == 4 && Cout == 64 && res_buf < 0 && bn2 < 0 && need_out1 &&
                       relu != 3 && !graph_outputs_.count(cur);
+    if (deferred_prep && !stem) {
+      in_buf = ensure_nhwc_input(x, n.in(0));
+      p.in = in_buf;
+    }
     if (stem) {
       p.kind = PlanOp::STEM;
+      if (in_buf == -2) {  // fused input prep: channel count and the input's pending affine
+        p.C = x.C;
+        if (x.has_affine) {
+          p.scale_off = push_f32(x.asc);
+          p.shift_off = push_f32(x.ash);
+        }
+      }
       std::vector<float> ws(64 * 224, 0.f);
       for (int co = 0; co < Cout; ++co)
         for (int ci = 0; ci < Cin; ++ci)

@@ -471,13 +471,19 @@ constexpr int kBnlMaxK = 2048;  // pre-activation on load: channels staged in LD
 // SPLIT (fp32 mode): each stage holds [A_hi][B_hi][A_lo][B_lo]; the lo tiles are DMA'd from the
 // planes wplane / xplane elements after the hi ones (zero-page rows stay zero-page), and every
 // fragment pair takes three MFMAs (hi*hi + lo*hi + hi*lo).
-template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false>
+template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false, int BKS = BK>
 __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
+  static_assert(BKS == 64 || BKS == 32, "K-step width");
+  constexpr int CPR = BKS / 8;        // 16-byte chunks per LDS row
+  constexpr int RPI = 512 / BKS;      // rows per 1 KiB DMA wave-instruction
+  constexpr int KSUB = BKS / 32;      // MFMA K=32 substeps per K-step
+  constexpr int KR = BK / BKS;        // K-steps per 64-wide split-K unit
+  auto sw = [](int row, int chunk) { return row * BKS + ((chunk ^ ((row >> 1) & (CPR - 1))) << 3); };
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
-  constexpr int GA = BN / 32, GB = BM / 32, G = NP * (GA + GB);  // DMA instructions per wave per stage
+  constexpr int A_ELEMS = BN * BKS, B_ELEMS = BM * BKS, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
+  constexpr int GA = BN / 4 / RPI, GB = BM / 4 / RPI, G = NP * (GA + GB);  // DMA instructions per wave per stage
   constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
@@ -488,27 +494,27 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   int tile_m, tile_n, split, tile;
   if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int nk_total = p.Kpad / BK;
-  const int kt_begin = split * kt_per_split;
-  const int kt_end = min(nk_total, kt_begin + kt_per_split);
+  const int nk_total = p.Kpad / BKS;
+  const int kt_begin = split * kt_per_split * KR;  // kt_per_split counts 64-wide K-steps
+  const int kt_end = min(nk_total, kt_begin + kt_per_split * KR);
   const int nk = kt_end - kt_begin;
   // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
   __shared__ __attribute__((aligned(16))) float bnl[BNL ? 2 * kBnlMaxK : 4];
   if constexpr (BNL) {
-    for (int i = tid; i < nk * BK; i += 256) {
-      bnl[i] = p.in_scale[kt_begin * BK + i];
-      bnl[kBnlMaxK + i] = p.in_shift[kt_begin * BK + i];
+    for (int i = tid; i < nk * BKS; i += 256) {
+      bnl[i] = p.in_scale[kt_begin * BKS + i];
+      bnl[kBnlMaxK + i] = p.in_shift[kt_begin * BKS + i];
     }
     // visible to every wave after the main loop's first barrier
   }
 
   // Per-lane DMA sources.  Wave `wave` fills rows [wave*R/4, (wave+1)*R/4) of each operand, 8 rows
-  // per instruction; lane L -> row (L>>3) of that group, physical chunk L&7.
+  // per instruction (16 for 32-wide K-steps); lane L -> row L / CPR of that group, physical chunk L % CPR.
   const uint16_t* asrc[GA];
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = wave * (BN / 4) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
     asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
   }
   // MODE 0: each lane's row pointer, M-tail rows pointed into the zero page (which holds a whole
@@ -520,8 +526,8 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   long long bdel[GB];  // SPLIT, MODE 0: distance to the lo plane (0 for zero-page tail rows)
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
-    const int r = wave * (BM / 4) + i * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = wave * (BM / 4) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
     const int m = m0 + r;
     bval[i] = m < p.M;
     bdel[i] = bval[i] ? p.xplane : 0;
@@ -541,12 +547,12 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     }
   }
   // uniform state of the next K-step to issue (MODE 2: channel offset within the tap, tap x/y)
-  int nx_k0 = kt_begin * BK;
+  int nx_k0 = kt_begin * BKS;
   int nx_ci0 = 0, nx_kx = 0, nx_ky = 0;
   if (MODE == 2) {
-    const int cpt = p.Cin / BK;  // K-steps per filter tap
+    const int cpt = p.Cin / BKS;  // K-steps per filter tap
     const int tap = kt_begin / cpt;
-    nx_ci0 = (kt_begin - tap * cpt) * BK;
+    nx_ci0 = (kt_begin - tap * cpt) * BKS;
     nx_ky = tap / p.KW;
     nx_kx = tap - nx_ky * p.KW;
   }
@@ -555,16 +561,16 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     uint16_t* A = lds + buf * STAGE;
     uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) glds16(asrc[i] + nx_k0, A + (wave * (BN / 4) + i * 8) * BK);
+    for (int i = 0; i < GA; ++i) glds16(asrc[i] + nx_k0, A + (wave * (BN / 4) + i * RPI) * BKS);
     if constexpr (SPLIT) {
 #pragma unroll
-      for (int i = 0; i < GA; ++i) glds16(asrc[i] + p.wplane + nx_k0, A + PLANE + (wave * (BN / 4) + i * 8) * BK);
+      for (int i = 0; i < GA; ++i) glds16(asrc[i] + p.wplane + nx_k0, A + PLANE + (wave * (BN / 4) + i * RPI) * BKS);
     }
     if (MODE == 0) {
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
-        glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * 8) * BK);
-        if constexpr (SPLIT) glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 4) + i * 8) * BK);
+        glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * RPI) * BKS);
+        if constexpr (SPLIT) glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
       }
     } else {
       const int dy = nx_ky * p.dil, dx = nx_kx * p.dil;
@@ -575,10 +581,10 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
         const bool v = static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
                        static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
         const uint16_t* src = v ? bsrc[i] + ((ih * p.W + iw) * p.Cin + nx_ci0) : p.zeros;
-        glds16(src, Bt + (wave * (BM / 4) + i * 8) * BK);
-        if constexpr (SPLIT) glds16(v ? src + p.xplane : p.zeros, Bt + PLANE + (wave * (BM / 4) + i * 8) * BK);
+        glds16(src, Bt + (wave * (BM / 4) + i * RPI) * BKS);
+        if constexpr (SPLIT) glds16(v ? src + p.xplane : p.zeros, Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
       }
-      nx_ci0 += BK;
+      nx_ci0 += BKS;
       if (nx_ci0 == p.Cin) {
         nx_ci0 = 0;
         if (++nx_kx == p.KW) {
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
         }
       }
     }
-    nx_k0 += BK;
+    nx_k0 += BKS;
   };
 
   f32x4 acc[TN][TM];
@@ -600,23 +606,23 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   auto compute = [&](const uint16_t* A, int t) {
     const uint16_t* Bt = A + A_ELEMS;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KSUB; ++s) {
       const int chunk = s * 4 + (lane >> 4);
       bf16x8 af[TN], bfr[TM];
 #pragma unroll
       for (int i = 0; i < TN; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * WN + i * 16 + (lane & 15), chunk));
+        af[i] = *reinterpret_cast<const bf16x8*>(A + sw(wn * WN + i * 16 + (lane & 15), chunk));
 #pragma unroll
       for (int j = 0; j < TM; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + sw(wm * WM + j * 16 + (lane & 15), chunk));
       if constexpr (SPLIT) {
         bf16x8 afl[TN], bfl[TM];
 #pragma unroll
         for (int i = 0; i < TN; ++i)
-          afl[i] = *reinterpret_cast<const bf16x8*>(A + PLANE + swz(wn * WN + i * 16 + (lane & 15), chunk));
+          afl[i] = *reinterpret_cast<const bf16x8*>(A + PLANE + sw(wn * WN + i * 16 + (lane & 15), chunk));
 #pragma unroll
         for (int j = 0; j < TM; ++j)
-          bfl[j] = *reinterpret_cast<const bf16x8*>(Bt + PLANE + swz(wm * WM + j * 16 + (lane & 15), chunk));
+          bfl[j] = *reinterpret_cast<const bf16x8*>(Bt + PLANE + sw(wm * WM + j * 16 + (lane & 15), chunk));
 #pragma unroll
         for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
           }
       }
       if constexpr (BNL) {
-        const float* sc = bnl + t * BK + chunk * 8;
+        const float* sc = bnl + t * BKS + chunk * 8;
         const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
         const float4 h0 = *reinterpret_cast<const float4*>(sc + kBnlMaxK);
         const float4 h1 = *reinterpret_cast<const float4*>(sc + kBnlMaxK + 4);
@@ -675,20 +681,20 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
 }
 
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, int BKS = BK>
 void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
   if (b.split) {  // only ring depths whose doubled stages fit the LDS are instantiated
-    if constexpr (STAGES * (BM + BN) * BK * 4 <= 160 * 1024) {
-      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true>), grid, dim3(256), 0, s, b, kt_per);
-      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, true>), grid, dim3(256), 0, s, b, kt_per);
+    if constexpr (STAGES * (BM + BN) * BKS * 4 <= 160 * 1024) {
+      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
+      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
     }
   } else if (b.in_scale) {
-    if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
-    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, true>), grid, dim3(256), 0, s, b, kt_per);
+    if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, true, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, true, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
   } else if (mode0) {
-    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
   } else {
-    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES>), grid, dim3(256), 0, s, b, kt_per);
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
   }
 }
 
@@ -725,7 +731,8 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
     if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
     // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS); variant 5 =
-    // one stage, no ring
+    // one stage, no ring.  (32-wide K-step rings, conv_glds_kernel<..., BKS = 32>, were measured
+    // as 2/3-stage variants and never beat the 1-stage 64-wide loop: profiles/r2_conv_sweep_fp32_b32.md)
     constexpr int kStageBytes = (BM + BN) * BK * 2;
     if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
     // split stages are twice as large: 128x128 fits 2 stages, 64-wide tiles 3-4 (160 KiB LDS)

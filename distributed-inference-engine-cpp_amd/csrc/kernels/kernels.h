@@ -137,6 +137,12 @@ hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s, 
 // split: x/out are split tensors and w holds the hi plane [64][224] followed by the lo plane.
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
                         int Ho, int Wo, int relu, hipStream_t s, const long long* live = nullptr, int split = 0);
+// Persistent stem that reads the graph input directly: x fp32 NCHW [B][C][H][W], C <= 4, with the
+// input's pending per-channel affine (in_scale/in_shift, nullable) applied on load -- replaces
+// input_prep + conv_stem7x7.  max_blocks <= 0: two blocks per CU.
+hipError_t conv_stem7x7_nchw(const float* x, int C, const float* in_scale, const float* in_shift, const uint16_t* w,
+                             const float* bias, uint16_t* out, int B, int H, int W, int Ho, int Wo, int relu,
+                             hipStream_t s, const long long* live = nullptr, int split = 0, int max_blocks = 0);
 
 // Evict the L2s: stream-read `bytes` (> 8 x 4 MiB) of a scratch buffer (autotuning in the cache
 // state a layer sees inside a forward: L2 cold, Infinity Cache warm).

@@ -14,6 +14,8 @@
 //     128 bytes go out as 16-byte stores.
 //   * SPLIT (fp32 mode, common.h): input, weights and output are hi/lo planes; both planes of the
 //     patch and the weights sit in LDS and each fragment pair takes three MFMAs.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -139,6 +141,146 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
   }
 }
 
+// Fused variant: reads the graph input itself (fp32 NCHW, C <= 4 channels), applies the input's
+// pending BatchNormalization (scale/shift per channel, the former input_prep pass), and is
+// persistent: a block stages the weights in LDS ONCE and then walks output tiles (blockIdx.x,
+// + gridDim.x, ...), prefetching the next tile's patch into registers while the MFMAs of the
+// current one run.  The epilogue stores straight from the accumulators (8 bytes = 4 channels per
+// lane and plane) because the LDS holds the weights for the whole walk.
+constexpr int PPT = (PY * PX + 255) / 256;  // patch pixels per thread
+
+template <bool SPLIT>
+__global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __restrict__ x, int C,
+                                                             const float* __restrict__ in_scale,
+                                                             const float* __restrict__ in_shift,
+                                                             const uint16_t* __restrict__ w,
+                                                             const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                             int B, int H, int W, int Ho, int Wo, int relu, int tiles_x,
+                                                             int tiles_per_img, const long long* __restrict__ live) {
+  constexpr int NP = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t wl[NP * NCH * WP];
+  __shared__ __attribute__((aligned(16))) uint16_t patch[NP * PY * PX * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long oplane = static_cast<long long>(B) * Ho * Wo * NCH;
+  const int nb = live ? min(B, static_cast<int>(*live)) : B;
+  const int total = nb * tiles_per_img;
+  if (static_cast<int>(blockIdx.x) >= total) return;  // whole block, before any barrier
+  for (int i = tid; i < NP * NCH * (KS / 8); i += 256) {
+    const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
+    const int r = q / (KS / 8), c = q % (KS / 8);
+    *reinterpret_cast<uint4*>(wl + pl * NCH * WP + r * WP + c * 8) =
+        *reinterpret_cast<const uint4*>(w + pl * NCH * KS + r * KS + c * 8);
+  }
+  float sc[4], sh[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    sc[c] = (c < C && in_scale) ? in_scale[c] : 1.f;
+    sh[c] = (c < C && in_shift) ? in_shift[c] : 0.f;
+  }
+  const size_t HW = static_cast<size_t>(H) * W;
+  // raw input of this thread's patch pixels for tile t (0 outside the image; BN applied on store)
+  float pre[PPT][4];
+  bool inb[PPT];
+  auto fetch = [&](int t) {
+    const int b = t / tiles_per_img, tt = t - b * tiles_per_img;
+    const int iy0 = 2 * ((tt / tiles_x) * TY) - 3, ix0 = 2 * ((tt % tiles_x) * TX) - 3;
+    const float* xb = x + static_cast<size_t>(b) * C * HW;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int q = tid + k * 256;
+      const int py = q / PX, px = q - (q / PX) * PX;
+      const int iy = iy0 + py, ix = ix0 + px;
+      inb[k] = q < PY * PX && iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pre[k][c] = (inb[k] && c < C) ? xb[c * HW + static_cast<size_t>(iy) * W + ix] : 0.f;
+    }
+  };
+  fetch(blockIdx.x);
+  const int j = lane >> 4, px_l = lane & 15;
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    __syncthreads();  // weights staged / every wave done reading the previous tile's patch
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int q = tid + k * 256;
+      if (q >= PY * PX) continue;
+      float v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = (inb[k] && c < C) ? fmaf(pre[k][c], sc[c], sh[c]) : 0.f;
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if constexpr (SPLIT) split1(v[c], h[c], l[c]);
+        else h[c] = f2bf(v[c]);
+      }
+      *reinterpret_cast<uint2*>(patch + q * 4) = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+      if constexpr (SPLIT)
+        *reinterpret_cast<uint2*>(patch + PY * PX * 4 + q * 4) =
+            make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
+    }
+    __syncthreads();
+    const int tn = t + static_cast<int>(gridDim.x);
+    if (tn < total) fetch(tn);  // in flight during this tile's MFMAs
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      bf16x8 bf[NP][2];
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int py = 2 * (2 * wave + m) + ky, px = 2 * px_l + 2 * j;
+          bf[pl][m] = *reinterpret_cast<const bf16x8*>(patch + pl * PY * PX * 4 + (py * PX + px) * 4);
+        }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int wo = (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + wo);
+        if constexpr (SPLIT) {
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(wl + NCH * WP + wo);
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf[0][m], acc[n][m], 0, 0, 0);
+            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[NP - 1][m], acc[n][m], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[0][m], acc[n][m], 0, 0, 0);
+      }
+    }
+    const int b = t / tiles_per_img, tt = t - b * tiles_per_img;
+    const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int oy = ty0 + 2 * wave + m, ox = tx0 + px_l;
+      if (oy >= Ho || ox >= Wo) continue;
+      uint16_t* o = out + ((static_cast<size_t>(b) * Ho + oy) * Wo + ox) * NCH;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int ch = n * 16 + 4 * j;
+        const float4 bv = *reinterpret_cast<const float4*>(bias + ch);
+        float v[4] = {acc[n][m][0] + bv.x, acc[n][m][1] + bv.y, acc[n][m][2] + bv.z, acc[n][m][3] + bv.w};
+        if (relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        if constexpr (SPLIT) {
+          uint16_t h[4], l[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) split1(v[q], h[q], l[q]);
+          *reinterpret_cast<uint2*>(o + ch) = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+          *reinterpret_cast<uint2*>(o + oplane + ch) = make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
+        } else {
+          *reinterpret_cast<uint2*>(o + ch) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 static_assert(TY * TX * NCH <= NCH * WP, "output stage must fit in the weight buffer");
@@ -153,6 +295,28 @@ hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias,
   else
     hipLaunchKernelGGL(stem7x7_kernel<false>, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, x, w, bias, out, H, W, Ho,
                        Wo, relu, tiles_x, live);
+  return hipGetLastError();
+}
+
+hipError_t conv_stem7x7_nchw(const float* x, int C, const float* in_scale, const float* in_shift, const uint16_t* w,
+                             const float* bias, uint16_t* out, int B, int H, int W, int Ho, int Wo, int relu,
+                             hipStream_t s, const long long* live, int split, int max_blocks) {
+  if (C < 1 || C > 4 || Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1) return hipErrorInvalidValue;
+  const int tiles_x = (Wo + TX - 1) / TX, tiles_y = (Ho + TY - 1) / TY;
+  const int per_img = tiles_x * tiles_y;
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
+  }();
+  int grid = std::min(B * per_img, max_blocks > 0 ? max_blocks : 2 * cus);  // 2 blocks (72 KiB LDS each) per CU
+  grid = std::max(grid, 1);
+  if (split)
+    hipLaunchKernelGGL(stem7x7_nchw_kernel<true>, dim3(grid), dim3(256), 0, s, x, C, in_scale, in_shift, w, bias, out, B,
+                       H, W, Ho, Wo, relu, tiles_x, per_img, live);
+  else
+    hipLaunchKernelGGL(stem7x7_nchw_kernel<false>, dim3(grid), dim3(256), 0, s, x, C, in_scale, in_shift, w, bias, out,
+                       B, H, W, Ho, Wo, relu, tiles_x, per_img, live);
   return hipGetLastError();
 }
 

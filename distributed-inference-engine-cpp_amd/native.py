@@ -562,6 +562,8 @@ def _sig_kernels():
     L.die_kern_nhwc_to_nchw.argtypes = [u64, u64] + [i] * 4 + [u64, i]
     L.die_kern_stem.restype = i
     L.die_kern_stem.argtypes = [u64] * 4 + [i] * 6 + [u64, i]
+    L.die_kern_stem_nchw.restype = i
+    L.die_kern_stem_nchw.argtypes = [u64, i] + [u64] * 5 + [i] * 6 + [u64, i, i]
     L.die_kern_gconv.restype = i
     L.die_kern_gconv.argtypes = [C.c_char_p] + [u64] * 5
     L.die_kern_softmax.restype = i

@@ -375,6 +375,27 @@ def conv_stem7x7(x_nhwc4, w, bias, relu=True, split=False):
     return _out(out, split)
 
 
+def conv_stem7x7_nchw(x_nchw, w, bias, scale=None, shift=None, relu=True, split=False, max_blocks=0):
+    """Persistent fused stem: x [B,C<=4,H,W] fp32 NCHW (the graph input, no input_prep pass), the
+    per-channel input affine x*scale+shift applied on load, w [64,C,7,7] -> [B,Ho,Wo,64] (bf16, or the
+    fp32 values of the split planes).  max_blocks > 0 caps the grid (tests: several tiles per block)."""
+    import torch
+
+    B, C, H, W = x_nchw.shape
+    assert C <= 4 and w.shape[0] == 64
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty(((2,) if split else ()) + (B, Ho, Wo, 64), dtype=torch.bfloat16, device=x_nchw.device)
+    xin = x_nchw.float().contiguous()
+    b = bias.float().contiguous()
+    sc = None if scale is None else scale.float().contiguous()
+    sh = None if shift is None else shift.float().contiguous()
+    wp = pack_stem_weight(w, split)
+    rc = native.kernels().die_kern_stem_nchw(_ptr(xin), C, _ptr(sc), _ptr(sh), _ptr(wp), _ptr(b), _ptr(out),
+                                             B, H, W, Ho, Wo, int(relu), _stream(), int(split), int(max_blocks))
+    _check(rc, "conv_stem7x7_nchw")
+    return _out(out, split)
+
+
 # ---- grouped conv / row softmax (csrc/kernels/gconv.hip, transformer.hip) ---------------------------
 
 def grouped_conv(x_nhwc, w, bias=None, stride=1, pads=(0, 0, 0, 0), groups=1, clip=None, relu=False, split=False):

@@ -267,3 +267,27 @@ def test_split_stem_kernel(native, B, H, W, relu):
         ref = torch.relu(ref)
     torch.cuda.synchronize()
     assert rel_err(got.permute(0, 3, 1, 2), ref) < TOL, rel_err(got.permute(0, 3, 1, 2), ref)
+
+
+@pytest.mark.parametrize("B,H,W,relu,max_blocks", [(3, 224, 224, True, 0), (2, 37, 45, False, 5), (1, 64, 80, True, 1)])
+@pytest.mark.parametrize("split", [True, False])
+def test_fused_nchw_stem_kernel(native, B, H, W, relu, max_blocks, split):
+    """Persistent stem reading the fp32 NCHW graph input with the input BN applied on load (replaces
+    input_prep + stem) vs torch fp32; max_blocks forces every block to walk several tiles."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    g = torch.Generator(device="cuda").manual_seed(B * 11 + H + int(split))
+    x = torch.rand(B, 3, H, W, device="cuda", generator=g) * 255.0
+    scale = torch.tensor([0.017, 0.018, 0.0175], device="cuda")
+    shift = torch.tensor([-2.1, -2.0, -1.8], device="cuda")
+    w = torch.randn(64, 3, 7, 7, device="cuda", generator=g) / 12.0
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    got = K.conv_stem7x7_nchw(x, w, bias, scale=scale, shift=shift, relu=relu, split=split, max_blocks=max_blocks)
+    xn = x.double() * scale.double().view(1, 3, 1, 1) + shift.double().view(1, 3, 1, 1)
+    ref = torch.nn.functional.conv2d(xn, w.double(), bias.double(), stride=2, padding=3)
+    if relu:
+        ref = torch.relu(ref)
+    torch.cuda.synchronize()
+    err = rel_err(got.permute(0, 3, 1, 2), ref)
+    assert err < (TOL if split else 8e-3), err
