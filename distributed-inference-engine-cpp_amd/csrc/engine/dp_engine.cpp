@@ -50,6 +50,11 @@ size_t text_cap_for(size_t numel, const EngineOptions& opt) {
   return opt.device != "cpu" && opt.device_decode ? (numel * 24 + 4095) / 4096 * 4096 : 0;
 }
 
+// Arena sizing and back-pressure, in units of one rank's local batch (local_max_ requests):
+// requests staged per rank in the arena, and requests one rank may have queued + in flight.
+constexpr int kDpArenaBatches = 12;
+constexpr int kDpInflightBatches = 4;
+
 struct DpAbandoned : std::runtime_error {
   DpAbandoned() : std::runtime_error("data-parallel group abandoned before attach") {}
 };
@@ -67,7 +72,7 @@ class DpEngine : public Engine {
     local_max_ = std::max(1, std::min((opt.max_batch + world_ - 1) / world_, kDpSubMax));
     if (rank_ == 0) {
       // every rank stages its in-flight requests in the arena: N x (sub-batches queued + pipeline)
-      const size_t items = static_cast<size_t>(local_max_) * world_ * (kDpSubRing + 4) + 64;
+      const size_t items = static_cast<size_t>(local_max_) * world_ * kDpArenaBatches + 64;
       const size_t arena = opt.dp_arena_mb ? opt.dp_arena_mb << 20 : item_bytes_ * items;
       group_ = DpGroup::create(opt.dp_group, world_, arena, 4u << 20);
     } else {
@@ -112,9 +117,17 @@ class DpEngine : public Engine {
   size_t text_capacity() const override { return std::min(local_->text_capacity(), item_bytes_); }
   bool text_packing() const override { return local_->text_packing(); }
   void register_host_memory(void*, size_t) override {}
+  // The worker's batcher hands over whatever it has queued as soon as this returns; the leader
+  // merges everything queued at dispatch time, so requests accumulate in the ring (not in the
+  // batcher) while the GPU is busy.  Bounded by ring slots and by this rank's items in flight
+  // (queued + in the pipeline), not by sub-batch count: tiny eager sub-batches must not starve the
+  // next merge.
   void wait_for_slot() override {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return stop_ || pending_.size() < static_cast<size_t>(kDpSubRing - 1); });
+    cv_.wait(lk, [&] {
+      return stop_ || (pending_.size() < static_cast<size_t>(kDpSubRing - 1) &&
+                       pending_items_ < static_cast<size_t>(kDpInflightBatches) * local_max_);
+    });
   }
   void synchronize() override {
     std::unique_lock<std::mutex> lk(mu_);
@@ -181,6 +194,7 @@ class DpEngine : public Engine {
     s.sub_id = ++next_sub_;
     {
       std::lock_guard<std::mutex> g(mu_);
+      pending_items_ += static_cast<size_t>(B);
       pending_.emplace(s.sub_id, std::move(pd));
     }
     subs_sent_++;
@@ -324,6 +338,7 @@ class DpEngine : public Engine {
       auto it = pending_.find(ref.sub_id);
       if (it == pending_.end()) return;
       pd = std::move(it->second);
+      pending_items_ -= static_cast<size_t>(pd.n);
       pending_.erase(it);
     }
     BatchResult o;
@@ -352,6 +367,7 @@ class DpEngine : public Engine {
     {
       std::lock_guard<std::mutex> g(mu_);
       left.swap(pending_);
+      pending_items_ = 0;
     }
     for (auto& kv : left) {
       BatchResult r;
@@ -375,6 +391,7 @@ class DpEngine : public Engine {
   std::mutex submit_mu_, mu_;
   std::condition_variable cv_;
   std::map<uint32_t, Pending> pending_;
+  size_t pending_items_ = 0;  // requests in this rank's queued + in-flight sub-batches (guarded by mu_)
   uint32_t next_sub_ = 0;
   std::atomic<bool> stop_{false};
   std::thread dispatcher_, shard_thread_;

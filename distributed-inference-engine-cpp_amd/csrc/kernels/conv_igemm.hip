@@ -485,7 +485,10 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   constexpr int A_ELEMS = BN * BKS, B_ELEMS = BM * BKS, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
   constexpr int GA = BN / 4 / RPI, GB = BM / 4 / RPI, G = NP * (GA + GB);  // DMA instructions per wave per stage
   constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
+  // One LDS array: the stage ring / epilogue tile, then (BNL) the channel table.  No separate
+  // dummy arrays: a 1-stage split 64x64 block is exactly 32 KiB.
+  constexpr int BNL_ELEMS = BNL ? 2 * 2 * kBnlMaxK : 0;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS + BNL_ELEMS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const int kt_end = min(nk_total, kt_begin + kt_per_split * KR);
   const int nk = kt_end - kt_begin;
   // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
-  __shared__ __attribute__((aligned(16))) float bnl[BNL ? 2 * kBnlMaxK : 4];
+  float* bnl = reinterpret_cast<float*>(lds + LDS_ELEMS);  // BNL only: [scale | shift] x kBnlMaxK
   if constexpr (BNL) {
     for (int i = tid; i < nk * BKS; i += 256) {
       bnl[i] = p.in_scale[kt_begin * BKS + i];
@@ -557,6 +560,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     nx_kx = tap - nx_ky * p.KW;
   }
 
+  // DMA the K-step at the current state into stage `buf` and advance the state.
   auto issue = [&](int buf) {
     uint16_t* A = lds + buf * STAGE;
     uint16_t* Bt = A + A_ELEMS;
@@ -731,8 +735,9 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
     if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
     // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS); variant 5 =
-    // one stage, no ring.  (32-wide K-step rings, conv_glds_kernel<..., BKS = 32>, were measured
-    // as 2/3-stage variants and never beat the 1-stage 64-wide loop: profiles/r2_conv_sweep_fp32_b32.md)
+    // one stage, no ring.  (Measured and dropped: rings of 32-wide K-steps, conv_glds_kernel<...,
+    // BKS = 32>, at the 1-stage footprint, and a 1-stage loop that also touched the next K-step's
+    // lines toward L2 with 4-byte LDS-DMA loads: both slower, profiles/r2_feed_calibration.md.)
     constexpr int kStageBytes = (BM + BN) * BK * 2;
     if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
     // split stages are twice as large: 128x128 fits 2 stages, 64-wide tiles 3-4 (160 KiB LDS)

@@ -146,11 +146,14 @@ __global__ __launch_bounds__(256) void stem7x7_kernel(const uint16_t* __restrict
 // persistent: a block stages the weights in LDS ONCE and then walks output tiles (blockIdx.x,
 // + gridDim.x, ...), prefetching the next tile's patch into registers while the MFMAs of the
 // current one run.  The epilogue stores straight from the accumulators (8 bytes = 4 channels per
-// lane and plane) because the LDS holds the weights for the whole walk.
-constexpr int PPT = (PY * PX + 255) / 256;  // patch pixels per thread
+// lane and plane) because the LDS holds the weights for the whole walk.  8 waves per block (one
+// output row each) and 2 blocks per CU: 4 waves per SIMD to overlap one wave's patch staging and
+// stores with the others' MFMAs.
+constexpr int SNT = 512;                       // 8 waves: one output row of the tile each
+constexpr int PPT = (PY * PX + SNT - 1) / SNT;  // patch pixels per thread
 
 template <bool SPLIT>
-__global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __restrict__ x, int C,
+__global__ __launch_bounds__(SNT, 2) void stem7x7_nchw_kernel(const float* __restrict__ x, int C,
                                                              const float* __restrict__ in_scale,
                                                              const float* __restrict__ in_shift,
                                                              const uint16_t* __restrict__ w,
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __res
   const int nb = live ? min(B, static_cast<int>(*live)) : B;
   const int total = nb * tiles_per_img;
   if (static_cast<int>(blockIdx.x) >= total) return;  // whole block, before any barrier
-  for (int i = tid; i < NP * NCH * (KS / 8); i += 256) {
+  for (int i = tid; i < NP * NCH * (KS / 8); i += SNT) {
     const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
     const int r = q / (KS / 8), c = q % (KS / 8);
     *reinterpret_cast<uint4*>(wl + pl * NCH * WP + r * WP + c * 8) =
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __res
     const float* xb = x + static_cast<size_t>(b) * C * HW;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-      const int q = tid + k * 256;
+      const int q = tid + k * SNT;
       const int py = q / PX, px = q - (q / PX) * PX;
       const int iy = iy0 + py, ix = ix0 + px;
       inb[k] = q < PY * PX && iy >= 0 && iy < H && ix >= 0 && ix < W;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __res
     __syncthreads();  // weights staged / every wave done reading the previous tile's patch
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-      const int q = tid + k * 256;
+      const int q = tid + k * SNT;
       if (q >= PY * PX) continue;
       float v[4];
 #pragma unroll
@@ -220,43 +223,34 @@ __global__ __launch_bounds__(256, 2) void stem7x7_nchw_kernel(const float* __res
     __syncthreads();
     const int tn = t + static_cast<int>(gridDim.x);
     if (tn < total) fetch(tn);  // in flight during this tile's MFMAs
-    f32x4 acc[4][2];
+    f32x4 acc[4][1];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int m = 0; m < 2; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < 4; ++n) acc[n][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ky = 0; ky < 7; ++ky) {
-      bf16x8 bf[NP][2];
+      bf16x8 bf[NP][1];
 #pragma unroll
-      for (int pl = 0; pl < NP; ++pl)
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const int py = 2 * (2 * wave + m) + ky, px = 2 * px_l + 2 * j;
-          bf[pl][m] = *reinterpret_cast<const bf16x8*>(patch + pl * PY * PX * 4 + (py * PX + px) * 4);
-        }
+      for (int pl = 0; pl < NP; ++pl) {
+        const int py = 2 * wave + ky, px = 2 * px_l + 2 * j;
+        bf[pl][0] = *reinterpret_cast<const bf16x8*>(patch + pl * PY * PX * 4 + (py * PX + px) * 4);
+      }
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const int wo = (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8;
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + wo);
         if constexpr (SPLIT) {
           const bf16x8 al = *reinterpret_cast<const bf16x8*>(wl + NCH * WP + wo);
-#pragma unroll
-          for (int m = 0; m < 2; ++m) {
-            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf[0][m], acc[n][m], 0, 0, 0);
-            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[NP - 1][m], acc[n][m], 0, 0, 0);
-          }
+          acc[n][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf[0][0], acc[n][0], 0, 0, 0);
+          acc[n][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[NP - 1][0], acc[n][0], 0, 0, 0);
         }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[0][m], acc[n][m], 0, 0, 0);
+        acc[n][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[0][0], acc[n][0], 0, 0, 0);
       }
     }
     const int b = t / tiles_per_img, tt = t - b * tiles_per_img;
     const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int oy = ty0 + 2 * wave + m, ox = tx0 + px_l;
-      if (oy >= Ho || ox >= Wo) continue;
+    constexpr int m = 0;
+    const int oy = ty0 + wave, ox = tx0 + px_l;
+    if (oy < Ho && ox < Wo) {
       uint16_t* o = out + ((static_cast<size_t>(b) * Ho + oy) * Wo + ox) * NCH;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
@@ -312,10 +306,10 @@ hipError_t conv_stem7x7_nchw(const float* x, int C, const float* in_scale, const
   int grid = std::min(B * per_img, max_blocks > 0 ? max_blocks : 2 * cus);  // 2 blocks (72 KiB LDS each) per CU
   grid = std::max(grid, 1);
   if (split)
-    hipLaunchKernelGGL(stem7x7_nchw_kernel<true>, dim3(grid), dim3(256), 0, s, x, C, in_scale, in_shift, w, bias, out, B,
+    hipLaunchKernelGGL(stem7x7_nchw_kernel<true>, dim3(grid), dim3(SNT), 0, s, x, C, in_scale, in_shift, w, bias, out, B,
                        H, W, Ho, Wo, relu, tiles_x, per_img, live);
   else
-    hipLaunchKernelGGL(stem7x7_nchw_kernel<false>, dim3(grid), dim3(256), 0, s, x, C, in_scale, in_shift, w, bias, out,
+    hipLaunchKernelGGL(stem7x7_nchw_kernel<false>, dim3(grid), dim3(SNT), 0, s, x, C, in_scale, in_shift, w, bias, out,
                        B, H, W, Ho, Wo, relu, tiles_x, per_img, live);
   return hipGetLastError();
 }

@@ -30,8 +30,8 @@ constexpr int kDpMaxRanks = 16;
 constexpr int kDpMaxItems = 2048;  // requests per DP batch
 constexpr int kDpRing = 4;         // batch descriptors in flight
 constexpr int kDpSubMax = 256;     // requests per sub-batch (one rank's local batch)
-constexpr int kDpSubRing = 8;      // sub-batches queued per rank
-constexpr int kDpMaxSubs = 64;     // sub-batches merged into one DP batch
+constexpr int kDpSubRing = 32;     // sub-batches queued per rank (a rank pushes whatever it has, eagerly)
+constexpr int kDpMaxSubs = 256;    // sub-batches merged into one DP batch
 
 struct DpItem {
   uint64_t off = 0;  // byte offset of the item's buffer in the arena
