@@ -1,0 +1,770 @@
+// Implicit-GEMM conv kernels and their launcher template (included by the per-tile translation
+// units conv_tile_*.hip, which instantiate one tile shape each so the build runs them in parallel).
+// Design notes: conv_igemm.hip.
+#pragma once
+
+#include "common.h"
+#include "kernels.h"
+
+namespace die {
+namespace kern {
+namespace igemm {
+namespace {  // internal linkage: each conv_tile_*.hip gets its own copy of what it instantiates
+
+using namespace die::k;
+
+
+constexpr int BK = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+// Epilogue activation: 1 = ReLU, 2 = exact (erf) GELU, 3 = Clip(lo, hi).
+__device__ __forceinline__ float act_fn(float v, int act, float lo = 0.f, float hi = 0.f) {
+  if (act == 3) return fminf(fmaxf(v, lo), hi);
+  return act == 1 ? fmaxf(v, 0.f) : 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
+// fp32 mode (p.split): the residual is read as hi + lo and out/out2 are stored as split planes.
+__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
+  const size_t o = static_cast<size_t>(m) * p.N + n;
+  const bool split = p.split != 0;
+  if (p.bias) {
+    const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (p.res) {
+    float r[8];
+    load8v(p.res + o, p.oplane, split, r);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] += r[t];
+  }
+  if (p.relu) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu, p.clip_lo, p.clip_hi);
+  }
+  if (p.out) store8v(p.out + o, p.oplane, split, v);
+  if (p.out_f32) {
+    *reinterpret_cast<float4*>(p.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p.out_f32 + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  if (p.out2) {
+    const float4 s0 = ldf4(p.scale2 + n), s1 = ldf4(p.scale2 + n + 4);
+    const float4 h0 = ldf4(p.shift2 + n), h1 = ldf4(p.shift2 + n + 4);
+    float u[8] = {v[0] * s0.x + h0.x, v[1] * s0.y + h0.y, v[2] * s0.z + h0.z, v[3] * s0.w + h0.w,
+                  v[4] * s1.x + h1.x, v[5] * s1.y + h1.y, v[6] * s1.z + h1.z, v[7] * s1.w + h1.w};
+    if (p.relu2) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) u[t] = fmaxf(u[t], 0.f);
+    }
+    store8v(p.out2 + o, p.oplane, split, u);
+  }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split);
+
+// XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
+// id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
+// tile = blockIdx.x spreads the N-tiles of one M-tile (same activation rows) or the M-tiles of
+// one N-tile (same weight rows) over 8 L2s.  The bijective remap gives every XCD a contiguous range
+// of logical ids; a tile's split-K slices are adjacent (same XCD for the fused reducer), and tiles
+// are ordered so the operand with more bytes is the one shared within an XCD: N-fastest (an
+// M-tile's activations read once per XCD, every XCD reads all weights) when weights are the
+// smaller operand (N <= M), M-fastest otherwise (stage-4 / FC shapes with M < N).
+// With a live batch (ConvArgs::live) only the tiles holding real samples get work: the first
+// live_tiles * S blocks (spread evenly over the XCDs) are remapped over them and the rest exit.
+// Returns false for a block without work.
+__device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
+                                             int& tile) {
+  const int S = gridDim.y;  // split-K slices
+  const int ntn = (p.N + BN - 1) / BN;
+  const int Ml = p.live ? min(p.M, static_cast<int>(*p.live) * p.Ho * p.Wo) : p.M;
+  const int ntm = (Ml + BM - 1) / BM;
+  const int nwg = min(static_cast<int>(gridDim.x * gridDim.y), ntm * ntn * S);
+  const int b = blockIdx.x + blockIdx.y * gridDim.x;
+  if (b >= nwg) return false;
+  const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  tile = id / S;
+  split = id - tile * S;
+  if (p.N <= p.M) {
+    tile_m = tile / ntn;
+    tile_n = tile - tile_m * ntn;
+  } else {
+    tile_n = tile / ntm;
+    tile_m = tile - tile_n * ntm;
+  }
+  return true;
+}
+
+// Register-staged main loop (any shape).  SPLIT (fp32 mode): both operands come as hi/lo planes, a
+// stage holds four tiles [A_hi][B_hi][A_lo][B_lo] and every fragment pair takes three MFMAs.
+template <int BM, int BN, int MODE, int VEC, bool SPLIT = false>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const int kt_per_split) {
+  constexpr int NP = SPLIT ? 2 : 1;                   // operand planes
+  constexpr int WM = BM / 2, WN = BN / 2;  // per-wave pixels / channels
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_ELEMS = BN * BK, B_ELEMS = BM * BK, STAGE = A_ELEMS + B_ELEMS;
+  constexpr int W_CH = BN / 32;                       // 16-B weight chunks per thread per stage
+  constexpr int X_CH = VEC == 8 ? BM / 32 : BM / 16;  // activation units per thread per stage
+  static_assert(2 * STAGE * NP * 2 >= BM * BN * 4, "epilogue staging must fit in the operand LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE * NP];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  int tile_m, tile_n, split, tile;
+  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk_total = p.Kpad / BK;
+  const int kt_begin = split * kt_per_split;
+  const int kt_end = min(nk_total, kt_begin + kt_per_split);
+
+  // ---- per-thread loader state ----
+  const int wc = tid & 7;
+  const int wr = tid >> 3;
+  const uint16_t* wsrc = p.w + static_cast<size_t>(n0 + wr) * p.Kpad + wc * 8;
+
+  constexpr int XC_SHIFT = VEC == 8 ? 3 : 4;  // threads per row
+  const int xc = tid & ((1 << XC_SHIFT) - 1);
+  const int xr = tid >> XC_SHIFT;
+  constexpr int XR_STEP = 256 >> XC_SHIFT;
+  bool mvalid[X_CH];
+  int ih0[X_CH], iw0[X_CH];
+  size_t xbase[X_CH];
+#pragma unroll
+  for (int i = 0; i < X_CH; ++i) {
+    const int m = m0 + xr + XR_STEP * i;
+    mvalid[i] = m < p.M;
+    const int mm = mvalid[i] ? m : 0;
+    if (MODE == 0) {
+      xbase[i] = static_cast<size_t>(mm) * p.Cin;
+      ih0[i] = iw0[i] = 0;
+    } else {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int r = mm - b * hw;
+      const int oh = r / p.Wo;
+      const int ow = r - oh * p.Wo;
+      ih0[i] = oh * p.stride - p.pad_h;
+      iw0[i] = ow * p.stride - p.pad_w;
+      xbase[i] = static_cast<size_t>(b) * p.H * p.W * p.Cin;
+    }
+  }
+
+  uint4 wreg[NP][W_CH];
+  uint4 xreg8[NP][VEC == 8 ? X_CH : 1];
+  uint2 xreg4[NP][VEC == 4 ? X_CH : 1];
+
+  auto load_stage = [&](int k0) {
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i)
+        wreg[pl][i] = *reinterpret_cast<const uint4*>(wsrc + pl * p.wplane + static_cast<size_t>(32 * i) * p.Kpad + k0);
+    const int kk = k0 + xc * VEC;
+    bool kvalid = kk < p.K;
+    int off = 0, ky = 0, kx = 0;
+    if (MODE == 0) {
+      off = kk;
+    } else if (kvalid) {
+      const int t = kk / p.Cin;
+      const int ci = kk - t * p.Cin;
+      ky = t / p.KW;
+      kx = t - ky * p.KW;
+      off = ci;
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      bool v = kvalid && mvalid[i];
+      size_t addr = xbase[i] + off;
+      if (MODE == 1) {
+        const int ih = ih0[i] + ky * p.dil;
+        const int iw = iw0[i] + kx * p.dil;
+        v = v && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        addr += (static_cast<size_t>(ih) * p.W + iw) * p.Cin;
+      }
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        const uint16_t* src = p.x + addr + pl * p.xplane;
+        if (VEC == 8) {
+          xreg8[pl][i] = v ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        } else {
+          xreg4[pl][i] = v ? *reinterpret_cast<const uint2*>(src) : make_uint2(0, 0);
+        }
+      }
+    }
+  };
+
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      uint16_t* A = lds + (buf * NP + pl) * STAGE;
+      uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i) *reinterpret_cast<uint4*>(A + swz(wr + 32 * i, wc)) = wreg[pl][i];
+#pragma unroll
+      for (int i = 0; i < X_CH; ++i) {
+        const int row = xr + XR_STEP * i;
+        if (VEC == 8) {
+          *reinterpret_cast<uint4*>(Bt + swz(row, xc)) = xreg8[pl][i];
+        } else {
+          *reinterpret_cast<uint2*>(Bt + swz(row, xc >> 1) + 4 * (xc & 1)) = xreg4[pl][i];
+        }
+      }
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt_begin < kt_end) {
+    load_stage(kt_begin * BK);
+    store_stage(0);
+    __syncthreads();
+  }
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_begin) & 1;
+    const bool more = kt + 1 < kt_end;
+    if (more) load_stage((kt + 1) * BK);  // in flight under the MFMAs below
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int chunk = s * 4 + (lane >> 4);
+      bf16x8 af[NP][TN], bfr[NP][TM];
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        const uint16_t* A = lds + (cur * NP + pl) * STAGE;
+        const uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          af[pl][i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * WN + i * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          bfr[pl][j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wm * WM + j * 16 + (lane & 15), chunk));
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          if constexpr (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[1][j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (more) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
+}
+
+// Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
+// past their last operand read).
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int lm = lane & 15;
+  const int ln = (lane >> 4) * 4;
+  if ((p.N & 7) == 0) {
+    // ---- LDS-staged, coalesced epilogue ----
+    constexpr int CPR = BN / 4;  // 16-B chunks per staged row
+    float* st = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int row = wm * WM + j * 16 + lm;
+        const int c = (wn * WN + i * 16 + ln) >> 2;
+        *reinterpret_cast<f32x4*>(st + row * BN + ((c ^ (row & (CPR - 1))) << 2)) = acc[i][j];
+      }
+    __syncthreads();
+    constexpr int GPR = BN / 8;
+    const bool partial = p.splits > 1;
+    float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
+    for (int g = tid; g < BM * GPR; g += 256) {
+      const int row = g / GPR;
+      const int cg = g - row * GPR;
+      const int m = m0 + row;
+      const int n = n0 + cg * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float4 a = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg) ^ (row & (CPR - 1))) << 2));
+      const float4 b = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg + 1) ^ (row & (CPR - 1))) << 2));
+      if (partial) {
+        float* o = ws + static_cast<size_t>(m) * p.N + n;
+        *reinterpret_cast<float4*>(o) = a;
+        *reinterpret_cast<float4*>(o + 4) = b;
+      } else {
+        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        epilogue8(p, m, n, v);
+      }
+    }
+    if (!partial || !p.counters) return;
+    // Fused split-K reduction: the last split block of this tile to arrive sums every split's
+    // partial and runs the epilogue (no second kernel).  Hand-off per the agent-scope recipe
+    // (cdna_hip_programming §6 G16): every wave drains its slab stores, block barrier, ONE lane
+    // releases at agent scope and takes a ticket; the reducer's lane acquires at agent scope (which
+    // invalidates this CU's L1) before the barrier that precedes the plain slab loads.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);  // staging tile is dead now: reuse it for the broadcast
+    if (tid == 0) {
+      int* ctr = p.counters + tile;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == p.splits - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const size_t slab = static_cast<size_t>(p.M) * p.N;
+    for (int g = tid; g < BM * GPR; g += 256) {
+      const int row = g / GPR;
+      const int cg = g - row * GPR;
+      const int m = m0 + row;
+      const int n = n0 + cg * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int s = 0; s < p.splits; ++s) {
+        const float4 a = ldf4(src + s * slab), b = ldf4(src + s * slab + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      epilogue8(p, m, n, v);
+    }
+    return;
+  }
+  // ---- ragged N (e.g. a 10-class head): element-wise epilogue from registers ----
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn * WN + i * 16 + ln;
+    if (n >= p.N) continue;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + lm;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (n + r >= p.N) break;
+        const size_t o = static_cast<size_t>(m) * p.N + n + r;
+        float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
+        if (p.res) v += load1v(p.res + o, p.oplane, p.split);
+        if (p.relu) v = act_fn(v, p.relu, p.clip_lo, p.clip_hi);
+        if (p.out) store1v(p.out + o, p.oplane, p.split, v);
+        if (p.out_f32) p.out_f32[o] = v;
+        if (p.out2) {
+          float u = v * p.scale2[n + r] + p.shift2[n + r];
+          if (p.relu2) u = fmaxf(u, 0.f);
+          store1v(p.out2 + o, p.oplane, p.split, u);
+        }
+      }
+    }
+  }
+}
+
+// Sum the split-K partials and apply the epilogue; one thread per 8 channels of one pixel.
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
+  const int GPR = p.N / 8;
+  const long long total = static_cast<long long>(p.M) * GPR;
+  const size_t slab = static_cast<size_t>(p.M) * p.N;
+  for (long long g = blockIdx.x * 256ll + threadIdx.x; g < total; g += static_cast<long long>(gridDim.x) * 256) {
+    const int m = static_cast<int>(g / GPR);
+    const int n = static_cast<int>(g - static_cast<long long>(m) * GPR) * 8;
+    const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < p.splits; ++s) {
+      const float4 a = ldf4(src + s * slab), b = ldf4(src + s * slab + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    epilogue8(p, m, n, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// v3 main loop: operands stream global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging,
+// no ds_write), STAGES-deep ring with a counted `s_waitcnt vmcnt(N)` and a raw s_barrier per K-step,
+// so STAGES-1 K-steps stay in flight across the barrier.  The DMA writes 1 KiB per wave-instruction
+// lane-linearly (8 rows x 128 B), so the (row>>1)&7 chunk swizzle goes on the per-lane SOURCE
+// address.  Padding pixels and M tails read a zero page instead of being predicated.
+// MODE 0: dense rows (1x1/s1 conv, GEMM), K % 64 == 0.  MODE 2: implicit conv with Cin % 64 == 0
+// (one 64-channel K-step never straddles a filter tap, so the tap is wave-uniform per K-step).
+// ------------------------------------------------------------------------------------------------
+// s_waitcnt with only the vector-memory counter constrained (gfx9 simm16: vmcnt = bits 3:0 + 15:14,
+// expcnt 6:4 and lgkmcnt 11:8 left at their maxima).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Wait until at most j*G of this wave's DMA instructions are outstanding, j <= J (j wave-uniform).
+template <int G, int J>
+__device__ __forceinline__ void wait_stages(int j) {
+  if constexpr (J == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (j >= J) wait_vmcnt<G * J>();
+    else wait_stages<G, J - 1>(j);
+  }
+}
+
+__device__ __forceinline__ void glds16(const uint16_t* g, uint16_t* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// 8 bf16 (one MFMA operand fragment, 8 consecutive channels) -> act(v * s + h), re-rounded to bf16.
+__device__ __forceinline__ bf16x8 bn_act8(bf16x8 f, float4 s0, float4 s1, float4 h0, float4 h1, int relu) {
+  const uint4 q = __builtin_bit_cast(uint4, f);
+  float v[8];
+  unpack2(q.x, v[0], v[1]);
+  unpack2(q.y, v[2], v[3]);
+  unpack2(q.z, v[4], v[5]);
+  unpack2(q.w, v[6], v[7]);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    v[t] = fmaf(v[t], sc[t], sh[t]);
+    if (relu) v[t] = fmaxf(v[t], 0.f);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])));
+}
+
+constexpr int kBnlMaxK = 2048;  // pre-activation on load: channels staged in LDS
+
+// SPLIT (fp32 mode): each stage holds [A_hi][B_hi][A_lo][B_lo]; the lo tiles are DMA'd from the
+// planes wplane / xplane elements after the hi ones (zero-page rows stay zero-page), and every
+// fragment pair takes three MFMAs (hi*hi + lo*hi + hi*lo).
+template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false, int BKS = BK>
+__global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
+  static_assert(BKS == 64 || BKS == 32, "K-step width");
+  constexpr int CPR = BKS / 8;        // 16-byte chunks per LDS row
+  constexpr int RPI = 512 / BKS;      // rows per 1 KiB DMA wave-instruction
+  constexpr int KSUB = BKS / 32;      // MFMA K=32 substeps per K-step
+  constexpr int KR = BK / BKS;        // K-steps per 64-wide split-K unit
+  auto sw = [](int row, int chunk) { return row * BKS + ((chunk ^ ((row >> 1) & (CPR - 1))) << 3); };
+  constexpr int NP = SPLIT ? 2 : 1;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_ELEMS = BN * BKS, B_ELEMS = BM * BKS, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
+  constexpr int GA = BN / 4 / RPI, GB = BM / 4 / RPI, G = NP * (GA + GB);  // DMA instructions per wave per stage
+  constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
+  // One LDS array: the stage ring / epilogue tile, then (BNL) the channel table.  No separate
+  // dummy arrays: a 1-stage split 64x64 block is exactly 32 KiB.
+  constexpr int BNL_ELEMS = BNL ? 2 * 2 * kBnlMaxK : 0;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS + BNL_ELEMS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  int tile_m, tile_n, split, tile;
+  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk_total = p.Kpad / BKS;
+  const int kt_begin = split * kt_per_split * KR;  // kt_per_split counts 64-wide K-steps
+  const int kt_end = min(nk_total, kt_begin + kt_per_split * KR);
+  const int nk = kt_end - kt_begin;
+  // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
+  float* bnl = reinterpret_cast<float*>(lds + LDS_ELEMS);  // BNL only: [scale | shift] x kBnlMaxK
+  if constexpr (BNL) {
+    for (int i = tid; i < nk * BKS; i += 256) {
+      bnl[i] = p.in_scale[kt_begin * BKS + i];
+      bnl[kBnlMaxK + i] = p.in_shift[kt_begin * BKS + i];
+    }
+    // visible to every wave after the main loop's first barrier
+  }
+
+  // Per-lane DMA sources.  Wave `wave` fills rows [wave*R/4, (wave+1)*R/4) of each operand, 8 rows
+  // per instruction (16 for 32-wide K-steps); lane L -> row L / CPR of that group, physical chunk L % CPR.
+  const uint16_t* asrc[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int r = wave * (BN / 4) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
+    asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
+  }
+  // MODE 0: each lane's row pointer, M-tail rows pointed into the zero page (which holds a whole
+  // K row), so a K-step is one pointer add.  MODE 2: image base + channel chunk and the output
+  // pixel's top-left input coordinate; taps advance incrementally (no divisions in the loop).
+  const uint16_t* bsrc[GB];
+  int bih[GB], biw[GB];
+  bool bval[GB];
+  long long bdel[GB];  // SPLIT, MODE 0: distance to the lo plane (0 for zero-page tail rows)
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int r = wave * (BM / 4) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
+    const int m = m0 + r;
+    bval[i] = m < p.M;
+    bdel[i] = bval[i] ? p.xplane : 0;
+    const int mm = bval[i] ? m : 0;
+    if (MODE == 0) {
+      bsrc[i] = (bval[i] ? p.x + static_cast<size_t>(mm) * p.Cin : p.zeros) + c * 8;
+      bih[i] = biw[i] = 0;
+    } else {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int rr = mm - b * hw;
+      const int oh = rr / p.Wo;
+      const int ow = rr - oh * p.Wo;
+      bih[i] = bval[i] ? oh * p.stride - p.pad_h : -(1 << 20);  // tail rows never pass the bounds test
+      biw[i] = ow * p.stride - p.pad_w;
+      bsrc[i] = p.x + static_cast<size_t>(b) * p.H * p.W * p.Cin + c * 8;
+    }
+  }
+  // uniform state of the next K-step to issue (MODE 2: channel offset within the tap, tap x/y)
+  int nx_k0 = kt_begin * BKS;
+  int nx_ci0 = 0, nx_kx = 0, nx_ky = 0;
+  if (MODE == 2) {
+    const int cpt = p.Cin / BKS;  // K-steps per filter tap
+    const int tap = kt_begin / cpt;
+    nx_ci0 = (kt_begin - tap * cpt) * BKS;
+    nx_ky = tap / p.KW;
+    nx_kx = tap - nx_ky * p.KW;
+  }
+
+  // DMA the K-step at the current state into stage `buf` and advance the state.
+  auto issue = [&](int buf) {
+    uint16_t* A = lds + buf * STAGE;
+    uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) glds16(asrc[i] + nx_k0, A + (wave * (BN / 4) + i * RPI) * BKS);
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < GA; ++i) glds16(asrc[i] + p.wplane + nx_k0, A + PLANE + (wave * (BN / 4) + i * RPI) * BKS);
+    }
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * RPI) * BKS);
+        if constexpr (SPLIT) glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
+      }
+    } else {
+      const int dy = nx_ky * p.dil, dx = nx_kx * p.dil;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int ih = bih[i] + dy;
+        const int iw = biw[i] + dx;
+        const bool v = static_cast<unsigned>(ih) < static_cast<unsigned>(p.H) &&
+                       static_cast<unsigned>(iw) < static_cast<unsigned>(p.W);
+        const uint16_t* src = v ? bsrc[i] + ((ih * p.W + iw) * p.Cin + nx_ci0) : p.zeros;
+        glds16(src, Bt + (wave * (BM / 4) + i * RPI) * BKS);
+        if constexpr (SPLIT) glds16(v ? src + p.xplane : p.zeros, Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
+      }
+      nx_ci0 += BKS;
+      if (nx_ci0 == p.Cin) {
+        nx_ci0 = 0;
+        if (++nx_kx == p.KW) {
+          nx_kx = 0;
+          ++nx_ky;
+        }
+      }
+    }
+    nx_k0 += BKS;
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // One K-step's MFMAs on the stage at A (K-step t of this slice, for the BNL channel table).
+  auto compute = [&](const uint16_t* A, int t) {
+    const uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+    for (int s = 0; s < KSUB; ++s) {
+      const int chunk = s * 4 + (lane >> 4);
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(A + sw(wn * WN + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + sw(wm * WM + j * 16 + (lane & 15), chunk));
+      if constexpr (SPLIT) {
+        bf16x8 afl[TN], bfl[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          afl[i] = *reinterpret_cast<const bf16x8*>(A + PLANE + sw(wn * WN + i * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          bfl[j] = *reinterpret_cast<const bf16x8*>(Bt + PLANE + sw(wm * WM + j * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+          }
+      }
+      if constexpr (BNL) {
+        const float* sc = bnl + t * BKS + chunk * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sc + kBnlMaxK);
+        const float4 h1 = *reinterpret_cast<const float4*>(sc + kBnlMaxK + 4);
+#pragma unroll
+        for (int j = 0; j < TM; ++j) bfr[j] = bn_act8(bfr[j], s0, s1, h0, h1, p.in_relu);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (STAGES == 1) {
+    // No ring: load, wait, compute, once per K-step.  Meant for nk == 1 (K <= 64: the expand /
+    // reduce convs of stage 1), where a ring buys nothing and a 1-stage LDS footprint lets 2-4x
+    // more blocks share a CU to hide the load and epilogue latency.
+    for (int t = 0; t < nk; ++t) {
+      if (t) __syncthreads();  // everyone done reading the previous K-step
+      issue(0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(lds, t);
+    }
+  } else {
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nk) issue(s);
+    int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
+    for (int t = 0; t < nk; ++t) {
+      // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
+      // instructions each) are outstanding.
+      wait_stages<G, STAGES - 2>(nk - 1 - t);
+      __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
+      asm volatile("" ::: "memory");
+      if (t + STAGES - 1 < nk) issue(wr);
+      wr = wr + 1 == STAGES ? 0 : wr + 1;
+      const uint16_t* A = lds + rd * STAGE;
+      rd = rd + 1 == STAGES ? 0 : rd + 1;
+      compute(A, t);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // all operand reads done before the epilogue reuses the LDS
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
+}
+
+template <int BM, int BN, int STAGES, int BKS = BK>
+void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
+  if (b.split) {  // only ring depths whose doubled stages fit the LDS are instantiated
+    if constexpr (STAGES * (BM + BN) * BKS * 4 <= 160 * 1024) {
+      if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
+      else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
+    }
+  } else if (b.in_scale) {
+    if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, true, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+    else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, true, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+  } else if (mode0) {
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+  } else {
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+  }
+}
+
+template <int BM, int BN>
+hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
+  const bool dense1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
+                        a.W == a.Wo;
+  const int vec = a.Cin % 8 == 0 ? 8 : 4;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int nk = a.Kpad / BK;
+  const int splits = std::max(1, std::min(a.splits, nk));
+  const int kt_per = (nk + splits - 1) / splits;
+  const int eff = (nk + kt_per - 1) / kt_per;  // no empty slices
+  ConvArgs b = a;
+  b.splits = eff;
+  if (a.split) {  // plane distances of the split activations (weights: set by the planner)
+    b.xplane = static_cast<long long>(a.B) * a.H * a.W * a.Cin;
+    b.oplane = static_cast<long long>(a.M) * a.N;
+    if (a.wplane <= 0 || a.in_scale) return hipErrorInvalidValue;
+  } else {
+    b.xplane = b.oplane = 0;
+  }
+  // fused split-K reduction needs a zeroed counter per output tile
+  const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
+  if (!fused) b.counters = nullptr;
+  dim3 grid(tiles, eff);
+  if (a.in_scale) {  // pre-activation on load: 1x1 convs in the LDS-DMA loop only
+    if (a.KH != 1 || a.KW != 1 || a.pad_h || a.pad_w || a.K != a.Cin || a.K > kBnlMaxK || a.Cin % BK || !a.in_shift)
+      return hipErrorInvalidValue;
+    if (variant == 0) variant = 1;  // the register-staged loop has no pre-activation: 2-stage ring
+  }
+  if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
+    const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
+    const bool mode2 = !dense1x1 && a.Cin % BK == 0;
+    if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
+    // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS); variant 5 =
+    // one stage, no ring.  (Measured and dropped: rings of 32-wide K-steps, conv_glds_kernel<...,
+    // BKS = 32>, at the 1-stage footprint, and a 1-stage loop that also touched the next K-step's
+    // lines toward L2 with 4-byte LDS-DMA loads: both slower, profiles/r2_feed_calibration.md.)
+    constexpr int kStageBytes = (BM + BN) * BK * 2;
+    if (a.in_scale && variant == 4) return hipErrorInvalidValue;  // 6 stages + the channel table exceed the LDS
+    // split stages are twice as large: 128x128 fits 2 stages, 64-wide tiles 3-4 (160 KiB LDS)
+    const int np = a.split ? 2 : 1;
+    const int stages = variant == 1 ? 2 : variant == 2 ? 3 : variant == 3 ? 4 : variant == 4 ? 6 : 1;
+    if (stages * kStageBytes * np > 160 * 1024) return hipErrorInvalidValue;
+    switch (variant) {
+      case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
+      case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;
+      case 3: launch_glds<BM, BN, 4>(mode0, grid, s, b, kt_per); break;
+      case 5: launch_glds<BM, BN, 1>(mode0, grid, s, b, kt_per); break;
+      default:
+        if constexpr (6 * kStageBytes <= 160 * 1024) launch_glds<BM, BN, 6>(mode0, grid, s, b, kt_per);
+        else return hipErrorInvalidValue;
+    }
+  } else if (a.split) {
+    if (dense1x1 && vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8, true>), grid, dim3(256), 0, s, b, kt_per);
+    else if (vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8, true>), grid, dim3(256), 0, s, b, kt_per);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4, true>), grid, dim3(256), 0, s, b, kt_per);
+  } else if (dense1x1 && vec == 8) {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8>), grid, dim3(256), 0, s, b, kt_per);
+  } else if (vec == 8) {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8>), grid, dim3(256), 0, s, b, kt_per);
+  } else {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4>), grid, dim3(256), 0, s, b, kt_per);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || eff == 1 || fused) return e;
+  const long long groups = static_cast<long long>(b.M) * (b.N / 8);
+  const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+
+}  // namespace
+
+// One launcher per tile shape, defined in conv_tile_<BM>x<BN>.hip.
+hipError_t launch_tile_128x128(const ConvArgs& a, hipStream_t s, int variant);
+hipError_t launch_tile_128x64(const ConvArgs& a, hipStream_t s, int variant);
+hipError_t launch_tile_64x128(const ConvArgs& a, hipStream_t s, int variant);
+hipError_t launch_tile_64x64(const ConvArgs& a, hipStream_t s, int variant);
+
+}  // namespace igemm
+}  // namespace kern
+}  // namespace die

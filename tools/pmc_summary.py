@@ -36,7 +36,8 @@ def load(pass_dir):
                                                      "agpr": int(r["Accum_VGPR_Count"]), "lds": int(r["LDS_Block_Size"])})
         d["c"][r["Counter_Name"]] += float(r["Counter_Value"])
     seq = [v for _, v in sorted(disp.items()) if "die::kern" in v["name"]]
-    start = max(i for i, v in enumerate(seq) if "input_prep" in v["name"])
+    # the forward starts at its input pass: input_prep, or the stem that fused it
+    start = max(i for i, v in enumerate(seq) if "input_prep" in v["name"] or "stem7x7_nchw" in v["name"])
     return seq[start:]
 
 
