@@ -62,7 +62,7 @@ def main():
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
     ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
-    ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--pipeline-depth", type=int, default=3)
     ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
     ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")

@@ -42,7 +42,7 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
   eo.device = f.str("device", "hip");
   eo.device_id = static_cast<int>(f.i("device-id", 0));
   eo.max_batch = static_cast<int>(f.i("max-batch", 32));
-  eo.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 2));
+  eo.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 3));
   eo.use_graphs = !f.b("no-graphs");
   eo.device_decode = !f.b("no-device-decode");
   eo.dp_group = f.str("dp-group", "");
@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
               << "  --cache-capacity N (1000)  --max-batch N (32)  --batch-timeout-ms N (20)\n"
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
-              << "  --pipeline-depth N (2)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
+              << "  --pipeline-depth N (3)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --http-threads N  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
               << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
@@ -131,7 +131,7 @@ int main(int argc, char** argv) {
   o.engine.device = f.str("device", "auto");
   o.engine.device_id = static_cast<int>(f.i("device-id", 0));
   o.engine.precision = f.str("precision", "fp32");
-  o.engine.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 2));
+  o.engine.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 3));
   o.engine.use_graphs = !f.b("no-graphs");
   o.engine.device_decode = !f.b("no-device-decode");
   o.engine.stage_slots = static_cast<int>(f.i("stage-slots", 0));

@@ -164,7 +164,7 @@ struct EngineOptions {
   std::string device = "auto";   // auto | cpu | hip
   int device_id = 0;             // HIP device ordinal
   int max_batch = 32;
-  int pipeline_depth = 2;        // batches in flight (HIP)
+  int pipeline_depth = 3;        // batches in flight (HIP); 3 measured +2-4 % over 2 on the fp32 headline
   int exec_streams = 1;          // of those, batches executing concurrently (HIP; 1 = serialised)
   bool use_graphs = true;        // hipGraph per batch bucket (HIP)
   bool autotune = true;          // time (tile, split-K) candidates per conv at start-up (HIP)

@@ -74,8 +74,8 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
 // one N-tile (same weight rows) over 8 L2s.  The bijective remap gives every XCD a contiguous range
 // of logical ids; a tile's split-K slices are adjacent (same XCD for the fused reducer), and tiles
 // are ordered so the operand with more bytes is the one shared within an XCD: N-fastest (an
-// M-tile's activations read once per XCD, every XCD reads all weights) when weights are the
-// smaller operand (N <= M), M-fastest otherwise (stage-4 / FC shapes with M < N).
+// M-tile's activations read once per XCD, every XCD reads all weights) when the weights are the
+// smaller operand, M-fastest otherwise (stage-4 3x3 / expand / FC shapes).
 // With a live batch (ConvArgs::live) only the tiles holding real samples get work: the first
 // live_tiles * S blocks (spread evenly over the XCDs) are remapped over them and the rest exit.
 // Returns false for a block without work.
@@ -92,7 +92,12 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   tile = id / S;
   split = id - tile * S;
-  if (p.N <= p.M) {
+  // Replicate (read on every XCD) the operand with fewer bytes: the weights are N x K, the
+  // activations the INPUT tensor, B*H*W*Cin -- not the im2col M x K, which counts a 3x3 conv's
+  // input 9 times (stage-4 3x3 at batch 16-32: weights 4.7x the input, so M-fastest).
+  const long long wts = static_cast<long long>(p.N) * p.K;
+  const long long acts = static_cast<long long>(p.B) * p.H * p.W * p.Cin;
+  if (wts <= acts) {
     tile_m = tile / ntn;
     tile_n = tile - tile_m * ntn;
   } else {
