@@ -322,20 +322,23 @@ void WorkerNode::dispatch(Pending p, Responder res) {
                                        std::to_string(engine_->input_numel()), true));
       return;
     }
-    cache_.put(key, r->output);
     h_queue_.add(r->t_dispatch - t_queued);
     h_engine_.add(r->t_done - r->t_dispatch);
     auto out = std::make_shared<std::vector<float>>(std::move(r->output));
     const int64_t us = r->inference_time_us;
     std::string node = opt_.node_id;
     const auto t_done = r->t_done;
-    res.defer([this, out, id = std::move(id), node = std::move(node), us, t_start, t_done] {
+    // This callback runs once per request, in a row, on the batch's completion thread: keep it to a
+    // hand-off.  The JSON and the cache insert happen on the connection's reactor, in parallel
+    // over the reactors, after the response is built.
+    res.defer([this, out, key, id = std::move(id), node = std::move(node), us, t_start, t_done] {
       TraceRange tr_resp("worker.respond");
       HttpResponse resp;
       resp.body = build_response(id, out->data(), out->size(), node, false, us);
       const auto now = std::chrono::steady_clock::now();
       h_respond_.add(now - t_done);
       h_total_.add(now - t_start);
+      cache_.put(key, *out);
       return resp;
     });
   });
