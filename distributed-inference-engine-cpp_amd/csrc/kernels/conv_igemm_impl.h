@@ -3,6 +3,8 @@
 // Design notes: conv_igemm.hip.
 #pragma once
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -64,9 +66,16 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   }
 }
 
-template <int BM, int BN>
+// Row r of a tile -> output pixel m0 + r (GEMM rows are consecutive pixels); -1 = no pixel.
+struct LinearRows {
+  int m0, M;
+  __device__ __forceinline__ int operator()(int r) const { return m0 + r < M ? m0 + r : -1; }
+};
+
+template <int BM, int BN, typename RowMap = LinearRows>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split);
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
+                                              RowMap rows = RowMap{0, 0});
 
 // XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
 // id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
@@ -275,9 +284,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
 
 // Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
 // past their last operand read).
-template <int BM, int BN>
+template <int BM, int BN, typename RowMap>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split) {
+                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
+                                              RowMap rows) {
+  if constexpr (std::is_same_v<RowMap, LinearRows>) rows = LinearRows{m0, p.M};
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   const int lm = lane & 15;
@@ -301,9 +312,9 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     for (int g = tid; g < BM * GPR; g += 256) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
-      const int m = m0 + row;
+      const int m = rows(row);
       const int n = n0 + cg * 8;
-      if (m >= p.M || n >= p.N) continue;
+      if (m < 0 || n >= p.N) continue;
       const float4 a = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg) ^ (row & (CPR - 1))) << 2));
       const float4 b = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg + 1) ^ (row & (CPR - 1))) << 2));
       if (partial) {
@@ -343,9 +354,9 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     for (int g = tid; g < BM * GPR; g += 256) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
-      const int m = m0 + row;
+      const int m = rows(row);
       const int n = n0 + cg * 8;
-      if (m >= p.M || n >= p.N) continue;
+      if (m < 0 || n >= p.N) continue;
       const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
       float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int s = 0; s < p.splits; ++s) {
@@ -364,8 +375,8 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     if (n >= p.N) continue;
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * WM + j * 16 + lm;
-      if (m >= p.M) continue;
+      const int m = rows(wm * WM + j * 16 + lm);
+      if (m < 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (n + r >= p.N) break;
@@ -674,6 +685,160 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Spatially tiled 3x3 / stride 1 / pad 1 conv (Cin % 64 == 0), 64 output channels x an 8x8 pixel
+// tile per block.  The implicit-GEMM loop above reads one 64-channel row per output pixel per
+// filter tap, i.e. every input pixel ~9 times per N-tile; here a block stages the 10x10 input patch
+// of its tile once per 64-channel slice and serves all 9 taps from it (tap (dy, dx) = the patch
+// window shifted by (dy, dx)), so a slice costs one patch + 9 weight K-steps (~19 KB/tap in fp32
+// split mode instead of 32 KB).  One stage, no ring (the loop the tuner prefers at these sizes).
+// Patch LDS layout: pixel q = row * 10 + col, 128 B per pixel, 16-B chunk c stored at
+// c ^ g(col) ^ h(row): tables found by exhaustive search so that every ds_read_b128 lane group of
+// every (tap, fragment, K-half) hits 16 distinct bank slots.
+// Split-K runs over channel slices (kt_per_split counts slices here).
+constexpr uint32_t kPatchSwzCol = 0x37b77b77u, kPatchSwzRow = 0x1d5c7555u;
+__device__ __forceinline__ int patch_swz(int row, int col) {
+  return static_cast<int>(((kPatchSwzCol >> (3 * col)) ^ (kPatchSwzRow >> (3 * row))) & 7u);
+}
+
+struct SpatialRows {  // tile row r (8x8 pixel tile, raster) -> output pixel, -1 outside the image
+  int b, ty0, tx0, Ho, Wo;
+  __device__ __forceinline__ int operator()(int r) const {
+    const int oy = ty0 + (r >> 3), ox = tx0 + (r & 7);
+    return oy < Ho && ox < Wo ? (b * Ho + oy) * Wo + ox : -1;
+  }
+};
+
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void conv3x3_spatial_kernel(const ConvArgs p, const int sl_per_split) {
+  constexpr int BM = 64, BN = 64, NP = SPLIT ? 2 : 1;
+  constexpr int PW = 10, NPIX = 100, PINSTR = 13;          // patch pixels; 1 KiB (8-pixel) DMA pieces
+  constexpr int PPLANE = PINSTR * 8 * 64, APLANE = BN * BK;  // elements per plane
+  constexpr int PATCH = NP * PPLANE, WTS = NP * APLANE;
+  constexpr int LDS_ELEMS = PATCH + WTS > BM * BN * 2 ? PATCH + WTS : BM * BN * 2;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
+  uint16_t* patch = lds;
+  uint16_t* A = lds + PATCH;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  // block -> (image tile, N-tile, channel-slice range), XCD-aware as block_coords
+  const int tiles_x = (p.Wo + 7) >> 3, tiles_y = (p.Ho + 7) >> 3, tpi = tiles_x * tiles_y;
+  const int Bl = p.live ? min(p.B, static_cast<int>(*p.live)) : p.B;
+  const int ntm = Bl * tpi, ntn = (p.N + BN - 1) / BN, S = gridDim.y;
+  const int nwg = min(static_cast<int>(gridDim.x * gridDim.y), ntm * ntn * S);
+  const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+  if (bid >= nwg) return;  // whole block, before any barrier
+  const int q8 = nwg >> 3, r8 = nwg & 7, x8 = bid & 7;
+  const int id = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
+  const int tile = id / S, split = id - tile * S;
+  int tile_m, tile_n;
+  if (static_cast<long long>(p.N) * p.K <= static_cast<long long>(p.B) * p.H * p.W * p.Cin) {
+    tile_m = tile / ntn;
+    tile_n = tile - tile_m * ntn;
+  } else {
+    tile_n = tile / ntm;
+    tile_m = tile - tile_n * ntm;
+  }
+  const int b = tile_m / tpi, tt = tile_m - b * tpi;
+  const int ty0 = (tt / tiles_x) * 8, tx0 = (tt - (tt / tiles_x) * tiles_x) * 8;
+  const int n0 = tile_n * BN;
+  const int nsl = p.Cin / BK;
+  const int cs0 = split * sl_per_split, cs1 = min(nsl, cs0 + sl_per_split);
+
+  // patch DMA sources: piece I = wave + 4i (< 13), lane -> pixel I*8 + lane/8, physical chunk lane%8
+  const uint16_t* psrc[4];
+  bool pval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int I = wave + 4 * i;
+    const int q = I * 8 + (lane >> 3);
+    const int py = q / PW, px = q - (q / PW) * PW;
+    const int iy = ty0 - 1 + py, ix = tx0 - 1 + px;
+    pval[i] = I < PINSTR && q < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+    const int c = (lane & 7) ^ (q < NPIX ? patch_swz(py, px) : 0);
+    psrc[i] = pval[i] ? p.x + ((static_cast<size_t>(b) * p.H + iy) * p.W + ix) * p.Cin + c * 8 : p.zeros;
+  }
+  // weight DMA sources: rows wave*16 + i*8 + lane/8 of this N-tile
+  const uint16_t* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
+  }
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int cs = cs0; cs < cs1; ++cs) {
+    for (int tap = 0; tap < 9; ++tap) {
+      if (cs != cs0 || tap) __syncthreads();  // every wave done reading the patch / weights
+      if (tap == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int I = wave + 4 * i;
+          if (I >= PINSTR) break;  // wave-uniform
+          const uint16_t* src = psrc[i] + (pval[i] ? cs * BK : 0);
+          glds16(src, patch + I * 512);
+          if constexpr (SPLIT) glds16(pval[i] ? src + p.xplane : p.zeros, patch + PPLANE + I * 512);
+        }
+      }
+      const int k0 = tap * p.Cin + cs * BK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        glds16(asrc[i] + k0, A + (wave * (BN / 4) + i * 8) * BK);
+        if constexpr (SPLIT) glds16(asrc[i] + p.wplane + k0, A + APLANE + (wave * (BN / 4) + i * 8) * BK);
+      }
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int dy = tap / 3, dx = tap - dy * 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int chunk = s * 4 + (lane >> 4);
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(A + swz(wn * 32 + i * 16 + (lane & 15), chunk));
+        int boff[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int pix = j * 16 + (lane & 15);
+          const int row = wm * 4 + (pix >> 3) + dy, col = (pix & 7) + dx;
+          boff[j] = (row * PW + col) * BK + ((chunk ^ patch_swz(row, col)) << 3);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(patch + boff[j]);
+        }
+        if constexpr (SPLIT) {
+          bf16x8 afl[2], bfl[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            afl[i] = *reinterpret_cast<const bf16x8*>(A + APLANE + swz(wn * 32 + i * 16 + (lane & 15), chunk));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bfl[j] = *reinterpret_cast<const bf16x8*>(patch + PPLANE + boff[j]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // all operand reads done before the epilogue reuses the LDS
+  tile_epilogue<BM, BN>(p, acc, lds, 0, n0, wm, wn, lane, tid, tile, split, SpatialRows{b, ty0, tx0, p.Ho, p.Wo});
+}
+
 template <int BM, int BN, int STAGES, int BKS = BK>
 void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
   if (b.split) {  // only ring depths whose doubled stages fit the LDS are instantiated
@@ -718,6 +883,31 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     if (a.KH != 1 || a.KW != 1 || a.pad_h || a.pad_w || a.K != a.Cin || a.K > kBnlMaxK || a.Cin % BK || !a.in_shift)
       return hipErrorInvalidValue;
     if (variant == 0) variant = 1;  // the register-staged loop has no pre-activation: 2-stage ring
+  }
+  if (variant == 6) {  // spatially tiled 3x3/s1/p1 (64x64 tile only): split-K over channel slices
+    if constexpr (BM == 64 && BN == 64) {
+      if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.dil != 1 || a.pad_h != 1 || a.pad_w != 1 || a.H != a.Ho ||
+          a.W != a.Wo || a.Cin % BK || a.K != 9 * a.Cin || a.Kpad != a.K || a.N % 8 || !a.zeros || a.in_scale)
+        return hipErrorInvalidValue;
+      const int nsl = a.Cin / BK;
+      const int sp = std::max(1, std::min(a.splits, nsl));
+      const int per = (nsl + sp - 1) / sp, effs = (nsl + per - 1) / per;
+      const int stiles = a.B * ((a.Ho + 7) / 8) * ((a.Wo + 7) / 8) * ((a.N + 63) / 64);
+      ConvArgs c = b;
+      c.splits = effs;
+      const bool sfused = effs > 1 && a.counters && stiles <= a.counters_n;
+      if (!sfused) c.counters = nullptr;
+      if (c.split) hipLaunchKernelGGL(conv3x3_spatial_kernel<true>, dim3(stiles, effs), dim3(256), 0, s, c, per);
+      else hipLaunchKernelGGL(conv3x3_spatial_kernel<false>, dim3(stiles, effs), dim3(256), 0, s, c, per);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess || effs == 1 || sfused) return e;
+      const long long groups = static_cast<long long>(c.M) * (c.N / 8);
+      hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(static_cast<int>(std::min<long long>((groups + 255) / 256, 8192))),
+                         dim3(256), 0, s, c);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
   }
   if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;

@@ -68,8 +68,9 @@ struct ConvArgs {
 // 6 stages only where they fit the LDS; they return hipErrorInvalidValue otherwise so a tuner can
 // skip them).  The deep rings keep more K-steps in flight for the latency-bound small-M layers.
 // Variant 5 = the LDS-DMA loop with ONE stage (no ring): for K <= 64 layers, where the smaller LDS
-// footprint fits more blocks per CU.
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 24 };
+// footprint fits more blocks per CU.  Variant 6 = spatially tiled 3x3/s1/p1 kernel (8x8 pixels x 64
+// channels per block, input patch staged once per 64-channel slice; 64x64 tile config only).
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 28 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

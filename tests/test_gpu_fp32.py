@@ -66,7 +66,8 @@ def test_split_conv_matches_fp32(native, shape):
     assert rel_err(ob.permute(0, 3, 1, 2), ref) > 20 * rel_err(out32.permute(0, 3, 1, 2), ref)
 
 
-@pytest.mark.parametrize("shape", [(3, 28, 128, 256, 1, 1, 0), (2, 14, 256, 256, 3, 1, 1), (2, 14, 512, 1024, 1, 2, 0)])
+@pytest.mark.parametrize("shape", [(3, 28, 128, 256, 1, 1, 0), (2, 14, 256, 256, 3, 1, 1), (2, 14, 512, 1024, 1, 2, 0),
+                                   (3, 11, 128, 64, 3, 1, 1)])
 @pytest.mark.parametrize("splits,fused", [(1, True), (3, True), (3, False)])
 def test_split_conv_every_variant_and_epilogue(native, shape, splits, fused):
     """Every launch config that fits (split stages are twice as large), split-K fused/unfused, with
@@ -100,6 +101,8 @@ def test_split_conv_every_variant_and_epilogue(native, shape, splits, fused):
         assert rel_err(out2, u) < TOL, (cfg, rel_err(out2, u))
         ran.append(cfg)
     assert any(c < 4 for c in ran) and any(c >= 4 for c in ran), ran
+    if k == 3 and s == 1:
+        assert 27 in ran, ran  # spatially tiled 3x3 kernel (variant 6)
 
 
 def test_split_conv_repeatable_bitwise(native):

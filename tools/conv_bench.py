@@ -169,11 +169,11 @@ def main():
                  ("fp32 split mode. " if a.split else "") +
                  "Best of %d configs x split-K {1..16} x {separate, fused} reduction; hipGraph of %d launches, "
                  "median of %d replays. Weighted total %.1f us." % (K.NUM_CFGS, a.reps, a.trials, total), "",
-                 "| shape | x | M | N | K | best us | TFLOP/s | cfg/split | v0 | v1 (2st) | v2 (3st) | v3 (4st) | v4 (6st) | v5 (1st) |",
-                 "|---|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|"]
+                 "| shape | x | M | N | K | best us | TFLOP/s | cfg/split | v0 | v1 (2st) | v2 (3st) | v3 (4st) | v4 (6st) | v5 (1st) | v6 (3x3 spatial) |",
+                 "|---|---:|---:|---:|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|"]
         for r in results:
             pv = r["best_per_variant"]
-            cells = ["%.1f" % pv[str(v)]["us"] if str(v) in pv else "-" for v in range(6)]
+            cells = ["%.1f" % pv[str(v)]["us"] if str(v) in pv else "-" for v in range(7)]
             lines.append("| %s | %d | %d | %d | %d | %.1f | %.0f | %d/%d%s | %s |" % (
                 r["name"], r["count"], r["M"], r["N"], r["K"], r["us"], r["tflops"], r["cfg"], r["splits"],
                 "f" if r["fused"] else "", " | ".join(cells)))
