@@ -179,11 +179,19 @@ class HipEngine : public Engine {
         sl.d_prep.push_back(pbuf);
       }
     }
-    // Batch buckets ~sqrt(2) apart (1, 2, 4, 6, 8, 12, 16, 24, 32, ...): a batch runs the graph of
-    // the smallest bucket >= B, so padding waste stays under a third.
+    // Batch buckets ~sqrt(2) apart up to 16 (1, 2, 4, 6, 8, 12, 16), quarter steps above
+    // (20, 24, 28, 32, 40, ...): a batch runs the graph of the smallest bucket >= B, and the
+    // serving loop's batches (17-24 at the headline load) get kernels tuned within 4 of their size.
+    // DIE_COARSE_BUCKETS=1: sqrt(2) steps throughout.
+    const bool coarse = std::getenv("DIE_COARSE_BUCKETS") && std::atoi(std::getenv("DIE_COARSE_BUCKETS")) != 0;
     for (int b = 1; b < max_batch_; b *= 2) {
       buckets_.push_back(b);
-      if (b >= 4 && b + b / 2 < max_batch_) buckets_.push_back(b + b / 2);
+      if (b >= 16 && !coarse) {
+        for (int q = 1; q < 4; ++q)
+          if (b + q * b / 4 < max_batch_) buckets_.push_back(b + q * b / 4);
+      } else if (b >= 4 && b + b / 2 < max_batch_) {
+        buckets_.push_back(b + b / 2);
+      }
     }
     buckets_.push_back(max_batch_);
     est_ms_.assign(buckets_.size(), 0.0);
