@@ -16,7 +16,7 @@ HIPFLAGS := -std=c++17 -O3 --offload-arch=$(ARCH) -fPIC -g -Wall -Wno-unused-par
             -munsafe-fp-atomics
 LDLIBS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lgomp -lpthread
 
-HOST_SRCS := core/json.cpp core/http.cpp core/http_async.cpp core/log.cpp core/shm_arena.cpp core/textpack.cpp parallel/dp_group.cpp parallel/comm.cpp engine/dp_engine.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
+HOST_SRCS := core/json.cpp core/http.cpp core/http_async.cpp core/log.cpp core/metrics.cpp core/shm_arena.cpp core/textpack.cpp parallel/dp_group.cpp parallel/comm.cpp engine/dp_engine.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
              serve/worker.cpp serve/gateway.cpp serve/loadgen.cpp onnx/onnx_model.cpp \
              engine/engine.cpp engine/cpu_exec.cpp engine/hip_plan.cpp capi/capi.cpp capi/capi_kernels.cpp
 HIP_SRCS  := $(notdir $(wildcard $(SRC)/engine/*.hip)) $(notdir $(wildcard $(SRC)/kernels/*.hip))
@@ -54,7 +54,7 @@ clean:
 	rm -rf $(BUILD) $(LIBDIR) $(BINDIR)
 
 # Host-runtime concurrency stress under sanitizers; no GPU code is linked.
-STRESS_SRCS := core/json.cpp core/http.cpp core/http_async.cpp core/log.cpp core/shm_arena.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
+STRESS_SRCS := core/json.cpp core/http.cpp core/http_async.cpp core/log.cpp core/metrics.cpp core/shm_arena.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
                serve/gateway.cpp tests/stress_main.cpp
 SANFLAGS := -std=c++17 -O1 -g -march=x86-64-v3 -fno-omit-frame-pointer -Wall -Wno-unused-parameter
 stress-tsan: $(BINDIR)/die_stress_tsan

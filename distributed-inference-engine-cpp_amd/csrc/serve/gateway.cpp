@@ -5,6 +5,7 @@
 #include <iostream>
 
 #include "../core/log.h"
+#include "../core/metrics.h"
 #include "../core/sysinfo.h"
 
 namespace die {
@@ -97,6 +98,12 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
   server_.route("GET", "/stats", [this](HttpRequest&, Responder res) {
     HttpResponse r;
     r.body = getStats().dump();
+    res.send(std::move(r));
+  });
+  server_.route("GET", "/metrics", [this](HttpRequest&, Responder res) {
+    HttpResponse r;
+    r.content_type = "text/plain; version=0.0.4";
+    r.body = prometheus_text(getStats(), "die_gateway", "");
     res.send(std::move(r));
   });
 }

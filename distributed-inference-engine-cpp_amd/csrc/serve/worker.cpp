@@ -1,6 +1,7 @@
 #include "worker.h"
 
 #include "../core/log.h"
+#include "../core/metrics.h"
 #include "../core/textpack.h"
 #include "../core/trace.h"
 
@@ -114,6 +115,12 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
   server_.route("GET", "/health", [this](HttpRequest&, Responder res) {
     HttpResponse r;
     r.body = getHealth().dump();
+    res.send(std::move(r));
+  });
+  server_.route("GET", "/metrics", [this](HttpRequest&, Responder res) {
+    HttpResponse r;
+    r.content_type = "text/plain; version=0.0.4";
+    r.body = prometheus_text(getHealth(), "die_worker", "node=\"" + opt_.node_id + "\"");
     res.send(std::move(r));
   });
   server_.route("POST", "/admin/fault", [this](HttpRequest& req, Responder res) { handle_admin_fault(req, res); });

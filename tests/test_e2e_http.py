@@ -296,6 +296,40 @@ def test_health_io_and_log_counters(cluster):
     assert "log_lines" in s and "log_lines_suppressed" in s
 
 
+def _metrics(url):
+    with urllib.request.urlopen(url + "/metrics", timeout=10) as r:
+        assert r.headers.get("Content-Type", "").startswith("text/plain")
+        text = r.read().decode()
+    samples = {}
+    for line in text.splitlines():
+        assert line and not line.startswith(" "), line
+        name_labels, value = line.rsplit(" ", 1)
+        samples[name_labels] = float(value)
+    return text, samples
+
+
+def test_prometheus_metrics_endpoints(cluster):
+    """GET /metrics on worker and gateway: Prometheus text exposition of the /health and /stats
+    numbers (one sample per numeric leaf, strings as labels of `<prefix>_info`), moving with traffic."""
+    w = cluster["workers"][2]
+    text0, m0 = _metrics(w.url)
+    key = 'die_worker_total_requests{node="w2"}'
+    assert key in m0, text0[:500]
+    assert any(k.startswith("die_worker_io_batches{") for k in m0)
+    assert any(k.startswith("die_worker_info{") and 'node_id="w2"' in k for k in m0), text0[-300:]
+    for i in range(3):
+        st, _ = post(w.url + "/infer", {"request_id": "prom_%d" % i, "input_data": [float(i), 1.5]})
+        assert st == 200
+    _, m1 = _metrics(w.url)
+    assert m1[key] >= m0[key] + 3
+    gtext, g = _metrics(cluster["gw"].url)
+    assert "die_gateway_routed" in g, gtext[:500]
+    info = [k for k in g if k.startswith("die_gateway_info")]
+    assert info and 'circuit_breakers_0_state="CLOSED"' in info[0], info
+    # per-worker breaker entries come from a JSON array: an `index` label each
+    assert any("index=" in k for k in g), gtext[:800]
+
+
 def test_gateway_failure_logging_is_rate_limited(native, models):
     """A dead worker produces one WARN line per second per call site, not one per request (the
     reference flushes two lines per request: SURVEY Q11)."""
