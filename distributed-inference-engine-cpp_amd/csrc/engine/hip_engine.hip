@@ -179,16 +179,19 @@ class HipEngine : public Engine {
         sl.d_prep.push_back(pbuf);
       }
     }
-    // Batch buckets ~sqrt(2) apart up to 16 (1, 2, 4, 6, 8, 12, 16), quarter steps above
-    // (20, 24, 28, 32, 40, ...): a batch runs the graph of the smallest bucket >= B, and the
-    // serving loop's batches (17-24 at the headline load) get kernels tuned within 4 of their size.
+    // Batch buckets ~sqrt(2) apart up to 16 (1, 2, 4, 6, 8, 12, 16), eighth steps above
+    // (18, 20, ..., 32, 36, ...): a batch runs the graph of the smallest bucket >= B, and the
+    // serving loop's batches (17-24 at the headline load) get kernels tuned within 2 of their size
+    // (fp32 headline A/B: sqrt(2) steps 13.1-13.2k, quarter steps 13.6-13.7k, eighth steps
+    // 13.9-14.1k req/s; profiles/r2_state.md).  DIE_BUCKET_DIV=N: N steps per octave above 16;
     // DIE_COARSE_BUCKETS=1: sqrt(2) steps throughout.
     const bool coarse = std::getenv("DIE_COARSE_BUCKETS") && std::atoi(std::getenv("DIE_COARSE_BUCKETS")) != 0;
+    const int fine = std::getenv("DIE_BUCKET_DIV") ? std::max(1, std::atoi(std::getenv("DIE_BUCKET_DIV"))) : 8;
     for (int b = 1; b < max_batch_; b *= 2) {
       buckets_.push_back(b);
       if (b >= 16 && !coarse) {
-        for (int q = 1; q < 4; ++q)
-          if (b + q * b / 4 < max_batch_) buckets_.push_back(b + q * b / 4);
+        for (int q = 1; q < fine; ++q)
+          if (b + q * b / fine < max_batch_) buckets_.push_back(b + q * b / fine);
       } else if (b >= 4 && b + b / 2 < max_batch_) {
         buckets_.push_back(b + b / 2);
       }
