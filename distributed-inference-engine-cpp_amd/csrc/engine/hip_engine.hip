@@ -121,8 +121,9 @@ class HipEngine : public Engine {
       if (comm_) n_stage_ = 0;
       HIP_CHECK(hipMalloc(&d_text_, text_cap_ * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
       // 4-bit packed texts (BatchItem::packed; early-uploaded or copied at submit) land here, slot
-      // for slot like d_text_; the decode kernels expand them in registers (no character copy in HBM)
-      if (!comm_ && opt.pack_text)
+      // for slot like d_text_; the decode kernels expand them in registers (no character copy in HBM).
+      // Data-parallel ranks take packed texts too: the ingesting rank packs into the DP arena.
+      if (opt.pack_text)
         HIP_CHECK(hipMalloc(&d_packed_, text_cap_ / 2 * (static_cast<size_t>(n_stage_) + static_cast<size_t>(depth_) * max_batch_)));
       stage_ev_.resize(n_stage_);
       stage_seq_.assign(n_stage_, 0);
@@ -546,14 +547,17 @@ class HipEngine : public Engine {
       if (comm_) {
         // data parallel: every rank contributes its B rows (and decode status) to rank 0 over xGMI;
         // the same collectives in the same order on every rank, whatever its shard holds.
-        comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
-        comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, cs);
+        // (a group of one has nothing to gather: its rows go to the host straight from d_out)
+        if (dp_world_ > 1) {
+          comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
+          comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, cs);
+        }
         HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
         {  // every rank answers the sub-batches it ingested: all rows come back to every host
-          HIP_CHECK(hipMemcpyAsync(sl.h_gather, sl.d_gather, sizeof(float) * out_numel_ * B * dp_world_,
-                                   hipMemcpyDeviceToHost, cs));
-          HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_,
-                                   hipMemcpyDeviceToHost, cs));
+          HIP_CHECK(hipMemcpyAsync(sl.h_gather, dp_world_ > 1 ? sl.d_gather : sl.d_out,
+                                   sizeof(float) * out_numel_ * B * dp_world_, hipMemcpyDeviceToHost, cs));
+          HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, dp_world_ > 1 ? sl.d_gstatus : sl.d_status,
+                                   sizeof(int) * 2 * max_batch_ * dp_world_, hipMemcpyDeviceToHost, cs));
           d2h_bytes_.fetch_add(static_cast<long long>((sizeof(float) * out_numel_ * B + sizeof(int) * 2 * max_batch_) *
                                                       dp_world_),
                                std::memory_order_relaxed);
