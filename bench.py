@@ -64,6 +64,8 @@ def main():
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=3)
     ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
+    ap.add_argument("--parse-threads", type=int, default=-1,
+                    help="worker body-parse pool (-1 auto, 0 = parse on the HTTP reactors)")
     ap.add_argument("--stage-slots", type=int, default=0,
                     help="early-upload text slots on the device (-1 auto, 0 = copy at batch submit)")
     ap.add_argument("--no-numa", action="store_true", help="keep the inherited CPU affinity (no NUMA binding)")
@@ -141,7 +143,8 @@ def main():
                    "device_decode": not args.no_device_decode}
     if args.mode in ("gateway", "http"):
         t_init = time.perf_counter()
-        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts)
+        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
+                           parse_threads=args.parse_threads)
         t_ready = time.perf_counter()
         gw = None
         target_port = wk.port
@@ -231,7 +234,7 @@ def main():
         port = hg.broadcast_object(port, src=0)
         eng_opts = dict(engine_opts, dp_world=world, dp_group=group, dp_rank=rank)
         wk = native.Worker(model, node_id="dp-r%d" % rank, port=port, reuse_port=True, max_batch=Btot,
-                           engine=eng_opts)
+                           engine=eng_opts, parse_threads=args.parse_threads)
         lg = dict(port=port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
         native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, **lg)

@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (3)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
-              << "  --http-threads N  --host ADDR (0.0.0.0)\n"
+              << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
               << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose\n"
@@ -128,6 +128,7 @@ int main(int argc, char** argv) {
   o.batch_timeout = std::chrono::milliseconds(f.i("batch-timeout-ms", 20));
   o.policy = f.b("deadline") ? die::BatchPolicy::DEADLINE : die::BatchPolicy::GREEDY;
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
+  o.parse_threads = static_cast<int>(f.i("parse-threads", -1));
   o.engine.device = f.str("device", "auto");
   o.engine.device_id = static_cast<int>(f.i("device-id", 0));
   o.engine.precision = f.str("precision", "fp32");

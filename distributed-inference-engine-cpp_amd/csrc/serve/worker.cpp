@@ -3,6 +3,7 @@
 #include "../core/log.h"
 #include "../core/metrics.h"
 #include "../core/textpack.h"
+#include "../core/sysinfo.h"
 #include "../core/trace.h"
 
 #include <algorithm>
@@ -111,7 +112,21 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       [eng] { eng->wait_for_slot(); }, opt_.policy, [eng] { return eng->dispatch_not_before(); });
   batcher_->start();
 
-  server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) { handle_infer(req, res); });
+  int npt = opt_.parse_threads;
+  if (npt < 0) npt = std::max(2, available_cpus() / 4);
+  for (int i = 0; i < npt; ++i) parse_threads_.emplace_back([this] { parse_loop(); });
+  if (npt > 0) {
+    server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
+      ParseJob j{std::make_shared<HttpRequest>(std::move(req)), std::move(res)};
+      {
+        std::lock_guard<std::mutex> g(parse_mu_);
+        parse_q_.push_back(std::move(j));
+      }
+      parse_cv_.notify_one();
+    });
+  } else {
+    server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) { handle_infer(req, res); });
+  }
   server_.route("GET", "/health", [this](HttpRequest&, Responder res) {
     HttpResponse r;
     r.body = getHealth().dump();
@@ -134,8 +149,30 @@ void WorkerNode::wait() { server_.wait(); }
 
 void WorkerNode::stop() {
   server_.stop();
+  {
+    std::lock_guard<std::mutex> g(parse_mu_);
+    parse_stop_ = true;
+  }
+  parse_cv_.notify_all();
+  for (auto& t : parse_threads_)
+    if (t.joinable()) t.join();
+  parse_threads_.clear();
   if (batcher_) batcher_->stop();
   if (engine_) engine_->synchronize();
+}
+
+void WorkerNode::parse_loop() {
+  while (true) {
+    ParseJob j;
+    {
+      std::unique_lock<std::mutex> lk(parse_mu_);
+      parse_cv_.wait(lk, [&] { return parse_stop_ || !parse_q_.empty(); });
+      if (parse_q_.empty()) return;  // stopping and drained
+      j = std::move(parse_q_.front());
+      parse_q_.pop_front();
+    }
+    handle_infer(*j.req, std::move(j.res));
+  }
 }
 
 HttpResponse WorkerNode::error_response(int status, const std::string& msg, bool client_error) const {
@@ -432,6 +469,7 @@ Json WorkerNode::getHealth() const {
   st["total"] = h_total_.snapshot();
   h["stages_us"] = st;
   h["http_threads"] = opt_.http_threads;
+  h["parse_threads"] = static_cast<int>(parse_threads_.size());
   h["engine"] = engine_->stats();
   h["engine"]["name"] = engine_->name();
   // per-GPU I/O counters, one schema for every engine (zeros where not applicable)

@@ -11,9 +11,12 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../core/http.h"
@@ -45,6 +48,10 @@ struct WorkerOptions {
   bool accept_shm = true;
   // Share the listening port with other processes (the ranks of a data-parallel worker).
   bool reuse_port = false;
+  // /infer bodies are parsed (JSON scan, 4-bit text packing, cache key) on this many pool threads
+  // instead of the connection's reactor, so a reactor busy parsing a 1 MB body never holds a
+  // finished response back.  0 = parse on the reactor; -1 = auto (a quarter of the CPUs, >= 2).
+  int parse_threads = -1;
 };
 
 class WorkerNode {
@@ -108,6 +115,17 @@ class WorkerNode {
   std::atomic<double> fault_fail_rate_{0.0};
   std::atomic<int> fault_latency_ms_{0};
   std::chrono::steady_clock::time_point started_;
+  // parse pool (WorkerOptions::parse_threads)
+  struct ParseJob {
+    std::shared_ptr<HttpRequest> req;
+    Responder res;
+  };
+  void parse_loop();
+  std::mutex parse_mu_;
+  std::condition_variable parse_cv_;
+  std::deque<ParseJob> parse_q_;
+  bool parse_stop_ = false;
+  std::vector<std::thread> parse_threads_;
 };
 
 }  // namespace die

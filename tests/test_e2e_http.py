@@ -341,16 +341,21 @@ def test_gateway_failure_logging_is_rate_limited(native, models):
     s.close()
     path = models["tiny"][0]
     live = native.Worker(path, node_id="live", engine={"device": "cpu"})
-    gw = native.GatewayServer(["127.0.0.1:%d" % dead, "127.0.0.1:%d" % live.port], failure_threshold=1000)
+    names = ["127.0.0.1:%d" % dead, "127.0.0.1:%d" % live.port]
+    gw = native.GatewayServer(names, failure_threshold=1000)
+    # request ids whose ring primary is the dead worker (the ports are random, so the share of
+    # ids that land on it varies run to run): each one is a failure + failover
+    ring, keys = py_ring(names)
+    ids = [rid for rid in ("rl_%d" % i for i in range(5000)) if py_get(ring, keys, rid) == names[0]][:60]
     try:
         _, s0 = get(gw.url + "/stats")
-        for i in range(200):
-            st, _ = post(gw.url + "/infer", {"request_id": "rl_%d" % i, "input_data": [1.0]})
+        for rid in ids:
+            st, _ = post(gw.url + "/infer", {"request_id": rid, "input_data": [1.0]})
             assert st == 200
         _, s1 = get(gw.url + "/stats")
         emitted = s1["log_lines"] - s0["log_lines"]
         suppressed = s1["log_lines_suppressed"] - s0["log_lines_suppressed"]
-        assert s1["failovers"] - s0["failovers"] > 10
+        assert s1["failovers"] - s0["failovers"] >= 60
         assert emitted <= 5 and suppressed > 5, (emitted, suppressed)
     finally:
         gw.stop()
