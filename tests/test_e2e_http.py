@@ -374,11 +374,16 @@ def test_large_bodies_cross_shared_memory(native, models):
     gw = native.GatewayServer(["127.0.0.1:%d" % a.port, "127.0.0.1:%d" % b.port])
     try:
         rng = np.random.default_rng(3)
-        for i in range(16):
+        seen = set()
+        # the ring depends on the workers' (random) ports: send until both nodes have had traffic
+        for i in range(96):
+            if i >= 16 and len(seen) == 2:
+                break
             vals = np.round(rng.random(3 * 64 * 64), 4).tolist()
             body = {"request_id": "big_%d" % i, "input_data": vals}
             st, out = post(gw.url + "/infer", body)
             assert st == 200, out
+            seen.add(out["node_id"])
             direct = a if out["node_id"] == "shm_a" else b
             st2, ref = post(direct.url + "/infer", dict(body, request_id="d_%d" % i))
             assert st2 == 200 and ref["output_data"] == out["output_data"]
