@@ -187,7 +187,8 @@ def main():
             "worker_init_s": round(t_ready - t_init, 2),
             "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
             "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
-            "pace_lead_ms": e1.get("avg_pace_lead_ms"),
+            "pace_lead_ms": e1.get("avg_pace_lead_ms"), "submit_us_avg": e1.get("staging_diag", {}).get("submit_us_avg"),
+            "pace_input_ms": e1.get("pace_input_ms"), "pace_margin_ms": e1.get("pace_margin_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
             # host CPU spent per request by this process (client + gateway + worker threads together)
             "cpu_us_per_request": {"user": round((ru1.ru_utime - ru0.ru_utime) * 1e6 / max(1, res["ok"]), 1),
@@ -256,7 +257,10 @@ def main():
                  "client_connections_per_gpu": args.connections,
                  "subbatches_sent_this_rank": e1.get("dp_subbatches_sent", 0) - h0["engine"].get("dp_subbatches_sent", 0),
                  "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"), "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"),
-                 "pace_lead_ms": e1.get("avg_pace_lead_ms"),
+                 "pace_lead_ms": e1.get("avg_pace_lead_ms"), "prep_ms_per_batch": e1.get("avg_prep_ms"),
+                 "leader_wait_ms_per_batch": {k: e1.get("dp_%s_wait_ms_per_batch" % k) for k in ("pop", "slot", "pace")},
+                 "submit_us_avg": e1.get("staging_diag", {}).get("submit_us_avg"),
+                 "pace_input_ms": e1.get("pace_input_ms"), "pace_margin_ms": e1.get("pace_margin_ms"),
                  "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()}}
         if extra["dp_batches_rank0"]:
             extra["avg_dp_batch"] = world * SR * args.steps / extra["dp_batches_rank0"] if rank == 0 else None

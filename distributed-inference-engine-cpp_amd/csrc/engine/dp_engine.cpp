@@ -18,10 +18,12 @@
 // match.  CPU engines gather through the segment (host communicator), which is what the multi-process
 // CPU tests exercise.
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -80,6 +82,13 @@ class DpEngine : public Engine {
       if (!group_) throw DpAbandoned();
       world_ = group_->world();
     }
+    // A group of one has nothing to merge or gather: its batcher feeds a plain local engine
+    // directly (same pacing, slots and pinned staging as a plain worker) instead of queueing
+    // sub-batches in the shared arena for the leader's merge loop.  The communicator is still
+    // formed (weights are broadcast), the engine just never needs it.  DIE_DP_FORCE_MERGE=1 keeps
+    // the N>1 path (arena staging, merge loop, device gather) at world=1 for measuring it.
+    const char* fm = std::getenv("DIE_DP_FORCE_MERGE");
+    solo_ = world_ == 1 && !(fm && std::atoi(fm) != 0);
     build_local(path);
     if (rank_ == 0) {
       if (!group_->wait_joined(600000)) throw std::runtime_error("dp followers did not join");
@@ -90,7 +99,11 @@ class DpEngine : public Engine {
     DpGroup* g = group_.get();
     pool_ = std::make_unique<SamplePool>(
         item_bytes_ / sizeof(float), [g](size_t bytes) { return g->arena_alloc(bytes); }, [](void*) {}, 16);
-    if (rank_ == 0) dispatcher_ = std::thread([this] { dispatch_loop(); });
+    if (rank_ == 0)
+      dispatcher_ = std::thread([this] {
+        prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // paced dispatch: wake within ~1 us, not 50 us
+        dispatch_loop();
+      });
     else shard_thread_ = std::thread([this] { follower_loop(); });
   }
 
@@ -106,15 +119,17 @@ class DpEngine : public Engine {
   }
 
   std::string name() const override {
-    return "dp" + std::to_string(world_) + "(" + std::string(comm_->backend()) + "):" + local_->name();
+    return "dp" + std::to_string(world_) + "(" + std::string(comm_ ? comm_->backend() : "none") + "):" + local_->name();
   }
   const std::string& getModelPath() const override { return local_->getModelPath(); }
   std::vector<int64_t> getInputShape() const override { return local_->getInputShape(); }
   std::vector<int64_t> getOutputShape() const override { return local_->getOutputShape(); }
   // one submit() = one sub-batch of this rank; DP batches merge up to world x this
   int max_batch() const override { return local_max_; }
-  SamplePool& sample_pool() override { return *pool_; }
-  size_t text_capacity() const override { return std::min(local_->text_capacity(), item_bytes_); }
+  SamplePool& sample_pool() override { return solo_ ? local_->sample_pool() : *pool_; }
+  size_t text_capacity() const override {
+    return solo_ ? local_->text_capacity() : std::min(local_->text_capacity(), item_bytes_);
+  }
   bool text_packing() const override { return local_->text_packing(); }
   void register_host_memory(void*, size_t) override {}
   // The worker's batcher hands over whatever it has queued as soon as this returns; the leader
@@ -122,7 +137,14 @@ class DpEngine : public Engine {
   // batcher) while the GPU is busy.  Bounded by ring slots and by this rank's items in flight
   // (queued + in the pipeline), not by sub-batch count: tiny eager sub-batches must not starve the
   // next merge.
+  std::chrono::steady_clock::time_point dispatch_not_before() override {
+    return solo_ ? local_->dispatch_not_before() : std::chrono::steady_clock::now();
+  }
   void wait_for_slot() override {
+    if (solo_) {
+      local_->wait_for_slot();
+      return;
+    }
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] {
       return stop_ || (pending_.size() < static_cast<size_t>(kDpSubRing - 1) &&
@@ -130,6 +152,7 @@ class DpEngine : public Engine {
     });
   }
   void synchronize() override {
+    if (solo_) local_->synchronize();
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait_for(lk, std::chrono::seconds(30), [&] { return stop_ || pending_.empty(); });
   }
@@ -139,12 +162,19 @@ class DpEngine : public Engine {
     Json j = local_->stats();
     j["dp_world"] = world_;
     j["dp_rank"] = rank_;
-    j["dp_backend"] = comm_->backend();
+    j["dp_backend"] = comm_ ? comm_->backend() : "none";
     j["dp_device_gather"] = device_gather_;
+    j["dp_solo"] = solo_;
     j["dp_batches"] = static_cast<long long>(batches_.load());
     j["dp_subbatches_sent"] = static_cast<long long>(subs_sent_.load());
     j["dp_subbatches_merged"] = static_cast<long long>(subs_merged_.load());
     j["dp_arena_mib"] = static_cast<double>(group_->arena_bytes()) / (1 << 20);
+    if (rank_ == 0) {
+      const double nb = static_cast<double>(std::max<long long>(1, batches_.load()));
+      j["dp_pop_wait_ms_per_batch"] = pop_wait_us_.load() / nb / 1000.0;
+      j["dp_slot_wait_ms_per_batch"] = slot_wait_us_.load() / nb / 1000.0;
+      j["dp_pace_wait_ms_per_batch"] = pace_wait_us_.load() / nb / 1000.0;
+    }
     return j;
   }
 
@@ -155,6 +185,12 @@ class DpEngine : public Engine {
       r.ok = B == 0;
       if (B) r.error = "batch of " + std::to_string(B) + " exceeds dp sub-batch max " + std::to_string(local_max_);
       done(r);
+      return;
+    }
+    if (solo_) {
+      batches_++;
+      subs_sent_++;
+      local_->submit(std::move(items), std::move(done));
       return;
     }
     std::lock_guard<std::mutex> sg(submit_mu_);  // single producer of this rank's ring
@@ -220,13 +256,15 @@ class DpEngine : public Engine {
       if (hipSetDevice(opt_.device_id) != hipSuccess)
         throw std::runtime_error("dp rank " + std::to_string(rank_) + ": cannot select HIP device " +
                                  std::to_string(opt_.device_id));
-      comm_ = make_rccl_comm(*group_);
-      lo.dp_comm = comm_.get();
+      // (experiment knob: a solo group without any communicator)
+      const char* nc = std::getenv("DIE_DP_SOLO_NO_COMM");
+      if (!(solo_ && nc && std::atoi(nc) != 0)) comm_ = make_rccl_comm(*group_);
+      lo.dp_comm = solo_ ? nullptr : comm_.get();
       std::string why;
       local_ = create_hip_engine(path, lo, &why);
       if (!local_) throw std::runtime_error("dp rank " + std::to_string(rank_) + ": HIP engine unavailable: " + why);
     }
-    local_->register_host_memory(group_->arena(), group_->arena_bytes());
+    if (!solo_) local_->register_host_memory(group_->arena(), group_->arena_bytes());
   }
 
   // Leader: merge queued sub-batches into DP batches, paced on the local GPU.
@@ -236,12 +274,20 @@ class DpEngine : public Engine {
     const int cap = std::min(kDpMaxItems, local_max_ * world_);
     while (!stop_ && !group_->stopping()) {
       int rank = 0;
+      const auto tp0 = std::chrono::steady_clock::now();
       if (!group_->pop_sub(*s, rank, 50)) continue;
       // the local pipeline has a free slot and the batch on the GPU is about to drain: everything
       // queued by then rides in this batch
+      const auto tp1 = std::chrono::steady_clock::now();
       local_->wait_for_slot();
+      const auto tp2 = std::chrono::steady_clock::now();
       const auto not_before = local_->dispatch_not_before();
       if (not_before > std::chrono::steady_clock::now()) std::this_thread::sleep_until(not_before);
+      const auto tp3 = std::chrono::steady_clock::now();
+      // where the leader's time goes between DP batches (stats: dp_*_ms_per_batch)
+      pop_wait_us_ = pop_wait_us_.load() + std::chrono::duration<double, std::micro>(tp1 - tp0).count();
+      slot_wait_us_ = slot_wait_us_.load() + std::chrono::duration<double, std::micro>(tp2 - tp1).count();
+      pace_wait_us_ = pace_wait_us_.load() + std::chrono::duration<double, std::micro>(tp3 - tp2).count();
       b->B = 0;
       b->nsub = 0;
       while (true) {
@@ -386,6 +432,7 @@ class DpEngine : public Engine {
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<Engine> local_;
   bool device_gather_ = false;
+  bool solo_ = false;  // world of one: submit straight to the local engine (no merge loop)
   std::unique_ptr<SamplePool> pool_;
   std::unique_ptr<DpSub> sub_ = std::make_unique<DpSub>();
   std::mutex submit_mu_, mu_;
@@ -396,6 +443,7 @@ class DpEngine : public Engine {
   std::atomic<bool> stop_{false};
   std::thread dispatcher_, shard_thread_;
   std::atomic<long long> batches_{0}, subs_sent_{0}, subs_merged_{0};
+  std::atomic<double> pop_wait_us_{0.0}, slot_wait_us_{0.0}, pace_wait_us_{0.0};  // leader only
 };
 
 }  // namespace

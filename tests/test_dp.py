@@ -79,6 +79,38 @@ def test_dp_worker_cpu(native, models, world):
         assert "served" in out and int(out.split("served")[1].split()[0]) >= 1, out
 
 
+@pytest.mark.parametrize("merge", [False, True])
+def test_dp_world1_solo_and_merge(native, models, monkeypatch, merge):
+    """A group of one feeds its local engine directly (dp_solo); DIE_DP_FORCE_MERGE=1 keeps the
+    sub-batch ring + merge loop N>1 runs.  Both answer like the plain executor, over HTTP too."""
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["tiny"]
+    if merge:
+        monkeypatch.setenv("DIE_DP_FORCE_MERGE", "1")
+    else:
+        monkeypatch.delenv("DIE_DP_FORCE_MERGE", raising=False)
+    group = "die_dp_s%d_%d" % (os.getpid(), merge)
+    wk = native.Worker(path, node_id="dp1", max_batch=8, engine={"device": "cpu", "dp_world": 1, "dp_group": group})
+    try:
+        h = wk.health()
+        assert h["engine"]["dp_solo"] is (not merge)
+        res = native.loadgen(port=wk.port, connections=8, requests=48, payload="full", input_numel=3 * 64 * 64)
+        assert res["ok"] == 48 and res["failed"] == 0
+        x = r.synthetic_input(2, cfg).reshape(2, -1)
+        for i in range(2):
+            body = json.dumps({"request_id": "s%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            out = json.loads(urllib.request.urlopen(urllib.request.Request(wk.url + "/infer", data=body),
+                                                    timeout=30).read())
+            ref = native.cpu_run(path, x[i:i + 1].reshape(1, 3, 64, 64))[0]
+            np.testing.assert_allclose(np.array(out["output_data"], np.float32), ref, rtol=1e-5, atol=1e-5)
+        h = wk.health()
+        assert h["engine"]["dp_batches"] >= 1
+        assert (h["engine"]["dp_subbatches_merged"] > 0) is merge
+    finally:
+        wk.stop()
+
+
 def test_dp_engine_uneven_shards(native, models):
     """B not divisible by the world size: the last rank pads; rows come back in item order."""
     from die_amd.models import resnet_v2 as r

@@ -16,15 +16,27 @@ from conftest import gpu_available
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
 
 
-def test_dp_engine_rccl_world1_matches_plain_engine(native, models):
+@pytest.fixture(params=["solo", "merge"])
+def dp_path(request, monkeypatch):
+    """solo: a world of one feeds its local engine directly; merge: DIE_DP_FORCE_MERGE=1 keeps the
+    multi-rank sub-batch ring + leader merge loop (what N>1 runs) at world=1."""
+    if request.param == "merge":
+        monkeypatch.setenv("DIE_DP_FORCE_MERGE", "1")
+    else:
+        monkeypatch.delenv("DIE_DP_FORCE_MERGE", raising=False)
+    return request.param
+
+
+def test_dp_engine_rccl_world1_matches_plain_engine(native, models, dp_path):
     from die_amd.models import resnet_v2 as r
 
     path, w, cfg = models["tiny"]
     plain = native.Engine(path, device="hip", max_batch=8, autotune=False)
     dp = native.Engine(path, device="hip", max_batch=8, autotune=False, dp_world=1,
-                       dp_group="die_gpu_dp_%d" % os.getpid())
+                       dp_group="die_gpu_dp_%s_%d" % (dp_path, os.getpid()))
     info = dp.refresh_info()
     assert info["name"].startswith("dp1(rccl):hip:gfx950")
+    assert info["dp_solo"] is (dp_path == "solo")
     for B in (1, 3, 8):
         x = r.synthetic_input(B, cfg, seed=B).reshape(B, -1)
         np.testing.assert_array_equal(dp.run(x), plain.run(x))
@@ -32,17 +44,19 @@ def test_dp_engine_rccl_world1_matches_plain_engine(native, models):
     plain.close()
 
 
-def test_dp_worker_rccl_world1_http(native, models):
+def test_dp_worker_rccl_world1_http(native, models, dp_path):
     from die_amd.models import resnet_v2 as r
 
     path, w, cfg = models["tiny"]
     wk = native.Worker(path, node_id="dp", max_batch=8,
-                       engine={"device": "hip", "dp_world": 1, "dp_group": "die_gpu_dpw_%d" % os.getpid(),
-                               "autotune": False})
+                       engine={"device": "hip", "dp_world": 1,
+                               "dp_group": "die_gpu_dpw_%s_%d" % (dp_path, os.getpid()), "autotune": False})
     ref_eng = native.Engine(path, device="hip", max_batch=8, autotune=False)
     try:
         h = wk.health()
-        assert h["engine"]["dp_backend"] == "rccl" and h["engine"]["dp_device_gather"] is True
+        # solo: the group's communicator exists but the local engine never gathers
+        assert h["engine"]["dp_backend"] == "rccl" and h["engine"]["dp_device_gather"] is (dp_path == "merge")
+        assert h["engine"]["dp_solo"] is (dp_path == "solo")
         res = native.loadgen(port=wk.port, connections=8, requests=64, payload="full", input_numel=3 * 64 * 64)
         assert res["ok"] == 64 and res["failed"] == 0
         x = r.synthetic_input(2, cfg).reshape(2, -1)
