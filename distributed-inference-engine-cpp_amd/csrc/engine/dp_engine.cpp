@@ -84,9 +84,9 @@ class DpEngine : public Engine {
     }
     // A group of one has nothing to merge or gather: its batcher feeds a plain local engine
     // directly (same pacing, slots and pinned staging as a plain worker) instead of queueing
-    // sub-batches in the shared arena for the leader's merge loop.  The communicator is still
-    // formed (weights are broadcast), the engine just never needs it.  DIE_DP_FORCE_MERGE=1 keeps
-    // the N>1 path (arena staging, merge loop, device gather) at world=1 for measuring it.
+    // sub-batches in the shared arena for the leader's merge loop, and no communicator is formed.
+    // DIE_DP_FORCE_MERGE=1 keeps the N>1 path (RCCL communicator, arena staging, merge loop,
+    // device gather) at world=1 for measuring and testing it.
     const char* fm = std::getenv("DIE_DP_FORCE_MERGE");
     solo_ = world_ == 1 && !(fm && std::atoi(fm) != 0);
     build_local(path);
@@ -256,9 +256,10 @@ class DpEngine : public Engine {
       if (hipSetDevice(opt_.device_id) != hipSuccess)
         throw std::runtime_error("dp rank " + std::to_string(rank_) + ": cannot select HIP device " +
                                  std::to_string(opt_.device_id));
-      // (experiment knob: a solo group without any communicator)
-      const char* nc = std::getenv("DIE_DP_SOLO_NO_COMM");
-      if (!(solo_ && nc && std::atoi(nc) != 0)) comm_ = make_rccl_comm(*group_);
+      // A solo group forms no RCCL communicator at all: merely having one initialised cost the
+      // co-located HTTP/JSON host path ~13 % of throughput on a 16-CPU share (12.4-12.5k vs
+      // 14.3-14.7k req/s, gpurun_out/r2_43; profiles/r2_dp_world1.md).
+      if (!solo_) comm_ = make_rccl_comm(*group_);
       lo.dp_comm = solo_ ? nullptr : comm_.get();
       std::string why;
       local_ = create_hip_engine(path, lo, &why);
