@@ -251,6 +251,7 @@ def main():
         extra = {"p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
                  "mean_ms": res["latency_ms"]["mean"], "failed": failed,
                  "engine": e1.get("device"), "dp_backend": e1.get("dp_backend"), "precision": e1.get("precision"),
+                 "dp_affinity_restores": e1.get("dp_affinity_restores"), "host_cpus": len(os.sched_getaffinity(0)),
                  "device_ms_per_batch": e1.get("avg_device_ms"),
                  "dp_batches_rank0": e1.get("dp_batches", 0) - h0["engine"].get("dp_batches", 0),
                  "requests_parsed_this_rank": h1["total_requests"] - h0["total_requests"],

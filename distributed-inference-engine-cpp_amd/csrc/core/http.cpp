@@ -1,3 +1,4 @@
+#include <pthread.h>
 #include "http.h"
 
 #include <arpa/inet.h>
@@ -258,7 +259,10 @@ int HttpServer::start(const std::string& host, int port, int threads, bool reuse
     epoll_ctl(r->ep, EPOLL_CTL_ADD, r->box->efd, &ev);
     reactors_.push_back(std::move(r));
   }
-  for (auto& r : reactors_) threads_.emplace_back([this, rp = r.get()] { reactor_loop(rp); });
+  for (auto& r : reactors_) threads_.emplace_back([this, rp = r.get()] {
+    pthread_setname_np(pthread_self(), "die-http");
+    reactor_loop(rp);
+  });
   return port_;
 }
 

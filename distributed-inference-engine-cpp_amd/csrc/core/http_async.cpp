@@ -1,3 +1,4 @@
+#include <pthread.h>
 #include "http_async.h"
 
 #include <arpa/inet.h>
@@ -69,7 +70,10 @@ AsyncHttpClient::AsyncHttpClient(Options opt) : opt_(opt) {
     epoll_ctl(L->ep, EPOLL_CTL_ADD, L->efd, &ev);
     loops_.push_back(std::move(L));
   }
-  for (auto& L : loops_) threads_.emplace_back([this, p = L.get()] { run(p); });
+  for (auto& L : loops_) threads_.emplace_back([this, p = L.get()] {
+    pthread_setname_np(pthread_self(), "die-fwd");
+    run(p);
+  });
 }
 
 AsyncHttpClient::~AsyncHttpClient() { stop(); }

@@ -17,6 +17,7 @@
 // every GPU runs the same batch bucket (each rank submits exactly `per` items) so the collectives
 // match.  CPU engines gather through the segment (host communicator), which is what the multi-process
 // CPU tests exercise.
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 
@@ -102,9 +103,13 @@ class DpEngine : public Engine {
     if (rank_ == 0)
       dispatcher_ = std::thread([this] {
         prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // paced dispatch: wake within ~1 us, not 50 us
+        pthread_setname_np(pthread_self(), "die-dp-lead");
         dispatch_loop();
       });
-    else shard_thread_ = std::thread([this] { follower_loop(); });
+    else shard_thread_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "die-dp-shard");
+        follower_loop();
+      });
   }
 
   ~DpEngine() override {
@@ -165,6 +170,7 @@ class DpEngine : public Engine {
     j["dp_backend"] = comm_ ? comm_->backend() : "none";
     j["dp_device_gather"] = device_gather_;
     j["dp_solo"] = solo_;
+    j["dp_affinity_restores"] = rccl_affinity_restores();
     j["dp_batches"] = static_cast<long long>(batches_.load());
     j["dp_subbatches_sent"] = static_cast<long long>(subs_sent_.load());
     j["dp_subbatches_merged"] = static_cast<long long>(subs_merged_.load());

@@ -1,3 +1,4 @@
+#include <pthread.h>
 #include "engine.h"
 
 #include "../core/log.h"
@@ -141,7 +142,10 @@ class CpuEngine : public Engine {
       out_shape_[0] = 1;
     }
     pool_ = std::make_unique<SamplePool>(input_numel());
-    worker_ = std::thread([this] { loop(); });
+    worker_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "die-cpu-exec");
+      loop();
+    });
   }
   ~CpuEngine() override {
     {

@@ -10,6 +10,7 @@
 //    bucket and pipeline slot), D2H of the logits; `pipeline_depth` slots let batch k+1's copies
 //    overlap batch k's forward;
 //  * a completion thread waits for each slot's D2H event in FIFO order and runs the callback.
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -101,6 +102,7 @@ class HipEngine : public Engine {
     if (const char* e = std::getenv("DIE_PACE_LEAD_SCALE")) lead_scale_ = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("DIE_LIVE_BATCH")) use_live_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("DIE_PREP_ON_COMPUTE")) prep_on_compute_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("DIE_COMPLETION_POLL_US")) completion_poll_us_ = std::max(0, std::atoi(e));
     if (branches_) {
       HIP_CHECK(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -256,8 +258,15 @@ class HipEngine : public Engine {
       HIP_CHECK(hipStreamSynchronize(s_compute_));
     }
     for (auto& e : tev_) HIP_CHECK(hipEventCreate(&e));
-    completion_ = std::thread([this] { completion_loop(); });
-    if (n_stage_) stager_ = std::thread([this] { stager_loop(); });
+    completion_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "die-complete");
+      completion_loop();
+    });
+    if (n_stage_)
+      stager_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "die-stager");
+        stager_loop();
+      });
   }
 
   ~HipEngine() override {
@@ -659,6 +668,7 @@ class HipEngine : public Engine {
     j["pack_text"] = d_packed_ != nullptr;
     j["branch_streams"] = branches_;
     j["prep_on_compute"] = prep_on_compute_;
+    j["completion_poll_us"] = completion_poll_us_;
     j["live_batch"] = use_live_;
     j["paced_batches"] = static_cast<long long>(paced_batches_.load());
     {
@@ -1238,7 +1248,15 @@ class HipEngine : public Engine {
       TraceRange tr_done("engine.completion(d2h wait+callback)");
       BatchResult r;
       if (job.error.empty()) {
-        hipError_t e = hipEventSynchronize(sl.ev_d2h);
+        hipError_t e;
+        if (completion_poll_us_ > 0) {
+          // sleep-poll instead of the runtime wait, which was seen spinning a whole CPU even with a
+          // blocking-sync event (gpurun_out/r2_46 threads_*.txt): that CPU serves HTTP/JSON instead
+          while ((e = hipEventQuery(sl.ev_d2h)) == hipErrorNotReady)
+            std::this_thread::sleep_for(std::chrono::microseconds(completion_poll_us_));
+        } else {
+          e = hipEventSynchronize(sl.ev_d2h);
+        }
         if (e != hipSuccess) {
           r.ok = false;
           r.error = std::string("device error: ") + hipGetErrorString(e);
@@ -1365,6 +1383,7 @@ class HipEngine : public Engine {
   static constexpr int kMaxExec = 2;
   int n_exec_ = 1;
   bool branches_ = false;  // side-branch stream in use (PlanOp::join)
+  int completion_poll_us_ = 0;     // DIE_COMPLETION_POLL_US: > 0 = sleep-poll the D2H event (0 = hipEventSynchronize)
   bool prep_on_compute_ = false;  // PREP runs on the compute stream before MAIN (EngineOptions)
   bool use_live_ = true;          // skip the bucket's padding samples (EngineOptions::live_batch)
   double lead_scale_ = 1.0;       // DIE_PACE_LEAD_SCALE (< 1: dispatch later, trading GPU idle for batch size)

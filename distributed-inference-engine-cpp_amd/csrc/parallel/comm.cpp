@@ -1,11 +1,17 @@
 #include "comm.h"
 
+#include <pthread.h>
 #include <rccl/rccl.h>
+#include <sched.h>
 
+#include <atomic>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
 namespace die {
+
+std::atomic<int> g_affinity_restores{0};
 
 namespace {
 
@@ -23,7 +29,21 @@ class RcclComm : public Communicator {
     } else if (!g.wait_id(&id, sizeof(id), timeout_ms)) {
       throw std::runtime_error("timed out waiting for the RCCL unique id from rank 0");
     }
+    // The communicator init may pin the calling thread to the CPUs it deems local to the GPU.  This
+    // thread goes on to create the worker's reactors, parse pool and batcher, which inherit its
+    // mask: restore the mask the process chose (bench.py / worker_main bind per NUMA node).
+    cpu_set_t before;
+    CPU_ZERO(&before);
+    const bool have = pthread_getaffinity_np(pthread_self(), sizeof before, &before) == 0;
     nccl_check(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");
+    if (have) {
+      cpu_set_t after;
+      CPU_ZERO(&after);
+      if (pthread_getaffinity_np(pthread_self(), sizeof after, &after) == 0 && !CPU_EQUAL(&before, &after)) {
+        pthread_setaffinity_np(pthread_self(), sizeof before, &before);
+        g_affinity_restores.fetch_add(1);
+      }
+    }
   }
   ~RcclComm() override {
     if (comm_) ncclCommDestroy(comm_);
@@ -64,5 +84,7 @@ std::unique_ptr<Communicator> make_rccl_comm(DpGroup& g, int timeout_ms) {
   return std::make_unique<RcclComm>(g, timeout_ms);
 }
 std::unique_ptr<Communicator> make_host_comm(DpGroup& g) { return std::make_unique<HostComm>(g); }
+
+int rccl_affinity_restores() { return g_affinity_restores.load(); }
 
 }  // namespace die

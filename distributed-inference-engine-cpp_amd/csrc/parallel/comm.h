@@ -30,5 +30,7 @@ class Communicator {
 // Collective constructor: every rank of `g` must call it (after hipSetDevice on its GPU).
 std::unique_ptr<Communicator> make_rccl_comm(DpGroup& g, int timeout_ms = 120000);
 std::unique_ptr<Communicator> make_host_comm(DpGroup& g);
+// Times an RCCL communicator init changed the calling thread's CPU mask (restored afterwards).
+int rccl_affinity_restores();
 
 }  // namespace die

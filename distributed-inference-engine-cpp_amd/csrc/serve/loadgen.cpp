@@ -1,3 +1,4 @@
+#include <pthread.h>
 #include "loadgen.h"
 
 #include <algorithm>
@@ -95,6 +96,7 @@ Json run_loadgen(const LoadgenOptions& o) {
   std::vector<std::thread> threads;
   for (int c = 0; c < C; ++c) {
     threads.emplace_back([&, c] {
+      pthread_setname_np(pthread_self(), "die-loadgen");
       HttpClient client(o.host, o.port, std::chrono::milliseconds(o.timeout_ms), std::chrono::milliseconds(o.timeout_ms), 2);
       Template tpl;
       if (full) tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(c));

@@ -1,3 +1,4 @@
+#include <pthread.h>
 #include "worker.h"
 
 #include "../core/log.h"
@@ -114,7 +115,10 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
 
   int npt = opt_.parse_threads;
   if (npt < 0) npt = std::max(2, available_cpus() / 4);
-  for (int i = 0; i < npt; ++i) parse_threads_.emplace_back([this] { parse_loop(); });
+  for (int i = 0; i < npt; ++i) parse_threads_.emplace_back([this] {
+      pthread_setname_np(pthread_self(), "die-parse");
+      parse_loop();
+    });
   if (npt > 0) {
     server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
       ParseJob j{std::make_shared<HttpRequest>(std::move(req)), std::move(res)};
