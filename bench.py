@@ -57,6 +57,8 @@ def main():
                          "forward-only (a step = one batch)")
     ap.add_argument("--no-direct", action="store_true", help="skip the extra direct-to-worker measurement")
     ap.add_argument("--gw-client-threads", type=int, default=0, help="gateway forwarding loops (0 = auto)")
+    ap.add_argument("--worker-http-threads", type=int, default=0, help="worker HTTP reactors (0 = auto: CPU share)")
+    ap.add_argument("--gw-http-threads", type=int, default=0, help="gateway HTTP reactors (0 = auto: CPU share)")
     ap.add_argument("--no-local-shm", action="store_true",
                     help="gateway sends co-located workers the body bytes instead of a shared-memory descriptor")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
@@ -144,7 +146,7 @@ def main():
     if args.mode in ("gateway", "http"):
         t_init = time.perf_counter()
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
-                           parse_threads=args.parse_threads)
+                           parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
         t_ready = time.perf_counter()
         gw = None
         target_port = wk.port
@@ -152,7 +154,7 @@ def main():
             # every rank's gateway routes over every rank's worker (ring on request_id)
             ports = hg.all_gather_object(wk.port)
             gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
-                                      local_shm=not args.no_local_shm)
+                                      local_shm=not args.no_local_shm, http_threads=args.gw_http_threads)
             target_port = gw.port
         lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4,
                   seed=1000 + rank, timeout_ms=60000)
