@@ -264,9 +264,15 @@ class DpEngine : public Engine {
                                  std::to_string(opt_.device_id));
       // A solo group forms no RCCL communicator at all: merely having one initialised cost the
       // co-located HTTP/JSON host path ~13 % of throughput on a 16-CPU share (12.4-12.5k vs
-      // 14.3-14.7k req/s, gpurun_out/r2_43; profiles/r2_dp_world1.md).
-      if (!solo_) comm_ = make_rccl_comm(*group_);
-      lo.dp_comm = solo_ ? nullptr : comm_.get();
+      // 14.3-14.7k req/s, gpurun_out/r2_43; profiles/r2_dp_world1.md).  DIE_DP_COMM=host: the
+      // ranks gather their (small: 4 KB per image) logits and decode status through the host
+      // segment instead, every rank loads the weights itself, and no RCCL communicator exists.
+      const char* cb = std::getenv("DIE_DP_COMM");
+      const bool host_comm = cb && std::string(cb) == "host";
+      if (host_comm) comm_ = make_host_comm(*group_);
+      else if (!solo_) comm_ = make_rccl_comm(*group_);
+      lo.dp_comm = solo_ || host_comm ? nullptr : comm_.get();
+      device_decode_ = lo.device_decode;
       std::string why;
       local_ = create_hip_engine(path, lo, &why);
       if (!local_) throw std::runtime_error("dp rank " + std::to_string(rank_) + ": HIP engine unavailable: " + why);
@@ -373,6 +379,23 @@ class DpEngine : public Engine {
         try {
           group_->all_gather_host(mine_rows.data(), gathered.data(), mine_rows.size() * sizeof(float));
           rows = gathered.data();
+          if (device_decode_) {
+            // device-decoded texts: every rank also needs the decode status and token count of
+            // every row (host fallback / size errors are answered by the rank that queued them)
+            std::vector<int> mine_st(2 * static_cast<size_t>(per), 0), all_st(2 * static_cast<size_t>(per) * world_);
+            if (r.ok && r.status)
+              for (int j = 0; j < per; ++j) {
+                mine_st[2 * j] = r.status[j];
+                mine_st[2 * j + 1] = r.ntok ? r.ntok[j] : 0;
+              }
+            group_->all_gather_host(mine_st.data(), all_st.data(), mine_st.size() * sizeof(int));
+            st.resize(B);
+            nt.resize(B);
+            for (int i = 0; i < B; ++i) {
+              st[i] = all_st[2 * static_cast<size_t>(i)];
+              nt[i] = all_st[2 * static_cast<size_t>(i) + 1];
+            }
+          }
         } catch (const std::exception& e) {
           ok = false;
           err = e.what();
@@ -439,6 +462,7 @@ class DpEngine : public Engine {
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<Engine> local_;
   bool device_gather_ = false;
+  bool device_decode_ = false;  // HIP ranks decode JSON text on the device (status rows to gather)
   bool solo_ = false;  // world of one: submit straight to the local engine (no merge loop)
   std::unique_ptr<SamplePool> pool_;
   std::unique_ptr<DpSub> sub_ = std::make_unique<DpSub>();

@@ -6,6 +6,7 @@ logits and decode status, leader D2H of the gathered rows.  Multi-rank DP is cov
 (tests/test_dp.py) with the same sharding code."""
 import json
 import os
+import urllib.error
 import urllib.request
 
 import numpy as np
@@ -16,15 +17,22 @@ from conftest import gpu_available
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
 
 
-@pytest.fixture(params=["solo", "merge"])
+@pytest.fixture(params=["solo", "merge", "merge_host"])
 def dp_path(request, monkeypatch):
     """solo: a world of one feeds its local engine directly; merge: DIE_DP_FORCE_MERGE=1 keeps the
-    multi-rank sub-batch ring + leader merge loop (what N>1 runs) at world=1."""
-    if request.param == "merge":
+    multi-rank sub-batch ring + leader merge loop (what N>1 runs) at world=1, RCCL device gather;
+    merge_host: the same with DIE_DP_COMM=host (logits + decode status through the host segment)."""
+    monkeypatch.delenv("DIE_DP_COMM", raising=False)
+    if request.param.startswith("merge"):
         monkeypatch.setenv("DIE_DP_FORCE_MERGE", "1")
     else:
         monkeypatch.delenv("DIE_DP_FORCE_MERGE", raising=False)
+    if request.param == "merge_host":
+        monkeypatch.setenv("DIE_DP_COMM", "host")
     return request.param
+
+
+BACKEND = {"solo": "none", "merge": "rccl", "merge_host": "host"}
 
 
 def test_dp_engine_rccl_world1_matches_plain_engine(native, models, dp_path):
@@ -36,7 +44,7 @@ def test_dp_engine_rccl_world1_matches_plain_engine(native, models, dp_path):
                        dp_group="die_gpu_dp_%s_%d" % (dp_path, os.getpid()))
     info = dp.refresh_info()
     # solo: no communicator is formed (its host threads cost the serving path ~13 %)
-    assert info["name"].startswith("dp1(none):hip:gfx950" if dp_path == "solo" else "dp1(rccl):hip:gfx950")
+    assert info["name"].startswith("dp1(%s):hip:gfx950" % BACKEND[dp_path])
     assert info["dp_solo"] is (dp_path == "solo")
     for B in (1, 3, 8):
         x = r.synthetic_input(B, cfg, seed=B).reshape(B, -1)
@@ -55,9 +63,8 @@ def test_dp_worker_rccl_world1_http(native, models, dp_path):
     ref_eng = native.Engine(path, device="hip", max_batch=8, autotune=False)
     try:
         h = wk.health()
-        merge = dp_path == "merge"
-        assert h["engine"]["dp_backend"] == ("rccl" if merge else "none")
-        assert h["engine"]["dp_device_gather"] is merge
+        assert h["engine"]["dp_backend"] == BACKEND[dp_path]
+        assert h["engine"]["dp_device_gather"] is (dp_path == "merge")
         assert h["engine"]["dp_solo"] is (dp_path == "solo")
         res = native.loadgen(port=wk.port, connections=8, requests=64, payload="full", input_numel=3 * 64 * 64)
         assert res["ok"] == 64 and res["failed"] == 0
@@ -68,6 +75,18 @@ def test_dp_worker_rccl_world1_http(native, models, dp_path):
                                                     timeout=60).read())
             np.testing.assert_array_equal(np.array(out["output_data"], np.float32), ref_eng.run(x[i:i + 1])[0])
         assert wk.health()["device_decoded"] >= 2
+        # decode status travels with the rows: too many values -> the size error, a subnormal
+        # (device decode flags it) -> host re-parse, same answer as the plain engine
+        vals = [float(v) for v in x[0]]
+        body = json.dumps({"request_id": "big", "input_data": vals + [0.5] * 5}).encode()
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(urllib.request.Request(wk.url + "/infer", data=body), timeout=60)
+        assert ei.value.code == 500 and b"values" in ei.value.read()
+        text = json.dumps({"request_id": "sub", "input_data": vals[:-1] + [7.0]}).replace("7.0]", "1e-45]")
+        out = json.loads(urllib.request.urlopen(urllib.request.Request(wk.url + "/infer", data=text.encode()),
+                                                timeout=60).read())
+        xs = np.array(vals[:-1] + [1e-45], np.float32).reshape(1, -1)
+        np.testing.assert_array_equal(np.array(out["output_data"], np.float32), ref_eng.run(xs)[0])
     finally:
         wk.stop()
         ref_eng.close()
