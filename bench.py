@@ -11,6 +11,12 @@ connections per GPU into that gateway.  Payloads are ResNet-shaped (3x224x224 fl
 ~1.1 MB of JSON) and unique per request, so every request is a real inference (no cache hits).
 Weights are random-init (no checkpoint offline).
 
+After the headline (and only reported as extra keys): the same requests straight to the worker
+(`direct_worker`), and BASELINE config 4 -- ONE data-parallel worker over all N ranks with RCCL
+(weights ncclBroadcast from rank 0, per-batch logits + decode status ncclAllGather over xGMI; at
+N=1 the multi-rank merge path is forced so the communicator still forms) -- run in child processes
+under a watchdog, as `dp_rccl` ({"error": ...} if it fails or hangs; the headline is never lost).
+
 A "step" = --step-requests (500) requests per GPU, so the driver's `--steps 20` times 10,000
 requests per GPU: the reference's run length.  W warmup steps (after engine autotune and graph
 capture), then exactly K timed steps bracketed by barrier + torch.cuda.synchronize(); the max wall
@@ -22,12 +28,16 @@ import argparse
 import json
 import os
 import resource
+import signal
+import subprocess
 import sys
 import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+
+import die_amd  # noqa: E402,F401  (first: sets the HIP runtime environment before anything touches the GPU)
 
 BASELINE_RPS = 522.64  # BASELINE.md / README.md:282
 
@@ -81,6 +91,13 @@ def main():
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
     ap.add_argument("--device", choices=["hip", "cpu"], default="hip",
                     help="cpu: rehearse the multi-rank contract on the host executor (tests; no GPU)")
+    ap.add_argument("--dp-backend", choices=["rccl", "host"], default="rccl",
+                    help="--mode dp: gather logits over RCCL (xGMI) or through the host segment")
+    ap.add_argument("--dp-force-merge", action="store_true",
+                    help="--mode dp at 1 rank: keep the multi-rank merge path (RCCL communicator, collectives)")
+    ap.add_argument("--no-dp", action="store_true", help="skip the extra data-parallel (dp_rccl) measurement")
+    ap.add_argument("--dp-steps", type=int, default=0, help="timed steps of the dp_rccl measurement (0 = steps/2)")
+    ap.add_argument("--dp-timeout", type=float, default=240.0, help="watchdog of the dp_rccl measurement (s)")
     args = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         # n_gpus and global_batch come from --gpus: a torchrun launch must say how many ranks it has
@@ -156,15 +173,18 @@ def main():
             gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
                                       local_shm=not args.no_local_shm, http_threads=args.gw_http_threads)
             target_port = gw.port
-        lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4,
-                  seed=1000 + rank, timeout_ms=60000)
-        native.loadgen(port=target_port, requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, **lg)
+        # every pass and rank gets its own payload seed: no input recurs across the warm-up, timed and
+        # direct passes (cache_hits_timed below proves it)
+        lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4, timeout_ms=60000)
+        native.loadgen(port=target_port, requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank,
+                       seed=1000 + rank, **lg)
         h0 = wk.health()
         g0 = gw.stats() if gw else {}
         barrier()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
-        res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, **lg)
+        res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank,
+                             seed=2000 + rank, **lg)
         barrier()
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
@@ -178,6 +198,7 @@ def main():
         extra = {
             "p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
             "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+            "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
             "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
             "precision": e1.get("precision"),
@@ -192,6 +213,8 @@ def main():
             "pace_lead_ms": e1.get("avg_pace_lead_ms"), "submit_us_avg": e1.get("staging_diag", {}).get("submit_us_avg"),
             "pace_input_ms": e1.get("pace_input_ms"), "pace_margin_ms": e1.get("pace_margin_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
+            "stages_p99_us": {k: round(v.get("p99_us", 0.0), 1) for k, v in h1.get("stages_us", {}).items()},
+            "engine_options": e1.get("options"),
             # host CPU spent per request by this process (client + gateway + worker threads together)
             "cpu_us_per_request": {"user": round((ru1.ru_utime - ru0.ru_utime) * 1e6 / max(1, res["ok"]), 1),
                                    "sys": round((ru1.ru_stime - ru0.ru_stime) * 1e6 / max(1, res["ok"]), 1)},
@@ -207,7 +230,8 @@ def main():
             barrier()
             rd0 = resource.getrusage(resource.RUSAGE_SELF)
             td = time.perf_counter()
-            rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank, **lg)
+            rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank,
+                                seed=3000 + rank, **lg)
             barrier()
             el = time.perf_counter() - td
             rd1 = resource.getrusage(resource.RUSAGE_SELF)
@@ -219,6 +243,8 @@ def main():
         if gw:
             gw.stop()
         wk.stop()
+        if not args.no_dp:
+            extra["dp_rccl"] = _dp_child(args, hg, rank, world)
     elif args.mode == "dp":
         # BASELINE config 4: ONE data-parallel worker over all ranks.  Every rank serves HTTP on the
         # same port (SO_REUSEPORT) and parses its own connections' requests; the leader merges the
@@ -235,16 +261,17 @@ def main():
             port = sk.getsockname()[1]
             sk.close()
         port = hg.broadcast_object(port, src=0)
-        eng_opts = dict(engine_opts, dp_world=world, dp_group=group, dp_rank=rank)
+        eng_opts = dict(engine_opts, dp_world=world, dp_group=group, dp_rank=rank, dp_backend=args.dp_backend,
+                        dp_force_merge=args.dp_force_merge)
         wk = native.Worker(model, node_id="dp-r%d" % rank, port=port, reuse_port=True, max_batch=Btot,
                            engine=eng_opts, parse_threads=args.parse_threads)
         lg = dict(port=port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
-                  seed=1000 + rank, timeout_ms=60000)
-        native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, **lg)
+                  timeout_ms=60000)
+        native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, seed=1000 + rank, **lg)
         h0 = wk.health()
         barrier()
         t0 = time.perf_counter()
-        res = native.loadgen(requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, **lg)
+        res = native.loadgen(requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, seed=2000 + rank, **lg)
         barrier()
         elapsed = time.perf_counter() - t0
         ok, failed = res["ok"], res["failed"]
@@ -252,7 +279,10 @@ def main():
         e1 = h1["engine"]
         extra = {"p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
                  "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+                 "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
                  "engine": e1.get("device"), "dp_backend": e1.get("dp_backend"), "precision": e1.get("precision"),
+                 "dp_solo": e1.get("dp_solo"), "dp_world": e1.get("dp_world"),
+                 "dp_shard_failed_items": e1.get("dp_shard_failed_items"),
                  "dp_affinity_restores": e1.get("dp_affinity_restores"), "host_cpus": len(os.sched_getaffinity(0)),
                  "device_ms_per_batch": e1.get("avg_device_ms"),
                  "dp_batches_rank0": e1.get("dp_batches", 0) - h0["engine"].get("dp_batches", 0),
@@ -320,6 +350,63 @@ def main():
         out.update({k: v for k, v in extra.items() if v is not None})
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     hg.close()
+
+
+def _dp_child(args, hg, rank, world):
+    """BASELINE config 4 after the headline: ONE data-parallel worker over all ranks (RCCL weight
+    broadcast + per-batch all-gather; at world 1 the merge path is forced so the communicator forms),
+    each rank in a child process on a fresh rendezvous, under a watchdog: a failing or hung DP run
+    costs this key, never the headline.  Returns rank 0's result (extra keys of that run)."""
+    port = 0
+    if rank == 0:
+        import socket
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+    port = hg.broadcast_object(port, src=0)
+    steps = args.dp_steps or max(2, args.steps // 2)
+    cmd = [sys.executable, os.path.abspath(__file__), "--mode", "dp", "--gpus", str(world), "--steps", str(steps),
+           "--warmup", str(max(1, args.warmup // 2)), "--step-requests", str(args.step_requests),
+           "--batch", str(args.batch), "--connections", str(args.connections), "--precision", args.precision,
+           "--arch", args.arch, "--pipeline-depth", str(args.pipeline_depth), "--dp-backend", "rccl",
+           "--device", args.device]
+    if world == 1:
+        cmd.append("--dp-force-merge")
+    if args.model:
+        cmd += ["--model", args.model]
+    # a fresh rendezvous of its own (rank 0's child hosts the store): not torchrun's agent store
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    out = {"error": "no result"}
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=args.dp_timeout)
+        if p.returncode == 0 and rank == 0:
+            out = json.loads(so.decode().strip().splitlines()[-1])
+        elif p.returncode == 0:
+            out = {}
+        else:
+            out = {"error": "dp run exited %d: %s" % (p.returncode, se.decode(errors="replace")[-400:])}
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        out = {"error": "dp run exceeded the %.0f s watchdog" % args.dp_timeout}
+    except Exception as e:  # noqa: BLE001 (the headline must survive anything here)
+        out = {"error": "dp run failed: %r" % (e,)}
+    hg.barrier()
+    if rank != 0:
+        return None
+    keep = ("value", "p50_ms", "p99_ms", "failed", "avg_dp_batch", "dp_backend", "dp_world", "dp_solo",
+            "device_ms_per_batch", "engine", "cache_hits_timed", "dp_shard_failed_items", "error")
+    res = {k: out[k] for k in keep if k in out}
+    if "value" in res:
+        res["requests_per_s"] = res.pop("value")
+        res["requests"] = out.get("config", {}).get("requests")
+    res["wall_s"] = round(time.perf_counter() - t0, 1)
+    return res
 
 
 if __name__ == "__main__":

@@ -8,6 +8,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <csignal>
 #include <iostream>
@@ -16,6 +17,7 @@
 
 #include "../core/flags.h"
 #include "../core/log.h"
+#include "../core/sysinfo.h"
 #include "../serve/worker.h"
 
 extern char** environ;
@@ -31,24 +33,47 @@ std::vector<int> parse_devices(const std::string& s) {
   return d;
 }
 
-// worker_node --dp-follower <model> --dp-group G --dp-rank R --dp-world N --device-id D [--max-batch M]
+// Engine options from the command line: the same flags for an ingesting worker, a DP rank it
+// spawns and a compute-only follower, so every rank of a group plans the same program.
+die::EngineOptions engine_options_from_flags(const die::Flags& f, const std::string& default_device) {
+  die::EngineOptions eo;
+  eo.device = f.str("device", default_device);
+  eo.device_id = static_cast<int>(f.i("device-id", 0));
+  eo.max_batch = static_cast<int>(f.i("max-batch", 32));
+  eo.precision = f.str("precision", "fp32");
+  eo.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 3));
+  eo.use_graphs = !f.b("no-graphs");
+  eo.device_decode = !f.b("no-device-decode");
+  eo.stage_slots = static_cast<int>(f.i("stage-slots", 0));
+  eo.pace = !f.b("no-pace");
+  eo.pack_text = !f.b("no-pack-text");
+  eo.branch_streams = f.b("branch-streams");
+  eo.exec_streams = static_cast<int>(f.i("exec-streams", 1));
+  eo.tune_cache = f.str("tune-cache", "auto");
+  eo.copy_streams = static_cast<int>(f.i("copy-streams", 0));
+  eo.bucket_div = static_cast<int>(f.i("bucket-div", 8));
+  eo.coarse_buckets = f.b("coarse-buckets");
+  eo.pace_lead_scale = f.f("pace-lead-scale", 1.0);
+  eo.completion_poll_us = static_cast<int>(f.i("completion-poll-us", 0));
+  eo.bn_on_load = f.b("bn-on-load");
+  eo.tune_cold = !f.b("tune-warm");
+  eo.dp_backend = f.str("dp-backend", "rccl");
+  eo.dp_force_merge = f.b("dp-force-merge");
+  eo.fail_batch_every = static_cast<int>(f.i("fail-batch-every", 0));
+  return eo;
+}
+
+// worker_node --dp-follower <model> --dp-group G --dp-rank R --dp-world N --device-id D [engine flags]
 int follower_main(die::Flags& f, sigset_t& sigs) {
   const auto& pos = f.positional();
   if (pos.empty()) {
     std::cerr << "--dp-follower needs the model path" << std::endl;
     return 1;
   }
-  die::EngineOptions eo;
-  eo.device = f.str("device", "hip");
-  eo.device_id = static_cast<int>(f.i("device-id", 0));
-  eo.max_batch = static_cast<int>(f.i("max-batch", 32));
-  eo.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 3));
-  eo.use_graphs = !f.b("no-graphs");
-  eo.device_decode = !f.b("no-device-decode");
+  die::EngineOptions eo = engine_options_from_flags(f, "hip");
   eo.dp_group = f.str("dp-group", "");
   eo.dp_rank = static_cast<int>(f.i("dp-rank", 1));
   eo.dp_world = static_cast<int>(f.i("dp-world", 2));
-  eo.precision = f.str("precision", "fp32");
   std::atomic<bool> stop{false};
   std::thread sig_thread([&] {
     int sig = 0;
@@ -69,11 +94,16 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
   return rc;
 }
 
+const std::vector<std::string> kBoolFlags = {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower",
+                                             "no-shm", "reuse-port", "dp-no-ingest", "no-pace", "no-pack-text",
+                                             "branch-streams", "coarse-buckets", "bn-on-load", "tune-warm",
+                                             "dp-force-merge"};
+
 }  // namespace
 
 int main(int argc, char** argv) {
-  die::Flags f(argc, argv, {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower", "no-shm",
-                            "reuse-port", "dp-no-ingest", "no-pace", "no-pack-text", "branch-streams"});
+  die::configure_hip_runtime_env();  // before anything touches HIP (spawned DP ranks inherit it)
+  die::Flags f(argc, argv, kBoolFlags);
   const auto& pos = f.positional();
   if (f.b("dp-follower")) {
     sigset_t fs;
@@ -91,6 +121,9 @@ int main(int argc, char** argv) {
               << "  --deadline (wait up to the timeout for full batches; default: greedy)\n"
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (3)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
+              << "  --no-pace  --no-pack-text  --branch-streams  --copy-streams N (0 = auto)  --bucket-div N (8)  --coarse-buckets\n"
+              << "  --pace-lead-scale X (1)  --completion-poll-us N (0)  --bn-on-load  --tune-warm  --tune-cache PATH|auto|''\n"
+              << "  --dp-backend rccl|host (rccl)  --dp-force-merge  --fail-batch-every N (fault injection, 0 = off)\n"
               << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
               << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
@@ -129,17 +162,7 @@ int main(int argc, char** argv) {
   o.policy = f.b("deadline") ? die::BatchPolicy::DEADLINE : die::BatchPolicy::GREEDY;
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.parse_threads = static_cast<int>(f.i("parse-threads", -1));
-  o.engine.device = f.str("device", "auto");
-  o.engine.device_id = static_cast<int>(f.i("device-id", 0));
-  o.engine.precision = f.str("precision", "fp32");
-  o.engine.pipeline_depth = static_cast<int>(f.i("pipeline-depth", 3));
-  o.engine.use_graphs = !f.b("no-graphs");
-  o.engine.device_decode = !f.b("no-device-decode");
-  o.engine.stage_slots = static_cast<int>(f.i("stage-slots", 0));
-  o.engine.pace = !f.b("no-pace");
-  o.engine.pack_text = !f.b("no-pack-text");
-  o.engine.branch_streams = f.b("branch-streams");
-  o.engine.exec_streams = static_cast<int>(f.i("exec-streams", 1));
+  o.engine = engine_options_from_flags(f, "auto");
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);
   o.fault_latency_ms = static_cast<int>(f.i("fault-latency-ms", 0));
@@ -166,22 +189,38 @@ int main(int argc, char** argv) {
     // ingest on every rank: all ranks listen on the same port (needs a fixed port)
     const bool ingest = !f.b("dp-no-ingest") && o.port > 0;
     o.reuse_port = o.reuse_port || ingest;
+    // Every rank gets this worker's own flags (engine AND serving: precision, depth, batch
+    // timeout, cache, parse/http threads, shm, log level, ...), then its rank-specific ones, which
+    // win (later flags override earlier ones): all ranks plan the same program.
+    std::vector<std::string> shared;
+    for (int k = 1; k < argc; ++k) {
+      const std::string a = argv[k];
+      if (a.rfind("--", 0) != 0) continue;  // positionals are rank-specific
+      const std::string key = a.substr(2, a.find('=') == std::string::npos ? std::string::npos : a.find('=') - 2);
+      const bool is_bool = std::find(kBoolFlags.begin(), kBoolFlags.end(), key) != kBoolFlags.end();
+      const bool has_value = a.find('=') == std::string::npos && !is_bool && k + 1 < argc;
+      if (key == "devices" || key == "dp-no-ingest" || key == "device-id" || key == "reuse-port") {
+        if (has_value) ++k;
+        continue;
+      }
+      shared.push_back(a);
+      if (has_value) shared.push_back(argv[++k]);
+    }
     for (size_t r = 1; r < devices.size(); ++r) {
       std::vector<std::string> args;
       if (ingest) {
-        args = {argv[0], std::to_string(o.port), o.node_id + "-r" + std::to_string(r), o.model_path, "--reuse-port",
-                "--host", o.host, "--precision", o.engine.precision};
+        args = {argv[0], std::to_string(o.port), o.node_id + "-r" + std::to_string(r), o.model_path};
       } else {
         args = {argv[0], "--dp-follower", o.model_path};
       }
+      args.insert(args.end(), shared.begin(), shared.end());
+      if (ingest) args.push_back("--reuse-port");
       for (const std::string& a : {std::string("--dp-group"), o.engine.dp_group, std::string("--dp-rank"),
                                    std::to_string(r), std::string("--dp-world"), std::to_string(devices.size()),
                                    std::string("--device-id"), std::to_string(devices[r]), std::string("--device"),
                                    o.engine.device, std::string("--max-batch"), std::to_string(o.max_batch),
-                                   std::string("--pipeline-depth"), std::to_string(o.engine.pipeline_depth)})
+                                   std::string("--precision"), o.engine.precision})
         args.push_back(a);
-      if (!o.engine.use_graphs) args.push_back("--no-graphs");
-      if (!o.engine.device_decode) args.push_back("--no-device-decode");
       std::vector<char*> av;
       for (auto& a : args) av.push_back(const_cast<char*>(a.c_str()));
       av.push_back(nullptr);

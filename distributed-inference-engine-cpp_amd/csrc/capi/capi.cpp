@@ -17,6 +17,7 @@
 #include "../serve/consistent_hash.h"
 #include "../serve/gateway.h"
 #include "../serve/loadgen.h"
+#include "../parallel/dp_layout.h"
 #include "../serve/lru_cache.h"
 #include "../serve/worker.h"
 
@@ -86,6 +87,17 @@ EngineOptions engine_opts(const Json& j) {
   e.dp_rank = jget<int>(j, "dp_rank", e.dp_rank);
   e.dp_group = jget<std::string>(j, "dp_group", e.dp_group);
   e.dp_arena_mb = static_cast<size_t>(jget<long>(j, "dp_arena_mb", 0));
+  e.dp_backend = jget<std::string>(j, "dp_backend", e.dp_backend);
+  e.dp_force_merge = jget<bool>(j, "dp_force_merge", e.dp_force_merge);
+  e.cpu_threads = jget<int>(j, "cpu_threads", e.cpu_threads);
+  e.copy_streams = jget<int>(j, "copy_streams", e.copy_streams);
+  e.bucket_div = jget<int>(j, "bucket_div", e.bucket_div);
+  e.coarse_buckets = jget<bool>(j, "coarse_buckets", e.coarse_buckets);
+  e.pace_lead_scale = jget<double>(j, "pace_lead_scale", e.pace_lead_scale);
+  e.completion_poll_us = jget<int>(j, "completion_poll_us", e.completion_poll_us);
+  e.bn_on_load = jget<bool>(j, "bn_on_load", e.bn_on_load);
+  e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
+  e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);
   return e;
 }
 
@@ -555,23 +567,66 @@ char* die_gateway_stats(void* g) { return dup(static_cast<Gateway*>(g)->getStats
 void die_gateway_stop(void* g) { static_cast<Gateway*>(g)->stop(); }
 void die_gateway_destroy(void* g) { delete static_cast<Gateway*>(g); }
 
+static LoadgenOptions loadgen_opts(const Json& j) {
+  LoadgenOptions o;
+  o.host = jget<std::string>(j, "host", o.host);
+  o.port = jget<int>(j, "port", o.port);
+  o.path = jget<std::string>(j, "path", o.path);
+  o.connections = jget<int>(j, "connections", o.connections);
+  o.requests = jget<long>(j, "requests", o.requests);
+  o.warmup = jget<long>(j, "warmup", o.warmup);
+  o.payload = jget<std::string>(j, "payload", o.payload);
+  o.input_numel = static_cast<size_t>(jget<long>(j, "input_numel", static_cast<long>(o.input_numel)));
+  o.decimals = jget<int>(j, "decimals", o.decimals);
+  o.distinct = jget<long>(j, "distinct", o.distinct);
+  o.timeout_ms = jget<int>(j, "timeout_ms", o.timeout_ms);
+  o.seed = static_cast<uint64_t>(jget<long>(j, "seed", static_cast<long>(o.seed)));
+  o.id_prefix = jget<std::string>(j, "id_prefix", o.id_prefix);
+  o.verify_tol = jget<double>(j, "verify_tol", o.verify_tol);
+  return o;
+}
+
+// ---- data-parallel row bookkeeping (parallel/dp_layout.h), for the CPU unit tests ----
+// per <= 0: ceil(B / world).  Returns rank r's shard size and its first item in *begin.
+int die_dp_shard(int B, int world, int per, int r, int* begin) {
+  const DpLayout L = per > 0 ? DpLayout::with_per(B, world, per) : DpLayout::make(B, world);
+  *begin = L.shard_begin(r);
+  return L.shard_count(r);
+}
+int die_dp_per(int B, int world) { return DpLayout::make(B, world).per; }
+void die_dp_items_from_gathered(int B, int world, int per, const int* gathered, long stride, int* out) {
+  dp_items_from_gathered(DpLayout::with_per(B, world, per), gathered, static_cast<size_t>(stride), out);
+}
+void die_dp_rows_from_gathered(int B, int world, int per, const float* gathered, long rows_per_rank, long row_len,
+                               float* out) {
+  dp_rows_from_gathered(DpLayout::with_per(B, world, per), gathered, static_cast<size_t>(rows_per_rank),
+                        static_cast<size_t>(row_len), out);
+}
+void die_dp_item_ok(int B, int world, int per, const int* rank_ok, unsigned char* out) {
+  const auto ok = dp_item_ok(DpLayout::with_per(B, world, per), rank_ok);
+  std::copy(ok.begin(), ok.end(), out);
+}
+
 char* die_loadgen_run(const char* opts_json, char** err) {
   try {
-    Json j = Json::parse(opts_json);
-    LoadgenOptions o;
-    o.host = jget<std::string>(j, "host", o.host);
-    o.port = jget<int>(j, "port", o.port);
-    o.path = jget<std::string>(j, "path", o.path);
-    o.connections = jget<int>(j, "connections", o.connections);
-    o.requests = jget<long>(j, "requests", o.requests);
-    o.warmup = jget<long>(j, "warmup", o.warmup);
-    o.payload = jget<std::string>(j, "payload", o.payload);
-    o.input_numel = static_cast<size_t>(jget<long>(j, "input_numel", static_cast<long>(o.input_numel)));
-    o.decimals = jget<int>(j, "decimals", o.decimals);
-    o.distinct = jget<long>(j, "distinct", o.distinct);
-    o.timeout_ms = jget<int>(j, "timeout_ms", o.timeout_ms);
-    o.seed = static_cast<uint64_t>(jget<long>(j, "seed", static_cast<long>(o.seed)));
-    o.id_prefix = jget<std::string>(j, "id_prefix", o.id_prefix);
+    return dup(run_loadgen(loadgen_opts(Json::parse(opts_json))).dump());
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+// Verify mode: k distinct inputs (k x input_numel floats) cycled over the requests, every answer
+// compared with `expected` (k x out_numel floats).
+char* die_loadgen_run_verify(const char* opts_json, const float* inputs, long k, const float* expected, long out_numel,
+                             char** err) {
+  try {
+    LoadgenOptions o = loadgen_opts(Json::parse(opts_json));
+    o.payload = "verify";
+    o.verify_inputs = inputs;
+    o.verify_expected = expected;
+    o.verify_count = static_cast<size_t>(k);
+    o.output_numel = static_cast<size_t>(out_numel);
     return dup(run_loadgen(o).dump());
   } catch (const std::exception& e) {
     set_err(err, e.what());

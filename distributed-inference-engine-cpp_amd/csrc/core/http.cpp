@@ -181,6 +181,19 @@ void Responder::defer(std::function<HttpResponse()> build) const {
   state_->box->post(Mailbox::Item{state_->conn_id, state_->keep_alive, HttpResponse{}, std::move(build)});
 }
 
+namespace {
+bool is_loopback(const sockaddr_storage& a) {
+  if (a.ss_family == AF_INET)
+    return (ntohl(reinterpret_cast<const sockaddr_in&>(a).sin_addr.s_addr) >> 24) == 127;
+  if (a.ss_family == AF_INET6) {
+    const in6_addr& v6 = reinterpret_cast<const sockaddr_in6&>(a).sin6_addr;
+    if (IN6_IS_ADDR_LOOPBACK(&v6)) return true;
+    return IN6_IS_ADDR_V4MAPPED(&v6) && v6.s6_addr[12] == 127;
+  }
+  return a.ss_family == AF_UNIX;
+}
+}  // namespace
+
 struct HttpServer::Conn {
   int fd = -1;
   uint64_t id = 0;
@@ -195,6 +208,7 @@ struct HttpServer::Conn {
   bool busy = false;       // a request is being handled
   bool peer_eof = false;
   bool close_after = false;
+  bool loopback = false;   // peer address is 127.0.0.0/8 or ::1
   // output
   std::string out_head, out_body;
   size_t out_off = 0;      // offset across head+body
@@ -453,6 +467,7 @@ void HttpServer::reactor_loop(Reactor* r) {
         c->in.erase(0, he + 4);
         c->headers_done = true;
         c->req.t_headers = std::chrono::steady_clock::now();
+        c->req.peer_loopback = c->loopback;
         c->ext = BodyBuffer{};
         if (!c->chunked && body_alloc_ && c->body_len >= body_alloc_min_ && c->body_len > 0) {
           c->ext = body_alloc_(c->body_len + 64);
@@ -583,11 +598,14 @@ void HttpServer::reactor_loop(Reactor* r) {
       const uint64_t tag = events[i].data.u64;
       if (tag == 0) {
         while (true) {
-          int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          sockaddr_storage peer{};
+          socklen_t plen = sizeof peer;
+          int fd = ::accept4(listen_fd_, reinterpret_cast<sockaddr*>(&peer), &plen, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (fd < 0) break;
           set_nodelay(fd);
           auto c = std::make_unique<Conn>();
           c->fd = fd;
+          c->loopback = is_loopback(peer);
           c->id = (r->next_id++) + 16;  // 0/1 reserved
           epoll_event ev{};
           ev.events = EPOLLIN | EPOLLRDHUP;

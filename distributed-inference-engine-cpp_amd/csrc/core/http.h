@@ -43,6 +43,7 @@ struct HttpRequest {
   size_t ext_len = 0;
   std::shared_ptr<void> ext_owner;
   bool keep_alive = true;
+  bool peer_loopback = false;  // the connection comes from this host (127.0.0.0/8, ::1)
   std::chrono::steady_clock::time_point t_headers{};  // when the request head was parsed
   std::string_view header(std::string_view name) const;  // name must be lower-case
   std::string_view body_view() const { return ext_body ? std::string_view(ext_body, ext_len) : std::string_view(body); }

@@ -6,7 +6,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cerrno>
+#include <cstdio>
+#include <random>
 #include <cstdlib>
 #include <cstring>
 #include <iterator>
@@ -17,10 +20,25 @@ namespace die {
 namespace {
 constexpr size_t kGrain = 4096;
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// "/die_gw_<...>_<16 hex digits>": the trailing random token makes a segment name unguessable, so a
+// descriptor can only come from the gateway that created the arena (shm_arena_name).
 bool valid_name(const std::string& n) {
-  return n.rfind("/die_gw_", 0) == 0 && n.find('/', 1) == std::string::npos && n.size() < 200;
+  if (n.rfind("/die_gw_", 0) != 0 || n.find('/', 1) != std::string::npos || n.size() >= 200) return false;
+  const size_t u = n.rfind('_');
+  if (u == std::string::npos || n.size() - u - 1 != 16) return false;
+  for (size_t i = u + 1; i < n.size(); ++i)
+    if (!std::isxdigit(static_cast<unsigned char>(n[i]))) return false;
+  return true;
 }
 }  // namespace
+
+std::string shm_arena_name(const std::string& stem) {
+  std::random_device rd;
+  const uint64_t token = (static_cast<uint64_t>(rd()) << 32) ^ rd();
+  char hex[17];
+  std::snprintf(hex, sizeof hex, "%016llx", static_cast<unsigned long long>(token));
+  return "/die_gw_" + stem + "_" + hex;
+}
 
 std::shared_ptr<ShmArena> ShmArena::create(const std::string& name, size_t bytes, std::string* error) {
   auto fail = [&](const std::string& why) -> std::shared_ptr<ShmArena> {
@@ -108,7 +126,8 @@ size_t ShmArena::in_use() const {
   return in_use_;
 }
 
-bool ShmReader::resolve(std::string_view desc, const char** data, size_t* len, std::string* error) {
+bool ShmReader::resolve(std::string_view desc, const char** data, size_t* len, std::string* error,
+                        std::shared_ptr<const void>* keep) {
   const size_t c2 = desc.rfind(':');
   const size_t c1 = c2 == std::string_view::npos || c2 == 0 ? std::string_view::npos : desc.rfind(':', c2 - 1);
   if (c1 == std::string_view::npos) {
@@ -124,7 +143,7 @@ bool ShmReader::resolve(std::string_view desc, const char** data, size_t* len, s
     *error = "malformed shm descriptor";
     return false;
   }
-  Map m;
+  std::shared_ptr<const Map> m;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = maps_.find(name);
@@ -146,21 +165,42 @@ bool ShmReader::resolve(std::string_view desc, const char** data, size_t* len, s
         *error = "cannot map shm segment " + name;
         return false;
       }
-      it = maps_.emplace(name, Map{static_cast<const char*>(p), static_cast<size_t>(st.st_size)}).first;
+      // A new gateway arena: drop views of arenas whose segment is gone (a restarted gateway's
+      // old arena is unlinked; without this every worker would keep its pages pinned).  In-flight
+      // parses hold their own reference, so the unmap waits for them.
+      for (auto o = maps_.begin(); o != maps_.end();) {
+        const int ofd = shm_open(o->first.c_str(), O_RDONLY, 0);
+        if (ofd < 0 && errno == ENOENT) {
+          o = maps_.erase(o);
+          unmapped_++;
+          continue;
+        }
+        if (ofd >= 0) close(ofd);
+        ++o;
+      }
+      auto map = std::shared_ptr<Map>(new Map{static_cast<const char*>(p), static_cast<size_t>(st.st_size)}, [](Map* mp) {
+        munmap(const_cast<char*>(mp->base), mp->size);
+        delete mp;
+      });
+      it = maps_.emplace(name, std::move(map)).first;
     }
     m = it->second;
   }
-  if (off > m.size || n > m.size - off || m.size - off - n < 64) {
+  if (off > m->size || n > m->size - off || m->size - off - n < 64) {
     *error = "shm range outside the segment";
     return false;
   }
-  *data = m.base + off;
+  *data = m->base + off;
   *len = static_cast<size_t>(n);
+  if (keep) *keep = m;
   return true;
 }
 
-ShmReader::~ShmReader() {
-  for (auto& kv : maps_) munmap(const_cast<char*>(kv.second.base), kv.second.size);
+size_t ShmReader::mapped() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return maps_.size();
 }
+
+ShmReader::~ShmReader() = default;
 
 }  // namespace die

@@ -7,6 +7,7 @@
 // protocol to remote workers stays plain HTTP/JSON.
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <map>
@@ -18,9 +19,13 @@
 
 namespace die {
 
+// A fresh arena name "/die_gw_<stem>_<16 hex digits of a random token>".  Workers only accept
+// descriptors of names in this form, so another client cannot point a worker at a guessed segment.
+std::string shm_arena_name(const std::string& stem);
+
 class ShmArena {
  public:
-  // Create `name` (leading '/'; must start with "/die_gw_") of `bytes`, with the pages reserved up
+  // Create `name` (from shm_arena_name) of `bytes`, with the pages reserved up
   // front (posix_fallocate), so a full /dev/shm fails here instead of faulting later.  Returns
   // nullptr (and sets *error) when shared memory is unavailable.
   static std::shared_ptr<ShmArena> create(const std::string& name, size_t bytes, std::string* error = nullptr);
@@ -45,12 +50,17 @@ class ShmArena {
   size_t in_use_ = 0;
 };
 
-// Read-only views of arenas created by other processes, mapped once per segment name.
+// Read-only views of arenas created by other processes, mapped once per segment name.  Views of
+// segments that no longer exist are unmapped when a new segment is first seen.
 class ShmReader {
  public:
-  // Resolve "<segment>:<offset>:<length>"; the view is followed by >= 64 readable bytes.  Returns
-  // false with *error set for a malformed descriptor, a foreign segment name or a range outside it.
-  bool resolve(std::string_view desc, const char** data, size_t* len, std::string* error);
+  // Resolve "<segment>:<offset>:<length>"; the view is followed by >= 64 readable bytes and stays
+  // valid while *keep (if given) is held.  Returns false with *error set for a malformed
+  // descriptor, a foreign segment name or a range outside it.
+  bool resolve(std::string_view desc, const char** data, size_t* len, std::string* error,
+               std::shared_ptr<const void>* keep = nullptr);
+  size_t mapped() const;
+  long long unmapped() const { return unmapped_.load(); }
   ~ShmReader();
 
  private:
@@ -58,8 +68,9 @@ class ShmReader {
     const char* base = nullptr;
     size_t size = 0;
   };
-  std::mutex mu_;
-  std::unordered_map<std::string, Map> maps_;
+  mutable std::mutex mu_;
+  std::unordered_map<std::string, std::shared_ptr<const Map>> maps_;
+  std::atomic<long long> unmapped_{0};
 };
 
 }  // namespace die

@@ -14,6 +14,16 @@
 
 namespace die {
 
+// HIP runtime environment of a serving process; call first thing in main(), before any HIP call
+// (the runtime reads it once, at initialisation).  GPU_MAX_HW_QUEUES = 8: HIP shares hardware
+// queues between streams beyond that limit (default 4), and the engine's 3-4 streams plus an RCCL
+// communicator's internal ones then serialise copies behind kernels (data-parallel ranks lost
+// 13-15 % of throughput at 4; profiles/r3_rccl_hw_queues.md).  Explicit settings win.
+inline void configure_hip_runtime_env() {
+  setenv("GPU_MAX_HW_QUEUES", "8", 0);
+  setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
+}
+
 inline int available_cpus() {
   static const int n = [] {
     int cpus = static_cast<int>(std::thread::hardware_concurrency());

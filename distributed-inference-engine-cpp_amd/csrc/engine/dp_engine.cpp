@@ -24,9 +24,11 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <vector>
 #include <stdexcept>
 #include <thread>
 
@@ -34,11 +36,35 @@
 #include "../onnx/onnx_model.h"
 #include "../parallel/comm.h"
 #include "../parallel/dp_group.h"
+#include "../parallel/dp_layout.h"
 #include "engine.h"
 
 namespace die {
 
 namespace {
+
+// 64-bit FNV-1a over the model file: ranks must load the same bytes (plan signature).
+uint64_t file_hash(const std::string& path) {
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return 0;
+  uint64_t h = 0xcbf29ce484222325ull;
+  std::vector<unsigned char> buf(1 << 20);
+  size_t n;
+  while ((n = std::fread(buf.data(), 1, buf.size(), f)) > 0)
+    for (size_t i = 0; i < n; ++i) h = (h ^ buf[i]) * 0x100000001b3ull;
+  std::fclose(f);
+  return h;
+}
+
+// What every rank's local engine must agree on before the first collective: the program (model
+// bytes, precision, device type, local batch and the plan-shaping options) and the gather backend.
+std::string plan_signature(const std::string& path, const EngineOptions& o, int local_max) {
+  char h[17];
+  std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(file_hash(path)));
+  return std::string(h) + "|" + (o.device == "cpu" ? "cpu" : "hip") + "|" + o.precision + "|b" +
+         std::to_string(local_max) + "|" + o.dp_backend + "|dec" + std::to_string(o.device_decode) + "|pk" +
+         std::to_string(o.pack_text) + "|br" + std::to_string(o.branch_streams) + "|bn" + std::to_string(o.bn_on_load);
+}
 
 size_t model_input_numel(const std::string& path) {
   onnx::Model m = onnx::load_onnx(path);
@@ -86,10 +112,16 @@ class DpEngine : public Engine {
     // A group of one has nothing to merge or gather: its batcher feeds a plain local engine
     // directly (same pacing, slots and pinned staging as a plain worker) instead of queueing
     // sub-batches in the shared arena for the leader's merge loop, and no communicator is formed.
-    // DIE_DP_FORCE_MERGE=1 keeps the N>1 path (RCCL communicator, arena staging, merge loop,
-    // device gather) at world=1 for measuring and testing it.
-    const char* fm = std::getenv("DIE_DP_FORCE_MERGE");
-    solo_ = world_ == 1 && !(fm && std::atoi(fm) != 0);
+    // EngineOptions::dp_force_merge keeps the N>1 path (RCCL communicator, arena staging, merge
+    // loop, device gather) at world=1 for measuring and testing it.
+    solo_ = world_ == 1 && !opt.dp_force_merge;
+    // every rank must plan the same program before any collective sizes a buffer from its own plan
+    group_->publish_signature(plan_signature(path, opt_, local_max_));
+    std::string why;
+    if (!group_->check_signatures(600000, &why)) {
+      if (rank_ == 0) group_->stop();
+      throw std::runtime_error(why);
+    }
     build_local(path);
     if (rank_ == 0) {
       if (!group_->wait_joined(600000)) throw std::runtime_error("dp followers did not join");
@@ -170,10 +202,12 @@ class DpEngine : public Engine {
     j["dp_backend"] = comm_ ? comm_->backend() : "none";
     j["dp_device_gather"] = device_gather_;
     j["dp_solo"] = solo_;
+    j["dp_force_merge"] = opt_.dp_force_merge;
     j["dp_affinity_restores"] = rccl_affinity_restores();
     j["dp_batches"] = static_cast<long long>(batches_.load());
     j["dp_subbatches_sent"] = static_cast<long long>(subs_sent_.load());
     j["dp_subbatches_merged"] = static_cast<long long>(subs_merged_.load());
+    j["dp_shard_failed_items"] = static_cast<long long>(shard_failures_.load());
     j["dp_arena_mib"] = static_cast<double>(group_->arena_bytes()) / (1 << 20);
     if (rank_ == 0) {
       const double nb = static_cast<double>(std::max<long long>(1, batches_.load()));
@@ -262,13 +296,12 @@ class DpEngine : public Engine {
       if (hipSetDevice(opt_.device_id) != hipSuccess)
         throw std::runtime_error("dp rank " + std::to_string(rank_) + ": cannot select HIP device " +
                                  std::to_string(opt_.device_id));
-      // A solo group forms no RCCL communicator at all: merely having one initialised cost the
-      // co-located HTTP/JSON host path ~13 % of throughput on a 16-CPU share (12.4-12.5k vs
-      // 14.3-14.7k req/s, gpurun_out/r2_43; profiles/r2_dp_world1.md).  DIE_DP_COMM=host: the
-      // ranks gather their (small: 4 KB per image) logits and decode status through the host
-      // segment instead, every rank loads the weights itself, and no RCCL communicator exists.
-      const char* cb = std::getenv("DIE_DP_COMM");
-      const bool host_comm = cb && std::string(cb) == "host";
+      // dp_backend "host": the ranks gather their (small: 4 KB per image) logits and decode status
+      // through the host segment instead, every rank loads the weights itself, and no RCCL
+      // communicator exists.  The default "rccl" broadcasts the weights and all-gathers over xGMI.
+      if (opt_.dp_backend != "rccl" && opt_.dp_backend != "host")
+        throw std::runtime_error("unknown dp_backend '" + opt_.dp_backend + "' (rccl | host)");
+      const bool host_comm = opt_.dp_backend == "host";
       if (host_comm) comm_ = make_host_comm(*group_);
       else if (!solo_) comm_ = make_rccl_comm(*group_);
       lo.dp_comm = solo_ || host_comm ? nullptr : comm_.get();
@@ -337,11 +370,10 @@ class DpEngine : public Engine {
   // every rank runs the same bucket); on completion, every sub-batch this rank queued is answered.
   void run_shard(const DpBatch& b, uint64_t seq) {
     const int per = b.per, B = b.B;
-    std::vector<BatchItem> items(static_cast<size_t>(per));
-    for (int j = 0; j < per; ++j) {
-      const int i = rank_ * per + j;
-      if (i >= B) break;
-      const DpItem& d = b.items[i];
+    const DpLayout L = DpLayout::with_per(B, world_, per);
+    std::vector<BatchItem> items(static_cast<size_t>(per));  // padded to `per`: every rank runs one bucket
+    for (int j = 0; j < L.shard_count(rank_); ++j) {
+      const DpItem& d = b.items[L.shard_begin(rank_) + j];
       if (d.is_text) {
         items[j].text = static_cast<const char*>(group_->at(d.off));
         items[j].text_len = d.len;
@@ -356,51 +388,66 @@ class DpEngine : public Engine {
       if (b.subs[k].rank == rank_) mine.push_back(b.subs[k]);
     batches_++;
     const size_t out_numel = output_numel();
-    local_->submit(std::move(items), [this, seq, per, B, out_numel, mine](BatchResult& r) {
+    local_->submit(std::move(items), [this, seq, L, out_numel, mine](BatchResult& r) {
       std::vector<float> gathered;
       const float* rows = nullptr;
-      std::vector<int> st, nt;
-      bool ok = r.ok;
+      std::vector<int> st(static_cast<size_t>(L.B), 0), nt(static_cast<size_t>(L.B), 0), rank_ok(static_cast<size_t>(world_), 0);
+      bool have_status = false;
+      bool ok = true;
       std::string err = r.error;
       if (device_gather_) {
-        rows = r.outputs;  // rank-major = item order
-        if (r.ok && r.status) {
-          st.resize(B);
-          nt.resize(B);
-          for (int i = 0; i < B; ++i) {
-            st[i] = r.status[(i / per) * r.status_stride + i % per];
-            nt[i] = r.ntok[(i / per) * r.status_stride + i % per];
-          }
+        // rank-major logits: rank r's `per` rows are items [r*per, (r+1)*per), i.e. item order
+        rows = r.outputs;
+        if (r.ok && r.rank_ok) {
+          std::copy(r.rank_ok, r.rank_ok + world_, rank_ok.begin());
+        } else {
+          ok = false;  // this rank's own batch failed (or never ran the collectives' D2H)
         }
-      } else {  // host gather: every rank contributes `per` rows (zeros when its shard failed)
-        std::vector<float> mine_rows(static_cast<size_t>(per) * out_numel, 0.f);
-        if (r.ok && r.outputs) std::memcpy(mine_rows.data(), r.outputs, mine_rows.size() * sizeof(float));
-        gathered.resize(mine_rows.size() * world_);
-        try {
-          group_->all_gather_host(mine_rows.data(), gathered.data(), mine_rows.size() * sizeof(float));
-          rows = gathered.data();
-          if (device_decode_) {
-            // device-decoded texts: every rank also needs the decode status and token count of
-            // every row (host fallback / size errors are answered by the rank that queued them)
-            std::vector<int> mine_st(2 * static_cast<size_t>(per), 0), all_st(2 * static_cast<size_t>(per) * world_);
-            if (r.ok && r.status)
-              for (int j = 0; j < per; ++j) {
-                mine_st[2 * j] = r.status[j];
-                mine_st[2 * j + 1] = r.ntok ? r.ntok[j] : 0;
-              }
-            group_->all_gather_host(mine_st.data(), all_st.data(), mine_st.size() * sizeof(int));
-            st.resize(B);
-            nt.resize(B);
-            for (int i = 0; i < B; ++i) {
-              st[i] = all_st[2 * static_cast<size_t>(i)];
-              nt[i] = all_st[2 * static_cast<size_t>(i) + 1];
-            }
+        if (ok && r.status) {
+          dp_items_from_gathered(L, r.status, static_cast<size_t>(r.status_stride), st.data());
+          dp_items_from_gathered(L, r.ntok, static_cast<size_t>(r.status_stride), nt.data());
+          have_status = true;
+        }
+      } else {
+        // host gather: every rank contributes `per` rows (zeros when its shard failed) and a
+        // [shard ok, status x per, ntok x per] table, every batch (the flag is never optional)
+        const size_t per_rows = static_cast<size_t>(L.per) * out_numel;
+        std::vector<float> mine_rows(per_rows, 0.f);
+        if (r.ok && r.outputs) std::memcpy(mine_rows.data(), r.outputs, per_rows * sizeof(float));
+        const size_t tl = 1 + 2 * static_cast<size_t>(L.per);
+        std::vector<int> mine_st(tl, 0), all_st(tl * static_cast<size_t>(world_));
+        mine_st[0] = r.ok ? 1 : 0;
+        if (r.ok && r.status)
+          for (int j = 0; j < L.per; ++j) {
+            mine_st[1 + j] = r.status[j];
+            mine_st[1 + L.per + j] = r.ntok ? r.ntok[j] : 0;
           }
+        gathered.resize(per_rows * static_cast<size_t>(world_));
+        try {
+          group_->all_gather_host(mine_rows.data(), gathered.data(), per_rows * sizeof(float));
+          group_->all_gather_host(mine_st.data(), all_st.data(), tl * sizeof(int));
+          rows = gathered.data();
+          for (int k = 0; k < world_; ++k) rank_ok[static_cast<size_t>(k)] = all_st[static_cast<size_t>(k) * tl];
+          dp_items_from_gathered(L, all_st.data() + 1, tl, st.data());
+          dp_items_from_gathered(L, all_st.data() + 1 + L.per, tl, nt.data());
+          have_status = device_decode_;
         } catch (const std::exception& e) {
           ok = false;
           err = e.what();
         }
       }
+      if (ok) {
+        // items of a failed rank's shard fail on their own; every other item is answered
+        const std::vector<uint8_t> item_ok = dp_item_ok(L, rank_ok.data());
+        for (int i = 0; i < L.B; ++i)
+          if (!item_ok[static_cast<size_t>(i)]) {
+            st[static_cast<size_t>(i)] = kItemShardFailed;
+            have_status = true;
+            shard_failures_++;
+          }
+      }
+      if (!have_status) st.clear(), nt.clear();
+      if (err.empty()) err = "data-parallel shard failed";
       for (const DpSubRef& ref : mine) complete(ref, ok, err, rows, out_numel, st, nt, r);
       if (rank_ != 0) group_->done(seq);
     });
@@ -473,7 +520,7 @@ class DpEngine : public Engine {
   uint32_t next_sub_ = 0;
   std::atomic<bool> stop_{false};
   std::thread dispatcher_, shard_thread_;
-  std::atomic<long long> batches_{0}, subs_sent_{0}, subs_merged_{0};
+  std::atomic<long long> batches_{0}, subs_sent_{0}, subs_merged_{0}, shard_failures_{0};
   std::atomic<double> pop_wait_us_{0.0}, slot_wait_us_{0.0}, pace_wait_us_{0.0};  // leader only
 };
 

@@ -186,6 +186,7 @@ class CpuEngine : public Engine {
     j["device"] = "cpu";
     j["batches"] = static_cast<long long>(batches_.load());
     j["images"] = static_cast<long long>(images_.load());
+    j["options"] = engine_options_json(opt_);
     return j;
   }
 
@@ -210,6 +211,8 @@ class CpuEngine : public Engine {
       BatchResult r;
       std::vector<float> outbuf;
       try {
+        if (opt_.fail_batch_every > 0 && ++nth_batch_ % opt_.fail_batch_every == 0)
+          throw std::runtime_error("injected batch failure (fail_batch_every)");
         const size_t B = job.items.size(), numel = input_numel();
         auto x = std::make_shared<CpuValue>();
         x->shape = in_shape_;
@@ -250,10 +253,45 @@ class CpuEngine : public Engine {
   std::deque<Job> q_;
   int inflight_ = 0;
   bool stop_ = false;
+  long long nth_batch_ = 0;  // executor thread only (fault injection)
   std::atomic<long long> batches_{0}, images_{0};
 };
 
 }  // namespace
+
+Json engine_options_json(const EngineOptions& o) {
+  Json j = Json::object();
+  j["device"] = o.device;
+  j["device_id"] = o.device_id;
+  j["max_batch"] = o.max_batch;
+  j["precision"] = o.precision;
+  j["pipeline_depth"] = o.pipeline_depth;
+  j["exec_streams"] = o.exec_streams;
+  j["use_graphs"] = o.use_graphs;
+  j["autotune"] = o.autotune;
+  j["device_decode"] = o.device_decode;
+  j["stage_slots"] = o.stage_slots;
+  j["pace"] = o.pace;
+  j["pack_text"] = o.pack_text;
+  j["branch_streams"] = o.branch_streams;
+  j["prep_on_compute"] = o.prep_on_compute;
+  j["live_batch"] = o.live_batch;
+  j["tune_cache"] = o.tune_cache;
+  j["cpu_threads"] = o.cpu_threads;
+  j["dp_world"] = o.dp_world;
+  j["dp_rank"] = o.dp_rank;
+  j["dp_backend"] = o.dp_backend;
+  j["dp_force_merge"] = o.dp_force_merge;
+  j["copy_streams"] = o.copy_streams;
+  j["bucket_div"] = o.bucket_div;
+  j["coarse_buckets"] = o.coarse_buckets;
+  j["pace_lead_scale"] = o.pace_lead_scale;
+  j["completion_poll_us"] = o.completion_poll_us;
+  j["bn_on_load"] = o.bn_on_load;
+  j["tune_cold"] = o.tune_cold;
+  j["fail_batch_every"] = o.fail_batch_every;
+  return j;
+}
 
 std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const EngineOptions& opt) {
   return std::make_unique<CpuEngine>(model_path, opt);

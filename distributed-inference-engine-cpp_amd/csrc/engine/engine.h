@@ -80,7 +80,15 @@ struct BatchResult {
   // between ranks is `status_stride`.
   int gathered = 1;
   int status_stride = 0;
+  // Data parallel: per-rank shard flags (`gathered` entries; 0 = that rank's forward did not run,
+  // its rows are garbage).  Null when the engine does not gather.
+  const int* rank_ok = nullptr;
 };
+
+// BatchResult::status bits (per item)
+constexpr int kItemNeedsHostParse = 1;  // unusual token: re-parse on the host and re-dispatch
+constexpr int kItemTooManyValues = 2;   // more values than the model input (ntok = count)
+constexpr int kItemShardFailed = 4;     // data parallel: the rank computing this item failed
 
 using BatchDone = std::function<void(BatchResult&)>;
 
@@ -201,8 +209,31 @@ struct EngineOptions {
   int dp_rank = 0;
   std::string dp_group;
   size_t dp_arena_mb = 0;          // input arena size (0 = sized from the model)
+  // How HIP ranks gather logits + decode status: "rccl" (ncclAllGather over xGMI, the default) or
+  // "host" (through the DpGroup segment; no communicator, every rank loads the weights itself).
+  std::string dp_backend = "rccl";
+  // A group of one normally feeds its local engine directly (no merge loop, no communicator);
+  // true keeps the N>1 path (sub-batch ring, leader merge, collectives) at world=1.
+  bool dp_force_merge = false;
   Communicator* dp_comm = nullptr;  // set internally: RCCL communicator handed to the HIP engine
+
+  // ---- HIP tuning knobs (round 2 kept these in DIE_* environment variables; every one is now an
+  // option, echoed in the engine's stats()["options"] and the bench JSON) ----
+  int copy_streams = 0;           // H2D copy streams (0 = auto: 2 with one executor, else 1)
+  int bucket_div = 8;             // batch-bucket steps per octave above 16 (graphs for 18, 20, ..., 32)
+  bool coarse_buckets = false;    // sqrt(2) bucket steps throughout (fewer graphs, faster cold start)
+  double pace_lead_scale = 1.0;   // != 1: pacing lead = measured input time x this (< 1 dispatches later)
+  int completion_poll_us = 0;     // > 0: sleep-poll each batch's D2H event instead of hipEventSynchronize
+  bool bn_on_load = false;        // bf16 plans: next unit's BN+ReLU applied on the 1x1 conv operand load
+  bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
+  // Fault injection: every Nth batch this engine runs fails before reaching the
+  // device (0 = off).  Drives the data-parallel shard-failure tests.
+  int fail_batch_every = 0;
 };
+
+// Every option as a JSON object (the /health "engine" document and bench.py echo it, so a run's
+// configuration can be reconstructed from its output).
+Json engine_options_json(const EngineOptions& o);
 
 // Factory: HIP engine when a GPU is visible and device != cpu, else the CPU executor (the
 // reference's ORT CUDA-EP -> CPU-EP fallback, src/inference_engine.cpp:21-29, made explicit).

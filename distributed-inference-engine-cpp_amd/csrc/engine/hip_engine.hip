@@ -61,7 +61,7 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     onnx::Model model = onnx::load_onnx(path);
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
-    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32");
+    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -85,12 +85,14 @@ class HipEngine : public Engine {
     }
     s_compute_ = s_exec_[0];
     // Streams = hardware queues: the executor streams (graphs + the small result D2H) and copy
-    // streams (early uploads, submit-time copies, PREP).  HIP gives a process GPU_MAX_HW_QUEUES (4)
-    // queues; more streams than that share queues (serialising copies behind kernels), and raising
-    // the limit lets the queue scheduler time-slice the compute queues (measured: forwards 1.8x
-    // longer), so the engine stays within three: 1 executor + 2 copy streams, or 2 + 1.
+    // streams (early uploads, submit-time copies, PREP).  HIP gives a process GPU_MAX_HW_QUEUES
+    // queues; more streams than that share queues (serialising copies behind kernels).  The engine
+    // stays within four (1 executor + 2 copy streams [+ prep/side], or 2 + 1), and the serving
+    // processes raise the limit to 8 (configure_hip_runtime_env) so that an RCCL communicator's
+    // internal streams do not push the engine's onto shared queues (profiles/r3_rccl_hw_queues.md).
+    // Two executors time-slice the compute queues instead of overlapping (forwards 1.8x longer).
     n_copy_streams_ = n_exec_ > 1 ? 1 : kStageStreams;
-    if (const char* e = std::getenv("DIE_COPY_STREAMS")) n_copy_streams_ = std::max(1, std::min(kStageStreams, std::atoi(e)));
+    if (opt.copy_streams > 0) n_copy_streams_ = std::min(kStageStreams, opt.copy_streams);
     for (int i = 0; i < n_copy_streams_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_[i], hipStreamNonBlocking));
     // side-branch stream (plan ops with join >= 0): the fourth and last queue; only with one executor
     branches_ = opt.branch_streams && n_exec_ == 1;
@@ -99,10 +101,8 @@ class HipEngine : public Engine {
       HIP_CHECK(hipStreamCreateWithFlags(&s_prep_, hipStreamNonBlocking));
     prep_on_compute_ = opt.prep_on_compute;
     use_live_ = opt.live_batch;
-    if (const char* e = std::getenv("DIE_PACE_LEAD_SCALE")) lead_scale_ = std::max(0.0, std::atof(e));
-    if (const char* e = std::getenv("DIE_LIVE_BATCH")) use_live_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("DIE_PREP_ON_COMPUTE")) prep_on_compute_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("DIE_COMPLETION_POLL_US")) completion_poll_us_ = std::max(0, std::atoi(e));
+    lead_scale_ = std::max(0.0, opt.pace_lead_scale);
+    completion_poll_us_ = std::max(0, opt.completion_poll_us);
     if (branches_) {
       HIP_CHECK(hipStreamCreateWithFlags(&s_side_, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -145,14 +145,14 @@ class HipEngine : public Engine {
       HIP_CHECK(hipMemset(sl.d_lens, 0xFF, sizeof(long long) * max_batch_));  // all -1: no text samples
       HIP_CHECK(hipMemset(sl.d_lens + max_batch_, 0, sizeof(long long) * max_batch_));
       HIP_CHECK(hipMemset(sl.d_lens + 2 * max_batch_, 0xFF, sizeof(long long) * max_batch_));
-      HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * 2 * max_batch_));
-      HIP_CHECK(hipMemset(sl.d_status, 0, sizeof(int) * 2 * max_batch_));
+      HIP_CHECK(hipMalloc(&sl.d_status, sizeof(int) * status_len()));
+      HIP_CHECK(hipMemset(sl.d_status, 0, sizeof(int) * status_len()));
       if (comm_) {
         HIP_CHECK(hipMalloc(&sl.d_gather, sizeof(float) * out_numel_ * max_batch_ * dp_world_));
-        HIP_CHECK(hipMalloc(&sl.d_gstatus, sizeof(int) * 2 * max_batch_ * dp_world_));
+        HIP_CHECK(hipMalloc(&sl.d_gstatus, sizeof(int) * status_len() * dp_world_));
         HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_gather), sizeof(float) * out_numel_ * max_batch_ * dp_world_,
                                 hipHostMallocDefault));
-        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_gstatus), sizeof(int) * 2 * max_batch_ * dp_world_,
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.h_gstatus), sizeof(int) * status_len() * dp_world_,
                                 hipHostMallocDefault));
         HIP_CHECK(hipEventCreateWithFlags(&sl.ev_gather, hipEventDisableTiming));
       }
@@ -186,10 +186,10 @@ class HipEngine : public Engine {
     // (18, 20, ..., 32, 36, ...): a batch runs the graph of the smallest bucket >= B, and the
     // serving loop's batches (17-24 at the headline load) get kernels tuned within 2 of their size
     // (fp32 headline A/B: sqrt(2) steps 13.1-13.2k, quarter steps 13.6-13.7k, eighth steps
-    // 13.9-14.1k req/s; profiles/r2_state.md).  DIE_BUCKET_DIV=N: N steps per octave above 16;
-    // DIE_COARSE_BUCKETS=1: sqrt(2) steps throughout.
-    const bool coarse = std::getenv("DIE_COARSE_BUCKETS") && std::atoi(std::getenv("DIE_COARSE_BUCKETS")) != 0;
-    const int fine = std::getenv("DIE_BUCKET_DIV") ? std::max(1, std::atoi(std::getenv("DIE_BUCKET_DIV"))) : 8;
+    // 13.9-14.1k req/s; profiles/r2_state.md).  EngineOptions::bucket_div = steps per octave above
+    // 16; coarse_buckets: sqrt(2) steps throughout.
+    const bool coarse = opt.coarse_buckets;
+    const int fine = std::max(1, opt.bucket_div);
     for (int b = 1; b < max_batch_; b *= 2) {
       buckets_.push_back(b);
       if (b >= 16 && !coarse) {
@@ -435,6 +435,8 @@ class HipEngine : public Engine {
     job.t0 = std::chrono::steady_clock::now();
     try {
       HIP_CHECK(hipSetDevice(dev_));
+      if (opt_.fail_batch_every > 0 && ++nth_batch_ % opt_.fail_batch_every == 0)
+        throw std::runtime_error("injected batch failure (fail_batch_every)");
       Slot& sl = slots_[slot];
       job.ev = static_cast<int>((job_seq_++ % kTimingJobs) * kEvPerJob);
       job.bi = static_cast<int>(bucket_index(B));
@@ -554,24 +556,10 @@ class HipEngine : public Engine {
       }
       HIP_CHECK(hipEventRecord(tev_[job.ev + 2], cs));
       if (comm_) {
-        // data parallel: every rank contributes its B rows (and decode status) to rank 0 over xGMI;
-        // the same collectives in the same order on every rank, whatever its shard holds.
-        // (a group of one has nothing to gather: its rows go to the host straight from d_out)
-        if (dp_world_ > 1) {
-          comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
-          comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * 2 * max_batch_, cs);
-        }
-        HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
-        {  // every rank answers the sub-batches it ingested: all rows come back to every host
-          HIP_CHECK(hipMemcpyAsync(sl.h_gather, dp_world_ > 1 ? sl.d_gather : sl.d_out,
-                                   sizeof(float) * out_numel_ * B * dp_world_, hipMemcpyDeviceToHost, cs));
-          HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, dp_world_ > 1 ? sl.d_gstatus : sl.d_status,
-                                   sizeof(int) * 2 * max_batch_ * dp_world_, hipMemcpyDeviceToHost, cs));
-          d2h_bytes_.fetch_add(static_cast<long long>((sizeof(float) * out_numel_ * B + sizeof(int) * 2 * max_batch_) *
-                                                      dp_world_),
-                               std::memory_order_relaxed);
-          HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
-        }
+        // this rank's shard ran: its flag travels with the status rows, so the other ranks answer
+        // this shard's items from the gathered rows (flag 0: they fail them; see the catch below)
+        HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 1, 1, cs));
+        dp_collectives(sl, B, cs);
         job.has_text = text_cap_ > 0;
       } else {
         HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, cs));
@@ -584,7 +572,20 @@ class HipEngine : public Engine {
       }
     } catch (const std::exception& e) {
       job.error = e.what();
+      if (comm_ && !dp_issued_) {
+        // The other ranks' collectives are waiting for this rank's: issue them anyway with the
+        // shard flag cleared (a rank that skipped them would hang the whole group), so they fail
+        // this shard's items and answer the rest.
+        try {
+          Slot& sl = slots_[slot];
+          HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 0, 1,
+                                      s_exec_[slot % n_exec_]));
+          dp_collectives(sl, B, s_exec_[slot % n_exec_]);
+        } catch (const std::exception&) {
+        }
+      }
     }
+    dp_issued_ = false;
     diag_submit_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -664,6 +665,7 @@ class HipEngine : public Engine {
     j["avg_copy_wait_ms"] = nb ? copy_wait_ms_total_.load() / nb : 0.0;
     j["avg_gpu_gap_ms"] = nb ? gpu_gap_ms_total_.load() / nb : 0.0;
     j["avg_prep_ms"] = nb ? prep_ms_total_.load() / nb : 0.0;  // decode + input prep, on the copy stream
+    j["options"] = engine_options_json(opt_);
     j["pace"] = opt_.pace && n_exec_ == 1 && !comm_ && !graphs_.empty();
     j["pack_text"] = d_packed_ != nullptr;
     j["branch_streams"] = branches_;
@@ -725,9 +727,8 @@ class HipEngine : public Engine {
   // ---- autotune persistence (kernel configs cached in a tuning file) ----
   std::string tune_cache_path() const {
     std::string p = opt_.tune_cache;
-    if (p == "auto") {
-      if (const char* e = std::getenv("DIE_TUNE_CACHE")) p = e;
-      else if (const char* h = std::getenv("HOME")) p = std::string(h) + "/.cache/die_amd/tune.json";
+    if (p == "auto") {  // (the Python layer resolves $DIE_TUNE_CACHE before it gets here)
+      if (const char* h = std::getenv("HOME")) p = std::string(h) + "/.cache/die_amd/tune.json";
       else p.clear();
     }
     return p;
@@ -846,7 +847,7 @@ class HipEngine : public Engine {
   // Time every (tile, split-K) candidate of every conv at every bucket and keep the fastest.
   // Runs once at start-up on the real buffers (a full forward first, so inputs hold real data).
   // Autotune every conv/GEMM at every bucket.  Candidates are timed one launch at a time behind
-  // an L2 scrub (DIE_TUNE_WARM=1: back-to-back launches instead): inside a forward a layer reads
+  // an L2 scrub (EngineOptions::tune_cold = false: back-to-back launches instead): inside a forward a layer reads
   // its input just written by the previous layer and its weights from the Infinity Cache, never a
   // warm L2 -- warm back-to-back timing favoured shallow LDS rings whose load latency is exposed
   // once the operands come from further away (stage-3 3x3 convs: 17.5 us tuned, 27 us in the graph).
@@ -854,8 +855,7 @@ class HipEngine : public Engine {
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    const char* warm_env = std::getenv("DIE_TUNE_WARM");
-    const bool cold = !(warm_env && std::atoi(warm_env) != 0);
+    const bool cold = opt_.tune_cold;
     constexpr size_t kScrubBytes = 96u << 20;
     void* scrub = nullptr;
     float* sink = nullptr;
@@ -1300,7 +1300,11 @@ class HipEngine : public Engine {
             r.outputs = sl.h_gather;
             r.status = job.has_text ? sl.h_gstatus : nullptr;
             r.ntok = r.status ? sl.h_gstatus + max_batch_ : nullptr;
-            r.status_stride = 2 * max_batch_;
+            r.status_stride = static_cast<int>(status_len());
+            rank_ok_copy_.resize(static_cast<size_t>(dp_world_));
+            for (int k = 0; k < dp_world_; ++k)
+              rank_ok_copy_[static_cast<size_t>(k)] = sl.h_gstatus[static_cast<size_t>(k) * status_len() + rank_ok_index()];
+            r.rank_ok = rank_ok_copy_.data();
           }
           batches_++;
           images_ += job.B;
@@ -1321,7 +1325,7 @@ class HipEngine : public Engine {
           r.outputs = out_copy_.data();
         }
         if (r.status) {
-          const size_t n = comm_ ? static_cast<size_t>(r.status_stride) * dp_world_ : 2 * static_cast<size_t>(max_batch_);
+          const size_t n = comm_ ? status_len() * dp_world_ : 2 * static_cast<size_t>(max_batch_);
           const int* base = r.status;
           status_copy_.assign(base, base + n);
           r.status = status_copy_.data();
@@ -1360,10 +1364,33 @@ class HipEngine : public Engine {
   static constexpr int kTableRows = 3;  // per-slot decode table: lens, text offsets, packed offsets
   // ... followed by one element: the live batch (samples of the bucket that are real)
   size_t table_len() const { return static_cast<size_t>(kTableRows) * max_batch_ + 1; }
+  // per-slot status table: [status x max_batch][ntok x max_batch][shard ok flag, 3 x pad]; a
+  // data-parallel rank all-gathers the whole table, so the flag rides with the rows
+  size_t status_len() const { return 2 * static_cast<size_t>(max_batch_) + 4; }
+  size_t rank_ok_index() const { return 2 * static_cast<size_t>(max_batch_); }
+
+  // Data parallel: every rank contributes its B rows and its status table to every other rank over
+  // xGMI (the same collectives in the same order on every rank, whatever its shard holds), then
+  // copies all rows and tables to its host; a group of one copies straight from d_out.
+  void dp_collectives(Slot& sl, int B, hipStream_t cs) {
+    dp_issued_ = true;
+    if (dp_world_ > 1) {
+      comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
+      comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * status_len(), cs);
+    }
+    HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
+    HIP_CHECK(hipMemcpyAsync(sl.h_gather, dp_world_ > 1 ? sl.d_gather : sl.d_out, sizeof(float) * out_numel_ * B * dp_world_,
+                             hipMemcpyDeviceToHost, cs));
+    HIP_CHECK(hipMemcpyAsync(sl.h_gstatus, dp_world_ > 1 ? sl.d_gstatus : sl.d_status, sizeof(int) * status_len() * dp_world_,
+                             hipMemcpyDeviceToHost, cs));
+    d2h_bytes_.fetch_add(static_cast<long long>((sizeof(float) * out_numel_ * B + sizeof(int) * status_len()) * dp_world_),
+                         std::memory_order_relaxed);
+    HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
+  }
   size_t live_index() const { return static_cast<size_t>(kTableRows) * max_batch_; }
   int n_stage_ = 0;                  // early-upload slots (stage_text)
   hipStream_t s_stage_[kStageStreams] = {};
-  int n_copy_streams_ = kStageStreams;  // copy streams in use (DIE_COPY_STREAMS, 1..kStageStreams)
+  int n_copy_streams_ = kStageStreams;  // copy streams in use (EngineOptions::copy_streams, 1..kStageStreams)
   unsigned long long stage_counter_[kStageStreams] = {};
   std::vector<hipEvent_t> stage_ev_;
   std::vector<unsigned long long> stage_seq_;  // guarded by stage_mu_ (like the three below)
@@ -1383,10 +1410,10 @@ class HipEngine : public Engine {
   static constexpr int kMaxExec = 2;
   int n_exec_ = 1;
   bool branches_ = false;  // side-branch stream in use (PlanOp::join)
-  int completion_poll_us_ = 0;     // DIE_COMPLETION_POLL_US: > 0 = sleep-poll the D2H event (0 = hipEventSynchronize)
+  int completion_poll_us_ = 0;     // EngineOptions::completion_poll_us: > 0 = sleep-poll the D2H event (0 = hipEventSynchronize)
   bool prep_on_compute_ = false;  // PREP runs on the compute stream before MAIN (EngineOptions)
   bool use_live_ = true;          // skip the bucket's padding samples (EngineOptions::live_batch)
-  double lead_scale_ = 1.0;       // DIE_PACE_LEAD_SCALE (< 1: dispatch later, trading GPU idle for batch size)
+  double lead_scale_ = 1.0;       // EngineOptions::pace_lead_scale (< 1: dispatch later, trading GPU idle for batch size)
   hipStream_t s_side_{};
   hipStream_t s_prep_{};  // PREP stream (early upload), else PREP shares copy stream 0
   hipEvent_t ev_fork_{}, ev_join_{};
@@ -1429,6 +1456,9 @@ class HipEngine : public Engine {
   int callbacks_running_ = 0;           // submitted batches whose callback has not returned yet
   std::vector<float> out_copy_;         // completion thread: results of the batch being called back
   std::vector<int> status_copy_;
+  std::vector<int> rank_ok_copy_;       // data parallel: gathered shard flags of the batch being called back
+  bool dp_issued_ = false;              // submit(): this batch's collectives are issued (guarded by submit_mu_)
+  long long nth_batch_ = 0;             // submit(): batches seen (fault injection; guarded by submit_mu_)
   int next_slot_ = 0;
   int last_ev_ = -1, last_bi_ = 0;  // most recent submitted job (guarded by mu_)
   mutable std::mutex pace_mu_;

@@ -67,8 +67,8 @@ struct Val {
 
 class Planner {
  public:
-  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split)
-      : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split) {}
+  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load)
+      : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load) {}
 
   Plan run() {
     if (m_.inputs.empty() || m_.outputs.empty()) throw std::runtime_error("model needs an input and an output");
@@ -98,7 +98,7 @@ class Planner {
     }
     finalize_output();
     fuse_pool_affine();
-    if (std::getenv("DIE_BN_ON_LOAD") && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
+    if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
     return std::move(plan_);
@@ -1572,7 +1572,7 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
-  // Pre-activation on load (opt-in, DIE_BN_ON_LOAD=1).  A dual-store conv writes x (the raw sum: next residual) AND
+  // Pre-activation on load (opt-in, EngineOptions::bn_on_load).  A dual-store conv writes x (the raw sum: next residual) AND
   // a = act(bn(x)) (the next unit's input).  When every reader of `a` is a 1x1 conv the LDS-DMA
   // loop can run (K = Cin <= 2048, Cin % 64 == 0), those convs read x and apply bn+act to their
   // operand fragments instead, and the producer stores x only: one activation-sized write and
@@ -1687,6 +1687,7 @@ class Planner {
   int max_batch_;
   bool side_branches_ = false;
   bool split_ = false;  // fp32 mode: split (hi, lo) activations and weights
+  bool bn_on_load_ = false;  // EngineOptions::bn_on_load (bf16 plans only)
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -1707,8 +1708,8 @@ std::string Plan::summary() const {
   return os.str();
 }
 
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split) {
-  return Planner(m, max_batch, side_branches, split).run();
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load) {
+  return Planner(m, max_batch, side_branches, split, bn_on_load).run();
 }
 
 }  // namespace die

@@ -87,6 +87,7 @@ struct Plan {
 // Build the plan for batches up to max_batch.  Throws on unsupported graphs.  side_branches: mark
 // independent convs to run on a second stream (PlanOp::join; extends their inputs' lifetimes).
 // split: fp32 mode (Plan::split).
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false);
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
+                bool bn_on_load = false);
 
 }  // namespace die

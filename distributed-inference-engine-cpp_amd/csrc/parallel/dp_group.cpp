@@ -11,6 +11,7 @@
 #include <chrono>
 #include <climits>
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -54,6 +55,9 @@ struct DpGroup::Control {
   std::atomic<int32_t> port;
   std::atomic<uint64_t> gseq;
   std::atomic<uint32_t> subs_posted, subs_taken;
+  std::atomic<uint32_t> sig_ready[kDpMaxRanks];
+  std::atomic<uint32_t> sig_any;
+  char sig[kDpMaxRanks][192];
   struct SubRing {
     std::atomic<uint32_t> head, tail;  // head: next slot to fill (producer), tail: next to take (leader)
     DpSub slots[kDpSubRing];
@@ -112,6 +116,8 @@ std::unique_ptr<DpGroup> DpGroup::create(const std::string& name, int world, siz
   c->gseq = 0;
   c->subs_posted = 0;
   c->subs_taken = 0;
+  for (auto& r : c->sig_ready) r = 0;
+  c->sig_any = 0;
   for (auto& q : c->subq) {
     q.head = 0;
     q.tail = 0;
@@ -206,6 +212,42 @@ bool DpGroup::wait_joined(int timeout_ms) {
     if (std::chrono::steady_clock::now() > deadline) return false;
     futex_wait(&ctl_->joined, j, 50);
   }
+}
+
+void DpGroup::publish_signature(const std::string& sig) {
+  const size_t n = std::min(sig.size(), sizeof(ctl_->sig[0]) - 1);
+  std::memcpy(ctl_->sig[rank_], sig.data(), n);
+  ctl_->sig[rank_][n] = 0;
+  ctl_->sig_ready[rank_].store(1, std::memory_order_release);
+  ctl_->sig_any.fetch_add(1, std::memory_order_release);
+  futex_wake(&ctl_->sig_any);
+}
+
+bool DpGroup::check_signatures(int timeout_ms, std::string* why) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (true) {
+    const uint32_t snap = ctl_->sig_any.load(std::memory_order_acquire);
+    bool all = true;
+    for (int r = 0; r < world_; ++r) all = all && ctl_->sig_ready[r].load(std::memory_order_acquire) != 0;
+    if (all) break;
+    if (ctl_->stop.load()) {
+      if (why) *why = "data-parallel group stopped before every rank published its plan signature";
+      return false;
+    }
+    if (std::chrono::steady_clock::now() > deadline) {
+      if (why) *why = "timed out waiting for every rank's plan signature";
+      return false;
+    }
+    futex_wait(&ctl_->sig_any, snap, 50);
+  }
+  for (int r = 1; r < world_; ++r)
+    if (std::strcmp(ctl_->sig[r], ctl_->sig[0]) != 0) {
+      if (why)
+        *why = "data-parallel rank " + std::to_string(r) + " plans a different program (" + std::string(ctl_->sig[r]) +
+               ") than rank 0 (" + std::string(ctl_->sig[0]) + ")";
+      return false;
+    }
+  return true;
 }
 
 uint64_t DpGroup::post(const DpBatch& b) {

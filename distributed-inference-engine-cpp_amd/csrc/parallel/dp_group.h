@@ -93,6 +93,11 @@ class DpGroup {
   bool wait_id(void* id, size_t n, int timeout_ms);  // followers
   void mark_joined();                              // followers, once ready to receive batches
   bool wait_joined(int timeout_ms);                // leader: all followers joined
+  // Plan signature (model, precision, local batch, ...): every rank publishes its own, then
+  // check_signatures waits for all of them and returns false (with *why) on any mismatch, before
+  // a collective could run with different buffer sizes on different ranks.
+  void publish_signature(const std::string& sig);
+  bool check_signatures(int timeout_ms, std::string* why);
 
   // ---- batch ring ----
   // Leader: publish a batch (blocks while the ring is full, i.e. some follower still works on the

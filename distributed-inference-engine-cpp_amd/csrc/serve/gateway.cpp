@@ -61,7 +61,7 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
   if (opt_.local_shm && any_local) {
     static std::atomic<int> instance{0};
     std::string err;
-    shm_ = ShmArena::create("/die_gw_" + std::to_string(getpid()) + "_" + std::to_string(instance++),
+    shm_ = ShmArena::create(shm_arena_name(std::to_string(getpid()) + "_" + std::to_string(instance++)),
                             opt_.shm_mb << 20, &err);
     if (!shm_) DIE_LOG(WARN, "gateway: no shared-memory body arena (" << err << "); forwarding bytes");
   }

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <cmath>
 #include <random>
 #include <thread>
 
@@ -53,6 +54,47 @@ Template make_full_template(const LoadgenOptions& o, uint64_t seed) {
   return t;
 }
 
+// Verify-mode body of input k: shortest round-trip float text, so a worker that parses (or decodes
+// on the device) exactly gets verify_inputs[k].
+Template make_verify_template(const LoadgenOptions& o, size_t k) {
+  Template t;
+  std::string& b = t.body;
+  b += "{\"request_id\":\"";
+  b += o.id_prefix;
+  t.id_pos = b.size();
+  t.id_len = kIdDigits;
+  b.append(kIdDigits, '0');
+  b += "\",\"input_data\":";
+  append_float_array(b, o.verify_inputs + k * o.input_numel, o.input_numel);
+  b += "}";
+  return t;
+}
+
+// Relative L2 error of a response's output_data against `ref` (n floats); < 0 when the body has no
+// numeric output_data of length n.  `id_ok` reports whether the request_id echo equals `id`.
+double response_error(const std::string& body, const float* ref, size_t n, const std::string& id, bool& id_ok) {
+  Json j;
+  try {
+    j = Json::parse(body);
+  } catch (const std::exception&) {
+    id_ok = false;
+    return -1.0;
+  }
+  const Json* rid = j.find("request_id");
+  id_ok = rid && rid->is_string() && rid->as_string() == id;
+  const Json* out = j.find("output_data");
+  if (!out || !out->is_array() || out->size() != n) return -1.0;
+  double num = 0.0, den = 0.0;
+  for (size_t i = 0; i < n; ++i) {
+    const Json& v = (*out)[i];
+    if (!v.is_number()) return -1.0;
+    const double d = v.as_double() - static_cast<double>(ref[i]);
+    num += d * d;
+    den += static_cast<double>(ref[i]) * ref[i];
+  }
+  return den > 0.0 ? std::sqrt(num / den) : std::sqrt(num);
+}
+
 void patch_digits(std::string& b, size_t pos, size_t width, uint64_t v) {
   for (size_t k = 0; k < width; ++k) {
     b[pos + width - 1 - k] = static_cast<char>('0' + v % 10);
@@ -88,7 +130,14 @@ Json run_loadgen(const LoadgenOptions& o) {
   Gate gate;
   gate.total = C + 1;
   std::chrono::steady_clock::time_point t0, t1;
+  const bool verify = o.payload == "verify";
+  if (verify && (!o.verify_inputs || !o.verify_expected || o.verify_count == 0 || o.output_numel == 0))
+    throw std::runtime_error("loadgen verify mode needs verify_inputs, verify_expected, verify_count, output_numel");
   const bool full = o.payload == "full";
+  std::vector<Template> vt;  // verify mode: one shared template per distinct input
+  for (size_t k = 0; verify && k < o.verify_count; ++k) vt.push_back(make_verify_template(o, k));
+  std::vector<long> verified(C, 0), mismatched(C, 0), bad_id(C, 0);
+  std::vector<double> max_err(C, 0.0);
   const int d = std::max(1, std::min(o.decimals, 8));
   uint64_t scale = 1;
   for (int k = 0; k < d; ++k) scale *= 10;
@@ -100,8 +149,15 @@ Json run_loadgen(const LoadgenOptions& o) {
       HttpClient client(o.host, o.port, std::chrono::milliseconds(o.timeout_ms), std::chrono::milliseconds(o.timeout_ms), 2);
       Template tpl;
       if (full) tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(c));
+      std::string vbody;  // verify mode: this request's copy of its input's template
       auto body_for = [&](long id) -> std::string& {
         static thread_local std::string small;
+        if (verify) {
+          const Template& t = vt[static_cast<size_t>(id) % vt.size()];
+          vbody = t.body;
+          patch_digits(vbody, t.id_pos, t.id_len, static_cast<uint64_t>(id));
+          return vbody;
+        }
         const long key = o.distinct > 0 ? id % o.distinct : id;
         if (full) {
           patch_digits(tpl.body, tpl.id_pos, tpl.id_len, static_cast<uint64_t>(id));
@@ -126,6 +182,18 @@ Json run_loadgen(const LoadgenOptions& o) {
         if (r && r->status == 200) {
           ++ok[c];
           lat[c].push_back(ms);
+          if (verify) {
+            const size_t k = static_cast<size_t>(id) % vt.size();
+            char idbuf[32];
+            std::snprintf(idbuf, sizeof idbuf, "%0*ld", kIdDigits, id);
+            bool id_ok = false;
+            const double e = response_error(r->body, o.verify_expected + k * o.output_numel, o.output_numel,
+                                            o.id_prefix + idbuf, id_ok);
+            ++verified[c];
+            if (!id_ok) ++bad_id[c];
+            if (e < 0.0 || e > o.verify_tol) ++mismatched[c];
+            max_err[c] = std::max(max_err[c], e < 0.0 ? 1e30 : e);
+          }
         } else {
           ++fail[c];
           errs[c][r ? "HTTP " + std::to_string(r->status) : err]++;
@@ -188,7 +256,21 @@ Json run_loadgen(const LoadgenOptions& o) {
   for (auto& kv : merged) e[kv.first] = static_cast<long long>(kv.second);
   j["errors"] = e;
   j["payload"] = o.payload;
-  j["body_bytes"] = static_cast<long long>(full ? make_full_template(o, 1).body.size() : 60);
+  j["body_bytes"] = static_cast<long long>(verify ? vt[0].body.size() : full ? make_full_template(o, 1).body.size() : 60);
+  if (verify) {
+    long nv = 0, nm = 0, nb = 0;
+    double me = 0.0;
+    for (int c = 0; c < C; ++c) {
+      nv += verified[c];
+      nm += mismatched[c];
+      nb += bad_id[c];
+      me = std::max(me, max_err[c]);
+    }
+    j["verified"] = static_cast<long long>(nv);
+    j["mismatched"] = static_cast<long long>(nm);
+    j["bad_request_id"] = static_cast<long long>(nb);
+    j["max_rel_err"] = me;
+  }
   return j;
 }
 

@@ -30,10 +30,20 @@ struct LoadgenOptions {
   std::string id_prefix = "req_";
   // Distinct payloads cycled (0 = every request unique).  With "ref" this is always 10.
   long distinct = 0;
+  // Verify mode (payload "verify"): `verify_count` distinct inputs (verify_inputs: K x input_numel
+  // floats, sent as shortest round-trip text) cycled over the requests, each with a unique
+  // request_id; every 200 answer's output_data is compared with verify_expected (K x output_numel
+  // floats) by relative L2 error <= verify_tol (0 = bit-exact) and its request_id echo is checked.
+  // A shard / gather / batch-row mix-up shows up as `mismatched`, not as a slower run.
+  const float* verify_inputs = nullptr;
+  const float* verify_expected = nullptr;
+  size_t verify_count = 0;
+  size_t output_numel = 0;
+  double verify_tol = 0.0;
 };
 
 // Runs warmup then the timed phase; returns {"ok","failed","wall_s","rps","latency_ms":{...},
-// "errors":{...}}.
+// "errors":{...}} (+ "verified","mismatched","max_rel_err","bad_request_id" in verify mode).
 Json run_loadgen(const LoadgenOptions& opt);
 
 }  // namespace die

@@ -175,7 +175,12 @@ void WorkerNode::parse_loop() {
       j = std::move(parse_q_.front());
       parse_q_.pop_front();
     }
-    handle_infer(*j.req, std::move(j.res));
+    try {
+      handle_infer(*j.req, j.res);
+    } catch (const std::exception& e) {  // never let a request take the parse thread (and the process) down
+      errors_++;
+      j.res.send(error_response(500, e.what()));  // no-op when handle_infer already answered
+    }
   }
 }
 
@@ -221,7 +226,16 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   Engine& eng = *engine_;
   SamplePool& pool = eng.sample_pool();
   SampleSink sink;
-  sink.buf = pool.acquire();
+  try {
+    sink.buf = pool.acquire();
+  } catch (const std::exception&) {
+    // staging exhausted (e.g. a data-parallel rank's share of the shared arena under a burst): a
+    // retryable 503, not a dead parse thread
+    errors_++;
+    staging_exhausted_.fetch_add(1, std::memory_order_relaxed);
+    res.send(error_response(503, "server busy: input staging exhausted"));
+    return;
+  }
   const size_t numel = eng.input_numel();
   sink.float_cap = std::min(sink.buf.capacity, numel);
   const size_t text_cap = std::min(eng.text_capacity(), sink.buf.capacity * sizeof(float));
@@ -235,14 +249,18 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   size_t text_len = 0, text_off = 0;
   bool packed = false;
   std::string_view body = req.body_view();
+  std::shared_ptr<const void> shm_keep;  // keeps the gateway arena's view mapped while we parse
   if (const std::string_view desc = req.header("x-die-shm"); !desc.empty()) {
-    // co-located gateway: the body lies in its shared-memory arena (core/shm_arena.h)
+    // co-located gateway: the body lies in its shared-memory arena (core/shm_arena.h).  Only a
+    // loopback peer may send a descriptor, and the segment name carries the arena's random token.
     const char* p = nullptr;
     size_t n = 0;
-    std::string err;
-    if (!opt_.accept_shm || !shm_reader_.resolve(desc, &p, &n, &err)) {
+    std::string err = "shared-memory bodies disabled";
+    if (opt_.accept_shm && !req.peer_loopback) err = "shared-memory bodies are accepted from loopback peers only";
+    if (!opt_.accept_shm || !req.peer_loopback || !shm_reader_.resolve(desc, &p, &n, &err, &shm_keep)) {
       pool.release(sink.buf);
-      HttpResponse r = error_response(500, opt_.accept_shm ? err : "shared-memory bodies disabled");
+      errors_++;
+      HttpResponse r = error_response(500, err);
       r.headers.emplace_back("X-Die-Error", "shm");
       res.send(std::move(r));
       return;
@@ -359,7 +377,13 @@ void WorkerNode::dispatch(Pending p, Responder res) {
       res.send(error_response(500, msg));
       return;
     }
-    if (r->decode_status & 1) {
+    if (r->decode_status & kItemShardFailed) {
+      engine_->sample_pool().release(buf);
+      errors_++;
+      res.send(error_response(500, "inference failed on a data-parallel rank"));
+      return;
+    }
+    if (r->decode_status & kItemNeedsHostParse) {
       host_fallback(buf, text_len, packed, text_off, std::move(id), key, std::move(res));
       return;
     }
@@ -417,7 +441,14 @@ void WorkerNode::host_fallback(SampleBuffer text_buf, size_t text_len, bool pack
   body += "]}";
   pool.release(text_buf);
   SampleSink sink;
-  sink.buf = pool.acquire();
+  try {
+    sink.buf = pool.acquire();
+  } catch (const std::exception&) {
+    errors_++;
+    staging_exhausted_.fetch_add(1, std::memory_order_relaxed);
+    res.send(error_response(503, "server busy: input staging exhausted"));
+    return;
+  }
   sink.float_cap = std::min(sink.buf.capacity, numel);
   try {
     parse_infer_body(body, sink);
@@ -463,6 +494,9 @@ Json WorkerNode::getHealth() const {
   h["parse_gbps"] = parse_ns_.load() ? static_cast<double>(parse_bytes_.load()) / parse_ns_.load() : 0.0;
   h["device_decoded"] = static_cast<long long>(device_decoded_.load());
   h["shm_bodies"] = static_cast<long long>(shm_bodies_.load());
+  h["shm_segments_mapped"] = static_cast<long long>(shm_reader_.mapped());
+  h["shm_segments_unmapped"] = shm_reader_.unmapped();
+  h["staging_exhausted"] = static_cast<long long>(staging_exhausted_.load());
   h["decode_fallbacks"] = static_cast<long long>(decode_fallbacks_.load());
   Json st = Json::object();
   st["recv"] = h_recv_.snapshot();

@@ -107,7 +107,7 @@ class WorkerNode {
   std::atomic<int64_t> cache_hits_{0};
   std::atomic<int64_t> errors_{0};
   std::atomic<int64_t> parse_ns_{0}, parse_bytes_{0}, parsed_{0};
-  std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0}, shm_bodies_{0};
+  std::atomic<int64_t> device_decoded_{0}, decode_fallbacks_{0}, shm_bodies_{0}, staging_exhausted_{0};
   ShmReader shm_reader_;
   // request stages: parse (body -> staging), queue (batcher wait), engine (submit -> outputs on
   // host), respond (outputs -> serialised response), total (handler entry -> response)

@@ -104,7 +104,14 @@ def lib() -> C.CDLL:
         sig("die_gateway_stop", None, vp)
         sig("die_gateway_destroy", None, vp)
         sig("die_loadgen_run", vp, cp, errp)
+        sig("die_loadgen_run_verify", vp, cp, f32p, C.c_long, f32p, C.c_long, errp)
         sig("die_parse_bench", C.c_double, cp, C.c_long, C.c_int, C.c_int)
+        i32p = C.POINTER(C.c_int)
+        sig("die_dp_shard", C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p)
+        sig("die_dp_per", C.c_int, C.c_int, C.c_int)
+        sig("die_dp_items_from_gathered", None, C.c_int, C.c_int, C.c_int, i32p, C.c_long, i32p)
+        sig("die_dp_rows_from_gathered", None, C.c_int, C.c_int, C.c_int, f32p, C.c_long, C.c_long, f32p)
+        sig("die_dp_item_ok", None, C.c_int, C.c_int, C.c_int, i32p, C.POINTER(C.c_ubyte))
         _LIB = L
     return _LIB
 
@@ -333,9 +340,19 @@ class TestBatcher:
 
 # ---- engines ----------------------------------------------------------------------------------------
 
+def engine_options(opts: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+    """EngineOptions as JSON (csrc/engine/engine.h).  tune_cache "auto" (the default) resolves here:
+    $DIE_TUNE_CACHE, else the native default (~/.cache/die_amd/tune.json)."""
+    o = dict(opts or {})
+    if o.get("tune_cache", "auto") == "auto" and os.environ.get("DIE_TUNE_CACHE"):
+        o["tune_cache"] = os.environ["DIE_TUNE_CACHE"]
+    return o
+
+
 class Engine:
     def __init__(self, model_path: str, **opts):
         err = _err_box()
+        opts = engine_options(opts)
         self.h = lib().die_engine_create(model_path.encode(), json.dumps(opts).encode(), C.byref(err))
         if not self.h:
             _raise_if(err, "engine")
@@ -449,13 +466,52 @@ def onnx_summary(model_path: str) -> Dict[str, Any]:
 
 # ---- servers ------------------------------------------------------------------------------------------
 
+class DpLayout:
+    """Row bookkeeping of one data-parallel batch (csrc/parallel/dp_layout.h): B items over `world`
+    ranks, `per` items per rank (default ceil(B / world)); rank r computes [r*per, min(B, (r+1)*per))."""
+
+    def __init__(self, B: int, world: int, per: int = 0):
+        self.B, self.world = B, world
+        self.per = per if per > 0 else lib().die_dp_per(B, world)
+
+    def shard(self, r: int) -> Tuple[int, int]:
+        begin = C.c_int(0)
+        n = lib().die_dp_shard(self.B, self.world, self.per, r, C.byref(begin))
+        return begin.value, n
+
+    def items_from_gathered(self, gathered: np.ndarray, stride: int) -> np.ndarray:
+        g = np.ascontiguousarray(gathered, np.int32)
+        assert g.size >= self.world * stride
+        out = np.zeros(self.B, np.int32)
+        ip = C.POINTER(C.c_int)
+        lib().die_dp_items_from_gathered(self.B, self.world, self.per, g.ctypes.data_as(ip), stride,
+                                         out.ctypes.data_as(ip))
+        return out
+
+    def rows_from_gathered(self, gathered: np.ndarray, rows_per_rank: int) -> np.ndarray:
+        g = np.ascontiguousarray(gathered, np.float32)
+        row_len = g.shape[-1]
+        assert g.reshape(-1, row_len).shape[0] >= self.world * rows_per_rank
+        out = np.zeros((self.B, row_len), np.float32)
+        lib().die_dp_rows_from_gathered(self.B, self.world, self.per, _f32(g), rows_per_rank, row_len, _f32(out))
+        return out
+
+    def item_ok(self, rank_ok) -> np.ndarray:
+        r = np.ascontiguousarray(rank_ok, np.int32)
+        assert r.size == self.world
+        out = np.zeros(self.B, np.uint8)
+        lib().die_dp_item_ok(self.B, self.world, self.per, r.ctypes.data_as(C.POINTER(C.c_int)),
+                             out.ctypes.data_as(C.POINTER(C.c_ubyte)))
+        return out.astype(bool)
+
+
 class DpFollower:
     """Data-parallel follower rank (csrc/engine/dp_engine.cpp): attaches to the leader's DpGroup
     `group`, builds its local engine (RCCL communicator for HIP, host communicator for CPU) and
     serves its shard of every batch on a background native thread."""
 
     def __init__(self, model_path: str, group: str, rank: int, world: int, max_batch: int = 32, **engine):
-        eng = dict(engine)
+        eng = engine_options(engine)
         eng.update(dp_group=group, dp_rank=rank, dp_world=world)
         o = dict(model_path=model_path, max_batch=max_batch, engine=eng)
         err = _err_box()
@@ -480,7 +536,7 @@ class Worker:
 
     def __init__(self, model_path: str, node_id: str = "w1", port: int = 0, **opts):
         o = dict(opts)
-        o.update(model_path=model_path, node_id=node_id, port=port)
+        o.update(model_path=model_path, node_id=node_id, port=port, engine=engine_options(opts.get("engine")))
         err = _err_box()
         self.h = lib().die_worker_create(json.dumps(o).encode(), C.byref(err))
         if not self.h:
@@ -531,9 +587,21 @@ class GatewayServer:
             pass
 
 
-def loadgen(**opts) -> Dict[str, Any]:
+def loadgen(verify_inputs: Optional[np.ndarray] = None, verify_expected: Optional[np.ndarray] = None,
+            **opts) -> Dict[str, Any]:
+    """Closed-loop C++ load generator.  With verify_inputs ([K, input_numel]) and verify_expected
+    ([K, output_numel]) every request carries one of the K inputs (unique request_id) and every answer
+    is checked against its expected row (relative L2 <= verify_tol, 0 = bit-exact): the result adds
+    "verified", "mismatched", "bad_request_id" and "max_rel_err"."""
     err = _err_box()
-    p = lib().die_loadgen_run(json.dumps(opts).encode(), C.byref(err))
+    if verify_inputs is not None:
+        xi = np.ascontiguousarray(verify_inputs, np.float32).reshape(len(verify_inputs), -1)
+        xe = np.ascontiguousarray(verify_expected, np.float32).reshape(len(xi), -1)
+        opts = dict(opts, input_numel=xi.shape[1])
+        p = lib().die_loadgen_run_verify(json.dumps(opts).encode(), _f32(xi), len(xi), _f32(xe), xe.shape[1],
+                                         C.byref(err))
+    else:
+        p = lib().die_loadgen_run(json.dumps(opts).encode(), C.byref(err))
     if not p:
         _raise_if(err, "loadgen")
     return json.loads(_take_str(p))

@@ -8,6 +8,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+import die_amd  # noqa: E402,F401  (sets the HIP runtime environment before any test touches the GPU)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

@@ -41,6 +41,11 @@ def _check(out, n, steps, warmup, mode):
     if mode == "gateway":
         assert out["gateway"]["failed"] == 0 and set(out["gateway"]["breakers"]) == {"CLOSED"}
         assert out["direct_worker"]["failed"] == 0
+        assert out["cache_hits_timed"] == 0  # unique payloads per pass: every timed request was computed
+        # BASELINE config 4 after the headline: one DP worker over all ranks, in watchdogged children
+        dp = out["dp_rccl"]
+        assert "error" not in dp, dp
+        assert dp["dp_world"] == n and dp["failed"] == 0 and dp["requests_per_s"] > 0 and dp["dp_solo"] is False
 
 
 STEP_REQ = 4

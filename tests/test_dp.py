@@ -80,21 +80,18 @@ def test_dp_worker_cpu(native, models, world):
 
 
 @pytest.mark.parametrize("merge", [False, True])
-def test_dp_world1_solo_and_merge(native, models, monkeypatch, merge):
-    """A group of one feeds its local engine directly (dp_solo); DIE_DP_FORCE_MERGE=1 keeps the
+def test_dp_world1_solo_and_merge(native, models, merge):
+    """A group of one feeds its local engine directly (dp_solo); dp_force_merge keeps the
     sub-batch ring + merge loop N>1 runs.  Both answer like the plain executor, over HTTP too."""
     from die_amd.models import resnet_v2 as r
 
     path, w, cfg = models["tiny"]
-    if merge:
-        monkeypatch.setenv("DIE_DP_FORCE_MERGE", "1")
-    else:
-        monkeypatch.delenv("DIE_DP_FORCE_MERGE", raising=False)
     group = "die_dp_s%d_%d" % (os.getpid(), merge)
-    wk = native.Worker(path, node_id="dp1", max_batch=8, engine={"device": "cpu", "dp_world": 1, "dp_group": group})
+    wk = native.Worker(path, node_id="dp1", max_batch=8, engine={"device": "cpu", "dp_world": 1, "dp_group": group,
+                                                                "dp_force_merge": merge})
     try:
         h = wk.health()
-        assert h["engine"]["dp_solo"] is (not merge)
+        assert h["engine"]["dp_solo"] is (not merge) and h["engine"]["dp_force_merge"] is merge
         res = native.loadgen(port=wk.port, connections=8, requests=48, payload="full", input_numel=3 * 64 * 64)
         assert res["ok"] == 48 and res["failed"] == 0
         x = r.synthetic_input(2, cfg).reshape(2, -1)
@@ -212,3 +209,152 @@ def test_dp_every_rank_ingests(native, models, world):
     merged = h0["engine"]["dp_subbatches_merged"]
     sent = h0["engine"]["dp_subbatches_sent"] + sum(h["engine"]["dp_subbatches_sent"] for h in healths)
     assert merged == sent and merged > h0["engine"]["dp_batches"] / 2
+
+
+# ---- row bookkeeping of a DP batch (csrc/parallel/dp_layout.h): pure functions, any world size ----
+
+def _ref_layout(B, world, per):
+    """Independent model: item i -> (rank, slot in that rank's shard)."""
+    return [(i // per, i % per) for i in range(B)]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("B", [1, 5, 17, 31, 32, 64, 255])
+def test_dp_layout_shards_and_gather_mapping(native, world, B):
+    L = native.DpLayout(B, world)
+    per = -(-B // world)
+    assert L.per == per
+    # shards cover [0, B) in rank order without overlap; the tail ranks may be short or empty
+    covered = []
+    for r in range(world):
+        begin, n = L.shard(r)
+        assert begin == min(B, r * per) and 0 <= n <= per
+        covered += list(range(begin, begin + n))
+    assert covered == list(range(B))
+    # status tables: rank r's block at r*stride, slot j holds a value naming (r, j); padding and
+    # the block's tail (ntok rows, shard flag) hold garbage that must never be read
+    for stride in (per, 2 * 32 + 4, 2 * per + 7):
+        if stride < per:
+            continue
+        g = np.full(world * stride, -999, np.int32)
+        for r in range(world):
+            begin, n = L.shard(r)
+            for j in range(n):
+                g[r * stride + j] = 1000 * r + j
+        got = L.items_from_gathered(g, stride)
+        want = [1000 * r + j for r, j in _ref_layout(B, world, per)]
+        np.testing.assert_array_equal(got, want)
+    # logits: every rank contributes exactly `per` rows, so the rank-major gather is item order
+    row_len = 3
+    rows = np.arange(world * per * row_len, dtype=np.float32).reshape(world * per, row_len)
+    np.testing.assert_array_equal(L.rows_from_gathered(rows, per), rows[:B])
+
+
+@pytest.mark.parametrize("world,B,failed", [(2, 7, [1]), (3, 8, [0]), (8, 61, [2, 7]), (8, 5, [6])])
+def test_dp_layout_failed_rank_fails_only_its_items(native, world, B, failed):
+    L = native.DpLayout(B, world)
+    rank_ok = [0 if r in failed else 1 for r in range(world)]
+    ok = L.item_ok(rank_ok)
+    for i in range(B):
+        assert ok[i] == (i // L.per not in failed), (i, L.per)
+
+
+def test_dp_layout_explicit_per(native):
+    """The leader fixes `per` for a batch (ceil(B / world)); followers read it from the descriptor."""
+    L = native.DpLayout(10, 4, per=3)
+    assert [L.shard(r) for r in range(4)] == [(0, 3), (3, 3), (6, 3), (9, 1)]
+    L = native.DpLayout(10, 4, per=4)  # a larger bucket: the last rank computes nothing
+    assert [L.shard(r) for r in range(4)] == [(0, 4), (4, 4), (8, 2), (10, 0)]
+
+
+# ---- answers verified under concurrent load (multi-row DP batches, every response checked) ----
+
+def _verify_set(native, path, cfg, k, seed):
+    from die_amd.models import resnet_v2 as r
+
+    x = r.synthetic_input(k, cfg, seed=seed).reshape(k, -1)
+    ref = np.stack([native.cpu_run(path, x[i:i + 1].reshape(1, 3, 64, 64))[0] for i in range(k)])
+    return x, ref
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_concurrent_rows_verified(native, models, world):
+    """16 concurrent connections over K=12 distinct inputs (cache off, so every request is computed):
+    DP batches carry several rows from several sub-batches, and every answer is compared with its
+    input's expected logits -- a swapped row or a rank-order mix-up is a mismatch, not a pass."""
+    path, w, cfg = models["tiny"]
+    group = "die_dp_v%d_%d" % (os.getpid(), world)
+    ps = _spawn_followers(path, group, world, 8)
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dpv", max_batch=8, cache_capacity=0,
+                           engine={"device": "cpu", "dp_world": world, "dp_group": group})
+        x, ref = _verify_set(native, path, cfg, 12, seed=11)
+        res = native.loadgen(port=wk.port, connections=16, requests=192, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-5, timeout_ms=120000)
+        assert res["ok"] == 192 and res["failed"] == 0, res
+        assert res["verified"] == 192 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        h = wk.health()
+        assert h["cache_hits"] == 0
+        assert h["engine"]["dp_batches"] < 192  # batches carried several rows
+    finally:
+        if wk is not None:
+            wk.stop()
+        outs = _reap(ps)
+    assert all(rc == 0 for rc, _ in outs), outs
+
+
+FAILING_FOLLOWER = """
+import sys, os
+sys.path.insert(0, {repo!r}); os.environ['DIE_NO_TORCH'] = '1'
+import die_amd
+from die_amd import native
+f = native.DpFollower({model!r}, {group!r}, 1, 2, max_batch=8, device='cpu', fail_batch_every=2)
+print('served', f.join(), flush=True)
+"""
+
+
+def test_dp_shard_failure_fails_only_that_shard(native, models):
+    """with the host gather a failed rank used to contribute zero rows and zero status,
+    and the other ranks answered those rows with ok=true.  Now every rank gathers a shard flag:
+    rank 1 fails every 2nd batch (fault injection) and exactly its items get a 500 -- no answer is
+    wrong, and the rank-0 items of the same batches still succeed."""
+    path, w, cfg = models["tiny"]
+    group = "die_dp_f%d" % os.getpid()
+    env = dict(os.environ, DIE_NO_TORCH="1")
+    p = subprocess.Popen([sys.executable, "-c", FAILING_FOLLOWER.format(repo=REPO, model=path, group=group)],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dpf", max_batch=8, cache_capacity=0,
+                           engine={"device": "cpu", "dp_world": 2, "dp_group": group})
+        x, ref = _verify_set(native, path, cfg, 8, seed=3)
+        res = native.loadgen(port=wk.port, connections=8, requests=160, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-5, timeout_ms=120000)
+        assert res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        assert res["failed"] > 0 and res["ok"] > 0, res
+        assert res["verified"] == res["ok"]
+        h = wk.health()
+        assert h["engine"]["dp_shard_failed_items"] > 0
+        assert h["errors"] >= res["failed"]
+    finally:
+        if wk is not None:
+            wk.stop()
+        out, _ = p.communicate(timeout=60)
+    assert p.returncode == 0, out
+
+
+def test_dp_rejects_mismatched_ranks(native, models):
+    """a follower planning another program (here: bf16 vs the leader's fp32)
+    must fail the group at join time, before any collective sizes a buffer from its own plan."""
+    path, w, cfg = models["tiny"]
+    group = "die_dp_m%d" % os.getpid()
+    code = FOLLOWER.replace("device='cpu')", "device='cpu', precision='bf16')")
+    env = dict(os.environ, DIE_NO_TORCH="1")
+    p = subprocess.Popen([sys.executable, "-c", code.format(repo=REPO, model=path, group=group, rank=1, world=2, mb=8)],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+    try:
+        with pytest.raises(native.NativeError, match="plans a different program"):
+            native.Worker(path, node_id="dpm", max_batch=8, engine={"device": "cpu", "dp_world": 2, "dp_group": group})
+    finally:
+        out, _ = p.communicate(timeout=60)

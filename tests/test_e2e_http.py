@@ -375,18 +375,24 @@ def test_large_bodies_cross_shared_memory(native, models):
     try:
         rng = np.random.default_rng(3)
         seen = set()
-        # the ring depends on the workers' (random) ports: send until both nodes have had traffic
-        for i in range(96):
-            if i >= 16 and len(seen) == 2:
-                break
+        # the ring depends on the workers' (random) ports, and FNV-1a placements can be lopsided for
+        # similar ids (e.g. every "big_<i>", i < 96, on one node for some port pairs): pick 8 ids
+        # whose primary is each node
+        names = ["127.0.0.1:%d" % a.port, "127.0.0.1:%d" % b.port]
+        ring, keys = py_ring(names)
+        ids = []
+        for n in names:
+            ids += [rid for rid in ("big_%d" % i for i in range(20000)) if py_get(ring, keys, rid) == n][:8]
+        for i, rid in enumerate(ids):
             vals = np.round(rng.random(3 * 64 * 64), 4).tolist()
-            body = {"request_id": "big_%d" % i, "input_data": vals}
+            body = {"request_id": rid, "input_data": vals}
             st, out = post(gw.url + "/infer", body)
             assert st == 200, out
             seen.add(out["node_id"])
             direct = a if out["node_id"] == "shm_a" else b
             st2, ref = post(direct.url + "/infer", dict(body, request_id="d_%d" % i))
             assert st2 == 200 and ref["output_data"] == out["output_data"]
+        assert seen == {"shm_a", "shm_b"}
         _, s = get(gw.url + "/stats")
         assert s["shm_arena_mib"] > 0 and s["shm_forwards"] > 0 and s["byte_forwards"] > 0, s
         assert all(x["state"] == "CLOSED" and x["failures"] == 0 for x in s["circuit_breakers"]), s

@@ -18,18 +18,15 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 
 
 @pytest.fixture(params=["solo", "merge", "merge_host"])
-def dp_path(request, monkeypatch):
-    """solo: a world of one feeds its local engine directly; merge: DIE_DP_FORCE_MERGE=1 keeps the
-    multi-rank sub-batch ring + leader merge loop (what N>1 runs) at world=1, RCCL device gather;
-    merge_host: the same with DIE_DP_COMM=host (logits + decode status through the host segment)."""
-    monkeypatch.delenv("DIE_DP_COMM", raising=False)
-    if request.param.startswith("merge"):
-        monkeypatch.setenv("DIE_DP_FORCE_MERGE", "1")
-    else:
-        monkeypatch.delenv("DIE_DP_FORCE_MERGE", raising=False)
-    if request.param == "merge_host":
-        monkeypatch.setenv("DIE_DP_COMM", "host")
+def dp_path(request):
+    """Engine options of each DP path.  solo: a world of one feeds its local engine directly;
+    merge: dp_force_merge keeps the multi-rank sub-batch ring + leader merge loop (what N>1 runs)
+    at world=1, RCCL device gather; merge_host: the same with dp_backend "host" (logits + decode
+    status through the host segment)."""
     return request.param
+
+
+DP_OPTS = {"solo": {}, "merge": {"dp_force_merge": True}, "merge_host": {"dp_force_merge": True, "dp_backend": "host"}}
 
 
 BACKEND = {"solo": "none", "merge": "rccl", "merge_host": "host"}
@@ -41,7 +38,7 @@ def test_dp_engine_rccl_world1_matches_plain_engine(native, models, dp_path):
     path, w, cfg = models["tiny"]
     plain = native.Engine(path, device="hip", max_batch=8, autotune=False)
     dp = native.Engine(path, device="hip", max_batch=8, autotune=False, dp_world=1,
-                       dp_group="die_gpu_dp_%s_%d" % (dp_path, os.getpid()))
+                       dp_group="die_gpu_dp_%s_%d" % (dp_path, os.getpid()), **DP_OPTS[dp_path])
     info = dp.refresh_info()
     # solo: no communicator is formed (its host threads cost the serving path ~13 %)
     assert info["name"].startswith("dp1(%s):hip:gfx950" % BACKEND[dp_path])
@@ -58,8 +55,9 @@ def test_dp_worker_rccl_world1_http(native, models, dp_path):
 
     path, w, cfg = models["tiny"]
     wk = native.Worker(path, node_id="dp", max_batch=8,
-                       engine={"device": "hip", "dp_world": 1,
-                               "dp_group": "die_gpu_dpw_%s_%d" % (dp_path, os.getpid()), "autotune": False})
+                       engine=dict({"device": "hip", "dp_world": 1,
+                                    "dp_group": "die_gpu_dpw_%s_%d" % (dp_path, os.getpid()), "autotune": False},
+                                   **DP_OPTS[dp_path]))
     ref_eng = native.Engine(path, device="hip", max_batch=8, autotune=False)
     try:
         h = wk.health()
@@ -92,13 +90,62 @@ def test_dp_worker_rccl_world1_http(native, models, dp_path):
         ref_eng.close()
 
 
+def _verify_set(native, path, cfg, k, seed, max_batch=8):
+    from die_amd.models import resnet_v2 as r
+
+    x = r.synthetic_input(k, cfg, seed=seed).reshape(k, -1)
+    plain = native.Engine(path, device="hip", max_batch=max_batch, autotune=False)
+    ref = np.concatenate([plain.run(x[i:i + max_batch]) for i in range(0, k, max_batch)])
+    plain.close()
+    return x, ref
+
+
+def test_dp_rccl_world1_concurrent_rows_verified(native, models, dp_path):
+    """Every DP path under concurrent load (16 connections, K=12 distinct inputs, cache off so every
+    request is computed): multi-row batches from several sub-batches, every answer compared with its
+    input's expected logits (fp32 across batch buckets: rel-L2 <= 1e-4)."""
+    path, w, cfg = models["tiny"]
+    wk = native.Worker(path, node_id="dpv", max_batch=8, cache_capacity=0,
+                       engine=dict({"device": "hip", "dp_world": 1, "autotune": False,
+                                    "dp_group": "die_gpu_dpv_%s_%d" % (dp_path, os.getpid())}, **DP_OPTS[dp_path]))
+    try:
+        x, ref = _verify_set(native, path, cfg, 12, seed=21)
+        res = native.loadgen(port=wk.port, connections=16, requests=384, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4)
+        assert res["ok"] == 384 and res["failed"] == 0, res
+        assert res["verified"] == 384 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        h = wk.health()
+        assert h["cache_hits"] == 0 and h["engine"]["dp_batches"] < 384
+    finally:
+        wk.stop()
+
+
+def test_dp_rccl_world1_injected_failure_does_not_hang(native, models):
+    """A rank whose batch fails before reaching the device still issues its collectives (shard flag
+    cleared), so RCCL never waits on it: the failed batches' requests get 500s, every other answer
+    is right, and the worker keeps serving."""
+    path, w, cfg = models["tiny"]
+    wk = native.Worker(path, node_id="dpf", max_batch=8, cache_capacity=0,
+                       engine={"device": "hip", "dp_world": 1, "autotune": False, "dp_force_merge": True,
+                               "fail_batch_every": 3, "dp_group": "die_gpu_dpf_%d" % os.getpid()})
+    try:
+        x, ref = _verify_set(native, path, cfg, 8, seed=4)
+        res = native.loadgen(port=wk.port, connections=8, requests=160, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4, timeout_ms=30000)
+        assert res["mismatched"] == 0 and res["failed"] > 0 and res["ok"] > 0, res
+        h = wk.health()
+        assert h["engine"]["dp_backend"] == "rccl" and h["engine"]["options"]["fail_batch_every"] == 3
+    finally:
+        wk.stop()
+
+
 RANK1 = """
 import sys, os, json
 sys.path.insert(0, {repo!r})
-import torch
 import die_amd
+import torch
 from die_amd import native
-w = native.Worker({model!r}, node_id='dp-r1', port={port}, reuse_port=True, max_batch=16,
+w = native.Worker({model!r}, node_id='dp-r1', port={port}, reuse_port=True, max_batch=16, cache_capacity=0,
                   engine=dict(device='hip', device_id=1, dp_world=2, dp_group={group!r}, dp_rank=1, autotune=False))
 print('READY', flush=True)
 sys.stdin.readline()
@@ -109,8 +156,10 @@ w.stop()
 
 def test_dp_rccl_two_ranks(native, models):
     """Two RCCL ranks on two GPUs (skipped on a 1-GPU box: RCCL refuses two ranks on one device):
-    the follower's weights arrive by ncclBroadcast, per-sample-identifiable inputs come back in item
-    order through ncclAllGather, and both ranks ingest HTTP on the shared port."""
+    the follower's weights arrive by ncclBroadcast, both ranks ingest HTTP on the shared port, and
+    under 32 concurrent connections (multi-row DP batches merged from both ranks' sub-batches) every
+    answer is checked against its input's expected logits -- a shard/gather order mix-up would
+    swap rows and show up as a mismatch."""
     import socket
     import subprocess
     import sys
@@ -119,8 +168,6 @@ def test_dp_rccl_two_ranks(native, models):
 
     if torch.cuda.device_count() < 2:
         pytest.skip("needs 2 GPUs")
-    from die_amd.models import resnet_v2 as r
-
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path, w, cfg = models["tiny"]
     s = socket.socket()
@@ -131,27 +178,22 @@ def test_dp_rccl_two_ranks(native, models):
     p = subprocess.Popen([sys.executable, "-c", RANK1.format(repo=repo, model=path, port=port, group=group)],
                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     wk = None
-    plain = native.Engine(path, device="hip", max_batch=16, autotune=False)
+    x, ref = _verify_set(native, path, cfg, 24, seed=5, max_batch=16)
     try:
-        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=16,
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=16, cache_capacity=0,
                            engine={"device": "hip", "dp_world": 2, "dp_group": group, "autotune": False})
         line = p.stdout.readline().decode()
         assert "READY" in line, line
-        res = native.loadgen(port=port, connections=16, requests=256, payload="full", input_numel=3 * 64 * 64)
-        assert res["ok"] == 256 and res["failed"] == 0, res
-        x = r.synthetic_input(12, cfg, seed=5).reshape(12, -1)
-        ref = plain.run(x)
-        for i in range(12):  # distinct inputs: a shard/gather order mix-up would swap rows
-            body = json.dumps({"request_id": "two%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
-            out = json.loads(urllib.request.urlopen(urllib.request.Request("http://127.0.0.1:%d/infer" % port,
-                                                                           data=body), timeout=60).read())
-            np.testing.assert_allclose(np.array(out["output_data"], np.float32), ref[i], rtol=1e-4, atol=1e-5)
+        res = native.loadgen(port=port, connections=32, requests=768, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4)
+        assert res["ok"] == 768 and res["failed"] == 0, res
+        assert res["verified"] == 768 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
         h0 = wk.health()
         assert h0["engine"]["dp_backend"] == "rccl" and h0["engine"]["dp_world"] == 2
+        assert h0["engine"]["dp_batches"] < 768
     finally:
         if wk is not None:
             wk.stop()
         out, _ = p.communicate(b"stop\n", timeout=120)
-        plain.close()
     h1 = [json.loads(l[7:]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
     assert h1 and h1[0]["total_requests"] > 0 and h0["total_requests"] > 0
