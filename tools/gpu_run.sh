@@ -1,0 +1,94 @@
+#!/bin/bash
+# One parameterised runner for GPU-box work (replaces round 1-2's one-off tools/gpu_r*.sh scripts).
+# Run on the box, e.g.  gpurun -- 'bash tools/gpu_run.sh <out-name> <task> [args...]'
+#
+# Every step runs under its own time limit and the chain stops at the first failure.  Results go to
+# gpurun_out/<out-name>/ (merged back by gpurun); summaries worth keeping are copied to profiles/.
+#
+# tasks:
+#   tests [pytest -k expr]        the GPU suite (-m gpu), one process, per-test timeouts
+#   smoke                         __graft_entry__.smoke()
+#   bench NAME [bench.py args]    one bench.py run -> NAME.json, one summary line
+#   ab N NAME=ARGS...             N interleaved rounds of bench.py variants: "fp32=--precision fp32" ...
+#   ops ARCH B PREC               per-op device time table (tools/op_profile.py)
+#   rocprof NAME [bench.py args]  rocprofv3 --kernel-trace --stats around bench.py, summary via tools/prof_summary.py
+#   pmc ARCH B PREC               4 PMC passes of one forward (tools/pmc_forward.py) -> pmc_<arch>_<prec>_b<B>.md
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+NAME=$1; TASK=$2; shift 2
+O=$R/gpurun_out/$NAME
+mkdir -p "$O"
+export DIE_TUNE_CACHE=${DIE_TUNE_CACHE:-$O/tune.json}
+cd "$R" || exit 1
+
+summ() {  # one line per bench JSON
+  python3 - "$1" "$2" <<'EOF'
+import json, sys
+d = json.load(open(sys.argv[1]))
+dw = d.get("direct_worker", {})
+dp = d.get("dp_rccl") or {}
+print(sys.argv[2], round(d["value"]), "p50", d.get("p50_ms"), "p99", d.get("p99_ms"), "batch", d.get("avg_batch") or d.get("avg_dp_batch"),
+      "dev_ms", d.get("device_ms_per_batch"), "gap_ms", d.get("gpu_gap_ms_per_batch"), "cache_hits", d.get("cache_hits_timed"),
+      "direct", round(dw.get("rps_this_rank", 0)), dw.get("p99_ms"), "dp_rccl", dp.get("requests_per_s"), dp.get("p99_ms"), dp.get("error", ""))
+EOF
+}
+
+bench() {
+  local n=$1; shift
+  timeout -k 10 600 python3 bench.py "$@" > "$O/$n.json" 2> "$O/$n.err" || { tail -20 "$O/$n.err"; return 1; }
+  summ "$O/$n.json" "$n"
+}
+
+case "$TASK" in
+  tests)
+    K=()
+    [ -n "$1" ] && K=(-k "$1")
+    timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${K[@]}" > "$O/tests.log" 2>&1 \
+      || { grep -E "Error|assert|FAIL" "$O/tests.log" | cut -c1-300 | tail -20; tail -5 "$O/tests.log"; exit 1; }
+    tail -2 "$O/tests.log" ;;
+  smoke)
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -20 "$O/smoke.log"; exit 1; }
+    tail -1 "$O/smoke.log" ;;
+  bench)
+    n=$1; shift
+    bench "$n" "$@" || exit 1 ;;
+  ab)
+    rounds=$1; shift
+    for r in $(seq 1 "$rounds"); do
+      for v in "$@"; do
+        n=${v%%=*}; a=${v#*=}
+        # shellcheck disable=SC2086
+        bench "${n}_$r" $a || exit 1
+      done
+    done ;;
+  ops)
+    timeout -k 10 300 python3 -u tools/op_profile.py --arch "$1" --batch "$2" --precision "$3" --out "$O/ops_$1_$3_b$2.md" \
+      > "$O/ops.log" 2>&1 || { tail -20 "$O/ops.log"; exit 1; }
+    sed -n 3p "$O/ops_$1_$3_b$2.md" ;;
+  rocprof)
+    n=$1; shift
+    cd /tmp && export TMPDIR=/tmp && cd "$R" || exit 1
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$n" -o p -- python3 bench.py --no-dp "$@" > "$O/$n.json" 2> "$O/$n.err" \
+      || { tail -20 "$O/$n.err"; exit 1; }
+    summ "$O/$n.json" "$n"
+    python3 tools/prof_summary.py "$O/$n" > "$O/$n.md" 2>&1 && head -30 "$O/$n.md" ;;
+  pmc)
+    A=$1; B=$2; P=$3; D=$O/pmc_${A}_${P}_b$B
+    cd /tmp && export TMPDIR=/tmp && cd "$R" || exit 1
+    run_pass() {
+      local k=$1; shift
+      timeout -s KILL 180 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$D/p$k" -o p -- \
+        python3 tools/pmc_forward.py "$A" "$B" 2 "$P" tuned > "$D.p$k.log" 2>&1
+    }
+    run_pass 1 GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS && \
+    run_pass 2 FETCH_SIZE && \
+    run_pass 3 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum && \
+    run_pass 4 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_MFMA \
+      || { tail "$D".p*.log; exit 1; }
+    python3 tools/pmc_summary.py "$D" --title "$A $P B=$B tuned" --note "production (autotuned) kernel configs, eager launches" \
+      > "$O/pmc_${A}_${P}_b$B.md" || exit 1
+    tail -1 "$O/pmc_${A}_${P}_b$B.md" ;;
+  *)
+    echo "unknown task $TASK"; exit 2 ;;
+esac
