@@ -224,7 +224,10 @@ def main():
                                 "upstream_connections": g1.get("upstream_connections_opened"),
                                 "shm_forwards": g1.get("shm_forwards", 0) - g0.get("shm_forwards", 0),
                                 "byte_forwards": g1.get("byte_forwards", 0) - g0.get("byte_forwards", 0),
-                                "breakers": [b["state"] for b in g1["circuit_breakers"]]}
+                                "breakers": [b["state"] for b in g1["circuit_breakers"]],
+                                # per-stage p50/p99 (warm-up included): where a gateway tail comes from
+                                "stages_us": {k: [round(v["p50_us"], 1), round(v["p99_us"], 1)]
+                                              for k, v in g1.get("stages_us", {}).items()}}
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()
@@ -347,6 +350,7 @@ def main():
                        "max_batch_per_gpu": B, "requests": int(ok + failed), "connections_per_gpu": args.connections},
         }
         extra["numa"] = numa
+        extra["hip_hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
         out.update({k: v for k, v in extra.items() if v is not None})
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     hg.close()

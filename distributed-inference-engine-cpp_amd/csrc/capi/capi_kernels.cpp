@@ -203,6 +203,30 @@ int die_kern_stem_nchw(uint64_t x, int C, uint64_t scale, uint64_t shift, uint64
                                                   Ho, Wo, relu, S(stream), nullptr, split, max_blocks));
 }
 
+// Load-time support report: every node the HIP planner cannot lower, with the reason.
+char* die_plan_report(const char* model_path, int split, char** err) {
+  try {
+    const PlanReport r = plan_report(onnx::load_onnx(model_path), 8, split != 0);
+    Json j = Json::object();
+    j["supported"] = r.supported;
+    Json items = Json::array();
+    for (const auto& it : r.unsupported) {
+      Json e = Json::object();
+      e["node"] = it.node;
+      e["op"] = it.op;
+      e["error"] = it.error;
+      items.push_back(e);
+    }
+    j["unsupported"] = items;
+    j["blocked"] = r.blocked;
+    j["text"] = r.text();
+    return dup(j.dump());
+  } catch (const std::exception& e) {
+    if (err) *err = dup(e.what());
+    return nullptr;
+  }
+}
+
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, char** err) {
   try {
@@ -216,7 +240,9 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
     Json ops = Json::array();
     for (auto& o : p.ops) {
       Json e = Json::object();
-      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32", "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax"};
+      static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
+                                    "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
+                                    "rows_prep", "copy_cols", "binary", "unary"};
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;

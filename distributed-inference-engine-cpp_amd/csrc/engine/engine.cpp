@@ -305,7 +305,15 @@ std::unique_ptr<Engine> create_engine(const std::string& model_path, const Engin
   if (opt.dp_world >= 1 && !opt.dp_group.empty() && opt.dp_comm == nullptr) return create_dp_engine(model_path, opt);
   if (opt.device != "cpu") {
     std::string why;
-    auto e = create_hip_engine(model_path, opt, &why);
+    std::unique_ptr<Engine> e;
+    try {
+      e = create_hip_engine(model_path, opt, &why);
+    } catch (const std::exception& ex) {
+      // device "auto" keeps the reference's EP fallback (src/inference_engine.cpp:21-29): a graph
+      // the HIP planner cannot lower (every unsupported node is listed) runs on the CPU executor
+      if (opt.device == "hip") throw;
+      why = ex.what();
+    }
     if (e) return e;
     if (opt.device == "hip") throw std::runtime_error("HIP engine unavailable: " + why);
     DIE_LOG(WARN, "HIP engine unavailable (" << why << "); falling back to the CPU executor");

@@ -987,8 +987,32 @@ class HipEngine : public Engine {
       }
       switch (op.kind) {
         case PlanOp::INPUT_PREP:
-          e = kern::input_prep(static_cast<const float*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
-                               static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st, sp_);
+          if (op.Cp > 8)
+            e = kern::input_prep_wide(static_cast<const float*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
+                                      static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st, sp_);
+          else
+            e = kern::input_prep(static_cast<const float*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
+                                 static_cast<uint16_t*>(buf(op.out)), B, op.C, op.H, op.W, op.Cp, st, sp_);
+          break;
+        case PlanOp::ROWS_PREP:
+          e = kern::rows_prep(static_cast<const float*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
+                              op.rows_per_sample * B, op.C, op.Cp, st, sp_);
+          break;
+        case PlanOp::COPY_COLS: {
+          const long long R = op.rows_per_sample * B;
+          e = kern::copy_cols(static_cast<const uint16_t*>(buf(op.in)), R * op.ld[0], op.ld[0], op.col[0],
+                              static_cast<uint16_t*>(buf(op.out)), R * op.ld[1], op.ld[1], op.col[1], R, op.C, st, sp_);
+          break;
+        }
+        case PlanOp::BINARY:
+          e = kern::binary_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
+                                static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, op.rows_per_sample,
+                                op.S, op.gidx, op.act, op.clip_lo, op.clip_hi, st, live, sp_);
+          break;
+        case PlanOp::UNARY:
+          e = kern::unary_rows(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
+                               static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, op.act, op.clip_lo,
+                               op.clip_hi, st, live, op.rows_per_sample, sp_);
           break;
         case PlanOp::CONV: {
           kern::ConvArgs a = conv_args(op, B, s);
@@ -1016,8 +1040,12 @@ class HipEngine : public Engine {
                                op.rows_per_sample * B, op.C, st, live, op.rows_per_sample, sp_, op.clip_lo, op.clip_hi);
           break;
         case PlanOp::TO_NCHW_F32:
-          e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
-                                     op.H, op.W, op.C, st, sp_);
+          if (op.ld_store > 0)
+            e = kern::nhwc_to_nchw_f32_strided(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
+                                               B, op.H, op.W, op.C, op.ld_store, st, sp_);
+          else
+            e = kern::nhwc_to_nchw_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)), B,
+                                       op.H, op.W, op.C, st, sp_);
           break;
         case PlanOp::STEM:
           if (op.in == -2) {  // graph input, input prep fused
@@ -1081,11 +1109,15 @@ class HipEngine : public Engine {
         }
         case PlanOp::SOFTMAX:
           e = kern::softmax_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                 static_cast<float*>(buf(op.out_f32)), op.rows_per_sample * B, op.C, st, sp_);
+                                 static_cast<float*>(buf(op.out_f32)), op.rows_per_sample * B, op.C, st, sp_, op.ld_store);
           break;
         case PlanOp::BF16_TO_F32:
-          e = kern::bf16_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
-                                static_cast<long long>(B) * op.C, st, sp_);
+          if (op.ld_store > 0)
+            e = kern::rows_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
+                                  op.rows_per_sample * B, op.C, op.ld_store, st, sp_);
+          else
+            e = kern::bf16_to_f32(static_cast<const uint16_t*>(buf(op.in)), static_cast<float*>(buf(op.out_f32)),
+                                  static_cast<long long>(B) * op.C, st, sp_);
           break;
       }
       if (e != hipSuccess)

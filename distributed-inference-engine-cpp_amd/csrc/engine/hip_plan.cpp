@@ -44,9 +44,17 @@ struct Val {
     ATTN,        // attention chain: stage 0 = Q K^T, 1 = softmax, 2 = (P V) with logical perm
     SHAPE,       // int64 shape-computation value (ints known unless `known` is false)
     BCAST_INIT,  // Expand(initializer, shape) -> [B, 1, C]
-    TOKCAT       // Concat([cls, patch rows], axis=1)
+    TOKCAT,      // Concat([cls, patch rows], axis=1)
+    UNKNOWN      // produced by a node the planner could not lower (support report)
   } kind = NHWC;
   int C = 0, H = 1, W = 1;
+  // Stored vs logical channels: rows / NHWC pixels are stored with C channels (a multiple of 8:
+  // 16-byte vectors, MFMA K/N steps); `cl` is the model's channel count when that is smaller (pad
+  // channels hold finite values that every consumer ignores: zero weights, dropped on output).
+  int cl = 0;
+  // ROWS_BF16 from Flatten/Reshape of an NHWC map with H*W > 1: ONNX order is (c, h, w), the buffer
+  // holds (h, w, c); a Gemm/MatMul consumer permutes its weight rows instead of the data.
+  int flat_hw = 0, flat_c = 0;
   int buf = -1;
   int rank = 0;         // ROWS: 2 or 3
   int ld = 0, col = 0;  // ROWS/HEADS: row pitch (0 -> C) and column offset, in elements
@@ -63,39 +71,53 @@ struct Val {
   std::string init_name;
   int patches = -1;
   int pitch() const { return ld ? ld : C; }
+  int logical() const { return cl ? cl : C; }
+  bool padded() const { return cl && cl != C; }
 };
+
+int round8(int c) { return (c + 7) / 8 * 8; }
 
 class Planner {
  public:
   Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load) {}
 
+  // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
+  // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
+  PlanReport report_;
+
   Plan run() {
     if (m_.inputs.empty() || m_.outputs.empty()) throw std::runtime_error("model needs an input and an output");
     for (size_t i = 0; i < m_.nodes.size(); ++i)
       for (auto& in : m_.nodes[i].inputs) consumers_[in].push_back(static_cast<int>(i));
     for (auto& o : m_.outputs) graph_outputs_.insert(o.name);
-    // graph input
-    const auto& vi = m_.inputs[0];
-    if (vi.dims.size() != 4) throw std::runtime_error("HIP engine expects a 4-D NCHW image input, got rank " + std::to_string(vi.dims.size()));
-    Val in;
-    in.kind = Val::GRAPH_IN;
-    in.C = static_cast<int>(vi.dims[1]);
-    in.H = static_cast<int>(vi.dims[2]);
-    in.W = static_cast<int>(vi.dims[3]);
-    in.buf = kBufGraphIn;
-    if (in.C <= 0 || in.H <= 0 || in.W <= 0) throw std::runtime_error("input dims must be static except the batch");
-    define(vi.name, in);
-    plan_.input_shape = {1, in.C, in.H, in.W};
     plan_.split = split_;
-    plan_.input_numel = static_cast<size_t>(in.C) * in.H * in.W;
+    define_graph_input();
 
     done_.assign(m_.nodes.size(), false);
     for (size_t i = 0; i < m_.nodes.size(); ++i) {
       if (done_[i]) continue;
       done_[i] = true;
-      lower(static_cast<int>(i));
+      const Node& n = m_.nodes[i];
+      bool blocked = false;
+      for (const auto& in : n.inputs) {
+        auto it = vid_.find(in);
+        if (it != vid_.end() && vals_[it->second].kind == Val::UNKNOWN) blocked = true;
+      }
+      if (blocked) {
+        report_.blocked++;
+        mark_unknown(n);
+        continue;
+      }
+      try {
+        lower(static_cast<int>(i));
+      } catch (const std::exception& e) {
+        report_.supported = false;
+        report_.unsupported.push_back(PlanReport::Item{n.name, n.op_type, e.what()});
+        mark_unknown(n);
+      }
     }
+    if (!report_.supported) throw std::runtime_error("HIP engine cannot lower this graph:\n" + report_.text());
     finalize_output();
     fuse_pool_affine();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
@@ -169,6 +191,59 @@ class Planner {
   }
   void add_op(PlanOp op) { plan_.ops.push_back(std::move(op)); }
 
+  void mark_unknown(const Node& n) {
+    Val u;
+    u.kind = Val::UNKNOWN;
+    for (const auto& o : n.outputs)
+      if (!vid_.count(o)) define(o, u);
+  }
+
+  // Graph input 0 (the reference binds input 0 of any model, src/inference_engine.cpp:35-52):
+  //  * rank 4 [N, C, H, W]: an image (lazy: folded into the stem or an input-prep pass);
+  //  * rank 2 [N, F] / rank 3 [N, S, F]: rows -> one ROWS_PREP pass (f32 -> bf16 / split, F padded
+  //    to a multiple of 8).
+  void define_graph_input() {
+    const auto& vi = m_.inputs[0];
+    const size_t r = vi.dims.size();
+    for (size_t k = 1; k < r; ++k)
+      if (vi.dims[k] <= 0) throw std::runtime_error("input dims must be static except the batch");
+    if (r == 4) {
+      Val in;
+      in.kind = Val::GRAPH_IN;
+      in.C = static_cast<int>(vi.dims[1]);
+      in.H = static_cast<int>(vi.dims[2]);
+      in.W = static_cast<int>(vi.dims[3]);
+      in.buf = kBufGraphIn;
+      define(vi.name, in);
+      plan_.input_shape = {1, in.C, in.H, in.W};
+      plan_.input_numel = static_cast<size_t>(in.C) * in.H * in.W;
+      return;
+    }
+    if (r != 2 && r != 3)
+      throw std::runtime_error("HIP engine takes a rank-2, -3 or -4 input, got rank " + std::to_string(r));
+    const int S = r == 3 ? static_cast<int>(vi.dims[1]) : 1;
+    const int F = static_cast<int>(vi.dims[r - 1]);
+    PlanOp p;
+    p.kind = PlanOp::ROWS_PREP;
+    p.name = "rows_prep";
+    p.in = kBufGraphIn;
+    p.C = F;
+    p.Cp = round8(F);
+    p.rows_per_sample = S;
+    p.out = new_buf(static_cast<size_t>(S) * p.Cp * 2);
+    Val v;
+    v.kind = Val::ROWS_BF16;
+    v.C = p.Cp;
+    v.cl = p.Cp != F ? F : 0;
+    v.H = S;
+    v.rank = static_cast<int>(r);
+    v.buf = p.out;
+    add_op(std::move(p));
+    define(vi.name, v);
+    plan_.input_shape = r == 3 ? std::vector<int64_t>{1, S, F} : std::vector<int64_t>{1, F};
+    plan_.input_numel = static_cast<size_t>(S) * F;
+  }
+
   // BN parameters -> per-channel (scale, shift).
   void bn_affine(const Node& bn, std::vector<float>& sc, std::vector<float>& sh) {
     const auto& g = init(bn.in(1), bn).f;
@@ -208,6 +283,7 @@ class Planner {
     if (op == "LayerNormalization") return lower_layernorm(idx);
     if (op == "Gather") return lower_gather(idx);
     if (op == "Concat") return lower_concat(idx);
+    if (op == "Sigmoid" || op == "Tanh" || op == "LeakyRelu" || op == "Gelu") return lower_unary(idx);
     if (op == "Identity" || op == "Dropout") {
       Val v = val(n.in(0), n);
       define(n.outputs[0], v);
@@ -227,8 +303,7 @@ class Planner {
     p.C = x.C;
     p.H = x.H;
     p.W = x.W;
-    if (x.C > 8) throw std::runtime_error("HIP engine: input with more than 8 channels is not supported");
-    p.Cp = x.C <= 4 ? 4 : 8;
+    p.Cp = x.C <= 4 ? 4 : round8(x.C);  // > 8 channels: input_prep_wide
     if (x.has_affine) {
       p.scale_off = push_f32(x.asc);
       p.shift_off = push_f32(x.ash);
@@ -261,14 +336,14 @@ class Planner {
     if (x.kind == Val::GRAPH_IN) {
       deferred_prep = KH == 7 && KW == 7 && x.C <= 4;
       in_buf = deferred_prep ? -2 : ensure_nhwc_input(x, n.in(0));
-      Cstore = x.C <= 4 ? 4 : 8;
+      Cstore = x.C <= 4 ? 4 : round8(x.C);
     } else if (x.kind == Val::NHWC) {
       in_buf = x.buf;
-      Cstore = x.C;
+      Cstore = x.C;  // stored channels (pad channels get zero weights)
     } else {
       throw std::runtime_error("Conv " + n.name + ": input must be an image tensor");
     }
-    if (Cin != x.C) throw std::runtime_error("Conv " + n.name + ": channel mismatch");
+    if (Cin != (x.kind == Val::GRAPH_IN ? x.C : x.logical())) throw std::runtime_error("Conv " + n.name + ": channel mismatch");
     if (ap == "SAME_UPPER" || ap == "SAME_LOWER") {
       for (int d = 0; d < 2; ++d) {
         const int in = d ? x.W : x.H, k = d ? KW : KH;
@@ -286,10 +361,12 @@ class Planner {
     const int s = static_cast<int>(st[0]), d = static_cast<int>(dl[0]);
     const int Ho = (x.H + static_cast<int>(pads[0] + pads[2]) - d * (KH - 1) - 1) / s + 1;
     const int Wo = (x.W + static_cast<int>(pads[1] + pads[3]) - d * (KW - 1) - 1) / s + 1;
-    if (Cout % 8) throw std::runtime_error("Conv " + n.name + ": output channels must be a multiple of 8");
+    // Cout % 8 != 0: computed and stored with Cp channels (zero weights and bias: pad channels are
+    // act(0)), the Val remembers the logical count
+    const int Cp = round8(Cout);
 
     // --- fusion lookahead ---
-    std::vector<float> scale(Cout, 1.f), shift(Cout, 0.f);
+    std::vector<float> scale(Cp, 1.f), shift(Cp, 0.f);
     if (!n.in(2).empty()) {
       const auto& b = init(n.in(2), n).f;
       for (int c = 0; c < Cout; ++c) shift[c] = b[c];
@@ -322,8 +399,9 @@ class Planner {
       const Node& add = m_.nodes[c1];
       const std::string other = add.in(0) == cur ? add.in(1) : add.in(0);
       auto it = vid_.find(other);
-      if (it != vid_.end() && vals_[it->second].kind == Val::NHWC && vals_[it->second].C == Cout &&
-          vals_[it->second].H == Ho && vals_[it->second].W == Wo && add.in(0) != add.in(1)) {
+      if (it != vid_.end() && vals_[it->second].kind == Val::NHWC && vals_[it->second].C == Cp &&
+          vals_[it->second].logical() == Cout && vals_[it->second].H == Ho && vals_[it->second].W == Wo &&
+          add.in(0) != add.in(1)) {
         res_buf = vals_[it->second].buf;
         res_name = other;
         done_[c1] = true;
@@ -349,6 +427,8 @@ class Planner {
     }
     if (bn2 >= 0) {
       bn_affine(m_.nodes[bn2], s2, b2);
+      s2.resize(Cp, 1.f);
+      b2.resize(Cp, 0.f);
       done_[bn2] = true;
       out2_name = m_.nodes[bn2].outputs[0];
       const int c3 = sole_consumer(out2_name);
@@ -365,7 +445,7 @@ class Planner {
     // --- weights: [Npad][Kpad] bf16, k = (ky*KW + kx)*Cstore + ci ---
     const int K = KH * KW * Cstore;
     const int Kpad = static_cast<int>(round_up(K, 64));
-    const int Npad = static_cast<int>(round_up(Cout, 128));
+    const int Npad = static_cast<int>(round_up(Cp, 128));
     std::vector<float> wp(static_cast<size_t>(Npad) * Kpad, 0.f);
     for (int co = 0; co < Cout; ++co)
       for (int ci = 0; ci < Cin; ++ci)
@@ -414,7 +494,7 @@ class Planner {
     a.Cin = Cstore;
     a.Ho = Ho;
     a.Wo = Wo;
-    a.N = Cout;
+    a.N = Cp;
     a.KH = KH;
     a.KW = KW;
     a.stride = s;
@@ -428,11 +508,12 @@ class Planner {
     a.clip_lo = clip_lo;
     a.clip_hi = clip_hi;
     p.flops_per_sample = 2.0 * Ho * Wo * Cout * (KH * KW * Cin);
-    p.tile_bmax = kern::choose_tile(max_batch_ * Ho * Wo, Cout, K);
-    const size_t out_bytes = static_cast<size_t>(Ho) * Wo * Cout * 2;
+    p.tile_bmax = kern::choose_tile(max_batch_ * Ho * Wo, Cp, K);
+    const size_t out_bytes = static_cast<size_t>(Ho) * Wo * Cp * 2;
     Val o;
     o.kind = Val::NHWC;
-    o.C = Cout;
+    o.C = Cp;
+    o.cl = Cp != Cout ? Cout : 0;
     o.H = Ho;
     o.W = Wo;
     if (need_out1) {
@@ -507,15 +588,15 @@ class Planner {
     std::vector<int> used;
   };
   // Epilogue fusion lookahead for a MatMul/Gemm producing `N` columns over `rows` rows per sample.
-  GemmTail gemm_tail(const Node& n, int N, int rows, bool is_gemm) const {
+  GemmTail gemm_tail(const Node& n, int N, int rows, bool is_gemm, int N_logical) const {
     GemmTail t;
     t.out = n.outputs[0];
     int c1 = sole_consumer(t.out);
     if (!is_gemm && c1 >= 0 && m_.nodes[c1].op_type == "Add" && is_init(other_input(m_.nodes[c1], t.out))) {
       const auto& c = m_.initializers.at(other_input(m_.nodes[c1], t.out)).f;
-      if (c.size() == static_cast<size_t>(N) || c.size() == 1) {
-        t.bias.resize(N);
-        for (int j = 0; j < N; ++j) t.bias[j] = c[c.size() == 1 ? 0 : j];
+      if (c.size() == static_cast<size_t>(N_logical) || c.size() == 1) {
+        t.bias.assign(N, 0.f);
+        for (int j = 0; j < N_logical; ++j) t.bias[j] = c[c.size() == 1 ? 0 : j];
         t.used.push_back(c1);
         t.out = m_.nodes[c1].outputs[0];
         c1 = sole_consumer(t.out);
@@ -537,7 +618,8 @@ class Planner {
       auto it = vid_.find(other);
       if (it != vid_.end() && add.in(0) != add.in(1)) {
         const Val& r = vals_[it->second];
-        if (r.kind == Val::ROWS_BF16 && r.C == N && r.H * r.W == rows && r.pitch() == r.C && r.col == 0) {
+        if (r.kind == Val::ROWS_BF16 && r.C == N && r.logical() == N_logical && r.H * r.W == rows &&
+            r.pitch() == r.C && r.col == 0) {
           t.res = other;
           t.used.push_back(c1);
           t.out = add.outputs[0];
@@ -595,9 +677,13 @@ class Planner {
     const bool tb = gemm && n.get_int("transB", 0);
     const float alpha = gemm ? n.get_float("alpha", 1.f) : 1.f;
     const float beta = gemm ? n.get_float("beta", 1.f) : 1.f;
+    // K: the model's inner dimension; Ks: the stored row length (pads / NHWC-flatten order)
     const int K = static_cast<int>(tb ? wt.dims[1] : wt.dims[0]);
-    if (K != x.C) throw std::runtime_error(n.op_type + " " + n.name + ": inner dimension mismatch");
-    if (K % 8) throw std::runtime_error(n.op_type + " " + n.name + ": K % 8 must be 0");
+    const int Ks = x.C;
+    const int hw = x.flat_hw;  // Flatten of an NHWC map: logical k = c*hw + p sits at p*Cs + c
+    const int Kl = hw ? x.flat_c * hw : x.logical();
+    if (K != Kl) throw std::runtime_error(n.op_type + " " + n.name + ": inner dimension mismatch");
+    auto kstore = [&](int k) { return hw ? (k % hw) * (Ks / hw) + k / hw : k; };
 
     const std::vector<int> group = gemm ? std::vector<int>{idx} : qkv_group(idx, n.in(0), K);
     // columns of each member
@@ -610,10 +696,11 @@ class Planner {
       Ns.push_back(Nj);
       Ntot += Nj;
     }
-    const int Kpad = static_cast<int>(round_up(K, 64));
-    const int Npad = static_cast<int>(round_up(Ntot, 128));
+    const int Np = group.size() > 1 ? Ntot : round8(Ntot);  // stored columns (QKV members are % 8 already)
+    const int Kpad = static_cast<int>(round_up(Ks, 64));
+    const int Npad = static_cast<int>(round_up(Np, 128));
     std::vector<float> wp(static_cast<size_t>(Npad) * Kpad, 0.f);
-    std::vector<float> bias(Ntot, 0.f);
+    std::vector<float> bias(Np, 0.f);
     for (size_t g = 0; g < group.size(); ++g) {
       const Node& nd = m_.nodes[group[g]];
       const auto& w = init(nd.in(1), nd);
@@ -621,7 +708,7 @@ class Planner {
       for (int j = 0; j < Nj; ++j)
         for (int k = 0; k < K; ++k) {
           const float v = tb ? w.f[static_cast<size_t>(j) * K + k] : w.f[static_cast<size_t>(k) * Nj + j];
-          wp[static_cast<size_t>(offs[g] + j) * Kpad + k] = alpha * v;
+          wp[static_cast<size_t>(offs[g] + j) * Kpad + kstore(k)] = alpha * v;
         }
       if (gemm && !nd.in(2).empty()) {
         const auto& c = init(nd.in(2), nd).f;
@@ -636,12 +723,12 @@ class Planner {
     p.conv.split = split_;
     auto& a = p.conv;
     a.H = a.Ho = rows;
-    a.Cin = K;
-    a.N = Ntot;
-    a.K = K;
+    a.Cin = Ks;
+    a.N = Np;
+    a.K = Ks;
     a.Kpad = Kpad;
     p.flops_per_sample = 2.0 * rows * Ntot * K;
-    p.tile_bmax = kern::choose_tile(max_batch_ * rows, Ntot, K);
+    p.tile_bmax = kern::choose_tile(max_batch_ * rows, Np, Ks);
 
     if (group.size() > 1) {
       // bias of each member's Add; outputs are column slices of one [rows][Ntot] buffer
@@ -668,22 +755,23 @@ class Planner {
       return;
     }
 
-    const GemmTail t = gemm_tail(n, Ntot, rows, gemm);
+    const GemmTail t = gemm_tail(n, Np, rows, gemm, Ntot);
     for (int u : t.used) done_[u] = true;
-    for (int j = 0; j < Ntot && !t.bias.empty(); ++j) bias[j] += t.bias[j];
+    for (int j = 0; j < Np && !t.bias.empty(); ++j) bias[j] += t.bias[j];
     p.bias_off = push_f32(bias);
     a.relu = t.act;
     if (!t.res.empty()) p.in2 = vals_[vid_.at(t.res)].buf;
     Val o;
-    o.C = Ntot;
+    o.C = Np;
+    o.cl = Np != Ntot ? Ntot : 0;
     o.H = rows;
     o.rank = rank;
-    if (graph_outputs_.count(t.out) && consumers(t.out).empty()) {
+    if (graph_outputs_.count(t.out) && consumers(t.out).empty() && Np == Ntot) {
       p.out_f32 = kBufGraphOut;
       o.kind = Val::ROWS_F32;
       o.buf = kBufGraphOut;
     } else {
-      p.out = new_buf(static_cast<size_t>(rows) * Ntot * 2);
+      p.out = new_buf(static_cast<size_t>(rows) * Np * 2);
       o.kind = Val::ROWS_BF16;
       o.buf = p.out;
     }
@@ -843,6 +931,49 @@ class Planner {
       define(n.outputs[0], o);
       return;
     }
+    // NHWC map -> [B, C*H*W] (NCHW order): the flatten view
+    if (x.kind == Val::NHWC && x.H * x.W > 1 && shp.size() == 2 && is_batch(shp[0]) &&
+        (shp[1] == -1 || shp[1] == static_cast<int64_t>(x.logical()) * x.H * x.W)) {
+      define(n.outputs[0], flatten_nhwc(x));
+      return;
+    }
+    // dense rows [B, S*D] <-> [B, S, D] (same memory): rank-2 <-> rank-3 views
+    if (x.kind == Val::ROWS_BF16 && !x.padded() && !x.flat_hw && x.pitch() == x.C && !x.col) {
+      const int64_t total = static_cast<int64_t>(x.H) * x.W * x.C;
+      if (shp.size() == 3 && is_batch(shp[0])) {
+        int64_t S = shp[1], D = shp[2];
+        if (S == -1 && D > 0) S = total / D;
+        if (D == -1 && S > 0) D = total / S;
+        if (S > 0 && D > 0 && S * D == total && D % 8 == 0) {
+          Val o = x;
+          o.H = static_cast<int>(S);
+          o.W = 1;
+          o.C = static_cast<int>(D);
+          o.cl = 0;
+          o.rank = 3;
+          define(n.outputs[0], o);
+          return;
+        }
+      }
+      if (shp.size() == 2 && is_batch(shp[0]) && (shp[1] == -1 || shp[1] == total) && total % 8 == 0) {
+        Val o = x;
+        o.H = o.W = 1;
+        o.C = static_cast<int>(total);
+        o.cl = 0;
+        o.rank = 2;
+        define(n.outputs[0], o);
+        return;
+      }
+    }
+    // one row per sample [B, C] -> [B, C, 1, 1] (gates broadcast over an image: squeeze-excitation)
+    if ((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H * x.W == 1 && shp.size() == 4 && is_batch(shp[0]) &&
+        shp[1] == x.logical() && shp[2] == 1 && shp[3] == 1 && !x.flat_hw) {
+      Val o = x;
+      o.kind = Val::NHWC;
+      o.rank = 0;
+      define(n.outputs[0], o);
+      return;
+    }
     // rows with a single row per sample -> [B, C]
     if ((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H * x.W == 1 && shp.size() == 2) {
       Val o = x;
@@ -904,6 +1035,19 @@ class Planner {
 
   void lower_scale(int idx) {
     const Node& n = m_.nodes[idx];
+    {  // standalone erf-GELU (x / sqrt2 -> Erf -> + 1 -> * x -> * 0.5) on any activation
+      std::vector<int> used;
+      std::string gout;
+      auto xi = vid_.find(n.in(0));
+      if ((n.op_type == "Div" || n.op_type == "Mul") && xi != vid_.end() &&
+          (vals_[xi->second].kind == Val::NHWC || vals_[xi->second].kind == Val::ROWS_BF16) &&
+          match_gelu(n.in(0), used, gout)) {
+        const Val x = vals_[xi->second];
+        for (int u : used) done_[u] = true;
+        return emit_unary(n, x, 2, 0.f, 0.f, gout);
+      }
+    }
+    if (lower_binary_acts(n)) return;
     auto it = m_.initializers.find(n.in(1));
     if (n.op_type != "Sub" && vid_.count(n.in(0))) {
       const Val& x = vals_[vid_.at(n.in(0))];
@@ -921,9 +1065,9 @@ class Planner {
       if (!vid_.count(an) || !is_init(cn)) continue;
       const Val& x = vals_[vid_.at(an)];
       const auto& c = m_.initializers.at(cn).f;
-      if (c.size() != 1 && static_cast<int>(c.size()) != x.C) continue;
+      if (c.size() != 1 && static_cast<int>(c.size()) != x.logical()) continue;
       std::vector<float> sc(x.C, 1.f), sh(x.C, 0.f);
-      for (int k = 0; k < x.C; ++k) {
+      for (int k = 0; k < x.logical(); ++k) {
         const float v = c[c.size() == 1 ? 0 : k];
         if (n.op_type == "Mul") sc[k] = v;
         else if (n.op_type == "Div" && side == 0) sc[k] = 1.f / v;
@@ -956,13 +1100,14 @@ class Planner {
       return;
     }
     const int rank = x.rank ? x.rank : 2;
-    if ((x.kind == Val::ROWS_BF16 || (x.kind == Val::NHWC && x.H * x.W == 1)) && x.pitch() == x.C && !x.col &&
+    if ((x.kind == Val::ROWS_BF16 || (x.kind == Val::NHWC && x.H * x.W == 1)) && dense(x) &&
         (axis == -1 || axis == rank - 1)) {
       PlanOp p;
       p.kind = PlanOp::SOFTMAX;
       p.name = n.name;
       p.in = x.buf;
-      p.C = x.C;
+      p.C = x.logical();  // pad columns: skipped by the reduction, written 0
+      p.ld_store = x.padded() ? x.C : 0;
       p.rows_per_sample = static_cast<long long>(x.H) * x.W;
       Val o = x;
       o.kind = Val::ROWS_BF16;
@@ -985,8 +1130,8 @@ class Planner {
   void lower_layernorm(int idx) {
     const Node& n = m_.nodes[idx];
     const Val x = val(n.in(0), n);
-    if (x.kind != Val::ROWS_BF16 || x.pitch() != x.C || x.col)
-      throw std::runtime_error("LayerNormalization " + n.name + ": input must be dense rows");
+    if (x.kind != Val::ROWS_BF16 || !dense(x) || x.padded())
+      throw std::runtime_error("LayerNormalization " + n.name + ": input must be dense rows with C % 8 == 0");
     const int64_t axis = n.get_int("axis", -1);
     if (!(axis == -1 || axis == (x.rank ? x.rank : 2) - 1)) throw std::runtime_error("LayerNormalization: axis must be last");
     if (x.C % 8 || x.C > 2048) throw std::runtime_error("LayerNormalization: C % 8 == 0 and C <= 2048 required");
@@ -1057,7 +1202,7 @@ class Planner {
         return;
       }
     }
-    throw std::runtime_error("Concat " + n.name + ": only the [cls, patches] token concat is supported");
+    return general_concat(n, n.get_int("axis", 0));
   }
 
   // TOKCAT (+ optional position embedding initializer) -> token assembly kernel.
@@ -1229,6 +1374,33 @@ class Planner {
   void lower_reduce_mean(int idx) {
     const Node& n = m_.nodes[idx];
     const Val x = val(n.in(0), n);
+    {  // mean over the spatial axes of an image / the token axis of rows: the GAP kernel
+      std::vector<int64_t> ax = n.get_ints("axes");
+      if (ax.empty() && n.inputs.size() > 1 && !n.in(1).empty()) ints_of(n.in(1), ax);
+      std::sort(ax.begin(), ax.end());
+      const bool keep = n.get_int("keepdims", 1) != 0;
+      const bool spatial = x.kind == Val::NHWC && (ax == std::vector<int64_t>{2, 3} || ax == std::vector<int64_t>{-2, -1});
+      const bool tokens = x.kind == Val::ROWS_BF16 && x.rank == 3 && (ax == std::vector<int64_t>{1} || ax == std::vector<int64_t>{-2});
+      if ((spatial || tokens) && dense(x)) {
+        PlanOp p;
+        p.kind = PlanOp::GAP;
+        p.name = n.name;
+        p.in = x.buf;
+        p.C = x.C;
+        p.H = x.H;
+        p.W = x.W;
+        p.out = new_buf(static_cast<size_t>(x.C) * 2);
+        Val o;
+        o.kind = spatial && keep ? Val::NHWC : Val::ROWS_BF16;
+        o.C = x.C;
+        o.cl = x.cl;
+        o.rank = tokens && keep ? 3 : 2;
+        o.buf = p.out;
+        define(n.outputs[0], o);
+        add_op(std::move(p));
+        return;
+      }
+    }
     auto fail = [&](const std::string& why) {
       throw std::runtime_error("ReduceMean " + n.name + ": only the decomposed LayerNormalization pattern is supported (" +
                                why + ")");
@@ -1337,7 +1509,36 @@ class Planner {
         return;
       }
     }
-    throw std::runtime_error("Slice " + n.name + ": only a single token along axis 1 of [B, S, C] rows is supported");
+    // channel-axis slice [start, end) with start % 8 == 0: a column copy
+    if (dense(x) && starts.size() == 1 && ends.size() == 1 && axes.size() == 1 && is_channel_axis(x, axes[0]) &&
+        (steps.empty() || steps[0] == 1)) {
+      const int64_t Cl = x.logical();
+      int64_t s0 = starts[0] < 0 ? starts[0] + Cl : std::min<int64_t>(starts[0], Cl);
+      int64_t e0 = ends[0] < 0 ? ends[0] + Cl : std::min<int64_t>(ends[0], Cl);
+      if (s0 >= 0 && e0 > s0 && s0 % 8 == 0 && (e0 % 8 == 0 || e0 == Cl)) {
+        const int len = static_cast<int>(e0 - s0), Cs = round8(len);
+        PlanOp p;
+        p.kind = PlanOp::COPY_COLS;
+        p.name = n.name;
+        p.in = x.buf;
+        p.col[0] = static_cast<int>(s0);
+        p.ld[0] = x.C;
+        p.col[1] = 0;
+        p.ld[1] = Cs;
+        p.C = std::min(Cs, x.C - static_cast<int>(s0));
+        p.rows_per_sample = rows_of(x);
+        p.out = new_buf(static_cast<size_t>(rows_of(x)) * Cs * 2);
+        Val o = x;
+        o.C = Cs;
+        o.cl = Cs != len ? len : 0;
+        o.buf = p.out;
+        define(n.outputs[0], o);
+        add_op(std::move(p));
+        return;
+      }
+    }
+    throw std::runtime_error("Slice " + n.name + ": supported: one token along axis 1 of [B, S, C] rows, or a channel "
+                             "range starting at a multiple of 8");
   }
 
   void lower_bn(int idx) {
@@ -1360,6 +1561,8 @@ class Planner {
       define(n.outputs[0], v);
       return;
     }
+    sc.resize(x.C, 1.f);
+    sh.resize(x.C, 0.f);
     standalone_affine(n, x, &sc, &sh, nullptr);
   }
 
@@ -1383,11 +1586,12 @@ class Planner {
       if (!vid_.count(n.in(side)) || !is_init(n.in(1 - side))) continue;
       const Val& x = vals_[vid_.at(n.in(side))];
       const auto& c = m_.initializers.at(n.in(1 - side)).f;
-      if (c.size() != 1 && static_cast<int>(c.size()) != x.C) continue;
-      std::vector<float> sc(x.C, 1.f), sh(x.C);
-      for (int k = 0; k < x.C; ++k) sh[k] = c[c.size() == 1 ? 0 : k];
+      if (c.size() != 1 && static_cast<int>(c.size()) != x.logical()) continue;
+      std::vector<float> sc(x.C, 1.f), sh(x.C, 0.f);
+      for (int k = 0; k < x.logical(); ++k) sh[k] = c[c.size() == 1 ? 0 : k];
       return standalone_affine(n, x, &sc, &sh, nullptr);
     }
+    if (lower_binary_acts(n)) return;
     const Val a = val(n.in(0), n);
     const Val b = val(n.in(1), n);
     if (a.pitch() != a.C || b.pitch() != b.C || a.col || b.col)
@@ -1395,6 +1599,127 @@ class Planner {
     if (a.kind != b.kind || a.C != b.C || a.H != b.H || a.W != b.W)
       throw std::runtime_error("Add " + n.name + ": broadcasting adds are not supported by the HIP engine");
     standalone_affine(n, a, nullptr, nullptr, &b);
+  }
+
+  // ---- general path: any-activation unary, broadcast binary, concat / slice -----------------------
+  static bool dense(const Val& v) { return (v.kind == Val::NHWC || v.kind == Val::ROWS_BF16) && v.pitch() == v.C && !v.col && !v.flat_hw; }
+  static long long rows_of(const Val& v) { return static_cast<long long>(v.H) * v.W; }
+
+  void lower_unary(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = val(n.in(0), n);
+    const std::string& op = n.op_type;
+    if (op == "Gelu" && n.get_string("approximate", "none") != "none")
+      throw std::runtime_error("Gelu " + n.name + ": only the exact (erf) form is supported");
+    const int act = op == "Sigmoid" ? 4 : op == "Tanh" ? 5 : op == "LeakyRelu" ? 6 : 2;
+    emit_unary(n, x, act, op == "LeakyRelu" ? n.get_float("alpha", 0.01f) : 0.f, 0.f, n.outputs[0]);
+  }
+
+  void emit_unary(const Node& n, const Val& x, int act, float a, float b, const std::string& out_name) {
+    if (!dense(x)) throw std::runtime_error(n.op_type + " " + n.name + ": input must be a dense image or rows tensor");
+    PlanOp p;
+    p.kind = PlanOp::UNARY;
+    p.name = n.name;
+    p.in = x.buf;
+    p.act = act;
+    p.clip_lo = a;
+    p.clip_hi = b;
+    p.C = x.C;
+    p.rows_per_sample = rows_of(x);
+    p.out = new_buf(static_cast<size_t>(rows_of(x)) * x.C * 2);
+    Val o = x;
+    o.buf = p.out;
+    o.has_affine = false;
+    define(out_name, o);
+    add_op(std::move(p));
+  }
+
+  // Add / Sub / Mul / Div of two activations: same shape, or the second one broadcast per sample
+  // ([B, C, 1, 1] or [B, C] gates over an image's pixels / a sequence's rows: squeeze-excitation,
+  // GLU-style gating).  Returns false when the operands do not fit (the caller tries other forms).
+  bool lower_binary_acts(const Node& n) {
+    if (n.inputs.size() != 2 || !vid_.count(n.in(0)) || !vid_.count(n.in(1))) return false;
+    const int op = n.op_type == "Add" ? 0 : n.op_type == "Sub" ? 1 : n.op_type == "Mul" ? 2 : n.op_type == "Div" ? 3 : -1;
+    if (op < 0) return false;
+    Val a = vals_[vid_.at(n.in(0))], b = vals_[vid_.at(n.in(1))];
+    if (!dense(a) || !dense(b) || a.C != b.C || a.logical() != b.logical()) return false;
+    int ymode;
+    if (a.kind == b.kind && a.H == b.H && a.W == b.W) {
+      if (op == 0) return false;  // plain same-shape Add: the affine kernel's residual path
+      ymode = 0;
+    } else if (rows_of(b) == 1 && rows_of(a) > 1) {
+      ymode = 1;
+    } else if (rows_of(a) == 1 && rows_of(b) > 1 && (op == 0 || op == 2)) {
+      std::swap(a, b);  // commutative: broadcast operand second
+      ymode = 1;
+    } else {
+      return false;
+    }
+    std::string cur = n.outputs[0];
+    float lo = 0.f, hi = 0.f;
+    PlanOp p;
+    p.kind = PlanOp::BINARY;
+    p.name = n.name;
+    p.in = a.buf;
+    p.in2 = b.buf;
+    p.gidx = op;
+    p.S = ymode;
+    p.act = take_act(cur, lo, hi);
+    p.clip_lo = lo;
+    p.clip_hi = hi;
+    p.C = a.C;
+    p.rows_per_sample = rows_of(a);
+    p.out = new_buf(static_cast<size_t>(rows_of(a)) * a.C * 2);
+    Val o = a;
+    o.buf = p.out;
+    o.has_affine = false;
+    define(cur, o);
+    add_op(std::move(p));
+    return true;
+  }
+
+  // The channel axis of a value (NHWC: NCHW axis 1; rows: the last axis) for Concat / Slice.
+  static bool is_channel_axis(const Val& v, int64_t axis) {
+    if (v.kind == Val::NHWC) return axis == 1 || axis == -3;
+    const int r = v.rank ? v.rank : 2;
+    return v.kind == Val::ROWS_BF16 && (axis == -1 || axis == r - 1);
+  }
+
+  void general_concat(const Node& n, int64_t axis) {
+    std::vector<Val> xs;
+    for (auto& in : n.inputs) xs.push_back(val(in, n));
+    int Cs = 0, Cl = 0;
+    for (size_t i = 0; i < xs.size(); ++i) {
+      const Val& v = xs[i];
+      if (!dense(v) || !is_channel_axis(v, axis) || v.kind != xs[0].kind || v.H != xs[0].H || v.W != xs[0].W)
+        throw std::runtime_error("Concat " + n.name + ": inputs must be dense tensors of one shape, joined on the channel axis");
+      if (i + 1 < xs.size() && v.padded())
+        throw std::runtime_error("Concat " + n.name + ": only the last input may have a channel count that is not a multiple of 8");
+      Cs += i + 1 < xs.size() ? v.logical() : v.C;
+      Cl += v.logical();
+    }
+    const int out = new_buf(static_cast<size_t>(rows_of(xs[0])) * Cs * 2);
+    int col = 0;
+    for (size_t i = 0; i < xs.size(); ++i) {
+      PlanOp p;
+      p.kind = PlanOp::COPY_COLS;
+      p.name = n.name + "#" + std::to_string(i);
+      p.in = xs[i].buf;
+      p.out = out;
+      p.col[0] = 0;
+      p.ld[0] = xs[i].C;
+      p.col[1] = col;
+      p.ld[1] = Cs;
+      p.C = xs[i].C;
+      p.rows_per_sample = rows_of(xs[0]);
+      add_op(std::move(p));
+      col += xs[i].logical();
+    }
+    Val o = xs[0];
+    o.C = Cs;
+    o.cl = Cl != Cs ? Cl : 0;
+    o.buf = out;
+    define(n.outputs[0], o);
   }
 
   void standalone_affine(const Node& n, const Val& x, const std::vector<float>* sc, const std::vector<float>* sh,
@@ -1485,6 +1810,7 @@ class Planner {
     Val o;
     o.kind = Val::NHWC;  // [C,1,1]
     o.C = x.C;
+    o.cl = x.cl;
     o.buf = p.out;
     define(n.outputs[0], o);
     add_op(std::move(p));
@@ -1494,12 +1820,29 @@ class Planner {
     const Node& n = m_.nodes[idx];
     Val x = val(n.in(0), n);
     if (n.op_type == "Flatten" && n.get_int("axis", 1) != 1) throw std::runtime_error("Flatten: axis must be 1");
+    if (x.kind == Val::NHWC && x.H * x.W > 1 && n.op_type == "Flatten") {
+      define(n.outputs[0], flatten_nhwc(x));
+      return;
+    }
     if (!((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H == 1 && x.W == 1))
       throw std::runtime_error(n.op_type + " " + n.name + ": only flattening of 1x1 feature maps is supported");
     Val o = x;
     o.kind = Val::ROWS_BF16;
     o.rank = 2;
     define(n.outputs[0], o);
+  }
+
+  // [B, C, H, W] -> [B, C*H*W] over an NHWC buffer: a lazy view in (h, w, c) order that only a
+  // Gemm/MatMul with an initializer can consume (it permutes its weight rows to match).
+  Val flatten_nhwc(const Val& x) const {
+    Val o;
+    o.kind = Val::ROWS_BF16;
+    o.rank = 2;
+    o.C = x.H * x.W * x.C;
+    o.buf = x.buf;
+    o.flat_hw = x.H * x.W;
+    o.flat_c = x.logical();
+    return o;
   }
 
   void finalize_output() {
@@ -1512,31 +1855,35 @@ class Planner {
       v = vals_[vid_.at(name + "#tokens")];
     }
     if (v.kind == Val::ROWS_F32 && v.buf == kBufGraphOut) {
-      plan_.output_shape = {1, v.C};
-      if (v.rank == 3) plan_.output_shape = {1, v.H, v.C};
+      plan_.output_shape = {1, v.logical()};
+      if (v.rank == 3) plan_.output_shape = {1, v.H, v.logical()};
     } else if (v.kind == Val::ROWS_BF16 || (v.kind == Val::NHWC && v.H == 1 && v.W == 1 &&
                                            m_.outputs[0].dims.size() == 2)) {
       PlanOp p;
       p.kind = PlanOp::BF16_TO_F32;
       p.name = "output_cast";
-      if (v.pitch() != v.C || v.col) throw std::runtime_error("graph output is a strided view");
+      if (v.pitch() != v.C || v.col || v.flat_hw) throw std::runtime_error("graph output is a strided view");
       p.in = v.buf;
-      p.C = v.C * v.H * v.W;
+      // padded rows: [rows][logical] f32 from rows of pitch C
+      p.C = v.padded() ? v.logical() : v.C * v.H * v.W;
+      p.ld_store = v.padded() ? v.C : 0;
+      p.rows_per_sample = v.padded() ? static_cast<long long>(v.H) * v.W : 1;
       p.out_f32 = kBufGraphOut;
       add_op(std::move(p));
-      plan_.output_shape = {1, v.C};
-      if (v.kind == Val::ROWS_BF16 && v.rank == 3) plan_.output_shape = {1, v.H * v.W, v.C};
+      plan_.output_shape = {1, v.logical()};
+      if (v.kind == Val::ROWS_BF16 && v.rank == 3) plan_.output_shape = {1, v.H * v.W, v.logical()};
     } else if (v.kind == Val::NHWC) {
       PlanOp p;
       p.kind = PlanOp::TO_NCHW_F32;
       p.name = "output_nchw";
       p.in = v.buf;
-      p.C = v.C;
+      p.C = v.logical();
+      p.ld_store = v.padded() ? v.C : 0;
       p.H = v.H;
       p.W = v.W;
       p.out_f32 = kBufGraphOut;
       add_op(std::move(p));
-      plan_.output_shape = {1, v.C, v.H, v.W};
+      plan_.output_shape = {1, v.logical(), v.H, v.W};
     } else {
       throw std::runtime_error("unsupported graph output layout");
     }
@@ -1710,6 +2057,26 @@ std::string Plan::summary() const {
 
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load) {
   return Planner(m, max_batch, side_branches, split, bn_on_load).run();
+}
+
+std::string PlanReport::text() const {
+  std::ostringstream os;
+  for (const Item& it : unsupported) os << "  " << it.op << " '" << it.node << "': " << it.error << "\n";
+  if (blocked) os << "  (" << blocked << " further node(s) depend on these)\n";
+  return os.str();
+}
+
+PlanReport plan_report(const onnx::Model& m, int max_batch, bool split) {
+  Planner p(m, max_batch, false, split, false);
+  try {
+    p.run();
+  } catch (const std::exception& e) {
+    if (p.report_.supported) {  // failed outside the per-node walk (input, output layout)
+      p.report_.supported = false;
+      p.report_.unsupported.push_back(PlanReport::Item{"(graph)", "", e.what()});
+    }
+  }
+  return p.report_;
 }
 
 }  // namespace die

@@ -38,7 +38,12 @@ struct PlanBuf {
 struct PlanOp {
   enum Kind {
     INPUT_PREP, CONV, POOL, GAP, AFFINE, TO_NCHW_F32, BF16_TO_F32,
-    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION, STEM, GCONV, SOFTMAX
+    LAYERNORM, TOKENS, GATHER_ROWS, ATTENTION, STEM, GCONV, SOFTMAX,
+    // general path (kernels/generic.hip)
+    ROWS_PREP,  // rank-2/3 graph input: f32 [rows][C] -> bf16 rows [rows][Cp]
+    COPY_COLS,  // out[:, col[1] + j] = in[:, col[0] + j], j < C (concat / slice); pitches ld[0], ld[1]
+    BINARY,     // out = act(in (op gidx) in2); S = 0: same shape, 1: in2 = one row per sample
+    UNARY       // out = act(in * scale + shift) with any activation code
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
@@ -52,6 +57,9 @@ struct PlanOp {
   // generic geometry
   int C = 0, H = 0, W = 0, Ho = 0, Wo = 0, Cp = 0;
   int kh = 0, kw = 0, sh = 1, sw = 1, ph = 0, pw = 0, is_max = 0, cip = 0, act = 0;
+  // stored row pitch when it differs from the logical channel count C (padded channels; 0 = C):
+  // BF16_TO_F32 / TO_NCHW_F32 drop the pad columns, SOFTMAX reads and writes rows of this pitch
+  int ld_store = 0;
   int groups = 1;                      // GCONV
   float clip_lo = 0.f, clip_hi = 0.f;  // act == 3 (Clip) of AFFINE / GCONV
   long long rows_per_sample = 0;  // AFFINE / LAYERNORM: rows of C per sample
@@ -84,10 +92,23 @@ struct Plan {
   std::string summary() const;
 };
 
-// Build the plan for batches up to max_batch.  Throws on unsupported graphs.  side_branches: mark
-// independent convs to run on a second stream (PlanOp::join; extends their inputs' lifetimes).
-// split: fp32 mode (Plan::split).
+// Build the plan for batches up to max_batch.  Throws on unsupported graphs, listing EVERY node
+// the engine cannot lower (not only the first).  side_branches: mark independent convs to run on
+// a second stream (PlanOp::join; extends their inputs' lifetimes).  split: fp32 mode (Plan::split).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
                 bool bn_on_load = false);
+
+// Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
+// nodes not tried because an input came from an unsupported node.
+struct PlanReport {
+  bool supported = true;
+  struct Item {
+    std::string node, op, error;
+  };
+  std::vector<Item> unsupported;
+  int blocked = 0;
+  std::string text() const;  // one line per unsupported node
+};
+PlanReport plan_report(const onnx::Model& m, int max_batch = 8, bool split = false);
 
 }  // namespace die

@@ -124,9 +124,35 @@ struct GConvArgs {
 hipError_t grouped_conv(const GConvArgs& a, hipStream_t s);
 
 // Softmax over the last axis of [rows][C] (one wave per row, fp32 math); writes bf16/split `y`
-// and/or f32 `y_f32`.
+// (row pitch ld) and/or f32 `y_f32` (dense [rows][C]).  ld = stored row pitch of x and y (0 = C).
 hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long rows, int C, hipStream_t s,
-                        int split = 0);
+                        int split = 0, int ld = 0);
+
+// ---- generic kernels (generic.hip): the planner's general path ----
+// fp32 [R][F] -> bf16 / split rows [R][Fp] (Fp % 8 == 0, pad columns zero): rank-2/3 graph inputs.
+hipError_t rows_prep(const float* x, uint16_t* y, long long R, int F, int Fp, hipStream_t s, int split = 0);
+// input_prep for any channel count: fp32 NCHW -> affine -> NHWC with Cp % 8 == 0 stored channels.
+hipError_t input_prep_wide(const float* x, const float* scale, const float* shift, uint16_t* out, int B, int C, int H,
+                           int W, int Cp, hipStream_t s, int split = 0);
+// y[r][coly + j] = x[r][colx + j], j < ncols, over R rows (concat / slice along the channel axis).
+// xplane / yplane: lo-plane distances of split tensors (elements).
+hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uint16_t* y, long long yplane, int ldy,
+                     int coly, long long R, int ncols, hipStream_t s, int split = 0);
+// out = act(x op y) over [R][C] rows; ymode 0: y same shape; 1: y one row per sample (broadcast over
+// its rows_per_sample rows).  op 0 add, 1 sub, 2 mul, 3 div.  act codes as unary_rows.
+hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
+                       int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live = nullptr,
+                       int split = 0);
+// y = act(x * scale[c] + shift[c]) (scale/shift nullable); act 0 none, 1 ReLU, 2 GELU (erf),
+// 3 Clip(a, b), 4 sigmoid, 5 tanh, 6 leaky ReLU (slope a).
+hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, long long R, int C,
+                      int act, float a, float b, hipStream_t s, const long long* live = nullptr,
+                      long long rows_per_sample = 0, int split = 0);
+// f32 [R][C] from bf16 / split rows of pitch ld >= C (graph outputs with padded columns).
+hipError_t rows_to_f32(const uint16_t* x, float* y, long long R, int C, int ld, hipStream_t s, int split = 0);
+// f32 NCHW [B][C][H][W] from bf16 NHWC with Cs >= C stored channels.
+hipError_t nhwc_to_nchw_f32_strided(const uint16_t* x, float* y, int B, int H, int W, int C, int Cs, hipStream_t s,
+                                    int split = 0);
 // bf16 NHWC [B,H,W,C] -> f32 NCHW [B,C,H,W]
 hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, int C, hipStream_t s, int split = 0);
 // f32 -> bf16 / bf16 -> f32 copies

@@ -285,12 +285,13 @@ __global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restri
 // Softmax over rows (one wave per row, fp32 max / sum with exp2): classifier heads and any softmax
 // outside the fused attention.
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-                                                           float* __restrict__ yf, long long rows, int C, int split) {
+                                                           float* __restrict__ yf, long long rows, int C, int ld,
+                                                           int split) {
   const int lane = threadIdx.x & 63;
   const long long row = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const long long plane = rows * C;
-  const uint16_t* xr = x + row * C;
+  const long long plane = rows * ld;
+  const uint16_t* xr = x + row * ld;
   const bool sp = split != 0;
   float m = -INFINITY;
   for (int c = lane; c < C; c += 64) m = fmaxf(m, load1v(xr + c, plane, sp));
@@ -302,9 +303,11 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(const uint16_t* __res
   const float inv = 1.f / wave_sum(s);
   for (int c = lane; c < C; c += 64) {
     const float p = exp2f((load1v(xr + c, plane, sp) - m) * kLog2e) * inv;
-    if (y) store1v(y + row * C + c, plane, sp, p);
+    if (y) store1v(y + row * ld + c, plane, sp, p);
     if (yf) yf[row * C + c] = p;
   }
+  if (y)  // pad columns of a padded row stay finite (consumers give them zero weight)
+    for (int c = C + lane; c < ld; c += 64) store1v(y + row * ld + c, plane, sp, 0.f);
 }
 
 inline int grid_for(long long work, int cap = 4096) {
@@ -342,10 +345,11 @@ hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, in
 }
 
 hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long rows, int C, hipStream_t s,
-                        int split) {
-  if (C <= 0 || rows <= 0 || (!y && !y_f32)) return hipErrorInvalidValue;
+                        int split, int ld) {
+  if (ld <= 0) ld = C;
+  if (C <= 0 || rows <= 0 || ld < C || (!y && !y_f32)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(softmax_rows_kernel, dim3(static_cast<unsigned>((rows + 3) / 4)), dim3(256), 0, s, x, y, y_f32,
-                     rows, C, split);
+                     rows, C, ld, split);
   return hipGetLastError();
 }
 

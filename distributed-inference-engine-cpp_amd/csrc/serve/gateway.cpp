@@ -36,6 +36,7 @@ struct Gateway::Route {
   std::string target;
   std::vector<std::string> order;
   size_t next = 0;
+  std::chrono::steady_clock::time_point t_head, t_body, t_try;
 };
 
 Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) {
@@ -84,6 +85,9 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
         64 << 10);
   }
   server_.route("POST", "/infer", [this](HttpRequest& req, Responder res) {
+    const auto t_body = std::chrono::steady_clock::now();
+    const auto t_head = req.t_headers.time_since_epoch().count() ? req.t_headers : t_body;
+    h_recv_.add(t_body - t_head);
     AsyncHttpClient::BodyRef b;
     long long off = -1;
     if (req.ext_body) {
@@ -93,7 +97,12 @@ Gateway::Gateway(GatewayOptions opt) : opt_(std::move(opt)), ring_(opt_.vnodes) 
       auto body = std::make_shared<const std::string>(std::move(req.body));
       b = AsyncHttpClient::BodyRef{body->data(), body->size(), body};
     }
-    routeRequest(std::move(b), off, [res](HttpResponse&& r) { res.send(std::move(r)); });
+    routeRequest(std::move(b), off, [this, res, t_head, t_body](HttpResponse&& r) {
+      const auto now = std::chrono::steady_clock::now();
+      h_route_.add(now - t_body);
+      h_total_.add(now - t_head);
+      res.send(std::move(r));
+    });
   });
   server_.route("GET", "/stats", [this](HttpRequest&, Responder res) {
     HttpResponse r;
@@ -167,8 +176,10 @@ void Gateway::try_next(std::shared_ptr<Route> r) {
     } else {
       byte_forwards_++;
     }
+    r->t_try = std::chrono::steady_clock::now();
     client_->post(upstream_.at(node), "/infer", std::move(send), "application/json", extra,
                   [this, r, node, via_shm](std::optional<HttpResponse> resp, const std::string& err) {
+                    h_upstream_.add(std::chrono::steady_clock::now() - r->t_try);
                     CircuitBreaker& br = *breakers_.at(node);
                     if (via_shm && resp && resp->header("x-die-error") == "shm") {
                       // this worker cannot map the arena (other host / namespace): send it bytes
@@ -233,6 +244,12 @@ Json Gateway::getStats() const {
   s["in_flight"] = client_->in_flight();
   s["upstream_connections_opened"] = client_->connections_opened();
   s["shm_forwards"] = static_cast<long long>(shm_forwards_.load());
+  Json st = Json::object();
+  st["recv"] = h_recv_.snapshot();
+  st["upstream"] = h_upstream_.snapshot();
+  st["route"] = h_route_.snapshot();
+  st["total"] = h_total_.snapshot();
+  s["stages_us"] = st;
   s["byte_forwards"] = static_cast<long long>(byte_forwards_.load());
   s["shm_arena_mib"] = shm_ ? static_cast<double>(shm_->size()) / (1 << 20) : 0.0;
   s["log_lines"] = static_cast<long long>(log_lines_emitted());

@@ -30,6 +30,7 @@
 #include "../core/json.h"
 #include "../core/shm_arena.h"
 #include "circuit_breaker.h"
+#include "stage_stats.h"
 #include "consistent_hash.h"
 
 namespace die {
@@ -89,6 +90,10 @@ class Gateway {
   std::unique_ptr<AsyncHttpClient> client_;
   HttpServer server_;
   std::atomic<int64_t> routed_{0}, failovers_{0}, failed_{0}, client_errors_{0};
+  // per-stage latency (tail analysis): request head parsed -> body received (recv); forward issued
+  // -> worker answer received, per attempt (upstream); body received -> answer handed to the
+  // reactor (route); head parsed -> answer handed over (total)
+  StageHist h_recv_, h_upstream_, h_route_, h_total_;
 };
 
 }  // namespace die

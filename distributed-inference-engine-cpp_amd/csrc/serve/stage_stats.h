@@ -1,6 +1,7 @@
-// Lock-free latency histograms for the worker's request stages (per-stage
-// histograms on /health, extra keys only).  Buckets are powers of two of nanoseconds / 1024
-// (~1 us resolution at the bottom, > 1 h at the top); percentiles are bucket upper bounds.
+// Lock-free latency histograms for the worker's and gateway's request stages (SURVEY §5.1/§5.5:
+// per-stage histograms on /health and /stats, extra keys only).  Log-linear buckets: 4 per octave
+// of ~microseconds (ns / 1024), i.e. <= 19 % wide above 4 us (tail percentiles to about +-10 %,
+// > 1 h at the top); percentiles report bucket upper bounds.
 #pragma once
 
 #include <atomic>
@@ -13,12 +14,26 @@ namespace die {
 
 class StageHist {
  public:
-  static constexpr int kBuckets = 40;
+  static constexpr int kSub = 4;                  // buckets per octave
+  static constexpr int kBuckets = 4 + 38 * kSub;  // u < 4 exactly, then 4 per octave
+  // bucket of u = ns / 1024: u < 4 -> u; else octave o = floor(log2 u) >= 2 split by the next 2 bits
+  static int bucket(uint64_t u) {
+    if (u < 4) return static_cast<int>(u);
+    const int o = 63 - __builtin_clzll(u);
+    const int sub = static_cast<int>((u >> (o - 2)) & 3);
+    const int b = 4 + (o - 2) * kSub + sub;
+    return b < kBuckets ? b : kBuckets - 1;
+  }
+  // exclusive upper bound of bucket b, in u units
+  static double upper(int b) {
+    if (b < 4) return b + 1.0;
+    const int o = (b - 4) / kSub + 2, sub = (b - 4) % kSub;
+    return static_cast<double>(1ull << o) * (1.0 + (sub + 1) / 4.0);
+  }
   void add(std::chrono::steady_clock::duration d) {
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(d).count();
     const uint64_t u = ns > 0 ? static_cast<uint64_t>(ns) >> 10 : 0;  // ~us
-    const int b = u ? 64 - __builtin_clzll(u) : 0;
-    buckets_[b < kBuckets ? b : kBuckets - 1].fetch_add(1, std::memory_order_relaxed);
+    buckets_[bucket(u)].fetch_add(1, std::memory_order_relaxed);
     count_.fetch_add(1, std::memory_order_relaxed);
     sum_ns_.fetch_add(ns, std::memory_order_relaxed);
   }
@@ -34,12 +49,14 @@ class StageHist {
       uint64_t acc = 0;
       for (int i = 0; i < kBuckets; ++i) {
         acc += c[i];
-        if (acc > target) return static_cast<double>((1ull << i) * 1024) / 1e3;
+        if (acc > target) return upper(i) * 1024.0 / 1e3;
       }
       return 0.0;
     };
     j["p50_us"] = n ? pct(0.5) : 0.0;
+    j["p90_us"] = n ? pct(0.9) : 0.0;
     j["p99_us"] = n ? pct(0.99) : 0.0;
+    j["p999_us"] = n ? pct(0.999) : 0.0;
     return j;
   }
 

@@ -1,0 +1,196 @@
+"""Generated models for the HIP planner's general path ("model-agnostic device execution").
+
+The reference serves whatever single-input ONNX model it is given (input 0 / output 0,
+/root/reference/src/inference_engine.cpp:33-69).  These generators build small models with the op
+mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX writer:
+
+* `mlp`       2-D input [N, F], Gemm (transB) / MatMul layers with Relu / Tanh / Sigmoid / LeakyRelu,
+              hidden and output widths that are NOT multiples of 8, Softmax head;
+* `bert`      2-D input [N, S*D] reshaped to [N, S, D], post-LN encoder layers (attention in the
+              torch export pattern, erf-GELU FFN), mean-pool over tokens, 3-class head;
+* `se_cnn`    an image CNN with 12 input channels (> 8), odd channel counts, a squeeze-excitation
+              gate (GAP -> FC -> ReLU -> FC -> Sigmoid -> broadcast Mul), channel Concat and
+              Slice, and a Flatten of a 4x4 map (NCHW order) into the classifier.
+`synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
+oracle for all of them (tests/test_gpu_general.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Tuple
+
+import numpy as np
+
+from ..utils.onnx_writer import GraphBuilder
+
+SPECS = {
+    "mlp": dict(in_features=300, hidden=(100, 60, 36), classes=10),
+    "bert": dict(seq=32, dim=128, heads=2, ffn=256, layers=2, classes=3),
+    "se_cnn": dict(in_ch=12, image=16, classes=10),
+}
+
+
+def _rng(seed):
+    return np.random.default_rng(seed)
+
+
+def _lin(rng, fan_in, shape):
+    return (rng.standard_normal(shape) / math.sqrt(fan_in)).astype(np.float32)
+
+
+def build_mlp(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["mlp"]
+    rng = _rng(seed)
+    g = GraphBuilder(name="mlp")
+    x = g.input("features", ["N", s["in_features"]])
+    h, fan = x, s["in_features"]
+    acts = ["Relu", "Tanh", "LeakyRelu"]
+    for i, width in enumerate(s["hidden"]):
+        if i % 2 == 0:  # Gemm with transB (torch nn.Linear export)
+            w = g.init("fc%d.weight" % i, _lin(rng, fan, (width, fan)))
+            b = g.init("fc%d.bias" % i, (0.1 * rng.standard_normal(width)).astype(np.float32))
+            h = g.node("Gemm", [h, w, b], name="fc%d" % i, transB=1)
+        else:  # MatMul + Add (the other common export)
+            w = g.init("fc%d.weight" % i, _lin(rng, fan, (fan, width)))
+            b = g.init("fc%d.bias" % i, (0.1 * rng.standard_normal(width)).astype(np.float32))
+            h = g.node("Add", [g.node("MatMul", [h, w], name="fc%d/MatMul" % i), b], name="fc%d/Add" % i)
+        a = acts[i % len(acts)]
+        h = g.node(a, [h], name="act%d" % i, **({"alpha": 0.1} if a == "LeakyRelu" else {}))
+        fan = width
+    # a sigmoid gate on the last hidden layer, then the classifier
+    gate = g.node("Sigmoid", [h], name="gate")
+    h = g.node("Mul", [h, gate], name="gated")
+    w = g.init("head.weight", _lin(rng, fan, (s["classes"], fan)))
+    b = g.init("head.bias", (0.1 * rng.standard_normal(s["classes"])).astype(np.float32))
+    y = g.node("Gemm", [h, w, b], name="head", transB=1)
+    y = g.node("Softmax", [y], name="prob", axis=-1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
+def build_bert(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["bert"]
+    rng = _rng(seed)
+    S, D, H, F = s["seq"], s["dim"], s["heads"], s["ffn"]
+    hd = D // H
+    g = GraphBuilder(name="bert_encoder")
+    x = g.input("embeddings", ["N", S * D])  # token embeddings, flattened (2-D input)
+    h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
+    heads_shape = g.const(np.array([0, 0, H, hd], np.int64), "heads_shape")
+    merge_shape = g.const(np.array([0, 0, D], np.int64), "merge_shape")
+    scale = g.const(np.array(math.sqrt(hd), np.float32), "sqrt_d")
+    sqrt2 = g.const(np.array(1.4142135381698608, np.float32), "sqrt2")
+    one = g.const(np.array(1.0, np.float32), "one")
+    half = g.const(np.array(0.5, np.float32), "half")
+
+    def linear(inp, name, fin, fout):
+        w = g.init(name + ".weight", _lin(rng, fin, (fin, fout)))
+        b = g.init(name + ".bias", (0.02 * rng.standard_normal(fout)).astype(np.float32))
+        return g.node("Add", [g.node("MatMul", [inp, w], name=name + "/MatMul"), b], name=name + "/Add")
+
+    def ln(inp, name):
+        gw = g.init(name + ".weight", (1.0 + 0.1 * rng.standard_normal(D)).astype(np.float32))
+        gb = g.init(name + ".bias", (0.1 * rng.standard_normal(D)).astype(np.float32))
+        return g.node("LayerNormalization", [inp, gw, gb], name=name, axis=-1, epsilon=1e-12)
+
+    for i in range(s["layers"]):
+        p = "layer%d." % i
+        q = linear(h, p + "query", D, D)
+        k = linear(h, p + "key", D, D)
+        v = linear(h, p + "value", D, D)
+        q = g.node("Transpose", [g.node("Reshape", [q, heads_shape], name=p + "q_heads")], name=p + "q_perm",
+                   perm=[0, 2, 1, 3])
+        k = g.node("Transpose", [g.node("Reshape", [k, heads_shape], name=p + "k_heads")], name=p + "k_perm",
+                   perm=[0, 2, 3, 1])
+        v = g.node("Transpose", [g.node("Reshape", [v, heads_shape], name=p + "v_heads")], name=p + "v_perm",
+                   perm=[0, 2, 1, 3])
+        sc = g.node("Div", [g.node("MatMul", [q, k], name=p + "scores"), scale], name=p + "scale")
+        sc = g.node("Softmax", [sc], name=p + "softmax", axis=-1)
+        c = g.node("MatMul", [sc, v], name=p + "context")
+        c = g.node("Reshape", [g.node("Transpose", [c], name=p + "ctx_perm", perm=[0, 2, 1, 3]), merge_shape],
+                   name=p + "ctx_merge")
+        o = linear(c, p + "attn_out", D, D)
+        h = ln(g.node("Add", [o, h], name=p + "residual1"), p + "ln1")  # post-LN (BERT)
+        m = linear(h, p + "intermediate", D, F)
+        t = g.node("Div", [m, sqrt2], name=p + "gelu/div")
+        t = g.node("Add", [g.node("Erf", [t], name=p + "gelu/erf"), one], name=p + "gelu/add")
+        t = g.node("Mul", [g.node("Mul", [m, t], name=p + "gelu/mul"), half], name=p + "gelu/half")
+        o = linear(t, p + "output", F, D)
+        h = ln(g.node("Add", [o, h], name=p + "residual2"), p + "ln2")
+    pooled = g.node("ReduceMean", [h], name="mean_pool", axes=[1], keepdims=0)
+    w = g.init("classifier.weight", _lin(rng, D, (s["classes"], D)))
+    b = g.init("classifier.bias", (0.1 * rng.standard_normal(s["classes"])).astype(np.float32))
+    y = g.node("Gemm", [pooled, w, b], name="classifier", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
+def build_se_cnn(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["se_cnn"]
+    rng = _rng(seed)
+    g = GraphBuilder(name="se_cnn")
+    x = g.input("image", ["N", s["in_ch"], s["image"], s["image"]])
+
+    def conv(inp, name, cin, cout, k, stride=1, pad=None, bias=True):
+        pad = k // 2 if pad is None else pad
+        w = g.init(name + ".weight", _lin(rng, cin * k * k, (cout, cin, k, k)))
+        ins = [inp, w]
+        if bias:
+            ins.append(g.init(name + ".bias", (0.1 * rng.standard_normal(cout)).astype(np.float32)))
+        return g.node("Conv", ins, name=name, kernel_shape=[k, k], strides=[stride, stride], pads=[pad] * 4)
+
+    def bn(inp, name, c):
+        ps = [g.init(name + "." + k, v) for k, v in (
+            ("gamma", (1 + 0.1 * rng.standard_normal(c)).astype(np.float32)),
+            ("beta", (0.1 * rng.standard_normal(c)).astype(np.float32)),
+            ("mean", (0.1 * rng.standard_normal(c)).astype(np.float32)),
+            ("var", (0.5 + rng.random(c)).astype(np.float32)))]
+        return g.node("BatchNormalization", [inp] + ps, name=name, epsilon=1e-5)
+
+    h = g.node("Relu", [bn(conv(x, "conv1", s["in_ch"], 20, 3, bias=False), "bn1", 20)], name="relu1")  # 20 % 8 != 0
+    h = g.node("Relu", [conv(h, "conv2", 20, 24, 3, stride=2)], name="relu2")  # 8x8
+    # squeeze-excitation: GAP -> FC(24->6) -> ReLU -> FC(6->24) -> Sigmoid -> broadcast Mul
+    z = g.node("Flatten", [g.node("GlobalAveragePool", [h], name="se_gap")], name="se_flat", axis=1)
+    z = g.node("Relu", [g.node("Gemm", [z, g.init("se1.weight", _lin(rng, 24, (6, 24))),
+                                         g.init("se1.bias", np.zeros(6, np.float32))], name="se1", transB=1)],
+               name="se_relu")
+    z = g.node("Sigmoid", [g.node("Gemm", [z, g.init("se2.weight", _lin(rng, 6, (24, 6))),
+                                            g.init("se2.bias", np.zeros(24, np.float32))], name="se2", transB=1)],
+               name="se_sigmoid")
+    z = g.node("Reshape", [z, g.const(np.array([-1, 24, 1, 1], np.int64), "se_shape")], name="se_gate")
+    h = g.node("Mul", [h, z], name="se_scale")
+    # two branches joined on the channel axis, then a channel slice
+    b1 = g.node("Relu", [conv(h, "branch1", 24, 16, 1)], name="b1_relu")
+    b2 = g.node("Tanh", [conv(h, "branch2", 24, 12, 3)], name="b2_tanh")  # last input: 12 % 8 != 0
+    h = g.node("Concat", [b1, b2], name="concat", axis=1)  # 28 channels
+    h = g.node("Slice", [h, g.const(np.array([8], np.int64), "sl_start"), g.const(np.array([28], np.int64), "sl_end"),
+                         g.const(np.array([1], np.int64), "sl_axes")], name="slice")  # 20 channels
+    h = g.node("MaxPool", [h], name="pool", kernel_shape=[2, 2], strides=[2, 2])  # 4x4
+    h = g.node("Flatten", [h], name="flatten", axis=1)  # NCHW order over a 4x4 map
+    w = g.init("fc.weight", _lin(rng, 20 * 16, (s["classes"], 20 * 16)))
+    y = g.node("Gemm", [h, w, g.init("fc.bias", (0.1 * rng.standard_normal(s["classes"])).astype(np.float32))],
+               name="fc", transB=1)
+    y = g.node("Softmax", [y], name="prob", axis=-1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
+BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn}
+
+
+def build_onnx(name: str, seed: int = 0) -> bytes:
+    return BUILDERS[name](seed)[0]
+
+
+def input_shape(name: str):
+    s = SPECS[name]
+    if name == "mlp":
+        return (s["in_features"],)
+    if name == "bert":
+        return (s["seq"] * s["dim"],)
+    return (s["in_ch"], s["image"], s["image"])
+
+
+def synthetic_input(name: str, batch: int, seed: int = 1) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((batch,) + input_shape(name)).astype(np.float32)

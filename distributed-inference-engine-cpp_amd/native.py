@@ -665,6 +665,20 @@ def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = Fal
     return json.loads(_take_str(p))
 
 
+def plan_report(model_path: str, precision: str = "fp32") -> Dict[str, Any]:
+    """Which nodes the HIP planner cannot lower (and why): {"supported", "unsupported": [{node, op,
+    error}], "blocked", "text"}.  Runs on the CPU (no GPU needed)."""
+    L = lib()
+    fn = L.die_plan_report
+    fn.restype = C.c_void_p
+    fn.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+    err = _err_box()
+    p = fn(model_path.encode(), int(precision == "fp32"), C.byref(err))
+    if not p:
+        _raise_if(err, "plan_report")
+    return json.loads(_take_str(p))
+
+
 def kernels():
     """The raw kernel-launch entry points (see ops/kernels.py for the torch-facing wrappers)."""
     return _sig_kernels()

@@ -1,0 +1,75 @@
+"""HIP engine on the general-path models vs the fp32 CPU executor (VERDICT r2 "done" bar: a generated
+MLP and a BERT-style encoder with a 2-D input run on --device hip and match the CPU executor at
+rel-L2 <= 1e-4).  Exercises the generic kernels (kernels/generic.hip: rows_prep, copy_cols,
+binary_rows, unary_rows, rows_to_f32, input_prep_wide) and padded channel counts through conv,
+GEMM, softmax and the output casts, at several batch sizes (bucket padding) in fp32 and bf16."""
+import json
+import urllib.request
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+GENERIC = ["mlp", "bert", "se_cnn"]
+
+
+@pytest.fixture(scope="module")
+def gen_models(native, tmp_path_factory):
+    from die_amd.models import generic as G
+
+    d = tmp_path_factory.mktemp("generic_gpu")
+    out = {}
+    for name in GENERIC:
+        p = str(d / (name + ".onnx"))
+        open(p, "wb").write(G.build_onnx(name))
+        out[name] = p
+    return out
+
+
+def _rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.mark.parametrize("name", GENERIC)
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
+def test_generic_model_matches_cpu_executor(native, gen_models, name, precision, tol):
+    from die_amd.models import generic as G
+
+    path = gen_models[name]
+    eng = native.Engine(path, device="hip", max_batch=8, precision=precision, autotune=False)
+    assert eng.refresh_info()["name"].startswith("hip:gfx950")
+    try:
+        for B in (1, 5, 8):
+            x = G.synthetic_input(name, B, seed=B)
+            ref = native.cpu_run(path, x).reshape(B, -1)
+            got = eng.run(x.reshape(B, -1))
+            assert got.shape == ref.shape and np.isfinite(got).all()
+            err = _rel_l2(got, ref)
+            assert err <= tol, (name, precision, B, err)
+            if precision == "fp32":
+                assert (got.argmax(1) == ref.argmax(1)).all()
+    finally:
+        eng.close()
+
+
+def test_generic_mlp_served_over_http(native, gen_models):
+    """A 2-D-input model behind the worker: input_data is the feature vector (300 floats), the
+    device decodes the JSON text and the answer equals the CPU executor's."""
+    from die_amd.models import generic as G
+
+    path = gen_models["mlp"]
+    wk = native.Worker(path, node_id="mlp", max_batch=8, engine={"device": "hip", "autotune": False})
+    try:
+        x = G.synthetic_input("mlp", 3, seed=7)
+        ref = native.cpu_run(path, x)
+        for i in range(3):
+            body = json.dumps({"request_id": "m%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            out = json.loads(urllib.request.urlopen(urllib.request.Request(wk.url + "/infer", data=body),
+                                                    timeout=60).read())
+            assert _rel_l2(np.array(out["output_data"], np.float32), ref[i]) <= 1e-4
+        assert wk.health()["engine"]["device"].startswith("hip")
+    finally:
+        wk.stop()

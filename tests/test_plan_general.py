@@ -1,0 +1,85 @@
+"""The HIP planner's general path, checked on the CPU (no GPU): rank-2/3 inputs, channel counts that
+are not a multiple of 8, broadcast gates, concat / slice, NCHW flatten into a classifier, a
+BERT-style encoder, and the load-time report that lists EVERY node the engine cannot lower
+(VERDICT r2 "model-agnostic device execution"; reference: any single-input ONNX model,
+/root/reference/src/inference_engine.cpp:33-69).  Numerics: tests/test_gpu_general.py."""
+import os
+
+import numpy as np
+import pytest
+
+GENERIC = ["mlp", "bert", "se_cnn"]
+
+
+@pytest.fixture(scope="module")
+def gen_models(native, tmp_path_factory):
+    from die_amd.models import generic as G
+
+    d = tmp_path_factory.mktemp("generic")
+    out = {}
+    for name in GENERIC:
+        p = str(d / (name + ".onnx"))
+        open(p, "wb").write(G.build_onnx(name))
+        out[name] = p
+    return out
+
+
+@pytest.mark.parametrize("name", GENERIC)
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_generic_models_plan_for_the_device(native, gen_models, name, precision):
+    r = native.plan_report(gen_models[name], precision)
+    assert r["supported"], r["text"]
+    s = native.plan_summary(gen_models[name], 8, precision=precision)
+    kinds = [o["kind"] for o in s["ops"]]
+    assert "conv" in kinds  # the GEMMs run on the MFMA kernel
+    if name == "mlp":
+        assert kinds[0] == "rows_prep" and "binary" in kinds and "unary" in kinds and kinds[-1] == "softmax"
+    if name == "bert":
+        assert kinds[0] == "rows_prep" and kinds.count("attention") == 2 and "gap" in kinds
+        assert kinds[-1] == "bf16_to_f32"  # 3 classes stored as 8 columns: the cast drops the pads
+    if name == "se_cnn":
+        assert kinds[0] == "input_prep" and "binary" in kinds and kinds.count("copy_cols") == 3
+
+
+def test_generic_models_run_on_the_cpu_oracle(native, gen_models):
+    from die_amd.models import generic as G
+
+    for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10))):
+        y = native.cpu_run(gen_models[name], G.synthetic_input(name, 2))
+        assert y.shape == shape and np.isfinite(y).all()
+        if name != "bert":
+            np.testing.assert_allclose(y.sum(1), 1.0, rtol=1e-5)  # softmax heads
+
+
+def _unsupported_model(path):
+    """Image model with two ops the planner does not lower (Abs, Exp; the CPU executor runs them) in
+    separate branches, and nodes that depend on them."""
+    from die_amd.utils.onnx_writer import GraphBuilder
+
+    rng = np.random.default_rng(0)
+    g = GraphBuilder(name="odd")
+    x = g.input("x", ["N", 3, 8, 8])
+    w = g.init("w", (0.1 * rng.standard_normal((16, 3, 3, 3))).astype(np.float32))
+    h = g.node("Conv", [x, w], name="conv", kernel_shape=[3, 3], pads=[1, 1, 1, 1])
+    a = g.node("Abs", [h], name="abs")
+    b = g.node("Exp", [h], name="exp")
+    s = g.node("Add", [a, b], name="join")
+    g.output(g.node("Relu", [s], name="relu"), ["N", 16, 8, 8])
+    open(path, "wb").write(g.model_proto(opset=13))
+
+
+def test_report_lists_every_unsupported_node(native, tmp_path):
+    p = str(tmp_path / "odd.onnx")
+    _unsupported_model(p)
+    r = native.plan_report(p)
+    assert not r["supported"]
+    ops = sorted(i["op"] for i in r["unsupported"])
+    assert ops == ["Abs", "Exp"], r
+    assert r["blocked"] == 2  # join + relu depend on them
+    assert "Abs 'abs'" in r["text"] and "Exp 'exp'" in r["text"]
+    # an engine on "auto" keeps the reference's EP-style fallback and runs it on the CPU executor
+    eng = native.Engine(p, device="auto", max_batch=2)
+    assert eng.refresh_info()["name"] == "cpu"
+    x = np.random.default_rng(1).standard_normal((2, 3 * 8 * 8)).astype(np.float32)
+    np.testing.assert_allclose(eng.run(x), native.cpu_run(p, x.reshape(2, 3, 8, 8)).reshape(2, -1), rtol=1e-6)
+    eng.close()
