@@ -171,7 +171,10 @@ def main():
             # every rank's gateway routes over every rank's worker (ring on request_id)
             ports = hg.all_gather_object(wk.port)
             gw = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
-                                      local_shm=not args.no_local_shm, http_threads=args.gw_http_threads)
+                                      local_shm=not args.no_local_shm, http_threads=args.gw_http_threads,
+                                      # a CPU-executor batch can outlast the reference's 5 s read timeout
+                                      # on a loaded host; the HIP path keeps the reference value
+                                      read_timeout_ms=5000 if hip else 120000)
             target_port = gw.port
         # every pass and rank gets its own payload seed: no input recurs across the warm-up, timed and
         # direct passes (cache_hits_timed below proves it)
