@@ -13,6 +13,8 @@
 #   ops ARCH B PREC               per-op device time table (tools/op_profile.py)
 #   rocprof NAME [bench.py args]  rocprofv3 --kernel-trace --stats around bench.py, summary via tools/prof_summary.py
 #   pmc ARCH B PREC               4 PMC passes of one forward (tools/pmc_forward.py) -> pmc_<arch>_<prec>_b<B>.md
+#   micro NAME                    a prebuilt tools/micro/NAME probe -> micro_NAME.md
+#   refbench [ref_bench.py args]  the reference's benchmark.py run: gateway + 3 HIP workers on GPU 0 -> refbench.json
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -89,6 +91,13 @@ case "$TASK" in
     python3 tools/pmc_summary.py "$D" --title "$A $P B=$B tuned" --note "production (autotuned) kernel configs, eager launches" \
       > "$O/pmc_${A}_${P}_b$B.md" || exit 1
     tail -1 "$O/pmc_${A}_${P}_b$B.md" ;;
+  micro)  # a prebuilt tools/micro/<name> binary (built here: hipcc ... -o tools/micro/<name>)
+    timeout -k 10 300 "tools/micro/$1" > "$O/micro_$1.md" 2>&1 || { tail -20 "$O/micro_$1.md"; exit 1; }
+    cat "$O/micro_$1.md" ;;
+  refbench)
+    timeout -k 10 900 python3 -u tools/ref_bench.py --out "$O/refbench.json" --log-dir "$O/refbench_logs" "$@" \
+      > "$O/refbench.log" 2>&1 || { tail -20 "$O/refbench.log"; exit 1; }
+    tail -1 "$O/refbench.log" ;;
   *)
     echo "unknown task $TASK"; exit 2 ;;
 esac
