@@ -15,12 +15,18 @@
 namespace die {
 
 // HIP runtime environment of a serving process; call first thing in main(), before any HIP call
-// (the runtime reads it once, at initialisation).  GPU_MAX_HW_QUEUES = 8: HIP shares hardware
-// queues between streams beyond that limit (default 4), and the engine's 3-4 streams plus an RCCL
-// communicator's internal ones then serialise copies behind kernels (data-parallel ranks lost
-// 13-15 % of throughput at 4; profiles/r3_rccl_hw_queues.md).  Explicit settings win.
+// (the runtime reads it once, at initialisation).  GPU_MAX_HW_QUEUES >= 8: HIP shares hardware
+// queues between streams beyond that limit (default 4, also what the GPU boxes export), and the
+// engine's 3-4 streams plus an RCCL communicator's internal ones then serialise copies behind
+// kernels (data-parallel ranks lost 13-23 % of throughput at 4; profiles/r3_rccl_hw_queues.md).
+// Values below 8 are raised; DIE_HIP_HW_QUEUES sets it explicitly (same rule as die_amd/__init__.py).
 inline void configure_hip_runtime_env() {
-  setenv("GPU_MAX_HW_QUEUES", "8", 0);
+  if (const char* want = std::getenv("DIE_HIP_HW_QUEUES"); want && *want) {
+    setenv("GPU_MAX_HW_QUEUES", want, 1);
+  } else {
+    const char* cur = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!cur || std::atoi(cur) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+  }
   setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
 }
 

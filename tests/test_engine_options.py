@@ -30,3 +30,17 @@ def test_unknown_precision_is_rejected(native, models):
     path, _, _ = models["tiny"]
     with pytest.raises(Exception, match="precision"):
         native.Engine(path, device="cpu", precision="fp8")
+
+
+def test_hip_hw_queue_env_rule():
+    """GPU_MAX_HW_QUEUES below 8 (HIP's / the boxes' default 4) is raised to 8; DIE_HIP_HW_QUEUES
+    sets it explicitly; larger explicit values stay (profiles/r3_rccl_hw_queues.md)."""
+    import die_amd
+
+    for given, want in (({}, "8"), ({"GPU_MAX_HW_QUEUES": "4"}, "8"), ({"GPU_MAX_HW_QUEUES": "16"}, "16"),
+                        ({"GPU_MAX_HW_QUEUES": "4", "DIE_HIP_HW_QUEUES": "4"}, "4"),
+                        ({"DIE_HIP_HW_QUEUES": "6"}, "6"), ({"GPU_MAX_HW_QUEUES": "junk"}, "8")):
+        env = dict(given)
+        die_amd.configure_hip_env(env)
+        assert env["GPU_MAX_HW_QUEUES"] == want, (given, env)
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"

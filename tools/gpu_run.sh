@@ -65,7 +65,7 @@ case "$TASK" in
       done
     done ;;
   ops)
-    timeout -k 10 300 python3 -u tools/op_profile.py --arch "$1" --batch "$2" --precision "$3" --out "$O/ops_$1_$3_b$2.md" \
+    timeout -k 10 300 python3 -u tools/op_profile.py --arch "$1" --batch "$2" --precision "$3" --out "$O/ops_$1_$3_b$2" \
       > "$O/ops.log" 2>&1 || { tail -20 "$O/ops.log"; exit 1; }
     sed -n 3p "$O/ops_$1_$3_b$2.md" ;;
   rocprof)
