@@ -152,7 +152,8 @@ def main():
         r = dict(name=name, count=count, M=B * Ho * Ho, N=cout, K=cin * k * k, us=best[0], cfg=best[1],
                  splits=best[2], fused=best[3], tflops=pr.flops / best[0] / 1e6, ref=ref,
                  best_per_variant={str(v): dict(us=t[0], cfg=t[1], splits=t[2], fused=t[3])
-                                   for v, t in sorted(by_variant.items())})
+                                   for v, t in sorted(by_variant.items())},
+                 top=[dict(us=round(t[0], 2), cfg=t[1], splits=t[2], fused=t[3]) for t in cands[:16]])
         results.append(r)
         print("%-14s x%d M=%-6d N=%-5d K=%-5d best %7.2f us (cfg %2d split %2d%s) %5.0f TF | per variant: %s" % (
             name, count, r["M"], cout, r["K"], best[0], best[1], best[2], "f" if best[3] else "", r["tflops"],
