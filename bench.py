@@ -203,7 +203,7 @@ def main():
             "mean_ms": res["latency_ms"]["mean"], "failed": failed,
             "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
-            "device_ms_per_batch": e1.get("avg_device_ms"), "engine": e1.get("device"),
+            "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
             "precision": e1.get("precision"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
             "parse_us_avg": h1.get("parse_us_avg"), "host_cpus": len(os.sched_getaffinity(0)),
@@ -211,8 +211,12 @@ def main():
             "decode_fallbacks": h1.get("decode_fallbacks"),
             "pipeline_depth": args.pipeline_depth, "exec_streams": e1.get("executors"),
             "worker_init_s": round(t_ready - t_init, 2),
-            "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"), "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"),
-            "prep_ms_per_batch": e1.get("avg_prep_ms"), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
+            # engine averages over the timed window only (the engine keeps lifetime totals, which
+            # include warm-up and autotune-time batches)
+            "copy_wait_ms_per_batch": _win(e0, e1, "avg_copy_wait_ms"),
+            "gpu_gap_ms_per_batch": _win(e0, e1, "avg_gpu_gap_ms"),
+            "prep_ms_per_batch": _win(e0, e1, "avg_prep_ms"),
+            "device_busy_frac": _busy(e0, e1, elapsed), "pace": e1.get("pace"), "pack_text": e1.get("pack_text"),
             "pace_lead_ms": e1.get("avg_pace_lead_ms"), "submit_us_avg": e1.get("staging_diag", {}).get("submit_us_avg"),
             "pace_input_ms": e1.get("pace_input_ms"), "pace_margin_ms": e1.get("pace_margin_ms"),
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
@@ -357,6 +361,22 @@ def main():
         out.update({k: v for k, v in extra.items() if v is not None})
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     hg.close()
+
+
+def _win(e0, e1, key):
+    """Per-batch average of an engine statistic over the timed window: the engine reports lifetime
+    averages (total / batches), so window = (avg1*n1 - avg0*n0) / (n1 - n0)."""
+    n0, n1 = e0.get("batches", 0), e1.get("batches", 0)
+    if key not in e1 or n1 <= n0:
+        return e1.get(key)
+    return (e1[key] * n1 - e0.get(key, 0.0) * n0) / (n1 - n0)
+
+
+def _busy(e0, e1, elapsed_s):
+    """Fraction of the timed window the GPU spent in forward passes (MAIN graphs)."""
+    if "device_busy_ms" not in e1 or elapsed_s <= 0:
+        return None
+    return round((e1["device_busy_ms"] - e0.get("device_busy_ms", 0.0)) / (elapsed_s * 1000.0), 4)
 
 
 def _dp_child(args, hg, rank, world):
