@@ -114,9 +114,11 @@ __global__ void gather_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __r
 
 // ---- fused attention ------------------------------------------------------------------------------
 // FlashAttention-style, on v_mfma_f32_32x32x16_bf16, for head dim 64 and S <= 256 (ViT: 197 tokens).
-// A block = (image b, head h, 4 query tiles of 32); each wave owns one 32-query tile.  K and V of the
-// (b, h) pair are staged in LDS once per block (K with XOR-swizzled 16-B chunks, V in plain rows
-// padded to 96 elements so the transposed reads below are bank-conflict free).
+// A block = one (image b, head h) pair, 8 waves (two per SIMD); wave w owns query tile w (32 queries).
+// K and V of the pair are staged in LDS once (K with XOR-swizzled 16-B chunks, V in plain rows padded
+// to 96 elements so the transposed reads below are bank-conflict free); every thread issues all of
+// its staging loads before its first LDS write, so the whole K/V image is in flight at once (round 2
+// staged it in dependent load->store rounds from two blocks per pair: 52 us per ViT layer at B=32).
 //  * S^T = K Q^T (A = K rows from LDS, B = this wave's Q fragments kept in registers): the result has
 //    the QUERY on the lane and 32 KEYS in the 16 accumulator registers x 2 lane halves, so the
 //    softmax over keys is in-lane plus one xor-32 shuffle (online softmax across key tiles, exp2).
@@ -140,32 +142,46 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const uint16_t* p) {
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) { return make_uint2(pack2(a, b), pack2(c, d)); }
 
 template <int NKT, bool SPLIT = false>
-__global__ __launch_bounds__(256) void attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+__global__ __launch_bounds__(512) void attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                                                         const uint16_t* __restrict__ v, uint16_t* __restrict__ out,
                                                         int S, int ldq, int ldk, int ldv, int ldo, float scale_log2) {
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int SK = NKT * 32;
+  constexpr int NT = 512;
+  constexpr int PER = (SK * 8 + NT - 1) / NT;  // 16-B chunks per thread per (tensor, plane)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[NP][SK * AT_D];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[NP][SK * VP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.y, b = blockIdx.z;
   const long long rowbase = static_cast<long long>(b) * S;
   const long long rows = static_cast<long long>(gridDim.z) * S;  // plane distances: rows x pitch
-  for (int i = tid; i < SK * 8; i += 256) {
-    const int s = i >> 3, c = i & 7;
+  {
+    uint4 kq[NP][PER], vq[NP][PER];
 #pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      uint4 kq = make_uint4(0, 0, 0, 0), vq = make_uint4(0, 0, 0, 0);
-      if (s < S) {
-        kq = *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * AT_D + c * 8);
-        vq = *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * AT_D + c * 8);
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * NT, s = i >> 3, c = i & 7;
+      const bool ok = i < SK * 8 && s < S;
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        kq[pl][j] = ok ? *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * AT_D + c * 8)
+                       : make_uint4(0, 0, 0, 0);
+        vq[pl][j] = ok ? *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * AT_D + c * 8)
+                       : make_uint4(0, 0, 0, 0);
       }
-      *reinterpret_cast<uint4*>(Ks[pl] + s * AT_D + ((c ^ ((s >> 1) & 7)) << 3)) = kq;
-      *reinterpret_cast<uint4*>(Vs[pl] + s * VP + c * 8) = vq;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * NT, s = i >> 3, c = i & 7;
+      if (i >= SK * 8) continue;
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        *reinterpret_cast<uint4*>(Ks[pl] + s * AT_D + ((c ^ ((s >> 1) & 7)) << 3)) = kq[pl][j];
+        *reinterpret_cast<uint4*>(Vs[pl] + s * VP + c * 8) = vq[pl][j];
+      }
     }
   }
   __syncthreads();
-  const int q0 = (blockIdx.x * 4 + wave) * 32;
+  const int q0 = wave * 32;
   if (q0 >= S) return;  // whole wave (EXEC stays full for the transposed reads)
   const int r = lane & 31, hh = lane >> 5;
   bf16x8 qf[NP][4];
@@ -356,20 +372,19 @@ hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long 
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
   if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
-  const int qtiles = (S + 31) / 32;
-  dim3 grid((qtiles + 3) / 4, H, B);
+  dim3 grid(1, H, B);  // one 8-wave block per (image, head): wave w = query tile w (S <= 256)
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
   if (split) {
-    if (S <= 64) hipLaunchKernelGGL((attention_kernel<2, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else if (S <= 128) hipLaunchKernelGGL((attention_kernel<4, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else if (S <= 224) hipLaunchKernelGGL((attention_kernel<7, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    if (S <= 64) hipLaunchKernelGGL((attention_kernel<2, true>), grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (S <= 128) hipLaunchKernelGGL((attention_kernel<4, true>), grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (S <= 224) hipLaunchKernelGGL((attention_kernel<7, true>), grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if (S <= 64) hipLaunchKernelGGL(attention_kernel<2>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<7>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-  else hipLaunchKernelGGL(attention_kernel<8>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  if (S <= 64) hipLaunchKernelGGL(attention_kernel<2>, grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else if (S <= 128) hipLaunchKernelGGL(attention_kernel<4>, grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else if (S <= 224) hipLaunchKernelGGL(attention_kernel<7>, grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+  else hipLaunchKernelGGL(attention_kernel<8>, grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
   return hipGetLastError();
 }
 
