@@ -34,11 +34,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   const int nch = C / 8;
   const uint16_t* xr = x + row * C;
   float v[CPL][8];
+  float4 gv[CPL][2], bv[CPL][2];  // gamma / beta fetched with the row, off the reduction's critical path
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
+      gv[i][0] = *reinterpret_cast<const float4*>(g + c * 8);
+      gv[i][1] = *reinterpret_cast<const float4*>(g + c * 8 + 4);
+      bv[i][0] = *reinterpret_cast<const float4*>(b + c * 8);
+      bv[i][1] = *reinterpret_cast<const float4*>(b + c * 8 + 4);
       load8v(xr + c * 8, plane, split != 0, v[i]);
 #pragma unroll
       for (int t = 0; t < 8; ++t) s += v[i][t];
@@ -63,9 +68,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c >= nch) continue;
+    const float gg[8] = {gv[i][0].x, gv[i][0].y, gv[i][0].z, gv[i][0].w, gv[i][1].x, gv[i][1].y, gv[i][1].z, gv[i][1].w};
+    const float bb[8] = {bv[i][0].x, bv[i][0].y, bv[i][0].z, bv[i][0].w, bv[i][1].x, bv[i][1].y, bv[i][1].z, bv[i][1].w};
     float o[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o[t] = (v[i][t] - mean) * inv * g[c * 8 + t] + b[c * 8 + t];
+    for (int t = 0; t < 8; ++t) o[t] = (v[i][t] - mean) * inv * gg[t] + bb[t];
     store8v(y + row * C + c * 8, plane, split != 0, o);
   }
 }
