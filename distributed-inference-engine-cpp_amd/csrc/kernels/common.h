@@ -29,6 +29,29 @@ __device__ __forceinline__ void unpack2(uint32_t v, float& a, float& b) {
   b = __uint_as_float(v & 0xFFFF0000u);
 }
 
+// Exact-form GELU, 0.5 v (1 + erf(v / sqrt 2)) = 0.5 v erfc(-v / sqrt 2), with erfc from the
+// Chebyshev fit of Numerical Recipes' erfcc (fractional error < 1.2e-7 for every argument) in place
+// of ocml's erff: 1 rcp + 1 exp2 + 10 FMAs against ~45 instructions with lane-divergent branches.
+// Written without the 1 + erf cancellation, so the negative tail keeps its relative accuracy: max
+// relative error 1.7e-5 over all v (5e-7 for v > -2), max absolute 4e-7 -- below the split-fp32
+// representation error (2^-17 relative).  Replaces erff in the GEMM epilogues (ViT MLP1: 19M GELUs
+// per batch-32 forward).
+__device__ __forceinline__ float gelu_erf(float v) {
+  const float z = fabsf(v) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.f));
+  float p = fmaf(0.17087277f, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float ec = t * __builtin_amdgcn_exp2f((p - z * z) * 1.4426950408889634f);  // erfc(|v| / sqrt 2)
+  return v >= 0.f ? v * fmaf(-0.5f, ec, 1.f) : 0.5f * v * ec;
+}
+
 // ---- fp32 mode: split (hi, lo) bf16 planes -------------------------------------------------------
 // A "split" tensor stores each fp32 value v as hi = bf16(v) in a hi plane and lo = bf16(v - hi) in a
 // lo plane `plane` elements after it (same indexing in both).  hi + lo carries ~16 significant bits

@@ -23,7 +23,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 // Epilogue activation: 1 = ReLU, 2 = exact (erf) GELU, 3 = Clip(lo, hi).
 __device__ __forceinline__ float act_fn(float v, int act, float lo = 0.f, float hi = 0.f) {
   if (act == 3) return fminf(fmaxf(v, lo), hi);
-  return act == 1 ? fmaxf(v, 0.f) : 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  return act == 1 ? fmaxf(v, 0.f) : gelu_erf(v);
 }
 
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }

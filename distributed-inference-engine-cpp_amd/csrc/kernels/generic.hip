@@ -86,7 +86,7 @@ __global__ void copy_cols_kernel(const uint16_t* __restrict__ x, long long xplan
 __device__ __forceinline__ float apply_act(float v, int act, float a, float b) {
   switch (act) {
     case 1: return fmaxf(v, 0.f);
-    case 2: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case 2: return gelu_erf(v);
     case 3: return fminf(fmaxf(v, a), b);
     case 4: return 1.f / (1.f + __expf(-v));
     case 5: return tanhf(v);

@@ -21,15 +21,26 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// One wave per row; each lane holds up to CPL 8-element chunks of the row in registers
-// (two-pass mean/variance in fp32).  C % 8 == 0, C <= 64*8*CPL.
-template <int CPL>
+// Sum over aligned groups of LPR lanes (LPR = 64: the whole wave).
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LPR lanes per row (64 / LPR rows per wave); each lane holds up to CPL 8-element chunks of the row
+// in registers (two-pass mean/variance in fp32).  C % 8 == 0, C <= LPR*8*CPL.  C = 768 (ViT-B) runs
+// as 32 lanes x 3 chunks: every lane busy and two rows' loads in flight per wave (one row per wave
+// with 64 x 2 chunks left half the lanes idle in the second round).
+template <int CPL, int LPR = 64>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         const float* __restrict__ g, const float* __restrict__ b,
                                                         float eps, long long rows, int C, int split) {
-  const int lane = threadIdx.x & 63;
-  const long long row = static_cast<long long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  constexpr int RPB = 256 / LPR;  // rows per block
+  const int lane = threadIdx.x & (LPR - 1);
+  const long long row = static_cast<long long>(blockIdx.x) * RPB + (threadIdx.x / LPR);
+  if (row >= rows) return;  // a whole row group; the shuffles below stay inside it
   const long long plane = rows * C;
   const int nch = C / 8;
   const uint16_t* xr = x + row * C;
@@ -38,7 +49,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+    const int c = lane + LPR * i;
     if (c < nch) {
       gv[i][0] = *reinterpret_cast<const float4*>(g + c * 8);
       gv[i][1] = *reinterpret_cast<const float4*>(g + c * 8 + 4);
@@ -52,21 +63,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
       for (int t = 0; t < 8; ++t) v[i][t] = 0.f;
     }
   }
-  const float mean = wave_sum(s) / C;
+  const float mean = group_sum<LPR>(s) / C;
   float q2 = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i)
-    if (lane + 64 * i < nch) {
+    if (lane + LPR * i < nch) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const float d = v[i][t] - mean;
         q2 += d * d;
       }
     }
-  const float inv = rsqrtf(wave_sum(q2) / C + eps);
+  const float inv = rsqrtf(group_sum<LPR>(q2) / C + eps);
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+    const int c = lane + LPR * i;
     if (c >= nch) continue;
     const float gg[8] = {gv[i][0].x, gv[i][0].y, gv[i][0].z, gv[i][0].w, gv[i][1].x, gv[i][1].y, gv[i][1].z, gv[i][1].w};
     const float bb[8] = {bv[i][0].x, bv[i][0].y, bv[i][0].z, bv[i][0].w, bv[i][1].x, bv[i][1].y, bv[i][1].z, bv[i][1].w};
@@ -345,6 +356,11 @@ hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, co
                           long long rows, int C, hipStream_t s, int split) {
   if (C % 8) return hipErrorInvalidValue;
   const int blocks = static_cast<int>((rows + 3) / 4);
+  if (C > 512 && C <= 32 * 8 * 3) {  // 513..768 (ViT-B: 768): 32 lanes x 3 chunks, 2 rows per wave
+    hipLaunchKernelGGL((layernorm_kernel<3, 32>), dim3(static_cast<int>((rows + 7) / 8)), dim3(256), 0, s, x, y, gamma,
+                       beta, eps, rows, C, split);
+    return hipGetLastError();
+  }
   if (C <= 64 * 8) hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
   else if (C <= 128 * 8) hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
   else if (C <= 256 * 8) hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);

@@ -74,7 +74,8 @@ case "$TASK" in
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$n" -o p -- python3 bench.py --no-dp "$@" > "$O/$n.json" 2> "$O/$n.err" \
       || { tail -20 "$O/$n.err"; exit 1; }
     summ "$O/$n.json" "$n"
-    python3 tools/prof_summary.py "$O/$n" > "$O/$n.md" 2>&1 && head -30 "$O/$n.md" ;;
+    python3 tools/prof_summary.py "$O/$n" > "$O/$n.md" 2>&1 && head -30 "$O/$n.md"
+    rm -rf "${O:?}/$n" ;;
   pmc)
     A=$1; B=$2; P=$3; D=$O/pmc_${A}_${P}_b$B
     cd /tmp && export TMPDIR=/tmp && cd "$R" || exit 1
@@ -90,6 +91,7 @@ case "$TASK" in
       || { tail "$D".p*.log; exit 1; }
     python3 tools/pmc_summary.py "$D" --title "$A $P B=$B tuned" --note "production (autotuned) kernel configs, eager launches" \
       > "$O/pmc_${A}_${P}_b$B.md" || exit 1
+    rm -rf "$D"  # raw traces: tens of MB, past gpurun's 64 MiB copy-back limit
     tail -1 "$O/pmc_${A}_${P}_b$B.md" ;;
   micro)  # a prebuilt tools/micro/<name> binary (built here: hipcc ... -o tools/micro/<name>)
     timeout -k 10 300 "tools/micro/$1" > "$O/micro_$1.md" 2>&1 || { tail -20 "$O/micro_$1.md"; exit 1; }
