@@ -711,7 +711,8 @@ class HipEngine : public Engine {
       for (size_t oi = 0; oi < plan_.ops.size(); ++oi)
         if (plan_.ops[oi].kind == PlanOp::CONV) {
           const Tune& x = tune_.back()[oi];
-          t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits) + (x.fused ? "f" : ""));
+          t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits) + (x.fused ? "f" : "") +
+                      (x.order == 2 ? "m" : x.order == 1 ? "n" : ""));
         }
       j["tile_split_at_max_batch"] = t;
     }
@@ -722,6 +723,7 @@ class HipEngine : public Engine {
     int tile = 0;
     int splits = 1;
     bool fused = false;  // split-K reduced in-kernel by the last split block (else a second kernel)
+    int order = 0;       // ConvArgs::order (0 heuristic, 1 N-fastest, 2 M-fastest)
   };
 
   // ---- autotune persistence (kernel configs cached in a tuning file) ----
@@ -746,7 +748,8 @@ class HipEngine : public Engine {
       for (const auto& kv : arch->as_object()) {
         const auto& a = kv.second.as_array();
         if (a.size() < 4) continue;
-        out[kv.first] = {Tune{static_cast<int>(a[0].as_int()), static_cast<int>(a[1].as_int()), a[2].as_bool()},
+        out[kv.first] = {Tune{static_cast<int>(a[0].as_int()), static_cast<int>(a[1].as_int()), a[2].as_bool(),
+                              a.size() > 4 ? static_cast<int>(a[4].as_int()) : 0},
                          a[3].as_double()};
       }
     } catch (const std::exception&) {
@@ -773,6 +776,7 @@ class HipEngine : public Engine {
         a.push_back(kv.second.first.splits);
         a.push_back(kv.second.first.fused);
         a.push_back(kv.second.second);
+        a.push_back(kv.second.first.order);
         arch[kv.first] = a;
       }
       root[arch_] = arch;
@@ -881,7 +885,7 @@ class HipEngine : public Engine {
         base.live = nullptr;  // tune the whole bucket
         // identical problems (repeated blocks) share one measurement
         char key[256];
-        std::snprintf(key, sizeof(key), "%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
+        std::snprintf(key, sizeof(key), "o%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
         auto memo = tuned_shapes.find(key);
@@ -896,9 +900,14 @@ class HipEngine : public Engine {
         for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
           for (int sp = 1; sp <= 16; sp *= 2) {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
-            for (int fused = 0; fused < (sp > 1 ? 2 : 1); ++fused) {
+            for (int fused = 0; fused < (sp > 1 ? 2 : 1); ++fused)
+            // Tile order stays the heuristic (ConvArgs::order 0): tuning N- vs M-fastest per shape
+            // picked M-fastest for ~30 % of shapes behind a cold L2 but made the in-graph forwards
+            // 1-2 % slower (profiles/r3_gemm_feed.md section 6).
+            for (int order = 0; order <= 0; ++order) {
               kern::ConvArgs a = base;
               a.splits = sp;
+              a.order = order;
               if (!fused) a.counters = nullptr;
               if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;  // warm-up / validity
               float ms = 0;
@@ -922,7 +931,7 @@ class HipEngine : public Engine {
               }
               if (ms < best) {
                 best = ms;
-                bt = Tune{tile, sp, fused != 0};
+                bt = Tune{tile, sp, fused != 0, order};
               }
             }
           }
@@ -1019,6 +1028,7 @@ class HipEngine : public Engine {
           if (!use_live_) a.live = nullptr;
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
+          a.order = t.order;
           a.ws = side ? ws_side_ : wss_[s % n_exec_];
           if (side) a.counters = counters_side_;
           if (!t.fused) a.counters = nullptr;
@@ -1173,6 +1183,7 @@ class HipEngine : public Engine {
         o["tile"] = t.tile;
         o["splits"] = t.splits;
         o["fused_splitk"] = t.fused;
+        o["tile_order"] = t.order;
       }
       total += us[i];
       ops.push_back(o);

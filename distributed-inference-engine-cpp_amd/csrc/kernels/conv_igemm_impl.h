@@ -106,7 +106,7 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   // input 9 times (stage-4 3x3 at batch 16-32: weights 4.7x the input, so M-fastest).
   const long long wts = static_cast<long long>(p.N) * p.K;
   const long long acts = static_cast<long long>(p.B) * p.H * p.W * p.Cin;
-  if (wts <= acts) {
+  if (p.order == 1 || (p.order == 0 && wts <= acts)) {
     tile_m = tile / ntn;
     tile_n = tile - tile_m * ntn;
   } else {
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void conv3x3_spatial_kernel(const ConvArgs p, 
   const int id = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bid >> 3);
   const int tile = id / S, split = id - tile * S;
   int tile_m, tile_n;
-  if (static_cast<long long>(p.N) * p.K <= static_cast<long long>(p.B) * p.H * p.W * p.Cin) {
+  if (p.order == 1 || (p.order == 0 && static_cast<long long>(p.N) * p.K <= static_cast<long long>(p.B) * p.H * p.W * p.Cin)) {
     tile_m = tile / ntn;
     tile_n = tile - tile_m * ntn;
   } else {

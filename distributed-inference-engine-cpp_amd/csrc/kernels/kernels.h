@@ -61,6 +61,10 @@ struct ConvArgs {
   int split = 0;
   long long wplane = 0;
   long long xplane = 0, oplane = 0;
+  // Tile order of the XCD-aware block mapping (autotuned): 0 = heuristic (replicate the smaller
+  // operand on every XCD), 1 = N-fastest (an XCD owns a range of pixel rows, reads all weights),
+  // 2 = M-fastest (an XCD owns a range of output channels, reads all activations).
+  int order = 0;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),

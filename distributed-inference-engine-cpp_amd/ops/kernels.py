@@ -124,9 +124,10 @@ class ConvProblem:
         self.flops = 2.0 * B * Ho * Wo * cout * cin * kh * kw
         self._L = native.kernels()
 
-    def launch(self, tile=-1, splits=1, fused_splitk=True) -> int:
-        """Launch on torch's current stream; returns the hipError code (1 = config not applicable)."""
-        g = dict(self.geom, splits=int(splits))
+    def launch(self, tile=-1, splits=1, fused_splitk=True, order=0) -> int:
+        """Launch on torch's current stream; returns the hipError code (1 = config not applicable).
+        order: XCD tile order (ConvArgs::order: 0 heuristic, 1 N-fastest, 2 M-fastest)."""
+        g = dict(self.geom, splits=int(splits), order=int(order))
         if splits > 1:
             g["ws"] = int(self.ws.data_ptr())
             if fused_splitk:

@@ -86,8 +86,8 @@ def main():
             for sp in (1, 2, 4, 8, 16):
                 if sp > nk or (sp > 1 and cout % 8):
                     continue
-                for fused in ((False, True) if sp > 1 else (False,)):
-                    rc = pr.launch(cfg, sp, fused)
+                for fused, order in [(f, o) for f in ((False, True) if sp > 1 else (False,)) for o in (1, 2)]:
+                    rc = pr.launch(cfg, sp, fused, order)
                     if rc == 1:
                         continue
                     if rc != 0:
@@ -96,7 +96,7 @@ def main():
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g):
                         for _ in range(a.reps):
-                            pr.launch(cfg, sp, fused)
+                            pr.launch(cfg, sp, fused, order)
                     g.replay()
                     torch.cuda.synchronize()
                     ts = []
@@ -109,7 +109,7 @@ def main():
                         e1.synchronize()
                         ts.append(e0.elapsed_time(e1) * 1000.0 / a.reps)
                     del g
-                    cands.append((statistics.median(ts), cfg, sp, fused))
+                    cands.append((statistics.median(ts), cfg, sp, fused, order))
         cands.sort()
         ref = {}
         if a.ref:
@@ -145,7 +145,7 @@ def main():
                 ref["conv2d_error"] = str(ex)[:80]
         best = cands[0]
         by_variant = {}
-        for us, cfg, sp, fused in cands:
+        for us, cfg, sp, fused, order in cands:
             v = cfg // 4
             if v not in by_variant:
                 by_variant[v] = (us, cfg, sp, fused)
@@ -153,7 +153,7 @@ def main():
                  splits=best[2], fused=best[3], tflops=pr.flops / best[0] / 1e6, ref=ref,
                  best_per_variant={str(v): dict(us=t[0], cfg=t[1], splits=t[2], fused=t[3])
                                    for v, t in sorted(by_variant.items())},
-                 top=[dict(us=round(t[0], 2), cfg=t[1], splits=t[2], fused=t[3]) for t in cands[:16]])
+                 top=[dict(us=round(t[0], 2), cfg=t[1], splits=t[2], fused=t[3], order=t[4]) for t in cands[:16]])
         results.append(r)
         print("%-14s x%d M=%-6d N=%-5d K=%-5d best %7.2f us (cfg %2d split %2d%s) %5.0f TF | per variant: %s" % (
             name, count, r["M"], cout, r["K"], best[0], best[1], best[2], "f" if best[3] else "", r["tflops"],
