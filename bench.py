@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--no-numa", action="store_true", help="keep the inherited CPU affinity (no NUMA binding)")
     ap.add_argument("--no-pace", action="store_true",
                     help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
+    ap.add_argument("--tune-warm-input", action="store_true",
+                    help="autotune: run each conv's input producer right before every timing (default: L2 scrub only)")
     ap.add_argument("--pace-lead-scale", type=float, default=1.0,
                     help="pacing lead: 1 = measured input path + adaptive margin; other values = input path x this")
     ap.add_argument("--branch-streams", action="store_true",
@@ -160,7 +162,7 @@ def main():
     engine_opts = {"device": args.device, "device_id": dev, "max_batch": B, "precision": args.precision,
                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
-                   "pace_lead_scale": args.pace_lead_scale,
+                   "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode}
     if args.mode in ("gateway", "http"):

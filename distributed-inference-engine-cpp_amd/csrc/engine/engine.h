@@ -226,6 +226,8 @@ struct EngineOptions {
   int completion_poll_us = 0;     // > 0: sleep-poll each batch's D2H event instead of hipEventSynchronize
   bool bn_on_load = false;        // bf16 plans: next unit's BN+ReLU applied on the 1x1 conv operand load
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
+  bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
+                                  // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;

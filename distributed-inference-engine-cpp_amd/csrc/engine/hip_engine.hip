@@ -883,9 +883,18 @@ class HipEngine : public Engine {
         kern::ConvArgs base = conv_args(op, B, 0);
         base.ws = ws_;
         base.live = nullptr;  // tune the whole bucket
+        // EngineOptions::tune_warm_input: the op that produced this conv's input runs right before
+        // every timed launch (after the L2 scrub), so the candidate reads its input warm from the
+        // producer and its weights cold -- as inside a forward
+        int producer = -1;
+        if (opt_.tune_warm_input)
+          for (int j = static_cast<int>(oi) - 1; j >= 0 && producer < 0; --j) {
+            const PlanOp& q = plan_.ops[static_cast<size_t>(j)];
+            if ((q.out >= 0 && q.out == op.in) || (q.out2 >= 0 && q.out2 == op.in)) producer = j;
+          }
         // identical problems (repeated blocks) share one measurement
         char key[256];
-        std::snprintf(key, sizeof(key), "o%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
+        std::snprintf(key, sizeof(key), "o%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
         auto memo = tuned_shapes.find(key);
@@ -914,6 +923,9 @@ class HipEngine : public Engine {
               if (cold) {
                 for (int r = 0; r < 3; ++r) {
                   HIP_CHECK(kern::l2_scrub(scrub, kScrubBytes, sink, s_compute_));
+                  if (producer >= 0)
+                    encode_forward(B, 0, s_compute_, nullptr, ALL, static_cast<size_t>(producer),
+                                   static_cast<size_t>(producer) + 1);
                   HIP_CHECK(hipEventRecord(e0, s_compute_));
                   HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
                   HIP_CHECK(hipEventRecord(e1, s_compute_));
@@ -957,11 +969,15 @@ class HipEngine : public Engine {
   // PREP = decode-table fetch + device decode + the leading input-prep ops (per-slot buffers only);
   // MAIN = the rest.  submit() runs PREP on the copy stream so it overlaps the previous batch's
   // MAIN on the compute stream.
-  void encode_forward(int B, int s, hipStream_t st, hipEvent_t* op_events = nullptr, Part part = ALL) {
+  // range_begin/range_end (autotune): encode only ops [range_begin, range_end), nothing else.
+  void encode_forward(int B, int s, hipStream_t st, hipEvent_t* op_events = nullptr, Part part = ALL,
+                      size_t range_begin = SIZE_MAX, size_t range_end = 0) {
     auto buf = [&](int id) -> void* { return buf_ptr(id, s); };
     auto prm = [&](size_t off) -> const float* { return prm_ptr(off); };
-    const size_t op_begin = part == MAIN ? n_prep_ops_ : 0;
-    const size_t op_end = part == PREP ? n_prep_ops_ : plan_.ops.size();
+    const bool ranged = range_begin != SIZE_MAX;
+    if (ranged) part = MAIN;
+    const size_t op_begin = ranged ? range_begin : part == MAIN ? n_prep_ops_ : 0;
+    const size_t op_end = ranged ? range_end : part == PREP ? n_prep_ops_ : plan_.ops.size();
     if (part != MAIN) {  // the slot's table (live batch; decode lens/offsets) from host-coherent memory
       const hipError_t ec = kern::copy_i64(slots_[s].h_lens_dev, slots_[s].d_lens, static_cast<int>(table_len()), st);
       if (ec != hipSuccess) throw std::runtime_error("launch of table fetch failed: " + std::string(hipGetErrorString(ec)));
