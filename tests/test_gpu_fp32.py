@@ -122,6 +122,25 @@ def test_split_conv_repeatable_bitwise(native):
                 assert torch.equal(ref.view(torch.int16), pr.out.view(torch.int16)), (cfg, splits)
 
 
+def test_split_conv_tile_order_bitwise(native):
+    """ConvArgs::order only remaps blocks to tiles (XCD placement): N-fastest, M-fastest and the
+    heuristic give bit-identical outputs for every config, with and without split-K."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    x = torch.randn(2, 28, 28, 128, device="cuda")
+    w = torch.randn(256, 128, 3, 3, device="cuda") * 0.05
+    pr = K.ConvProblem(x, w, pad=1, max_splits=4, split=True)
+    for cfg in range(K.NUM_CFGS):
+        for splits in (1, 4):
+            if pr.launch(cfg, splits, True, 0) == 1:
+                continue
+            ref = pr.out.clone()
+            for order in (1, 2):
+                assert pr.launch(cfg, splits, True, order) == 0
+                assert torch.equal(ref.view(torch.int16), pr.out.view(torch.int16)), (cfg, splits, order)
+
+
 def test_split_memory_bound_kernels(native):
     torch = _t()
     from die_amd.ops import kernels as K
