@@ -74,9 +74,16 @@ case "$TASK" in
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$n" -o p -- python3 bench.py --no-dp "$@" > "$O/$n.json" 2> "$O/$n.err" \
       || { tail -20 "$O/$n.err"; exit 1; }
     summ "$O/$n.json" "$n"
-    f=$(find "$O/$n" -name '*kernel_stats.csv' -print -quit)
-    [ -n "$f" ] || { echo "no kernel_stats.csv under $O/$n"; exit 1; }
-    python3 tools/prof_summary.py "${f%_kernel_stats.csv}" > "$O/$n.md" 2>&1 && head -30 "$O/$n.md"
+    # rocprofv3 (ROCm 7.2) writes a rocpd SQLite database by default, CSVs with --output-format csv
+    f=$(find "$O/$n" -name '*_results.db' -print -quit)
+    if [ -n "$f" ]; then
+      python3 tools/rocpd_stats.py "$f" --top 40 --md "$O/$n.md" > /dev/null || exit 1
+    else
+      f=$(find "$O/$n" -name '*kernel_stats.csv' -print -quit)
+      [ -n "$f" ] || { echo "no rocprofv3 output under $O/$n"; exit 1; }
+      python3 tools/prof_summary.py "${f%_kernel_stats.csv}" > "$O/$n.md" || exit 1
+    fi
+    head -30 "$O/$n.md"
     rm -rf "${O:?}/$n" ;;
   pmc)
     A=$1; B=$2; P=$3; D=$O/pmc_${A}_${P}_b$B
