@@ -5,11 +5,14 @@
 // raw text into pinned staging and the GPU converts it (inside the same hipGraph as the forward):
 //   (samples uploaded 4-bit packed are expanded to characters in registers as each kernel loads them)
 //   1. dec_count : per 4 KiB chunk, count ',' separators and note non-blank bytes
-//   2. dec_scan  : per sample, exclusive prefix over the chunk counts -> token index of each chunk;
-//                  token count, "too many values" status, zero-fill of the padded tail
-//   3. dec_parse : a chunk is staged in LDS (+ halo); token starts are found per 16 bytes and
-//                  compacted with a block scan; each lane then converts whole tokens from registers
-//                  and stores them at out[sample][token index]
+//   2. dec_parse : a chunk is staged in LDS (+ halo); its token index is the sum of the earlier
+//                  chunks' counts; token starts are found per 16 bytes and compacted with a block
+//                  scan; each lane then converts whole tokens from registers and stores them at
+//                  out[sample][token index].  The block holding a sample's last chunk writes its
+//                  token count, the "too many values" status and the zero-fill of the padded tail.
+// Both kernels run a fixed grid (hipGraph-capturable) that strides over the LIVE chunks only: the
+// chunk table is sized for the largest accepted body (24 B per value), ~3.5x a typical request, and
+// a grid over the whole table spent most of its blocks on empty chunks.
 // Conversion is bit-identical to the host parser: integers up to 2^24 scaled by an exact power of
 // ten in fp32 (one rounding), otherwise an exact-power double product/quotient checked for the
 // double-rounding hazard.  Anything unusual (exponent overflow, > 19 significant digits, subnormal,
@@ -91,6 +94,17 @@ __device__ __forceinline__ bool nonblank(uint4 q) {
   return any;
 }
 
+// true when none of the 16 bytes is ' ', '\n', '\r' or '\t'
+__device__ __forceinline__ bool nonblank_all(uint4 q) {
+  uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    any |= eq_bytes(w[i], 0x20202020u) | eq_bytes(w[i], 0x0A0A0A0Au) | eq_bytes(w[i], 0x0D0D0D0Du) |
+           eq_bytes(w[i], 0x09090909u);
+  return any == 0;
+}
+
 __device__ __forceinline__ int block_sum(int v, int* red) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -119,72 +133,76 @@ __device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
   return base + x - v;
 }
 
+constexpr int kDecMaxB = 1024;  // samples per launch (LDS chunk-prefix table)
+constexpr int kDecGrid = 2048;  // blocks of the grid-stride kernels (8 per CU)
+
+// Per block: pre[b] = exclusive prefix over samples of their chunk counts (a sample with text has
+// max(1, ceil(len / CHUNK)) chunks -- an empty body still gets one work item; a skipped sample
+// none).  Returns the number of work items.
+__device__ int chunk_prefix(const long long* __restrict__ lens, int B, int* pre, int* red) {
+  int carry = 0;
+  for (int i0 = 0; i0 < B; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    int v = 0;
+    if (i < B) {
+      const long long len = lens[i];
+      v = len < 0 ? 0 : len == 0 ? 1 : static_cast<int>((len + CHUNK - 1) / CHUNK);
+    }
+    int tot;
+    const int ex = block_excl_scan(v, red, tot);
+    if (i < B) pre[i] = carry + ex;
+    carry += tot;
+  }
+  __syncthreads();
+  return carry;
+}
+
+// work item -> sample: the last b with pre[b] <= item (samples without chunks share their
+// successor's prefix and are skipped over)
+__device__ __forceinline__ int item_sample(const int* pre, int B, int item) {
+  int lo = 0, hi = B;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pre[mid] <= item) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
                                                  const unsigned char* __restrict__ packed,
                                                  const long long* __restrict__ poffs,
-                                                 const long long* __restrict__ lens, int* __restrict__ counts,
-                                                 int* __restrict__ blank, int max_chunks) {
+                                                 const long long* __restrict__ lens, int B, int* __restrict__ counts,
+                                                 int* __restrict__ blank, int* __restrict__ status,
+                                                 int* __restrict__ ntok, int max_chunks) {
   __shared__ int red[4];
-  const int b = blockIdx.y, chunk = blockIdx.x;
-  const long long len = lens[b];
-  if (len < 0 || static_cast<long long>(chunk) * CHUNK >= len) {
-    if (threadIdx.x == 0) {
-      counts[b * max_chunks + chunk] = 0;
-      blank[b * max_chunks + chunk] = 1;
-    }
-    return;
-  }
-  const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
-  int c = 0, nb = 0;
-  if (off < len) {
-    const long long po = poffs ? poffs[b] : -1;
-    const uint4 q = load16(text + (offs ? offs[b] : b * cap), po >= 0 ? packed + po : nullptr, off, len);
-    c = popc_commas(q);
-    nb = nonblank(q);
-  }
-  const int tc = block_sum(c, red);
-  const int tn = block_sum(nb, red);
-  if (threadIdx.x == 0) {
-    counts[b * max_chunks + chunk] = tc;
-    blank[b * max_chunks + chunk] = tn == 0;
-  }
-}
-
-__global__ __launch_bounds__(256) void dec_scan(const long long* __restrict__ lens, int* __restrict__ counts,
-                                                const int* __restrict__ blank, int* __restrict__ status,
-                                                int* __restrict__ ntok, float* __restrict__ out, long long numel,
-                                                int max_chunks) {
-  __shared__ int red[4];
-  const int b = blockIdx.x;
-  const long long len = lens[b];
-  if (len < 0) {
-    if (threadIdx.x == 0) {
+  __shared__ int pre[kDecMaxB];
+  if (blockIdx.x == 0) {  // per-sample results start clean; dec_parse ORs its bits in
+    for (int b = threadIdx.x; b < B; b += 256) {
       status[b] = 0;
-      ntok[b] = -1;
+      if (lens[b] < 0) ntok[b] = -1;
     }
-    return;
   }
-  const int nch = static_cast<int>((len + CHUNK - 1) / CHUNK);
-  int carry = 0, anynb = 0;
-  for (int c0 = 0; c0 < nch; c0 += 256) {
-    const int c = c0 + threadIdx.x;
-    const int v = c < nch ? counts[b * max_chunks + c] : 0;
-    anynb |= c < nch && !blank[b * max_chunks + c];
-    int tot;
-    const int ex = block_excl_scan(v, red, tot);
-    if (c < nch) counts[b * max_chunks + c] = carry + ex;  // in place: exclusive prefix
-    carry += tot;
+  const int items = chunk_prefix(lens, B, pre, red);
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int b = item_sample(pre, B, it), chunk = it - pre[b];
+    const long long len = lens[b];
+    const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
+    int c = 0, nb = 0;
+    if (off < len) {
+      const long long po = poffs ? poffs[b] : -1;
+      const uint4 q = load16(text + (offs ? offs[b] : b * cap), po >= 0 ? packed + po : nullptr, off, len);
+      c = popc_commas(q);
+      nb = nonblank(q);
+    }
+    const int tc = block_sum(c, red);
+    const int tn = block_sum(nb, red);
+    if (threadIdx.x == 0) {
+      counts[b * max_chunks + chunk] = tc;
+      blank[b * max_chunks + chunk] = tn == 0;
+    }
   }
-  const int nonblank_any = block_sum(anynb, red) > 0;
-  const long long n = nonblank_any ? static_cast<long long>(carry) + 1 : 0;
-  if (threadIdx.x == 0) {
-    status[b] = n > numel ? 2 : 0;
-    ntok[b] = static_cast<int>(n);
-  }
-  // zero-fill [n, numel)
-  float* o = out + b * numel;
-  for (long long i = n + threadIdx.x; i < numel; i += 256) o[i] = 0.f;
 }
 
 __constant__ float kP10f[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
@@ -409,95 +427,129 @@ __device__ __forceinline__ bool convert_token_fast(const uint32_t (&r)[8], int n
 
 // Token-parallel parse of one 4 KiB chunk: (1) every thread finds the token starts in its 16 bytes,
 // (2) a block scan compacts them into an LDS list, (3) each lane converts whole tokens, loading 32
-// bytes into registers with aligned LDS reads + alignbyte.
+// bytes into registers with aligned LDS reads + alignbyte.  A token's end is the next token's start
+// (only the chunk's last token scans for its comma), and the per-token whitespace screen runs only
+// in chunks that hold a blank byte.
 __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
                                                  const unsigned char* __restrict__ packed,
                                                  const long long* __restrict__ poffs,
-                                                 const long long* __restrict__ lens, const int* __restrict__ prefix,
-                                                 int* __restrict__ status, float* __restrict__ out, long long numel,
-                                                 int max_chunks) {
+                                                 const long long* __restrict__ lens, int B,
+                                                 const int* __restrict__ counts, const int* __restrict__ blank,
+                                                 int* __restrict__ status, int* __restrict__ ntok,
+                                                 float* __restrict__ out, long long numel, int max_chunks) {
   __shared__ __attribute__((aligned(16))) unsigned char buf[PRE + CHUNK + HALO];
   __shared__ unsigned short starts[CHUNK / 2 + 1];
   __shared__ int red[4];
-  const int b = blockIdx.y, chunk = blockIdx.x;
-  const long long len = lens[b];
-  const long long c0 = static_cast<long long>(chunk) * CHUNK;
-  if (len < 0 || c0 >= len) return;
-  const unsigned char* t = text + (offs ? offs[b] : b * cap);
-  const long long po = poffs ? poffs[b] : -1;
-  const unsigned char* pk = po >= 0 ? packed + po : nullptr;
-  // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
-  for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
-    const long long off = c0 - PRE + 16ll * i;
-    uint4 q;
-    if (off < 0) q = make_uint4(0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu);
-    else if (off >= len) q = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    else q = load16(t, pk, off, len);
-    *reinterpret_cast<uint4*>(buf + 16 * i) = q;
-  }
-  __syncthreads();
-  const int lim = static_cast<int>(len - c0 < CHUNK + HALO ? len - c0 : CHUNK + HALO) + PRE;  // LDS end of text
-  const int lo = PRE + threadIdx.x * 16;
-  const uint4 mine = *reinterpret_cast<const uint4*>(buf + lo);
-  const uint32_t cm = mask16(mine, 0x2C2C2C2Cu);
-  uint32_t sm = ((cm << 1) | (buf[lo - 1] == ',' ? 1u : 0u)) & 0xFFFFu;  // token starts in my 16 bytes
-  if (lo + 16 > lim) sm &= lim > lo ? (1u << (lim - lo)) - 1u : 0u;
-  int total;
-  int k = block_excl_scan(__popc(sm), red, total);
-  while (sm) {
-    const int j = __builtin_ctz(sm);
-    sm &= sm - 1;
-    starts[k++] = static_cast<unsigned short>(lo + j);
-  }
-  __syncthreads();
-  const long long base = static_cast<long long>(prefix[b * max_chunks + chunk]) + (buf[PRE - 1] != ',' ? 1 : 0);
-  bool bad = threadIdx.x == 0 && c0 + CHUNK >= len && buf[lim - 1] == ',';  // trailing comma
-  for (int tk = threadIdx.x; tk < total; tk += 256) {
-    const long long idx = base + tk;  // idx >= numel: still validated, not stored (dec_scan sets status 2)
-    const int p = starts[tk];
-    const int a4 = p & ~3, sh = p & 3;
-    uint32_t x[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) x[i] = *reinterpret_cast<const uint32_t*>(buf + a4 + 4 * i);
-    uint32_t r[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
-    // first ',' and first whitespace in the 32-byte window
-    int n = 32;
-    bool ws = false;
-#pragma unroll
-    for (int i = 7; i >= 0; --i) {
-      const uint32_t c = eq_bytes(r[i], 0x2C2C2C2Cu);
-      if (c) n = 4 * i + (__builtin_ctz(c) >> 3);
-    }
-    const int rem = lim - p;
-    if (rem < n) n = rem;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t w = eq_bytes(r[i], 0x20202020u) | eq_bytes(r[i], 0x0A0A0A0Au) | eq_bytes(r[i], 0x0D0D0D0Du) |
-                         eq_bytes(r[i], 0x09090909u);
-      const int lo_b = 4 * i;
-      if (w && lo_b < n) {
-        const int first = lo_b + (__builtin_ctz(w) >> 3);
-        ws |= first < n;
+  __shared__ int pre[kDecMaxB];
+  const int items = chunk_prefix(lens, B, pre, red);
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int b = item_sample(pre, B, it), chunk = it - pre[b];
+    const long long len = lens[b];
+    const long long c0 = static_cast<long long>(chunk) * CHUNK;
+    const bool last = c0 + CHUNK >= len;
+    // token index of this chunk: the separators of the chunks before it
+    const int* crow = counts + static_cast<size_t>(b) * max_chunks;
+    int s = 0, nbv = 0;
+    for (int c = threadIdx.x; c < chunk; c += 256) s += crow[c];
+    if (last)
+      for (int c = threadIdx.x; c <= chunk; c += 256) nbv |= !blank[static_cast<size_t>(b) * max_chunks + c];
+    const int prefix = block_sum(s, red);
+    const int anynb = last ? block_sum(nbv, red) : 0;  // block-uniform condition
+    if (c0 < len) {
+      const unsigned char* t = text + (offs ? offs[b] : b * cap);
+      const long long po = poffs ? poffs[b] : -1;
+      const unsigned char* pk = po >= 0 ? packed + po : nullptr;
+      const int lim = static_cast<int>(len - c0 < CHUNK + HALO ? len - c0 : CHUNK + HALO) + PRE;  // LDS end of text
+      // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
+      int wsf = 0;
+      for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
+        const long long off = c0 - PRE + 16ll * i;
+        uint4 q;
+        if (off < 0) q = make_uint4(0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu);
+        else if (off >= len) q = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+        else q = load16(t, pk, off, len);
+        *reinterpret_cast<uint4*>(buf + 16 * i) = q;
+        if (16 * i >= PRE && 16 * i < lim) wsf |= nonblank_all(q) ? 0 : 1;
       }
+      const bool anyws = __syncthreads_or(wsf) != 0;
+      const int lo = PRE + threadIdx.x * 16;
+      const uint4 mine = *reinterpret_cast<const uint4*>(buf + lo);
+      const uint32_t cm = mask16(mine, 0x2C2C2C2Cu);
+      uint32_t sm = ((cm << 1) | (buf[lo - 1] == ',' ? 1u : 0u)) & 0xFFFFu;  // token starts in my 16 bytes
+      if (lo + 16 > lim) sm &= lim > lo ? (1u << (lim - lo)) - 1u : 0u;
+      int total;
+      int k = block_excl_scan(__popc(sm), red, total);
+      while (sm) {
+        const int j = __builtin_ctz(sm);
+        sm &= sm - 1;
+        starts[k++] = static_cast<unsigned short>(lo + j);
+      }
+      __syncthreads();
+      const long long base = static_cast<long long>(prefix) + (buf[PRE - 1] != ',' ? 1 : 0);
+      bool bad = threadIdx.x == 0 && last && buf[lim - 1] == ',';  // trailing comma
+      for (int tk = threadIdx.x; tk < total; tk += 256) {
+        const long long idx = base + tk;  // idx >= numel: still validated, not stored (status 2 below)
+        const int p = starts[tk];
+        const int rem = lim - p;
+        const bool inner = tk + 1 < total;  // the next start bounds the token
+        int n = inner ? starts[tk + 1] - 1 - p : 32;
+        float v;
+        bool good;
+        if (inner && n > 32) {  // longer than the register window: LDS path
+          good = convert_token(buf + p, n, v);
+        } else {
+          const int a4 = p & ~3, sh = p & 3;
+          uint32_t x[9];
+#pragma unroll
+          for (int i = 0; i < 9; ++i) x[i] = *reinterpret_cast<const uint32_t*>(buf + a4 + 4 * i);
+          uint32_t r[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
+          if (!inner) {  // the chunk's last token: first ',' in the 32-byte window
+#pragma unroll
+            for (int i = 7; i >= 0; --i) {
+              const uint32_t c = eq_bytes(r[i], 0x2C2C2C2Cu);
+              if (c) n = 4 * i + (__builtin_ctz(c) >> 3);
+            }
+            if (rem < n) n = rem;
+          }
+          bool ws = false;
+          if (anyws) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const uint32_t w = eq_bytes(r[i], 0x20202020u) | eq_bytes(r[i], 0x0A0A0A0Au) |
+                                 eq_bytes(r[i], 0x0D0D0D0Du) | eq_bytes(r[i], 0x09090909u);
+              const int lo_b = 4 * i;
+              if (w && lo_b < n) ws |= lo_b + static_cast<int>(__builtin_ctz(w) >> 3) < n;
+            }
+          }
+          if (!inner && n == 32 && rem > 32) {  // no ',' in the window: LDS path
+            int e = p;
+            while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
+            good = !(e == PRE + CHUNK + HALO && e < lim) && convert_token(buf + p, e - p, v);
+          } else if (ws) {
+            good = convert_token(buf + p, n, v);
+          } else {
+            good = n > 0 && (convert_token_fast(r, n, v) || convert_token_regs(r, n, v));
+          }
+        }
+        if (good && idx < numel) out[b * numel + idx] = v;
+        bad |= !good;
+      }
+      if (bad) atomicOr(status + b, 1);
     }
-    float v;
-    bool good;
-    if (n == 32 && rem > 32) {  // longer than the register window: LDS path
-      int e = p;
-      while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
-      good = !(e == PRE + CHUNK + HALO && e < lim) && convert_token(buf + p, e - p, v);
-    } else if (ws) {
-      good = convert_token(buf + p, n, v);
-    } else {
-      good = n > 0 && (convert_token_fast(r, n, v) || convert_token_regs(r, n, v));
+    if (last) {  // the sample's token count, overflow status and zero-filled tail
+      const long long n = anynb ? static_cast<long long>(prefix) + crow[chunk] + 1 : 0;
+      if (threadIdx.x == 0) {
+        ntok[b] = static_cast<int>(n);
+        if (n > numel) atomicOr(status + b, 2);
+      }
+      float* o = out + b * numel;
+      for (long long i = n + threadIdx.x; i < numel; i += 256) o[i] = 0.f;
     }
-    if (good && idx < numel) out[b * numel + idx] = v;
-    bad |= !good;
+    __syncthreads();  // LDS (buf, starts, red) reused by the next item
   }
-  if (bad) atomicOr(status + b, 1);
 }
 
 }  // namespace
@@ -510,15 +562,15 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
                                void* scratch, hipStream_t s, const unsigned char* packed, const long long* poffs) {
-  if (text_cap % CHUNK) return hipErrorInvalidValue;
+  if (text_cap % CHUNK || B > kDecMaxB || B < 1) return hipErrorInvalidValue;
   const int max_chunks = static_cast<int>(text_cap / CHUNK);
   int* counts = static_cast<int*>(scratch);
   int* blank = counts + static_cast<size_t>(B) * max_chunks;
-  hipLaunchKernelGGL(dec_count, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
-                     packed, poffs, lens, counts, blank, max_chunks);
-  hipLaunchKernelGGL(dec_scan, dim3(B), dim3(256), 0, s, lens, counts, blank, status, ntok, out, numel, max_chunks);
-  hipLaunchKernelGGL(dec_parse, dim3(max_chunks, B), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs,
-                     packed, poffs, lens, counts, status, out, numel, max_chunks);
+  const int grid = static_cast<int>(std::min<long long>(static_cast<long long>(max_chunks) * B, kDecGrid));
+  hipLaunchKernelGGL(dec_count, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,
+                     poffs, lens, B, counts, blank, status, ntok, max_chunks);
+  hipLaunchKernelGGL(dec_parse, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,
+                     poffs, lens, B, counts, blank, status, ntok, out, numel, max_chunks);
   return hipGetLastError();
 }
 

@@ -9,7 +9,16 @@ import numpy as np  # noqa: E402
 
 
 def main():
+    import argparse
+
     import torch
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--styles", default="4dec,repr_f32")
+    ap.add_argument("--batches", default="16,32")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--packed-only", action="store_true")
+    args = ap.parse_args()
 
     import die_amd  # noqa: F401
     from die_amd import native
@@ -22,8 +31,9 @@ def main():
         "repr_f32": lambda: json.dumps([float(v) for v in rng.random(numel).astype(np.float32)])[1:-1].encode(),
     }
     res = {}
+    styles = {k: v for k, v in styles.items() if k in args.styles.split(",")}
     for name, gen in styles.items():
-        for B in (16, 32):
+        for B in [int(b) for b in args.batches.split(",")]:
             texts = [gen() for _ in range(4)] * (B // 4)
             cap = (numel * 24 + 4095) // 4096 * 4096
             host = np.zeros(B * cap, np.uint8)
@@ -57,17 +67,17 @@ def main():
                                            st.data_ptr(), st.data_ptr() + 4 * B, scratch.data_ptr(), s)
                 assert rc == 0
 
-            for packed in ((False, True) if packed_ok else (False,)):
+            for packed in (((True,) if args.packed_only else (False, True)) if packed_ok else (False,)):
                 for _ in range(3):
                     run(packed)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(20):
+                for _ in range(args.iters):
                     run(packed)
                 e1.record()
                 torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) * 1000 / 20
+                us = e0.elapsed_time(e1) * 1000 / args.iters
                 assert int(st[:B].abs().sum()) == 0
                 res["%s%s_B%d" % (name, "_packed" if packed else "", B)] = {
                     "us": round(us, 1), "MB": round(lens.sum() / 1e6, 1), "GBps": round(lens.sum() / us / 1e3, 1),
