@@ -133,8 +133,34 @@ __device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
   return base + x - v;
 }
 
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// exclusive scan over the 64 lanes of this wave; total = the wave's sum
+__device__ __forceinline__ int wave_excl_scan(int v, int& total) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// This wave's LDS writes are complete and visible to its other lanes (and not reordered by the
+// compiler); LDS traffic of one wave needs no workgroup barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 constexpr int kDecMaxB = 1024;  // samples per launch (LDS chunk-prefix table)
-constexpr int kDecGrid = 2048;  // blocks of the grid-stride kernels (8 per CU)
+constexpr int kDecGrid = 2048;  // blocks (4 waves = 4 work items each) of the grid-stride kernels
 
 // Per block: pre[b] = exclusive prefix over samples of their chunk counts (a sample with text has
 // max(1, ceil(len / CHUNK)) chunks -- an empty body still gets one work item; a skipped sample
@@ -169,6 +195,8 @@ __device__ __forceinline__ int item_sample(const int* pre, int B, int item) {
   return lo;
 }
 
+// One WAVE per 4 KiB chunk (no workgroup barriers in the loop): lane l counts the separators of
+// 16-byte words l, l+64, l+128, l+192 (coalesced), the wave sums them.
 __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
                                                  const unsigned char* __restrict__ packed,
@@ -185,22 +213,29 @@ __global__ __launch_bounds__(256) void dec_count(const unsigned char* __restrict
     }
   }
   const int items = chunk_prefix(lens, B, pre, red);
-  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {
     const int b = item_sample(pre, B, it), chunk = it - pre[b];
     const long long len = lens[b];
-    const long long off = static_cast<long long>(chunk) * CHUNK + threadIdx.x * 16;
+    const long long c0 = static_cast<long long>(chunk) * CHUNK;
+    const long long po = poffs ? poffs[b] : -1;
+    const unsigned char* t = text + (offs ? offs[b] : b * cap);
+    const unsigned char* pk = po >= 0 ? packed + po : nullptr;
     int c = 0, nb = 0;
-    if (off < len) {
-      const long long po = poffs ? poffs[b] : -1;
-      const uint4 q = load16(text + (offs ? offs[b] : b * cap), po >= 0 ? packed + po : nullptr, off, len);
-      c = popc_commas(q);
-      nb = nonblank(q);
+#pragma unroll
+    for (int k = 0; k < CHUNK / 16 / 64; ++k) {
+      const long long off = c0 + 16ll * (k * 64 + lane);
+      if (off < len) {
+        const uint4 q = load16(t, pk, off, len);
+        c += popc_commas(q);
+        nb |= nonblank(q);
+      }
     }
-    const int tc = block_sum(c, red);
-    const int tn = block_sum(nb, red);
-    if (threadIdx.x == 0) {
-      counts[b * max_chunks + chunk] = tc;
-      blank[b * max_chunks + chunk] = tn == 0;
+    c = wave_sum(c);
+    nb = wave_sum(nb);
+    if (lane == 0) {
+      counts[b * max_chunks + chunk] = c;
+      blank[b * max_chunks + chunk] = nb == 0;
     }
   }
 }
@@ -209,33 +244,34 @@ __constant__ float kP10f[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 
 __constant__ double kP10d[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-// Convert the token s[0..n) (separators excluded).  Returns false -> host fallback.
-__device__ bool convert_token(const unsigned char* s, int n, float& out) {
+// Convert the token s(0..n) (separators excluded).  Returns false -> host fallback.
+template <class At>
+__device__ bool convert_token(At s, int n, float& out) {  // s(i): byte i of the token
   int i = 0;
-  while (i < n && is_ws(s[i])) ++i;
-  while (n > i && is_ws(s[n - 1])) --n;
+  while (i < n && is_ws(s(i))) ++i;
+  while (n > i && is_ws(s(n - 1))) --n;
   if (i >= n) return false;
-  const bool neg = s[i] == '-';
+  const bool neg = s(i) == '-';
   i += neg;
-  if (i >= n || s[i] - '0' > 9u) return false;
+  if (i >= n || s(i) - '0' > 9u) return false;
   uint64_t mant = 0;
   int nd = 0, exp10 = 0;
-  if (s[i] == '0') {
+  if (s(i) == '0') {
     ++i;
-    if (i < n && s[i] - '0' <= 9u) return false;  // leading zero
+    if (i < n && s(i) - '0' <= 9u) return false;  // leading zero
   } else {
-    while (i < n && s[i] - '0' <= 9u) {
+    while (i < n && s(i) - '0' <= 9u) {
       if (nd >= 19) return false;
-      mant = mant * 10 + (s[i] - '0');
+      mant = mant * 10 + (s(i) - '0');
       ++nd;
       ++i;
     }
   }
-  if (i < n && s[i] == '.') {
+  if (i < n && s(i) == '.') {
     ++i;
-    if (i >= n || s[i] - '0' > 9u) return false;
-    while (i < n && s[i] - '0' <= 9u) {
-      const unsigned d = s[i] - '0';
+    if (i >= n || s(i) - '0' > 9u) return false;
+    while (i < n && s(i) - '0' <= 9u) {
+      const unsigned d = s(i) - '0';
       if (mant != 0 || d != 0) {
         if (nd >= 19) return false;
         mant = mant * 10 + d;
@@ -245,17 +281,17 @@ __device__ bool convert_token(const unsigned char* s, int n, float& out) {
       ++i;
     }
   }
-  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+  if (i < n && (s(i) == 'e' || s(i) == 'E')) {
     ++i;
     int es = 1;
-    if (i < n && (s[i] == '+' || s[i] == '-')) {
-      es = s[i] == '-' ? -1 : 1;
+    if (i < n && (s(i) == '+' || s(i) == '-')) {
+      es = s(i) == '-' ? -1 : 1;
       ++i;
     }
-    if (i >= n || s[i] - '0' > 9u) return false;
+    if (i >= n || s(i) - '0' > 9u) return false;
     int e = 0;
-    while (i < n && s[i] - '0' <= 9u) {
-      e = e * 10 + (s[i] - '0');
+    while (i < n && s(i) - '0' <= 9u) {
+      e = e * 10 + (s(i) - '0');
       if (e > 10000) e = 10000;
       ++i;
     }
@@ -393,44 +429,66 @@ __device__ __forceinline__ bool convert_token_regs(const uint32_t (&r)[8], int n
 // else (exponent, > 8 digits, malformed) returns false and the caller runs the full converter,
 // which decides acceptance and error status exactly as before.
 __device__ __forceinline__ bool convert_token_fast(const uint32_t (&r)[8], int n, float& out) {
-  if (n > 10) return false;
+  // SWAR form (no per-byte loop): body = the token after an optional '-', at most 10 bytes; the one
+  // optional '.' is squeezed out and the <= 8 digits converted with three multiply-shift steps.
+  if (n > 10 || n < 1) return false;
   const bool neg = (r[0] & 0xFFu) == '-';
-  uint32_t mant = 0;
-  int nd = 0, frac = -1;
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    if (i < n && i >= static_cast<int>(neg)) {
-      const uint32_t c = (r[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      const uint32_t d = c - '0';
-      if (c == '.') {
-        ok &= frac < 0 && nd > 0;
-        frac = 0;
-      } else {
-        ok &= d <= 9u;
-        mant = mant * 10 + d;
-        ++nd;
-        frac += frac >= 0;
-      }
-    }
+  const int f = neg ? 1 : 0, L = n - f;  // body length
+  const uint32_t d0 = __builtin_amdgcn_alignbyte(r[1], r[0], f), d1 = __builtin_amdgcn_alignbyte(r[2], r[1], f);
+  const uint32_t d2 = r[2] >> (8 * f);
+  // per-byte flags (0x80) over body bytes [0, L): '.', and "is a digit"
+  auto digit = [](uint32_t x) {
+    const uint32_t ge0 = (x | 0x80808080u) - 0x30303030u;
+    const uint32_t gt9 = (x & 0x7F7F7F7Fu) + 0x46464646u;
+    return ge0 & ~gt9 & ~x & 0x80808080u;
+  };
+  const uint64_t lo = static_cast<uint64_t>(d0) | (static_cast<uint64_t>(d1) << 32);
+  const uint64_t in = L >= 8 ? ~0ull : (1ull << (8 * L)) - 1;                    // body bytes 0..7
+  const uint32_t in2 = L <= 8 ? 0u : (L >= 12 ? ~0u : (1u << (8 * (L - 8))) - 1);  // body bytes 8..11
+  const uint64_t dots = (static_cast<uint64_t>(eq_bytes(d0, 0x2E2E2E2Eu)) | (static_cast<uint64_t>(eq_bytes(d1, 0x2E2E2E2Eu)) << 32)) & in;
+  const uint32_t dots2 = eq_bytes(d2, 0x2E2E2E2Eu) & in2;
+  const uint64_t digs = (static_cast<uint64_t>(digit(d0)) | (static_cast<uint64_t>(digit(d1)) << 32)) & in;
+  const uint32_t digs2 = digit(d2) & in2;
+  const uint64_t all = in & 0x8080808080808080ull;
+  const uint32_t all2 = in2 & 0x80808080u;
+  if (dots2 || (digs2 != all2) || __popcll(dots) > 1 || ((digs | dots) != all)) return false;
+  const int dp = dots ? (__builtin_ctzll(dots) >> 3) : -1;  // '.' position in the body
+  const int nd = L - (dp >= 0 ? 1 : 0);
+  if (nd < 1 || nd > 8 || dp == 0 || dp == L - 1) return false;  // digits before and after a '.'
+  const uint32_t b0 = d0 & 0xFFu, b1 = (d0 >> 8) & 0xFFu;
+  if (b0 == '0' && L > 1 && b1 != '.') return false;  // a leading '0' must be the whole integer part
+  // squeeze the '.' out: digits now fill bytes [0, nd) of w (nd <= 8, so the dot is in bytes 0..7)
+  uint64_t w = lo;
+  if (dp >= 0) {
+    const uint64_t below = (1ull << (8 * dp)) - 1;
+    w = (lo & below) | (((lo >> 8) | (static_cast<uint64_t>(d2) << 56)) & ~below);
   }
-  // a leading '0' must be the whole integer part
-  const int f = neg ? 1 : 0;
-  const uint32_t c0 = (r[0] >> (8 * f)) & 0xFFu, c1 = (r[0] >> (8 * (f + 1))) & 0xFFu;
-  ok &= !(c0 == '0' && n > f + 1 && c1 != '.');
-  ok &= nd > 0 && nd <= 8 && frac != 0 && mant <= (1u << 24);
-  if (!ok) return false;
-  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / kP10f[frac] : static_cast<float>(mant) * kP10f[0]);
+  // right-align the nd digits at the top, '0'-padded below, then the 8-digit SWAR conversion
+  const int sh = 8 * (8 - nd);
+  w = sh ? ((w << sh) | (0x3030303030303030ull >> (64 - sh))) : w;
+  w -= 0x3030303030303030ull;
+  w = (w * 10) + (w >> 8);
+  w = (((w & 0x000000FF000000FFull) * (100 + (1000000ull << 32))) +
+       (((w >> 16) & 0x000000FF000000FFull) * (1 + (10000ull << 32)))) >> 32;
+  const uint32_t mant = static_cast<uint32_t>(w);
+  if (mant > (1u << 24)) return false;
+  const int frac = dp >= 0 ? L - dp - 1 : 0;
+  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / kP10f[frac] : static_cast<float>(mant));
   out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
   return true;
 }
 
-// Token-parallel parse of one 4 KiB chunk: (1) every thread finds the token starts in its 16 bytes,
-// (2) a block scan compacts them into an LDS list, (3) each lane converts whole tokens, loading 32
-// bytes into registers with aligned LDS reads + alignbyte.  A token's end is the next token's start
-// (only the chunk's last token scans for its comma), and the per-token whitespace screen runs only
-// in chunks that hold a blank byte.
-__global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
+// Per-wave LDS image of the staged bytes: logical byte L (0 = chunk start - PRE) lives at
+// L + 4 * ((L + 48) / 64), i.e. every lane's 64-byte region (and the PRE bytes before region 0) is
+// followed by a 4-byte gap.  Lane regions then start 17 dwords apart, so the 64 lanes' token-window
+// reads (one region each) hit distinct banks instead of 2 (a 16-way conflict on every read).
+constexpr int kWaveLds = PRE + CHUNK + HALO + 4 * ((PRE + CHUNK + HALO + 48) / 64 + 1);
+__device__ __forceinline__ int lpos(int L) { return L + 4 * ((L + 48) >> 6); }
+__device__ __forceinline__ uint32_t ld32(const unsigned char* buf, int L) {  // L % 4 == 0
+  return *reinterpret_cast<const uint32_t*>(buf + lpos(L));
+}
+
+__global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
                                                  const unsigned char* __restrict__ packed,
                                                  const long long* __restrict__ poffs,
@@ -438,12 +496,14 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
                                                  const int* __restrict__ counts, const int* __restrict__ blank,
                                                  int* __restrict__ status, int* __restrict__ ntok,
                                                  float* __restrict__ out, long long numel, int max_chunks) {
-  __shared__ __attribute__((aligned(16))) unsigned char buf[PRE + CHUNK + HALO];
-  __shared__ unsigned short starts[CHUNK / 2 + 1];
+  constexpr int WB = PRE + CHUNK + HALO;  // staged bytes per wave
+  __shared__ __attribute__((aligned(16))) unsigned char sbuf[4][kWaveLds];
   __shared__ int red[4];
   __shared__ int pre[kDecMaxB];
   const int items = chunk_prefix(lens, B, pre, red);
-  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char* buf = sbuf[wave];
+  for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {
     const int b = item_sample(pre, B, it), chunk = it - pre[b];
     const long long len = lens[b];
     const long long c0 = static_cast<long long>(chunk) * CHUNK;
@@ -451,11 +511,11 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
     // token index of this chunk: the separators of the chunks before it
     const int* crow = counts + static_cast<size_t>(b) * max_chunks;
     int s = 0, nbv = 0;
-    for (int c = threadIdx.x; c < chunk; c += 256) s += crow[c];
+    for (int c = lane; c < chunk; c += 64) s += crow[c];
     if (last)
-      for (int c = threadIdx.x; c <= chunk; c += 256) nbv |= !blank[static_cast<size_t>(b) * max_chunks + c];
-    const int prefix = block_sum(s, red);
-    const int anynb = last ? block_sum(nbv, red) : 0;  // block-uniform condition
+      for (int c = lane; c <= chunk; c += 64) nbv |= !blank[static_cast<size_t>(b) * max_chunks + c];
+    const int prefix = wave_sum(s);
+    const int anynb = last ? wave_sum(nbv) : 0;
     if (c0 < len) {
       const unsigned char* t = text + (offs ? offs[b] : b * cap);
       const long long po = poffs ? poffs[b] : -1;
@@ -463,50 +523,57 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
       const int lim = static_cast<int>(len - c0 < CHUNK + HALO ? len - c0 : CHUNK + HALO) + PRE;  // LDS end of text
       // stage [c0 - 16, c0 + CHUNK + HALO) (bytes outside [0, len) read as ' '; the byte before 0 as ',')
       int wsf = 0;
-      for (int i = threadIdx.x; i < (PRE + CHUNK + HALO) / 16; i += 256) {
+      for (int i = lane; i < WB / 16; i += 64) {
         const long long off = c0 - PRE + 16ll * i;
         uint4 q;
         if (off < 0) q = make_uint4(0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu, 0x2C2C2C2Cu);
         else if (off >= len) q = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
         else q = load16(t, pk, off, len);
-        *reinterpret_cast<uint4*>(buf + 16 * i) = q;
+        uint32_t* d = reinterpret_cast<uint32_t*>(buf + lpos(16 * i));  // a 16-byte word never straddles a gap
+        d[0] = q.x;
+        d[1] = q.y;
+        d[2] = q.z;
+        d[3] = q.w;
         if (16 * i >= PRE && 16 * i < lim) wsf |= nonblank_all(q) ? 0 : 1;
       }
-      const bool anyws = __syncthreads_or(wsf) != 0;
-      const int lo = PRE + threadIdx.x * 16;
-      const uint4 mine = *reinterpret_cast<const uint4*>(buf + lo);
-      const uint32_t cm = mask16(mine, 0x2C2C2C2Cu);
-      uint32_t sm = ((cm << 1) | (buf[lo - 1] == ',' ? 1u : 0u)) & 0xFFFFu;  // token starts in my 16 bytes
-      if (lo + 16 > lim) sm &= lim > lo ? (1u << (lim - lo)) - 1u : 0u;
+      wave_lds_sync();
+      const bool anyws = __ballot(wsf) != 0;
+      // token starts in my 64 bytes
+      const int lo = PRE + 64 * lane;
+      uint64_t cm = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        cm |= static_cast<uint64_t>(mask16(make_uint4(ld32(buf, lo + 16 * k), ld32(buf, lo + 16 * k + 4),
+                                                       ld32(buf, lo + 16 * k + 8), ld32(buf, lo + 16 * k + 12)),
+                                            0x2C2C2C2Cu))
+              << (16 * k);
+      uint64_t sm = (cm << 1) | (buf[lpos(lo - 1)] == ',' ? 1ull : 0ull);
+      if (lo + 64 > lim) sm &= lim > lo ? (1ull << (lim - lo)) - 1ull : 0ull;
       int total;
-      int k = block_excl_scan(__popc(sm), red, total);
+      const int k0 = wave_excl_scan(__popcll(sm), total);
+      long long idx = static_cast<long long>(prefix) + (buf[lpos(PRE - 1)] != ',' ? 1 : 0) + k0;
+      bool bad = lane == 0 && last && buf[lpos(lim - 1)] == ',';  // trailing comma
       while (sm) {
-        const int j = __builtin_ctz(sm);
+        const int j = __builtin_ctzll(sm);
         sm &= sm - 1;
-        starts[k++] = static_cast<unsigned short>(lo + j);
-      }
-      __syncthreads();
-      const long long base = static_cast<long long>(prefix) + (buf[PRE - 1] != ',' ? 1 : 0);
-      bool bad = threadIdx.x == 0 && last && buf[lim - 1] == ',';  // trailing comma
-      for (int tk = threadIdx.x; tk < total; tk += 256) {
-        const long long idx = base + tk;  // idx >= numel: still validated, not stored (status 2 below)
-        const int p = starts[tk];
+        const int p = lo + j;
         const int rem = lim - p;
-        const bool inner = tk + 1 < total;  // the next start bounds the token
-        int n = inner ? starts[tk + 1] - 1 - p : 32;
-        float v;
-        bool good;
-        if (inner && n > 32) {  // longer than the register window: LDS path
-          good = convert_token(buf + p, n, v);
+        const bool inner = sm != 0;  // my next start bounds the token
+        int n = inner ? __builtin_ctzll(sm) - j - 1 : 32;
+        float v = 0.f;
+        bool good = false;
+        int slow = -1;  // > = 0: convert bytes [p, p + slow) with the byte-wise converter
+        if (inner && n > 32) {  // longer than the register window
+          slow = n;
         } else {
           const int a4 = p & ~3, sh = p & 3;
           uint32_t x[9];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) x[i] = *reinterpret_cast<const uint32_t*>(buf + a4 + 4 * i);
+          for (int i = 0; i < 9; ++i) x[i] = ld32(buf, a4 + 4 * i);
           uint32_t r[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
-          if (!inner) {  // the chunk's last token: first ',' in the 32-byte window
+          if (!inner) {  // my last token: first ',' in the 32-byte window
 #pragma unroll
             for (int i = 7; i >= 0; --i) {
               const uint32_t c = eq_bytes(r[i], 0x2C2C2C2Cu);
@@ -524,31 +591,33 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
               if (w && lo_b < n) ws |= lo_b + static_cast<int>(__builtin_ctz(w) >> 3) < n;
             }
           }
-          if (!inner && n == 32 && rem > 32) {  // no ',' in the window: LDS path
+          if (!inner && n == 32 && rem > 32) {  // no ',' in the window: find it in LDS
             int e = p;
-            while (e < PRE + CHUNK + HALO && e < lim && buf[e] != ',') ++e;
-            good = !(e == PRE + CHUNK + HALO && e < lim) && convert_token(buf + p, e - p, v);
+            while (e < WB && e < lim && buf[lpos(e)] != ',') ++e;
+            if (!(e == WB && e < lim)) slow = e - p;  // else: longer than the halo -> host fallback
           } else if (ws) {
-            good = convert_token(buf + p, n, v);
+            slow = n;
           } else {
             good = n > 0 && (convert_token_fast(r, n, v) || convert_token_regs(r, n, v));
           }
         }
-        if (good && idx < numel) out[b * numel + idx] = v;
+        if (slow >= 0) good = convert_token([&](int i) -> unsigned { return buf[lpos(p + i)]; }, slow, v);
+        if (good && idx < numel) out[b * numel + idx] = v;  // idx >= numel: validated, not stored
         bad |= !good;
+        ++idx;
       }
       if (bad) atomicOr(status + b, 1);
     }
     if (last) {  // the sample's token count, overflow status and zero-filled tail
       const long long n = anynb ? static_cast<long long>(prefix) + crow[chunk] + 1 : 0;
-      if (threadIdx.x == 0) {
+      if (lane == 0) {
         ntok[b] = static_cast<int>(n);
         if (n > numel) atomicOr(status + b, 2);
       }
       float* o = out + b * numel;
-      for (long long i = n + threadIdx.x; i < numel; i += 256) o[i] = 0.f;
+      for (long long i = n + lane; i < numel; i += 64) o[i] = 0.f;
     }
-    __syncthreads();  // LDS (buf, starts, red) reused by the next item
+    wave_lds_sync();  // every lane done reading buf before the next item's staging
   }
 }
 
@@ -566,7 +635,7 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
   const int max_chunks = static_cast<int>(text_cap / CHUNK);
   int* counts = static_cast<int*>(scratch);
   int* blank = counts + static_cast<size_t>(B) * max_chunks;
-  const int grid = static_cast<int>(std::min<long long>(static_cast<long long>(max_chunks) * B, kDecGrid));
+  const int grid = static_cast<int>(std::min<long long>((static_cast<long long>(max_chunks) * B + 3) / 4, kDecGrid));
   hipLaunchKernelGGL(dec_count, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,
                      poffs, lens, B, counts, blank, status, ntok, max_chunks);
   hipLaunchKernelGGL(dec_parse, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,

@@ -181,7 +181,8 @@ def test_dp_every_rank_ingests(native, models, world):
         for p in ps:
             line = p.stdout.readline().decode()
             assert "READY" in line, line + p.stdout.read().decode()
-        res = native.loadgen(port=port, connections=24, requests=240, payload="full", input_numel=3 * 64 * 64)
+        res = native.loadgen(port=port, connections=24, requests=240, payload="full", input_numel=3 * 64 * 64,
+                             timeout_ms=60000)
         assert res["ok"] == 240 and res["failed"] == 0, res
         x = r.synthetic_input(3, cfg).reshape(3, -1)
         for i in range(3):  # answers are right whichever rank took the connection
