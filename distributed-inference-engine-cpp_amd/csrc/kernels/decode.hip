@@ -428,6 +428,14 @@ __device__ __forceinline__ bool convert_token_regs(const uint32_t (&r)[8], int n
 // the same single fp32 rounding (mant <= 2^24, |exp10| <= 8), so it is bit-identical.  Anything
 // else (exponent, > 8 digits, malformed) returns false and the caller runs the full converter,
 // which decides acceptance and error status exactly as before.
+// 10^k for k in [0, 15] without a (lane-divergent) memory lookup; exact in fp32 for k <= 10
+__device__ __forceinline__ float pow10f_small(int k) {
+  float p = (k & 1) ? 10.f : 1.f;
+  p *= (k & 2) ? 100.f : 1.f;
+  p *= (k & 4) ? 1e4f : 1.f;
+  return (k & 8) ? p * 1e8f : p;
+}
+
 __device__ __forceinline__ bool convert_token_fast(const uint32_t (&r)[8], int n, float& out) {
   // SWAR form (no per-byte loop): body = the token after an optional '-', at most 10 bytes; the one
   // optional '.' is squeezed out and the <= 8 digits converted with three multiply-shift steps.
@@ -473,7 +481,7 @@ __device__ __forceinline__ bool convert_token_fast(const uint32_t (&r)[8], int n
   const uint32_t mant = static_cast<uint32_t>(w);
   if (mant > (1u << 24)) return false;
   const int frac = dp >= 0 ? L - dp - 1 : 0;
-  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / kP10f[frac] : static_cast<float>(mant));
+  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / pow10f_small(frac) : static_cast<float>(mant));
   out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
   return true;
 }
@@ -488,7 +496,7 @@ __device__ __forceinline__ uint32_t ld32(const unsigned char* buf, int L) {  // 
   return *reinterpret_cast<const uint32_t*>(buf + lpos(L));
 }
 
-__global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restrict__ text, long long cap,
+__global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict__ text, long long cap,
                                                  const long long* __restrict__ offs,
                                                  const unsigned char* __restrict__ packed,
                                                  const long long* __restrict__ poffs,
@@ -498,11 +506,13 @@ __global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restr
                                                  float* __restrict__ out, long long numel, int max_chunks) {
   constexpr int WB = PRE + CHUNK + HALO;  // staged bytes per wave
   __shared__ __attribute__((aligned(16))) unsigned char sbuf[4][kWaveLds];
+  __shared__ unsigned short sstarts[4][CHUNK / 2 + 2];
   __shared__ int red[4];
   __shared__ int pre[kDecMaxB];
   const int items = chunk_prefix(lens, B, pre, red);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char* buf = sbuf[wave];
+  unsigned short* starts = sstarts[wave];
   for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {
     const int b = item_sample(pre, B, it), chunk = it - pre[b];
     const long long len = lens[b];
@@ -549,21 +559,34 @@ __global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restr
               << (16 * k);
       uint64_t sm = (cm << 1) | (buf[lpos(lo - 1)] == ',' ? 1ull : 0ull);
       if (lo + 64 > lim) sm &= lim > lo ? (1ull << (lim - lo)) - 1ull : 0ull;
+      // compact the starts into this wave's list, then take the tokens round-robin (lane l: tokens
+      // l, l + 64, ...) so that consecutive lanes store consecutive values
       int total;
-      const int k0 = wave_excl_scan(__popcll(sm), total);
-      long long idx = static_cast<long long>(prefix) + (buf[lpos(PRE - 1)] != ',' ? 1 : 0) + k0;
-      bool bad = lane == 0 && last && buf[lpos(lim - 1)] == ',';  // trailing comma
+      int k = wave_excl_scan(__popcll(sm), total);
       while (sm) {
-        const int j = __builtin_ctzll(sm);
+        starts[k++] = static_cast<unsigned short>(lo + __builtin_ctzll(sm));
         sm &= sm - 1;
-        const int p = lo + j;
+      }
+      wave_lds_sync();
+      const long long base = static_cast<long long>(prefix) + (buf[lpos(PRE - 1)] != ',' ? 1 : 0);
+      bool bad = lane == 0 && last && buf[lpos(lim - 1)] == ',';  // trailing comma
+      for (int tk = lane; tk < total; tk += 64) {
+        const long long idx = base + tk;  // idx >= numel: validated, not stored
+        const int p = starts[tk];
         const int rem = lim - p;
-        const bool inner = sm != 0;  // my next start bounds the token
-        int n = inner ? __builtin_ctzll(sm) - j - 1 : 32;
+        const bool inner = tk + 1 < total;  // the next start bounds the token
+        int n = inner ? starts[tk + 1] - 1 - p : 32;
         float v = 0.f;
         bool good = false;
-        int slow = -1;  // > = 0: convert bytes [p, p + slow) with the byte-wise converter
-        if (inner && n > 32) {  // longer than the register window
+        int slow = -1;  // >= 0: convert bytes [p, p + slow) with the byte-wise converter
+        if (inner && n <= 10 && !anyws) {  // hot path: a short token from a 12-byte window
+          const int a4 = p & ~3, sh = p & 3;
+          const uint32_t x0 = ld32(buf, a4), x1 = ld32(buf, a4 + 4), x2 = ld32(buf, a4 + 8), x3 = ld32(buf, a4 + 12);
+          uint32_t r[8] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), 0, 0, 0, 0, 0};
+          good = convert_token_fast(r, n, v);
+          if (!good) slow = n;  // malformed or unusual: the byte-wise converter decides
+        } else if (inner && n > 32) {  // longer than the register window
           slow = n;
         } else {
           const int a4 = p & ~3, sh = p & 3;
@@ -573,7 +596,7 @@ __global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restr
           uint32_t r[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
-          if (!inner) {  // my last token: first ',' in the 32-byte window
+          if (!inner) {  // the chunk's last token: first ',' in the 32-byte window
 #pragma unroll
             for (int i = 7; i >= 0; --i) {
               const uint32_t c = eq_bytes(r[i], 0x2C2C2C2Cu);
@@ -602,9 +625,8 @@ __global__ __launch_bounds__(256, 5) void dec_parse(const unsigned char* __restr
           }
         }
         if (slow >= 0) good = convert_token([&](int i) -> unsigned { return buf[lpos(p + i)]; }, slow, v);
-        if (good && idx < numel) out[b * numel + idx] = v;  // idx >= numel: validated, not stored
+        if (good && idx < numel) out[b * numel + idx] = v;
         bad |= !good;
-        ++idx;
       }
       if (bad) atomicOr(status + b, 1);
     }

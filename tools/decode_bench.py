@@ -34,7 +34,9 @@ def main():
     styles = {k: v for k, v in styles.items() if k in args.styles.split(",")}
     for name, gen in styles.items():
         for B in [int(b) for b in args.batches.split(",")]:
-            texts = [gen() for _ in range(4)] * (B // 4)
+            base = [gen() for _ in range(min(4, B))]
+            texts = (base * ((B + len(base) - 1) // len(base)))[:B]
+            assert len(texts) == B  # one text per sample: the kernels read lens[0..B)
             cap = (numel * 24 + 4095) // 4096 * 4096
             host = np.zeros(B * cap, np.uint8)
             lens = np.array([len(t) for t in texts], np.int64)
