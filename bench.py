@@ -337,6 +337,20 @@ def main():
         eng.close()
 
     if world > 1:
+        # where the time goes, rank by rank (a SCALE number blends host-CPU partitioning with GPU
+        # scaling: each rank's own throughput, latency, batch size, device time and host CPU)
+        mine = {"rank": rank, "requests_per_s": round(ok / elapsed, 1) if elapsed > 0 else None,
+                "elapsed_s": round(elapsed, 3), "failed": failed}
+        for k in ("p50_ms", "p99_ms", "avg_batch", "avg_dp_batch", "device_ms_per_batch", "device_busy_frac",
+                  "gpu_gap_ms_per_batch", "cpu_us_per_request", "requests_parsed_this_rank"):
+            if extra.get(k) is not None:
+                mine[k] = extra[k]
+        if isinstance(extra.get("direct_worker"), dict):
+            mine["direct_rps"] = round(extra["direct_worker"].get("rps_this_rank", 0.0), 1)
+        mine["numa_cpus"] = numa.get("cpu_share") if isinstance(numa, dict) else None
+        per_rank = hg.all_gather_object(mine)
+        if rank == 0:
+            extra["per_rank"] = per_rank
         elapsed = hg.reduce([elapsed], "max")[0]
         ok, failed = hg.reduce([ok, failed], "sum")
         extra["p50_ms"], extra["p99_ms"] = hg.reduce([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], "max")

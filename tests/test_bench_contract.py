@@ -67,6 +67,10 @@ def test_bench_two_ranks_torchrun_cpu(mode):
                 "--mode", mode] + ARGS)
     _check(out, 2, 2, 1, mode)
     assert out["config"]["global_batch"] == 4
+    # per-rank breakdown of the multi-GPU number (rank order, each rank's own throughput)
+    pr = out["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert all(r["requests_per_s"] > 0 and r["failed"] == 0 for r in pr)
 
 
 def test_bench_rejects_gpus_world_mismatch():
