@@ -146,6 +146,10 @@ __global__ void gather_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __r
 //    4-key reads per k-step in exactly that key order.
 constexpr int AT_D = 64;
 constexpr int VP = 96;  // V row pitch (elements)
+#ifndef DIE_ATTN_STREAM
+#define DIE_ATTN_STREAM 1
+#endif
+constexpr bool kAttnStream = DIE_ATTN_STREAM != 0;  // streaming (tiled K/V) attention kernel
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -316,6 +320,184 @@ __global__ __launch_bounds__(512) void attention_kernel(const uint16_t* __restri
   }
 }
 
+// Streaming variant: K/V pass through LDS in 32-key tiles, double-buffered (tile kt+1's global loads
+// are in flight during tile kt's MFMAs), so a block needs 40 KiB of LDS in fp32 (split) mode instead of
+// the whole pair's K/V image (143 KiB at S = 197: one block per CU).  A block = 4 waves = 128 queries
+// of one (image, head) pair: ViT-B/16 at B = 32 is 768 blocks, all resident at 4 blocks per CU.
+// The per-tile math (S^T = K Q^T, online exp2 softmax, O^T += V^T P^T with transposed V reads, split
+// hi/lo MFMAs) is the kernel above's, with tile-local K/V rows.
+template <bool SPLIT>
+__global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t* __restrict__ q,
+                                                               const uint16_t* __restrict__ k,
+                                                               const uint16_t* __restrict__ v,
+                                                               uint16_t* __restrict__ out, int S, int ldq, int ldk,
+                                                               int ldv, int ldo, float scale_log2) {
+  constexpr int NP = SPLIT ? 2 : 1;
+  constexpr int KT = 32;  // keys per tile
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][NP][KT * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][NP][KT * VP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const long long rowbase = static_cast<long long>(b) * S;
+  const long long rows = static_cast<long long>(gridDim.z) * S;  // plane distances: rows x pitch
+  const int nkt = (S + KT - 1) / KT;
+  // tile loader: thread = (key row ls, 16-B chunk lc) of every tensor plane
+  const int ls = tid >> 3, lc = tid & 7;
+  uint4 kr[NP], vr[NP];
+  auto fetch = [&](int kt) {
+    const int s = kt * KT + ls;
+    const bool ok = s < S;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      kr[pl] = ok ? *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * AT_D + lc * 8)
+                  : make_uint4(0, 0, 0, 0);
+      vr[pl] = ok ? *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * AT_D + lc * 8)
+                  : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      *reinterpret_cast<uint4*>(Ks[buf][pl] + ls * AT_D + ((lc ^ ((ls >> 1) & 7)) << 3)) = kr[pl];
+      *reinterpret_cast<uint4*>(Vs[buf][pl] + ls * VP + lc * 8) = vr[pl];
+    }
+  };
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const bool active = q0 < S;  // wave-uniform; an idle wave still loads tiles and meets every barrier
+  const int r = lane & 31, hh = lane >> 5;
+  bf16x8 qf[NP][4];
+  {
+    const int qr = q0 + r;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        uint4 t = make_uint4(0, 0, 0, 0);
+        if (qr < S)
+          t = *reinterpret_cast<const uint4*>(q + pl * rows * ldq + (rowbase + qr) * ldq + h * AT_D + ks * 16 + hh * 8);
+        qf[pl][ks] = __builtin_bit_cast(bf16x8, t);
+      }
+  }
+  // K/V tile 0 after the query loads: put(0)'s wait for the tile also covers the query fragments, so
+  // the loop's MFMAs never wait on vmcnt (which would drain the NEXT tile's in-flight loads each step)
+  fetch(0);
+  put(0);
+  __syncthreads();
+  f32x16 o0, o1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) fetch(kt + 1);  // in flight under this tile's MFMAs
+    if (active) {
+      f32x16 sc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int chunk = 2 * ks + hh;
+        const int ko = r * AT_D + ((chunk ^ ((r >> 1) & 7)) << 3);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks[buf][0] + ko);
+        if constexpr (SPLIT) {
+          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Ks[buf][1] + ko);
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[0][ks], sc, 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[NP - 1][ks], sc, 0, 0, 0);
+        }
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][ks], sc, 0, 0, 0);
+      }
+      float mt = -INFINITY;
+      if (kt * KT + KT <= S) {  // full tile (wave-uniform): no key mask
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sc[i] *= scale_log2;
+          mt = fmaxf(mt, sc[i]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const float x = key < S ? sc[i] * scale_log2 : -INFINITY;
+          sc[i] = x;
+          mt = fmaxf(mt, x);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first tile: 0
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o0[i] *= alpha;
+        o1[i] *= alpha;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sc[i] - mn);  // raw v_exp_f32 (args <= 0)
+        sc[i] = p;
+        l += p;
+      }
+      m = mn;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pf, pfl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pf[j] = static_cast<__bf16>(sc[8 * st + j]);
+          if constexpr (SPLIT) pfl[j] = static_cast<__bf16>(sc[8 * st + j] - static_cast<float>(pf[j]));
+        }
+        const int vo = (16 * st + 4 * hh + qq) * VP + 16 * g + 4 * pp;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const s16x4 lo = ds_read_tr16(Vs[buf][0] + vo + dt * 32);
+          const s16x4 hi = ds_read_tr16(Vs[buf][0] + vo + 8 * VP + dt * 32);
+          const bf16x8 af = __builtin_bit_cast(bf16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+          f32x16& o = dt == 0 ? o0 : o1;
+          if constexpr (SPLIT) {
+            const s16x4 lo2 = ds_read_tr16(Vs[buf][NP - 1] + vo + dt * 32);
+            const s16x4 hi2 = ds_read_tr16(Vs[buf][NP - 1] + vo + 8 * VP + dt * 32);
+            const bf16x8 al =
+                __builtin_bit_cast(bf16x8, s16x8{lo2[0], lo2[1], lo2[2], lo2[3], hi2[0], hi2[1], hi2[2], hi2[3]});
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, pf, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pfl, o, 0, 0, 0);
+          }
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o, 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 1 < nkt) put(buf ^ 1);  // that buffer's last readers passed the previous barrier
+    __syncthreads();
+  }
+  if (!active) return;
+  l += __shfl_xor(l, 32, 64);
+  const int qr = q0 + r;
+  if (qr >= S) return;
+  const float inv = 1.f / l;
+  uint16_t* orow = out + (rowbase + qr) * ldo + h * AT_D;
+  const long long oplane = rows * ldo;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int d = 8 * g4 + 4 * hh;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const f32x16& o = half ? o1 : o0;
+      float w[4] = {o[4 * g4] * inv, o[4 * g4 + 1] * inv, o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv};
+      uint16_t* dst = orow + 32 * half + d;
+      if constexpr (SPLIT) {
+        uint16_t hv[4], lv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) split1(w[t], hv[t], lv[t]);
+        *reinterpret_cast<uint2*>(dst) = make_uint2(hv[0] | (uint32_t(hv[1]) << 16), hv[2] | (uint32_t(hv[3]) << 16));
+        *reinterpret_cast<uint2*>(dst + oplane) =
+            make_uint2(lv[0] | (uint32_t(lv[1]) << 16), lv[2] | (uint32_t(lv[3]) << 16));
+      } else {
+        *reinterpret_cast<uint2*>(dst) = pack4(w[0], w[1], w[2], w[3]);
+      }
+    }
+  }
+}
+
 // Softmax over rows (one wave per row, fp32 max / sum with exp2): classifier heads and any softmax
 // outside the fused attention.
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
@@ -395,8 +577,14 @@ hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long 
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
   if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
-  dim3 grid(1, H, B);  // one 8-wave block per (image, head): wave w = query tile w (S <= 256)
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
+  if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S <= 256)
+    dim3 grid((S + 127) / 128, H, B);
+    if (split) hipLaunchKernelGGL(attention_stream_kernel<true>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else hipLaunchKernelGGL(attention_stream_kernel<false>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    return hipGetLastError();
+  }
+  dim3 grid(1, H, B);  // one 8-wave block per (image, head): wave w = query tile w (S <= 256)
   if (split) {
     if (S <= 64) hipLaunchKernelGGL((attention_kernel<2, true>), grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
     else if (S <= 128) hipLaunchKernelGGL((attention_kernel<4, true>), grid, dim3(512), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
