@@ -653,15 +653,24 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
                                void* scratch, hipStream_t s, const unsigned char* packed, const long long* poffs) {
-  if (text_cap % CHUNK || B > kDecMaxB || B < 1) return hipErrorInvalidValue;
+  if (text_cap % CHUNK || B < 1) return hipErrorInvalidValue;
   const int max_chunks = static_cast<int>(text_cap / CHUNK);
   int* counts = static_cast<int*>(scratch);
-  int* blank = counts + static_cast<size_t>(B) * max_chunks;
-  const int grid = static_cast<int>(std::min<long long>((static_cast<long long>(max_chunks) * B + 3) / 4, kDecGrid));
-  hipLaunchKernelGGL(dec_count, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,
-                     poffs, lens, B, counts, blank, status, ntok, max_chunks);
-  hipLaunchKernelGGL(dec_parse, dim3(grid), dim3(256), 0, s, text, static_cast<long long>(text_cap), offs, packed,
-                     poffs, lens, B, counts, blank, status, ntok, out, numel, max_chunks);
+  // batches above the kernels' per-launch sample table run in passes of kDecMaxB samples (the
+  // scratch is sized for the whole batch; each pass uses its front)
+  for (int b0 = 0; b0 < B; b0 += kDecMaxB) {
+    const int nb = std::min(B - b0, kDecMaxB);
+    int* blank = counts + static_cast<size_t>(nb) * max_chunks;
+    const unsigned char* t = offs ? text : text + static_cast<size_t>(b0) * text_cap;  // contiguous: slot b at b * cap
+    const long long* o = offs ? offs + b0 : nullptr;
+    const long long* po = poffs ? poffs + b0 : nullptr;
+    const int grid = static_cast<int>(std::min<long long>((static_cast<long long>(max_chunks) * nb + 3) / 4, kDecGrid));
+    hipLaunchKernelGGL(dec_count, dim3(grid), dim3(256), 0, s, t, static_cast<long long>(text_cap), o, packed, po,
+                       lens + b0, nb, counts, blank, status + b0, ntok + b0, max_chunks);
+    hipLaunchKernelGGL(dec_parse, dim3(grid), dim3(256), 0, s, t, static_cast<long long>(text_cap), o, packed, po,
+                       lens + b0, nb, counts, blank, status + b0, ntok + b0, out + static_cast<size_t>(b0) * numel, numel,
+                       max_chunks);
+  }
   return hipGetLastError();
 }
 

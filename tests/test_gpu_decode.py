@@ -266,3 +266,21 @@ def test_engine_run_text_packed_matches_raw(native, tmp_path):
     ref = e.run(x[:5])
     np.testing.assert_array_equal(packed[:5], ref)
     e.close()
+
+
+def test_decode_batch_above_one_launch(native):
+    """More samples than one launch's sample table (kDecMaxB = 1024): the launcher runs passes; every
+    sample (first, last, both sides of the pass boundary) decodes to its own values."""
+    from die_amd.ops import kernels as K
+
+    B = 1100
+    texts = [("%d,%d.5,-%d" % (i, i % 7, i)).encode() if i % 97 else None for i in range(B)]
+    vals, status, ntok = K.decode_json_numbers(texts, 4)
+    v, st, nt = vals.cpu().numpy(), status.cpu().numpy(), ntok.cpu().numpy()
+    for i in (0, 1, 1022, 1023, 1024, 1025, B - 1):
+        if texts[i] is None:
+            assert nt[i] == -1
+            continue
+        assert st[i] == 0 and nt[i] == 3, (i, st[i], nt[i])
+        assert list(v[i]) == [float(i), (i % 7) + 0.5, -float(i), 0.0], (i, v[i])
+    assert (st == 0).all()
