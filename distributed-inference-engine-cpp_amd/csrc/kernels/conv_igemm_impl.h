@@ -421,7 +421,9 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
 // so STAGES-1 K-steps stay in flight across the barrier.  The DMA writes 1 KiB per wave-instruction
 // lane-linearly (8 rows x 128 B), so the (row>>1)&7 chunk swizzle goes on the per-lane SOURCE
 // address.  Padding pixels and M tails read a zero page instead of being predicated.
-// MODE 0: dense rows (1x1/s1 conv, GEMM), K % 64 == 0.  MODE 2: implicit conv with Cin % 64 == 0
+// MODE 0: dense rows (1x1/s1 conv, GEMM), K % 64 == 0.  MODE 3: patchify conv (stride == kernel, no
+// padding, KW * Cin % 64 == 0: a K-step is a contiguous piece of one input row of the patch).
+// MODE 2: implicit conv with Cin % 64 == 0
 // (one 64-channel K-step never straddles a filter tap, so the tap is wave-uniform per K-step).
 // ------------------------------------------------------------------------------------------------
 // s_waitcnt with only the vector-memory counter constrained (gfx9 simm16: vmcnt = bits 3:0 + 15:14,
@@ -538,6 +540,15 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     if (MODE == 0) {
       bsrc[i] = (bval[i] ? p.x + static_cast<size_t>(mm) * p.Cin : p.zeros) + c * 8;
       bih[i] = biw[i] = 0;
+    } else if (MODE == 3) {  // patchify: the patch's top-left input pixel (tail rows: the zero page)
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int rr = mm - b * hw;
+      const int oh = rr / p.Wo;
+      const int ow = rr - oh * p.Wo;
+      bsrc[i] = (bval[i] ? p.x + ((static_cast<size_t>(b) * p.H + oh * p.stride) * p.W + ow * p.stride) * p.Cin : p.zeros) +
+                c * 8;
+      bih[i] = biw[i] = 0;
     } else {
       const int hw = p.Ho * p.Wo;
       const int b = mm / hw;
@@ -575,6 +586,18 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
       for (int i = 0; i < GB; ++i) {
         glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 4) + i * RPI) * BKS);
         if constexpr (SPLIT) glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
+      }
+    } else if (MODE == 3) {
+      // K order (ky, kx, c): a K-step is a contiguous piece of one kernel row of the patch, i.e. of
+      // one input row (stride == kernel, no padding)
+      const int rowlen = p.KW * p.Cin;
+      const int ky = nx_k0 / rowlen;
+      const long long d = static_cast<long long>(ky) * p.W * p.Cin + (nx_k0 - ky * rowlen);
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const uint16_t* src = bval[i] ? bsrc[i] + d : bsrc[i];
+        glds16(src, Bt + (wave * (BM / 4) + i * RPI) * BKS);
+        if constexpr (SPLIT) glds16(src + bdel[i], Bt + PLANE + (wave * (BM / 4) + i * RPI) * BKS);
       }
     } else {
       const int dy = nx_ky * p.dil, dx = nx_kx * p.dil;
@@ -840,7 +863,25 @@ __global__ __launch_bounds__(256) void conv3x3_spatial_kernel(const ConvArgs p, 
 }
 
 template <int BM, int BN, int STAGES, int BKS = BK>
-void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
+bool launch_glds(int mode, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_per) {
+  const bool mode0 = mode == 0;
+  if (mode == 3) {  // patchify convs (ViT patch embedding): 1- and 2-stage loops only
+    if constexpr (STAGES <= 2) {
+      if (b.split) {
+        if constexpr (STAGES * (BM + BN) * BKS * 4 <= 160 * 1024)
+          hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 3, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
+        else
+          return false;
+      } else if (!b.in_scale) {
+        hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 3, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
+      } else {
+        return false;
+      }
+      return true;
+    } else {
+      return false;
+    }
+  }
   if (b.split) {  // only ring depths whose doubled stages fit the LDS are instantiated
     if constexpr (STAGES * (BM + BN) * BKS * 4 <= 160 * 1024) {
       if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true, BKS>), grid, dim3(256), 0, s, b, kt_per);
@@ -854,6 +895,7 @@ void launch_glds(bool mode0, dim3 grid, hipStream_t s, const ConvArgs& b, int kt
   } else {
     hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
   }
+  return true;
 }
 
 template <int BM, int BN>
@@ -912,7 +954,12 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   if (variant > 0) {  // LDS-DMA pipeline: needs whole 64-wide K-steps of real data
     const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
     const bool mode2 = !dense1x1 && a.Cin % BK == 0;
-    if (!a.zeros || !(mode0 || mode2)) return hipErrorInvalidValue;
+    // patchify (stride == kernel, no padding, a kernel row = whole 64-wide K-steps): dense row pieces
+    const bool mode3 = !dense1x1 && !mode2 && a.KH == a.stride && a.KW == a.stride && a.stride > 1 && a.dil == 1 &&
+                       a.pad_h == 0 && a.pad_w == 0 && (a.KW * a.Cin) % BK == 0 && a.K == a.KH * a.KW * a.Cin &&
+                       a.Kpad == a.K && a.Ho == (a.H - a.KH) / a.stride + 1 && a.Wo == (a.W - a.KW) / a.stride + 1;
+    if (!a.zeros || !(mode0 || mode2 || mode3)) return hipErrorInvalidValue;
+    const int mode = mode0 ? 0 : mode2 ? 2 : 3;
     // ring depth per variant: 2, 3, 4, 6 stages (6 only where it fits the 160 KiB LDS); variant 5 =
     // one stage, no ring.  (Measured and dropped: rings of 32-wide K-steps, conv_glds_kernel<...,
     // BKS = 32>, at the 1-stage footprint, and a 1-stage loop that also touched the next K-step's
@@ -923,15 +970,17 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     const int np = a.split ? 2 : 1;
     const int stages = variant == 1 ? 2 : variant == 2 ? 3 : variant == 3 ? 4 : variant == 4 ? 6 : 1;
     if (stages * kStageBytes * np > 160 * 1024) return hipErrorInvalidValue;
+    bool ok = true;
     switch (variant) {
-      case 1: launch_glds<BM, BN, 2>(mode0, grid, s, b, kt_per); break;
-      case 2: launch_glds<BM, BN, 3>(mode0, grid, s, b, kt_per); break;
-      case 3: launch_glds<BM, BN, 4>(mode0, grid, s, b, kt_per); break;
-      case 5: launch_glds<BM, BN, 1>(mode0, grid, s, b, kt_per); break;
+      case 1: ok = launch_glds<BM, BN, 2>(mode, grid, s, b, kt_per); break;
+      case 2: ok = launch_glds<BM, BN, 3>(mode, grid, s, b, kt_per); break;
+      case 3: ok = launch_glds<BM, BN, 4>(mode, grid, s, b, kt_per); break;
+      case 5: ok = launch_glds<BM, BN, 1>(mode, grid, s, b, kt_per); break;
       default:
-        if constexpr (6 * kStageBytes <= 160 * 1024) launch_glds<BM, BN, 6>(mode0, grid, s, b, kt_per);
+        if constexpr (6 * kStageBytes <= 160 * 1024) ok = launch_glds<BM, BN, 6>(mode, grid, s, b, kt_per);
         else return hipErrorInvalidValue;
     }
+    if (!ok) return hipErrorInvalidValue;
   } else if (a.split) {
     if (dense1x1 && vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 0, 8, true>), grid, dim3(256), 0, s, b, kt_per);
     else if (vec == 8) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 8, true>), grid, dim3(256), 0, s, b, kt_per);

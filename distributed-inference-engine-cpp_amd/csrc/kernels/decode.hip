@@ -105,16 +105,6 @@ __device__ __forceinline__ bool nonblank_all(uint4 q) {
   return any == 0;
 }
 
-__device__ __forceinline__ int block_sum(int v, int* red) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
-}
-
 // exclusive block scan of one int per thread (256 threads)
 __device__ __forceinline__ int block_excl_scan(int v, int* red, int& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -313,3 +313,33 @@ def test_fused_nchw_stem_kernel(native, B, H, W, relu, max_blocks, split):
     torch.cuda.synchronize()
     err = rel_err(got.permute(0, 3, 1, 2), ref)
     assert err < (TOL if split else 8e-3), err
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_patchify_conv_lds_dma_mode(native, split):
+    """Patchify convs (stride == kernel, no padding: the ViT patch embedding) run the LDS-DMA loops
+    with each 64-wide K-step read as a contiguous piece of one input row (MODE 3), 1- and 2-stage."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    B, H, Cin, Cout, k = 3, 48, 4, 128, 16  # 3 x 3 patches per image, M = 27 (an M tail on every tile)
+    g = torch.Generator(device="cuda").manual_seed(29)
+    x = torch.randn(B, Cin, H, H, device="cuda", generator=g)
+    w = torch.randn(Cout, Cin, k, k, device="cuda", generator=g) / (Cin * k * k) ** 0.5
+    bias = torch.randn(Cout, device="cuda", generator=g)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), stride=k).permute(0, 2, 3, 1)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    if not split:
+        xn, w, ref = xn.to(torch.bfloat16), w.to(torch.bfloat16), torch.nn.functional.conv2d(
+            x.to(torch.bfloat16).double(), w.to(torch.bfloat16).double(), bias.double(), stride=k).permute(0, 2, 3, 1)
+    ran = []
+    for cfg in range(K.NUM_CFGS):
+        out, _ = K.conv2d_nhwc(xn, w.float(), bias=bias, stride=k, pad=0, tile=cfg, split=split, out_f32=False)
+        if out is None:
+            continue
+        torch.cuda.synchronize()
+        err = rel_err(out.double(), ref)
+        assert err < (TOL if split else 5e-3), (cfg, err)
+        ran.append(cfg)
+    assert any(4 <= c < 8 for c in ran), ran    # 2-stage LDS-DMA ring
+    assert any(20 <= c < 24 for c in ran), ran  # 1-stage LDS-DMA loop
