@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--dp-force-merge", action="store_true",
                     help="--mode dp at 1 rank: keep the multi-rank merge path (RCCL communicator, collectives)")
     ap.add_argument("--no-dp", action="store_true", help="skip the extra data-parallel (dp_rccl) measurement")
-    ap.add_argument("--dp-steps", type=int, default=0, help="timed steps of the dp_rccl measurement (0 = steps/2)")
+    ap.add_argument("--dp-steps", type=int, default=0, help="timed steps of the dp_rccl measurement (0 = --steps)")
     ap.add_argument("--dp-timeout", type=float, default=240.0, help="watchdog of the dp_rccl measurement (s)")
     args = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
@@ -412,9 +412,9 @@ def _dp_child(args, hg, rank, world):
         port = sk.getsockname()[1]
         sk.close()
     port = hg.broadcast_object(port, src=0)
-    steps = args.dp_steps or max(2, args.steps // 2)
+    steps = args.dp_steps or args.steps  # as long as the headline: a short run is dominated by pacing warm-up noise
     cmd = [sys.executable, os.path.abspath(__file__), "--mode", "dp", "--gpus", str(world), "--steps", str(steps),
-           "--warmup", str(max(1, args.warmup // 2)), "--step-requests", str(args.step_requests),
+           "--warmup", str(max(1, args.warmup)), "--step-requests", str(args.step_requests),
            "--batch", str(args.batch), "--connections", str(args.connections), "--precision", args.precision,
            "--arch", args.arch, "--pipeline-depth", str(args.pipeline_depth), "--dp-backend", "rccl",
            "--device", args.device]
