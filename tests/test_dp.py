@@ -359,3 +359,46 @@ def test_dp_rejects_mismatched_ranks(native, models):
             native.Worker(path, node_id="dpm", max_batch=8, engine={"device": "cpu", "dp_world": 2, "dp_group": group})
     finally:
         out, _ = p.communicate(timeout=60)
+
+
+def test_dp_two_ranks_concurrent_rows_verified(native, models):
+    """Multi-row DP batches merged from BOTH ranks' sub-batches under 32 concurrent connections (CPU
+    engines, host gather): every answer is checked against its own input's logits (rel 1e-4: the CPU
+    executor's summation order depends on the batch it runs in; a swapped row is off by O(1)), so a
+    shard / gather / answer-routing order mix-up shows up as a mismatch -- the flow an N-GPU dp_rccl
+    run executes, with the host collective in place of RCCL."""
+    import socket
+
+    from die_amd.models import resnet_v2 as r
+
+    path, w, cfg = models["tiny"]
+    k = 24
+    x = r.synthetic_input(k, cfg, seed=9).reshape(k, -1)
+    plain = native.Engine(path, device="cpu", max_batch=8)
+    ref = np.concatenate([plain.run(x[i:i + 8]) for i in range(0, k, 8)])
+    plain.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    group = "die_dp_v2_%d" % os.getpid()
+    env = dict(os.environ, DIE_NO_TORCH="1")
+    p = subprocess.Popen([sys.executable, "-c", INGEST_RANK.format(repo=REPO, model=path, rank=1, port=port, mb=8,
+                                                                   world=2, group=group)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=8, cache_capacity=0,
+                           engine={"device": "cpu", "dp_world": 2, "dp_group": group})
+        line = p.stdout.readline().decode()
+        assert "READY" in line, line + p.stdout.read().decode()
+        res = native.loadgen(port=port, connections=32, requests=384, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4, timeout_ms=60000)
+        assert res["ok"] == 384 and res["failed"] == 0, res
+        assert res["verified"] == 384 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        h = wk.health()
+        assert h["engine"]["dp_world"] == 2 and h["engine"]["dp_batches"] < 384
+    finally:
+        if wk is not None:
+            wk.stop()
+        p.communicate(b"stop\n", timeout=120)

@@ -197,3 +197,4 @@ def test_dp_rccl_two_ranks(native, models):
         out, _ = p.communicate(b"stop\n", timeout=120)
     h1 = [json.loads(l[7:]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
     assert h1 and h1[0]["total_requests"] > 0 and h0["total_requests"] > 0
+
