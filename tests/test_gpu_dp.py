@@ -154,6 +154,30 @@ w.stop()
 """
 
 
+def _wait_ready(p, timeout=120.0):
+    """Wait (bounded) for the rank's READY line.  Runtime notes (e.g. libdrm's missing amdgpu.ids on
+    the GPU boxes) can come first, and the rank then waits on stdin, so never read to EOF or block
+    without a deadline: raw reads behind select(), the rank killed if it does not come up."""
+    import select
+    import time
+
+    fd = p.stdout.fileno()
+    buf = b""
+    end = time.time() + timeout
+    while time.time() < end:
+        r, _, _ = select.select([fd], [], [], max(0.0, end - time.time()))
+        if not r:
+            break
+        chunk = os.read(fd, 4096)
+        if not chunk:
+            break
+        buf += chunk
+        if b"READY" in buf:
+            return
+    p.kill()
+    raise AssertionError("rank never became ready: " + buf.decode(errors="replace")[-2000:])
+
+
 def test_dp_rccl_two_ranks(native, models):
     """Two RCCL ranks on two GPUs (skipped on a 1-GPU box: RCCL refuses two ranks on one device):
     the follower's weights arrive by ncclBroadcast, both ranks ingest HTTP on the shared port, and
@@ -182,8 +206,7 @@ def test_dp_rccl_two_ranks(native, models):
     try:
         wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=16, cache_capacity=0,
                            engine={"device": "hip", "dp_world": 2, "dp_group": group, "autotune": False})
-        line = p.stdout.readline().decode()
-        assert "READY" in line, line
+        _wait_ready(p)
         res = native.loadgen(port=port, connections=32, requests=768, verify_inputs=x, verify_expected=ref,
                              verify_tol=1e-4)
         assert res["ok"] == 768 and res["failed"] == 0, res
@@ -198,3 +221,48 @@ def test_dp_rccl_two_ranks(native, models):
     h1 = [json.loads(l[7:]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
     assert h1 and h1[0]["total_requests"] > 0 and h0["total_requests"] > 0
 
+
+RANK1_HOST = RANK1.replace("device_id=1, dp_world=2", "device_id=0, dp_backend='host', dp_world=2")
+
+
+def test_dp_host_two_ranks_one_gpu(native, models):
+    """The multi-rank DP flow with real HIP engines on a 1-GPU box: two ranks (processes) share GPU 0
+    and gather logits + decode status through the host segment (dp_backend "host"; RCCL itself
+    refuses two ranks on one device).  Both ranks ingest HTTP on one port; under 32 concurrent
+    connections the leader merges both ranks' sub-batches into multi-row DP batches sharded over the
+    two engines, and every answer is checked against its own input's expected logits (a shard or
+    gather order mix-up swaps rows and shows up as a mismatch) -- the sharding, merge and answer
+    routing that an N-GPU run executes, minus the RCCL calls."""
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path, w, cfg = models["tiny"]
+    x, ref = _verify_set(native, path, cfg, 24, seed=6, max_batch=16)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    group = "die_gpu_dph2_%d" % os.getpid()
+    p = subprocess.Popen([sys.executable, "-c", RANK1_HOST.format(repo=repo, model=path, port=port, group=group)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=16, cache_capacity=0,
+                           engine={"device": "hip", "dp_world": 2, "dp_group": group, "dp_backend": "host",
+                                   "autotune": False})
+        _wait_ready(p)
+        res = native.loadgen(port=port, connections=32, requests=768, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4, timeout_ms=30000)
+        assert res["ok"] == 768 and res["failed"] == 0, res
+        assert res["verified"] == 768 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        h0 = wk.health()
+        assert h0["engine"]["dp_backend"] == "host" and h0["engine"]["dp_world"] == 2
+        assert h0["engine"]["dp_batches"] < 768  # multi-row batches were merged
+    finally:
+        if wk is not None:
+            wk.stop()
+        out, _ = p.communicate(b"stop\n", timeout=120)
+    h1 = [json.loads(l[7:]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
+    assert h1 and h1[0]["total_requests"] > 0 and h0["total_requests"] > 0
