@@ -164,11 +164,11 @@ struct Mailbox {
   std::atomic<bool> pending{false};  // items waiting: the reactor also checks between events
 
   void post(Item it) {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      if (!open) return;
-      items.push_back(std::move(it));
-    }
+    // the wake-up write stays under the lock: HttpServer::stop() closes efd under it, so a
+    // completion posted while the server stops never writes to a closed (or reused) descriptor
+    std::lock_guard<std::mutex> g(mu);
+    if (!open) return;
+    items.push_back(std::move(it));
     pending.store(true, std::memory_order_release);
     uint64_t one = 1;
     ssize_t r = ::write(efd, &one, sizeof one);
@@ -317,11 +317,12 @@ void HttpServer::stop() {
       std::lock_guard<std::mutex> g(r->box->mu);
       r->box->open = false;
       r->box->items.clear();
+      ::close(r->box->efd);  // under the lock: see Mailbox::post
+      r->box->efd = -1;
     }
     for (auto& kv : r->conns) ::close(kv.second->fd);
     r->conns.clear();
     ::close(r->ep);
-    ::close(r->box->efd);
   }
   reactors_.clear();
   if (listen_fd_ >= 0) ::close(listen_fd_);
