@@ -284,3 +284,30 @@ def test_decode_batch_above_one_launch(native):
         assert st[i] == 0 and nt[i] == 3, (i, st[i], nt[i])
         assert list(v[i]) == [float(i), (i % 7) + 0.5, -float(i), 0.0], (i, v[i])
     assert (st == 0).all()
+
+
+def test_decode_long_tokens_across_lanes_and_chunks(native):
+    """Tokens longer than the 32-byte register window (33-40 chars: many zeros after the point, few
+    significant digits) mixed with short ones over ~30 chunks: they start in one lane's 64-byte
+    region and end in the next, and straddle 4 KiB chunk boundaries (byte-wise LDS path, next-lane
+    and last-token ends).  Bit-exact against the host parser."""
+    from die_amd.ops import kernels as K
+
+    rng = np.random.default_rng(11)
+    parts = []
+    for i in range(12000):
+        v = int(rng.integers(1, 99999999))
+        if i % 3 == 0:
+            parts.append("0." + "0" * int(rng.integers(24, 31)) + str(v))  # 33-40 characters
+        elif i % 3 == 1:
+            parts.append("%.4f" % rng.random())
+        else:
+            parts.append("-%d.%d" % (v % 1000, v % 97))
+    text = ",".join(parts).encode()
+    vals, status, ntok = K.decode_json_numbers([text], len(parts))
+    hv, hn = _host(native, text, len(parts))
+    assert int(ntok[0]) == hn == len(parts)
+    st = int(status[0])
+    assert st in (0, 1)  # 1: a double-rounding hazard sent the sample to the host parser
+    if st == 0:
+        np.testing.assert_array_equal(vals.cpu().numpy()[0].view(np.uint32), hv.view(np.uint32))
