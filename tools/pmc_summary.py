@@ -20,6 +20,7 @@ usage: pmc_summary.py gpurun_out/r10/resnet50 [--title T]
 import argparse
 import csv
 import os
+import re
 from collections import OrderedDict, defaultdict
 
 SIMDS, CUS, XCDS = 1024, 256, 8  # GRBM_GUI_ACTIVE comes back summed over the 8 XCDs' GRBMs
@@ -56,7 +57,9 @@ def main():
     passes = [load(os.path.join(a.dir, p)) for p in ("p1", "p2", "p3", "p4") if os.path.isdir(os.path.join(a.dir, p))]
     n = min(len(p) for p in passes)
     lines = ["# rocprofv3 PMC counters: %s" % (a.title or os.path.basename(a.dir.rstrip("/"))), "",
-             "One eager forward at batch 32 (%s), counters from 4 separate" % a.note,
+             "One eager forward%s (%s), counters from 4 separate" % (
+                 (" at batch " + re.search(r"B=(\d+)", a.title).group(1)) if re.search(r"B=(\d+)", a.title) else "",
+                 a.note),
              "`rocprofv3 --kernel-trace --pmc` passes joined by dispatch order. Derived formulas: see tools/pmc_summary.py.",
              "", "| # | kernel | grid | VGPR/AGPR | LDS B | us | MfmaUtil % | Occ % | HBM GB/s (est) | L2 hit % | LDS conf/instr | park/stall/issue % | LDS-issue % |",
              "|---:|---|---:|---|---:|---:|---:|---:|---:|---:|---:|---|---:|"]
