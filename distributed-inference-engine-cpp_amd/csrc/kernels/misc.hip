@@ -110,15 +110,15 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
   }
 }
 
-// Grid: (C/8 groups / 16, B) blocks of 256 threads = 16 channel groups x 16 row-slices.  ResNet50's
+// Grid: (C/8 groups / 8, B) blocks of 256 threads = 8 channel groups x 32 row-slices.  ResNet50's
 // head (B~20, 7x7x2048) gets 16x more blocks than one-block-per-64-groups and each thread issues
 // its ~3 16-byte loads back to back, so the 4 MB read is not latency-bound on ~80 blocks.
 __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
                            const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
                            const long long* __restrict__ live, int split) {
   const long long xplane = static_cast<long long>(gridDim.y) * HW * C, oplane = static_cast<long long>(gridDim.y) * C;
-  constexpr int G = 16, S = 16;
-  __shared__ float part[S][G][9];  // +1 pad: the reduction reads 16 slices of one group
+  constexpr int G = 8, S = 32;
+  __shared__ float part[S][G][9];  // +1 pad: the reduction reads S slices of one group
   const int b = blockIdx.y;
   if (live && b >= *live) return;  // whole block: before any barrier
   const int gl = threadIdx.x % G, slice = threadIdx.x / G;
@@ -255,7 +255,7 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
                           int relu, int B, int HW, int C, hipStream_t s, const long long* live, int split) {
   if (C % 8) return hipErrorInvalidValue;
   const int CG = C / 8;
-  dim3 grid((CG + 15) / 16, B);
+  dim3 grid((CG + 7) / 8, B);  // 8 channel groups x 32 pixel slices per block
   hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split);
   return hipGetLastError();
 }
