@@ -89,6 +89,8 @@ def main():
                     help="pacing lead: 1 = measured input path + adaptive margin; other values = input path x this")
     ap.add_argument("--branch-streams", action="store_true",
                     help="run the projection-shortcut convs on a side stream (measured slower; off by default)")
+    ap.add_argument("--no-fuse-pairs", action="store_true",
+                    help="keep ResNet's expand and next reduce convs as two launches (EngineOptions::fuse_pairs)")
     ap.add_argument("--no-pack-text", action="store_true",
                     help="upload input text as-is instead of 4-bit packed (device decode)")
     ap.add_argument("--no-device-decode", action="store_true",
@@ -164,7 +166,7 @@ def main():
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                    "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
-                   "device_decode": not args.no_device_decode}
+                   "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs}
     if args.mode in ("gateway", "http"):
         t_init = time.perf_counter()
         wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,

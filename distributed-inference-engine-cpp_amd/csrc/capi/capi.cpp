@@ -96,6 +96,7 @@ EngineOptions engine_opts(const Json& j) {
   e.pace_lead_scale = jget<double>(j, "pace_lead_scale", e.pace_lead_scale);
   e.completion_poll_us = jget<int>(j, "completion_poll_us", e.completion_poll_us);
   e.bn_on_load = jget<bool>(j, "bn_on_load", e.bn_on_load);
+  e.fuse_pairs = jget<bool>(j, "fuse_pairs", e.fuse_pairs);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);

@@ -80,6 +80,40 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
   }
 }
 
+// geometry JSON: M, K1, N1, N2, relu, relu2, split, wplane1, wplane2, zeros
+int die_kern_conv_pair(const char* geom, uint64_t x, uint64_t w1, uint64_t bias1, uint64_t res, uint64_t xout,
+                       uint64_t scale2, uint64_t shift2, uint64_t w2, uint64_t bias2, uint64_t out, uint64_t stream) {
+  try {
+    Json j = Json::parse(geom);
+    kern::PairArgs a;
+    a.M = geti(j, "M", 0);
+    a.K1 = geti(j, "K1", 64);
+    a.N1 = geti(j, "N1", 256);
+    a.N2 = geti(j, "N2", 64);
+    a.relu = geti(j, "relu", 1);
+    a.relu2 = geti(j, "relu2", 1);
+    a.split = geti(j, "split", 0);
+    if (auto* v = j.find("wplane1")) a.wplane1 = v->as_int();
+    if (auto* v = j.find("wplane2")) a.wplane2 = v->as_int();
+    if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
+    a.x = P<const uint16_t>(x);
+    a.w1 = P<const uint16_t>(w1);
+    a.bias1 = P<const float>(bias1);
+    a.res = P<const uint16_t>(res);
+    a.xout = P<uint16_t>(xout);
+    a.scale2 = P<const float>(scale2);
+    a.shift2 = P<const float>(shift2);
+    a.w2 = P<const uint16_t>(w2);
+    a.bias2 = P<const float>(bias2);
+    a.out = P<uint16_t>(out);
+    return static_cast<int>(kern::conv_pair(a, S(stream)));
+  } catch (...) {
+    return -1;
+  }
+}
+
+int die_pair_permute_row(int n) { return kern::pair_permute_row(n); }
+
 int die_kern_input_prep(uint64_t x, uint64_t scale, uint64_t shift, uint64_t out, int B, int C, int H, int W, int Cp,
                         uint64_t stream, int split) {
   return static_cast<int>(kern::input_prep(P<const float>(x), P<const float>(scale), P<const float>(shift),
@@ -229,9 +263,9 @@ char* die_plan_report(const char* model_path, int split, char** err) {
 }
 
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
-char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, char** err) {
+char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse_pairs, char** err) {
   try {
-    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0);
+    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, fuse_pairs != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -243,7 +277,8 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
       Json e = Json::object();
       static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                     "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                    "rows_prep", "copy_cols", "binary", "unary"};
+                                    "rows_prep", "copy_cols", "binary", "unary", "conv_pair"};
+      static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::CONV_PAIR + 1, "one name per PlanOp kind");
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;
@@ -272,6 +307,15 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["store_main"] = o.out >= 0 || o.out_f32 != -1;
         e["relu2"] = o.conv.relu2;
         e["act"] = o.conv.relu;
+        e["rows"] = o.conv.Ho * o.conv.Wo;
+      }
+      if (o.kind == PlanOp::CONV_PAIR) {
+        e["K1"] = o.conv.K;
+        e["N1"] = o.conv.N;
+        e["N2"] = o.n2;
+        e["residual"] = o.in2 >= 0;
+        e["store_main"] = o.out >= 0;
+        e["relu"] = o.pair_relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
       }
       ops.push_back(e);

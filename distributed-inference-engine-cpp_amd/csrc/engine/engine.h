@@ -225,6 +225,7 @@ struct EngineOptions {
   double pace_lead_scale = 1.0;   // != 1: pacing lead = measured input time x this (< 1 dispatches later)
   int completion_poll_us = 0;     // > 0: sleep-poll each batch's D2H event instead of hipEventSynchronize
   bool bn_on_load = false;        // bf16 plans: next unit's BN+ReLU applied on the 1x1 conv operand load
+  bool fuse_pairs = true;         // expand conv + next reduce conv -> one CONV_PAIR launch (kernels/conv_pair.hip)
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)

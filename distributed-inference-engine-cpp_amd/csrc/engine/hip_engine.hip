@@ -61,7 +61,8 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     onnx::Model model = onnx::load_onnx(path);
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
-    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load);
+    plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
+                       opt.fuse_pairs);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -1032,7 +1033,7 @@ class HipEngine : public Engine {
         case PlanOp::BINARY:
           e = kern::binary_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
                                 static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, op.rows_per_sample,
-                                op.S, op.gidx, op.act, op.clip_lo, op.clip_hi, st, live, sp_);
+                                op.S, op.gidx, op.act, op.clip_lo, op.clip_hi, st, live, sp_, op.Cp);
           break;
         case PlanOp::UNARY:
           e = kern::unary_rows(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
@@ -1049,6 +1050,33 @@ class HipEngine : public Engine {
           if (side) a.counters = counters_side_;
           if (!t.fused) a.counters = nullptr;
           e = kern::conv_igemm(a, t.tile, st);
+          break;
+        }
+        case PlanOp::CONV_PAIR: {
+          kern::PairArgs a;
+          a.x = static_cast<const uint16_t*>(buf(op.in));
+          a.w1 = reinterpret_cast<const uint16_t*>(params_ + op.w_off);
+          a.bias1 = prm(op.bias_off);
+          a.res = static_cast<const uint16_t*>(buf(op.in2));
+          a.xout = static_cast<uint16_t*>(buf(op.out));
+          a.scale2 = prm(op.s2_off);
+          a.shift2 = prm(op.b2_off);
+          a.relu2 = op.conv.relu2;
+          a.w2 = reinterpret_cast<const uint16_t*>(params_ + op.w2_off);
+          a.bias2 = prm(op.bias2_off);
+          a.relu = op.pair_relu;
+          a.out = static_cast<uint16_t*>(buf(op.out2));
+          a.M = B * op.conv.Ho * op.conv.Wo;
+          a.K1 = op.conv.K;
+          a.N1 = op.conv.N;
+          a.N2 = op.n2;
+          a.rows_per_sample = op.conv.Ho * op.conv.Wo;
+          a.live = live;
+          a.zeros = zeros_;
+          a.split = sp_;
+          a.wplane1 = op.conv.wplane;
+          a.wplane2 = op.w2plane;
+          e = kern::conv_pair(a, st);
           break;
         }
         case PlanOp::POOL:
@@ -1182,7 +1210,9 @@ class HipEngine : public Engine {
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
-                                  "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax"};
+                                  "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
+                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair"};
+    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::CONV_PAIR + 1, "one name per PlanOp kind");
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

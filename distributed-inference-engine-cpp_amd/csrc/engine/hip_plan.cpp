@@ -79,8 +79,9 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 
 class Planner {
  public:
-  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load)
-      : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load) {}
+  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true)
+      : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
+        fuse_pairs_(fuse_pairs) {}
 
   // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
   // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
@@ -120,6 +121,7 @@ class Planner {
     if (!report_.supported) throw std::runtime_error("HIP engine cannot lower this graph:\n" + report_.text());
     finalize_output();
     fuse_pool_affine();
+    if (fuse_pairs_) fuse_conv_pairs();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
@@ -1668,6 +1670,7 @@ class Planner {
     p.clip_lo = lo;
     p.clip_hi = hi;
     p.C = a.C;
+    p.Cp = a.logical();  // pad columns are written 0 (Div of two zero pads would be NaN)
     p.rows_per_sample = rows_of(a);
     p.out = new_buf(static_cast<size_t>(rows_of(a)) * a.C * 2);
     Val o = a;
@@ -1919,6 +1922,70 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
+  // Back-to-back 1x1 pair (ResNet-v2 bottleneck boundary).  A dual-store expand conv P writes the
+  // raw sum x (next residual) and a = act(bn(x)); when a's ONLY reader is a plain 1x1/s1 reduce conv
+  // Q, both become one CONV_PAIR op at P's position (Q has no other input, so computing it early is
+  // safe) and `a` is never stored: kernels/conv_pair.hip consumes it from LDS.  Rows of both weight
+  // matrices are permuted in place (kern::pair_permute_row) -- P and Q exist only inside the pair.
+  void permute_weight_rows(size_t off, int rows, int kpad, long long plane) {
+    const int planes = plane > 0 ? 2 : 1;
+    std::vector<uint16_t> tmp(static_cast<size_t>(rows) * kpad);
+    for (int pl = 0; pl < planes; ++pl) {
+      uint16_t* w = reinterpret_cast<uint16_t*>(plan_.params.data() + off) + static_cast<size_t>(pl) * plane;
+      std::memcpy(tmp.data(), w, tmp.size() * 2);
+      for (int n = 0; n < rows; ++n)
+        std::memcpy(w + static_cast<size_t>(kern::pair_permute_row(n)) * kpad, tmp.data() + static_cast<size_t>(n) * kpad,
+                    static_cast<size_t>(kpad) * 2);
+    }
+  }
+  static bool plain_1x1(const kern::ConvArgs& c) {
+    return c.KH == 1 && c.KW == 1 && c.stride == 1 && c.pad_h == 0 && c.pad_w == 0 && c.dil == 1 && c.H == c.Ho &&
+           c.W == c.Wo && c.K == c.Cin && c.Kpad == c.K;
+  }
+  void fuse_conv_pairs() {
+    std::vector<int> readers(plan_.bufs.size(), 0), reader_op(plan_.bufs.size(), -1);
+    const int nops = static_cast<int>(plan_.ops.size());
+    for (int i = 0; i < nops; ++i)
+      for (int b : {plan_.ops[i].in, plan_.ops[i].in2, plan_.ops[i].in3})
+        if (b >= 0) {
+          readers[b]++;
+          reader_op[b] = i;
+        }
+    std::vector<bool> drop(nops, false);
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind != PlanOp::CONV || p.in2 < 0 || p.out2 < 0 || p.s2_off == SIZE_MAX || p.out_f32 >= 0 ||
+          p.conv.relu != 0 || p.in_scale_off != SIZE_MAX || !plain_1x1(p.conv) || p.join >= 0)
+        continue;
+      if (readers[p.out2] != 1) continue;
+      const int j = reader_op[p.out2];
+      if (j <= i || drop[j]) continue;
+      const PlanOp& q = plan_.ops[j];
+      if (q.kind != PlanOp::CONV || q.in != p.out2 || q.in2 >= 0 || q.in3 >= 0 || q.out < 0 || q.out2 >= 0 ||
+          q.out_f32 >= 0 || q.conv.relu > 1 || q.in_scale_off != SIZE_MAX || !plain_1x1(q.conv) ||
+          q.conv.Cin != p.conv.N || q.conv.H != p.conv.Ho || q.conv.W != p.conv.Wo || q.join >= 0 ||
+          !kern::conv_pair_supported(p.conv.K, p.conv.N, q.conv.N))
+        continue;
+      permute_weight_rows(p.w_off, static_cast<int>(round_up(p.conv.N, 128)), p.conv.Kpad, p.conv.wplane);
+      permute_weight_rows(q.w_off, static_cast<int>(round_up(q.conv.N, 128)), q.conv.Kpad, q.conv.wplane);
+      p.kind = PlanOp::CONV_PAIR;
+      p.name += "+" + q.name;
+      p.w2_off = q.w_off;
+      p.bias2_off = q.bias_off;
+      p.w2plane = q.conv.wplane;
+      p.n2 = q.conv.N;
+      p.pair_relu = q.conv.relu;
+      p.out2 = q.out;  // the pre-activation buffer is dropped (no op references it any more)
+      p.flops_per_sample += q.flops_per_sample;
+      drop[j] = true;
+    }
+    std::vector<PlanOp> out;
+    out.reserve(plan_.ops.size());
+    for (int i = 0; i < nops; ++i)
+      if (!drop[i]) out.push_back(std::move(plan_.ops[i]));
+    plan_.ops = std::move(out);
+  }
+
   // Pre-activation on load (opt-in, EngineOptions::bn_on_load).  A dual-store conv writes x (the raw sum: next residual) AND
   // a = act(bn(x)) (the next unit's input).  When every reader of `a` is a 1x1 conv the LDS-DMA
   // loop can run (K = Cin <= 2048, Cin % 64 == 0), those convs read x and apply bn+act to their
@@ -2035,6 +2102,7 @@ class Planner {
   bool side_branches_ = false;
   bool split_ = false;  // fp32 mode: split (hi, lo) activations and weights
   bool bn_on_load_ = false;  // EngineOptions::bn_on_load (bf16 plans only)
+  bool fuse_pairs_ = true;   // EngineOptions::fuse_pairs
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -2049,14 +2117,14 @@ class Planner {
 std::string Plan::summary() const {
   std::ostringstream os;
   size_t convs = 0;
-  for (auto& o : ops) convs += o.kind == PlanOp::CONV || o.kind == PlanOp::STEM;
+  for (auto& o : ops) convs += o.kind == PlanOp::CONV || o.kind == PlanOp::STEM || o.kind == PlanOp::CONV_PAIR;
   os << ops.size() << " device ops (" << convs << " MFMA conv/gemm), arena " << arena_bytes / (1 << 20) << " MiB, params "
      << params.size() / (1 << 20) << " MiB, " << flops_per_sample / 1e9 << " GFLOP/sample";
   return os.str();
 }
 
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load) {
-  return Planner(m, max_batch, side_branches, split, bn_on_load).run();
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs) {
+  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs).run();
 }
 
 std::string PlanReport::text() const {

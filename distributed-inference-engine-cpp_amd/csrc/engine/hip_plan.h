@@ -43,7 +43,10 @@ struct PlanOp {
     ROWS_PREP,  // rank-2/3 graph input: f32 [rows][C] -> bf16 rows [rows][Cp]
     COPY_COLS,  // out[:, col[1] + j] = in[:, col[0] + j], j < C (concat / slice); pitches ld[0], ld[1]
     BINARY,     // out = act(in (op gidx) in2); S = 0: same shape, 1: in2 = one row per sample
-    UNARY       // out = act(in * scale + shift) with any activation code
+    UNARY,      // out = act(in * scale + shift) with any activation code
+    // ResNet-v2 bottleneck boundary in one launch (kernels/conv_pair.hip): a dual-store 1x1 expand
+    // conv fused with the 1x1 reduce conv that is the sole reader of its pre-activation output
+    CONV_PAIR
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
@@ -74,6 +77,13 @@ struct PlanOp {
   // CONV: pre-activation on load (ConvArgs::in_scale/in_shift/in_relu), parameter offsets
   size_t in_scale_off = SIZE_MAX, in_shift_off = SIZE_MAX;
   int in_relu = 0;
+  // CONV_PAIR: in = expand input [M][K1], in2 = residual, out = raw sum x (-1: not stored), out2 =
+  // reduce output [M][n2]; conv/w_off/bias_off/s2_off/b2_off describe the expand conv and the BN of
+  // the pre-activation, w2_off/bias2_off/w2plane/pair_relu the reduce conv.  Both weight matrices
+  // have their rows permuted by kern::pair_permute_row.
+  size_t w2_off = 0, bias2_off = SIZE_MAX;
+  long long w2plane = 0;
+  int n2 = 0, pair_relu = 0;
 };
 
 struct Plan {
@@ -95,8 +105,9 @@ struct Plan {
 // Build the plan for batches up to max_batch.  Throws on unsupported graphs, listing EVERY node
 // the engine cannot lower (not only the first).  side_branches: mark independent convs to run on
 // a second stream (PlanOp::join; extends their inputs' lifetimes).  split: fp32 mode (Plan::split).
+// fuse_pairs: lower expand -> reduce 1x1 conv pairs to CONV_PAIR ops (EngineOptions::fuse_pairs).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
-                bool bn_on_load = false);
+                bool bn_on_load = false, bool fuse_pairs = true);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

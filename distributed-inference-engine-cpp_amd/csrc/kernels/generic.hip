@@ -100,7 +100,8 @@ __device__ __forceinline__ float apply_act(float v, int act, float a, float b) {
 // op: 0 add, 1 sub, 2 mul, 3 div.
 __global__ void binary_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ y, uint16_t* __restrict__ out,
                               long long R, int C, long long rows_per_sample, int ymode, int op, int act, float a,
-                              float b, long long plane, long long yplane, const long long* __restrict__ live, int split) {
+                              float b, long long plane, long long yplane, const long long* __restrict__ live, int split,
+                              int Cl) {
   long long Rl = R;
   if (live) Rl = min(R, *live * rows_per_sample);
   const int G = C / 8;
@@ -116,7 +117,7 @@ __global__ void binary_kernel(const uint16_t* __restrict__ x, const uint16_t* __
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float v = op == 0 ? u[t] + w[t] : op == 1 ? u[t] - w[t] : op == 2 ? u[t] * w[t] : u[t] / w[t];
-      u[t] = apply_act(v, act, a, b);
+      u[t] = c + t < Cl ? apply_act(v, act, a, b) : 0.f;  // pad columns stay 0 (finite)
     }
     store8v(out + r * C + c, plane, split != 0, u);
   }
@@ -200,12 +201,14 @@ hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uin
 }
 
 hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
-                       int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live, int split) {
-  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 3) return hipErrorInvalidValue;
+                       int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live, int split,
+                       int Cl) {
+  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 3 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+  if (Cl == 0) Cl = C;
   const long long plane = R * C;
   const long long yplane = ymode == 1 ? (R / rows_per_sample) * C : plane;
   hipLaunchKernelGGL(binary_kernel, dim3(grid_for(R * (C / 8))), dim3(256), 0, s, x, y, out, R, C, rows_per_sample,
-                     ymode, op, act, a, b, plane, yplane, live, split);
+                     ymode, op, act, a, b, plane, yplane, live, split, Cl);
   return hipGetLastError();
 }
 

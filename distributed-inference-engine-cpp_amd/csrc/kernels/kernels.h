@@ -144,9 +144,11 @@ hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uin
                      int coly, long long R, int ncols, hipStream_t s, int split = 0);
 // out = act(x op y) over [R][C] rows; ymode 0: y same shape; 1: y one row per sample (broadcast over
 // its rows_per_sample rows).  op 0 add, 1 sub, 2 mul, 3 div.  act codes as unary_rows.
+// Cl (0 = C): logical channels; the pad columns [Cl, C) are written 0, whatever the op gives for
+// them (Div of two zero pads is NaN, and NaN * 0 would poison the next GEMM's every output).
 hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
                        int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live = nullptr,
-                       int split = 0);
+                       int split = 0, int Cl = 0);
 // y = act(x * scale[c] + shift[c]) (scale/shift nullable); act 0 none, 1 ReLU, 2 GELU (erf),
 // 3 Clip(a, b), 4 sigmoid, 5 tanh, 6 leaky ReLU (slope a).
 hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, long long R, int C,
@@ -162,6 +164,47 @@ hipError_t nhwc_to_nchw_f32(const uint16_t* x, float* y, int B, int H, int W, in
 // f32 -> bf16 / bf16 -> f32 copies
 hipError_t f32_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 hipError_t bf16_to_f32(const uint16_t* x, float* y, long long n, hipStream_t s, int split = 0);
+
+// Back-to-back 1x1 GEMM pair of a ResNet-v2 bottleneck boundary (conv_pair.hip), one launch:
+//   v   = x · W1ᵀ + bias1 + res                 (unit u's expand conv + shortcut; [M][N1])
+//   xout = v                                    (the raw sum: unit u+1's residual; optional)
+//   a   = act2(v * scale2 + shift2)             (unit u+1's pre-activation BN+ReLU; never stored)
+//   out = act(a · W2ᵀ + bias2)                  (unit u+1's reduce conv; [M][N2])
+// `a` is produced 64 channels at a time in LDS and consumed there as one K-step of the second
+// GEMM, so the [M][N1] pre-activation tensor never goes to memory.  Weights [N][K] bf16 (split:
+// hi plane then lo plane, w*plane elements apart) with the rows of every 32-row block PERMUTED
+// (pair_permute_row): each lane's two accumulator fragments then hold 8 consecutive channels,
+// stored as 16-byte vectors without an LDS staging pass.  K1 in {64, 128}, N2 in {64, 128},
+// N1 % 64 == 0, rows of x/res/xout/out dense (ld = K1 / N1 / N1 / N2).
+struct PairArgs {
+  const uint16_t* x = nullptr;
+  const uint16_t* w1 = nullptr;
+  const float* bias1 = nullptr;
+  const uint16_t* res = nullptr;
+  uint16_t* xout = nullptr;
+  const float* scale2 = nullptr;
+  const float* shift2 = nullptr;
+  int relu2 = 1;
+  const uint16_t* w2 = nullptr;
+  const float* bias2 = nullptr;
+  int relu = 1;
+  uint16_t* out = nullptr;
+  int M = 0, K1 = 64, N1 = 256, N2 = 64;
+  int rows_per_sample = 1;            // for `live`
+  const long long* live = nullptr;
+  const uint16_t* zeros = nullptr;    // zero page >= K1 + 64 elements (M-tail rows)
+  int split = 0;
+  long long wplane1 = 0, wplane2 = 0;
+};
+// Physical row of logical output channel n in a pair weight matrix (a permutation inside each
+// block of 32 rows; the inverse maps physical -> logical).
+inline int pair_permute_row(int n) {
+  const int b = n & ~31, r = n & 31;  // logical r = 8g + 4h + t  ->  physical 16h + 4g + t
+  const int g = r >> 3, h = (r >> 2) & 1, t = r & 3;
+  return b + 16 * h + 4 * g + t;
+}
+bool conv_pair_supported(int K1, int N1, int N2);
+hipError_t conv_pair(const PairArgs& a, hipStream_t s);
 
 // 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:
 // w = [64][224] bf16 with k = ky*32 + kx*4 + c (kx padded to 8), out = act(conv + bias) NHWC bf16.

@@ -11,6 +11,8 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
 * `se_cnn`    an image CNN with 12 input channels (> 8), odd channel counts, a squeeze-excitation
               gate (GAP -> FC -> ReLU -> FC -> Sigmoid -> broadcast Mul), channel Concat and
               Slice, and a Flatten of a 4x4 map (NCHW order) into the classifier.
+* `ratio_mlp` a Div of two activations of width 10 (stored with 16 channels) feeding a Gemm: the
+              pad columns of both operands are 0, so 0/0 must not reach the next GEMM.
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -27,6 +29,7 @@ SPECS = {
     "mlp": dict(in_features=300, hidden=(100, 60, 36), classes=10),
     "bert": dict(seq=32, dim=128, heads=2, ffn=256, layers=2, classes=3),
     "se_cnn": dict(in_ch=12, image=16, classes=10),
+    "ratio_mlp": dict(in_features=40, hidden=10, classes=5),
 }
 
 
@@ -175,7 +178,28 @@ def build_se_cnn(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.nd
     return g.model_proto(opset=opset), {}
 
 
-BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn}
+def build_ratio_mlp(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["ratio_mlp"]
+    rng = _rng(seed)
+    g = GraphBuilder(name="ratio_mlp")
+    x = g.input("features", ["N", s["in_features"]])
+    F, Hd = s["in_features"], s["hidden"]
+
+    def fc(inp, name, fin, fout):
+        w = g.init(name + ".weight", _lin(rng, fin, (fout, fin)))
+        b = g.init(name + ".bias", (0.1 * rng.standard_normal(fout)).astype(np.float32))
+        return g.node("Gemm", [inp, w, b], name=name, transB=1)
+
+    num = g.node("Tanh", [fc(x, "num", F, Hd)], name="num_tanh")                       # pad columns 0
+    den = g.node("Relu", [fc(x, "den", F, Hd)], name="den_relu")                       # pad columns 0
+    den = g.node("Add", [den, g.const(np.array(1.0, np.float32), "one")], name="den_shift")  # >= 1, pads 0
+    r = g.node("Div", [num, den], name="ratio")                                        # pads: 0 / 0
+    y = fc(r, "head", Hd, s["classes"])
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
+BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:
@@ -184,7 +208,7 @@ def build_onnx(name: str, seed: int = 0) -> bytes:
 
 def input_shape(name: str):
     s = SPECS[name]
-    if name == "mlp":
+    if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
     if name == "bert":
         return (s["seq"] * s["dim"],)

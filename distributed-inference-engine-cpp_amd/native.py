@@ -615,10 +615,14 @@ def _sig_kernels():
         return L
     u64, i = C.c_uint64, C.c_int
     L.die_plan_summary.restype = C.c_void_p
-    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.die_plan_summary.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.die_kern_conv.restype = i
     L.die_kern_conv.argtypes = [C.c_char_p] + [u64] * 9 + [i, u64]
     L.die_kern_input_prep.restype = i
+    L.die_kern_conv_pair.restype = i
+    L.die_kern_conv_pair.argtypes = [C.c_char_p] + [u64] * 11
+    L.die_pair_permute_row.restype = i
+    L.die_pair_permute_row.argtypes = [i]
     L.die_kern_input_prep.argtypes = [u64] * 4 + [i] * 5 + [u64, i]
     L.die_kern_pool2d.restype = i
     L.die_kern_pool2d.argtypes = [u64, u64] + [i] * 14 + [u64, i]
@@ -655,11 +659,13 @@ def _sig_kernels():
 
 
 def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False,
-                 precision: str = "bf16") -> Dict[str, Any]:
-    """precision "fp32" plans the split (hi, lo) kernels of the HIP engine's default mode."""
+                 precision: str = "bf16", fuse_pairs: bool = True) -> Dict[str, Any]:
+    """precision "fp32" plans the split (hi, lo) kernels of the HIP engine's default mode.
+    fuse_pairs: expand + next reduce 1x1 convs as one conv_pair op (EngineOptions::fuse_pairs)."""
     L = _sig_kernels()
     err = _err_box()
-    p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), int(precision == "fp32"), C.byref(err))
+    p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), int(precision == "fp32"),
+                           int(fuse_pairs), C.byref(err))
     if not p:
         _raise_if(err, "plan")
     return json.loads(_take_str(p))

@@ -160,6 +160,58 @@ def conv2d_nhwc(x_nhwc, w, bias=None, stride=1, pad=0, dil=1, relu=False, res=No
     return pr.results()
 
 
+def pair_permute(n_rows: int):
+    """Row permutation of conv_pair weights (kernels.h pair_permute_row): physical row of logical n."""
+    perm = []
+    for n in range(n_rows):
+        b, r = n & ~31, n & 31
+        g, h, t = r >> 3, (r >> 2) & 1, r & 3
+        perm.append(b + 16 * h + 4 * g + t)
+    return perm
+
+
+def _pack_pair_weight(w, split):
+    """[N, K] float -> rows permuted by pair_permute, N padded to 128, bf16 or split planes."""
+    import torch
+
+    n, k = w.shape
+    npad = (n + 127) // 128 * 128
+    full = torch.zeros((npad, k), dtype=torch.float32, device=w.device)
+    perm = torch.tensor(pair_permute(n), device=w.device)
+    full[perm] = w.float()
+    return split_planes(full) if split else full.to(torch.bfloat16)
+
+
+def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False, store_x=True):
+    """Fused expand + next-reduce 1x1 pair (kernels/conv_pair.hip) over rows.
+    y [M, K1], w1 [N1, K1], b1 [N1], res [M, N1], s2/h2 [N1], w2 [N2, N1], b2 [N2] (float).
+    Returns (x, out): x = y @ w1.T + b1 + res  [M, N1] (None unless store_x) and
+    out = act(act2(x * s2 + h2) @ w2.T + b2)  [M, N2], as fp32 (split planes joined) or bf16."""
+    import torch
+
+    M, K1 = y.shape
+    N1, N2 = w1.shape[0], w2.shape[0]
+    dev = y.device
+    np_ = (2,) if split else ()
+    yy = _in(y, split)
+    rr = _in(res, split)
+    wp1 = _pack_pair_weight(w1, split)
+    wp2 = _pack_pair_weight(w2, split)
+    f = lambda v: v.float().contiguous()
+    xo = torch.empty(np_ + (M, N1), dtype=torch.bfloat16, device=dev) if store_x else None
+    out = torch.empty(np_ + (M, N2), dtype=torch.bfloat16, device=dev)
+    zeros = torch.zeros(4096, dtype=torch.int16, device=dev)
+    g = dict(M=M, K1=K1, N1=N1, N2=N2, relu=int(relu), relu2=int(relu2), split=int(split), zeros=int(zeros.data_ptr()))
+    if split:
+        g.update(wplane1=int(wp1[0].numel()), wplane2=int(wp2[0].numel()))
+    bb1, ss2, hh2, bb2 = f(b1), f(s2), f(h2), f(b2)
+    rc = native.kernels().die_kern_conv_pair(json.dumps(g).encode(), _ptr(yy), _ptr(wp1), _ptr(bb1), _ptr(rr),
+                                             _ptr(xo), _ptr(ss2), _ptr(hh2), _ptr(wp2), _ptr(bb2), _ptr(out),
+                                             _stream())
+    _check(rc, "conv_pair")
+    return (None if xo is None else _out(xo, split)), _out(out, split)
+
+
 def _in(x, split):
     return split_planes(x) if split else x.contiguous()
 

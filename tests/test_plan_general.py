@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp"]
 
 
 @pytest.fixture(scope="module")

@@ -64,10 +64,11 @@ case "$TASK" in
         bench "${n}_$r" $a || exit 1
       done
     done ;;
-  ops)
-    timeout -k 10 300 python3 -u tools/op_profile.py --arch "$1" --batch "$2" --precision "$3" --out "$O/ops_$1_$3_b$2" \
-      > "$O/ops.log" 2>&1 || { tail -20 "$O/ops.log"; exit 1; }
-    sed -n 3p "$O/ops_$1_$3_b$2.md" ;;
+  ops)  # ops ARCH B PREC [TAG [op_profile.py args]]
+    A=$1; B=$2; P=$3; T=${4:-}; shift 3; [ $# -gt 0 ] && shift
+    timeout -k 10 300 python3 -u tools/op_profile.py --arch "$A" --batch "$B" --precision "$P" --out "$O/ops_${A}_${P}_b$B$T" "$@" \
+      > "$O/ops$T.log" 2>&1 || { tail -20 "$O/ops$T.log"; exit 1; }
+    sed -n 3p "$O/ops_${A}_${P}_b$B$T.md" ;;
   rocprof)
     n=$1; shift
     cd /tmp && export TMPDIR=/tmp && cd "$R" || exit 1
