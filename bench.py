@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--no-local-shm", action="store_true",
                     help="gateway sends co-located workers the body bytes instead of a shared-memory descriptor")
     ap.add_argument("--model", default="", help="existing ONNX file (default: generate --arch)")
-    ap.add_argument("--arch", choices=["resnet50", "vit_b16"], default="resnet50",
+    ap.add_argument("--arch", choices=["resnet50", "vit_b16", "resnet_tiny"], default="resnet50",
                     help="resnet50 = headline config 2; vit_b16 = BASELINE config 5 (ViT-B/16, batch 32)")
     ap.add_argument("--pipeline-depth", type=int, default=3)
     ap.add_argument("--exec-streams", type=int, default=1, help="batches executing concurrently on the GPU")
@@ -104,6 +104,13 @@ def main():
     ap.add_argument("--no-dp", action="store_true", help="skip the extra data-parallel (dp_rccl) measurement")
     ap.add_argument("--dp-steps", type=int, default=0, help="timed steps of the dp_rccl measurement (0 = --steps)")
     ap.add_argument("--dp-timeout", type=float, default=240.0, help="watchdog of the dp_rccl measurement (s)")
+    ap.add_argument("--verify-every", type=int, default=50,
+                    help="every Nth timed request carries one of 8 fixed inputs whose logits the CPU executor "
+                         "computed beforehand; its answer is checked (0 = off; a mismatch zeroes the value)")
+    ap.add_argument("--no-ring-balance", action="store_true",
+                    help="N>1 gateway mode: ephemeral worker ports instead of ring-balanced ones")
+    ap.add_argument("--no-gateway-bytes", action="store_true",
+                    help="skip the extra pass with bodies re-sent over loopback HTTP (reference gateway hop)")
     args = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         # n_gpus and global_batch come from --gpus: a torchrun launch must say how many ranks it has
@@ -134,6 +141,11 @@ def main():
 
         cfg = r.ViTConfig()
         model_name, fname = "ViT-B/16 (ONNX, generated)", "vit-b16.onnx"
+    elif args.arch == "resnet_tiny":  # multi-rank CPU rehearsals only (tests/test_bench_contract.py)
+        from die_amd.models import resnet_v2 as r
+
+        cfg = r.tiny_config()
+        model_name, fname = "ResNet-v2 tiny (rehearsal)", "resnet-tiny.onnx"
     else:
         from die_amd.models import resnet_v2 as r
 
@@ -161,6 +173,19 @@ def main():
     extra = {}
 
     SR = args.step_requests
+    # Answer verification: K fixed inputs, logits from the CPU executor (fp32, an
+    # independent implementation of the same ONNX graph); the timed pass sends every Nth request as
+    # one of them, with its text zero-padded per request so it is computed, never a cache hit.
+    verify = None
+    if args.verify_every > 0 and args.mode in ("gateway", "http"):
+        import numpy as np
+
+        v4 = r.synthetic_input(8, cfg, seed=4242).astype(np.float32)
+        vx = v4.reshape(8, -1).copy()
+        vx[:, 0], vx[:, 1] = 0.5, 0.75  # plain decimals: the load generator pads them with zeros
+        vref = native.cpu_run(model, vx.reshape(v4.shape)).reshape(8, -1)
+        verify = dict(verify_inputs=vx, verify_expected=vref, verify_every=args.verify_every,
+                      verify_tol=1e-3 if args.precision == "fp32" else 5e-2)
     engine_opts = {"device": args.device, "device_id": dev, "max_batch": B, "precision": args.precision,
                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
@@ -168,9 +193,24 @@ def main():
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs}
     if args.mode in ("gateway", "http"):
+        # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
+        # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with
+        # ~1.5x its fair share of the requests
+        want_port = 0
+        if args.mode == "gateway" and world > 1 and not args.no_ring_balance:
+            from die_amd.parallel import ring_balance as rb
+
+            ports = rb.balanced_ports(world, range(20000, 22000), seed=world) if rank == 0 else None
+            want_port = hg.broadcast_object(ports, src=0)[rank]
         t_init = time.perf_counter()
-        wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
-                           parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
+        try:
+            wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts, port=want_port,
+                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
+        except native.NativeError:
+            if not want_port:
+                raise
+            wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
+                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
         t_ready = time.perf_counter()
         gw = None
         target_port = wk.port
@@ -184,8 +224,10 @@ def main():
                                       read_timeout_ms=5000 if hip else 120000)
             target_port = gw.port
         # every pass and rank gets its own payload seed: no input recurs across the warm-up, timed and
-        # direct passes (cache_hits_timed below proves it)
-        lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4, timeout_ms=60000)
+        # direct passes (cache_hits_timed below proves it); request numbers are printed scrambled
+        # (FNV-1a spreads them over the ring like random ids)
+        lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4, timeout_ms=60000,
+                  scramble_ids=True)
         native.loadgen(port=target_port, requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank,
                        seed=1000 + rank, **lg)
         h0 = wk.health()
@@ -194,7 +236,7 @@ def main():
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank,
-                             seed=2000 + rank, **lg)
+                             seed=2000 + rank, **dict(lg, **(verify or {})))
         barrier()
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
@@ -229,10 +271,18 @@ def main():
             "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()},
             "stages_p99_us": {k: round(v.get("p99_us", 0.0), 1) for k, v in h1.get("stages_us", {}).items()},
             "engine_options": e1.get("options"),
+            # windowed to the timed pass (histogram differences), 8 buckets per octave
+            "stages_window_us": _stage_window(h0.get("stages_us", {}), h1.get("stages_us", {})),
             # host CPU spent per request by this process (client + gateway + worker threads together)
             "cpu_us_per_request": {"user": round((ru1.ru_utime - ru0.ru_utime) * 1e6 / max(1, res["ok"]), 1),
                                    "sys": round((ru1.ru_stime - ru0.ru_stime) * 1e6 / max(1, res["ok"]), 1)},
         }
+        if verify:
+            extra["verify"] = {"every": args.verify_every, "inputs": 8, "oracle": "cpu_executor_fp32",
+                               "tol": verify["verify_tol"], "verified": res.get("verified", 0),
+                               "mismatched": res.get("mismatched", 0), "bad_request_id": res.get("bad_request_id", 0),
+                               "max_rel_err": res.get("max_rel_err")}
+        extra["worker_requests_timed"] = bp1["total_requests"] - bp0["total_requests"]
         if gw:
             extra["gateway"] = {"failovers": g1["failovers"] - g0["failovers"], "failed": g1["failed"] - g0["failed"],
                                 "upstream_connections": g1.get("upstream_connections_opened"),
@@ -241,7 +291,16 @@ def main():
                                 "breakers": [b["state"] for b in g1["circuit_breakers"]],
                                 # per-stage p50/p99 (warm-up included): where a gateway tail comes from
                                 "stages_us": {k: [round(v["p50_us"], 1), round(v["p99_us"], 1)]
-                                              for k, v in g1.get("stages_us", {}).items()}}
+                                              for k, v in g1.get("stages_us", {}).items()},
+                                "stages_window_us": _stage_window(g0.get("stages_us", {}), g1.get("stages_us", {}))}
+            if world > 1:
+                from die_amd.parallel import ring_balance as rb
+
+                names = ["127.0.0.1:%d" % p for p in ports]
+                ids = [x for k in range(world) for x in rb.request_ids("r%d_" % k, args.steps * SR)]
+                extra["ring"] = dict(rb.predict(names, ids), balanced_ports=not args.no_ring_balance,
+                                     ports=list(ports),
+                                     arc_max_over_fair=round(float(rb.arc_shares(names).max() * world), 3))
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()
@@ -257,6 +316,23 @@ def main():
                                       "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"],
                                       "cpu_us_per_request": {"user": round((rd1.ru_utime - rd0.ru_utime) * 1e6 / n_ok, 1),
                                                              "sys": round((rd1.ru_stime - rd0.ru_stime) * 1e6 / n_ok, 1)}}
+        if gw and not args.no_gateway_bytes:
+            # the reference's gateway hop: every body re-sent to the worker over loopback HTTP
+            # (/root/reference/src/gateway.cpp:99-103) instead of a shared-memory descriptor
+            gwb = native.GatewayServer(["127.0.0.1:%d" % p for p in ports], client_threads=args.gw_client_threads,
+                                       local_shm=False, http_threads=args.gw_http_threads,
+                                       read_timeout_ms=5000 if hip else 120000)
+            barrier()
+            tb = time.perf_counter()
+            rb_ = native.loadgen(port=gwb.port, requests=args.steps * SR, warmup=0, id_prefix="b%d_" % rank,
+                                 seed=4000 + rank, **lg)
+            barrier()
+            elb = time.perf_counter() - tb
+            gs = gwb.stats()
+            extra["gateway_bytes"] = {"rps_this_rank": rb_["ok"] / elb, "p50_ms": rb_["latency_ms"]["p50"],
+                                      "p99_ms": rb_["latency_ms"]["p99"], "failed": rb_["failed"],
+                                      "byte_forwards": gs.get("byte_forwards", 0), "shm_forwards": gs.get("shm_forwards", 0)}
+            gwb.stop()
         if gw:
             gw.stop()
         wk.stop()
@@ -344,7 +420,7 @@ def main():
         mine = {"rank": rank, "requests_per_s": round(ok / elapsed, 1) if elapsed > 0 else None,
                 "elapsed_s": round(elapsed, 3), "failed": failed}
         for k in ("p50_ms", "p99_ms", "avg_batch", "avg_dp_batch", "device_ms_per_batch", "device_busy_frac",
-                  "gpu_gap_ms_per_batch", "cpu_us_per_request", "requests_parsed_this_rank"):
+                  "gpu_gap_ms_per_batch", "cpu_us_per_request", "requests_parsed_this_rank", "worker_requests_timed"):
             if extra.get(k) is not None:
                 mine[k] = extra[k]
         if isinstance(extra.get("direct_worker"), dict):
@@ -352,11 +428,29 @@ def main():
         mine["numa_cpus"] = numa.get("cpu_share") if isinstance(numa, dict) else None
         per_rank = hg.all_gather_object(mine)
         if rank == 0:
+            tot = sum(x.get("worker_requests_timed", 0) for x in per_rank)
+            for x in per_rank:  # measured ring share of each rank's worker (ring.shares: predicted)
+                if tot and "worker_requests_timed" in x:
+                    x["worker_share"] = round(x["worker_requests_timed"] / tot, 4)
             extra["per_rank"] = per_rank
+        if isinstance(extra.get("verify"), dict):
+            v = extra["verify"]
+            v["verified"], v["mismatched"], v["bad_request_id"] = hg.reduce(
+                [v["verified"], v["mismatched"], v["bad_request_id"]], "sum")
+        if isinstance(extra.get("gateway_bytes"), dict):
+            gb = extra["gateway_bytes"]
+            gb["requests_per_s"] = hg.reduce([gb.pop("rps_this_rank")], "sum")[0]
+            gb["p99_ms"] = hg.reduce([gb["p99_ms"]], "max")[0]
         elapsed = hg.reduce([elapsed], "max")[0]
         ok, failed = hg.reduce([ok, failed], "sum")
         extra["p50_ms"], extra["p99_ms"] = hg.reduce([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], "max")
     value = ok / elapsed
+    v = extra.get("verify")
+    if isinstance(v, dict) and (v["mismatched"] or v["bad_request_id"] or not v["verified"]):
+        extra["error"] = "answer verification failed: %s" % (v,)
+        value = 0.0  # a wrong answer does not score
+    if world == 1 and isinstance(extra.get("gateway_bytes"), dict):
+        extra["gateway_bytes"]["requests_per_s"] = extra["gateway_bytes"].pop("rps_this_rank")
     if rank == 0:
         out = {
             "metric": "requests/sec + p50/p99 latency, %s ONNX /infer at 1/2/4/8 MI355X"
@@ -391,6 +485,41 @@ def _win(e0, e1, key):
     if key not in e1 or n1 <= n0:
         return e1.get(key)
     return (e1[key] * n1 - e0.get(key, 0.0) * n0) / (n1 - n0)
+
+
+def _stage_window(s0, s1):
+    """p50/p99 (us) of each stage over the window between two /health or /stats snapshots, from
+    their histogram buckets (csrc/serve/stage_stats.h: u = ns/1024, u < 8 exact, then 8 buckets per
+    octave); {stage: [count, p50, p99]}."""
+    def upper(b):
+        if b < 8:
+            return b + 1.0
+        o, sub = (b - 8) // 8 + 3, (b - 8) % 8
+        return (1 << o) * (1.0 + (sub + 1) / 8.0)
+
+    out = {}
+    for k, v1 in s1.items():
+        if not isinstance(v1, dict) or "hist" not in v1:
+            continue
+        c = {}
+        for b, n in v1["hist"]:
+            c[b] = c.get(b, 0) + n
+        for b, n in s0.get(k, {}).get("hist", []):
+            c[b] = c.get(b, 0) - n
+        items = sorted((b, n) for b, n in c.items() if n > 0)
+        n = sum(x for _, x in items)
+        if not n:
+            continue
+
+        def pct(q):
+            acc = 0
+            for b, x in items:
+                acc += x
+                if acc > q * n:
+                    return round(upper(b) * 1.024, 1)
+            return round(upper(items[-1][0]) * 1.024, 1)
+        out[k] = [n, pct(0.5), pct(0.99)]
+    return out
 
 
 def _busy(e0, e1, elapsed_s):

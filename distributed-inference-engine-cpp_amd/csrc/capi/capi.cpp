@@ -585,6 +585,8 @@ static LoadgenOptions loadgen_opts(const Json& j) {
   o.seed = static_cast<uint64_t>(jget<long>(j, "seed", static_cast<long>(o.seed)));
   o.id_prefix = jget<std::string>(j, "id_prefix", o.id_prefix);
   o.verify_tol = jget<double>(j, "verify_tol", o.verify_tol);
+  o.verify_every = jget<long>(j, "verify_every", o.verify_every);
+  o.scramble_ids = jget<bool>(j, "scramble_ids", o.scramble_ids);
   return o;
 }
 
@@ -596,6 +598,19 @@ int die_dp_shard(int B, int world, int per, int r, int* begin) {
   return L.shard_count(r);
 }
 int die_dp_per(int B, int world) { return DpLayout::make(B, world).per; }
+// Shared input arena of a DP group for `world` ranks (engine_json = EngineOptions, max_batch = the
+// whole DP batch): writes item bytes, items and total bytes.
+int die_dp_arena_plan(long long input_numel, const char* engine_json, int world, long long* out3) {
+  try {
+    const DpArenaPlan a = dp_arena_plan(static_cast<size_t>(input_numel), engine_opts(Json::parse(engine_json)), world);
+    out3[0] = static_cast<long long>(a.item_bytes);
+    out3[1] = static_cast<long long>(a.items);
+    out3[2] = static_cast<long long>(a.bytes);
+    return 0;
+  } catch (...) {
+    return -1;
+  }
+}
 void die_dp_items_from_gathered(int B, int world, int per, const int* gathered, long stride, int* out) {
   dp_items_from_gathered(DpLayout::with_per(B, world, per), gathered, static_cast<size_t>(stride), out);
 }
@@ -624,7 +639,7 @@ char* die_loadgen_run_verify(const char* opts_json, const float* inputs, long k,
                              char** err) {
   try {
     LoadgenOptions o = loadgen_opts(Json::parse(opts_json));
-    o.payload = "verify";
+    if (o.verify_every <= 0) o.payload = "verify";  // else: "full" with every verify_every-th request verified
     o.verify_inputs = inputs;
     o.verify_expected = expected;
     o.verify_count = static_cast<size_t>(k);

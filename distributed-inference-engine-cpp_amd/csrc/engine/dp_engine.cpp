@@ -84,6 +84,27 @@ size_t text_cap_for(size_t numel, const EngineOptions& opt) {
 constexpr int kDpArenaBatches = 12;
 constexpr int kDpInflightBatches = 4;
 
+}  // namespace
+
+// One staged request: its floats (numel x 4 B) or its input_data text.  With 4-bit packing (the
+// default, core/textpack.h) a text of up to 8 characters per value fits the float-sized item (the
+// bench's 4-decimal images average 7); a longer or unpackable text is parsed on the host into the
+// same item (serve/worker.cpp).  Only raw (unpacked) device decode needs the worst-case text room
+// of 24 bytes per value -- round 3 always reserved it: 3.45 MiB per item, 10.5 GiB of /dev/shm at
+// 8 ranks x batch 256, pinned by every rank.
+DpArenaPlan dp_arena_plan(size_t numel, const EngineOptions& opt, int world) {
+  DpArenaPlan a;
+  world = std::max(1, world);
+  const int local_max = std::max(1, std::min((opt.max_batch + world - 1) / world, kDpSubMax));
+  a.item_bytes = numel * sizeof(float);
+  if (!opt.pack_text) a.item_bytes = std::max(a.item_bytes, text_cap_for(numel, opt));
+  a.items = static_cast<size_t>(local_max) * world * kDpArenaBatches + 64;
+  a.bytes = opt.dp_arena_mb ? opt.dp_arena_mb << 20 : a.item_bytes * a.items;
+  return a;
+}
+
+namespace {
+
 struct DpAbandoned : std::runtime_error {
   DpAbandoned() : std::runtime_error("data-parallel group abandoned before attach") {}
 };
@@ -96,14 +117,13 @@ class DpEngine : public Engine {
     world_ = std::max(1, opt.dp_world);
     rank_ = opt.dp_rank;
     const size_t numel = model_input_numel(path);
-    item_bytes_ = std::max(numel * sizeof(float), text_cap_for(numel, opt));
+    const DpArenaPlan ap = dp_arena_plan(numel, opt, world_);
+    item_bytes_ = ap.item_bytes;
     // opt.max_batch is the whole DP batch (e.g. 256 over 8 GPUs); each rank's share is one sub-batch
     local_max_ = std::max(1, std::min((opt.max_batch + world_ - 1) / world_, kDpSubMax));
     if (rank_ == 0) {
       // every rank stages its in-flight requests in the arena: N x (sub-batches queued + pipeline)
-      const size_t items = static_cast<size_t>(local_max_) * world_ * kDpArenaBatches + 64;
-      const size_t arena = opt.dp_arena_mb ? opt.dp_arena_mb << 20 : item_bytes_ * items;
-      group_ = DpGroup::create(opt.dp_group, world_, arena, 4u << 20);
+      group_ = DpGroup::create(opt.dp_group, world_, ap.bytes, 4u << 20);
     } else {
       group_ = DpGroup::attach(opt.dp_group, rank_, 600000, ext_stop);
       if (!group_) throw DpAbandoned();

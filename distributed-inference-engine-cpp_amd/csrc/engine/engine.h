@@ -246,6 +246,12 @@ std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const E
 // Data-parallel leader (rank 0): creates the DpGroup, the communicator and the local engine, waits
 // for the followers, and shards every submitted batch over the ranks.
 std::unique_ptr<Engine> create_dp_engine(const std::string& model_path, const EngineOptions& opt);
+// Shared input arena of a data-parallel group (engine/dp_engine.cpp): bytes per staged request,
+// requests staged, total bytes (= the /dev/shm segment every rank maps and pins).
+struct DpArenaPlan {
+  size_t item_bytes = 0, items = 0, bytes = 0;
+};
+DpArenaPlan dp_arena_plan(size_t input_numel, const EngineOptions& opt, int world);
 // Data-parallel follower (rank >= 1): attach, build the local engine on this process's GPU and
 // serve shards until the leader stops the group or *stop becomes true.  Returns batches served.
 long run_dp_follower(const std::string& model_path, const EngineOptions& opt, const std::atomic<bool>* stop);

@@ -33,6 +33,7 @@
 #include "../kernels/kernels.h"
 #include "engine.h"
 #include "hip_plan.h"
+#include "../core/log.h"
 #include "../core/trace.h"
 #include "../parallel/comm.h"
 
@@ -112,8 +113,12 @@ class HipEngine : public Engine {
     if (!comm_ || comm_->rank() == 0)
       HIP_CHECK(hipMemcpy(params_, plan_.params.data(), plan_.params.size(), hipMemcpyHostToDevice));
     if (comm_) {  // data parallel: every rank gets the packed weights from rank 0 over xGMI
+      const auto tb = std::chrono::steady_clock::now();
       comm_->broadcast(params_, plan_.params.size(), 0, s_compute_);
       HIP_CHECK(hipStreamSynchronize(s_compute_));
+      weight_bcast_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count();
+      DIE_LOG(INFO, "dp rank " << comm_->rank() << ": weight broadcast " << plan_.params.size() / 1048576.0
+                                     << " MiB in " << weight_bcast_ms_ << " ms (" << comm_->backend() << ")");
     }
     if (opt.device_decode) text_cap_ = (in_numel_ * 24 + 4095) / 4096 * 4096;  // up to 23 chars + separator per value
     if (text_cap_) {
@@ -691,6 +696,8 @@ class HipEngine : public Engine {
     j["pinned_samples"] = static_cast<long long>(pool_->allocated());
     j["device_decode"] = text_cap_ > 0;
     j["dp_rank"] = comm_ ? comm_->rank() : 0;
+    j["dp_weight_broadcast_ms"] = weight_bcast_ms_;
+    j["dp_collective_ops"] = dp_collective_ops_.load();
     j["text_capacity"] = static_cast<long long>(text_cap_);
     j["stage_slots"] = n_stage_;
     j["staged_uploads"] = staged_total_.load();
@@ -1463,9 +1470,12 @@ class HipEngine : public Engine {
   // copies all rows and tables to its host; a group of one copies straight from d_out.
   void dp_collectives(Slot& sl, int B, hipStream_t cs) {
     dp_issued_ = true;
-    if (dp_world_ > 1) {
+    if (dp_world_ > 1) {  // one grouped operation: logits + status table (shard flag included)
+      comm_->group_begin();
       comm_->all_gather(sl.d_out, sl.d_gather, sizeof(float) * out_numel_ * B, cs);
       comm_->all_gather(sl.d_status, sl.d_gstatus, sizeof(int) * status_len(), cs);
+      comm_->group_end();
+      dp_collective_ops_.fetch_add(1, std::memory_order_relaxed);
     }
     HIP_CHECK(hipEventRecord(sl.ev_gather, cs));
     HIP_CHECK(hipMemcpyAsync(sl.h_gather, dp_world_ > 1 ? sl.d_gather : sl.d_out, sizeof(float) * out_numel_ * B * dp_world_,
@@ -1515,6 +1525,8 @@ class HipEngine : public Engine {
   size_t arena_bytes_ = 0;
   Communicator* comm_ = nullptr;  // data parallel (not owned)
   int dp_world_ = 1;
+  double weight_bcast_ms_ = 0;                 // RCCL weight broadcast at start-up (stats)
+  std::atomic<long long> dp_collective_ops_{0};  // grouped per-batch gathers issued
   std::vector<void*> registered_;
   uint8_t* params_ = nullptr;
   float* ws_ = nullptr;  // executor 0's (autotune)

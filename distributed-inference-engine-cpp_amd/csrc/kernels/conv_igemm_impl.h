@@ -28,6 +28,22 @@ __device__ __forceinline__ float act_fn(float v, int act, float lo = 0.f, float 
 
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// Write-through (sc1) 16-byte stores / loads of the split-K workspace through a buffer resource
+// (aux bit 4 = sc1 on gfx950): the fused split-K hand-off needs no agent-scope release/acquire
+// fences (MI355X_MICROARCH "Valid forms", row 1: sc1 stores drained by every storing wave, one
+// lane's agent-scope atomic add, the last adder's workgroup reads with sc1 loads).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kCpolSc1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, byte_off, 0, kCpolSc1);
+}
+__device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kCpolSc1));
+}
+
 // Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
 // fp32 mode (p.split): the residual is read as hi + lo and out/out2 are stored as split planes.
 __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
@@ -308,7 +324,9 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     __syncthreads();
     constexpr int GPR = BN / 8;
     const bool partial = p.splits > 1;
+    const bool fused = partial && p.counters;
     float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
+    const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
     for (int g = tid; g < BM * GPR; g += 256) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
@@ -317,7 +335,11 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
       if (m < 0 || n >= p.N) continue;
       const float4 a = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg) ^ (row & (CPR - 1))) << 2));
       const float4 b = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg + 1) ^ (row & (CPR - 1))) << 2));
-      if (partial) {
+      if (fused) {
+        const unsigned off = static_cast<unsigned>(((static_cast<size_t>(split) * p.M + m) * p.N + n) * 4);
+        st4_sc1(wsr, off, a);
+        st4_sc1(wsr, off + 16, b);
+      } else if (partial) {
         float* o = ws + static_cast<size_t>(m) * p.N + n;
         *reinterpret_cast<float4*>(o) = a;
         *reinterpret_cast<float4*>(o + 4) = b;
@@ -326,41 +348,37 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         epilogue8(p, m, n, v);
       }
     }
-    if (!partial || !p.counters) return;
+    if (!fused) return;
     // Fused split-K reduction: the last split block of this tile to arrive sums every split's
-    // partial and runs the epilogue (no second kernel).  Hand-off per the agent-scope recipe
-    // (cdna_hip_programming §6 G16): every wave drains its slab stores, block barrier, ONE lane
-    // releases at agent scope and takes a ticket; the reducer's lane acquires at agent scope (which
-    // invalidates this CU's L1) before the barrier that precedes the plain slab loads.
+    // partial (in split order, as splitk_epilogue_kernel does) and runs the epilogue, no second
+    // kernel.  Hand-off without fences (MI355X_MICROARCH "Valid forms", row 1): the partials went
+    // out as write-through (sc1) stores, every wave drains them, a block barrier, then ONE lane's
+    // agent-scope atomic add takes the ticket; the last arriver's waves read every partial with
+    // sc1 loads after the barrier that publishes the ticket.  (Round 3 used agent release/acquire
+    // fences here: a write-back of the L2 per block, which is why the autotuner never picked it.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(lds);  // staging tile is dead now: reuse it for the broadcast
     if (tid == 0) {
       int* ctr = p.counters + tile;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == p.splits - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-      }
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
       *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
-    const size_t slab = static_cast<size_t>(p.M) * p.N;
+    const unsigned slab = static_cast<unsigned>(static_cast<size_t>(p.M) * p.N * 4);  // bytes
     for (int g = tid; g < BM * GPR; g += 256) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
       const int m = rows(row);
       const int n = n0 + cg * 8;
       if (m < 0 || n >= p.N) continue;
-      const float* src = p.ws + static_cast<size_t>(m) * p.N + n;
+      const unsigned src = static_cast<unsigned>((static_cast<size_t>(m) * p.N + n) * 4);
       float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int s = 0; s < p.splits; ++s) {
-        const float4 a = ldf4(src + s * slab), b = ldf4(src + s * slab + 4);
+        const float4 a = ld4_sc1(wsr, src + s * slab), b = ld4_sc1(wsr, src + s * slab + 16);
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
         v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       }

@@ -57,6 +57,8 @@ class RcclComm : public Communicator {
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     nccl_check(ncclAllGather(send, recv, bytes, ncclChar, comm_, s), "ncclAllGather");
   }
+  void group_begin() override { nccl_check(ncclGroupStart(), "ncclGroupStart"); }
+  void group_end() override { nccl_check(ncclGroupEnd(), "ncclGroupEnd"); }
 
  private:
   int rank_, world_;

@@ -25,6 +25,11 @@ class Communicator {
   // completes before returning).  All ranks call collectives in the same order.
   virtual void broadcast(void* buf, size_t bytes, int root, hipStream_t stream) = 0;
   virtual void all_gather(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream) = 0;
+  // Collectives issued between group_begin() and group_end() go out as ONE fused operation (RCCL:
+  // ncclGroupStart / ncclGroupEnd -- one launch and one latency for a batch's logits + status
+  // gathers).  The host communicator runs them one by one.
+  virtual void group_begin() {}
+  virtual void group_end() {}
 };
 
 // Collective constructor: every rank of `g` must call it (after hipSetDevice on its GPU).

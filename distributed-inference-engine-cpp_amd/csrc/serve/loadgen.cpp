@@ -23,7 +23,15 @@ struct Template {
   std::string body;
   size_t id_pos = 0, id_len = 0;  // fixed-width decimal request number
   size_t v0_pos = 0, v1_pos = 0;  // fixed-width "0.dddd" values patched per request
+  size_t v0_end = 0, v1_end = 0;  // verify templates: end of the first two values' text (0 = no padding)
 };
+
+uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 
 constexpr int kIdDigits = 10;
 
@@ -65,9 +73,36 @@ Template make_verify_template(const LoadgenOptions& o, size_t k) {
   t.id_len = kIdDigits;
   b.append(kIdDigits, '0');
   b += "\",\"input_data\":";
+  const size_t arr = b.size();
   append_float_array(b, o.verify_inputs + k * o.input_numel, o.input_numel);
   b += "}";
+  // the first two values, if plain decimals ("0.5"), can take trailing zeros without changing them
+  const size_t e0 = b.find(',', arr), e1 = e0 == std::string::npos ? e0 : b.find(',', e0 + 1);
+  auto plain = [&](size_t from, size_t to) {
+    const std::string v = b.substr(from, to - from);
+    return v.find('.') != std::string::npos && v.find_first_of("eE") == std::string::npos;
+  };
+  if (e1 != std::string::npos && plain(arr + 1, e0) && plain(e0 + 1, e1)) {
+    t.v0_end = e0;
+    t.v1_end = e1;
+  }
   return t;
+}
+
+// Variant v of a verify body: 0..31 zeros after value 0 and v / 32 % 32 after value 1.
+void verify_body(const Template& t, long v, std::string& out) {
+  if (!t.v0_end) {
+    out = t.body;
+    return;
+  }
+  const size_t z0 = static_cast<size_t>(v % 32), z1 = static_cast<size_t>((v / 32) % 32);
+  out.clear();
+  out.reserve(t.body.size() + z0 + z1);
+  out.append(t.body, 0, t.v0_end);
+  out.append(z0, '0');
+  out.append(t.body, t.v0_end, t.v1_end - t.v0_end);
+  out.append(z1, '0');
+  out.append(t.body, t.v1_end, std::string::npos);
 }
 
 // Relative L2 error of a response's output_data against `ref` (n floats); < 0 when the body has no
@@ -131,11 +166,19 @@ Json run_loadgen(const LoadgenOptions& o) {
   gate.total = C + 1;
   std::chrono::steady_clock::time_point t0, t1;
   const bool verify = o.payload == "verify";
-  if (verify && (!o.verify_inputs || !o.verify_expected || o.verify_count == 0 || o.output_numel == 0))
-    throw std::runtime_error("loadgen verify mode needs verify_inputs, verify_expected, verify_count, output_numel");
   const bool full = o.payload == "full";
+  const bool sampled = full && o.verify_every > 0;  // full mode with a verified sample
+  if ((verify || sampled) && (!o.verify_inputs || !o.verify_expected || o.verify_count == 0 || o.output_numel == 0))
+    throw std::runtime_error("loadgen verify mode needs verify_inputs, verify_expected, verify_count, output_numel");
   std::vector<Template> vt;  // verify mode: one shared template per distinct input
-  for (size_t k = 0; verify && k < o.verify_count; ++k) vt.push_back(make_verify_template(o, k));
+  for (size_t k = 0; (verify || sampled) && k < o.verify_count; ++k) vt.push_back(make_verify_template(o, k));
+  auto printed = [&](long id) -> uint64_t {
+    return o.scramble_ids ? splitmix64(static_cast<uint64_t>(id)) % 10000000000ull : static_cast<uint64_t>(id);
+  };
+  auto is_verify = [&](long id) { return verify || (sampled && id % o.verify_every == 0); };
+  auto verify_k = [&](long id) -> size_t {
+    return static_cast<size_t>(sampled ? id / o.verify_every : id) % vt.size();
+  };
   std::vector<long> verified(C, 0), mismatched(C, 0), bad_id(C, 0);
   std::vector<double> max_err(C, 0.0);
   const int d = std::max(1, std::min(o.decimals, 8));
@@ -152,15 +195,16 @@ Json run_loadgen(const LoadgenOptions& o) {
       std::string vbody;  // verify mode: this request's copy of its input's template
       auto body_for = [&](long id) -> std::string& {
         static thread_local std::string small;
-        if (verify) {
-          const Template& t = vt[static_cast<size_t>(id) % vt.size()];
-          vbody = t.body;
-          patch_digits(vbody, t.id_pos, t.id_len, static_cast<uint64_t>(id));
+        if (is_verify(id)) {
+          const Template& t = vt[verify_k(id)];
+          if (sampled) verify_body(t, (id / o.verify_every) / static_cast<long>(vt.size()) + 1, vbody);
+          else vbody = t.body;
+          patch_digits(vbody, t.id_pos, t.id_len, printed(id));
           return vbody;
         }
         const long key = o.distinct > 0 ? id % o.distinct : id;
         if (full) {
-          patch_digits(tpl.body, tpl.id_pos, tpl.id_len, static_cast<uint64_t>(id));
+          patch_digits(tpl.body, tpl.id_pos, tpl.id_len, printed(id));
           // unique input: encode (key, connection) in the first two values
           const uint64_t u = static_cast<uint64_t>(key) * 64 + static_cast<uint64_t>(c);
           patch_digits(tpl.body, tpl.v0_pos + 2, static_cast<size_t>(d), u % scale);
@@ -168,7 +212,7 @@ Json run_loadgen(const LoadgenOptions& o) {
           return tpl.body;
         }
         const long a = key % 10;
-        small = "{\"request_id\":\"" + o.id_prefix + std::to_string(id) + "\",\"input_data\":[" +
+        small = "{\"request_id\":\"" + o.id_prefix + std::to_string(printed(id)) + "\",\"input_data\":[" +
                 std::to_string(a) + ".0," + std::to_string(a + 1) + ".0," + std::to_string(a + 2) + ".0]}";
         return small;
       };
@@ -182,10 +226,10 @@ Json run_loadgen(const LoadgenOptions& o) {
         if (r && r->status == 200) {
           ++ok[c];
           lat[c].push_back(ms);
-          if (verify) {
-            const size_t k = static_cast<size_t>(id) % vt.size();
+          if (is_verify(id)) {
+            const size_t k = verify_k(id);
             char idbuf[32];
-            std::snprintf(idbuf, sizeof idbuf, "%0*ld", kIdDigits, id);
+            std::snprintf(idbuf, sizeof idbuf, "%0*llu", kIdDigits, static_cast<unsigned long long>(printed(id)));
             bool id_ok = false;
             const double e = response_error(r->body, o.verify_expected + k * o.output_numel, o.output_numel,
                                             o.id_prefix + idbuf, id_ok);
@@ -257,7 +301,7 @@ Json run_loadgen(const LoadgenOptions& o) {
   j["errors"] = e;
   j["payload"] = o.payload;
   j["body_bytes"] = static_cast<long long>(verify ? vt[0].body.size() : full ? make_full_template(o, 1).body.size() : 60);
-  if (verify) {
+  if (verify || sampled) {
     long nv = 0, nm = 0, nb = 0;
     double me = 0.0;
     for (int c = 0; c < C; ++c) {

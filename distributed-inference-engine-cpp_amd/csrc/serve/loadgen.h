@@ -40,6 +40,14 @@ struct LoadgenOptions {
   size_t verify_count = 0;
   size_t output_numel = 0;
   double verify_tol = 0.0;
+  // Sampled verification in "full" mode (> 0): every verify_every-th request (id % verify_every ==
+  // 0) carries verify input k = (id / verify_every) % verify_count instead of a unique image, its
+  // answer is checked like verify mode, and its text is made unique by zero-padding the first two
+  // values (0.5 -> 0.5000...: same floats, another cache key), so it is computed, never a cache hit.
+  long verify_every = 0;
+  // Print request numbers scrambled (splitmix64(id) mod 10^10, fixed width) instead of in order:
+  // FNV-1a of consecutive decimal strings clusters on the gateway's ring (bench.py ring analysis).
+  bool scramble_ids = false;
 };
 
 // Runs warmup then the timed phase; returns {"ok","failed","wall_s","rps","latency_ms":{...},

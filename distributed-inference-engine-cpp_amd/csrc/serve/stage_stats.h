@@ -1,7 +1,9 @@
 // Lock-free latency histograms for the worker's and gateway's request stages (SURVEY §5.1/§5.5:
-// per-stage histograms on /health and /stats, extra keys only).  Log-linear buckets: 4 per octave
-// of ~microseconds (ns / 1024), i.e. <= 19 % wide above 4 us (tail percentiles to about +-10 %,
-// > 1 h at the top); percentiles report bucket upper bounds.
+// per-stage histograms on /health and /stats, extra keys only).  Log-linear buckets: 8 per octave
+// of ~microseconds (ns / 1024), i.e. <= 12.5 % wide above 8 us (tail percentiles to about +-6 %,
+// days at the top); percentiles report bucket upper bounds.  The snapshot also carries the
+// non-empty buckets ("hist": [[bucket, count], ...]) so a client can difference two snapshots and
+// take percentiles over a window (bench.py: the timed pass only, warm-up excluded).
 #pragma once
 
 #include <atomic>
@@ -14,21 +16,21 @@ namespace die {
 
 class StageHist {
  public:
-  static constexpr int kSub = 4;                  // buckets per octave
-  static constexpr int kBuckets = 4 + 38 * kSub;  // u < 4 exactly, then 4 per octave
-  // bucket of u = ns / 1024: u < 4 -> u; else octave o = floor(log2 u) >= 2 split by the next 2 bits
+  static constexpr int kBits = 3, kSub = 1 << kBits;    // 8 buckets per octave
+  static constexpr int kBuckets = kSub + (40 - kBits) * kSub;  // u < 8 exactly, then 8 per octave
+  // bucket of u = ns / 1024: u < 8 -> u; else octave o = floor(log2 u) >= 3 split by the next 3 bits
   static int bucket(uint64_t u) {
-    if (u < 4) return static_cast<int>(u);
+    if (u < kSub) return static_cast<int>(u);
     const int o = 63 - __builtin_clzll(u);
-    const int sub = static_cast<int>((u >> (o - 2)) & 3);
-    const int b = 4 + (o - 2) * kSub + sub;
+    const int sub = static_cast<int>((u >> (o - kBits)) & (kSub - 1));
+    const int b = kSub + (o - kBits) * kSub + sub;
     return b < kBuckets ? b : kBuckets - 1;
   }
   // exclusive upper bound of bucket b, in u units
   static double upper(int b) {
-    if (b < 4) return b + 1.0;
-    const int o = (b - 4) / kSub + 2, sub = (b - 4) % kSub;
-    return static_cast<double>(1ull << o) * (1.0 + (sub + 1) / 4.0);
+    if (b < kSub) return b + 1.0;
+    const int o = (b - kSub) / kSub + kBits, sub = (b - kSub) % kSub;
+    return static_cast<double>(1ull << o) * (1.0 + (sub + 1) / static_cast<double>(kSub));
   }
   void add(std::chrono::steady_clock::duration d) {
     const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(d).count();
@@ -57,6 +59,16 @@ class StageHist {
     j["p90_us"] = n ? pct(0.9) : 0.0;
     j["p99_us"] = n ? pct(0.99) : 0.0;
     j["p999_us"] = n ? pct(0.999) : 0.0;
+    Json h = Json::array();
+    for (int i = 0; i < kBuckets; ++i)
+      if (c[i]) {
+        Json e = Json::array();
+        e.push_back(static_cast<long long>(i));
+        e.push_back(static_cast<long long>(c[i]));
+        h.push_back(e);
+      }
+    j["hist"] = h;
+    j["bucket_us"] = 1.024;  // u unit in us; bucket b spans [lower, upper(b)) u
     return j;
   }
 

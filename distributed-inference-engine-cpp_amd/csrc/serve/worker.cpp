@@ -238,7 +238,12 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   }
   const size_t numel = eng.input_numel();
   sink.float_cap = std::min(sink.buf.capacity, numel);
-  const size_t text_cap = std::min(eng.text_capacity(), sink.buf.capacity * sizeof(float));
+  // device decode takes texts of up to text_capacity() characters; the staging item holds them
+  // 4-bit packed (half the bytes) when the engine packs, raw otherwise
+  const size_t item_bytes = sink.buf.capacity * sizeof(float);
+  const size_t dev_cap = eng.text_capacity();
+  const bool packing = eng.text_packing();
+  const size_t text_cap = std::min(dev_cap, packing ? 2 * item_bytes : item_bytes);
   sink.defer = text_cap > 0;
   int seen = 0;
   TraceRange tr_parse("worker.parse");
@@ -270,9 +275,18 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
   }
   try {
     seen = parse_infer_body(body, sink);
-    if ((seen & 4) && sink.text_n > text_cap) {  // too long for device decode: parse on the host
+    // too long for device decode, or not packable and too long to stage raw: parse on the host
+    bool host = (seen & 4) && sink.text_n > text_cap;
+    if ((seen & 4) && !host) {
+      auto* dst = reinterpret_cast<uint8_t*>(sink.buf.data);
+      if (packing && pack_nibbles(sink.text, sink.text_n, dst)) packed = true;  // half the bytes to copy
+      else if (sink.text_n > item_bytes) host = true;
+      else std::memcpy(dst, sink.text, sink.text_n);
+    }
+    if (host) {
       sink.defer = false;
       sink.text = nullptr;
+      packed = false;
       seen = parse_infer_body(body, sink);
     }
     if (!(seen & 1)) throw JsonError("key 'request_id' not found");
@@ -280,14 +294,8 @@ void WorkerNode::handle_infer(HttpRequest& req, Responder res) {
     if (seen & 4) {
       text_len = sink.text_n;
       text_off = static_cast<size_t>(sink.text - body.data());
-      auto* dst = reinterpret_cast<uint8_t*>(sink.buf.data);
-      if (eng.text_packing() && pack_nibbles(sink.text, sink.text_n, dst)) {
-        packed = true;  // half the bytes to copy to the device
-        key = hash_bytes(dst, (text_len + 1) / 2, 2);
-      } else {
-        std::memcpy(dst, sink.text, sink.text_n);
-        key = hash_text(sink.text, sink.text_n);
-      }
+      const auto* dst = reinterpret_cast<const uint8_t*>(sink.buf.data);
+      key = packed ? hash_bytes(dst, (text_len + 1) / 2, 2) : hash_text(sink.text, sink.text_n);
       // an empty list needs no conversion
       if (text_len == 0) {
         text_len = 0;

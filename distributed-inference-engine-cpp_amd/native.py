@@ -466,6 +466,19 @@ def onnx_summary(model_path: str) -> Dict[str, Any]:
 
 # ---- servers ------------------------------------------------------------------------------------------
 
+def dp_arena_plan(input_numel: int, world: int, **engine_opts) -> Dict[str, int]:
+    """Size of a data-parallel group's shared input arena (engine/dp_engine.cpp dp_arena_plan):
+    {item_bytes, items, bytes}; engine_opts as for Engine (max_batch = the whole DP batch)."""
+    L = lib()
+    fn = L.die_dp_arena_plan
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_longlong, C.c_char_p, C.c_int, C.POINTER(C.c_longlong)]
+    out = (C.c_longlong * 3)()
+    if fn(int(input_numel), json.dumps(engine_opts).encode(), int(world), out) != 0:
+        raise NativeError("dp_arena_plan failed")
+    return {"item_bytes": out[0], "items": out[1], "bytes": out[2]}
+
+
 class DpLayout:
     """Row bookkeeping of one data-parallel batch (csrc/parallel/dp_layout.h): B items over `world`
     ranks, `per` items per rank (default ceil(B / world)); rank r computes [r*per, min(B, (r+1)*per))."""
@@ -592,7 +605,9 @@ def loadgen(verify_inputs: Optional[np.ndarray] = None, verify_expected: Optiona
     """Closed-loop C++ load generator.  With verify_inputs ([K, input_numel]) and verify_expected
     ([K, output_numel]) every request carries one of the K inputs (unique request_id) and every answer
     is checked against its expected row (relative L2 <= verify_tol, 0 = bit-exact): the result adds
-    "verified", "mismatched", "bad_request_id" and "max_rel_err"."""
+    "verified", "mismatched", "bad_request_id" and "max_rel_err".  With payload="full" and
+    verify_every=N only every N-th request is such a verified one (zero-padded text: never a cache
+    hit); scramble_ids=True prints request numbers scrambled (hash-uniform on the gateway ring)."""
     err = _err_box()
     if verify_inputs is not None:
         xi = np.ascontiguousarray(verify_inputs, np.float32).reshape(len(verify_inputs), -1)

@@ -73,6 +73,30 @@ def test_bench_two_ranks_torchrun_cpu(mode):
     assert all(r["requests_per_s"] > 0 and r["failed"] == 0 for r in pr)
 
 
+@pytest.mark.parametrize("mode", ["gateway", "dp"])
+def test_bench_eight_ranks_torchrun_cpu(mode):
+    """the driver's N=8 launch line rehearsed with 8 CPU ranks (gloo, a tiny
+    ResNet-v2 so the CPU executor keeps up): gateway mode routes over all 8 workers on ring-balanced
+    ports with sampled answer verification; dp mode runs ONE data-parallel worker over 8 ranks."""
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+                "--mode", mode, "--arch", "resnet_tiny", "--device", "cpu", "--batch", "4", "--steps", "2",
+                "--warmup", "1", "--connections", "4", "--step-requests", "25", "--no-dp", "--verify-every", "10"],
+               timeout=600)
+    assert out["n_gpus"] == 8 and out["failed"] == 0 and out["value"] > 0
+    assert out["config"]["requests"] == 2 * 25 * 8
+    pr = out["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8)) and all(r["failed"] == 0 for r in pr)
+    if mode == "gateway":
+        v = out["verify"]
+        assert v["verified"] == 8 * 5 and v["mismatched"] == 0 and v["bad_request_id"] == 0, v
+        ring = out["ring"]
+        # ports balance the ring's arcs (400 ids are too few to pin the routed shares themselves)
+        assert ring["balanced_ports"] and len(set(ring["ports"])) == 8 and ring["arc_max_over_fair"] <= 1.1, ring
+        assert abs(sum(r["worker_share"] for r in pr) - 1.0) < 1e-3
+        assert out["gateway_bytes"]["failed"] == 0 and out["gateway_bytes"]["requests_per_s"] > 0
+
+
 def test_bench_rejects_gpus_world_mismatch():
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",

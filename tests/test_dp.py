@@ -25,7 +25,11 @@ print('served', f.join(), flush=True)
 
 
 def _spawn_followers(model, group, world, mb):
-    env = dict(os.environ, DIE_NO_TORCH="1")
+    # one OpenMP thread per follower: 8 processes x all-CPU OpenMP teams spin against each other
+    # (world 8 on an 8-CPU host: 214 s instead of 3 s)
+    env = dict(os.environ, DIE_NO_TORCH="1", OMP_NUM_THREADS="1" if world > 3 else os.environ.get("OMP_NUM_THREADS", ""))
+    if not env["OMP_NUM_THREADS"]:
+        env.pop("OMP_NUM_THREADS")
     return [subprocess.Popen([sys.executable, "-c", FOLLOWER.format(repo=REPO, model=model, group=group, rank=r,
                                                                       world=world, mb=mb)],
                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
@@ -278,7 +282,7 @@ def _verify_set(native, path, cfg, k, seed):
     return x, ref
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_dp_concurrent_rows_verified(native, models, world):
     """16 concurrent connections over K=12 distinct inputs (cache off, so every request is computed):
     DP batches carry several rows from several sub-batches, and every answer is compared with its
@@ -303,6 +307,75 @@ def test_dp_concurrent_rows_verified(native, models, world):
             wk.stop()
         outs = _reap(ps)
     assert all(rc == 0 for rc, _ in outs), outs
+
+
+INGEST_RANK_NOCACHE = INGEST_RANK.replace("max_batch={mb},", "max_batch={mb}, cache_capacity=0,")
+
+
+def test_dp_eight_ranks_every_rank_ingests_verified(native, models):
+    """an 8-process rehearsal of the N=8 DP flow.  Eight CPU ranks share one port
+    (SO_REUSEPORT), each parses its own connections into the shared arena, the leader merges all
+    ranks' sub-batches into DP batches sharded over the 8 ranks (host collective in place of RCCL),
+    and EVERY answer is checked against its input's logits."""
+    import socket
+
+    from die_amd.models import resnet_v2 as r
+
+    world = 8
+    path, w, cfg = models["tiny"]
+    k = 16
+    x = r.synthetic_input(k, cfg, seed=21).reshape(k, -1)
+    ref = np.stack([native.cpu_run(path, x[i:i + 1].reshape(1, 3, 64, 64))[0] for i in range(k)])
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    group = "die_dp_e8_%d" % os.getpid()
+    env = dict(os.environ, DIE_NO_TORCH="1", OMP_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, "-c", INGEST_RANK_NOCACHE.format(repo=REPO, model=path, rank=q, port=port,
+                                                                             mb=32, world=world, group=group)],
+                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+          for q in range(1, world)]
+    wk = None
+    try:
+        wk = native.Worker(path, node_id="dp-r0", port=port, reuse_port=True, max_batch=32, cache_capacity=0,
+                           engine={"device": "cpu", "dp_world": world, "dp_group": group})
+        for p in ps:
+            line = p.stdout.readline().decode()
+            assert "READY" in line, line + p.stdout.read().decode()
+        res = native.loadgen(port=port, connections=48, requests=480, verify_inputs=x, verify_expected=ref,
+                             verify_tol=1e-4, timeout_ms=120000)
+        assert res["ok"] == 480 and res["failed"] == 0, res
+        assert res["verified"] == 480 and res["mismatched"] == 0 and res["bad_request_id"] == 0, res
+        h0 = wk.health()
+        assert h0["engine"]["dp_world"] == world and h0["engine"]["dp_batches"] < 480
+    finally:
+        if wk is not None:
+            wk.stop()
+        healths = []
+        for p in ps:
+            try:
+                out, _ = p.communicate(b"stop\n", timeout=120)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                out, _ = p.communicate()
+            healths += [json.loads(l[len("HEALTH "):]) for l in out.decode().splitlines() if l.startswith("HEALTH ")]
+    assert len(healths) == world - 1
+    parsed = [h0["total_requests"]] + [h["total_requests"] for h in healths]
+    assert sum(parsed) >= 480 and sum(n > 0 for n in parsed) >= 4, parsed  # the kernel spread the connections
+
+
+def test_dp_arena_at_eight_ranks_batch_256(native):
+    """the shared input arena was sized for the worst-case text (24 B per value):
+    10.5 GiB of /dev/shm at 8 ranks x batch 256, pinned by every rank.  Packed texts fit the
+    float-sized item, so the same group now needs <= 2 GiB."""
+    numel = 3 * 224 * 224
+    a = native.dp_arena_plan(numel, 8, max_batch=256, device="hip", device_decode=True, pack_text=True)
+    assert a["item_bytes"] == numel * 4
+    assert a["bytes"] <= 2 << 30, a
+    raw = native.dp_arena_plan(numel, 8, max_batch=256, device="hip", device_decode=True, pack_text=False)
+    assert raw["bytes"] > 8 << 30  # the unpacked path keeps the worst-case room
+    assert native.dp_arena_plan(numel, 8, max_batch=256, dp_arena_mb=512)["bytes"] == 512 << 20
 
 
 FAILING_FOLLOWER = """
