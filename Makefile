@@ -18,7 +18,7 @@ LDLIBS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler
 
 HOST_SRCS := core/json.cpp core/http.cpp core/http_async.cpp core/log.cpp core/metrics.cpp core/shm_arena.cpp core/textpack.cpp parallel/dp_group.cpp parallel/comm.cpp engine/dp_engine.cpp serve/consistent_hash.cpp serve/circuit_breaker.cpp \
              serve/worker.cpp serve/gateway.cpp serve/loadgen.cpp onnx/onnx_model.cpp \
-             engine/engine.cpp engine/cpu_exec.cpp engine/hip_plan.cpp capi/capi.cpp capi/capi_kernels.cpp
+             engine/engine.cpp engine/cpu_exec.cpp engine/hybrid_engine.cpp engine/hip_plan.cpp capi/capi.cpp capi/capi_kernels.cpp
 HIP_SRCS  := $(notdir $(wildcard $(SRC)/engine/*.hip)) $(notdir $(wildcard $(SRC)/kernels/*.hip))
 HOST_OBJS := $(addprefix $(BUILD)/host/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS  := $(patsubst %.hip,$(BUILD)/hip/%.o,$(HIP_SRCS))

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "../core/json.h"
+#include "../engine/engine.h"
 #include "../engine/hip_plan.h"
 #include "../kernels/kernels.h"
 #include "../onnx/onnx_model.h"
@@ -263,6 +264,31 @@ char* die_plan_report(const char* model_path, int split, char** err) {
 }
 
 // Plan summary of a model (op list with fused epilogues), for tests and docs.
+// Hybrid HIP + CPU partition of a model (engine/hybrid_engine.cpp), computed on the host.
+char* die_hybrid_partition(const char* model_path, int max_batch, int split, char** err) {
+  try {
+    const onnx::Model m = onnx::load_onnx(model_path);
+    Json out = Json::array();
+    for (const HybridSegment& s : hybrid_partition(m, max_batch, split != 0)) {
+      Json e = Json::object();
+      e["device"] = s.hip ? "hip" : "cpu";
+      e["first"] = s.first;
+      e["last"] = s.last;
+      e["input"] = s.input;
+      e["output"] = s.output;
+      e["gemm_nodes"] = s.convs;
+      Json ops = Json::array();
+      for (int k = s.first; k <= s.last; ++k) ops.push_back(m.nodes[static_cast<size_t>(k)].op_type);
+      e["ops"] = ops;
+      out.push_back(e);
+    }
+    return dup(out.dump());
+  } catch (const std::exception& ex) {
+    if (err) *err = dup(ex.what());
+    return nullptr;
+  }
+}
+
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse_pairs, char** err) {
   try {
     Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, fuse_pairs != 0);

@@ -308,15 +308,28 @@ std::unique_ptr<Engine> create_engine(const std::string& model_path, const Engin
   if (opt.device != "cpu") {
     std::string why;
     std::unique_ptr<Engine> e;
+    bool unlowerable = false;
     try {
       e = create_hip_engine(model_path, opt, &why);
     } catch (const std::exception& ex) {
-      // device "auto" keeps the reference's EP fallback (src/inference_engine.cpp:21-29): a graph
-      // the HIP planner cannot lower (every unsupported node is listed) runs on the CPU executor
-      if (opt.device == "hip") throw;
       why = ex.what();
+      unlowerable = why.find("cannot lower") != std::string::npos;
+      if (opt.device == "hip" && !unlowerable) throw;
     }
     if (e) return e;
+    if (unlowerable) {
+      // the reference's per-node EP fallback (src/inference_engine.cpp:21-31): the nodes the HIP
+      // planner cannot lower run on the CPU executor, every other piece stays on the GPU
+      std::string why2;
+      try {
+        e = create_hybrid_engine(model_path, opt, &why2);
+      } catch (const std::exception& ex) {
+        why2 = ex.what();
+      }
+      if (e) return e;
+      DIE_LOG(WARN, "hybrid HIP + CPU partition unavailable: " << why2);
+      if (opt.device == "hip") throw std::runtime_error(why);
+    }
     if (opt.device == "hip") throw std::runtime_error("HIP engine unavailable: " + why);
     DIE_LOG(WARN, "HIP engine unavailable (" << why << "); falling back to the CPU executor");
   }

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../core/json.h"
+#include "../onnx/onnx_model.h"
 
 namespace die {
 
@@ -257,5 +258,22 @@ DpArenaPlan dp_arena_plan(size_t input_numel, const EngineOptions& opt, int worl
 long run_dp_follower(const std::string& model_path, const EngineOptions& opt, const std::atomic<bool>* stop);
 // Defined in the HIP translation unit; returns nullptr (with `why` set) when no GPU is usable.
 std::unique_ptr<Engine> create_hip_engine(const std::string& model_path, const EngineOptions& opt, std::string* why);
+// The same for a model already in memory (`label` names it in stats / getModelPath).
+std::unique_ptr<Engine> create_hip_engine_model(const std::string& label, onnx::Model model, const EngineOptions& opt,
+                                                std::string* why);
+// Hybrid HIP + CPU execution (engine/hybrid_engine.cpp), the reference's per-node execution-provider
+// fallback (/root/reference/src/inference_engine.cpp:21-31: ORT places the nodes the CUDA EP cannot
+// run on the CPU EP): the graph is cut at tensors that carry all live state, each piece runs on the
+// HIP engine if the planner lowers it and it holds GEMM work, else on the CPU executor.
+struct HybridSegment {
+  bool hip = false;
+  int first = 0, last = -1;        // node range [first, last] in the model's topological order
+  std::string input, output;       // the cut tensors it reads / produces
+  int convs = 0;                   // Conv / Gemm / MatMul nodes
+  std::vector<int64_t> in_shape;   // per sample, batch dim = 1
+};
+std::vector<HybridSegment> hybrid_partition(const onnx::Model& m, int max_batch, bool split);
+// nullptr when the graph needs no CPU island (or no GPU is usable: `why`).
+std::unique_ptr<Engine> create_hybrid_engine(const std::string& model_path, const EngineOptions& opt, std::string* why);
 
 }  // namespace die

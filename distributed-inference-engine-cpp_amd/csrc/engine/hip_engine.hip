@@ -49,7 +49,9 @@ namespace {
 
 class HipEngine : public Engine {
  public:
-  HipEngine(const std::string& path, const EngineOptions& opt) : path_(path), opt_(opt) {
+  HipEngine(const std::string& path, const EngineOptions& opt) : HipEngine(path, onnx::load_onnx(path), opt) {}
+  // `model` given in memory (a segment of a hybrid HIP + CPU partition); `path` labels it
+  HipEngine(const std::string& path, onnx::Model model, const EngineOptions& opt) : path_(path), opt_(opt) {
     shard_id_ = opt.shard_id;
     dev_ = opt.device_id;
     HIP_CHECK(hipSetDevice(dev_));
@@ -60,7 +62,6 @@ class HipEngine : public Engine {
       throw std::runtime_error("HIP engine is built for gfx950 (MI355X); device reports " + arch_);
     max_batch_ = std::max(1, opt.max_batch);
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
-    onnx::Model model = onnx::load_onnx(path);
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
     plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
                        opt.fuse_pairs);
@@ -1587,6 +1588,16 @@ std::unique_ptr<Engine> create_hip_engine(const std::string& model_path, const E
     return nullptr;
   }
   return std::make_unique<HipEngine>(model_path, opt);
+}
+
+std::unique_ptr<Engine> create_hip_engine_model(const std::string& label, onnx::Model model, const EngineOptions& opt,
+                                                std::string* why) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || opt.device_id >= n) {
+    if (why) *why = "no HIP device visible";
+    return nullptr;
+  }
+  return std::make_unique<HipEngine>(label, std::move(model), opt);
 }
 
 }  // namespace die

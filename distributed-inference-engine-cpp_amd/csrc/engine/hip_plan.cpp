@@ -317,6 +317,27 @@ class Planner {
     return buf;
   }
 
+  // An image graph input (lazy: f32 NCHW plus any pending BN affine) consumed by something other
+  // than a conv's input load -- a ReLU, a pool, the residual operand of an Add: the input-prep
+  // pass materialises it as an NHWC tensor once (per value: the raw input and its BN'd form are
+  // two values) and every later reader sees that.  Hybrid HIP + CPU segments start at such inputs
+  // (engine/hybrid_engine.cpp: a ResNet segment begins at a unit's raw sum x).
+  Val materialize_in(const std::string& name, const Node& n) {
+    Val v = val(name, n);
+    if (v.kind != Val::GRAPH_IN) return v;
+    const int buf = ensure_nhwc_input(v, name);
+    Val o = v;
+    o.kind = Val::NHWC;
+    o.C = v.C <= 4 ? 4 : round8(v.C);
+    o.cl = o.C != v.C ? v.C : 0;
+    o.buf = buf;
+    o.has_affine = false;
+    o.asc.clear();
+    o.ash.clear();
+    define(name, o);
+    return o;
+  }
+
   void lower_conv(int idx) {
     const Node& n = m_.nodes[idx];
     Val x = val(n.in(0), n);
@@ -400,6 +421,7 @@ class Planner {
     } else if (c1 >= 0 && m_.nodes[c1].op_type == "Add") {
       const Node& add = m_.nodes[c1];
       const std::string other = add.in(0) == cur ? add.in(1) : add.in(0);
+      if (vid_.count(other) && vals_[vid_.at(other)].kind == Val::GRAPH_IN) materialize_in(other, add);
       auto it = vid_.find(other);
       if (it != vid_.end() && vals_[it->second].kind == Val::NHWC && vals_[it->second].C == Cp &&
           vals_[it->second].logical() == Cout && vals_[it->second].H == Ho && vals_[it->second].W == Wo &&
@@ -1570,7 +1592,7 @@ class Planner {
 
   void lower_relu(int idx) {
     const Node& n = m_.nodes[idx];
-    Val& x = val(n.in(0), n);
+    const Val x = materialize_in(n.in(0), n);
     standalone_affine(n, x, nullptr, nullptr, nullptr);
   }
 
@@ -1593,6 +1615,8 @@ class Planner {
       for (int k = 0; k < x.logical(); ++k) sh[k] = c[c.size() == 1 ? 0 : k];
       return standalone_affine(n, x, &sc, &sh, nullptr);
     }
+    for (int side = 0; side < 2; ++side)
+      if (vid_.count(n.in(side)) && vals_[vid_.at(n.in(side))].kind == Val::GRAPH_IN) materialize_in(n.in(side), n);
     if (lower_binary_acts(n)) return;
     const Val a = val(n.in(0), n);
     const Val b = val(n.in(1), n);
@@ -1759,7 +1783,7 @@ class Planner {
 
   void lower_pool(int idx) {
     const Node& n = m_.nodes[idx];
-    Val x = val(n.in(0), n);
+    Val x = materialize_in(n.in(0), n);
     if (x.kind != Val::NHWC) throw std::runtime_error(n.op_type + " " + n.name + ": input must be an image tensor");
     auto k = n.get_ints("kernel_shape");
     auto st = n.get_ints("strides", {1, 1});

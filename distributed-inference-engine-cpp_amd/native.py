@@ -700,6 +700,21 @@ def plan_report(model_path: str, precision: str = "fp32") -> Dict[str, Any]:
     return json.loads(_take_str(p))
 
 
+def hybrid_partition(model_path: str, max_batch: int = 8, precision: str = "fp32") -> List[Dict[str, Any]]:
+    """How a model splits into HIP and CPU-executor segments when some of its nodes cannot be lowered
+    (engine/hybrid_engine.cpp; runs on the CPU): [{device, first, last, input, output, gemm_nodes,
+    ops}] in execution order."""
+    L = lib()
+    fn = L.die_hybrid_partition
+    fn.restype = C.c_void_p
+    fn.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    err = _err_box()
+    p = fn(model_path.encode(), int(max_batch), int(precision == "fp32"), C.byref(err))
+    if not p:
+        _raise_if(err, "hybrid_partition")
+    return json.loads(_take_str(p))
+
+
 def kernels():
     """The raw kernel-launch entry points (see ops/kernels.py for the torch-facing wrappers)."""
     return _sig_kernels()
