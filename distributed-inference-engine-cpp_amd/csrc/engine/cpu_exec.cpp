@@ -332,6 +332,18 @@ CpuValuePtr op_unary(const Node& n, const CpuValue& x) {
   else if (op == "Neg") f = [](float v) { return -v; };
   else if (op == "Abs") f = [](float v) { return std::fabs(v); };
   else if (op == "Reciprocal") f = [](float v) { return 1.f / v; };
+  else if (op == "Sin") f = [](float v) { return std::sin(v); };
+  else if (op == "Cos") f = [](float v) { return std::cos(v); };
+  else if (op == "Floor") f = [](float v) { return std::floor(v); };
+  else if (op == "Ceil") f = [](float v) { return std::ceil(v); };
+  else if (op == "Round") f = [](float v) { return std::nearbyint(v); };  // half to even
+  else if (op == "Sign") f = [](float v) { return static_cast<float>((v > 0.f) - (v < 0.f)); };
+  else if (op == "HardSwish") f = [](float v) { return v * std::min(std::max(v / 6.f + 0.5f, 0.f), 1.f); };
+  else if (op == "Softplus") f = [](float v) { return v > 20.f ? v : std::log1p(std::exp(v)); };
+  else if (op == "HardSigmoid") {
+    const float al = n.get_float("alpha", 0.2f), be = n.get_float("beta", 0.5f);
+    f = [al, be](float v) { return std::min(std::max(al * v + be, 0.f), 1.f); };
+  }
   else if (op == "LeakyRelu") {
     const float al = n.get_float("alpha", 0.01f);
     f = [al](float v) { return v >= 0.f ? v : al * v; };
@@ -630,7 +642,8 @@ CpuValuePtr op_reduce(const Node& n, const std::vector<const CpuValue*>& in, int
     }
   }
   auto y = make_f(os);
-  std::vector<double> acc(static_cast<size_t>(y->numel()), 0.0);
+  const bool is_max = n.op_type == "ReduceMax";
+  std::vector<double> acc(static_cast<size_t>(y->numel()), is_max ? -std::numeric_limits<double>::infinity() : 0.0);
   auto xs = strides_of(x.shape), kst = strides_of(ks);
   const int64_t total = x.numel();
   int64_t cnt = 1;
@@ -643,7 +656,8 @@ CpuValuePtr op_reduce(const Node& n, const std::vector<const CpuValue*>& in, int
       rem %= xs[k];
       if (!red[k]) o += idx * kst[k];
     }
-    acc[o] += x.f[e];
+    if (is_max) acc[o] = std::max(acc[o], static_cast<double>(x.f[e]));
+    else acc[o] += x.f[e];
   }
   const bool mean = n.op_type == "ReduceMean";
   for (size_t k = 0; k < acc.size(); ++k) y->f[k] = static_cast<float>(mean ? acc[k] / cnt : acc[k]);
@@ -651,6 +665,86 @@ CpuValuePtr op_reduce(const Node& n, const std::vector<const CpuValue*>& in, int
 }
 
 }  // namespace
+
+// Pad: constant (value from the attribute or input 2), reflect or edge, any rank; negative pads crop.
+CpuValuePtr op_pad(const Node& n, const std::vector<const CpuValue*>& in) {
+  const CpuValue& x = *in[0];
+  const size_t r = x.shape.size();
+  std::vector<int64_t> pads = n.get_ints("pads");
+  if (pads.empty() && in.size() > 1 && in[1]) pads = as_ints(*in[1]);
+  float value = n.get_float("value", 0.f);
+  if (in.size() > 2 && in[2]) value = in[2]->is_int ? static_cast<float>(in[2]->i.at(0)) : in[2]->f.at(0);
+  std::vector<int64_t> full(2 * r, 0);
+  if (in.size() > 3 && in[3]) {  // opset 18 axes
+    auto axes = as_ints(*in[3]);
+    if (pads.size() != 2 * axes.size()) fail(n, "pads/axes mismatch");
+    for (size_t k = 0; k < axes.size(); ++k) {
+      const int64_t a = norm_axis(axes[k], r);
+      full[a] = pads[k];
+      full[a + r] = pads[k + axes.size()];
+    }
+  } else {
+    if (pads.size() != 2 * r) fail(n, "expected 2 * rank pads");
+    full = pads;
+  }
+  const std::string mode = n.get_string("mode", "constant");
+  std::vector<int64_t> os(r);
+  for (size_t k = 0; k < r; ++k) os[k] = x.shape[k] + full[k] + full[k + r];
+  auto y = make_f(os);
+  auto xs = strides_of(x.shape), ys = strides_of(os);
+  const int64_t total = y->numel();
+#pragma omp parallel for if (total > 1 << 16)
+  for (int64_t e = 0; e < total; ++e) {
+    int64_t rem = e, src = 0;
+    bool inside = true;
+    for (size_t k = 0; k < r; ++k) {
+      int64_t i = rem / ys[k] - full[k];
+      rem %= ys[k];
+      const int64_t D = x.shape[k];
+      if (i < 0 || i >= D) {
+        if (mode == "edge") i = i < 0 ? 0 : D - 1;
+        else if (mode == "reflect") {
+          const int64_t p = 2 * (D - 1);
+          i = p ? ((i % p) + p) % p : 0;
+          if (i >= D) i = p - i;
+        } else inside = false;
+      }
+      src += i * xs[k];
+    }
+    y->f[e] = inside ? x.f[src] : value;
+  }
+  return y;
+}
+
+// Split: sizes from the attribute (opset < 13), input 1, or equal parts (the last may be smaller).
+std::vector<CpuValuePtr> op_split(const Node& n, const std::vector<const CpuValue*>& in) {
+  const CpuValue& x = *in[0];
+  const size_t r = x.shape.size();
+  const int64_t axis = norm_axis(n.get_int("axis", 0), r);
+  std::vector<int64_t> sizes = n.get_ints("split");
+  if (sizes.empty() && in.size() > 1 && in[1]) sizes = as_ints(*in[1]);
+  const int64_t parts = static_cast<int64_t>(n.outputs.size()), D = x.shape[axis];
+  if (sizes.empty()) {
+    const int64_t each = (D + parts - 1) / parts;
+    for (int64_t k = 0, s = 0; k < parts; ++k, s += each) sizes.push_back(std::min(each, D - s));
+  }
+  int64_t outer = 1, inner = 1;
+  for (int64_t k = 0; k < axis; ++k) outer *= x.shape[k];
+  for (size_t k = axis + 1; k < r; ++k) inner *= x.shape[k];
+  std::vector<CpuValuePtr> outs;
+  int64_t s0 = 0;
+  for (int64_t k = 0; k < parts; ++k) {
+    auto os = x.shape;
+    os[axis] = sizes[k];
+    auto y = make_f(os);
+    for (int64_t o = 0; o < outer; ++o)
+      std::copy_n(x.f.data() + (o * D + s0) * inner, sizes[k] * inner, y->f.data() + o * sizes[k] * inner);
+    s0 += sizes[k];
+    outs.push_back(y);
+  }
+  if (s0 != D) fail(n, "split sizes do not cover the axis");
+  return outs;
+}
 
 // ------------------------------------------------------------------------------------------------
 
@@ -709,7 +803,8 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
         }
     } else if (op == "Relu" || op == "Sigmoid" || op == "Tanh" || op == "Erf" || op == "Sqrt" || op == "Exp" ||
                op == "Log" || op == "Neg" || op == "Abs" || op == "Reciprocal" || op == "LeakyRelu" ||
-               op == "Gelu") {
+               op == "Gelu" || op == "HardSigmoid" || op == "HardSwish" || op == "Softplus" || op == "Sin" || op == "Cos" ||
+               op == "Floor" || op == "Ceil" || op == "Round" || op == "Sign") {
       out = op_unary(n, *in[0]);
     } else if (op == "Clip") {
       float lo = -std::numeric_limits<float>::infinity(), hi = std::numeric_limits<float>::infinity();
@@ -820,8 +915,18 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
       out = op_softmax(n, *in[0], opset);
     } else if (op == "LayerNormalization") {
       out = op_layernorm(n, *in[0], in.size() > 1 ? in[1] : nullptr, in.size() > 2 ? in[2] : nullptr);
-    } else if (op == "ReduceMean" || op == "ReduceSum") {
+    } else if (op == "ReduceMean" || op == "ReduceSum" || op == "ReduceMax") {
       out = op_reduce(n, in, opset);
+    } else if (op == "Pad") {
+      out = op_pad(n, in);
+    } else if (op == "Split") {
+      auto outs = op_split(n, in);
+      for (size_t k = 1; k < outs.size(); ++k)
+        if (!n.outputs[k].empty()) {
+          env[n.outputs[k]] = outs[k];
+          if (trace) (*trace)[n.outputs[k]] = outs[k];
+        }
+      out = outs[0];
     } else {
       throw std::runtime_error("cpu executor: unsupported op " + op + " (" + n.name + ")");
     }

@@ -1046,7 +1046,7 @@ class HipEngine : public Engine {
         case PlanOp::UNARY:
           e = kern::unary_rows(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
                                static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, op.act, op.clip_lo,
-                               op.clip_hi, st, live, op.rows_per_sample, sp_);
+                               op.clip_hi, st, live, op.rows_per_sample, sp_, op.Cp);
           break;
         case PlanOp::CONV: {
           kern::ConvArgs a = conv_args(op, B, s);
@@ -1087,6 +1087,10 @@ class HipEngine : public Engine {
           e = kern::conv_pair(a, st);
           break;
         }
+        case PlanOp::PAD:
+          e = kern::pad_nhwc(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
+                             op.C, op.Ho, op.Wo, op.ph, op.pw, st, sp_);
+          break;
         case PlanOp::POOL:
           e = kern::pool2d(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
                            op.C, op.Ho, op.Wo, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.is_max, op.cip, st, live,
@@ -1094,7 +1098,7 @@ class HipEngine : public Engine {
           break;
         case PlanOp::GAP:
           e = kern::global_avgpool(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live, sp_);
+                                   nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live, sp_, op.gidx);
           break;
         case PlanOp::AFFINE:
           e = kern::affine_act(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
@@ -1219,8 +1223,8 @@ class HipEngine : public Engine {
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                   "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair"};
-    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::CONV_PAIR + 1, "one name per PlanOp kind");
+                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad"};
+    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::PAD + 1, "one name per PlanOp kind");
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

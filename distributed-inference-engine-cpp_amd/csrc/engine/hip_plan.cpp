@@ -281,11 +281,25 @@ class Planner {
     if (op == "Softmax") return lower_softmax(idx);
     if (op == "Clip") return lower_clip(idx);
     if (op == "ReduceMean") return lower_reduce_mean(idx);
+    if (op == "ReduceSum" || op == "ReduceMax") {
+      if (lower_spatial_reduce(idx, op == "ReduceSum" ? 1 : 2)) return;
+      throw std::runtime_error(op + " " + n.name + ": only reductions over the spatial axes of an image or the token axis of rows");
+    }
+    if (op == "GlobalMaxPool") return lower_gap(idx, 2);
+    if (op == "Max" || op == "Min") {
+      if (n.inputs.size() == 2 && lower_binary_acts(n)) return;
+      throw std::runtime_error(op + " " + n.name + ": only two activations of one shape (or a per-sample broadcast)");
+    }
+    if (op == "Pad") return lower_pad(idx);
+    if (op == "Split") return lower_split(idx);
     if (op == "Slice") return lower_slice(idx);
     if (op == "LayerNormalization") return lower_layernorm(idx);
     if (op == "Gather") return lower_gather(idx);
     if (op == "Concat") return lower_concat(idx);
-    if (op == "Sigmoid" || op == "Tanh" || op == "LeakyRelu" || op == "Gelu") return lower_unary(idx);
+    if (op == "Sigmoid" || op == "Tanh" || op == "LeakyRelu" || op == "Gelu" || op == "Exp" || op == "Abs" ||
+        op == "Sqrt" || op == "Neg" || op == "Reciprocal" || op == "Log" || op == "Erf" || op == "Pow" ||
+        op == "HardSigmoid" || op == "HardSwish" || op == "Softplus")
+      return lower_unary(idx);
     if (op == "Identity" || op == "Dropout") {
       Val v = val(n.in(0), n);
       define(n.outputs[0], v);
@@ -348,7 +362,7 @@ class Planner {
     const int KH = static_cast<int>(wt.dims[2]), KW = static_cast<int>(wt.dims[3]);
     auto st = n.get_ints("strides", {1, 1});
     auto dl = n.get_ints("dilations", {1, 1});
-    auto pads = n.get_ints("pads", {0, 0, 0, 0});
+    auto pads = conv_pads(n);
     if (st[0] != st[1] || dl[0] != dl[1]) throw std::runtime_error("Conv " + n.name + ": anisotropic stride/dilation");
     const std::string ap = n.get_string("auto_pad", "NOTSET");
     int in_buf;
@@ -1303,7 +1317,7 @@ class Planner {
       throw std::runtime_error("Conv " + n.name + ": grouped conv needs Cin = group * Cin/group and channels % 8 == 0");
     auto st = n.get_ints("strides", {1, 1});
     auto dl = n.get_ints("dilations", {1, 1});
-    auto pads = n.get_ints("pads", {0, 0, 0, 0});
+    auto pads = conv_pads(n);
     if (st[0] != st[1] || dl[0] != dl[1]) throw std::runtime_error("Conv " + n.name + ": anisotropic stride/dilation");
     const std::string ap = n.get_string("auto_pad", "NOTSET");
     if (ap == "SAME_UPPER" || ap == "SAME_LOWER") {
@@ -1395,36 +1409,42 @@ class Planner {
 
   // torch's LayerNorm export below opset 17: ReduceMean -> Sub -> Pow(2) -> ReduceMean -> Add(eps)
   // -> Sqrt -> Div [-> Mul(gamma)] [-> Add(beta)]  ==> one LAYERNORM op.
+  // ReduceMean / ReduceSum / ReduceMax over the spatial axes of an image or the token axis of
+  // rows: the GAP kernel in mode 0 / 1 / 2.  False when the reduction is some other one.
+  bool lower_spatial_reduce(int idx, int mode) {
+    const Node& n = m_.nodes[idx];
+    const Val x = materialize_in(n.in(0), n);
+    std::vector<int64_t> ax = n.get_ints("axes");
+    if (ax.empty() && n.inputs.size() > 1 && !n.in(1).empty()) ints_of(n.in(1), ax);
+    std::sort(ax.begin(), ax.end());
+    const bool keep = n.get_int("keepdims", 1) != 0;
+    const bool spatial = x.kind == Val::NHWC && (ax == std::vector<int64_t>{2, 3} || ax == std::vector<int64_t>{-2, -1});
+    const bool tokens = x.kind == Val::ROWS_BF16 && x.rank == 3 && (ax == std::vector<int64_t>{1} || ax == std::vector<int64_t>{-2});
+    if (!(spatial || tokens) || !dense(x)) return false;
+    PlanOp p;
+    p.kind = PlanOp::GAP;
+    p.gidx = mode;
+    p.name = n.name;
+    p.in = x.buf;
+    p.C = x.C;
+    p.H = x.H;
+    p.W = x.W;
+    p.out = new_buf(static_cast<size_t>(x.C) * 2);
+    Val o;
+    o.kind = spatial && keep ? Val::NHWC : Val::ROWS_BF16;
+    o.C = x.C;
+    o.cl = x.cl;
+    o.rank = tokens && keep ? 3 : 2;
+    o.buf = p.out;
+    define(n.outputs[0], o);
+    add_op(std::move(p));
+    return true;
+  }
+
   void lower_reduce_mean(int idx) {
     const Node& n = m_.nodes[idx];
+    if (lower_spatial_reduce(idx, 0)) return;
     const Val x = val(n.in(0), n);
-    {  // mean over the spatial axes of an image / the token axis of rows: the GAP kernel
-      std::vector<int64_t> ax = n.get_ints("axes");
-      if (ax.empty() && n.inputs.size() > 1 && !n.in(1).empty()) ints_of(n.in(1), ax);
-      std::sort(ax.begin(), ax.end());
-      const bool keep = n.get_int("keepdims", 1) != 0;
-      const bool spatial = x.kind == Val::NHWC && (ax == std::vector<int64_t>{2, 3} || ax == std::vector<int64_t>{-2, -1});
-      const bool tokens = x.kind == Val::ROWS_BF16 && x.rank == 3 && (ax == std::vector<int64_t>{1} || ax == std::vector<int64_t>{-2});
-      if ((spatial || tokens) && dense(x)) {
-        PlanOp p;
-        p.kind = PlanOp::GAP;
-        p.name = n.name;
-        p.in = x.buf;
-        p.C = x.C;
-        p.H = x.H;
-        p.W = x.W;
-        p.out = new_buf(static_cast<size_t>(x.C) * 2);
-        Val o;
-        o.kind = spatial && keep ? Val::NHWC : Val::ROWS_BF16;
-        o.C = x.C;
-        o.cl = x.cl;
-        o.rank = tokens && keep ? 3 : 2;
-        o.buf = p.out;
-        define(n.outputs[0], o);
-        add_op(std::move(p));
-        return;
-      }
-    }
     auto fail = [&](const std::string& why) {
       throw std::runtime_error("ReduceMean " + n.name + ": only the decomposed LayerNormalization pattern is supported (" +
                                why + ")");
@@ -1496,6 +1516,113 @@ class Planner {
   }
 
   // Slice of one token along axis 1 of [B, S, C] rows (e.g. the cls token) -> row gather.
+  // Explicit pads of a conv plus those of a zero Pad folded into it (lower_pad).
+  std::vector<int64_t> conv_pads(const Node& n) const {
+    auto pads = n.get_ints("pads", {0, 0, 0, 0});
+    if (pads.size() != 4) throw std::runtime_error("Conv " + n.name + ": expected 4 pads");
+    auto it = folded_pad_.find(n.in(0));
+    if (it != folded_pad_.end())
+      for (int k = 0; k < 4; ++k) pads[k] += it->second[k];
+    return pads;
+  }
+
+  // Pad (constant mode, value 0, spatial axes of an NHWC image only, /root/reference has no Pad
+  // kernel -- ONNX Runtime's CPU EP runs it there).  A Pad whose only reader is a Conv with explicit
+  // pads folds into that conv (the conv kernels read out-of-range pixels as zero); otherwise one
+  // NHWC pad pass writes the padded image.
+  void lower_pad(int idx) {
+    const Node& n = m_.nodes[idx];
+    if (n.get_string("mode", "constant") != "constant") throw std::runtime_error("Pad " + n.name + ": only constant mode");
+    std::vector<int64_t> pads = n.get_ints("pads");
+    float value = n.get_float("value", 0.f);
+    if (pads.empty() && n.inputs.size() >= 2) ints_of(n.in(1), pads);
+    if (n.inputs.size() >= 3 && !n.in(2).empty()) {
+      const auto& cv = init(n.in(2), n);
+      value = cv.f.empty() ? (cv.i.empty() ? 0.f : static_cast<float>(cv.i[0])) : cv.f[0];
+    }
+    if (n.inputs.size() >= 4 && !n.in(3).empty()) throw std::runtime_error("Pad " + n.name + ": the axes input is not supported");
+    if (value != 0.f) throw std::runtime_error("Pad " + n.name + ": only zero padding");
+    const Val x = materialize_in(n.in(0), n);
+    if (x.kind != Val::NHWC || pads.size() != 8 || pads[0] || pads[1] || pads[4] || pads[5])
+      throw std::runtime_error("Pad " + n.name + ": only the spatial axes of an [N, C, H, W] image");
+    for (auto v : pads)
+      if (v < 0) throw std::runtime_error("Pad " + n.name + ": negative pads (cropping) are not supported");
+    const std::array<int64_t, 4> tlbr{{pads[2], pads[3], pads[6], pads[7]}};
+    const int c = sole_consumer(n.outputs[0]);
+    if (c >= 0 && m_.nodes[c].op_type == "Conv" && m_.nodes[c].in(0) == n.outputs[0] &&
+        m_.nodes[c].get_string("auto_pad", "NOTSET") == "NOTSET") {
+      folded_pad_[n.outputs[0]] = tlbr;
+      define(n.outputs[0], x);
+      return;
+    }
+    PlanOp p;
+    p.kind = PlanOp::PAD;
+    p.name = n.name;
+    p.in = x.buf;
+    p.C = x.C;
+    p.H = x.H;
+    p.W = x.W;
+    p.ph = static_cast<int>(tlbr[0]);
+    p.pw = static_cast<int>(tlbr[1]);
+    p.Ho = x.H + static_cast<int>(tlbr[0] + tlbr[2]);
+    p.Wo = x.W + static_cast<int>(tlbr[1] + tlbr[3]);
+    p.out = new_buf(static_cast<size_t>(p.Ho) * p.Wo * x.C * 2);
+    Val o = x;
+    o.H = p.Ho;
+    o.W = p.Wo;
+    o.buf = p.out;
+    define(n.outputs[0], o);
+    add_op(std::move(p));
+  }
+
+  // Channel range [s0, e0) of a dense image / rows value -> a column copy (s0 % 8 == 0).
+  void emit_channel_slice(const Node& n, const Val& x, int64_t s0, int64_t e0, const std::string& out) {
+    const int len = static_cast<int>(e0 - s0), Cs = round8(len);
+    PlanOp p;
+    p.kind = PlanOp::COPY_COLS;
+    p.name = n.name;
+    p.in = x.buf;
+    p.col[0] = static_cast<int>(s0);
+    p.ld[0] = x.C;
+    p.col[1] = 0;
+    p.ld[1] = Cs;
+    p.C = std::min(Cs, x.C - static_cast<int>(s0));
+    p.rows_per_sample = rows_of(x);
+    p.out = new_buf(static_cast<size_t>(rows_of(x)) * Cs * 2);
+    Val o = x;
+    o.C = Cs;
+    o.cl = Cs != len ? len : 0;
+    o.buf = p.out;
+    define(out, o);
+    add_op(std::move(p));
+  }
+
+  // Split along the channel axis (sizes from the attribute, the input, or equal parts): one column
+  // copy per output; every boundary but the end must be a multiple of 8.
+  void lower_split(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = materialize_in(n.in(0), n);
+    const int64_t axis = n.get_int("axis", 0);
+    if (!dense(x) || !is_channel_axis(x, axis))
+      throw std::runtime_error("Split " + n.name + ": only along the channel axis of an image or rows");
+    std::vector<int64_t> sizes = n.get_ints("split");
+    if (sizes.empty() && n.inputs.size() >= 2 && !n.in(1).empty()) ints_of(n.in(1), sizes);
+    const int64_t Cl = x.logical(), parts = static_cast<int64_t>(n.outputs.size());
+    if (sizes.empty()) {
+      const int64_t each = (Cl + parts - 1) / parts;  // equal parts (opset 18: the last may be smaller)
+      for (int64_t k = 0, s = 0; k < parts; ++k, s += each) sizes.push_back(std::min(each, Cl - s));
+    }
+    if (static_cast<int64_t>(sizes.size()) != parts) throw std::runtime_error("Split " + n.name + ": sizes/outputs mismatch");
+    int64_t s0 = 0;
+    for (int64_t k = 0; k < parts; ++k) {
+      if (s0 % 8 || sizes[k] <= 0 || s0 + sizes[k] > Cl)
+        throw std::runtime_error("Split " + n.name + ": parts must start at multiples of 8 channels");
+      if (!n.outputs[k].empty()) emit_channel_slice(n, x, s0, s0 + sizes[k], n.outputs[k]);
+      s0 += sizes[k];
+    }
+    if (s0 != Cl) throw std::runtime_error("Split " + n.name + ": sizes do not cover the axis");
+  }
+
   void lower_slice(int idx) {
     const Node& n = m_.nodes[idx];
     const Val x = val(n.in(0), n);
@@ -1540,24 +1667,7 @@ class Planner {
       int64_t s0 = starts[0] < 0 ? starts[0] + Cl : std::min<int64_t>(starts[0], Cl);
       int64_t e0 = ends[0] < 0 ? ends[0] + Cl : std::min<int64_t>(ends[0], Cl);
       if (s0 >= 0 && e0 > s0 && s0 % 8 == 0 && (e0 % 8 == 0 || e0 == Cl)) {
-        const int len = static_cast<int>(e0 - s0), Cs = round8(len);
-        PlanOp p;
-        p.kind = PlanOp::COPY_COLS;
-        p.name = n.name;
-        p.in = x.buf;
-        p.col[0] = static_cast<int>(s0);
-        p.ld[0] = x.C;
-        p.col[1] = 0;
-        p.ld[1] = Cs;
-        p.C = std::min(Cs, x.C - static_cast<int>(s0));
-        p.rows_per_sample = rows_of(x);
-        p.out = new_buf(static_cast<size_t>(rows_of(x)) * Cs * 2);
-        Val o = x;
-        o.C = Cs;
-        o.cl = Cs != len ? len : 0;
-        o.buf = p.out;
-        define(n.outputs[0], o);
-        add_op(std::move(p));
+        emit_channel_slice(n, x, s0, e0, n.outputs[0]);
         return;
       }
     }
@@ -1633,12 +1743,27 @@ class Planner {
 
   void lower_unary(int idx) {
     const Node& n = m_.nodes[idx];
-    const Val x = val(n.in(0), n);
+    const Val x = materialize_in(n.in(0), n);
     const std::string& op = n.op_type;
     if (op == "Gelu" && n.get_string("approximate", "none") != "none")
       throw std::runtime_error("Gelu " + n.name + ": only the exact (erf) form is supported");
-    const int act = op == "Sigmoid" ? 4 : op == "Tanh" ? 5 : op == "LeakyRelu" ? 6 : 2;
-    emit_unary(n, x, act, op == "LeakyRelu" ? n.get_float("alpha", 0.01f) : 0.f, 0.f, n.outputs[0]);
+    static const std::map<std::string, int> codes = {
+        {"Gelu", 2}, {"Sigmoid", 4}, {"Tanh", 5}, {"LeakyRelu", 6}, {"Exp", 7}, {"Abs", 8}, {"Sqrt", 9}, {"Neg", 10},
+        {"Reciprocal", 11}, {"Log", 12}, {"Erf", 13}, {"Pow", 14}, {"HardSigmoid", 15}, {"HardSwish", 16}, {"Softplus", 17}};
+    const int act = codes.at(op);
+    float a = 0.f, b = 0.f;
+    if (op == "LeakyRelu") a = n.get_float("alpha", 0.01f);
+    if (op == "HardSigmoid") {
+      a = n.get_float("alpha", 0.2f);
+      b = n.get_float("beta", 0.5f);
+    }
+    if (op == "Pow") {  // activation ^ scalar constant
+      auto it = m_.initializers.find(n.in(1));
+      if (it == m_.initializers.end() || it->second.f.size() != 1)
+        throw std::runtime_error("Pow " + n.name + ": the exponent must be a scalar constant");
+      a = it->second.f[0];
+    }
+    emit_unary(n, x, act, a, b, n.outputs[0]);
   }
 
   void emit_unary(const Node& n, const Val& x, int act, float a, float b, const std::string& out_name) {
@@ -1651,6 +1776,7 @@ class Planner {
     p.clip_lo = a;
     p.clip_hi = b;
     p.C = x.C;
+    p.Cp = x.logical();  // pad columns are written 0 (exp(0) = 1, 1/0 = inf must not reach a GEMM)
     p.rows_per_sample = rows_of(x);
     p.out = new_buf(static_cast<size_t>(rows_of(x)) * x.C * 2);
     Val o = x;
@@ -1665,8 +1791,11 @@ class Planner {
   // GLU-style gating).  Returns false when the operands do not fit (the caller tries other forms).
   bool lower_binary_acts(const Node& n) {
     if (n.inputs.size() != 2 || !vid_.count(n.in(0)) || !vid_.count(n.in(1))) return false;
-    const int op = n.op_type == "Add" ? 0 : n.op_type == "Sub" ? 1 : n.op_type == "Mul" ? 2 : n.op_type == "Div" ? 3 : -1;
+    const std::string& t = n.op_type;
+    const int op = t == "Add" ? 0 : t == "Sub" ? 1 : t == "Mul" ? 2 : t == "Div" ? 3 : t == "Max" ? 4 : t == "Min" ? 5 : -1;
     if (op < 0) return false;
+    for (int side = 0; side < 2; ++side)
+      if (vals_[vid_.at(n.in(side))].kind == Val::GRAPH_IN) materialize_in(n.in(side), n);
     Val a = vals_[vid_.at(n.in(0))], b = vals_[vid_.at(n.in(1))];
     if (!dense(a) || !dense(b) || a.C != b.C || a.logical() != b.logical()) return false;
     int ymode;
@@ -1675,7 +1804,7 @@ class Planner {
       ymode = 0;
     } else if (rows_of(b) == 1 && rows_of(a) > 1) {
       ymode = 1;
-    } else if (rows_of(a) == 1 && rows_of(b) > 1 && (op == 0 || op == 2)) {
+    } else if (rows_of(a) == 1 && rows_of(b) > 1 && (op == 0 || op == 2 || op == 4 || op == 5)) {
       std::swap(a, b);  // commutative: broadcast operand second
       ymode = 1;
     } else {
@@ -1822,12 +1951,14 @@ class Planner {
     add_op(std::move(p));
   }
 
-  void lower_gap(int idx) {
+  // GlobalAveragePool (mode 0) / GlobalMaxPool (mode 2)
+  void lower_gap(int idx, int mode = 0) {
     const Node& n = m_.nodes[idx];
-    Val x = val(n.in(0), n);
-    if (x.kind != Val::NHWC) throw std::runtime_error("GlobalAveragePool: input must be an image tensor");
+    Val x = materialize_in(n.in(0), n);
+    if (x.kind != Val::NHWC) throw std::runtime_error(n.op_type + ": input must be an image tensor");
     PlanOp p;
     p.kind = PlanOp::GAP;
+    p.gidx = mode;
     p.name = n.name;
     p.in = x.buf;
     p.C = x.C;
@@ -2133,6 +2264,7 @@ class Planner {
   std::unordered_map<std::string, std::vector<int>> consumers_;
   std::unordered_set<std::string> graph_outputs_;
   std::unordered_map<std::string, int> prepped_;
+  std::unordered_map<std::string, std::array<int64_t, 4>> folded_pad_;  // Pad output -> (t, l, b, r) for its conv
   std::vector<bool> done_;
 };
 

@@ -46,7 +46,8 @@ struct PlanOp {
     UNARY,      // out = act(in * scale + shift) with any activation code
     // ResNet-v2 bottleneck boundary in one launch (kernels/conv_pair.hip): a dual-store 1x1 expand
     // conv fused with the 1x1 reduce conv that is the sole reader of its pre-activation output
-    CONV_PAIR
+    CONV_PAIR,
+    PAD  // NHWC zero padding (ONNX Pad not folded into a conv): out [Ho][Wo] = in [H][W] at (ph, pw)
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).

@@ -83,6 +83,9 @@ __global__ void copy_cols_kernel(const uint16_t* __restrict__ x, long long xplan
   }
 }
 
+// Activation codes (kernels.h unary_rows).  The transcendental ones use the accurate libm forms
+// (not the __expf-style intrinsics): they also serve the fp32 (split) mode, whose values carry
+// ~16 significant bits.
 __device__ __forceinline__ float apply_act(float v, int act, float a, float b) {
   switch (act) {
     case 1: return fmaxf(v, 0.f);
@@ -91,6 +94,17 @@ __device__ __forceinline__ float apply_act(float v, int act, float a, float b) {
     case 4: return 1.f / (1.f + __expf(-v));
     case 5: return tanhf(v);
     case 6: return v >= 0.f ? v : v * a;
+    case 7: return expf(v);
+    case 8: return fabsf(v);
+    case 9: return sqrtf(v);
+    case 10: return -v;
+    case 11: return 1.f / v;
+    case 12: return logf(v);
+    case 13: return erff(v);
+    case 14: return a == 2.f ? v * v : a == 0.5f ? sqrtf(v) : a == 1.f ? v : powf(v, a);
+    case 15: return fminf(fmaxf(a * v + b, 0.f), 1.f);                   // HardSigmoid(alpha, beta)
+    case 16: return v * fminf(fmaxf(v * (1.f / 6.f) + 0.5f, 0.f), 1.f);  // HardSwish
+    case 17: return v > 20.f ? v : log1pf(expf(v));                       // Softplus
     default: return v;
   }
 }
@@ -116,7 +130,12 @@ __global__ void binary_kernel(const uint16_t* __restrict__ x, const uint16_t* __
     load8v(y + yr * C + c, yplane, split != 0, w);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      float v = op == 0 ? u[t] + w[t] : op == 1 ? u[t] - w[t] : op == 2 ? u[t] * w[t] : u[t] / w[t];
+      float v = op == 0   ? u[t] + w[t]
+                : op == 1 ? u[t] - w[t]
+                : op == 2 ? u[t] * w[t]
+                : op == 3 ? u[t] / w[t]
+                : op == 4 ? fmaxf(u[t], w[t])
+                          : fminf(u[t], w[t]);
       u[t] = c + t < Cl ? apply_act(v, act, a, b) : 0.f;  // pad columns stay 0 (finite)
     }
     store8v(out + r * C + c, plane, split != 0, u);
@@ -128,7 +147,7 @@ __global__ void binary_kernel(const uint16_t* __restrict__ x, const uint16_t* __
 __global__ void unary_kernel(const uint16_t* __restrict__ x, const float* __restrict__ scale,
                              const float* __restrict__ shift, uint16_t* __restrict__ y, long long R, int C, int act,
                              float a, float b, long long rows_per_sample, const long long* __restrict__ live,
-                             int split) {
+                             int split, int Cl) {
   const long long plane = R * C;
   long long Rl = R;
   if (live) Rl = min(R, *live * rows_per_sample);
@@ -143,9 +162,36 @@ __global__ void unary_kernel(const uint16_t* __restrict__ x, const float* __rest
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const float s = scale ? scale[c + t] : 1.f, h = scale ? shift[c + t] : 0.f;
-      v[t] = apply_act(v[t] * s + h, act, a, b);
+      v[t] = c + t < Cl ? apply_act(v[t] * s + h, act, a, b) : 0.f;  // pad columns stay 0 (1/0, log 0)
     }
     store8v(y + r * C + c, plane, split != 0, v);
+  }
+}
+
+// Zero padding of an NHWC image: y [B][Ho][Wo][C] holds x [B][H][W][C] at offset (t, l), zeros
+// around it (ONNX Pad, constant mode, value 0, spatial axes only).
+__global__ void pad_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
+                                int Ho, int Wo, int t, int l, long long xplane, long long yplane, int split) {
+  const int G = C / 8;
+  const long long total = static_cast<long long>(B) * Ho * Wo * G;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int cg = static_cast<int>(i % G);
+    long long r = i / G;
+    const int w = static_cast<int>(r % Wo);
+    r /= Wo;
+    const int h = static_cast<int>(r % Ho);
+    const long long b = r / Ho;
+    const int sh = h - t, sw = w - l;
+    uint16_t* d = y + ((b * Ho + h) * Wo + w) * C + cg * 8;
+    uint4 hi = make_uint4(0, 0, 0, 0), lo = hi;
+    if (sh >= 0 && sh < H && sw >= 0 && sw < W) {
+      const uint16_t* s = x + ((b * H + sh) * W + sw) * C + cg * 8;
+      hi = *reinterpret_cast<const uint4*>(s);
+      if (split) lo = *reinterpret_cast<const uint4*>(s + xplane);
+    }
+    *reinterpret_cast<uint4*>(d) = hi;
+    if (split) *reinterpret_cast<uint4*>(d + yplane) = lo;
   }
 }
 
@@ -177,6 +223,15 @@ __global__ void nhwc_to_nchw_strided_kernel(const uint16_t* __restrict__ x, floa
 
 }  // namespace
 
+hipError_t pad_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int t, int l,
+                    hipStream_t s, int split) {
+  if (C % 8 || t < 0 || l < 0 || Ho < H + t || Wo < W + l) return hipErrorInvalidValue;
+  const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(pad_nhwc_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, t, l,
+                     static_cast<long long>(B) * H * W * C, static_cast<long long>(B) * Ho * Wo * C, split);
+  return hipGetLastError();
+}
+
 hipError_t rows_prep(const float* x, uint16_t* y, long long R, int F, int Fp, hipStream_t s, int split) {
   if (Fp % 8 || Fp < F || F <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rows_prep_kernel, dim3(grid_for(R * (Fp / 8))), dim3(256), 0, s, x, y, R, F, Fp, split);
@@ -203,7 +258,7 @@ hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uin
 hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
                        int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live, int split,
                        int Cl) {
-  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 3 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 5 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
   if (Cl == 0) Cl = C;
   const long long plane = R * C;
   const long long yplane = ymode == 1 ? (R / rows_per_sample) * C : plane;
@@ -214,10 +269,10 @@ hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long
 
 hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, long long R, int C,
                       int act, float a, float b, hipStream_t s, const long long* live, long long rows_per_sample,
-                      int split) {
-  if (C % 8 || (live && rows_per_sample <= 0)) return hipErrorInvalidValue;
+                      int split, int Cl) {
+  if (C % 8 || (live && rows_per_sample <= 0) || Cl < 0 || Cl > C || act < 0 || act > 17) return hipErrorInvalidValue;
   hipLaunchKernelGGL(unary_kernel, dim3(grid_for(R * (C / 8))), dim3(256), 0, s, x, scale, shift, y, R, C, act, a, b,
-                     rows_per_sample, live, split);
+                     rows_per_sample, live, split, Cl ? Cl : C);
   return hipGetLastError();
 }
 

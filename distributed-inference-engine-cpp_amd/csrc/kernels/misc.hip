@@ -113,9 +113,10 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
 // Grid: (C/8 groups / 8, B) blocks of 256 threads = 8 channel groups x 32 row-slices.  ResNet50's
 // head (B~20, 7x7x2048) gets 16x more blocks than one-block-per-64-groups and each thread issues
 // its ~3 16-byte loads back to back, so the 4 MB read is not latency-bound on ~80 blocks.
+// mode 0 mean, 1 sum, 2 max over the HW pixels of each (sample, channel)
 __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
                            const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
-                           const long long* __restrict__ live, int split) {
+                           const long long* __restrict__ live, int split, int mode) {
   const long long xplane = static_cast<long long>(gridDim.y) * HW * C, oplane = static_cast<long long>(gridDim.y) * C;
   constexpr int G = 8, S = 32;
   __shared__ float part[S][G][9];  // +1 pad: the reduction reads S slices of one group
@@ -124,7 +125,8 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
   const int gl = threadIdx.x % G, slice = threadIdx.x / G;
   const int g = blockIdx.x * G + gl;
   const int CG = C / 8;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const float init = mode == 2 ? -INFINITY : 0.f;
+  float acc[8] = {init, init, init, init, init, init, init, init};
   if (g < CG) {
     float sc[8], sf[8];
 #pragma unroll
@@ -141,7 +143,7 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
       for (int t = 0; t < 8; ++t) {
         float u = v[t] * sc[t] + sf[t];
         if (relu) u = fmaxf(u, 0.f);
-        acc[t] += u;
+        acc[t] = mode == 2 ? fmaxf(acc[t], u) : acc[t] + u;
       }
     }
   }
@@ -149,13 +151,13 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
   for (int t = 0; t < 8; ++t) part[slice][gl][t] = acc[t];
   __syncthreads();
   if (slice == 0 && g < CG) {
-    const float inv = 1.f / HW;
+    const float inv = mode == 0 ? 1.f / HW : 1.f;
     float r[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      float sum = 0.f;
+      float sum = mode == 2 ? -INFINITY : 0.f;
 #pragma unroll
-      for (int k = 0; k < S; ++k) sum += part[k][gl][t];
+      for (int k = 0; k < S; ++k) sum = mode == 2 ? fmaxf(sum, part[k][gl][t]) : sum + part[k][gl][t];
       r[t] = sum * inv;
     }
     if (out) store8v(out + static_cast<long long>(b) * C + g * 8, oplane, split != 0, r);
@@ -252,11 +254,11 @@ hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, in
 }
 
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
-                          int relu, int B, int HW, int C, hipStream_t s, const long long* live, int split) {
-  if (C % 8) return hipErrorInvalidValue;
+                          int relu, int B, int HW, int C, hipStream_t s, const long long* live, int split, int mode) {
+  if (C % 8 || mode < 0 || mode > 2) return hipErrorInvalidValue;
   const int CG = C / 8;
   dim3 grid((CG + 7) / 8, B);  // 8 channel groups x 32 pixel slices per block
-  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split);
+  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split, mode);
   return hipGetLastError();
 }
 

@@ -13,6 +13,10 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
               Slice, and a Flatten of a 4x4 map (NCHW order) into the classifier.
 * `ratio_mlp` a Div of two activations of width 10 (stored with 16 channels) feeding a Gemm: the
               pad columns of both operands are 0, so 0/0 must not reach the next GEMM.
+* `ops_zoo`   the elementwise / data-movement ops of the wider ONNX op set on an image and on rows:
+              Pad folded into a conv, Pad before a MaxPool (a pad pass), HardSwish, channel Split,
+              Abs / Neg / Exp / Softplus / HardSigmoid / Max / Min / Pow / Reciprocal / Log / Sqrt /
+              Erf, ReduceMax / ReduceSum over the spatial axes, GlobalMaxPool, a rows Split.
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -30,6 +34,7 @@ SPECS = {
     "bert": dict(seq=32, dim=128, heads=2, ffn=256, layers=2, classes=3),
     "se_cnn": dict(in_ch=12, image=16, classes=10),
     "ratio_mlp": dict(in_features=40, hidden=10, classes=5),
+    "ops_zoo": dict(in_ch=8, image=16, classes=10),
 }
 
 
@@ -199,7 +204,55 @@ def build_ratio_mlp(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np
     return g.model_proto(opset=opset), {}
 
 
-BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp}
+def build_ops_zoo(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["ops_zoo"]
+    rng = _rng(seed)
+    g = GraphBuilder(name="ops_zoo")
+    x = g.input("image", ["N", s["in_ch"], s["image"], s["image"]])
+    one = g.const(np.array(1.0, np.float32), "one")
+    two = g.const(np.array(2.0, np.float32), "two")
+
+    def conv(inp, name, cin, cout, k, pad):
+        w = g.init(name + ".weight", _lin(rng, cin * k * k, (cout, cin, k, k)))
+        b = g.init(name + ".bias", (0.1 * rng.standard_normal(cout)).astype(np.float32))
+        return g.node("Conv", [inp, w, b], name=name, kernel_shape=[k, k], pads=[pad] * 4)
+
+    # relu first so the graph input is materialised once; Pad(1) folded into the 3x3 conv (pads 0)
+    h = g.node("Relu", [x], name="in_relu")
+    h = g.node("Pad", [h, g.const(np.array([0, 0, 1, 1, 0, 0, 1, 1], np.int64), "pad1")], name="pad1", mode="constant")
+    h = g.node("HardSwish", [conv(h, "conv1", s["in_ch"], 16, 3, 0)], name="hswish")
+    # asymmetric Pad before a MaxPool: not foldable (zeros vs -inf) -> a pad pass; 17x17 -> 8x8
+    h = g.node("Pad", [h, g.const(np.array([0, 0, 0, 1, 0, 0, 1, 0], np.int64), "pad2")], name="pad2", mode="constant")
+    h = g.node("MaxPool", [h], name="pool", kernel_shape=[2, 2], strides=[2, 2])
+    a, b = g.node("Split", [h, g.const(np.array([8, 8], np.int64), "split_sizes")], name="split", axis=1, n_out=2)
+    a = g.node("Exp", [g.node("Neg", [g.node("Abs", [a], name="abs")], name="neg")], name="exp")  # (0, 1]
+    sp = g.node("Softplus", [b], name="softplus")
+    hs = g.node("HardSigmoid", [b], name="hsigmoid", alpha=0.25, beta=0.4)
+    mx = g.node("Max", [a, sp], name="max")
+    mn = g.node("Min", [a, hs], name="min")
+    h = g.node("Concat", [mx, mn], name="cat", axis=1)  # 16 channels
+    h = conv(h, "conv2", 16, 12, 1, 0)  # 12 % 8 != 0
+    r = g.node("Reciprocal", [g.node("Add", [g.node("Pow", [h, two], name="pow"), one], name="pow1")], name="recip")
+    h = g.node("Erf", [g.node("Log", [r], name="log")], name="erf")  # log of (0, 1]
+    h = g.node("Sqrt", [g.node("Abs", [h], name="abs2")], name="sqrt")
+    rmax = g.node("ReduceMax", [h], name="rmax", axes=[2, 3], keepdims=1)
+    rsum = g.node("ReduceSum", [h, g.const(np.array([2, 3], np.int64), "rsum_axes")], name="rsum", keepdims=1)
+    gmax = g.node("GlobalMaxPool", [h], name="gmax")
+    z = g.node("Add", [g.node("Add", [rmax, rsum], name="pool_add"), gmax], name="pool_add2")
+    z = g.node("Flatten", [z], name="flatten", axis=1)  # rows [N, 12]
+    z = g.node("Gemm", [z, g.init("fc1.weight", _lin(rng, 12, (16, 12))),
+                        g.init("fc1.bias", (0.1 * rng.standard_normal(16)).astype(np.float32))], name="fc1", transB=1)
+    u, v = g.node("Split", [z], name="row_split", axis=1, n_out=2)  # equal parts of rows
+    z = g.node("Concat", [g.node("HardSwish", [u], name="row_hswish"), g.node("Softplus", [v], name="row_softplus")],
+               name="row_cat", axis=1)
+    w = g.init("fc2.weight", _lin(rng, 16, (s["classes"], 16)))
+    y = g.node("Gemm", [z, w, g.init("fc2.bias", np.zeros(s["classes"], np.float32))], name="fc2", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
+BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
+            "ops_zoo": build_ops_zoo}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:

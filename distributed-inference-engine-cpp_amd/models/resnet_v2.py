@@ -127,10 +127,11 @@ def make_weights(cfg: ResNetConfig) -> Tuple[Dict[str, np.ndarray], list]:
 
 def build_onnx(cfg: ResNetConfig = ResNetConfig(), opset: int = 7, dynamic_batch: bool = True,
                initializers_as_inputs: bool = True, inject_unit: int = -1,
-               inject_op: str = "Abs") -> Tuple[bytes, Dict[str, np.ndarray]]:
-    """inject_unit >= 0: an `inject_op` node (Abs: the identity on the ReLU output it follows, so the
-    model's function is unchanged) after that unit's second activation -- a node the HIP planner
-    may not lower, for the hybrid HIP + CPU tests (engine/hybrid_engine.cpp)."""
+               inject_op: str = "Sign") -> Tuple[bytes, Dict[str, np.ndarray]]:
+    """inject_unit >= 0: an `inject_op` node after that unit's second activation -- a node the HIP
+    planner may not lower, for the hybrid HIP + CPU tests (engine/hybrid_engine.cpp).  Sign is
+    applied as y * Sign(y), the identity on the ReLU output it follows; any other op is applied as
+    is (it should be the identity on y >= 0, e.g. Abs), so the model's function is unchanged."""
     w, ops = make_weights(cfg)
     p = cfg.prefix
     g = GraphBuilder(name="resnet_v2", initializers_as_inputs=initializers_as_inputs)
@@ -168,7 +169,8 @@ def build_onnx(cfg: ResNetConfig = ResNetConfig(), opset: int = 7, dynamic_batch
             y = conv(y, n["conv2"], 3, u["stride"], 1)
             y = g.node("Relu", [bn(y, n["bn3"])], name=u["tag"] + "_activation2")
             if i == inject_unit:
-                y = g.node(inject_op, [y], name=u["tag"] + "_injected")
+                z = g.node(inject_op, [y], name=u["tag"] + "_injected")
+                y = g.node("Mul", [y, z], name=u["tag"] + "_injected_mul") if inject_op == "Sign" else z
             y = conv(y, n["conv3"], 1, 1, 0)
         else:
             y = conv(a, n["conv1"], 3, u["stride"], 1)

@@ -13,13 +13,13 @@ def _odd_model(path):
     _unsupported_model(path)
 
 
-def test_partition_of_abs_exp_model(native, tmp_path):
+def test_partition_of_sin_cos_model(native, tmp_path):
     p = str(tmp_path / "odd.onnx")
     _odd_model(p)
     segs = native.hybrid_partition(p)
     assert [s["device"] for s in segs] == ["hip", "cpu"], segs
     assert segs[0]["ops"] == ["Conv"] and segs[0]["input"] == "x"
-    assert sorted(segs[1]["ops"]) == ["Abs", "Add", "Exp", "Relu"]
+    assert sorted(segs[1]["ops"]) == ["Add", "Cos", "Relu", "Sin"]
 
 
 @pytest.fixture(scope="module")
@@ -28,7 +28,7 @@ def injected_rn50(native, tmp_path_factory):
 
     cfg = r.ResNetConfig()
     blob, w = r.build_onnx(cfg, inject_unit=4)  # stage 2, second unit (0-based unit index 4)
-    p = str(tmp_path_factory.mktemp("hyb") / "rn50_abs.onnx")
+    p = str(tmp_path_factory.mktemp("hyb") / "rn50_sign.onnx")
     open(p, "wb").write(blob)
     return p, w, cfg
 
@@ -41,12 +41,12 @@ def test_partition_keeps_ninety_percent_of_resnet_convs_on_gpu(native, injected_
     on_gpu = sum(s["gemm_nodes"] for s in segs if s["device"] == "hip")
     assert gemm == 54 and on_gpu / gemm >= 0.9, (on_gpu, gemm)
     cpu = segs[1]
-    assert "Abs" in cpu["ops"] and cpu["gemm_nodes"] == 3  # just the unit holding the Abs
+    assert "Sign" in cpu["ops"] and cpu["gemm_nodes"] == 3  # just the unit holding the Sign
 
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_available(), reason="needs a GPU")
-def test_hybrid_engine_abs_exp_model_matches_cpu_oracle(native, tmp_path):
+def test_hybrid_engine_sin_cos_model_matches_cpu_oracle(native, tmp_path):
     p = str(tmp_path / "odd.onnx")
     _odd_model(p)
     eng = native.Engine(p, device="auto", max_batch=4)
@@ -78,7 +78,7 @@ def test_hybrid_engine_resnet50_with_injected_op(native, injected_rn50):
         for B in (1, 8):
             x = r.synthetic_input(B, cfg, seed=70 + B)
             with torch.no_grad():
-                ref = r.torch_forward(w, x, cfg, device="cuda").double().cpu().numpy()  # Abs(relu) = relu
+                ref = r.torch_forward(w, x, cfg, device="cuda").double().cpu().numpy()  # relu * Sign(relu) = relu
             got = eng.run(x.reshape(B, -1)).astype(np.float64)
             err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
             assert err <= 1e-4, (B, err)

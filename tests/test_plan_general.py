@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo"]
 
 
 @pytest.fixture(scope="module")
@@ -39,20 +39,26 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
         assert kinds[-1] == "bf16_to_f32"  # 3 classes stored as 8 columns: the cast drops the pads
     if name == "se_cnn":
         assert kinds[0] == "input_prep" and "binary" in kinds and kinds.count("copy_cols") == 3
+    if name == "ops_zoo":
+        # pad1 folds into conv1, pad2 (before a MaxPool) is a pad pass; two Splits and two Concats
+        # -> 8 column copies; ReduceMax / ReduceSum / GlobalMaxPool -> 3 spatial reductions
+        assert kinds.count("pad") == 1 and kinds.count("gap") == 3 and kinds.count("copy_cols") == 8
+        names = [o["name"] for o in s["ops"]]
+        assert "pad1" not in names and "pad2" in names
 
 
 def test_generic_models_run_on_the_cpu_oracle(native, gen_models):
     from die_amd.models import generic as G
 
-    for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10))):
+    for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10)), ("ops_zoo", (2, 10))):
         y = native.cpu_run(gen_models[name], G.synthetic_input(name, 2))
         assert y.shape == shape and np.isfinite(y).all()
-        if name != "bert":
+        if name in ("mlp", "se_cnn"):
             np.testing.assert_allclose(y.sum(1), 1.0, rtol=1e-5)  # softmax heads
 
 
 def _unsupported_model(path):
-    """Image model with two ops the planner does not lower (Abs, Exp; the CPU executor runs them) in
+    """Image model with two ops the planner does not lower (Sin, Cos; the CPU executor runs them) in
     separate branches, and nodes that depend on them."""
     from die_amd.utils.onnx_writer import GraphBuilder
 
@@ -61,8 +67,8 @@ def _unsupported_model(path):
     x = g.input("x", ["N", 3, 8, 8])
     w = g.init("w", (0.1 * rng.standard_normal((16, 3, 3, 3))).astype(np.float32))
     h = g.node("Conv", [x, w], name="conv", kernel_shape=[3, 3], pads=[1, 1, 1, 1])
-    a = g.node("Abs", [h], name="abs")
-    b = g.node("Exp", [h], name="exp")
+    a = g.node("Sin", [h], name="sin")
+    b = g.node("Cos", [h], name="cos")
     s = g.node("Add", [a, b], name="join")
     g.output(g.node("Relu", [s], name="relu"), ["N", 16, 8, 8])
     open(path, "wb").write(g.model_proto(opset=13))
@@ -74,9 +80,9 @@ def test_report_lists_every_unsupported_node(native, tmp_path):
     r = native.plan_report(p)
     assert not r["supported"]
     ops = sorted(i["op"] for i in r["unsupported"])
-    assert ops == ["Abs", "Exp"], r
+    assert ops == ["Cos", "Sin"], r
     assert r["blocked"] == 2  # join + relu depend on them
-    assert "Abs 'abs'" in r["text"] and "Exp 'exp'" in r["text"]
+    assert "Sin 'sin'" in r["text"] and "Cos 'cos'" in r["text"]
     # an engine on "auto" keeps the reference's EP-style fallback and runs it on the CPU executor
     eng = native.Engine(p, device="auto", max_batch=2)
     assert eng.refresh_info()["name"] == "cpu"
