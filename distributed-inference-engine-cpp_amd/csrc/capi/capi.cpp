@@ -97,6 +97,7 @@ EngineOptions engine_opts(const Json& j) {
   e.completion_poll_us = jget<int>(j, "completion_poll_us", e.completion_poll_us);
   e.bn_on_load = jget<bool>(j, "bn_on_load", e.bn_on_load);
   e.fuse_pairs = jget<bool>(j, "fuse_pairs", e.fuse_pairs);
+  e.fuse_stem_pool = jget<bool>(j, "fuse_stem_pool", e.fuse_stem_pool);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);

@@ -289,9 +289,11 @@ char* die_hybrid_partition(const char* model_path, int max_batch, int split, cha
   }
 }
 
-char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse_pairs, char** err) {
+// fuse: bit 0 conv pairs, bit 1 stem + pool
+char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse, char** err) {
   try {
-    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, fuse_pairs != 0);
+    Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, (fuse & 1) != 0,
+                        (fuse & 2) != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -334,6 +336,10 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["relu2"] = o.conv.relu2;
         e["act"] = o.conv.relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
+      }
+      if (o.kind == PlanOp::STEM) {
+        e["pool_fused"] = o.is_max != 0;
+        e["rows"] = o.is_max ? o.Ho * o.Wo : o.conv.Ho * o.conv.Wo;
       }
       if (o.kind == PlanOp::CONV_PAIR) {
         e["K1"] = o.conv.K;

@@ -289,6 +289,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["completion_poll_us"] = o.completion_poll_us;
   j["bn_on_load"] = o.bn_on_load;
   j["fuse_pairs"] = o.fuse_pairs;
+  j["fuse_stem_pool"] = o.fuse_stem_pool;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["fail_batch_every"] = o.fail_batch_every;

@@ -64,7 +64,7 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
     plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
-                       opt.fuse_pairs);
+                       opt.fuse_pairs, opt.fuse_stem_pool);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -1114,6 +1114,14 @@ class HipEngine : public Engine {
                                        op.H, op.W, op.C, st, sp_);
           break;
         case PlanOp::STEM:
+          if (op.is_max) {  // + max pool (+ the pooled value's affine), input prep fused
+            e = kern::conv_stem_pool_nchw(static_cast<const float*>(buf(op.in)), op.C, prm(op.scale_off), prm(op.shift_off),
+                                          reinterpret_cast<const uint16_t*>(params_ + op.w_off), prm(op.bias_off),
+                                          op.conv.relu, prm(op.s2_off), prm(op.b2_off), op.act,
+                                          static_cast<uint16_t*>(buf(op.out)), B, op.conv.H, op.conv.W, op.conv.Ho,
+                                          op.conv.Wo, op.Ho, op.Wo, st, live, sp_);
+            break;
+          }
           if (op.in == -2) {  // graph input, input prep fused
             e = kern::conv_stem7x7_nchw(static_cast<const float*>(buf(op.in)), op.C, prm(op.scale_off),
                                         prm(op.shift_off), reinterpret_cast<const uint16_t*>(params_ + op.w_off),

@@ -79,9 +79,10 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 
 class Planner {
  public:
-  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true)
+  Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true,
+          bool fuse_stem_pool = true)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
-        fuse_pairs_(fuse_pairs) {}
+        fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool) {}
 
   // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
   // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
@@ -121,6 +122,7 @@ class Planner {
     if (!report_.supported) throw std::runtime_error("HIP engine cannot lower this graph:\n" + report_.text());
     finalize_output();
     fuse_pool_affine();
+    if (fuse_stem_pool_) fuse_stem_pool();
     if (fuse_pairs_) fuse_conv_pairs();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
@@ -2077,6 +2079,41 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
+  // Stem -> 3x3/2 max pool (pad 1) [-> the pooled value's BN/ReLU, fuse_pool_affine] where the stem
+  // map has no other reader: one STEM op with is_max = 1 (kernels/stem.hip stem_pool_nchw_kernel);
+  // the stem map is never stored.  Ho/Wo become the pooled size, s2_off/b2_off/act the pool's affine.
+  void fuse_stem_pool() {
+    std::vector<int> readers(plan_.bufs.size(), 0);
+    for (const PlanOp& p : plan_.ops)
+      for (int b : {p.in, p.in2, p.in3})
+        if (b >= 0) readers[b]++;
+    std::vector<PlanOp> out;
+    out.reserve(plan_.ops.size());
+    for (size_t i = 0; i < plan_.ops.size(); ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind == PlanOp::POOL && p.is_max && p.kh == 3 && p.kw == 3 && p.sh == 2 && p.sw == 2 && p.ph == 1 &&
+          p.pw == 1 && p.act <= 1 && p.C == 64 && p.in >= 0 && readers[p.in] == 1 && !out.empty()) {
+        PlanOp& s = out.back();
+        const auto& c = s.conv;
+        if (s.kind == PlanOp::STEM && s.in == kBufGraphIn && !s.is_max && s.out == p.in && c.Ho == p.H && c.Wo == p.W &&
+            kern::stem_pool_supported(c.H, c.W, c.Ho, c.Wo, p.Ho, p.Wo, split_)) {
+          permute_weight_rows(s.w_off, 64, 224, c.wplane);
+          s.is_max = 1;
+          s.Ho = p.Ho;
+          s.Wo = p.Wo;
+          s.s2_off = p.scale_off;
+          s.b2_off = p.shift_off;
+          s.act = p.act;
+          s.out = p.out;
+          s.name += "+" + p.name;
+          continue;
+        }
+      }
+      out.push_back(std::move(p));
+    }
+    plan_.ops = std::move(out);
+  }
+
   // Back-to-back 1x1 pair (ResNet-v2 bottleneck boundary).  A dual-store expand conv P writes the
   // raw sum x (next residual) and a = act(bn(x)); when a's ONLY reader is a plain 1x1/s1 reduce conv
   // Q, both become one CONV_PAIR op at P's position (Q has no other input, so computing it early is
@@ -2258,6 +2295,7 @@ class Planner {
   bool split_ = false;  // fp32 mode: split (hi, lo) activations and weights
   bool bn_on_load_ = false;  // EngineOptions::bn_on_load (bf16 plans only)
   bool fuse_pairs_ = true;   // EngineOptions::fuse_pairs
+  bool fuse_stem_pool_ = true;  // EngineOptions::fuse_stem_pool
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -2279,8 +2317,9 @@ std::string Plan::summary() const {
   return os.str();
 }
 
-Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs) {
-  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs).run();
+Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs,
+                bool fuse_stem_pool) {
+  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool).run();
 }
 
 std::string PlanReport::text() const {

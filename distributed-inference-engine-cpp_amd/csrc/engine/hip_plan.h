@@ -107,8 +107,9 @@ struct Plan {
 // the engine cannot lower (not only the first).  side_branches: mark independent convs to run on
 // a second stream (PlanOp::join; extends their inputs' lifetimes).  split: fp32 mode (Plan::split).
 // fuse_pairs: lower expand -> reduce 1x1 conv pairs to CONV_PAIR ops (EngineOptions::fuse_pairs).
+// fuse_stem_pool: stem conv + max pool in one STEM op (EngineOptions::fuse_stem_pool).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
-                bool bn_on_load = false, bool fuse_pairs = true);
+                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

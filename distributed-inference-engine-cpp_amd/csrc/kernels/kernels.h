@@ -220,6 +220,15 @@ hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias,
 // Persistent stem that reads the graph input directly: x fp32 NCHW [B][C][H][W], C <= 4, with the
 // input's pending per-channel affine (in_scale/in_shift, nullable) applied on load -- replaces
 // input_prep + conv_stem7x7.  max_blocks <= 0: two blocks per CU.
+// Stem 7x7/2 (NCHW fp32 input, fused input BN) + 3x3/2 pad-1 max pool + per-channel affine (+ ReLU if
+// pact == 1) of the pooled value, one kernel (stem.hip).  Weight rows permuted by pair_permute_row;
+// bias / pscale / pshift in logical channel order.  out: [B][Hp][Wp][64].
+bool stem_pool_supported(int H, int W, int Hs, int Ws, int Hp, int Wp, int split);
+size_t stem_pool_lds_bytes(int Ws, int split);
+hipError_t conv_stem_pool_nchw(const float* x, int C, const float* in_scale, const float* in_shift, const uint16_t* w,
+                               const float* bias, int relu, const float* pscale, const float* pshift, int pact,
+                               uint16_t* out, int B, int H, int W, int Hs, int Ws, int Hp, int Wp, hipStream_t s,
+                               const long long* live = nullptr, int split = 0, int target_blocks = 0);
 hipError_t conv_stem7x7_nchw(const float* x, int C, const float* in_scale, const float* in_shift, const uint16_t* w,
                              const float* bias, uint16_t* out, int B, int H, int W, int Ho, int Wo, int relu,
                              hipStream_t s, const long long* live = nullptr, int split = 0, int max_blocks = 0);

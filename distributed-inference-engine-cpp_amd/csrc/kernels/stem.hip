@@ -275,9 +275,280 @@ __global__ __launch_bounds__(SNT, 2) void stem7x7_nchw_kernel(const float* __res
   }
 }
 
+// Stem + 3x3/2 max pool (pad 1) + the pooled value's BN/ReLU in one kernel (ResNet conv0 -> pool0
+// -> stage-1 pre-activation): the 112x112x64 stem map (64 MB per 20 images in fp32 mode) is never
+// stored or re-read; only the 56x56 pooled map is written.
+//   * a block owns a segment of pool rows [p0, p1) of one image over the FULL stem width: wave w
+//     computes stem columns [16w, 16w + 16) (CG = ceil(Ws / 16) <= 8 waves), and per pool row p the
+//     two stem rows 2p, 2p + 1 (acc[4][2], the stem7x7_nchw MFMA schedule); stem row 2p - 1 is
+//     carried in registers from the previous row (recomputed once at the segment start);
+//   * the input rows sit in an LDS ring of 11 rows (fp32 NCHW -> input BN -> bf16 / split on the
+//     way in); the 4 rows the next pool row adds are fetched into registers during this row's MFMAs;
+//   * pooling: vertical max of the 3 stem rows in registers, horizontal max over lanes px-1 / px+1
+//     with DPP row shifts (a 16-lane DPP row = the 16 stem columns of the wave), the column left of
+//     the wave's first one through LDS; the max runs on the stored representation (hi + lo), as the
+//     unfused pool reads it, so the fusion is bit-exact;
+//   * weight rows are permuted by pair_permute_row: lane group j holds logical channels
+//     32 blk + 8 j + [0, 8) of the two fragments 2 blk, 2 blk + 1 -> 16-byte pooled stores.
+constexpr int RING = 11;  // input rows: halo stem row (7) + two stem rows (9) share 11 at the segment start
+
+__device__ __forceinline__ float dpp_shr1(float v) {  // lane - 1 within its 16-lane row (-inf at column 0)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_shl1(float v) {  // lane + 1 within its 16-lane row (-inf at column 15)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x101, 0xf, 0xf, false));
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
+    const float* __restrict__ x, int C, const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    const uint16_t* __restrict__ w, const float* __restrict__ bias, int relu, const float* __restrict__ pscale,
+    const float* __restrict__ pshift, int pact, uint16_t* __restrict__ out, int B, int H, int W, int Hs, int Ws, int Hp,
+    int Wp, int seg_len, int segs_per_img, const long long* __restrict__ live) {
+  constexpr int NP = SPLIT ? 2 : 1;
+  const int CG = blockDim.x >> 6, PXF = 32 * CG + 6;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* wl = smem;                           // NP x [64][WP]
+  uint16_t* ring = wl + NP * NCH * WP;           // NP x [RING][PXF][4]
+  float* xbuf = reinterpret_cast<float*>(ring + NP * RING * PXF * 4);  // [CG][64]: column 15 of each wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
+  const int b = blockIdx.x / segs_per_img;
+  const int p0 = (blockIdx.x % segs_per_img) * seg_len, p1 = min(p0 + seg_len, Hp);
+  if ((live && b >= *live) || b >= B || p0 >= Hp) return;  // whole block, before any barrier
+  const long long oplane = static_cast<long long>(B) * Hp * Wp * NCH;
+  const long long ring_plane = static_cast<long long>(RING) * PXF * 4;
+  for (int i = tid; i < NP * NCH * (KS / 8); i += nthr) {
+    const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
+    const int r = q / (KS / 8), c = q % (KS / 8);
+    *reinterpret_cast<uint4*>(wl + pl * NCH * WP + r * WP + c * 8) =
+        *reinterpret_cast<const uint4*>(w + pl * NCH * KS + r * KS + c * 8);
+  }
+  float sc[4], sh[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    sc[c] = (c < C && in_scale) ? in_scale[c] : 1.f;
+    sh[c] = (c < C && in_shift) ? in_shift[c] : 0.f;
+  }
+  const size_t HW = static_cast<size_t>(H) * W;
+  const float* xb = x + static_cast<size_t>(b) * C * HW;
+  // input pixel (row iy, patch column q) -> ring (input BN, then bf16 / split; 0 outside the image)
+  auto put = [&](int iy, int q, const float* raw, bool inb) {
+    float v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = (inb && c < C) ? fmaf(raw[c], sc[c], sh[c]) : 0.f;
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if constexpr (SPLIT) split1(v[c], h[c], l[c]);
+      else h[c] = f2bf(v[c]);
+    }
+    uint16_t* d = ring + (static_cast<long long>((iy + 5 * RING) % RING) * PXF + q) * 4;
+    *reinterpret_cast<uint2*>(d) = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+    if constexpr (SPLIT)
+      *reinterpret_cast<uint2*>(d + ring_plane) = make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
+  };
+  auto load_px = [&](int iy, int q, float* raw) -> bool {
+    const int ix = q - 3;
+    const bool inb = iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) raw[c] = (inb && c < C) ? xb[c * HW + static_cast<size_t>(iy) * W + ix] : 0.f;
+    return inb;
+  };
+  // segment start: input rows 4 p0 - 5 .. 4 p0 + 5 (halo stem row 2 p0 - 1 and stem rows 2 p0, 2 p0 + 1)
+  for (int i = tid; i < RING * PXF; i += nthr) {
+    const int iy = 4 * p0 - 5 + i / PXF, q = i % PXF;
+    float raw[4];
+    const bool inb = load_px(iy, q, raw);
+    put(iy, q, raw, inb);
+  }
+  __syncthreads();
+  const int j = lane >> 4, px_l = lane & 15, sx = 16 * wave + px_l;
+  // one stem row (sy) of this wave's 16 columns: acc = 64 channels (4 fragments) of pixel (sy, sx)
+  auto stem_rows = [&](int sy0, int nrows, f32x4 (&acc)[4][2]) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      bf16x8 bf[NP][2];
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int iy = 2 * (sy0 + m) - 3 + ky;
+          bf[pl][m] = *reinterpret_cast<const bf16x8*>(ring + pl * ring_plane +
+                                                       (static_cast<long long>((iy + 5 * RING) % RING) * PXF + 2 * sx + 2 * j) * 4);
+        }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int wo = (n * 16 + (lane & 15)) * WP + ky * 32 + j * 8;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(wl + wo);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          if (m >= nrows) continue;
+          if constexpr (SPLIT) {
+            const bf16x8 al = *reinterpret_cast<const bf16x8*>(wl + NCH * WP + wo);
+            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bf[0][m], acc[n][m], 0, 0, 0);
+            acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[NP - 1][m], acc[n][m], 0, 0, 0);
+          }
+          acc[n][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[0][m], acc[n][m], 0, 0, 0);
+        }
+      }
+    }
+  };
+  // stem epilogue -> the value the unfused pool would read back (hi + lo, or bf16); -inf off the map
+  // (max pool padding).  Physical fragment n, lane group j, element t = logical channel
+  // 32 (n >> 1) + 8 j + 4 (n & 1) + t.
+  auto stem_val = [&](const f32x4 (&acc)[4][2], int m, int sy, float (&r)[4][4]) {
+    const bool ok = sy >= 0 && sy < Hs && sx < Ws;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int ch = 32 * (n >> 1) + 8 * j + 4 * (n & 1);
+      const float4 bv = *reinterpret_cast<const float4*>(bias + ch);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v = acc[n][m][t] + bb[t];
+        if (relu) v = fmaxf(v, 0.f);
+        if constexpr (SPLIT) {
+          uint16_t h, l;
+          split1(v, h, l);
+          v = bf2f(h) + bf2f(l);
+        } else {
+          v = bf2f(f2bf(v));
+        }
+        r[n][t] = ok ? v : -INFINITY;
+      }
+    }
+  };
+  float carry[4][4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) carry[n][t] = -INFINITY;
+  f32x4 acc[4][2];
+  if (p0 > 0) {  // halo: stem row 2 p0 - 1 (the previous segment's last row)
+    stem_rows(2 * p0 - 1, 1, acc);
+    stem_val(acc, 0, 2 * p0 - 1, carry);
+  }
+  constexpr int PPT = 3;  // 4 new input rows x PXF pixels over >= 64 * CG threads (4 * (32 CG + 6) <= 3 * 64 CG)
+  float pre[PPT][4];
+  bool pin[PPT];
+  for (int p = p0; p < p1; ++p) {
+    const bool more = p + 1 < p1;
+    if (more) {  // input rows 4 p + 6 .. 4 p + 9, in flight during the MFMAs
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const int i = tid + k * nthr;
+        pin[k] = false;
+        if (i < 4 * PXF) pin[k] = load_px(4 * p + 6 + i / PXF, i % PXF, pre[k]);
+      }
+    }
+    stem_rows(2 * p, 2, acc);
+    float r0[4][4], r1[4][4], vm[4][4];
+    stem_val(acc, 0, 2 * p, r0);
+    stem_val(acc, 1, 2 * p + 1, r1);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        vm[n][t] = fmaxf(fmaxf(carry[n][t], r0[n][t]), r1[n][t]);
+        carry[n][t] = r1[n][t];
+      }
+    if (px_l == 15) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) xbuf[wave * NCH + 32 * (n >> 1) + 8 * j + 4 * (n & 1) + t] = vm[n][t];
+    }
+    __syncthreads();  // xbuf written; every wave done reading the ring rows the prefetch replaces
+    float pv[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float left = dpp_shr1(vm[n][t]);
+        const float right = dpp_shl1(vm[n][t]);
+        if (px_l == 0) left = wave > 0 ? xbuf[(wave - 1) * NCH + 32 * (n >> 1) + 8 * j + 4 * (n & 1) + t] : -INFINITY;
+        pv[n][t] = fmaxf(fmaxf(left, vm[n][t]), right);
+      }
+    const int pc = sx >> 1;
+    if (!(px_l & 1) && pc < Wp) {
+      uint16_t* o = out + ((static_cast<long long>(b) * Hp + p) * Wp + pc) * NCH;
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        const int ch = 32 * blk + 8 * j;
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          v[t] = pv[2 * blk + (t >> 2)][t & 3];
+          if (pscale) v[t] = v[t] * pscale[ch + t] + pshift[ch + t];
+          if (pact == 1) v[t] = fmaxf(v[t], 0.f);
+        }
+        store8v(o + ch, oplane, SPLIT, v);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const int i = tid + k * nthr;
+        if (i < 4 * PXF) put(4 * p + 6 + i / PXF, i % PXF, pre[k], pin[k]);
+      }
+    }
+    __syncthreads();  // new rows in the ring; xbuf free for the next row
+  }
+}
+
 }  // namespace
 
 static_assert(TY * TX * NCH <= NCH * WP, "output stage must fit in the weight buffer");
+
+size_t stem_pool_lds_bytes(int Ws, int split) {
+  const int CG = (Ws + 15) / 16, NP = split ? 2 : 1;
+  return static_cast<size_t>(NP) * NCH * WP * 2 + static_cast<size_t>(NP) * RING * (32 * CG + 6) * 4 * 2 +
+         static_cast<size_t>(CG) * NCH * 4;
+}
+
+bool stem_pool_supported(int H, int W, int Hs, int Ws, int Hp, int Wp, int split) {
+  return Hs == (H + 6 - 7) / 2 + 1 && Ws == (W + 6 - 7) / 2 + 1 && Hp == (Hs + 2 - 3) / 2 + 1 &&
+         Wp == (Ws + 2 - 3) / 2 + 1 && Ws >= 1 && (Ws + 15) / 16 <= 8 && stem_pool_lds_bytes(Ws, split) <= 160 * 1024;
+}
+
+hipError_t conv_stem_pool_nchw(const float* x, int C, const float* in_scale, const float* in_shift, const uint16_t* w,
+                               const float* bias, int relu, const float* pscale, const float* pshift, int pact,
+                               uint16_t* out, int B, int H, int W, int Hs, int Ws, int Hp, int Wp, hipStream_t s,
+                               const long long* live, int split, int target_blocks) {
+  if (C < 1 || C > 4 || B < 1 || !stem_pool_supported(H, W, Hs, Ws, Hp, Wp, split) || (pscale == nullptr) != (pshift == nullptr))
+    return hipErrorInvalidValue;
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
+  }();
+  // segments of pool rows: about one block per CU over the batch (the halo row is recomputed per segment)
+  const int want = std::max(1, (target_blocks > 0 ? target_blocks : cus) / B);
+  const int seg_len = std::max(1, (Hp + want - 1) / want);
+  const int segs = (Hp + seg_len - 1) / seg_len;
+  const int CG = (Ws + 15) / 16;
+  const size_t lds = stem_pool_lds_bytes(Ws, split);
+  static const bool attr_set = [] {  // once, outside any graph capture's launches
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_nchw_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_nchw_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr_set;
+  if (split) {
+    hipLaunchKernelGGL(stem_pool_nchw_kernel<true>, dim3(B * segs), dim3(64 * CG), lds, s, x, C, in_scale, in_shift, w,
+                       bias, relu, pscale, pshift, pact, out, B, H, W, Hs, Ws, Hp, Wp, seg_len, segs, live);
+  } else {
+    hipLaunchKernelGGL(stem_pool_nchw_kernel<false>, dim3(B * segs), dim3(64 * CG), lds, s, x, C, in_scale, in_shift, w,
+                       bias, relu, pscale, pshift, pact, out, B, H, W, Hs, Ws, Hp, Wp, seg_len, segs, live);
+  }
+  return hipGetLastError();
+}
 
 hipError_t conv_stem7x7(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* out, int B, int H, int W,
                         int Ho, int Wo, int relu, hipStream_t s, const long long* live, int split) {

@@ -66,9 +66,11 @@ def test_dp_worker_rccl_world1_http(native, models, dp_path):
         assert h["engine"]["dp_solo"] is (dp_path == "solo")
         res = native.loadgen(port=wk.port, connections=8, requests=64, payload="full", input_numel=3 * 64 * 64)
         assert res["ok"] == 64 and res["failed"] == 0
-        x = r.synthetic_input(2, cfg).reshape(2, -1)
+        # 3-decimal texts: the DP staging items are sized for 4-bit packed bodies of short decimals
+        # (dp_arena_plan); 17-digit reprs would take the host-parse path
+        x = np.array([[float("%.3f" % v) for v in row] for row in r.synthetic_input(2, cfg).reshape(2, -1)], np.float32)
         for i in range(2):  # device-decoded text through the DP path == plain engine on parsed floats
-            body = json.dumps({"request_id": "g%d" % i, "input_data": [float(v) for v in x[i]]}).encode()
+            body = ('{"request_id": "g%d", "input_data": [%s]}' % (i, ",".join("%.3f" % v for v in x[i]))).encode()
             out = json.loads(urllib.request.urlopen(urllib.request.Request(wk.url + "/infer", data=body),
                                                     timeout=60).read())
             np.testing.assert_array_equal(np.array(out["output_data"], np.float32), ref_eng.run(x[i:i + 1])[0])

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--tune-warm-input", action="store_true", help="autotune with each conv's producer run first")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
+    ap.add_argument("--no-fuse-stem-pool", action="store_true", help="stem and max pool as two launches (EngineOptions::fuse_stem_pool)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
 
@@ -37,7 +38,8 @@ def main():
     path = os.path.join(d, a.arch + ".onnx")
     open(path, "wb").write(m.build_onnx(cfg)[0])
     e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision,
-                      tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs)
+                      tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
+                      fuse_stem_pool=not a.no_fuse_stem_pool)
     p = e.profile(a.batch, a.iters)
     e.close()
     lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
