@@ -716,6 +716,184 @@ CpuValuePtr op_pad(const Node& n, const std::vector<const CpuValue*>& in) {
   return y;
 }
 
+// ConvTranspose (2-D, any group / stride / dilation / pads / output_padding / output_shape), as the
+// scatter form of its definition: every input pixel adds its kernel-weighted copy into the output.
+CpuValuePtr op_conv_transpose(const Node& n, const CpuValue& x, const CpuValue& w, const CpuValue* b) {
+  if (x.shape.size() != 4 || w.shape.size() != 4) fail(n, "only 2-D transposed convolution is supported");
+  const int64_t N = x.shape[0], C = x.shape[1], H = x.shape[2], W = x.shape[3];
+  const int64_t G = n.get_int("group", 1), Mg = w.shape[1], M = Mg * G, kh = w.shape[2], kw = w.shape[3];
+  if (w.shape[0] != C || C % G) fail(n, "weight / channel mismatch");
+  const auto st = n.get_ints("strides", {1, 1}), dl = n.get_ints("dilations", {1, 1}), op = n.get_ints("output_padding", {0, 0});
+  auto pads = n.get_ints("pads", {0, 0, 0, 0});
+  const int64_t k[2] = {kh, kw}, in[2] = {H, W};
+  int64_t out[2];
+  const auto os = n.get_ints("output_shape");
+  const std::string ap = n.get_string("auto_pad", "NOTSET");
+  for (int d = 0; d < 2; ++d) {
+    const int64_t full = st[d] * (in[d] - 1) + op[d] + (k[d] - 1) * dl[d] + 1;
+    if (!os.empty() || ap == "SAME_UPPER" || ap == "SAME_LOWER") {
+      out[d] = !os.empty() ? os[os.size() - 2 + d] : in[d] * st[d];
+      const int64_t total = full - out[d];
+      const bool upper = ap != "SAME_LOWER";  // output_shape without auto_pad: the SAME_UPPER split
+      pads[d] = upper ? total / 2 : total - total / 2;
+      pads[d + 2] = total - pads[d];
+    } else {
+      out[d] = full - pads[d] - pads[d + 2];
+    }
+  }
+  auto y = make_f({N, M, out[0], out[1]});
+  const int64_t Cg = C / G;
+#pragma omp parallel for collapse(2)
+  for (int64_t bn = 0; bn < N; ++bn)
+    for (int64_t m = 0; m < M; ++m) {
+      const int64_t g = m / Mg, mo = m % Mg;
+      float* yo = y->f.data() + (bn * M + m) * out[0] * out[1];
+      if (b) std::fill(yo, yo + out[0] * out[1], b->f[m]);
+      for (int64_t c = g * Cg; c < (g + 1) * Cg; ++c) {
+        const float* xi = x.f.data() + (bn * C + c) * H * W;
+        const float* wk = w.f.data() + (c * Mg + mo) * kh * kw;
+        for (int64_t iy = 0; iy < H; ++iy)
+          for (int64_t ix = 0; ix < W; ++ix) {
+            const float v = xi[iy * W + ix];
+            for (int64_t ky = 0; ky < kh; ++ky) {
+              const int64_t oy = iy * st[0] - pads[0] + ky * dl[0];
+              if (oy < 0 || oy >= out[0]) continue;
+              for (int64_t kx = 0; kx < kw; ++kx) {
+                const int64_t ox = ix * st[1] - pads[1] + kx * dl[1];
+                if (ox >= 0 && ox < out[1]) yo[oy * out[1] + ox] += v * wk[ky * kw + kx];
+              }
+            }
+          }
+      }
+    }
+  return y;
+}
+
+// Resize (opset 10+) / Upsample on [N, C, H, W]: nearest or linear over H, W (N, C scales 1), the
+// ONNX coordinate transforms and nearest rounding modes; linear clamps neighbour indices (= the
+// specification's edge padding).
+CpuValuePtr op_resize(const Node& n, const std::vector<const CpuValue*>& in, int64_t opset) {
+  const CpuValue& x = *in[0];
+  if (x.shape.size() != 4) fail(n, "only 4-D inputs");
+  const bool upsample = n.op_type == "Upsample";
+  std::vector<float> scales = n.get_floats("scales");
+  std::vector<int64_t> sizes;
+  auto floats = [](const CpuValue* v) {
+    std::vector<float> f;
+    if (v) f = v->is_int ? std::vector<float>(v->i.begin(), v->i.end()) : v->f;
+    return f;
+  };
+  if (scales.empty()) {
+    if (upsample || (opset < 11 && in.size() > 1)) scales = floats(in.size() > 1 ? in[1] : nullptr);
+    else {
+      if (in.size() > 2) scales = floats(in[2]);
+      if (scales.empty() && in.size() > 3 && in[3]) sizes = as_ints(*in[3]);
+    }
+  }
+  const int64_t N = x.shape[0], C = x.shape[1], H = x.shape[2], W = x.shape[3];
+  int64_t Ho, Wo;
+  float sh, sw;
+  if (!sizes.empty()) {
+    Ho = sizes[2];
+    Wo = sizes[3];
+    sh = static_cast<float>(Ho) / H;
+    sw = static_cast<float>(Wo) / W;
+  } else {
+    if (scales.size() != 4) fail(n, "expected 4 scales");
+    sh = scales[2];
+    sw = scales[3];
+    Ho = static_cast<int64_t>(std::floor(H * static_cast<double>(sh)));
+    Wo = static_cast<int64_t>(std::floor(W * static_cast<double>(sw)));
+  }
+  const bool legacy = upsample || opset < 11;
+  const std::string mode = n.get_string("mode", "nearest");
+  const std::string cm = legacy ? "asymmetric" : n.get_string("coordinate_transformation_mode", "half_pixel");
+  const std::string nm = legacy ? "floor" : n.get_string("nearest_mode", "round_prefer_floor");
+  auto src = [&](int64_t o, float scale, int64_t len, int64_t olen) -> float {
+    if (cm == "asymmetric") return o / scale;
+    if (cm == "align_corners") return olen > 1 ? o * static_cast<float>(len - 1) / static_cast<float>(olen - 1) : 0.f;
+    if (cm == "pytorch_half_pixel") return olen > 1 ? (o + 0.5f) / scale - 0.5f : 0.f;
+    if (cm == "tf_half_pixel_for_nn") return (o + 0.5f) / scale;
+    if (cm == "half_pixel") return (o + 0.5f) / scale - 0.5f;
+    fail(n, "unsupported coordinate_transformation_mode " + cm);
+  };
+  auto nearest = [&](float v, int64_t len) -> int64_t {
+    const float f = std::floor(v);
+    int64_t i;
+    if (nm == "floor") i = static_cast<int64_t>(f);
+    else if (nm == "ceil") i = static_cast<int64_t>(std::ceil(v));
+    else if (v - f == 0.5f) i = static_cast<int64_t>(f) + (nm == "round_prefer_ceil" ? 1 : 0);
+    else i = static_cast<int64_t>(std::nearbyint(v));
+    return std::min(std::max<int64_t>(i, 0), len - 1);
+  };
+  const bool linear = mode == "linear" || mode == "bilinear";
+  if (!linear && mode != "nearest") fail(n, "unsupported mode " + mode);
+  auto y = make_f({N, C, Ho, Wo});
+#pragma omp parallel for collapse(2)
+  for (int64_t p = 0; p < N * C; ++p)
+    for (int64_t oy = 0; oy < Ho; ++oy) {
+      const float* xi = x.f.data() + p * H * W;
+      float* yo = y->f.data() + (p * Ho + oy) * Wo;
+      const float fy = src(oy, sh, H, Ho);
+      for (int64_t ox = 0; ox < Wo; ++ox) {
+        const float fx = src(ox, sw, W, Wo);
+        if (!linear) {
+          yo[ox] = xi[nearest(fy, H) * W + nearest(fx, W)];
+          continue;
+        }
+        const float y0f = std::floor(fy), x0f = std::floor(fx), ay = fy - y0f, ax = fx - x0f;
+        auto cl = [](int64_t v, int64_t len) { return std::min(std::max<int64_t>(v, 0), len - 1); };
+        const int64_t y0 = cl(static_cast<int64_t>(y0f), H), y1 = cl(static_cast<int64_t>(y0f) + 1, H);
+        const int64_t x0 = cl(static_cast<int64_t>(x0f), W), x1 = cl(static_cast<int64_t>(x0f) + 1, W);
+        const float top = xi[y0 * W + x0] * (1.f - ax) + xi[y0 * W + x1] * ax;
+        const float bot = xi[y1 * W + x0] * (1.f - ax) + xi[y1 * W + x1] * ax;
+        yo[ox] = top * (1.f - ay) + bot * ay;
+      }
+    }
+  return y;
+}
+
+// Comparisons -> bool (int 0 / 1); Where(cond, a, b) with broadcasting; Not / And / Or on bools.
+CpuValuePtr op_compare(const Node& n, const CpuValue& a, const CpuValue& b) {
+  const std::string& op = n.op_type;
+  auto os = broadcast_shape(n, a.shape, b.shape);
+  auto tof = [](const CpuValue& v) {
+    return v.is_int ? std::vector<float>(v.i.begin(), v.i.end()) : v.f;
+  };
+  const std::vector<float> fa = tof(a), fb = tof(b);
+  auto y = make_f(os);
+  std::function<float(float, float)> f;
+  if (op == "Greater") f = [](float p, float q) { return static_cast<float>(p > q); };
+  else if (op == "Less") f = [](float p, float q) { return static_cast<float>(p < q); };
+  else if (op == "Equal") f = [](float p, float q) { return static_cast<float>(p == q); };
+  else if (op == "GreaterOrEqual") f = [](float p, float q) { return static_cast<float>(p >= q); };
+  else if (op == "LessOrEqual") f = [](float p, float q) { return static_cast<float>(p <= q); };
+  else if (op == "And") f = [](float p, float q) { return static_cast<float>(p != 0.f && q != 0.f); };
+  else if (op == "Or") f = [](float p, float q) { return static_cast<float>(p != 0.f || q != 0.f); };
+  else fail(n, "unsupported comparison");
+  broadcast_apply<float>(os, fa.data(), a.shape, fb.data(), b.shape, y->f.data(), f);
+  auto r = make_i(os);
+  for (size_t k = 0; k < r->i.size(); ++k) r->i[k] = y->f[k] != 0.f;
+  return r;
+}
+
+CpuValuePtr op_where(const Node& n, const CpuValue& c, const CpuValue& a, const CpuValue& b) {
+  // select(c, a, b) = a * c + b * (1 - c) would turn inf * 0 into NaN: broadcast c against a, then
+  // pick per element
+  auto tof = [](const CpuValue& v) { return v.is_int ? std::vector<float>(v.i.begin(), v.i.end()) : v.f; };
+  const std::vector<float> fc = tof(c), fa = tof(a), fb = tof(b);
+  auto s1 = broadcast_shape(n, c.shape, a.shape);
+  auto os = broadcast_shape(n, s1, b.shape);
+  auto ca = make_f(os), cb = make_f(os), cc = make_f(os);
+  std::vector<float> zeros(1, 0.f);
+  const std::vector<int64_t> one = {1};
+  broadcast_apply<float>(os, fa.data(), a.shape, zeros.data(), one, ca->f.data(), [](float p, float) { return p; });
+  broadcast_apply<float>(os, fb.data(), b.shape, zeros.data(), one, cb->f.data(), [](float p, float) { return p; });
+  broadcast_apply<float>(os, fc.data(), c.shape, zeros.data(), one, cc->f.data(), [](float p, float) { return p; });
+  for (size_t k = 0; k < ca->f.size(); ++k) ca->f[k] = cc->f[k] != 0.f ? ca->f[k] : cb->f[k];
+  return ca;
+}
+
 // Split: sizes from the attribute (opset < 13), input 1, or equal parts (the last may be smaller).
 std::vector<CpuValuePtr> op_split(const Node& n, const std::vector<const CpuValue*>& in) {
   const CpuValue& x = *in[0];
@@ -818,7 +996,7 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
       out = make_f(in[0]->shape);
       for (size_t e = 0; e < out->f.size(); ++e) out->f[e] = std::clamp(in[0]->f[e], lo, hi);
     } else if (op == "Add" || op == "Sub" || op == "Mul" || op == "Div" || op == "Pow" || op == "Max" ||
-               op == "Min" || op == "Equal") {
+               op == "Min" || (op == "Equal" && in[0]->is_int && in[1]->is_int)) {
       out = op_binary(n, *in[0], *in[1]);
     } else if (op == "MaxPool" || op == "AveragePool") {
       out = op_pool(n, *in[0], op == "MaxPool");
@@ -895,7 +1073,10 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
       out = op_binary(add, *tmp, z2);
     } else if (op == "Cast") {
       const int to = static_cast<int>(n.get_int("to", onnx::FLOAT));
-      if (onnx::is_float_type(to)) {
+      if (to == onnx::BOOL) {
+        out = make_i(in[0]->shape);
+        for (size_t e = 0; e < out->i.size(); ++e) out->i[e] = in[0]->is_int ? in[0]->i[e] != 0 : in[0]->f[e] != 0.f;
+      } else if (onnx::is_float_type(to)) {
         out = make_f(in[0]->shape);
         if (in[0]->is_int) out->f.assign(in[0]->i.begin(), in[0]->i.end());
         else out->f = in[0]->f;
@@ -919,6 +1100,18 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
       out = op_reduce(n, in, opset);
     } else if (op == "Pad") {
       out = op_pad(n, in);
+    } else if (op == "ConvTranspose") {
+      out = op_conv_transpose(n, *in[0], *in[1], in.size() > 2 ? in[2] : nullptr);
+    } else if (op == "Resize" || op == "Upsample") {
+      out = op_resize(n, in, opset);
+    } else if (op == "Greater" || op == "Less" || op == "GreaterOrEqual" || op == "LessOrEqual" || op == "And" ||
+               op == "Or" || (op == "Equal" && !(in[0]->is_int && in[1]->is_int))) {
+      out = op_compare(n, *in[0], *in[1]);
+    } else if (op == "Where") {
+      out = op_where(n, *in[0], *in[1], *in[2]);
+    } else if (op == "Not") {
+      out = make_i(in[0]->shape);
+      for (size_t e = 0; e < out->i.size(); ++e) out->i[e] = in[0]->is_int ? in[0]->i[e] == 0 : in[0]->f[e] == 0.f;
     } else if (op == "Split") {
       auto outs = op_split(n, in);
       for (size_t k = 1; k < outs.size(); ++k)

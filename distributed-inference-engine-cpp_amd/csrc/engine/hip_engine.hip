@@ -1089,7 +1089,17 @@ class HipEngine : public Engine {
         }
         case PlanOp::PAD:
           e = kern::pad_nhwc(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
-                             op.C, op.Ho, op.Wo, op.ph, op.pw, st, sp_);
+                             op.C, op.Ho, op.Wo, op.ph, op.pw, st, sp_, op.sh, op.sw);
+          break;
+        case PlanOp::WHERE:
+          e = kern::where_rows(static_cast<const uint16_t*>(buf(op.in)), op.in2 >= 0 ? static_cast<const uint16_t*>(buf(op.in2)) : nullptr,
+                               op.in3 >= 0 ? static_cast<const uint16_t*>(buf(op.in3)) : nullptr, op.clip_lo, op.clip_hi,
+                               static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, st, live,
+                               op.rows_per_sample, sp_, op.Cp);
+          break;
+        case PlanOp::RESIZE:
+          e = kern::resize_nhwc(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
+                                op.C, op.Ho, op.Wo, op.clip_lo, op.clip_hi, op.gidx, op.act, op.is_max, st, live, sp_);
           break;
         case PlanOp::POOL:
           e = kern::pool2d(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
@@ -1231,8 +1241,8 @@ class HipEngine : public Engine {
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                   "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad"};
-    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::PAD + 1, "one name per PlanOp kind");
+                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize"};
+    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::RESIZE + 1, "one name per PlanOp kind");
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

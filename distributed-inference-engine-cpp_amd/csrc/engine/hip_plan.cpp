@@ -293,6 +293,17 @@ class Planner {
       throw std::runtime_error(op + " " + n.name + ": only two activations of one shape (or a per-sample broadcast)");
     }
     if (op == "Pad") return lower_pad(idx);
+    if (op == "ZeroInsert" && n.domain == "die") return lower_pad(idx);  // ConvTranspose rewrite (rewrite_for_device)
+    if (op == "Greater" || op == "Less" || op == "Equal" || op == "GreaterOrEqual" || op == "LessOrEqual")
+      return lower_compare(idx);
+    if (op == "And" || op == "Or") {
+      if (lower_binary_acts(n)) return;
+      throw std::runtime_error(op + " " + n.name + ": only two boolean activations of one shape");
+    }
+    if (op == "Not") return emit_unary(n, materialize_in(n.in(0), n), 23, 0.f, 0.f, n.outputs[0]);
+    if (op == "Where") return lower_where(idx);
+    if (op == "Cast") return lower_cast(idx);
+    if (op == "Resize" || op == "Upsample") return lower_resize(idx);
     if (op == "Split") return lower_split(idx);
     if (op == "Slice") return lower_slice(idx);
     if (op == "LayerNormalization") return lower_layernorm(idx);
@@ -1532,8 +1543,21 @@ class Planner {
   // kernel -- ONNX Runtime's CPU EP runs it there).  A Pad whose only reader is a Conv with explicit
   // pads folds into that conv (the conv kernels read out-of-range pixels as zero); otherwise one
   // NHWC pad pass writes the padded image.
+  // ZeroInsert (domain "die", from rewrite_conv_transpose): the same pass with strides: zeros between
+  // the input's pixels and `pads` = [top, left, bottom, right] around them.
   void lower_pad(int idx) {
     const Node& n = m_.nodes[idx];
+    int sy = 1, sx = 1;
+    std::array<int64_t, 4> tlbr{};
+    if (n.op_type == "ZeroInsert") {
+      const auto st = n.get_ints("strides", {1, 1}), pd = n.get_ints("pads", {0, 0, 0, 0});
+      sy = static_cast<int>(st.at(0));
+      sx = static_cast<int>(st.at(1));
+      for (int k = 0; k < 4; ++k) tlbr[k] = pd.at(k);
+      const Val x = materialize_in(n.in(0), n);
+      if (x.kind != Val::NHWC || !dense(x)) throw std::runtime_error("ConvTranspose " + n.name + ": input must be an image");
+      return emit_pad(n, x, tlbr, sy, sx);
+    }
     if (n.get_string("mode", "constant") != "constant") throw std::runtime_error("Pad " + n.name + ": only constant mode");
     std::vector<int64_t> pads = n.get_ints("pads");
     float value = n.get_float("value", 0.f);
@@ -1549,9 +1573,13 @@ class Planner {
       throw std::runtime_error("Pad " + n.name + ": only the spatial axes of an [N, C, H, W] image");
     for (auto v : pads)
       if (v < 0) throw std::runtime_error("Pad " + n.name + ": negative pads (cropping) are not supported");
-    const std::array<int64_t, 4> tlbr{{pads[2], pads[3], pads[6], pads[7]}};
+    tlbr = {{pads[2], pads[3], pads[6], pads[7]}};
+    emit_pad(n, x, tlbr, 1, 1);
+  }
+
+  void emit_pad(const Node& n, const Val& x, const std::array<int64_t, 4>& tlbr, int sy, int sx) {
     const int c = sole_consumer(n.outputs[0]);
-    if (c >= 0 && m_.nodes[c].op_type == "Conv" && m_.nodes[c].in(0) == n.outputs[0] &&
+    if (sy == 1 && sx == 1 && c >= 0 && m_.nodes[c].op_type == "Conv" && m_.nodes[c].in(0) == n.outputs[0] &&
         m_.nodes[c].get_string("auto_pad", "NOTSET") == "NOTSET") {
       folded_pad_[n.outputs[0]] = tlbr;
       define(n.outputs[0], x);
@@ -1566,12 +1594,158 @@ class Planner {
     p.W = x.W;
     p.ph = static_cast<int>(tlbr[0]);
     p.pw = static_cast<int>(tlbr[1]);
-    p.Ho = x.H + static_cast<int>(tlbr[0] + tlbr[2]);
-    p.Wo = x.W + static_cast<int>(tlbr[1] + tlbr[3]);
+    p.sh = sy;
+    p.sw = sx;
+    p.Ho = (x.H - 1) * sy + 1 + static_cast<int>(tlbr[0] + tlbr[2]);
+    p.Wo = (x.W - 1) * sx + 1 + static_cast<int>(tlbr[1] + tlbr[3]);
     p.out = new_buf(static_cast<size_t>(p.Ho) * p.Wo * x.C * 2);
     Val o = x;
     o.H = p.Ho;
     o.W = p.Wo;
+    o.buf = p.out;
+    define(n.outputs[0], o);
+    add_op(std::move(p));
+  }
+
+  bool scalar_init(const std::string& name, float& v) const {
+    auto it = m_.initializers.find(name);
+    if (it == m_.initializers.end() || it->second.numel() != 1) return false;
+    v = it->second.f.empty() ? static_cast<float>(it->second.i.at(0)) : it->second.f[0];
+    return true;
+  }
+
+  // Comparisons (bool results are stored as 1 / 0 activations): two activations -> a binary op,
+  // an activation and a scalar constant -> a unary code (the constant on the left mirrors the test).
+  void lower_compare(int idx) {
+    const Node& n = m_.nodes[idx];
+    static const std::map<std::string, int> codes = {
+        {"Greater", 18}, {"Less", 19}, {"Equal", 20}, {"GreaterOrEqual", 21}, {"LessOrEqual", 22}};
+    float c = 0.f;
+    if (scalar_init(n.in(1), c)) return emit_unary(n, materialize_in(n.in(0), n), codes.at(n.op_type), c, 0.f, n.outputs[0]);
+    if (scalar_init(n.in(0), c)) {
+      int code = codes.at(n.op_type);
+      code = code == 18 ? 19 : code == 19 ? 18 : code == 21 ? 22 : code == 22 ? 21 : code;
+      return emit_unary(n, materialize_in(n.in(1), n), code, c, 0.f, n.outputs[0]);
+    }
+    if (lower_binary_acts(n)) return;
+    throw std::runtime_error(n.op_type + " " + n.name + ": only two activations of one shape or one and a scalar");
+  }
+
+  // Where(cond, a, b): cond an activation; a / b activations of cond's shape or scalar constants.
+  void lower_where(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val c = materialize_in(n.in(0), n);
+    if (!dense(c)) throw std::runtime_error("Where " + n.name + ": the condition must be a dense activation");
+    PlanOp p;
+    p.kind = PlanOp::WHERE;
+    p.name = n.name;
+    p.in = c.buf;
+    float* sv[2] = {&p.clip_lo, &p.clip_hi};
+    int* bufs[2] = {&p.in2, &p.in3};
+    const Val* like = &c;
+    Val vb[2];
+    for (int k = 0; k < 2; ++k) {
+      if (scalar_init(n.in(1 + k), *sv[k])) continue;
+      vb[k] = materialize_in(n.in(1 + k), n);
+      if (!dense(vb[k]) || vb[k].kind != c.kind || vb[k].H != c.H || vb[k].W != c.W || vb[k].C != c.C ||
+          vb[k].logical() != c.logical())
+        throw std::runtime_error("Where " + n.name + ": the branches must be scalars or activations of the condition's shape");
+      *bufs[k] = vb[k].buf;
+      like = &vb[k];
+    }
+    p.C = c.C;
+    p.Cp = c.logical();
+    p.rows_per_sample = rows_of(c);
+    p.out = new_buf(static_cast<size_t>(rows_of(c)) * c.C * 2);
+    Val o = *like;
+    o.buf = p.out;
+    o.has_affine = false;
+    define(n.outputs[0], o);
+    add_op(std::move(p));
+  }
+
+  // Cast of an activation: to a float type -> the same values; to bool -> v != 0.  Integer targets
+  // would need rounding the stored representation cannot express exactly: rejected.
+  void lower_cast(int idx) {
+    const Node& n = m_.nodes[idx];
+    const int to = static_cast<int>(n.get_int("to", onnx::FLOAT));
+    if (to == onnx::BOOL) return emit_unary(n, materialize_in(n.in(0), n), 24, 0.f, 0.f, n.outputs[0]);
+    if (!onnx::is_float_type(to)) throw std::runtime_error("Cast " + n.name + ": only casts to float types or bool");
+    define(n.outputs[0], val(n.in(0), n));
+  }
+
+  // Resize (opset 10+: scales / sizes inputs) and Upsample (scales attribute or input) of an
+  // image: nearest or linear over H, W.
+  void lower_resize(int idx) {
+    const Node& n = m_.nodes[idx];
+    const Val x = materialize_in(n.in(0), n);
+    if (x.kind != Val::NHWC || !dense(x)) throw std::runtime_error(n.op_type + " " + n.name + ": only images");
+    const std::string mode = n.get_string("mode", "nearest");
+    if (mode != "nearest" && mode != "linear" && mode != "bilinear")
+      throw std::runtime_error(n.op_type + " " + n.name + ": mode " + mode + " is not supported (nearest, linear)");
+    if (n.get_int("antialias", 0) != 0) throw std::runtime_error(n.op_type + " " + n.name + ": antialias is not supported");
+    if (n.has("axes")) throw std::runtime_error(n.op_type + " " + n.name + ": the axes attribute is not supported");
+    std::vector<float> scales = n.get_floats("scales");
+    std::vector<int64_t> sizes;
+    const bool upsample = n.op_type == "Upsample";
+    auto floats_of = [&](const std::string& nm) {
+      auto it = m_.initializers.find(nm);
+      if (it == m_.initializers.end()) throw std::runtime_error(n.op_type + " " + n.name + ": scales must be a constant");
+      return it->second.f;
+    };
+    if (scales.empty()) {
+      if (upsample && n.inputs.size() >= 2) scales = floats_of(n.in(1));
+      if (!upsample && n.inputs.size() == 2 && !n.in(1).empty()) scales = floats_of(n.in(1));  // opset 10
+      if (!upsample && n.inputs.size() >= 3 && !n.in(2).empty() && !floats_of(n.in(2)).empty()) scales = floats_of(n.in(2));
+      if (!upsample && scales.empty() && n.inputs.size() >= 4 && !n.in(3).empty() && !ints_of(n.in(3), sizes))
+        throw std::runtime_error(n.op_type + " " + n.name + ": sizes must be known at load time");
+    }
+    float sh, sw;
+    int Ho, Wo;
+    if (!sizes.empty()) {
+      if (sizes.size() != 4 || (sizes[1] != x.logical() && sizes[1] != kBatchDim))
+        throw std::runtime_error(n.op_type + " " + n.name + ": sizes must be [N, C, H, W] with C unchanged");
+      Ho = static_cast<int>(sizes[2]);
+      Wo = static_cast<int>(sizes[3]);
+      sh = static_cast<float>(Ho) / x.H;
+      sw = static_cast<float>(Wo) / x.W;
+    } else {
+      if (scales.size() != 4 || scales[0] != 1.f || scales[1] != 1.f)
+        throw std::runtime_error(n.op_type + " " + n.name + ": scales must be [1, 1, sh, sw]");
+      sh = scales[2];
+      sw = scales[3];
+      Ho = static_cast<int>(std::floor(x.H * static_cast<double>(sh)));
+      Wo = static_cast<int>(std::floor(x.W * static_cast<double>(sw)));
+    }
+    if (Ho < 1 || Wo < 1 || !(sh > 0.f) || !(sw > 0.f)) throw std::runtime_error(n.op_type + " " + n.name + ": empty output");
+    static const std::map<std::string, int> coords = {{"half_pixel", 0}, {"asymmetric", 1}, {"align_corners", 2},
+                                                      {"pytorch_half_pixel", 3}, {"tf_half_pixel_for_nn", 4}};
+    static const std::map<std::string, int> nearests = {
+        {"round_prefer_floor", 0}, {"round_prefer_ceil", 1}, {"floor", 2}, {"ceil", 3}};
+    // Upsample and opset-10 Resize: asymmetric coordinates, floor rounding for nearest
+    const bool legacy = upsample || m_.opset() < 11;
+    const std::string cm = legacy ? "asymmetric" : n.get_string("coordinate_transformation_mode", "half_pixel");
+    const std::string nm = legacy ? "floor" : n.get_string("nearest_mode", "round_prefer_floor");
+    if (!coords.count(cm) || !nearests.count(nm))
+      throw std::runtime_error(n.op_type + " " + n.name + ": coordinate mode " + cm + " / nearest mode " + nm + " is not supported");
+    PlanOp p;
+    p.kind = PlanOp::RESIZE;
+    p.name = n.name;
+    p.in = x.buf;
+    p.C = x.C;
+    p.H = x.H;
+    p.W = x.W;
+    p.Ho = Ho;
+    p.Wo = Wo;
+    p.clip_lo = sh;
+    p.clip_hi = sw;
+    p.gidx = coords.at(cm);
+    p.act = mode == "nearest" ? 0 : 1;
+    p.is_max = nearests.at(nm);
+    p.out = new_buf(static_cast<size_t>(Ho) * Wo * x.C * 2);
+    Val o = x;
+    o.H = Ho;
+    o.W = Wo;
     o.buf = p.out;
     define(n.outputs[0], o);
     add_op(std::move(p));
@@ -1794,8 +1968,12 @@ class Planner {
   bool lower_binary_acts(const Node& n) {
     if (n.inputs.size() != 2 || !vid_.count(n.in(0)) || !vid_.count(n.in(1))) return false;
     const std::string& t = n.op_type;
-    const int op = t == "Add" ? 0 : t == "Sub" ? 1 : t == "Mul" ? 2 : t == "Div" ? 3 : t == "Max" ? 4 : t == "Min" ? 5 : -1;
-    if (op < 0) return false;
+    static const std::map<std::string, int> ops = {
+        {"Add", 0}, {"Sub", 1}, {"Mul", 2}, {"Div", 3}, {"Max", 4}, {"Min", 5}, {"Or", 4}, {"And", 5},
+        {"Greater", 6}, {"Less", 7}, {"Equal", 8}, {"GreaterOrEqual", 9}, {"LessOrEqual", 10}};
+    auto oi = ops.find(t);
+    if (oi == ops.end()) return false;
+    int op = oi->second;
     for (int side = 0; side < 2; ++side)
       if (vals_[vid_.at(n.in(side))].kind == Val::GRAPH_IN) materialize_in(n.in(side), n);
     Val a = vals_[vid_.at(n.in(0))], b = vals_[vid_.at(n.in(1))];
@@ -1806,8 +1984,9 @@ class Planner {
       ymode = 0;
     } else if (rows_of(b) == 1 && rows_of(a) > 1) {
       ymode = 1;
-    } else if (rows_of(a) == 1 && rows_of(b) > 1 && (op == 0 || op == 2 || op == 4 || op == 5)) {
-      std::swap(a, b);  // commutative: broadcast operand second
+    } else if (rows_of(a) == 1 && rows_of(b) > 1 && op != 1 && op != 3) {
+      std::swap(a, b);  // broadcast operand second: commutative ops, comparisons mirrored
+      if (op >= 6) op = op == 6 ? 7 : op == 7 ? 6 : op == 9 ? 10 : op == 10 ? 9 : op;
       ymode = 1;
     } else {
       return false;
@@ -2317,8 +2496,90 @@ std::string Plan::summary() const {
   return os.str();
 }
 
+namespace {
+
+onnx::Attribute ints_attr(const std::string& name, std::vector<int64_t> v) {
+  onnx::Attribute a;
+  a.name = name;
+  a.type = onnx::Attribute::INTS;
+  a.ints = std::move(v);
+  return a;
+}
+
+bool has_conv_transpose(const onnx::Model& m) {
+  for (const auto& n : m.nodes)
+    if (n.op_type == "ConvTranspose" && n.domain.empty()) return true;
+  return false;
+}
+
+// ConvTranspose (2-D, group 1, dilation 1, explicit pads, weights an initializer) -> ZeroInsert +
+// Conv: the input with stride - 1 zeros between its pixels and k - 1 - p zero borders (+ the output
+// padding at the end), convolved at stride 1 with the transposed, flipped kernel -- the MFMA conv
+// path instead of a scatter kernel.  Other ConvTranspose forms are left for the planner to report.
+onnx::Model rewrite_conv_transpose(const onnx::Model& src) {
+  onnx::Model m = src;
+  std::vector<onnx::Node> out;
+  for (const auto& n : src.nodes) {
+    auto wi = m.initializers.find(n.in(1));
+    bool ok = n.op_type == "ConvTranspose" && n.domain.empty() && wi != m.initializers.end() && wi->second.dims.size() == 4 &&
+              n.get_int("group", 1) == 1 && !n.has("output_shape") && n.get_string("auto_pad", "NOTSET") == "NOTSET";
+    const auto dl = n.get_ints("dilations", {1, 1}), st = n.get_ints("strides", {1, 1});
+    const auto pd = n.get_ints("pads", {0, 0, 0, 0}), op = n.get_ints("output_padding", {0, 0});
+    ok = ok && dl.size() == 2 && dl[0] == 1 && dl[1] == 1 && st.size() == 2 && pd.size() == 4 && op.size() == 2;
+    if (!ok) {
+      out.push_back(n);
+      continue;
+    }
+    const auto& w = wi->second;
+    const int64_t Cin = w.dims[0], Cout = w.dims[1], kh = w.dims[2], kw = w.dims[3];
+    const std::vector<int64_t> zp = {kh - 1 - pd[0], kw - 1 - pd[1], kh - 1 - pd[2] + op[0], kw - 1 - pd[3] + op[1]};
+    if (*std::min_element(zp.begin(), zp.end()) < 0) {  // cropping transposed convs: not rewritten
+      out.push_back(n);
+      continue;
+    }
+    onnx::Node zi;
+    zi.name = n.name + "/zero_insert";
+    zi.op_type = "ZeroInsert";
+    zi.domain = "die";
+    zi.inputs = {n.in(0)};
+    zi.outputs = {n.outputs.at(0) + "/zero_insert"};
+    zi.attrs["strides"] = ints_attr("strides", st);
+    zi.attrs["pads"] = ints_attr("pads", zp);
+    onnx::Tensor cw;
+    cw.name = n.in(1) + "/as_conv";
+    cw.dims = {Cout, Cin, kh, kw};
+    cw.f.resize(static_cast<size_t>(Cout * Cin * kh * kw));
+    for (int64_t ci = 0; ci < Cin; ++ci)
+      for (int64_t co = 0; co < Cout; ++co)
+        for (int64_t y = 0; y < kh; ++y)
+          for (int64_t x = 0; x < kw; ++x)
+            cw.f[((co * Cin + ci) * kh + y) * kw + x] = w.f[((ci * Cout + co) * kh + (kh - 1 - y)) * kw + (kw - 1 - x)];
+    m.initializers[cw.name] = cw;
+    onnx::Node cv;
+    cv.name = n.name;
+    cv.op_type = "Conv";
+    cv.inputs = {zi.outputs[0], cw.name};
+    if (!n.in(2).empty()) cv.inputs.push_back(n.in(2));
+    cv.outputs = n.outputs;
+    cv.attrs["kernel_shape"] = ints_attr("kernel_shape", {kh, kw});
+    cv.attrs["strides"] = ints_attr("strides", {1, 1});
+    cv.attrs["pads"] = ints_attr("pads", {0, 0, 0, 0});
+    cv.attrs["dilations"] = ints_attr("dilations", {1, 1});
+    out.push_back(std::move(zi));
+    out.push_back(std::move(cv));
+  }
+  m.nodes = std::move(out);
+  return m;
+}
+
+}  // namespace
+
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs,
                 bool fuse_stem_pool) {
+  if (has_conv_transpose(m)) {
+    const onnx::Model r = rewrite_conv_transpose(m);
+    return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool).run();
+  }
   return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool).run();
 }
 
@@ -2330,13 +2591,26 @@ std::string PlanReport::text() const {
 }
 
 PlanReport plan_report(const onnx::Model& m, int max_batch, bool split) {
-  Planner p(m, max_batch, false, split, false);
+  const bool rw = has_conv_transpose(m);
+  const onnx::Model r = rw ? rewrite_conv_transpose(m) : onnx::Model();
+  Planner p(rw ? r : m, max_batch, false, split, false);
   try {
     p.run();
   } catch (const std::exception& e) {
     if (p.report_.supported) {  // failed outside the per-node walk (input, output layout)
       p.report_.supported = false;
       p.report_.unsupported.push_back(PlanReport::Item{"(graph)", "", e.what()});
+    }
+  }
+  std::unordered_set<std::string> ct;
+  for (const auto& n : m.nodes)
+    if (n.op_type == "ConvTranspose") ct.insert(n.name);
+  for (auto& it : p.report_.unsupported) {  // report rewritten nodes under the model's own names
+    if (ct.count(it.node)) it.op = "ConvTranspose";
+    const std::string suf = "/zero_insert";
+    if (it.node.size() > suf.size() && it.node.compare(it.node.size() - suf.size(), suf.size(), suf) == 0) {
+      it.node.resize(it.node.size() - suf.size());
+      it.op = "ConvTranspose";
     }
   }
   return p.report_;

@@ -47,7 +47,11 @@ struct PlanOp {
     // ResNet-v2 bottleneck boundary in one launch (kernels/conv_pair.hip): a dual-store 1x1 expand
     // conv fused with the 1x1 reduce conv that is the sole reader of its pre-activation output
     CONV_PAIR,
-    PAD  // NHWC zero padding (ONNX Pad not folded into a conv): out [Ho][Wo] = in [H][W] at (ph, pw)
+    PAD,     // NHWC zero padding (ONNX Pad not folded into a conv): out [Ho][Wo] = in [H][W] at (ph, pw),
+             // stride sh, sw (zero insertion: ConvTranspose lowered to a stride-1 conv)
+    WHERE,   // out = in != 0 ? in2 : in3 (in2 / in3 = -1: the scalars clip_lo / clip_hi)
+    RESIZE   // NHWC Resize: in [H][W] -> out [Ho][Wo]; act = mode, gidx = coord, is_max = nearest mode,
+             // clip_lo / clip_hi = scales (output / input)
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).

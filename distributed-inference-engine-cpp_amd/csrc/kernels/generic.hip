@@ -105,6 +105,13 @@ __device__ __forceinline__ float apply_act(float v, int act, float a, float b) {
     case 15: return fminf(fmaxf(a * v + b, 0.f), 1.f);                   // HardSigmoid(alpha, beta)
     case 16: return v * fminf(fmaxf(v * (1.f / 6.f) + 0.5f, 0.f), 1.f);  // HardSwish
     case 17: return v > 20.f ? v : log1pf(expf(v));                       // Softplus
+    case 18: return v > a ? 1.f : 0.f;                                    // comparisons with a constant
+    case 19: return v < a ? 1.f : 0.f;
+    case 20: return v == a ? 1.f : 0.f;
+    case 21: return v >= a ? 1.f : 0.f;
+    case 22: return v <= a ? 1.f : 0.f;
+    case 23: return v == 0.f ? 1.f : 0.f;                                 // Not (bool as 0 / 1)
+    case 24: return v != 0.f ? 1.f : 0.f;                                 // Cast to bool
     default: return v;
   }
 }
@@ -130,12 +137,20 @@ __global__ void binary_kernel(const uint16_t* __restrict__ x, const uint16_t* __
     load8v(y + yr * C + c, yplane, split != 0, w);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      float v = op == 0   ? u[t] + w[t]
-                : op == 1 ? u[t] - w[t]
-                : op == 2 ? u[t] * w[t]
-                : op == 3 ? u[t] / w[t]
-                : op == 4 ? fmaxf(u[t], w[t])
-                          : fminf(u[t], w[t]);
+      float v;
+      switch (op) {
+        case 0: v = u[t] + w[t]; break;
+        case 1: v = u[t] - w[t]; break;
+        case 2: v = u[t] * w[t]; break;
+        case 3: v = u[t] / w[t]; break;
+        case 4: v = fmaxf(u[t], w[t]); break;
+        case 5: v = fminf(u[t], w[t]); break;
+        case 6: v = u[t] > w[t] ? 1.f : 0.f; break;
+        case 7: v = u[t] < w[t] ? 1.f : 0.f; break;
+        case 8: v = u[t] == w[t] ? 1.f : 0.f; break;
+        case 9: v = u[t] >= w[t] ? 1.f : 0.f; break;
+        default: v = u[t] <= w[t] ? 1.f : 0.f; break;
+      }
       u[t] = c + t < Cl ? apply_act(v, act, a, b) : 0.f;  // pad columns stay 0 (finite)
     }
     store8v(out + r * C + c, plane, split != 0, u);
@@ -168,10 +183,61 @@ __global__ void unary_kernel(const uint16_t* __restrict__ x, const float* __rest
   }
 }
 
-// Zero padding of an NHWC image: y [B][Ho][Wo][C] holds x [B][H][W][C] at offset (t, l), zeros
-// around it (ONNX Pad, constant mode, value 0, spatial axes only).
-__global__ void pad_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
-                                int Ho, int Wo, int t, int l, long long xplane, long long yplane, int split) {
+// out = cond != 0 ? a : b over rows [R][C]; a / b null: the scalar av / bv.  Where (bool as 0 / 1).
+__global__ void where_kernel(const uint16_t* __restrict__ c, const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                             float av, float bv, uint16_t* __restrict__ out, long long R, int C, long long plane,
+                             long long rows_per_sample, const long long* __restrict__ live, int split, int Cl) {
+  long long Rl = R;
+  if (live) Rl = min(R, *live * rows_per_sample);
+  const int G = C / 8;
+  const long long total = Rl * G;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long r = i / G;
+    const int col = static_cast<int>(i - r * G) * 8;
+    float cv[8], x[8], z[8];
+    load8v(c + r * C + col, plane, split != 0, cv);
+    if (a) load8v(a + r * C + col, plane, split != 0, x);
+    if (b) load8v(b + r * C + col, plane, split != 0, z);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float p = a ? x[t] : av, q = b ? z[t] : bv;
+      cv[t] = col + t < Cl ? (cv[t] != 0.f ? p : q) : 0.f;
+    }
+    store8v(out + r * C + col, plane, split != 0, cv);
+  }
+}
+
+// ONNX Resize / Upsample of an NHWC image (4-D, N and C scales 1).  coord: 0 half_pixel,
+// 1 asymmetric, 2 align_corners, 3 pytorch_half_pixel, 4 tf_half_pixel_for_nn; mode 0 nearest
+// (nearest: 0 round_prefer_floor, 1 round_prefer_ceil, 2 floor, 3 ceil; a bit copy of the source
+// pixel), 1 linear (bilinear, neighbour indices clamped to the image = the spec's edge padding).
+__device__ __forceinline__ float resize_src(int o, float scale, int in, int out, int coord) {
+  switch (coord) {
+    case 1: return o / scale;
+    case 2: return out > 1 ? o * static_cast<float>(in - 1) / static_cast<float>(out - 1) : 0.f;
+    case 3: return out > 1 ? (o + 0.5f) / scale - 0.5f : 0.f;
+    case 4: return (o + 0.5f) / scale;
+    default: return (o + 0.5f) / scale - 0.5f;
+  }
+}
+
+__device__ __forceinline__ int resize_nearest(float s, int nearest, int in) {
+  const float f = floorf(s);
+  int i;
+  switch (nearest) {
+    case 1: i = s - f == 0.5f ? static_cast<int>(f) + 1 : static_cast<int>(rintf(s)); break;
+    case 2: i = static_cast<int>(f); break;
+    case 3: i = static_cast<int>(ceilf(s)); break;
+    default: i = s - f == 0.5f ? static_cast<int>(f) : static_cast<int>(rintf(s)); break;
+  }
+  return min(max(i, 0), in - 1);
+}
+
+__global__ void resize_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
+                                   int Ho, int Wo, float sh, float sw, int coord, int mode, int nearest,
+                                   long long xplane, long long yplane, const long long* __restrict__ live, int split) {
+  if (live) B = min(B, static_cast<int>(*live));
   const int G = C / 8;
   const long long total = static_cast<long long>(B) * Ho * Wo * G;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
@@ -182,10 +248,54 @@ __global__ void pad_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __rest
     r /= Wo;
     const int h = static_cast<int>(r % Ho);
     const long long b = r / Ho;
-    const int sh = h - t, sw = w - l;
+    const float fy = resize_src(h, sh, H, Ho, coord), fx = resize_src(w, sw, W, Wo, coord);
+    uint16_t* d = y + ((b * Ho + h) * Wo + w) * C + cg * 8;
+    const uint16_t* xb = x + b * H * W * C + cg * 8;
+    if (mode == 0) {
+      const uint16_t* s = xb + (static_cast<long long>(resize_nearest(fy, nearest, H)) * W + resize_nearest(fx, nearest, W)) * C;
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+      if (split) *reinterpret_cast<uint4*>(d + yplane) = *reinterpret_cast<const uint4*>(s + xplane);
+      continue;
+    }
+    const float y0f = floorf(fy), x0f = floorf(fx);
+    const float ay = fy - y0f, ax = fx - x0f;
+    const int y0 = min(max(static_cast<int>(y0f), 0), H - 1), y1 = min(max(static_cast<int>(y0f) + 1, 0), H - 1);
+    const int x0 = min(max(static_cast<int>(x0f), 0), W - 1), x1 = min(max(static_cast<int>(x0f) + 1, 0), W - 1);
+    float p00[8], p01[8], p10[8], p11[8], v[8];
+    load8v(xb + (static_cast<long long>(y0) * W + x0) * C, xplane, split != 0, p00);
+    load8v(xb + (static_cast<long long>(y0) * W + x1) * C, xplane, split != 0, p01);
+    load8v(xb + (static_cast<long long>(y1) * W + x0) * C, xplane, split != 0, p10);
+    load8v(xb + (static_cast<long long>(y1) * W + x1) * C, xplane, split != 0, p11);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float top = p00[t] * (1.f - ax) + p01[t] * ax, bot = p10[t] * (1.f - ax) + p11[t] * ax;
+      v[t] = top * (1.f - ay) + bot * ay;
+    }
+    store8v(d, yplane, split != 0, v);
+  }
+}
+
+// Zero padding of an NHWC image: y [B][Ho][Wo][C] holds x [B][H][W][C] at offset (t, l), zeros
+// around it (ONNX Pad, constant mode, value 0, spatial axes only).  Strides sy, sx > 1 also insert
+// sy - 1 / sx - 1 zero rows / columns between the input's (ConvTranspose as a stride-1 conv).
+__global__ void pad_nhwc_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B, int H, int W, int C,
+                                int Ho, int Wo, int t, int l, long long xplane, long long yplane, int split, int sy,
+                                int sx) {
+  const int G = C / 8;
+  const long long total = static_cast<long long>(B) * Ho * Wo * G;
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int cg = static_cast<int>(i % G);
+    long long r = i / G;
+    const int w = static_cast<int>(r % Wo);
+    r /= Wo;
+    const int h = static_cast<int>(r % Ho);
+    const long long b = r / Ho;
+    const int dh = h - t, dw = w - l;
+    const int sh = dh / sy, sw = dw / sx;
     uint16_t* d = y + ((b * Ho + h) * Wo + w) * C + cg * 8;
     uint4 hi = make_uint4(0, 0, 0, 0), lo = hi;
-    if (sh >= 0 && sh < H && sw >= 0 && sw < W) {
+    if (dh >= 0 && dw >= 0 && dh == sh * sy && dw == sw * sx && sh < H && sw < W) {
       const uint16_t* s = x + ((b * H + sh) * W + sw) * C + cg * 8;
       hi = *reinterpret_cast<const uint4*>(s);
       if (split) lo = *reinterpret_cast<const uint4*>(s + xplane);
@@ -224,11 +334,33 @@ __global__ void nhwc_to_nchw_strided_kernel(const uint16_t* __restrict__ x, floa
 }  // namespace
 
 hipError_t pad_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int t, int l,
-                    hipStream_t s, int split) {
-  if (C % 8 || t < 0 || l < 0 || Ho < H + t || Wo < W + l) return hipErrorInvalidValue;
+                    hipStream_t s, int split, int sy, int sx) {
+  if (C % 8 || t < 0 || l < 0 || sy < 1 || sx < 1 || Ho < (H - 1) * sy + 1 + t || Wo < (W - 1) * sx + 1 + l)
+    return hipErrorInvalidValue;
   const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(pad_nhwc_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, t, l,
-                     static_cast<long long>(B) * H * W * C, static_cast<long long>(B) * Ho * Wo * C, split);
+                     static_cast<long long>(B) * H * W * C, static_cast<long long>(B) * Ho * Wo * C, split, sy, sx);
+  return hipGetLastError();
+}
+
+hipError_t where_rows(const uint16_t* c, const uint16_t* a, const uint16_t* b, float av, float bv, uint16_t* out,
+                      long long R, int C, hipStream_t s, const long long* live, long long rows_per_sample, int split,
+                      int Cl) {
+  if (C % 8 || rows_per_sample <= 0 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(where_kernel, dim3(grid_for(R * (C / 8))), dim3(256), 0, s, c, a, b, av, bv, out, R, C, R * C,
+                     rows_per_sample, live, split, Cl ? Cl : C);
+  return hipGetLastError();
+}
+
+hipError_t resize_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, float scale_h,
+                       float scale_w, int coord, int mode, int nearest, hipStream_t s, const long long* live, int split) {
+  if (C % 8 || H < 1 || W < 1 || Ho < 1 || Wo < 1 || !(scale_h > 0.f) || !(scale_w > 0.f) || coord < 0 || coord > 4 ||
+      mode < 0 || mode > 1 || nearest < 0 || nearest > 3)
+    return hipErrorInvalidValue;
+  const long long work = static_cast<long long>(B) * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(resize_nhwc_kernel, dim3(grid_for(work)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo, scale_h,
+                     scale_w, coord, mode, nearest, static_cast<long long>(B) * H * W * C,
+                     static_cast<long long>(B) * Ho * Wo * C, live, split);
   return hipGetLastError();
 }
 
@@ -258,7 +390,7 @@ hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uin
 hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
                        int ymode, int op, int act, float a, float b, hipStream_t s, const long long* live, int split,
                        int Cl) {
-  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 5 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+  if (C % 8 || rows_per_sample <= 0 || op < 0 || op > 10 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
   if (Cl == 0) Cl = C;
   const long long plane = R * C;
   const long long yplane = ymode == 1 ? (R / rows_per_sample) * C : plane;
@@ -270,7 +402,7 @@ hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long
 hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, long long R, int C,
                       int act, float a, float b, hipStream_t s, const long long* live, long long rows_per_sample,
                       int split, int Cl) {
-  if (C % 8 || (live && rows_per_sample <= 0) || Cl < 0 || Cl > C || act < 0 || act > 17) return hipErrorInvalidValue;
+  if (C % 8 || (live && rows_per_sample <= 0) || Cl < 0 || Cl > C || act < 0 || act > 24) return hipErrorInvalidValue;
   hipLaunchKernelGGL(unary_kernel, dim3(grid_for(R * (C / 8))), dim3(256), 0, s, x, scale, shift, y, R, C, act, a, b,
                      rows_per_sample, live, split, Cl ? Cl : C);
   return hipGetLastError();

@@ -144,7 +144,8 @@ hipError_t input_prep_wide(const float* x, const float* scale, const float* shif
 hipError_t copy_cols(const uint16_t* x, long long xplane, int ldx, int colx, uint16_t* y, long long yplane, int ldy,
                      int coly, long long R, int ncols, hipStream_t s, int split = 0);
 // out = act(x op y) over [R][C] rows; ymode 0: y same shape; 1: y one row per sample (broadcast over
-// its rows_per_sample rows).  op 0 add, 1 sub, 2 mul, 3 div, 4 max, 5 min.  act codes as unary_rows.
+// its rows_per_sample rows).  op 0 add, 1 sub, 2 mul, 3 div, 4 max, 5 min, 6-10 x > / < / == / >= / <= y (1 or 0).
+// act codes as unary_rows.
 // Cl (0 = C): logical channels; the pad columns [Cl, C) are written 0, whatever the op gives for
 // them (Div of two zero pads is NaN, and NaN * 0 would poison the next GEMM's every output).
 hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long long R, int C, long long rows_per_sample,
@@ -153,13 +154,25 @@ hipError_t binary_rows(const uint16_t* x, const uint16_t* y, uint16_t* out, long
 // y = act(x * scale[c] + shift[c]) (scale/shift nullable); act 0 none, 1 ReLU, 2 GELU (erf),
 // 3 Clip(a, b), 4 sigmoid, 5 tanh, 6 leaky ReLU (slope a), 7 exp, 8 abs, 9 sqrt, 10 neg,
 // 11 reciprocal, 12 log, 13 erf, 14 pow(x, a), 15 HardSigmoid(alpha a, beta b), 16 HardSwish,
-// 17 softplus.  Cl (0 = C): logical channels; pad columns [Cl, C) are written 0.
+// 17 softplus, 18-22 v > / < / == / >= / <= a (1 or 0), 23 Not (v == 0), 24 v != 0 (Cast to bool).
+// Cl (0 = C): logical channels; pad columns [Cl, C) are written 0.
 hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift, uint16_t* y, long long R, int C,
                       int act, float a, float b, hipStream_t s, const long long* live = nullptr,
                       long long rows_per_sample = 0, int split = 0, int Cl = 0);
 // NHWC zero padding: y [B][Ho][Wo][C] = x [B][H][W][C] placed at (t, l), zeros around (C % 8 == 0).
+// Strides sy, sx > 1 insert zeros between input pixels (ConvTranspose lowered to a stride-1 conv).
 hipError_t pad_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int t, int l,
-                    hipStream_t s, int split = 0);
+                    hipStream_t s, int split = 0, int sy = 1, int sx = 1);
+// out = cond != 0 ? a : b over rows [R][C] (a / b null: the scalars av / bv); pad columns written 0.
+hipError_t where_rows(const uint16_t* c, const uint16_t* a, const uint16_t* b, float av, float bv, uint16_t* out,
+                      long long R, int C, hipStream_t s, const long long* live = nullptr, long long rows_per_sample = 1,
+                      int split = 0, int Cl = 0);
+// ONNX Resize / Upsample of an NHWC image.  coord: 0 half_pixel, 1 asymmetric, 2 align_corners,
+// 3 pytorch_half_pixel, 4 tf_half_pixel_for_nn; mode 0 nearest (nearest: 0 round_prefer_floor,
+// 1 round_prefer_ceil, 2 floor, 3 ceil), 1 linear.  scale_*: output / input (the op's scales).
+hipError_t resize_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, float scale_h,
+                       float scale_w, int coord, int mode, int nearest, hipStream_t s, const long long* live = nullptr,
+                       int split = 0);
 // f32 [R][C] from bf16 / split rows of pitch ld >= C (graph outputs with padded columns).
 hipError_t rows_to_f32(const uint16_t* x, float* y, long long R, int C, int ld, hipStream_t s, int split = 0);
 // f32 NCHW [B][C][H][W] from bf16 NHWC with Cs >= C stored channels.

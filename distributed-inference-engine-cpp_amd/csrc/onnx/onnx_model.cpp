@@ -479,6 +479,10 @@ std::vector<int64_t> Node::get_ints(const std::string& k, const std::vector<int6
   auto it = attrs.find(k);
   return it == attrs.end() ? d : it->second.ints;
 }
+std::vector<float> Node::get_floats(const std::string& k, const std::vector<float>& d) const {
+  auto it = attrs.find(k);
+  return it == attrs.end() ? d : it->second.floats;
+}
 const std::string& Node::in(size_t i) const {
   static const std::string empty;
   return i < inputs.size() ? inputs[i] : empty;

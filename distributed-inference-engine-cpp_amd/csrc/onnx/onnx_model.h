@@ -63,6 +63,7 @@ struct Node {
   float get_float(const std::string& k, float d) const;
   std::string get_string(const std::string& k, const std::string& d) const;
   std::vector<int64_t> get_ints(const std::string& k, const std::vector<int64_t>& d = {}) const;
+  std::vector<float> get_floats(const std::string& k, const std::vector<float>& d = {}) const;
   // Input i or "" when absent/optional.
   const std::string& in(size_t i) const;
 };

@@ -17,6 +17,12 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
               Pad folded into a conv, Pad before a MaxPool (a pad pass), HardSwish, channel Split,
               Abs / Neg / Exp / Softplus / HardSigmoid / Max / Min / Pow / Reciprocal / Log / Sqrt /
               Erf, ReduceMax / ReduceSum over the spatial axes, GlobalMaxPool, a rows Split.
+* `upsample_net` a decoder-style CNN: ConvTranspose (stride 2, output_padding, 12 output channels),
+              Resize nearest (asymmetric / floor, the torch export), Resize linear down (half_pixel)
+              and up (align_corners), comparisons of two activations and with constants, Where
+              with activation and scalar branches, Not / And / Or, Cast of masks to float.  Every
+              mask multiplies a value that is 0 where the mask flips, so bf16 rounding near a
+              threshold cannot change the output discontinuously.
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -35,6 +41,7 @@ SPECS = {
     "se_cnn": dict(in_ch=12, image=16, classes=10),
     "ratio_mlp": dict(in_features=40, hidden=10, classes=5),
     "ops_zoo": dict(in_ch=8, image=16, classes=10),
+    "upsample_net": dict(in_ch=8, image=12, classes=10),
 }
 
 
@@ -251,8 +258,49 @@ def build_ops_zoo(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.n
     return g.model_proto(opset=opset), {}
 
 
+def build_upsample_net(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["upsample_net"]
+    rng = _rng(seed)
+    g = GraphBuilder(name="upsample_net")
+    x = g.input("image", ["N", s["in_ch"], s["image"], s["image"]])
+    f32 = 1  # onnx FLOAT
+    empty = g.const(np.zeros(0, np.float32), "no_roi")
+
+    def c(v, name):
+        return g.const(np.array(v, np.float32), name)
+
+    w1 = g.init("conv1.weight", _lin(rng, 8 * 9, (16, 8, 3, 3)))
+    h = g.node("Relu", [g.node("Conv", [x, w1, g.init("conv1.bias", (0.1 * rng.standard_normal(16)).astype(np.float32))],
+                               name="conv1", kernel_shape=[3, 3], pads=[1, 1, 1, 1])], name="relu1")  # 12x12x16
+    wt = g.init("up.weight", _lin(rng, 16 * 9 / 4, (16, 12, 3, 3)))  # ConvTranspose weight [Cin, Cout, kh, kw]
+    d = g.node("ConvTranspose", [h, wt, g.init("up.bias", (0.1 * rng.standard_normal(12)).astype(np.float32))],
+               name="up", kernel_shape=[3, 3], strides=[2, 2], pads=[1, 1, 1, 1], output_padding=[1, 1])  # 24x24x12
+    u = g.node("Resize", [h, empty, g.const(np.array([1, 1, 2, 2], np.float32), "nn_scales")], name="nn_up",
+               mode="nearest", coordinate_transformation_mode="asymmetric", nearest_mode="floor")  # 24x24x16
+    u2 = g.node("Conv", [u, g.init("proj.weight", _lin(rng, 16, (12, 16, 1, 1)))], name="proj", kernel_shape=[1, 1])
+    z = g.node("Where", [g.node("Greater", [d, u2], name="gt"), d, u2], name="pick_max")           # max(d, u2)
+    z = g.node("Where", [g.node("Less", [z, c(0.0, "zero")], name="neg"), c(0.0, "zero_f"), z], name="relu_where")
+    r = g.node("Resize", [z, empty, g.const(np.array([1, 1, 0.5, 0.5], np.float32), "down_scales")], name="down",
+               mode="linear", coordinate_transformation_mode="half_pixel")                          # 12x12
+    r2 = g.node("Resize", [r, empty, g.const(np.array([1, 1, 1.5, 1.5], np.float32), "up_scales")], name="up15",
+                mode="linear", coordinate_transformation_mode="align_corners")                      # 18x18
+    r2 = g.node("Sub", [r2, c(0.3, "shift")], name="center")
+    m1 = g.node("And", [g.node("Greater", [r2, c(0.0, "zero2")], name="pos"),
+                        g.node("Less", [c(50.0, "big"), r2], name="huge")], name="pos_and")  # r2 > 0 and 50 < r2: empty
+    m1 = g.node("Or", [m1, g.node("Greater", [r2, c(0.0, "zero3")], name="pos2")], name="pos_or")  # = r2 > 0
+    m2 = g.node("Not", [m1], name="nonpos")
+    pos = g.node("Mul", [r2, g.node("Cast", [m1], name="m1f", to=f32)], name="pos_part")
+    neg = g.node("Mul", [r2, g.node("Cast", [m2], name="m2f", to=f32)], name="neg_part")
+    hsum = g.node("Sub", [pos, g.node("Mul", [neg, c(0.1, "slope")], name="leak")], name="leaky")  # leaky ReLU
+    z = g.node("Flatten", [g.node("GlobalAveragePool", [hsum], name="gap")], name="flat", axis=1)
+    w = g.init("fc.weight", _lin(rng, 12, (s["classes"], 12)))
+    y = g.node("Gemm", [z, w, g.init("fc.bias", np.zeros(s["classes"], np.float32))], name="fc", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
-            "ops_zoo": build_ops_zoo}
+            "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:

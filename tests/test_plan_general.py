@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net"]
 
 
 @pytest.fixture(scope="module")
@@ -45,12 +45,18 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
         assert kinds.count("pad") == 1 and kinds.count("gap") == 3 and kinds.count("copy_cols") == 8
         names = [o["name"] for o in s["ops"]]
         assert "pad1" not in names and "pad2" in names
+    if name == "upsample_net":
+        # ConvTranspose -> zero insertion pass + stride-1 conv; 3 resizes; 2 Where selects
+        assert kinds.count("pad") == 1 and kinds.count("resize") == 3 and kinds.count("where") == 2
+        names = [o["name"] for o in s["ops"]]
+        assert "up/zero_insert" in names and "up" in names
 
 
 def test_generic_models_run_on_the_cpu_oracle(native, gen_models):
     from die_amd.models import generic as G
 
-    for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10)), ("ops_zoo", (2, 10))):
+    for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10)), ("ops_zoo", (2, 10)),
+                        ("upsample_net", (2, 10))):
         y = native.cpu_run(gen_models[name], G.synthetic_input(name, 2))
         assert y.shape == shape and np.isfinite(y).all()
         if name in ("mlp", "se_cnn"):
