@@ -305,8 +305,8 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
       Json e = Json::object();
       static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                     "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                    "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize"};
-      static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::RESIZE + 1, "one name per PlanOp kind");
+                                    "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm"};
+      static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::BMM + 1, "one name per PlanOp kind");
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;

@@ -1097,6 +1097,11 @@ class HipEngine : public Engine {
                                static_cast<uint16_t*>(buf(op.out)), op.rows_per_sample * B, op.C, st, live,
                                op.rows_per_sample, sp_, op.Cp);
           break;
+        case PlanOp::BMM:
+          e = kern::bmm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
+                             static_cast<uint16_t*>(buf(op.out)), B, op.S, op.Cp, op.gidx, op.ld[0], op.ld[1], op.C, st,
+                             live, sp_);
+          break;
         case PlanOp::RESIZE:
           e = kern::resize_nhwc(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.H, op.W,
                                 op.C, op.Ho, op.Wo, op.clip_lo, op.clip_hi, op.gidx, op.act, op.is_max, st, live, sp_);
@@ -1241,8 +1246,8 @@ class HipEngine : public Engine {
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                   "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize"};
-    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::RESIZE + 1, "one name per PlanOp kind");
+                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm"};
+    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::BMM + 1, "one name per PlanOp kind");
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

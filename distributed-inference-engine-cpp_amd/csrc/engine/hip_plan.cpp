@@ -1081,7 +1081,34 @@ class Planner {
       define(n.outputs[0], c);
       return;
     }
-    throw std::runtime_error("MatMul " + n.name + ": activation x activation MatMul outside the attention pattern");
+    // general batched MatMul of two dense rank-3 row activations: [S, K] x [K, N] per sample
+    if (a.kind == Val::ROWS_BF16 && b.kind == Val::ROWS_BF16 && a.rank == 3 && b.rank == 3 && dense(a) && dense(b) &&
+        a.logical() == b.H * b.W) {
+      PlanOp p;
+      p.kind = PlanOp::BMM;
+      p.name = n.name;
+      p.in = a.buf;
+      p.in2 = b.buf;
+      p.S = static_cast<int>(rows_of(a));
+      p.gidx = a.logical();
+      p.ld[0] = a.C;
+      p.ld[1] = b.C;
+      p.C = b.C;
+      p.Cp = b.logical();
+      p.rows_per_sample = rows_of(a);
+      p.flops_per_sample = 2.0 * p.S * p.gidx * p.Cp;
+      p.out = new_buf(static_cast<size_t>(p.S) * p.C * 2);
+      Val o = a;
+      o.C = b.C;
+      o.cl = b.cl;
+      o.buf = p.out;
+      o.has_affine = false;
+      define(n.outputs[0], o);
+      add_op(std::move(p));
+      return;
+    }
+    throw std::runtime_error("MatMul " + n.name + ": activation x activation MatMul outside the attention pattern and the "
+                             "[S, K] x [K, N] row form");
   }
 
   void lower_scale(int idx) {

@@ -50,8 +50,10 @@ struct PlanOp {
     PAD,     // NHWC zero padding (ONNX Pad not folded into a conv): out [Ho][Wo] = in [H][W] at (ph, pw),
              // stride sh, sw (zero insertion: ConvTranspose lowered to a stride-1 conv)
     WHERE,   // out = in != 0 ? in2 : in3 (in2 / in3 = -1: the scalars clip_lo / clip_hi)
-    RESIZE   // NHWC Resize: in [H][W] -> out [Ho][Wo]; act = mode, gidx = coord, is_max = nearest mode,
+    RESIZE,  // NHWC Resize: in [H][W] -> out [Ho][Wo]; act = mode, gidx = coord, is_max = nearest mode,
              // clip_lo / clip_hi = scales (output / input)
+    BMM      // batched MatMul of two row activations: out [S][Cp pitch C] = in [S][gidx of ld[0]] x
+             // in2 [gidx][ld[1]]; Cp = logical N
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).

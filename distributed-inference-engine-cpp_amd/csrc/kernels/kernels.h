@@ -163,6 +163,10 @@ hipError_t unary_rows(const uint16_t* x, const float* scale, const float* shift,
 // Strides sy, sx > 1 insert zeros between input pixels (ConvTranspose lowered to a stride-1 conv).
 hipError_t pad_nhwc(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, int Ho, int Wo, int t, int l,
                     hipStream_t s, int split = 0, int sy = 1, int sx = 1);
+// Batched MatMul of two row activations (kernels/bmm.hip): C[b] (M x ldc) = A[b] (M x lda, first K
+// columns) * B[b] (K x ldb, first N columns); output columns [N, ldc) written 0.
+hipError_t bmm_rows(const uint16_t* A, const uint16_t* Bm, uint16_t* C, int batch, int M, int N, int K, int lda, int ldb,
+                    int ldc, hipStream_t s, const long long* live = nullptr, int split = 0);
 // out = cond != 0 ? a : b over rows [R][C] (a / b null: the scalars av / bv); pad columns written 0.
 hipError_t where_rows(const uint16_t* c, const uint16_t* a, const uint16_t* b, float av, float bv, uint16_t* out,
                       long long R, int C, hipStream_t s, const long long* live = nullptr, long long rows_per_sample = 1,

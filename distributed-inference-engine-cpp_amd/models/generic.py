@@ -23,6 +23,9 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
               with activation and scalar branches, Not / And / Or, Cast of masks to float.  Every
               mask multiplies a value that is 0 where the mask flips, so bf16 rounding near a
               threshold cannot change the output discontinuously.
+* `token_mixer` data-dependent token mixing: MatMul of two activations outside the attention
+              pattern (softmax(h W) [S, S] x h [S, D], and x g [S, 20]: inner size 24 and an
+              output width that are not multiples of 8).
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -42,6 +45,7 @@ SPECS = {
     "ratio_mlp": dict(in_features=40, hidden=10, classes=5),
     "ops_zoo": dict(in_ch=8, image=16, classes=10),
     "upsample_net": dict(in_ch=8, image=12, classes=10),
+    "token_mixer": dict(seq=24, dim=40, classes=10),
 }
 
 
@@ -299,8 +303,30 @@ def build_upsample_net(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str,
     return g.model_proto(opset=opset), {}
 
 
+def build_token_mixer(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["token_mixer"]
+    rng = _rng(seed)
+    S, D = s["seq"], s["dim"]
+    g = GraphBuilder(name="token_mixer")
+    x = g.input("tokens", ["N", S * D])
+    h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
+    logits = g.node("MatMul", [h, g.init("mix.weight", _lin(rng, D, (D, S)))], name="mix_logits")  # [N, S, S]
+    a = g.node("Softmax", [logits], name="mix_softmax", axis=-1)
+    m = g.node("MatMul", [a, h], name="mix")                                                  # [S, S] x [S, D]
+    h = g.node("Add", [m, h], name="mix_residual")
+    gl = g.node("Add", [g.node("MatMul", [h, g.init("gate.weight", _lin(rng, D, (D, 20)))], name="gate/MatMul"),
+                        g.init("gate.bias", (0.1 * rng.standard_normal(20)).astype(np.float32))], name="gate/Add")
+    gl = g.node("Tanh", [gl], name="gate_tanh")                                               # [N, S, 20]
+    m2 = g.node("MatMul", [a, gl], name="mix2")                                               # [S, S] x [S, 20]
+    pooled = g.node("ReduceMean", [m2], name="pool", axes=[1], keepdims=0)                    # [N, 20]
+    w = g.init("head.weight", _lin(rng, 20, (s["classes"], 20)))
+    y = g.node("Gemm", [pooled, w, g.init("head.bias", np.zeros(s["classes"], np.float32))], name="head", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
-            "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net}
+            "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:
@@ -311,7 +337,7 @@ def input_shape(name: str):
     s = SPECS[name]
     if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
-    if name == "bert":
+    if name == "bert" or name == "token_mixer":
         return (s["seq"] * s["dim"],)
     return (s["in_ch"], s["image"], s["image"])
 
