@@ -2,6 +2,8 @@
 #include "http.h"
 
 #include <arpa/inet.h>
+
+#include <atomic>
 #include <errno.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -57,19 +59,33 @@ std::string_view trim(std::string_view s) {
 
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
-void set_nodelay(int fd) {
+namespace {
+std::atomic<int> g_sock_buf_effective{-1};
+}
+
+int sock_buf_effective() { return g_sock_buf_effective.load(std::memory_order_relaxed); }
+
+void set_nodelay(int fd, bool loopback_peer) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-  // Fixed 4 MiB socket buffers (DIE_SOCK_BUF_KB overrides, 0 = kernel autotuning): a ~1 MB request
-  // body crosses loopback in fewer send/recv rounds.  A/B on the headline (profiles/r3_sock_buf_ab.md):
-  // gateway path 13.77k vs 13.32k req/s mean over 4 interleaved pairs, 11 % less sys time per request.
+  // Loopback peers only: fixed 4 MiB socket buffers (DIE_SOCK_BUF_KB overrides, 0 = kernel
+  // autotuning), so a ~1 MB request body crosses loopback in fewer send/recv rounds.  A/B on the
+  // headline (profiles/r3_sock_buf_ab.md): gateway path 13.77k vs 13.32k req/s mean over 4
+  // interleaved pairs, 11 % less sys time per request.  Remote peers keep TCP autotuning (a fixed
+  // SO_RCVBUF turns it off).  The kernel caps the value at net.core.[rw]mem_max: the size it
+  // actually granted is read back and reported (sock_buf_effective, worker /health "io").
   static const int buf = [] {
     const char* e = std::getenv("DIE_SOCK_BUF_KB");
     return (e && *e ? std::atoi(e) : 4096) * 1024;
   }();
-  if (buf > 0) {
+  if (buf > 0 && loopback_peer) {
     setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
     setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+    if (g_sock_buf_effective.load(std::memory_order_relaxed) < 0) {
+      int got = 0;
+      socklen_t len = sizeof got;
+      if (getsockopt(fd, SOL_SOCKET, SO_RCVBUF, &got, &len) == 0) g_sock_buf_effective.store(got, std::memory_order_relaxed);
+    }
   }
 }
 
@@ -615,7 +631,7 @@ void HttpServer::reactor_loop(Reactor* r) {
           socklen_t plen = sizeof peer;
           int fd = ::accept4(listen_fd_, reinterpret_cast<sockaddr*>(&peer), &plen, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (fd < 0) break;
-          set_nodelay(fd);
+          set_nodelay(fd, is_loopback(peer));
           auto c = std::make_unique<Conn>();
           c->fd = fd;
           c->loopback = is_loopback(peer);
@@ -764,7 +780,9 @@ int HttpClient::connect_new(std::string* error) {
       return -1;
     }
   }
-  set_nodelay(fd);
+  sockaddr_storage peer{};
+  socklen_t plen = sizeof peer;
+  set_nodelay(fd, getpeername(fd, reinterpret_cast<sockaddr*>(&peer), &plen) == 0 && is_loopback(peer));
   return fd;
 }
 

@@ -346,7 +346,7 @@ void AsyncHttpClient::run(Loop* L) {
       finish(std::move(j), std::nullopt, "socket() failed");
       return;
     }
-    set_nodelay(fd);
+    set_nodelay(fd, (ntohl(addr.sin_addr.s_addr) >> 24) == 127);
     int rc = ::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof addr);
     if (rc != 0 && errno != EINPROGRESS) {
       const std::string err = std::string("connect failed: ") + strerror(errno);

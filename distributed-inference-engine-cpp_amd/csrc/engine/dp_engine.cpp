@@ -418,10 +418,12 @@ class DpEngine : public Engine {
       if (device_gather_) {
         // rank-major logits: rank r's `per` rows are items [r*per, (r+1)*per), i.e. item order
         rows = r.outputs;
-        if (r.ok && r.rank_ok) {
+        if (r.rank_ok) {
+          // gathered rows + shard flags (also when this rank's own shard failed: its flag is 0, so
+          // dp_item_ok fails exactly its items -- the host backend's semantics)
           std::copy(r.rank_ok, r.rank_ok + world_, rank_ok.begin());
         } else {
-          ok = false;  // this rank's own batch failed (or never ran the collectives' D2H)
+          ok = false;  // the collectives' D2H never completed: nothing to answer from
         }
         if (ok && r.status) {
           dp_items_from_gathered(L, r.status, static_cast<size_t>(r.status_stride), st.data());

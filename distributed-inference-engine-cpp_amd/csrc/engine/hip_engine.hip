@@ -588,6 +588,8 @@ class HipEngine : public Engine {
           HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 0, 1,
                                       s_exec_[slot % n_exec_]));
           dp_collectives(sl, B, s_exec_[slot % n_exec_]);
+          job.dp_gathered = true;
+          job.has_text = text_cap_ > 0;
         } catch (const std::exception&) {
         }
       }
@@ -1305,6 +1307,7 @@ class HipEngine : public Engine {
     std::chrono::steady_clock::time_point t0;
     std::string error;
     bool has_text = false;
+    bool dp_gathered = false;  // failed, but the collectives ran with this rank's shard flag cleared
     int ev = 0;  // first of its kEvPerJob timing events in tev_
     int bi = 0;  // batch bucket
   };
@@ -1437,12 +1440,26 @@ class HipEngine : public Engine {
       } else {
         r.ok = false;
         r.error = job.error;
+        if (job.dp_gathered && comm_ && hipEventSynchronize(sl.ev_d2h) == hipSuccess) {
+          // this rank's shard failed, the others' rows arrived: hand them over with the flags, so the
+          // DP engine fails exactly this shard's items (the host backend's semantics, dp_layout.h)
+          r.gathered = dp_world_;
+          r.outputs = sl.h_gather;
+          r.output_numel = out_numel_;
+          r.status = job.has_text ? sl.h_gstatus : nullptr;
+          r.ntok = r.status ? sl.h_gstatus + max_batch_ : nullptr;
+          r.status_stride = static_cast<int>(status_len());
+          rank_ok_copy_.resize(static_cast<size_t>(dp_world_));
+          for (int k = 0; k < dp_world_; ++k)
+            rank_ok_copy_[static_cast<size_t>(k)] = sl.h_gstatus[static_cast<size_t>(k) * status_len() + rank_ok_index()];
+          r.rank_ok = rank_ok_copy_.data();
+        }
       }
       r.wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - job.t0).count();
       // Take the results out of the slot's pinned buffers and free the slot BEFORE the callbacks
       // (cache inserts, response hand-off for B requests): the batcher can dispatch the next batch
       // into this slot while they run, so the GPU does not idle behind host bookkeeping.
-      if (r.ok) {
+      if (r.ok || r.rank_ok) {
         const size_t rows = static_cast<size_t>(job.B) * (comm_ ? dp_world_ : 1);
         if (r.outputs) {
           out_copy_.assign(r.outputs, r.outputs + rows * out_numel_);

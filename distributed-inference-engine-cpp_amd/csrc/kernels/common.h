@@ -33,9 +33,10 @@ __device__ __forceinline__ void unpack2(uint32_t v, float& a, float& b) {
 // Chebyshev fit of Numerical Recipes' erfcc (fractional error < 1.2e-7 for every argument) in place
 // of ocml's erff: 1 rcp + 1 exp2 + 10 FMAs against ~45 instructions with lane-divergent branches.
 // Written without the 1 + erf cancellation, so the negative tail keeps its relative accuracy: max
-// relative error 1.7e-5 over all v (5e-7 for v > -2), max absolute 4e-7 -- below the split-fp32
-// representation error (2^-17 relative).  Replaces erff in the GEMM epilogues (ViT MLP1: 19M GELUs
-// per batch-32 forward).
+// relative error 5e-7 for v > -2 (below the split-fp32 representation error, 2^-17 = 7.6e-6) and
+// 1.7e-5 in the negative tail v < -2 (ABOVE it, where |GELU(v)| < 0.046; max absolute error 4e-7
+// over all v).  fp32-mode parity in that tail is therefore ~2e-5 relative; no reference fixture pins
+// it (parity unpinned).  Replaces erff in the GEMM epilogues (ViT MLP1: 19M GELUs per batch-32 forward).
 __device__ __forceinline__ float gelu_erf(float v) {
   const float z = fabsf(v) * 0.70710678118654752f;
   const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.f));

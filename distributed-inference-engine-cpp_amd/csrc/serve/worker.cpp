@@ -1,6 +1,7 @@
 #include <pthread.h>
 #include "worker.h"
 
+#include "../core/http_util.h"
 #include "../core/log.h"
 #include "../core/metrics.h"
 #include "../core/textpack.h"
@@ -529,6 +530,7 @@ Json WorkerNode::getHealth() const {
   io["device_busy_ms"] = busy ? busy->as_double() : 0.0;
   const Json* dev = es.find("device_id");
   io["device_id"] = dev ? dev->as_int() : -1LL;
+  io["loopback_sock_buf_bytes"] = static_cast<long long>(http_detail::sock_buf_effective());
   h["io"] = io;
   Json lg = Json::object();
   lg["level"] = static_cast<long long>(log_level());

@@ -125,7 +125,8 @@ def test_dp_rccl_world1_concurrent_rows_verified(native, models, dp_path):
 def test_dp_rccl_world1_injected_failure_does_not_hang(native, models):
     """A rank whose batch fails before reaching the device still issues its collectives (shard flag
     cleared), so RCCL never waits on it: the failed batches' requests get 500s, every other answer
-    is right, and the worker keeps serving."""
+    is right, and the worker keeps serving.  The failing rank answers from the gathered rows too
+    (only its own shard's items fail, as on the host backend)."""
     path, w, cfg = models["tiny"]
     wk = native.Worker(path, node_id="dpf", max_batch=8, cache_capacity=0,
                        engine={"device": "hip", "dp_world": 1, "autotune": False, "dp_force_merge": True,
@@ -137,6 +138,9 @@ def test_dp_rccl_world1_injected_failure_does_not_hang(native, models):
         assert res["mismatched"] == 0 and res["failed"] > 0 and res["ok"] > 0, res
         h = wk.health()
         assert h["engine"]["dp_backend"] == "rccl" and h["engine"]["options"]["fail_batch_every"] == 3
+        # the failed batches still ran the collectives: their items fail through the gathered shard
+        # flag (exactly the failed shard's items, as with the host backend), one count per request
+        assert h["engine"]["dp_shard_failed_items"] == res["failed"], (h["engine"], res)
     finally:
         wk.stop()
 
