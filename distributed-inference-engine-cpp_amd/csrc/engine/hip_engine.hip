@@ -1153,7 +1153,8 @@ class HipEngine : public Engine {
           break;
         case PlanOp::LAYERNORM:
           e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_);
+                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_,
+                                   op.Cp);
           break;
         case PlanOp::TOKENS:
           e = kern::tokens_assemble(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),

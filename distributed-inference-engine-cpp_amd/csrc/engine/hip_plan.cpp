@@ -1016,6 +1016,31 @@ class Planner {
         return;
       }
     }
+    // the graph input's rows [B, S*D] -> [B, S, D] with D % 8 != 0: the input-prep pass itself writes
+    // S rows of D (stored round8(D)) per sample -- the f32 input is [B*S][D] in memory already
+    if (x.kind == Val::ROWS_BF16 && x.rank == 2 && consumers(n.in(0)).size() == 1 && shp.size() == 3 &&
+        is_batch(shp[0]) && !graph_outputs_.count(n.in(0))) {
+      for (PlanOp& q : plan_.ops)
+        if (q.kind == PlanOp::ROWS_PREP && q.out == x.buf && q.rows_per_sample == 1) {
+          const int64_t F = q.C;
+          int64_t S = shp[1], D = shp[2];
+          if (S == -1 && D > 0) S = F / D;
+          if (D == -1 && S > 0) D = F / S;
+          if (S <= 0 || D <= 0 || S * D != F) break;
+          q.C = static_cast<int>(D);
+          q.Cp = round8(static_cast<int>(D));
+          q.rows_per_sample = S;
+          plan_.bufs[q.out].bytes_per_sample = static_cast<size_t>(S) * q.Cp * 2 * (split_ ? 2 : 1);
+          Val o = x;
+          o.H = static_cast<int>(S);
+          o.W = 1;
+          o.C = q.Cp;
+          o.cl = q.Cp != D ? static_cast<int>(D) : 0;
+          o.rank = 3;
+          define(n.outputs[0], o);
+          return;
+        }
+    }
     // one row per sample [B, C] -> [B, C, 1, 1] (gates broadcast over an image: squeeze-excitation)
     if ((x.kind == Val::ROWS_BF16 || x.kind == Val::NHWC) && x.H * x.W == 1 && shp.size() == 4 && is_batch(shp[0]) &&
         shp[1] == x.logical() && shp[2] == 1 && shp[3] == 1 && !x.flat_hw) {
@@ -1208,15 +1233,17 @@ class Planner {
   void lower_layernorm(int idx) {
     const Node& n = m_.nodes[idx];
     const Val x = val(n.in(0), n);
-    if (x.kind != Val::ROWS_BF16 || !dense(x) || x.padded())
-      throw std::runtime_error("LayerNormalization " + n.name + ": input must be dense rows with C % 8 == 0");
+    if (x.kind != Val::ROWS_BF16 || !dense(x))
+      throw std::runtime_error("LayerNormalization " + n.name + ": input must be dense rows");
     const int64_t axis = n.get_int("axis", -1);
     if (!(axis == -1 || axis == (x.rank ? x.rank : 2) - 1)) throw std::runtime_error("LayerNormalization: axis must be last");
-    if (x.C % 8 || x.C > 2048) throw std::runtime_error("LayerNormalization: C % 8 == 0 and C <= 2048 required");
-    std::vector<float> g = init(n.in(1), n).f, b(x.C, 0.f);
+    const int Cl = x.logical();
+    std::vector<float> g = init(n.in(1), n).f, b(Cl, 0.f);
     if (n.inputs.size() > 2 && !n.in(2).empty()) b = init(n.in(2), n).f;
-    if (static_cast<int>(g.size()) != x.C || static_cast<int>(b.size()) != x.C)
+    if (static_cast<int>(g.size()) != Cl || static_cast<int>(b.size()) != Cl)
       throw std::runtime_error("LayerNormalization " + n.name + ": scale/bias size mismatch");
+    g.resize(x.C, 0.f);  // stored pad columns: written 0 by the kernel
+    b.resize(x.C, 0.f);
     PlanOp p;
     p.kind = PlanOp::LAYERNORM;
     p.name = n.name;
@@ -1225,6 +1252,7 @@ class Planner {
     p.shift_off = push_f32(b);
     p.eps = n.get_float("epsilon", 1e-5f);
     p.C = x.C;
+    p.Cp = Cl;
     p.rows_per_sample = static_cast<long long>(x.H) * x.W;
     p.out = new_buf(static_cast<size_t>(x.H) * x.W * x.C * 2);
     Val o = x;
@@ -1537,7 +1565,7 @@ class Planner {
       used.push_back(c);
       cur = m_.nodes[c].outputs[0];
     }
-    if (x.C % 8 || x.C > 2048) fail("C % 8 == 0 and C <= 2048");
+    if (x.padded()) fail("C % 8 == 0 (stored pad columns)");
     for (int u : used) done_[u] = true;
     PlanOp p;
     p.kind = PlanOp::LAYERNORM;
@@ -1555,7 +1583,6 @@ class Planner {
     add_op(std::move(p));
   }
 
-  // Slice of one token along axis 1 of [B, S, C] rows (e.g. the cls token) -> row gather.
   // Explicit pads of a conv plus those of a zero Pad folded into it (lower_pad).
   std::vector<int64_t> conv_pads(const Node& n) const {
     auto pads = n.get_ints("pads", {0, 0, 0, 0});
@@ -1826,6 +1853,8 @@ class Planner {
     if (s0 != Cl) throw std::runtime_error("Split " + n.name + ": sizes do not cover the axis");
   }
 
+  // Slice of one token along axis 1 of [B, S, C] rows (e.g. the cls token) -> row gather; a channel
+  // range -> a column copy.
   void lower_slice(int idx) {
     const Node& n = m_.nodes[idx];
     const Val x = val(n.in(0), n);

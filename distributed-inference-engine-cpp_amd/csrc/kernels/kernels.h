@@ -272,9 +272,10 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
                                const long long* poffs = nullptr);
 
 // ---- transformer (transformer.hip) ----
-// LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0, C <= 2048), fp32 statistics.
+// LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0: the stored pitch), fp32
+// statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split = 0);
+                          long long rows, int C, hipStream_t s, int split = 0, int Cl = 0);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
                            int C, hipStream_t s, int split = 0);

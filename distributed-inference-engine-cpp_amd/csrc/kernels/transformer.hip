@@ -30,13 +30,14 @@ __device__ __forceinline__ float group_sum(float v) {
 }
 
 // LPR lanes per row (64 / LPR rows per wave); each lane holds up to CPL 8-element chunks of the row
-// in registers (two-pass mean/variance in fp32).  C % 8 == 0, C <= LPR*8*CPL.  C = 768 (ViT-B) runs
-// as 32 lanes x 3 chunks: every lane busy and two rows' loads in flight per wave (one row per wave
-// with 64 x 2 chunks left half the lanes idle in the second round).
+// in registers (two-pass mean/variance in fp32).  C % 8 == 0 (stored pitch), C <= LPR*8*CPL; the
+// statistics run over the first Cl (logical) columns and the pad columns are written 0.  C = 768
+// (ViT-B) runs as 32 lanes x 3 chunks: every lane busy and two rows' loads in flight per wave (one
+// row per wave with 64 x 2 chunks left half the lanes idle in the second round).
 template <int CPL, int LPR = 64>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         const float* __restrict__ g, const float* __restrict__ b,
-                                                        float eps, long long rows, int C, int split) {
+                                                        float eps, long long rows, int C, int split, int Cl) {
   constexpr int RPB = 256 / LPR;  // rows per block
   const int lane = threadIdx.x & (LPR - 1);
   const long long row = static_cast<long long>(blockIdx.x) * RPB + (threadIdx.x / LPR);
@@ -57,24 +58,27 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
       bv[i][1] = *reinterpret_cast<const float4*>(b + c * 8 + 4);
       load8v(xr + c * 8, plane, split != 0, v[i]);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) s += v[i][t];
+      for (int t = 0; t < 8; ++t) {
+        if (c * 8 + t >= Cl) v[i][t] = 0.f;  // pad columns: out of the statistics
+        s += v[i][t];
+      }
     } else {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[i][t] = 0.f;
     }
   }
-  const float mean = group_sum<LPR>(s) / C;
+  const float mean = group_sum<LPR>(s) / Cl;
   float q2 = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i)
     if (lane + LPR * i < nch) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const float d = v[i][t] - mean;
+        const float d = (lane + LPR * i) * 8 + t < Cl ? v[i][t] - mean : 0.f;
         q2 += d * d;
       }
     }
-  const float inv = rsqrtf(group_sum<LPR>(q2) / C + eps);
+  const float inv = rsqrtf(group_sum<LPR>(q2) / Cl + eps);
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + LPR * i;
@@ -83,8 +87,54 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
     const float bb[8] = {bv[i][0].x, bv[i][0].y, bv[i][0].z, bv[i][0].w, bv[i][1].x, bv[i][1].y, bv[i][1].z, bv[i][1].w};
     float o[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o[t] = (v[i][t] - mean) * inv * gg[t] + bb[t];
+    for (int t = 0; t < 8; ++t) o[t] = c * 8 + t < Cl ? (v[i][t] - mean) * inv * gg[t] + bb[t] : 0.f;
     store8v(y + row * C + c * 8, plane, split != 0, o);
+  }
+}
+
+// Rows wider than the register kernels hold (C > 2048): one 256-thread block per row, the row read
+// twice from global / L2 (sum, then squared deviations) and once more for the output; block
+// reductions through LDS.
+__global__ __launch_bounds__(256) void layernorm_wide_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                             const float* __restrict__ g, const float* __restrict__ b,
+                                                             float eps, long long rows, int C, int split, int Cl) {
+  __shared__ float red[8];
+  const long long row = blockIdx.x;
+  const long long plane = rows * C;
+  const uint16_t* xr = x + row * C;
+  const int nch = C / 8, tid = threadIdx.x;
+  auto block_sum = [&](float v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();  // red[] free (previous reduction read)
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  float s = 0.f;
+  for (int c = tid; c < nch; c += 256) {
+    float v[8];
+    load8v(xr + c * 8, plane, split != 0, v);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) s += c * 8 + t < Cl ? v[t] : 0.f;
+  }
+  const float mean = block_sum(s) / Cl;
+  float q2 = 0.f;
+  for (int c = tid; c < nch; c += 256) {
+    float v[8];
+    load8v(xr + c * 8, plane, split != 0, v);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float d = c * 8 + t < Cl ? v[t] - mean : 0.f;
+      q2 += d * d;
+    }
+  }
+  const float inv = rsqrtf(block_sum(q2) / Cl + eps);
+  for (int c = tid; c < nch; c += 256) {
+    float v[8];
+    load8v(xr + c * 8, plane, split != 0, v);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = c * 8 + t < Cl ? (v[t] - mean) * inv * g[c * 8 + t] + b[c * 8 + t] : 0.f;
+    store8v(y + row * C + c * 8, plane, split != 0, v);
   }
 }
 
@@ -535,18 +585,24 @@ inline int grid_for(long long work, int cap = 4096) {
 }  // namespace
 
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split) {
-  if (C % 8) return hipErrorInvalidValue;
+                          long long rows, int C, hipStream_t s, int split, int Cl) {
+  if (C % 8 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+  if (Cl == 0) Cl = C;
   const int blocks = static_cast<int>((rows + 3) / 4);
   if (C > 512 && C <= 32 * 8 * 3) {  // 513..768 (ViT-B: 768): 32 lanes x 3 chunks, 2 rows per wave
     hipLaunchKernelGGL((layernorm_kernel<3, 32>), dim3(static_cast<int>((rows + 7) / 8)), dim3(256), 0, s, x, y, gamma,
-                       beta, eps, rows, C, split);
+                       beta, eps, rows, C, split, Cl);
     return hipGetLastError();
   }
-  if (C <= 64 * 8) hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
-  else if (C <= 128 * 8) hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
-  else if (C <= 256 * 8) hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split);
-  else return hipErrorInvalidValue;
+  if (C <= 64 * 8)
+    hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+  else if (C <= 128 * 8)
+    hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+  else if (C <= 256 * 8)
+    hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+  else
+    hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
+                       rows, C, split, Cl);
   return hipGetLastError();
 }
 

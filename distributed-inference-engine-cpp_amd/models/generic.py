@@ -26,6 +26,8 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
 * `token_mixer` data-dependent token mixing: MatMul of two activations outside the attention
               pattern (softmax(h W) [S, S] x h [S, D], and x g [S, 20]: inner size 24 and an
               output width that are not multiples of 8).
+* `ln_wide`    LayerNormalization over 20 features (stored with 24: pad columns out of the
+              statistics) and over 2560 features (wider than the register-resident kernels hold).
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -46,6 +48,7 @@ SPECS = {
     "ops_zoo": dict(in_ch=8, image=16, classes=10),
     "upsample_net": dict(in_ch=8, image=12, classes=10),
     "token_mixer": dict(seq=24, dim=40, classes=10),
+    "ln_wide": dict(seq=6, dim=20, wide=2560, classes=10),
 }
 
 
@@ -325,8 +328,33 @@ def build_token_mixer(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, 
     return g.model_proto(opset=opset), {}
 
 
+def build_ln_wide(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["ln_wide"]
+    rng = _rng(seed)
+    S, D, Wd = s["seq"], s["dim"], s["wide"]
+    g = GraphBuilder(name="ln_wide")
+    x = g.input("tokens", ["N", S * D])
+    h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
+
+    def ln(inp, name, c):
+        gw = g.init(name + ".weight", (1.0 + 0.1 * rng.standard_normal(c)).astype(np.float32))
+        gb = g.init(name + ".bias", (0.1 * rng.standard_normal(c)).astype(np.float32))
+        return g.node("LayerNormalization", [inp, gw, gb], name=name, axis=-1, epsilon=1e-5)
+
+    h = ln(h, "ln_in", D)  # 20 logical columns, 24 stored
+    h = g.node("Add", [g.node("MatMul", [h, g.init("up.weight", _lin(rng, D, (D, Wd)))], name="up/MatMul"),
+                       g.init("up.bias", (0.1 * rng.standard_normal(Wd)).astype(np.float32))], name="up/Add")
+    h = g.node("Tanh", [ln(h, "ln_wide", Wd)], name="act")  # 2560 columns
+    pooled = g.node("ReduceMean", [h], name="pool", axes=[1], keepdims=0)
+    w = g.init("head.weight", _lin(rng, Wd, (s["classes"], Wd)))
+    y = g.node("Gemm", [pooled, w, g.init("head.bias", np.zeros(s["classes"], np.float32))], name="head", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
-            "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer}
+            "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer,
+            "ln_wide": build_ln_wide}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:
@@ -337,7 +365,7 @@ def input_shape(name: str):
     s = SPECS[name]
     if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
-    if name == "bert" or name == "token_mixer":
+    if name in ("bert", "token_mixer", "ln_wide"):
         return (s["seq"] * s["dim"],)
     return (s["in_ch"], s["image"], s["image"])
 

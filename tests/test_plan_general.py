@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide"]
 
 
 @pytest.fixture(scope="module")
@@ -52,13 +52,15 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
         assert "up/zero_insert" in names and "up" in names
     if name == "token_mixer":
         assert kinds.count("bmm") == 2 and kinds[0] == "rows_prep"
+    if name == "ln_wide":
+        assert kinds.count("layernorm") == 2
 
 
 def test_generic_models_run_on_the_cpu_oracle(native, gen_models):
     from die_amd.models import generic as G
 
     for name, shape in (("mlp", (2, 10)), ("bert", (2, 3)), ("se_cnn", (2, 10)), ("ops_zoo", (2, 10)),
-                        ("upsample_net", (2, 10)), ("token_mixer", (2, 10))):
+                        ("upsample_net", (2, 10)), ("token_mixer", (2, 10)), ("ln_wide", (2, 10))):
         y = native.cpu_run(gen_models[name], G.synthetic_input(name, 2))
         assert y.shape == shape and np.isfinite(y).all()
         if name in ("mlp", "se_cnn"):
