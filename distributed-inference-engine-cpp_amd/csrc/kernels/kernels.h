@@ -274,6 +274,8 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // ---- transformer (transformer.hip) ----
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0: the stored pitch), fp32
 // statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
+// true when the streaming attention kernel is built in (any sequence length; else S <= 256)
+bool attention_any_length();
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
                           long long rows, int C, hipStream_t s, int split = 0, int Cl = 0);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)

@@ -630,11 +630,14 @@ hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long 
   return hipGetLastError();
 }
 
+bool attention_any_length() { return kAttnStream; }
+
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
-  if (D != AT_D || S <= 0 || S > 256 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
+  if (D != AT_D || S <= 0 || (!kAttnStream && S > 256) || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4)
+    return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
-  if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S <= 256)
+  if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S)
     dim3 grid((S + 127) / 128, H, B);
     if (split) hipLaunchKernelGGL(attention_stream_kernel<true>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
     else hipLaunchKernelGGL(attention_stream_kernel<false>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);

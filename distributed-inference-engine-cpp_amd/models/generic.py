@@ -28,6 +28,7 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
               output width that are not multiples of 8).
 * `ln_wide`    LayerNormalization over 20 features (stored with 24: pad columns out of the
               statistics) and over 2560 features (wider than the register-resident kernels hold).
+* `bert_long`  the `bert` encoder at 320 tokens: attention past 256 keys (streaming kernel).
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -49,6 +50,7 @@ SPECS = {
     "upsample_net": dict(in_ch=8, image=12, classes=10),
     "token_mixer": dict(seq=24, dim=40, classes=10),
     "ln_wide": dict(seq=6, dim=20, wide=2560, classes=10),
+    "bert_long": dict(seq=320, dim=128, heads=2, ffn=256, layers=1, classes=3),
 }
 
 
@@ -90,8 +92,8 @@ def build_mlp(seed: int = 0, opset: int = 13) -> Tuple[bytes, Dict[str, np.ndarr
     return g.model_proto(opset=opset), {}
 
 
-def build_bert(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.ndarray]]:
-    s = SPECS["bert"]
+def build_bert(seed: int = 0, opset: int = 17, spec: str = "bert") -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS[spec]
     rng = _rng(seed)
     S, D, H, F = s["seq"], s["dim"], s["heads"], s["ffn"]
     hd = D // H
@@ -354,7 +356,8 @@ def build_ln_wide(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.n
 
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
             "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer,
-            "ln_wide": build_ln_wide}
+            "ln_wide": build_ln_wide,
+            "bert_long": lambda seed=0: build_bert(seed, spec="bert_long")}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:
@@ -365,7 +368,7 @@ def input_shape(name: str):
     s = SPECS[name]
     if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
-    if name in ("bert", "token_mixer", "ln_wide"):
+    if name in ("bert", "bert_long", "token_mixer", "ln_wide"):
         return (s["seq"] * s["dim"],)
     return (s["in_ch"], s["image"], s["image"])
 

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long"]
 
 
 @pytest.fixture(scope="module")
@@ -54,6 +54,8 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
         assert kinds.count("bmm") == 2 and kinds[0] == "rows_prep"
     if name == "ln_wide":
         assert kinds.count("layernorm") == 2
+    if name == "bert_long":
+        assert kinds.count("attention") == 1
 
 
 def test_generic_models_run_on_the_cpu_oracle(native, gen_models):
