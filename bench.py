@@ -278,7 +278,12 @@ def main():
             "stages_window_us": _stage_window(h0.get("stages_us", {}), h1.get("stages_us", {})),
             # host CPU spent per request by this process (client + gateway + worker threads together)
             "cpu_us_per_request": {"user": round((ru1.ru_utime - ru0.ru_utime) * 1e6 / max(1, res["ok"]), 1),
-                                   "sys": round((ru1.ru_stime - ru0.ru_stime) * 1e6 / max(1, res["ok"]), 1)},
+                                   "sys": round((ru1.ru_stime - ru0.ru_stime) * 1e6 / max(1, res["ok"]), 1),
+                                   # where sys time can come from: page faults and context switches
+                                   "minflt": round((ru1.ru_minflt - ru0.ru_minflt) / max(1, res["ok"]), 2),
+                                   "majflt": round((ru1.ru_majflt - ru0.ru_majflt) / max(1, res["ok"]), 3),
+                                   "vcsw": round((ru1.ru_nvcsw - ru0.ru_nvcsw) / max(1, res["ok"]), 2),
+                                   "ivcsw": round((ru1.ru_nivcsw - ru0.ru_nivcsw) / max(1, res["ok"]), 2)},
         }
         if verify:
             extra["verify"] = {"every": args.verify_every, "inputs": 8, "oracle": "cpu_executor_fp32",
@@ -318,7 +323,10 @@ def main():
             extra["direct_worker"] = {"rps_this_rank": rd["ok"] / el, "p50_ms": rd["latency_ms"]["p50"],
                                       "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"],
                                       "cpu_us_per_request": {"user": round((rd1.ru_utime - rd0.ru_utime) * 1e6 / n_ok, 1),
-                                                             "sys": round((rd1.ru_stime - rd0.ru_stime) * 1e6 / n_ok, 1)}}
+                                                             "sys": round((rd1.ru_stime - rd0.ru_stime) * 1e6 / n_ok, 1),
+                                                             "minflt": round((rd1.ru_minflt - rd0.ru_minflt) / n_ok, 2),
+                                                             "vcsw": round((rd1.ru_nvcsw - rd0.ru_nvcsw) / n_ok, 2),
+                                                             "ivcsw": round((rd1.ru_nivcsw - rd0.ru_nivcsw) / n_ok, 2)}}
         if gw and not args.no_gateway_bytes:
             # the reference's gateway hop: every body re-sent to the worker over loopback HTTP
             # (/root/reference/src/gateway.cpp:99-103) instead of a shared-memory descriptor

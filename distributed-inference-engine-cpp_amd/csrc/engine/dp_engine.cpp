@@ -195,7 +195,10 @@ class DpEngine : public Engine {
   int max_batch() const override { return local_max_; }
   SamplePool& sample_pool() override { return solo_ ? local_->sample_pool() : *pool_; }
   size_t text_capacity() const override {
-    return solo_ ? local_->text_capacity() : std::min(local_->text_capacity(), item_bytes_);
+    // a staging item holds the text 4-bit packed when the local engine unpacks on the device (two
+    // characters per byte), raw otherwise; the worker checks each body against that (worker.cpp)
+    return solo_ ? local_->text_capacity()
+                 : std::min(local_->text_capacity(), local_->text_packing() ? 2 * item_bytes_ : item_bytes_);
   }
   bool text_packing() const override { return local_->text_packing(); }
   void register_host_memory(void*, size_t) override {}

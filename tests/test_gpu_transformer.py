@@ -92,9 +92,26 @@ def test_attention_rejects_bad_shapes(K):
 
     from die_amd import native
 
-    x = torch.zeros(1, 300, 128, device="cuda", dtype=torch.bfloat16)
+    x = torch.zeros(1, 64, 96, device="cuda", dtype=torch.bfloat16)  # 2 heads of 48: head dim must be 64
     with pytest.raises(native.NativeError):
         K.attention(x, x, x, 2)
+
+
+@pytest.mark.parametrize("S", [300, 520])
+def test_attention_long_sequences(K, S):
+    """The streaming kernel takes any sequence length (K/V in 32-key tiles, 128 queries per block)."""
+    import torch
+
+    g = torch.Generator(device="cuda").manual_seed(S)
+    B, H, D = 2, 2, 64
+    C = H * D
+    qkv = torch.randn(B, S, 3 * C, device="cuda", generator=g).bfloat16()
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    scale = 1.0 / math.sqrt(D)
+    out = K.attention(q, k, v, H, scale)
+    ref = _attn_ref(q, k, v, H, scale)
+    assert torch.isfinite(out.float()).all()
+    assert rel_l2(out, ref) < 2e-2, rel_l2(out, ref)
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
