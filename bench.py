@@ -85,6 +85,8 @@ def main():
                     help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
     ap.add_argument("--tune-warm-input", action="store_true",
                     help="autotune: run each conv's input producer right before every timing (default: L2 scrub only)")
+    ap.add_argument("--splitk-fused-margin", type=float, default=0.0,
+                    help="autotune: prefer in-kernel split-K when within this fraction of the best (EngineOptions)")
     ap.add_argument("--pace-lead-scale", type=float, default=1.0,
                     help="pacing lead: 1 = measured input path + adaptive margin; other values = input path x this")
     ap.add_argument("--branch-streams", action="store_true",
@@ -192,6 +194,7 @@ def main():
                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                    "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
+                   "splitk_fused_margin": args.splitk_fused_margin,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool}

@@ -54,6 +54,7 @@ die::EngineOptions engine_options_from_flags(const die::Flags& f, const std::str
   eo.bucket_div = static_cast<int>(f.i("bucket-div", 8));
   eo.coarse_buckets = f.b("coarse-buckets");
   eo.pace_lead_scale = f.f("pace-lead-scale", 1.0);
+  eo.splitk_fused_margin = static_cast<float>(f.f("splitk-fused-margin", 0.0));
   eo.completion_poll_us = static_cast<int>(f.i("completion-poll-us", 0));
   eo.bn_on_load = f.b("bn-on-load");
   eo.fuse_pairs = !f.b("no-fuse-pairs");
@@ -124,7 +125,7 @@ int main(int argc, char** argv) {
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (3)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --no-pace  --no-pack-text  --branch-streams  --copy-streams N (0 = auto)  --bucket-div N (8)  --coarse-buckets\n"
-              << "  --pace-lead-scale X (1)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --tune-warm  --tune-cache PATH|auto|''\n"
+              << "  --pace-lead-scale X (1)  --splitk-fused-margin X (0)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --tune-warm  --tune-cache PATH|auto|''\n"
               << "  --dp-backend rccl|host (rccl)  --dp-force-merge  --fail-batch-every N (fault injection, 0 = off)\n"
               << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"

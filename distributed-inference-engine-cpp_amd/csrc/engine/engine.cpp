@@ -292,6 +292,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["fuse_stem_pool"] = o.fuse_stem_pool;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
+  j["splitk_fused_margin"] = o.splitk_fused_margin;
   j["fail_batch_every"] = o.fail_batch_every;
   return j;
 }

@@ -230,6 +230,9 @@ struct EngineOptions {
   bool fuse_stem_pool = true;     // stem conv + max pool (+ its BN/ReLU) -> one launch (kernels/stem.hip)
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
+  // autotune: take the fastest in-kernel (fused) split-K candidate when it is within this fraction
+  // of the overall best (a separate reduction kernel is one more graph node: launch + drain)
+  float splitk_fused_margin = 0.f;
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.

@@ -905,7 +905,8 @@ class HipEngine : public Engine {
           }
         // identical problems (repeated blocks) share one measurement
         char key[256];
-        std::snprintf(key, sizeof(key), "o%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "", base.M, base.N, base.K, base.Cin,
+        std::snprintf(key, sizeof(key), "o%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "",
+                      opt_.splitk_fused_margin > 0.f ? "fm:" : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
         auto memo = tuned_shapes.find(key);
@@ -915,8 +916,8 @@ class HipEngine : public Engine {
           continue;
         }
         const int nk = base.Kpad / 64;
-        float best = 1e30f;
-        Tune bt{kern::choose_tile(base.M, base.N, base.K), 1};
+        float best = 1e30f, best_fused = 1e30f;
+        Tune bt{kern::choose_tile(base.M, base.N, base.K), 1}, bt_fused = bt;
         for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
           for (int sp = 1; sp <= 16; sp *= 2) {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
@@ -956,8 +957,16 @@ class HipEngine : public Engine {
                 best = ms;
                 bt = Tune{tile, sp, fused != 0, order};
               }
+              if (fused && ms < best_fused) {
+                best_fused = ms;
+                bt_fused = Tune{tile, sp, true, order};
+              }
             }
           }
+        }
+        if (bt.splits > 1 && !bt.fused && best_fused <= best * (1.f + opt_.splitk_fused_margin)) {
+          bt = bt_fused;  // EngineOptions::splitk_fused_margin: one graph node instead of two
+          best = best_fused;
         }
         tune_[bi][oi] = bt;
         tuned_shapes[key] = {bt, best / 3 * 1000.0};

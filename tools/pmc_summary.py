@@ -38,7 +38,7 @@ def load(pass_dir):
         d["c"][r["Counter_Name"]] += float(r["Counter_Value"])
     seq = [v for _, v in sorted(disp.items()) if "die::kern" in v["name"]]
     # the forward starts at its input pass: input_prep, or the stem that fused it
-    start = max(i for i, v in enumerate(seq) if "input_prep" in v["name"] or "stem7x7_nchw" in v["name"])
+    start = max(i for i, v in enumerate(seq) if "input_prep" in v["name"] or "stem7x7_nchw" in v["name"] or "stem_pool_nchw" in v["name"])
     return seq[start:]
 
 
