@@ -256,6 +256,9 @@ def main():
         extra = {
             "p50_ms": res["latency_ms"]["p50"], "p99_ms": res["latency_ms"]["p99"],
             "mean_ms": res["latency_ms"]["mean"], "failed": failed,
+            # tail attribution: p99 per tenth of the timed pass (by request start) + the slowest requests
+            "tail": {"p99_by_tenth_ms": [round(v, 2) for v in res.get("p99_by_tenth_ms", [])],
+                     "slowest_ms": res.get("slowest_ms", [])},
             "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
             "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
@@ -315,6 +318,7 @@ def main():
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()
+            hd0 = wk.health()
             rd0 = resource.getrusage(resource.RUSAGE_SELF)
             td = time.perf_counter()
             rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank,
@@ -322,6 +326,7 @@ def main():
             barrier()
             el = time.perf_counter() - td
             rd1 = resource.getrusage(resource.RUSAGE_SELF)
+            hd1 = wk.health()
             n_ok = max(1, rd["ok"])
             extra["direct_worker"] = {"rps_this_rank": rd["ok"] / el, "p50_ms": rd["latency_ms"]["p50"],
                                       "p99_ms": rd["latency_ms"]["p99"], "failed": rd["failed"],
@@ -329,7 +334,13 @@ def main():
                                                              "sys": round((rd1.ru_stime - rd0.ru_stime) * 1e6 / n_ok, 1),
                                                              "minflt": round((rd1.ru_minflt - rd0.ru_minflt) / n_ok, 2),
                                                              "vcsw": round((rd1.ru_nvcsw - rd0.ru_nvcsw) / n_ok, 2),
-                                                             "ivcsw": round((rd1.ru_nivcsw - rd0.ru_nivcsw) / n_ok, 2)}}
+                                                             "ivcsw": round((rd1.ru_nivcsw - rd0.ru_nivcsw) / n_ok, 2)},
+                                      # tail attribution: p99 per tenth of the pass by
+                                      # request start, the slowest requests [start ms, latency ms], and the
+                                      # worker's stage histograms over this pass only
+                                      "p99_by_tenth_ms": [round(v, 2) for v in rd.get("p99_by_tenth_ms", [])],
+                                      "slowest_ms": rd.get("slowest_ms", []),
+                                      "stages_window_us": _stage_window(hd0.get("stages_us", {}), hd1.get("stages_us", {}))}
         if gw and not args.no_gateway_bytes:
             # the reference's gateway hop: every body re-sent to the worker over loopback HTTP
             # (/root/reference/src/gateway.cpp:99-103) instead of a shared-memory descriptor

@@ -2,6 +2,7 @@
 #include "loadgen.h"
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -160,6 +161,7 @@ Json run_loadgen(const LoadgenOptions& o) {
   const int C = std::max(1, o.connections);
   std::atomic<long> next_warm{0}, next{0};
   std::vector<std::vector<double>> lat(C);
+  std::vector<std::vector<std::pair<double, double>>> when(C);  // (start offset in the timed window, latency) ms
   std::vector<long> ok(C, 0), fail(C, 0);
   std::vector<std::map<std::string, long>> errs(C);
   Gate gate;
@@ -226,6 +228,7 @@ Json run_loadgen(const LoadgenOptions& o) {
         if (r && r->status == 200) {
           ++ok[c];
           lat[c].push_back(ms);
+          when[c].emplace_back(std::chrono::duration<double, std::milli>(s - t0).count(), ms);
           if (is_verify(id)) {
             const size_t k = verify_k(id);
             char idbuf[32];
@@ -296,6 +299,31 @@ Json run_loadgen(const LoadgenOptions& o) {
   l["min"] = all.empty() ? 0.0 : all.front();
   l["max"] = all.empty() ? 0.0 : all.back();
   j["latency_ms"] = l;
+  // tail attribution: p99 per tenth of the timed window (by request start) and the slowest requests
+  // with their start offsets -- a tail clustered at the start is warm-up, a periodic one a stall
+  {
+    std::vector<std::pair<double, double>> w;
+    for (int c = 0; c < C; ++c) w.insert(w.end(), when[c].begin(), when[c].end());
+    const double span = wall * 1000.0;
+    Json dec = Json::array();
+    for (int k = 0; k < 10 && span > 0; ++k) {
+      std::vector<double> v;
+      for (auto& x : w)
+        if (x.first >= span * k / 10 && (x.first < span * (k + 1) / 10 || k == 9)) v.push_back(x.second);
+      std::sort(v.begin(), v.end());
+      dec.push_back(v.empty() ? 0.0 : v[std::min(v.size() - 1, static_cast<size_t>(v.size() * 0.99))]);
+    }
+    j["p99_by_tenth_ms"] = dec;
+    std::sort(w.begin(), w.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+    Json slow = Json::array();
+    for (size_t k = 0; k < std::min<size_t>(10, w.size()); ++k) {
+      Json e2 = Json::array();
+      e2.push_back(std::round(w[k].first * 10) / 10);
+      e2.push_back(std::round(w[k].second * 100) / 100);
+      slow.push_back(e2);
+    }
+    j["slowest_ms"] = slow;  // [start offset, latency]
+  }
   Json e = Json::object();
   for (auto& kv : merged) e[kv.first] = static_cast<long long>(kv.second);
   j["errors"] = e;
