@@ -32,6 +32,7 @@ import signal
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -85,6 +86,8 @@ def main():
                     help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
     ap.add_argument("--tune-warm-input", action="store_true",
                     help="autotune: run each conv's input producer right before every timing (default: L2 scrub only)")
+    ap.add_argument("--trace-device", action="store_true",
+                    help="sample the engine's per-batch device time every 50 ms during the timed pass (tail attribution)")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0,
                     help="autotune: prefer in-kernel split-K when within this fraction of the best (EngineOptions)")
     ap.add_argument("--pace-lead-scale", type=float, default=1.0,
@@ -240,9 +243,22 @@ def main():
         g0 = gw.stats() if gw else {}
         barrier()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
+        trace = []
+        stop_trace = threading.Event()
+        if args.trace_device:
+            # opt-in: sample the engine's batch / busy counters every 50 ms during the timed pass, so a
+            # tail late in the pass can be told apart from device slow-down (clocks) or host stalls
+            def _sampler():
+                while not stop_trace.wait(0.05):
+                    e = wk.health()["engine"]
+                    trace.append((time.perf_counter(), e.get("batches", 0), e.get("images", 0),
+                                  e.get("avg_device_ms", 0.0)))
+            th = threading.Thread(target=_sampler, daemon=True)
+            th.start()
         t0 = time.perf_counter()
         res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank,
                              seed=2000 + rank, **dict(lg, **(verify or {})))
+        stop_trace.set()
         barrier()
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
@@ -258,7 +274,7 @@ def main():
             "mean_ms": res["latency_ms"]["mean"], "failed": failed,
             # tail attribution: p99 per tenth of the timed pass (by request start) + the slowest requests
             "tail": {"p99_by_tenth_ms": [round(v, 2) for v in res.get("p99_by_tenth_ms", [])],
-                     "slowest_ms": res.get("slowest_ms", [])},
+                     "slowest_ms": res.get("slowest_ms", []), "device_trace": _device_trace(trace, t0)},
             "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
             "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
@@ -501,6 +517,18 @@ def main():
         out.update({k: v for k, v in extra.items() if v is not None})
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     hg.close()
+
+
+def _device_trace(trace, t0):
+    """[t ms, batches, images / batch, device ms / batch] per 50 ms sample interval (--trace-device)."""
+    out = []
+    for a, b in zip(trace, trace[1:]):
+        nb = b[1] - a[1]
+        if nb <= 0:
+            continue
+        dev = (b[3] * b[1] - a[3] * a[1]) / nb  # lifetime averages -> this interval's
+        out.append([round((b[0] - t0) * 1e3, 1), nb, round((b[2] - a[2]) / nb, 1), round(dev, 3)])
+    return out
 
 
 def _win(e0, e1, key):
