@@ -1021,56 +1021,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
 
 }  // namespace
 
-// The 128 x 256 tile (configs CFG_WIDE_BASE + v): LDS-DMA loops without pre-activation on load.
-// v 0 / 1: 2- / 3-stage rings of 32-wide K-steps; v 2: one 64-wide stage.  The epilogue stages the
-// f32 tile (128 KiB) through the same LDS.
-template <int BM, int BN>
-hipError_t launch_wide_cfg(const ConvArgs& a, hipStream_t s, int variant) {
-  if (a.N % BN || a.in_scale || !a.zeros || a.Kpad % BK) return hipErrorInvalidValue;
-  const bool dense1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
-                        a.W == a.Wo;
-  const bool mode0 = dense1x1 && a.K % BK == 0 && a.Cin == a.K;
-  const bool mode2 = !dense1x1 && a.Cin % BK == 0;
-  const bool mode3 = !dense1x1 && !mode2 && a.KH == a.stride && a.KW == a.stride && a.stride > 1 && a.dil == 1 &&
-                     a.pad_h == 0 && a.pad_w == 0 && (a.KW * a.Cin) % BK == 0 && a.K == a.KH * a.KW * a.Cin &&
-                     a.Kpad == a.K && a.Ho == (a.H - a.KH) / a.stride + 1 && a.Wo == (a.W - a.KW) / a.stride + 1;
-  if (!(mode0 || mode2 || mode3)) return hipErrorInvalidValue;
-  const int mode = mode0 ? 0 : mode2 ? 2 : 3;
-  const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-  const int nk = a.Kpad / BK;
-  const int splits = std::max(1, std::min(a.splits, nk));
-  const int kt_per = (nk + splits - 1) / splits;
-  const int eff = (nk + kt_per - 1) / kt_per;
-  ConvArgs b = a;
-  b.splits = eff;
-  if (a.split) {
-    b.xplane = static_cast<long long>(a.B) * a.H * a.W * a.Cin;
-    b.oplane = static_cast<long long>(a.M) * a.N;
-    if (a.wplane <= 0) return hipErrorInvalidValue;
-  } else {
-    b.xplane = b.oplane = 0;
-  }
-  const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
-  if (!fused) b.counters = nullptr;
-  const dim3 grid(tiles, eff);
-  bool ok;
-  switch (variant) {
-    case 0: ok = launch_glds<BM, BN, 2, 32>(mode, grid, s, b, kt_per); break;
-    case 1: ok = launch_glds<BM, BN, 3, 32>(mode, grid, s, b, kt_per); break;
-    case 2: ok = launch_glds<BM, BN, 1, 64>(mode, grid, s, b, kt_per); break;
-    default: return hipErrorInvalidValue;
-  }
-  if (!ok) return hipErrorInvalidValue;
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || eff == 1 || fused) return e;
-  const long long groups = static_cast<long long>(b.M) * (b.N / 8);
-  const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
-  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
-  return hipGetLastError();
-}
-
 // One launcher per tile shape, defined in conv_tile_<BM>x<BN>.hip.
-hipError_t launch_tile_128x256(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_128x128(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_128x64(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_64x128(const ConvArgs& a, hipStream_t s, int variant);

@@ -74,14 +74,7 @@ struct ConvArgs {
 // Variant 5 = the LDS-DMA loop with ONE stage (no ring): for K <= 64 layers, where the smaller LDS
 // footprint fits more blocks per CU.  Variant 6 = spatially tiled 3x3/s1/p1 kernel (8x8 pixels x 64
 // channels per block, input patch staged once per 64-channel slice; 64x64 tile config only).
-// Configs 28-30 (after the 4 x 7 grid, so the numbering above stays stable): a 128-pixel x 256-
-// channel tile (each wave 64 x 128: half the LDS fragment reads per MFMA of the 128x128 tile), LDS-DMA
-// only, N % 256 == 0: 28 = 2-stage ring of 32-wide K-steps, 29 = 3-stage ring of 32-wide K-steps,
-// 30 = one 64-wide stage.  For the large GEMMs (ViT QKV / MLP, ResNet at large batch).
-enum TileCfg {
-  TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4,
-  CFG_WIDE_BASE = 28, NUM_WIDE_CFGS = 3, NUM_CFGS = 31
-};
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 28 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

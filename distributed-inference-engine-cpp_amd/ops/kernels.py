@@ -71,10 +71,8 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split:
     return out, K, Kpad
 
 
-# launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg), then the 128x256 wide-tile
-# configs 28..30 (LDS-DMA only, N % 256 == 0)
-NUM_CFGS = 31
-WIDE_CFGS = (28, 29, 30)
+# launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg)
+NUM_CFGS = 28
 
 
 class ConvProblem:
