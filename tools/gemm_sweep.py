@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Time given launch configs of the implicit-GEMM kernel on ViT-B/16-shaped GEMMs (fp32 split mode
 by default), each as a captured hipGraph of back-to-back launches; hipBLASLt bf16 / fp32 on the same
-GEMM view for reference.  For the wide-tile (configs 28-30) vs 128x128 comparison.
+GEMM view for reference (profiles/r4_gemm_sweep_vit_*.md).
 
-  python tools/gemm_sweep.py --batch 32 --cfgs 0,4,20,21,22,28,29,30 [--md out.md]
+  python tools/gemm_sweep.py --batch 32 --cfgs 0,4,20,21,22 [--md out.md]
 """
 import argparse
 import os
@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--tokens", type=int, default=197)
-    ap.add_argument("--cfgs", default="0,4,20,21,22,28,29,30")
+    ap.add_argument("--cfgs", default="0,4,20,21,22")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--trials", type=int, default=5)
     ap.add_argument("--bf16", action="store_true", help="bf16 operands instead of split fp32")
