@@ -30,11 +30,6 @@ namespace kern {
 constexpr int BK = 64;  // K-step (conv_igemm_impl.h)
 
 void tile_dims(int cfg, int& bm, int& bn) {
-  if (cfg >= CFG_SMALL_BASE) {
-    bm = 32;
-    bn = 64;
-    return;
-  }
   switch (cfg % NUM_TILES) {
     case TILE_128x128: bm = 128; bn = 128; break;
     case TILE_128x64: bm = 128; bn = 64; break;
@@ -79,7 +74,6 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (a.out2 && (!a.scale2 || !a.shift2)) return hipErrorInvalidValue;
   if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
   if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
-  if (cfg >= CFG_SMALL_BASE) return igemm::launch_tile_32x64(a, s, cfg - CFG_SMALL_BASE);
   const int variant = cfg / NUM_TILES;
   switch (cfg % NUM_TILES) {
     case TILE_128x128: return igemm::launch_tile_128x128(a, s, variant);

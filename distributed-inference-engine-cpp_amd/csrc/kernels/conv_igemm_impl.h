@@ -1022,7 +1022,6 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
 }  // namespace
 
 // One launcher per tile shape, defined in conv_tile_<BM>x<BN>.hip.
-hipError_t launch_tile_32x64(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_128x128(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_128x64(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_64x128(const ConvArgs& a, hipStream_t s, int variant);

@@ -74,13 +74,7 @@ struct ConvArgs {
 // Variant 5 = the LDS-DMA loop with ONE stage (no ring): for K <= 64 layers, where the smaller LDS
 // footprint fits more blocks per CU.  Variant 6 = spatially tiled 3x3/s1/p1 kernel (8x8 pixels x 64
 // channels per block, input patch staged once per 64-channel slice; 64x64 tile config only).
-// Configs 28-33 (after the 4 x 7 grid, so the numbering above stays stable): a 32-pixel x 64-channel
-// tile, variants 0-5 as above (28 + variant): twice the blocks of the 64x64 tile for the
-// latency-bound small-M layers (ResNet stages 3-4 at serving batch sizes).
-enum TileCfg {
-  TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4,
-  CFG_SMALL_BASE = 28, NUM_CFGS = 34
-};
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 28 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

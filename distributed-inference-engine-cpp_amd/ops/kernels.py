@@ -71,9 +71,8 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split:
     return out, K, Kpad
 
 
-# launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg), then the 32x64 tile's
-# variants 0-5 as configs 28-33
-NUM_CFGS = 34
+# launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg)
+NUM_CFGS = 28
 
 
 class ConvProblem:
