@@ -146,9 +146,9 @@ int die_kern_nhwc_to_nchw(uint64_t x, uint64_t y, int B, int H, int W, int C, ui
 }
 
 int die_kern_layernorm(uint64_t x, uint64_t y, uint64_t gamma, uint64_t beta, float eps, long long rows, int C,
-                       uint64_t stream, int split) {
+                       uint64_t stream, int split, int variant) {
   return static_cast<int>(kern::layernorm_rows(P<const uint16_t>(x), P<uint16_t>(y), P<const float>(gamma),
-                                               P<const float>(beta), eps, rows, C, S(stream), split));
+                                               P<const float>(beta), eps, rows, C, S(stream), split, 0, variant));
 }
 
 int die_kern_tokens(uint64_t patches, uint64_t cls, uint64_t pos, uint64_t out, int B, int S0, int C, uint64_t stream,

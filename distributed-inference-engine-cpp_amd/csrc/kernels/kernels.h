@@ -276,8 +276,10 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
 // true when the streaming attention kernel is built in (any sequence length; else S <= 256)
 bool attention_any_length();
+// variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
+// per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split = 0, int Cl = 0);
+                          long long rows, int C, hipStream_t s, int split = 0, int Cl = 0, int variant = 0);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
                            int C, hipStream_t s, int split = 0);

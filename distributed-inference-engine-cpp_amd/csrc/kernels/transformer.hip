@@ -585,10 +585,21 @@ inline int grid_for(long long work, int cap = 4096) {
 }  // namespace
 
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split, int Cl) {
-  if (C % 8 || Cl < 0 || Cl > C) return hipErrorInvalidValue;
+                          long long rows, int C, hipStream_t s, int split, int Cl, int variant) {
+  if (C % 8 || Cl < 0 || Cl > C || variant < 0 || variant > 2) return hipErrorInvalidValue;
   if (Cl == 0) Cl = C;
   const int blocks = static_cast<int>((rows + 3) / 4);
+  if (variant == 1) {
+    if (C > 16 * 8 * 6) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((layernorm_kernel<6, 16>), dim3(static_cast<int>((rows + 15) / 16)), dim3(256), 0, s, x, y, gamma,
+                       beta, eps, rows, C, split, Cl);
+    return hipGetLastError();
+  }
+  if (variant == 2) {
+    hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
+                       rows, C, split, Cl);
+    return hipGetLastError();
+  }
   if (C > 512 && C <= 32 * 8 * 3) {  // 513..768 (ViT-B: 768): 32 lanes x 3 chunks, 2 rows per wave
     hipLaunchKernelGGL((layernorm_kernel<3, 32>), dim3(static_cast<int>((rows + 7) / 8)), dim3(256), 0, s, x, y, gamma,
                        beta, eps, rows, C, split, Cl);

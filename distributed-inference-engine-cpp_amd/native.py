@@ -656,7 +656,7 @@ def _sig_kernels():
     L.die_kern_softmax.restype = i
     L.die_kern_softmax.argtypes = [u64, u64, u64, C.c_longlong, i, u64, i]
     L.die_kern_layernorm.restype = i
-    L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64, i]
+    L.die_kern_layernorm.argtypes = [u64] * 4 + [C.c_float, C.c_longlong, i, u64, i, i]
     L.die_kern_tokens.restype = i
     L.die_kern_tokens.argtypes = [u64] * 4 + [i] * 3 + [u64, i]
     L.die_kern_gather_rows.restype = i

@@ -289,14 +289,14 @@ def linear(x, w, bias=None, act=0, res=None, tile=-1, splits=1, split=False):
     return None if out is None else out.reshape(*lead, N)
 
 
-def layernorm(x, gamma, beta, eps=1e-5, split=False):
+def layernorm(x, gamma, beta, eps=1e-5, split=False, variant=0):
     import torch
 
     C = x.shape[-1]
     y = torch.empty(((2,) if split else ()) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
     xin, gm, bt = _in(x, split), gamma.float().contiguous(), beta.float().contiguous()
     rc = native.kernels().die_kern_layernorm(_ptr(xin), _ptr(y), _ptr(gm), _ptr(bt), float(eps), x.numel() // C, C, _stream(),
-                                             int(split))
+                                             int(split), int(variant))
     _check(rc, "layernorm")
     return _out(y, split)
 
