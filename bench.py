@@ -86,6 +86,9 @@ def main():
                     help="dispatch the next batch as soon as a pipeline slot frees (no just-in-time pacing)")
     ap.add_argument("--tune-warm-input", action="store_true",
                     help="autotune: run each conv's input producer right before every timing (default: L2 scrub only)")
+    ap.add_argument("--loadgen-io-threads", type=int, default=0,
+                    help="drive the client connections from N epoll threads instead of one thread each "
+                         "(same closed loop; less client CPU in the shared CPU share)")
     ap.add_argument("--trace-device", action="store_true",
                     help="sample the engine's per-batch device time every 50 ms during the timed pass (tail attribution)")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0,
@@ -236,7 +239,7 @@ def main():
         # direct passes (cache_hits_timed below proves it); request numbers are printed scrambled
         # (FNV-1a spreads them over the ring like random ids)
         lg = dict(connections=args.connections, payload="full", input_numel=numel, decimals=4, timeout_ms=60000,
-                  scramble_ids=True)
+                  scramble_ids=True, io_threads=args.loadgen_io_threads)
         native.loadgen(port=target_port, requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank,
                        seed=1000 + rank, **lg)
         h0 = wk.health()
@@ -400,7 +403,7 @@ def main():
         wk = native.Worker(model, node_id="dp-r%d" % rank, port=port, reuse_port=True, max_batch=Btot,
                            engine=eng_opts, parse_threads=args.parse_threads)
         lg = dict(port=port, connections=args.connections, payload="full", input_numel=numel, decimals=4,
-                  timeout_ms=60000)
+                  timeout_ms=60000, io_threads=args.loadgen_io_threads)
         native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, seed=1000 + rank, **lg)
         h0 = wk.health()
         barrier()
@@ -601,7 +604,7 @@ def _dp_child(args, hg, rank, world):
            "--warmup", str(max(1, args.warmup)), "--step-requests", str(args.step_requests),
            "--batch", str(args.batch), "--connections", str(args.connections), "--precision", args.precision,
            "--arch", args.arch, "--pipeline-depth", str(args.pipeline_depth), "--dp-backend", "rccl",
-           "--device", args.device]
+           "--device", args.device, "--loadgen-io-threads", str(args.loadgen_io_threads)]
     if world == 1:
         cmd.append("--dp-force-merge")
     if args.model:

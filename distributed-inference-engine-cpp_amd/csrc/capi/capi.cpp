@@ -589,6 +589,7 @@ static LoadgenOptions loadgen_opts(const Json& j) {
   o.verify_tol = jget<double>(j, "verify_tol", o.verify_tol);
   o.verify_every = jget<long>(j, "verify_every", o.verify_every);
   o.scramble_ids = jget<bool>(j, "scramble_ids", o.scramble_ids);
+  o.io_threads = jget<int>(j, "io_threads", o.io_threads);
   return o;
 }
 

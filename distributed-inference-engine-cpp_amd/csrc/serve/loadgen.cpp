@@ -1,8 +1,17 @@
 #include <pthread.h>
 #include "loadgen.h"
 
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <strings.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
 #include <algorithm>
-#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -187,79 +196,312 @@ Json run_loadgen(const LoadgenOptions& o) {
   uint64_t scale = 1;
   for (int k = 0; k < d; ++k) scale *= 10;
 
-  std::vector<std::thread> threads;
-  for (int c = 0; c < C; ++c) {
-    threads.emplace_back([&, c] {
-      pthread_setname_np(pthread_self(), "die-loadgen");
-      HttpClient client(o.host, o.port, std::chrono::milliseconds(o.timeout_ms), std::chrono::milliseconds(o.timeout_ms), 2);
-      Template tpl;
-      if (full) tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(c));
-      std::string vbody;  // verify mode: this request's copy of its input's template
-      auto body_for = [&](long id) -> std::string& {
-        static thread_local std::string small;
-        if (is_verify(id)) {
-          const Template& t = vt[verify_k(id)];
-          if (sampled) verify_body(t, (id / o.verify_every) / static_cast<long>(vt.size()) + 1, vbody);
-          else vbody = t.body;
-          patch_digits(vbody, t.id_pos, t.id_len, printed(id));
-          return vbody;
+  // Per-connection request bodies: the connection's own copy of the full-payload template (patched
+  // in place per request), or a verify / reference body.  A body stays untouched until its request
+  // has been sent completely (one request in flight per connection).
+  struct Bodies {
+    Template tpl;
+    std::string vbody, small;
+  };
+  auto body_for = [&](Bodies& bd, int c, long id) -> const std::string& {
+    if (is_verify(id)) {
+      const Template& t = vt[verify_k(id)];
+      if (sampled) verify_body(t, (id / o.verify_every) / static_cast<long>(vt.size()) + 1, bd.vbody);
+      else bd.vbody = t.body;
+      patch_digits(bd.vbody, t.id_pos, t.id_len, printed(id));
+      return bd.vbody;
+    }
+    const long key = o.distinct > 0 ? id % o.distinct : id;
+    if (full) {
+      Template& tpl = bd.tpl;
+      patch_digits(tpl.body, tpl.id_pos, tpl.id_len, printed(id));
+      // unique input: encode (key, connection) in the first two values
+      const uint64_t u = static_cast<uint64_t>(key) * 64 + static_cast<uint64_t>(c);
+      patch_digits(tpl.body, tpl.v0_pos + 2, static_cast<size_t>(d), u % scale);
+      patch_digits(tpl.body, tpl.v1_pos + 2, static_cast<size_t>(d), (u / scale) % scale);
+      return tpl.body;
+    }
+    const long a = key % 10;
+    bd.small = "{\"request_id\":\"" + o.id_prefix + std::to_string(printed(id)) + "\",\"input_data\":[" +
+               std::to_string(a) + ".0," + std::to_string(a + 1) + ".0," + std::to_string(a + 2) + ".0]}";
+    return bd.small;
+  };
+  // Account one finished request of connection c (status 0 = transport error `err`).
+  auto finish = [&](int c, long id, std::chrono::steady_clock::time_point s, int status, const std::string& body,
+                    const std::string& err) {
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s).count();
+    if (status == 200) {
+      ++ok[c];
+      lat[c].push_back(ms);
+      when[c].emplace_back(std::chrono::duration<double, std::milli>(s - t0).count(), ms);
+      if (is_verify(id)) {
+        const size_t k = verify_k(id);
+        char idbuf[32];
+        std::snprintf(idbuf, sizeof idbuf, "%0*llu", kIdDigits, static_cast<unsigned long long>(printed(id)));
+        bool id_ok = false;
+        const double e = response_error(body, o.verify_expected + k * o.output_numel, o.output_numel,
+                                        o.id_prefix + idbuf, id_ok);
+        ++verified[c];
+        if (!id_ok) ++bad_id[c];
+        if (e < 0.0 || e > o.verify_tol) ++mismatched[c];
+        max_err[c] = std::max(max_err[c], e < 0.0 ? 1e30 : e);
+      }
+    } else {
+      ++fail[c];
+      errs[c][status ? "HTTP " + std::to_string(status) : err]++;
+    }
+  };
+
+  // One epoll loop over connections `mine`: warm-up ids until next_warm runs out, the gate (twice,
+  // as the threaded clients), timed ids until next runs out, the gate again.
+  auto async_loop = [&](const std::vector<int>& mine) {
+    struct AConn {
+      int c = 0, fd = -1;
+      Bodies bd;
+      std::string head, in;
+      const std::string* body = nullptr;
+      size_t sent = 0, hdr_end = std::string::npos, clen = 0;
+      int status = 0;
+      long id = -1;
+      bool record = false, busy = false;
+      std::chrono::steady_clock::time_point start;
+    };
+    const int ep = epoll_create1(EPOLL_CLOEXEC);
+    if (ep < 0) throw std::runtime_error("loadgen: epoll_create1 failed");
+    std::vector<AConn> cs(mine.size());
+    auto open_conn = [&](AConn& k) -> bool {
+      if (k.fd >= 0) {
+        epoll_ctl(ep, EPOLL_CTL_DEL, k.fd, nullptr);
+        ::close(k.fd);
+      }
+      k.fd = -1;
+      sockaddr_in addr{};
+      addr.sin_family = AF_INET;
+      addr.sin_port = htons(static_cast<uint16_t>(o.port));
+      if (inet_pton(AF_INET, o.host == "localhost" ? "127.0.0.1" : o.host.c_str(), &addr.sin_addr) != 1) return false;
+      const int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      if (fd < 0) return false;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      if (::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof addr) != 0) {
+        ::close(fd);
+        return false;
+      }
+      fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK);
+      epoll_event ev{};
+      ev.events = EPOLLIN;
+      ev.data.u64 = static_cast<uint64_t>(&k - cs.data());
+      epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+      k.fd = fd;
+      return true;
+    };
+    auto want = [&](AConn& k, uint32_t events) {
+      epoll_event ev{};
+      ev.events = events;
+      ev.data.u64 = static_cast<uint64_t>(&k - cs.data());
+      epoll_ctl(ep, EPOLL_CTL_MOD, k.fd, &ev);
+    };
+    // push as much of head + body as the socket takes; false on a transport error
+    auto pump_send = [&](AConn& k) -> bool {
+      while (true) {
+        const size_t hs = k.head.size(), total = hs + k.body->size();
+        if (k.sent >= total) return true;
+        iovec iov[2];
+        int n = 0;
+        if (k.sent < hs) iov[n++] = {const_cast<char*>(k.head.data()) + k.sent, hs - k.sent};
+        const size_t boff = k.sent > hs ? k.sent - hs : 0;
+        iov[n++] = {const_cast<char*>(k.body->data()) + boff, k.body->size() - boff};
+        const ssize_t w = ::writev(k.fd, iov, n);
+        if (w > 0) {
+          k.sent += static_cast<size_t>(w);
+          continue;
         }
-        const long key = o.distinct > 0 ? id % o.distinct : id;
-        if (full) {
-          patch_digits(tpl.body, tpl.id_pos, tpl.id_len, printed(id));
-          // unique input: encode (key, connection) in the first two values
-          const uint64_t u = static_cast<uint64_t>(key) * 64 + static_cast<uint64_t>(c);
-          patch_digits(tpl.body, tpl.v0_pos + 2, static_cast<size_t>(d), u % scale);
-          patch_digits(tpl.body, tpl.v1_pos + 2, static_cast<size_t>(d), (u / scale) % scale);
-          return tpl.body;
+        if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return true;
+        if (w < 0 && errno == EINTR) continue;
+        return false;
+      }
+    };
+    auto start_req = [&](AConn& k, long id, bool record) {
+      k.id = id;
+      k.record = record;
+      k.busy = true;
+      k.body = &body_for(k.bd, k.c, id);
+      k.head = "POST " + o.path + " HTTP/1.1\r\nHost: " + o.host + "\r\nContent-Type: application/json\r\nContent-Length: " +
+               std::to_string(k.body->size()) + "\r\n\r\n";
+      k.sent = 0;
+      k.in.clear();
+      k.hdr_end = std::string::npos;
+      k.clen = 0;
+      k.status = 0;
+      k.start = std::chrono::steady_clock::now();
+      if (k.fd < 0 && !open_conn(k)) {
+        k.busy = false;
+        if (record) finish(k.c, id, k.start, 0, std::string(), "connect failed");
+        return;
+      }
+      if (!pump_send(k)) {  // a stale keep-alive connection: reconnect once and resend
+        if (!open_conn(k) || (k.sent = 0, !pump_send(k))) {
+          k.busy = false;
+          if (record) finish(k.c, id, k.start, 0, std::string(), "send failed");
+          return;
         }
-        const long a = key % 10;
-        small = "{\"request_id\":\"" + o.id_prefix + std::to_string(printed(id)) + "\",\"input_data\":[" +
-                std::to_string(a) + ".0," + std::to_string(a + 1) + ".0," + std::to_string(a + 2) + ".0]}";
-        return small;
-      };
-      auto one = [&](long id, bool record) {
-        std::string& body = body_for(id);
-        auto s = std::chrono::steady_clock::now();
-        std::string err;
-        auto r = client.post(o.path, body, "application/json", &err);
-        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s).count();
-        if (!record) return;
-        if (r && r->status == 200) {
-          ++ok[c];
-          lat[c].push_back(ms);
-          when[c].emplace_back(std::chrono::duration<double, std::milli>(s - t0).count(), ms);
-          if (is_verify(id)) {
-            const size_t k = verify_k(id);
-            char idbuf[32];
-            std::snprintf(idbuf, sizeof idbuf, "%0*llu", kIdDigits, static_cast<unsigned long long>(printed(id)));
-            bool id_ok = false;
-            const double e = response_error(r->body, o.verify_expected + k * o.output_numel, o.output_numel,
-                                            o.id_prefix + idbuf, id_ok);
-            ++verified[c];
-            if (!id_ok) ++bad_id[c];
-            if (e < 0.0 || e > o.verify_tol) ++mismatched[c];
-            max_err[c] = std::max(max_err[c], e < 0.0 ? 1e30 : e);
+      }
+      want(k, k.sent < k.head.size() + k.body->size() ? EPOLLOUT : EPOLLIN);
+    };
+    auto fail_req = [&](AConn& k, const char* why) {
+      k.busy = false;
+      if (k.record) finish(k.c, k.id, k.start, 0, std::string(), why);
+      open_conn(k);
+    };
+    // parse what has arrived; true when the whole response is in
+    auto parse = [&](AConn& k) -> bool {
+      if (k.hdr_end == std::string::npos) {
+        k.hdr_end = k.in.find("\r\n\r\n");
+        if (k.hdr_end == std::string::npos) return false;
+        k.status = k.in.size() > 12 ? std::atoi(k.in.c_str() + 9) : 0;
+        bool have_len = false;
+        size_t pos = 0;
+        while (pos < k.hdr_end) {
+          size_t eol = k.in.find("\r\n", pos);
+          if (eol == std::string::npos || eol > k.hdr_end) eol = k.hdr_end;
+          static const char kCl[] = "content-length:";
+          if (eol - pos > sizeof(kCl) - 1 && strncasecmp(k.in.c_str() + pos, kCl, sizeof(kCl) - 1) == 0) {
+            k.clen = static_cast<size_t>(std::strtoull(k.in.c_str() + pos + sizeof(kCl) - 1, nullptr, 10));
+            have_len = true;
           }
-        } else {
-          ++fail[c];
-          errs[c][r ? "HTTP " + std::to_string(r->status) : err]++;
+          pos = eol + 2;
         }
-      };
-      while (true) {
-        long id = next_warm.fetch_add(1);
-        if (id >= o.warmup) break;
-        one(1000000000L + id, false);
+        if (!have_len) k.clen = 0;
       }
-      gate.arrive();  // all warm
-      gate.arrive();  // timed start
+      return k.in.size() >= k.hdr_end + 4 + k.clen;
+    };
+    bool timed = false;
+    long live = 0;  // requests in flight on this loop
+    // the connection's next request; one that fails at once (connect / send error) is accounted and
+    // the next id taken, as a blocking client moves on after a failed post
+    auto next_id = [&](AConn& k) {
       while (true) {
-        long id = next.fetch_add(1);
-        if (id >= o.requests) break;
-        one(id, true);
+        const long id = timed ? next.fetch_add(1) : next_warm.fetch_add(1);
+        if (id >= (timed ? o.requests : o.warmup)) break;
+        start_req(k, timed ? id : 1000000000L + id, timed);
+        if (k.busy) return;
       }
-      gate.arrive();
-    });
+      k.busy = false;
+    };
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs[i].c = mine[i];
+      if (full) cs[i].bd.tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(mine[i]));
+      open_conn(cs[i]);
+    }
+    std::vector<char> rbuf(1 << 16);
+    for (int phase = 0; phase < 2; ++phase) {
+      timed = phase == 1;
+      for (auto& k : cs) next_id(k);
+      while (true) {
+        live = 0;
+        for (auto& k : cs) live += k.busy;
+        if (!live) break;
+        epoll_event evs[64];
+        const int n = epoll_wait(ep, evs, 64, 50);
+        const auto now = std::chrono::steady_clock::now();
+        for (int e = 0; e < n; ++e) {
+          AConn& k = cs[evs[e].data.u64];
+          if (!k.busy) continue;
+          if (evs[e].events & EPOLLOUT) {
+            if (!pump_send(k)) {
+              fail_req(k, "send failed");
+              next_id(k);
+              continue;
+            }
+            if (k.sent >= k.head.size() + k.body->size()) want(k, EPOLLIN);
+          }
+          if (evs[e].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+            bool closed = false;
+            while (true) {
+              const ssize_t r = ::read(k.fd, rbuf.data(), rbuf.size());
+              if (r > 0) {
+                k.in.append(rbuf.data(), static_cast<size_t>(r));
+                continue;
+              }
+              if (r == 0) closed = true;
+              else if (errno == EINTR) continue;
+              else if (errno != EAGAIN && errno != EWOULDBLOCK) closed = true;
+              break;
+            }
+            if (parse(k)) {
+              k.busy = false;
+              if (k.record)
+                finish(k.c, k.id, k.start, k.status,
+                       is_verify(k.id) ? k.in.substr(k.hdr_end + 4, k.clen) : std::string(), std::string());
+              if (closed) open_conn(k);
+              next_id(k);
+            } else if (closed) {
+              fail_req(k, "connection closed");
+              next_id(k);
+            }
+          }
+        }
+        for (auto& k : cs)  // per-request timeout
+          if (k.busy && now - k.start > std::chrono::milliseconds(o.timeout_ms)) {
+            fail_req(k, "timeout");
+            next_id(k);
+          }
+      }
+      if (phase == 0) {
+        gate.arrive();  // all warm
+        gate.arrive();  // timed start
+      }
+    }
+    gate.arrive();
+    for (auto& k : cs)
+      if (k.fd >= 0) ::close(k.fd);
+    ::close(ep);
+  };
+
+  std::vector<std::thread> threads;
+  if (o.io_threads > 0) {
+    // Event-driven client: io_threads epoll loops share the C connections (one request in flight
+    // per connection, closed loop as below) -- no thread per connection competing with the server
+    // under test for the CPU share.
+    const int T = std::min(o.io_threads, C);
+    gate.total = T + 1;
+    for (int t = 0; t < T; ++t)
+      threads.emplace_back([&, t, T] {
+        pthread_setname_np(pthread_self(), "die-loadgen-io");
+        std::vector<int> mine;
+        for (int c = t; c < C; c += T) mine.push_back(c);
+        async_loop(mine);
+      });
+  } else {
+    for (int c = 0; c < C; ++c) {
+      threads.emplace_back([&, c] {
+        pthread_setname_np(pthread_self(), "die-loadgen");
+        HttpClient client(o.host, o.port, std::chrono::milliseconds(o.timeout_ms), std::chrono::milliseconds(o.timeout_ms), 2);
+        Bodies bd;
+        if (full) bd.tpl = make_full_template(o, o.seed * 7919 + static_cast<uint64_t>(c));
+        auto one = [&](long id, bool record) {
+          const std::string& body = body_for(bd, c, id);
+          auto s = std::chrono::steady_clock::now();
+          std::string err;
+          auto r = client.post(o.path, body, "application/json", &err);
+          if (!record) return;
+          finish(c, id, s, r ? r->status : 0, r ? r->body : std::string(), err);
+        };
+        while (true) {
+          long id = next_warm.fetch_add(1);
+          if (id >= o.warmup) break;
+          one(1000000000L + id, false);
+        }
+        gate.arrive();  // all warm
+        gate.arrive();  // timed start
+        while (true) {
+          long id = next.fetch_add(1);
+          if (id >= o.requests) break;
+          one(id, true);
+        }
+        gate.arrive();
+      });
+    }
   }
   gate.arrive();
   t0 = std::chrono::steady_clock::now();

@@ -48,6 +48,10 @@ struct LoadgenOptions {
   // Print request numbers scrambled (splitmix64(id) mod 10^10, fixed width) instead of in order:
   // FNV-1a of consecutive decimal strings clusters on the gateway's ring (bench.py ring analysis).
   bool scramble_ids = false;
+  // > 0: drive the connections from this many epoll threads instead of one blocking thread per
+  // connection (same closed loop, one request in flight per connection), so the client takes less
+  // of a CPU share it shares with the server under test.
+  int io_threads = 0;
 };
 
 // Runs warmup then the timed phase; returns {"ok","failed","wall_s","rps","latency_ms":{...},

@@ -607,7 +607,8 @@ def loadgen(verify_inputs: Optional[np.ndarray] = None, verify_expected: Optiona
     is checked against its expected row (relative L2 <= verify_tol, 0 = bit-exact): the result adds
     "verified", "mismatched", "bad_request_id" and "max_rel_err".  With payload="full" and
     verify_every=N only every N-th request is such a verified one (zero-padded text: never a cache
-    hit); scramble_ids=True prints request numbers scrambled (hash-uniform on the gateway ring)."""
+    hit); scramble_ids=True prints request numbers scrambled (hash-uniform on the gateway ring);
+    io_threads=N > 0 drives the connections from N epoll threads instead of one thread each."""
     err = _err_box()
     if verify_inputs is not None:
         xi = np.ascontiguousarray(verify_inputs, np.float32).reshape(len(verify_inputs), -1)
