@@ -1,0 +1,168 @@
+"""Random image-model graphs over the HIP planner's op set, for differential tests of the whole
+compile path (planner fusion passes + kernels) against the CPU executor (tests/test_plan_fuzz.py on
+the CPU: every graph plans; tests/test_gpu_fuzz.py: every graph matches the fp32 oracle).
+
+A graph is a chain of randomly chosen blocks on an NCHW image -- conv (1x1 / 3x3, stride 1 / 2,
+optional BN, one of several activations), residual add, squeeze-excitation gate, max / average
+pool, Pad + conv, nearest / linear resize, transposed conv, elementwise unary chains, channel
+concat + slice, Where / comparison masks -- then a global pool and a Gemm classifier.  Channel
+counts include values that are not multiples of 8 where the planner allows them.  Deterministic in
+the seed.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Tuple
+
+import numpy as np
+
+from ..utils.onnx_writer import GraphBuilder
+
+
+def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int], List[str]]:
+    """-> (model bytes, input (C, H, W), the block kinds used)."""
+    rng = np.random.default_rng(seed)
+    C0 = int(rng.choice([3, 8, 12]))
+    H = int(rng.choice([12, 16]))
+    H0 = H
+    g = GraphBuilder(name="fuzz%d" % seed)
+    x = g.input("image", ["N", C0, H, H])
+    used: List[str] = []
+    k = [0]
+
+    def nm(base):
+        k[0] += 1
+        return "%s%d" % (base, k[0])
+
+    def const(v):
+        return g.const(np.array(v, np.float32), nm("c"))
+
+    def lin(shape, fan):
+        return (rng.standard_normal(shape) / math.sqrt(fan)).astype(np.float32)
+
+    def conv(inp, cin, cout, ks, stride, pad, bias=True):
+        w = g.init(nm("w"), lin((cout, cin, ks, ks), cin * ks * ks))
+        ins = [inp, w]
+        if bias:
+            ins.append(g.init(nm("b"), (0.1 * rng.standard_normal(cout)).astype(np.float32)))
+        return g.node("Conv", ins, name=nm("conv"), kernel_shape=[ks, ks], strides=[stride, stride], pads=[pad] * 4)
+
+    def bn(inp, c):
+        ps = [g.init(nm("bn"), v) for v in ((1 + 0.1 * rng.standard_normal(c)).astype(np.float32),
+                                           (0.1 * rng.standard_normal(c)).astype(np.float32),
+                                           (0.1 * rng.standard_normal(c)).astype(np.float32),
+                                           (0.5 + rng.random(c)).astype(np.float32))]
+        return g.node("BatchNormalization", [inp] + ps, name=nm("bn"), epsilon=1e-5)
+
+    def act(inp):
+        a = str(rng.choice(["Relu", "Sigmoid", "Tanh", "LeakyRelu", "HardSwish", "Clip", "Softplus", "none"]))
+        if a == "none":
+            return inp
+        if a == "LeakyRelu":
+            return g.node(a, [inp], name=nm("act"), alpha=0.1)
+        if a == "Clip":
+            return g.node(a, [inp, const(0.0), const(6.0)], name=nm("act"))
+        return g.node(a, [inp], name=nm("act"))
+
+    # stem: a conv so the image becomes an NHWC activation with >= 8 channels
+    C = int(rng.choice([8, 16, 24]))
+    h = act(bn(conv(x, C0, C, 3, 1, 1, bias=False), C))
+    used.append("stem")
+    saved = [(h, C, H)]  # tensors a residual can join
+    for _ in range(blocks):
+        kinds = ["conv", "conv", "residual", "se", "pool", "padconv", "unary", "concat", "where"]
+        if H >= 8:
+            kinds += ["down"]
+        if H <= 12:
+            kinds += ["resize", "convT"]
+        kind = str(rng.choice(kinds))
+        if kind == "conv":
+            cout = int(rng.choice([8, 12, 16, 20, 24, 32])) if C % 8 == 0 else C
+            ks = int(rng.choice([1, 3]))
+            h = conv(h, C, cout, ks, 1, ks // 2)
+            if rng.random() < 0.5:
+                h = bn(h, cout)
+            h, C = act(h), cout
+        elif kind == "down":
+            cout = int(rng.choice([16, 24, 32]))
+            h = act(conv(h, C, cout, 3, 2, 1))
+            C, H = cout, (H + 1) // 2
+        elif kind == "residual":
+            same = [t for t in saved if t[1] == C and t[2] == H and t[0] != h]
+            if not same:
+                h2 = act(conv(h, C, C, 3, 1, 1))
+                h = g.node("Add", [h2, h], name=nm("res"))
+            else:
+                h = g.node("Add", [h, same[int(rng.integers(len(same)))][0]], name=nm("res"))
+            h = g.node("Relu", [h], name=nm("relu"))
+        elif kind == "se":
+            z = g.node("Flatten", [g.node("GlobalAveragePool", [h], name=nm("gap"))], name=nm("flat"), axis=1)
+            r = max(4, C // 4)
+            z = g.node("Relu", [g.node("Gemm", [z, g.init(nm("w"), lin((r, C), C)), g.init(nm("b"), np.zeros(r, np.float32))],
+                                       name=nm("fc"), transB=1)], name=nm("relu"))
+            z = g.node("Sigmoid", [g.node("Gemm", [z, g.init(nm("w"), lin((C, r), r)), g.init(nm("b"), np.zeros(C, np.float32))],
+                                          name=nm("fc"), transB=1)], name=nm("sig"))
+            z = g.node("Reshape", [z, g.const(np.array([-1, C, 1, 1], np.int64), nm("shape"))], name=nm("gate"))
+            h = g.node("Mul", [h, z], name=nm("se"))
+        elif kind == "pool":
+            if H < 4:
+                continue
+            op = str(rng.choice(["MaxPool", "AveragePool"]))
+            h = g.node(op, [h], name=nm("pool"), kernel_shape=[2, 2], strides=[2, 2])
+            H //= 2
+        elif kind == "padconv":
+            if C % 8:
+                continue
+            p = g.node("Pad", [h, g.const(np.array([0, 0, 1, 1, 0, 0, 1, 1], np.int64), nm("pads"))], name=nm("pad"),
+                       mode="constant")
+            h = act(conv(p, C, C, 3, 1, 0))
+        elif kind == "resize":
+            if rng.random() < 0.5:
+                h = g.node("Resize", [h, g.const(np.zeros(0, np.float32), nm("roi")),
+                                      g.const(np.array([1, 1, 2, 2], np.float32), nm("sc"))], name=nm("rs"),
+                           mode="nearest", coordinate_transformation_mode="asymmetric", nearest_mode="floor")
+            else:
+                h = g.node("Resize", [h, g.const(np.zeros(0, np.float32), nm("roi")),
+                                      g.const(np.array([1, 1, 2, 2], np.float32), nm("sc"))], name=nm("rs"),
+                           mode="linear", coordinate_transformation_mode="half_pixel")
+            H *= 2
+        elif kind == "convT":
+            if C % 8:
+                continue
+            cout = int(rng.choice([8, 12, 16]))
+            w = g.init(nm("wt"), lin((C, cout, 3, 3), C * 9 / 4))
+            h = g.node("ConvTranspose", [h, w, g.init(nm("b"), (0.1 * rng.standard_normal(cout)).astype(np.float32))],
+                       name=nm("convT"), kernel_shape=[3, 3], strides=[2, 2], pads=[1, 1, 1, 1], output_padding=[1, 1])
+            h, C, H = act(h), cout, H * 2
+        elif kind == "unary":
+            chain = str(rng.choice(["expneg", "softsign", "sqrt"]))
+            if chain == "expneg":  # exp(-|x|) in (0, 1]
+                h = g.node("Exp", [g.node("Neg", [g.node("Abs", [h], name=nm("abs"))], name=nm("neg"))], name=nm("exp"))
+            elif chain == "softsign":  # x / (1 + |x|)
+                den = g.node("Add", [g.node("Abs", [h], name=nm("abs")), const(1.0)], name=nm("den"))
+                h = g.node("Div", [h, den], name=nm("softsign"))
+            else:  # sqrt(x^2 + 1) - 1
+                h = g.node("Sub", [g.node("Sqrt", [g.node("Add", [g.node("Pow", [h, const(2.0)], name=nm("sq")),
+                                                                  const(1.0)], name=nm("p1"))], name=nm("sqrt")),
+                                   const(1.0)], name=nm("m1"))
+        elif kind == "concat":
+            if C % 8:
+                continue
+            b2 = act(conv(h, C, 8, 1, 1, 0))
+            h = g.node("Concat", [h, b2], name=nm("cat"), axis=1)
+            Cc = C + 8
+            keep = int(rng.choice([8, 16])) if C >= 16 else 8
+            h = g.node("Slice", [h, g.const(np.array([0], np.int64), nm("s0")), g.const(np.array([keep], np.int64), nm("s1")),
+                                 g.const(np.array([1], np.int64), nm("ax"))], name=nm("slice"))
+            C = keep if keep <= Cc else Cc
+        elif kind == "where":  # max(h, g(h)) through a comparison mask (continuous)
+            other = g.node("Tanh", [h], name=nm("tanh"))
+            h = g.node("Where", [g.node("Greater", [h, other], name=nm("gt")), h, other], name=nm("where"))
+        used.append(kind)
+        saved.append((h, C, H))
+    z = g.node("Flatten", [g.node("GlobalAveragePool", [h], name=nm("gap"))], name=nm("flat"), axis=1)
+    classes = int(rng.choice([5, 10, 16]))
+    y = g.node("Gemm", [z, g.init(nm("w"), lin((classes, C), C)), g.init(nm("b"), np.zeros(classes, np.float32))],
+               name="head", transB=1)
+    g.output(y, ["N", classes])
+    return g.model_proto(opset=13), (C0, H0, H0), used

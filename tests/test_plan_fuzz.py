@@ -1,0 +1,33 @@
+"""Random image graphs over the planner's op set (models/fuzz.py) all plan for the device, in both
+precisions, and run on the CPU executor (the oracle of tests/test_gpu_fuzz.py)."""
+import os
+
+import numpy as np
+import pytest
+
+SEEDS = list(range(30))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_graph_plans(native, tmp_path, seed):
+    from die_amd.models import fuzz
+
+    blob, shp, used = fuzz.build_random(seed)
+    p = str(tmp_path / ("f%d.onnx" % seed))
+    open(p, "wb").write(blob)
+    for prec in ("fp32", "bf16"):
+        r = native.plan_report(p, prec)
+        assert r["supported"], (seed, used, r["text"])
+    x = np.random.default_rng(seed).standard_normal((2,) + shp).astype(np.float32)
+    y = native.cpu_run(p, x)
+    assert y.shape[0] == 2 and np.isfinite(y).all()
+
+
+def test_fuzz_covers_every_block_kind():
+    from die_amd.models import fuzz
+
+    kinds = set()
+    for seed in SEEDS:
+        kinds.update(fuzz.build_random(seed)[2])
+    assert kinds >= {"stem", "conv", "down", "residual", "se", "pool", "padconv", "resize", "convT", "unary", "concat",
+                     "where"}, kinds
