@@ -1017,6 +1017,9 @@ CpuValuePtr CpuExecutor::run(const CpuValuePtr& input, std::unordered_map<std::s
         else known *= shape[d];
       }
       if (neg >= 0) shape[neg] = known ? in[0]->numel() / known : 0;
+      int64_t count = 1;
+      for (auto d : shape) count *= d;
+      if (count != in[0]->numel()) fail(n, "target shape does not match the element count");
       out = reshaped(*in[0], shape);
     } else if (op == "Squeeze" || op == "Unsqueeze") {
       std::vector<int64_t> axes = n.get_ints("axes");

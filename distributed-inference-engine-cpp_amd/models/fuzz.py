@@ -166,3 +166,76 @@ def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int
                name="head", transB=1)
     g.output(y, ["N", classes])
     return g.model_proto(opset=13), (C0, H0, H0), used
+
+
+def build_random_rows(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int], List[str]]:
+    """Random token-row graphs: input [N, S*D] reshaped to [N, S, D], then linear layers with
+    activations, LayerNorm, residuals, gated units, data-dependent token mixing (softmax(h W) h: a
+    MatMul of two activations), channel split / concat, and a mean over tokens into a classifier.
+    -> (model bytes, input (S*D,), the block kinds used)."""
+    rng = np.random.default_rng(10_000 + seed)
+    S = int(rng.choice([5, 9, 16, 20]))
+    D = int(rng.choice([16, 24, 32, 40]))
+    D0 = D
+    g = GraphBuilder(name="fuzzrows%d" % seed)
+    x = g.input("tokens", ["N", S * D])
+    h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
+    used: List[str] = []
+    k = [0]
+
+    def nm(base):
+        k[0] += 1
+        return "%s%d" % (base, k[0])
+
+    def lin(shape, fan):
+        return (rng.standard_normal(shape) / math.sqrt(fan)).astype(np.float32)
+
+    def linear(inp, din, dout):
+        w = g.init(nm("w"), lin((din, dout), din))
+        b = g.init(nm("b"), (0.1 * rng.standard_normal(dout)).astype(np.float32))
+        return g.node("Add", [g.node("MatMul", [inp, w], name=nm("mm")), b], name=nm("add"))
+
+    def act(inp):
+        a = str(rng.choice(["Relu", "Tanh", "Sigmoid", "Gelu", "none"]))
+        if a == "none":
+            return inp
+        if a == "Gelu":  # the erf form as torch exports it
+            t = g.node("Div", [inp, g.const(np.array(1.4142135381698608, np.float32), nm("c"))], name=nm("gd"))
+            t = g.node("Add", [g.node("Erf", [t], name=nm("erf")), g.const(np.array(1.0, np.float32), nm("c"))],
+                       name=nm("ga"))
+            return g.node("Mul", [g.node("Mul", [inp, t], name=nm("gm")), g.const(np.array(0.5, np.float32), nm("c"))],
+                          name=nm("gh"))
+        return g.node(a, [inp], name=nm("act"))
+
+    def ln(inp, c):
+        return g.node("LayerNormalization", [inp, g.init(nm("g"), (1 + 0.1 * rng.standard_normal(c)).astype(np.float32)),
+                                             g.init(nm("b"), (0.1 * rng.standard_normal(c)).astype(np.float32))],
+                      name=nm("ln"), axis=-1, epsilon=1e-5)
+
+    for _ in range(blocks):
+        kind = str(rng.choice(["linear", "linear", "ln", "residual", "gate", "mix", "splitcat"]))
+        if kind == "linear":
+            d2 = int(rng.choice([16, 24, 32, 40, 48]))
+            h, D = act(linear(h, D, d2)), d2
+        elif kind == "ln":
+            h = ln(h, D)
+        elif kind == "residual":
+            h = g.node("Add", [h, act(linear(h, D, D))], name=nm("res"))
+        elif kind == "gate":
+            h = g.node("Mul", [h, g.node("Sigmoid", [linear(h, D, D)], name=nm("sig"))], name=nm("gate"))
+        elif kind == "mix":
+            a = g.node("Softmax", [g.node("MatMul", [h, g.init(nm("wm"), lin((D, S), D))], name=nm("ml"))],
+                       name=nm("sm"), axis=-1)
+            h = g.node("MatMul", [a, h], name=nm("mix"))
+        elif kind == "splitcat":
+            if D % 16:
+                continue
+            a, b = g.node("Split", [h], name=nm("split"), axis=2, n_out=2)
+            h = g.node("Concat", [g.node("Tanh", [b], name=nm("t")), a], name=nm("cat"), axis=2)
+        used.append(kind)
+    pooled = g.node("ReduceMean", [h], name="pool", axes=[1], keepdims=0)
+    classes = int(rng.choice([3, 7, 10]))
+    y = g.node("Gemm", [pooled, g.init("head.w", lin((classes, D), D)), g.init("head.b", np.zeros(classes, np.float32))],
+               name="head", transB=1)
+    g.output(y, ["N", classes])
+    return g.model_proto(opset=13), (S * D0,), used

@@ -1,4 +1,4 @@
-"""Differential test of the whole HIP compile path on random graphs (models/fuzz.py): planner
+"""Differential test of the whole HIP compile path on random image and token-row graphs (models/fuzz.py): planner
 fusion passes + kernels vs the fp32 CPU executor, fp32 (split) mode at rel-L2 <= 2e-4 with the same
 top-1, bf16 at <= 5e-2, at batch 1 and a padded bucket."""
 import numpy as np
@@ -15,11 +15,11 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("seed", SEEDS)
-def test_random_graph_matches_cpu_executor(native, tmp_path, seed):
+@pytest.mark.parametrize("kind,seed", [("image", s) for s in SEEDS] + [("rows", s) for s in SEEDS])
+def test_random_graph_matches_cpu_executor(native, tmp_path, kind, seed):
     from die_amd.models import fuzz
 
-    blob, shp, used = fuzz.build_random(seed)
+    blob, shp, used = (fuzz.build_random if kind == "image" else fuzz.build_random_rows)(seed)
     p = str(tmp_path / ("f%d.onnx" % seed))
     open(p, "wb").write(blob)
     for prec, tol in (("fp32", 2e-4), ("bf16", 5e-2)):
