@@ -98,6 +98,7 @@ EngineOptions engine_opts(const Json& j) {
   e.bn_on_load = jget<bool>(j, "bn_on_load", e.bn_on_load);
   e.fuse_pairs = jget<bool>(j, "fuse_pairs", e.fuse_pairs);
   e.fuse_stem_pool = jget<bool>(j, "fuse_stem_pool", e.fuse_stem_pool);
+  e.fuse_gap_fc = jget<bool>(j, "fuse_gap_fc", e.fuse_gap_fc);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));

@@ -289,11 +289,11 @@ char* die_hybrid_partition(const char* model_path, int max_batch, int split, cha
   }
 }
 
-// fuse: bit 0 conv pairs, bit 1 stem + pool
+// fuse: bit 0 conv pairs, bit 1 stem + pool, bit 2 global pool + FC head
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse, char** err) {
   try {
     Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, (fuse & 1) != 0,
-                        (fuse & 2) != 0);
+                        (fuse & 2) != 0, (fuse & 4) != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -305,8 +305,8 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
       Json e = Json::object();
       static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                     "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                    "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm"};
-      static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::BMM + 1, "one name per PlanOp kind");
+                                    "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm", "gap_fc"};
+      static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::GAP_FC + 1, "one name per PlanOp kind");
       e["kind"] = kinds[o.kind];
       e["name"] = o.name;
       e["gflop"] = o.flops_per_sample / 1e9;

@@ -290,6 +290,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["bn_on_load"] = o.bn_on_load;
   j["fuse_pairs"] = o.fuse_pairs;
   j["fuse_stem_pool"] = o.fuse_stem_pool;
+  j["fuse_gap_fc"] = o.fuse_gap_fc;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;

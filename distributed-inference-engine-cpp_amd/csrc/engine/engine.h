@@ -228,6 +228,7 @@ struct EngineOptions {
   bool bn_on_load = false;        // bf16 plans: next unit's BN+ReLU applied on the 1x1 conv operand load
   bool fuse_pairs = true;         // expand conv + next reduce conv -> one CONV_PAIR launch (kernels/conv_pair.hip)
   bool fuse_stem_pool = true;     // stem conv + max pool (+ its BN/ReLU) -> one launch (kernels/stem.hip)
+  bool fuse_gap_fc = true;        // global pool + the FC head reading it -> one launch (kernels/misc.hip)
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
   // autotune: take the fastest in-kernel (fused) split-K candidate when it is within this fraction

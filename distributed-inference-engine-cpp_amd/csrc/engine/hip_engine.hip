@@ -64,7 +64,7 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
     plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
-                       opt.fuse_pairs, opt.fuse_stem_pool);
+                       opt.fuse_pairs, opt.fuse_stem_pool, opt.fuse_gap_fc);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -218,7 +218,7 @@ class HipEngine : public Engine {
         },
         [](void* p) { (void)hipHostFree(p); }, 32);
 
-    ws_bytes_ = 64u << 20;  // split-K partials (choose_splits / autotune stay within it)
+    ws_bytes_ = kern::kSplitKWorkspaceBytes;  // split-K / GAP_FC partials (choose_splits / autotune stay within it)
     // zero page for the LDS-DMA conv loads: padding pixels and M-tail rows (a whole K row)
     size_t zeros_bytes = 4096;
     for (const PlanOp& op : plan_.ops)
@@ -1126,6 +1126,13 @@ class HipEngine : public Engine {
           e = kern::global_avgpool(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
                                    nullptr, nullptr, nullptr, 0, B, op.H * op.W, op.C, st, live, sp_, op.gidx);
           break;
+        case PlanOp::GAP_FC:
+          e = kern::gap_fc(static_cast<const uint16_t*>(buf(op.in)), B, op.H * op.W, op.C, op.gidx,
+                           reinterpret_cast<const uint16_t*>(params_ + op.w_off), op.conv.wplane, op.conv.Kpad,
+                           prm(op.bias_off), op.Cp, op.act, static_cast<float*>(buf(op.out_f32)),
+                           side ? ws_side_ : wss_[s % n_exec_], ws_bytes_, side ? counters_side_ : counterss_[s % n_exec_],
+                           kCounters, st, live, sp_);
+          break;
         case PlanOp::AFFINE:
           e = kern::affine_act(static_cast<const uint16_t*>(buf(op.in)), static_cast<const uint16_t*>(buf(op.in2)),
                                prm(op.scale_off), prm(op.shift_off), op.act, static_cast<uint16_t*>(buf(op.out)),
@@ -1258,8 +1265,8 @@ class HipEngine : public Engine {
     for (auto& e : ev) (void)hipEventDestroy(e);
     static const char* kinds[] = {"input_prep", "conv", "pool", "gap", "affine", "to_nchw_f32", "bf16_to_f32",
                                   "layernorm", "tokens", "gather_rows", "attention", "stem", "gconv", "softmax",
-                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm"};
-    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::BMM + 1, "one name per PlanOp kind");
+                                  "rows_prep", "copy_cols", "binary", "unary", "conv_pair", "pad", "where", "resize", "bmm", "gap_fc"};
+    static_assert(sizeof(kinds) / sizeof(kinds[0]) == PlanOp::GAP_FC + 1, "one name per PlanOp kind");
     Json out = Json::object();
     Json ops = Json::array();
     double total = 0;

@@ -80,9 +80,9 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 class Planner {
  public:
   Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true,
-          bool fuse_stem_pool = true)
+          bool fuse_stem_pool = true, bool fuse_gap_fc = true)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
-        fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool) {}
+        fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool), fuse_gap_fc_(fuse_gap_fc) {}
 
   // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
   // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
@@ -124,6 +124,7 @@ class Planner {
     fuse_pool_affine();
     if (fuse_stem_pool_) fuse_stem_pool();
     if (fuse_pairs_) fuse_conv_pairs();
+    if (fuse_gap_fc_) fuse_gap_fc();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
@@ -2349,6 +2350,70 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
+  // Global pool -> the FC head (Gemm / 1x1 conv over the pooled [C] vector) that is its ONLY reader,
+  // with an fp32 output (a buffer or the graph output, directly or through a BF16_TO_F32 op) and no
+  // residual / second output: one GAP_FC op at the pool's position
+  // (kernels/misc.hip gap_fc_kernel); the pooled vector is never stored.
+  void fuse_gap_fc() {
+    std::vector<int> readers(plan_.bufs.size(), 0), reader_op(plan_.bufs.size(), -1);
+    const int nops = static_cast<int>(plan_.ops.size());
+    for (int i = 0; i < nops; ++i)
+      for (int b : {plan_.ops[i].in, plan_.ops[i].in2, plan_.ops[i].in3})
+        if (b >= 0) {
+          readers[b]++;
+          reader_op[b] = i;
+        }
+    std::vector<bool> drop(nops, false);
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind != PlanOp::GAP || p.out < 0 || p.out2 >= 0 || p.out_f32 != -1 || p.join >= 0 || p.in < 0 ||
+          readers[p.out] != 1)
+        continue;
+      const int j = reader_op[p.out];
+      if (j <= i || drop[j]) continue;
+      const PlanOp& q = plan_.ops[j];
+      const kern::ConvArgs& c = q.conv;
+      if (q.kind != PlanOp::CONV || q.in != p.out || q.in2 >= 0 || q.in3 >= 0 || q.out2 >= 0 || q.join >= 0 ||
+          c.relu > 1 || q.in_scale_off != SIZE_MAX || c.KH != 1 || c.KW != 1 || c.H != 1 || c.W != 1 ||
+          c.Cin != p.C || c.K != p.C)
+        continue;
+      // the f32 logits come from the conv itself, or (N % 8 != 0) from the BF16_TO_F32 op that is
+      // the only reader of its bf16 output -- the fused op writes them directly, in fp32
+      int conv_out = -1, nout = c.N, k = -1;
+      if (q.out_f32 != -1 && q.out < 0) {
+        conv_out = q.out_f32;
+      } else if (q.out_f32 == -1 && q.out >= 0 && readers[q.out] == 1) {
+        k = reader_op[q.out];
+        const PlanOp& r = plan_.ops[k];
+        if (k <= j || drop[k] || r.kind != PlanOp::BF16_TO_F32 || r.in != q.out || r.out_f32 == -1 || r.join >= 0 ||
+            (r.ld_store > 0 && r.rows_per_sample != 1) || r.C > c.N)
+          continue;
+        conv_out = r.out_f32;
+        nout = r.C;
+      } else {
+        continue;
+      }
+      if (!kern::gap_fc_slice(p.C, max_batch_, nout, kern::kSplitKWorkspaceBytes)) continue;
+      p.kind = PlanOp::GAP_FC;
+      p.name += "+" + q.name;
+      p.conv = c;
+      p.Cp = nout;  // logits per sample (= the f32 row pitch)
+      p.w_off = q.w_off;
+      p.bias_off = q.bias_off;
+      p.act = c.relu;
+      p.out = -1;  // the pooled buffer is dropped (no op references it any more)
+      p.out_f32 = conv_out;
+      p.flops_per_sample += q.flops_per_sample;
+      drop[j] = true;
+      if (k >= 0) drop[k] = true;
+    }
+    std::vector<PlanOp> out;
+    out.reserve(plan_.ops.size());
+    for (int i = 0; i < nops; ++i)
+      if (!drop[i]) out.push_back(std::move(plan_.ops[i]));
+    plan_.ops = std::move(out);
+  }
+
   // Back-to-back 1x1 pair (ResNet-v2 bottleneck boundary).  A dual-store expand conv P writes the
   // raw sum x (next residual) and a = act(bn(x)); when a's ONLY reader is a plain 1x1/s1 reduce conv
   // Q, both become one CONV_PAIR op at P's position (Q has no other input, so computing it early is
@@ -2531,6 +2596,7 @@ class Planner {
   bool bn_on_load_ = false;  // EngineOptions::bn_on_load (bf16 plans only)
   bool fuse_pairs_ = true;   // EngineOptions::fuse_pairs
   bool fuse_stem_pool_ = true;  // EngineOptions::fuse_stem_pool
+  bool fuse_gap_fc_ = true;     // EngineOptions::fuse_gap_fc
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -2631,12 +2697,12 @@ onnx::Model rewrite_conv_transpose(const onnx::Model& src) {
 }  // namespace
 
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs,
-                bool fuse_stem_pool) {
+                bool fuse_stem_pool, bool fuse_gap_fc) {
   if (has_conv_transpose(m)) {
     const onnx::Model r = rewrite_conv_transpose(m);
-    return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool).run();
+    return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc).run();
   }
-  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool).run();
+  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc).run();
 }
 
 std::string PlanReport::text() const {

@@ -52,8 +52,10 @@ struct PlanOp {
     WHERE,   // out = in != 0 ? in2 : in3 (in2 / in3 = -1: the scalars clip_lo / clip_hi)
     RESIZE,  // NHWC Resize: in [H][W] -> out [Ho][Wo]; act = mode, gidx = coord, is_max = nearest mode,
              // clip_lo / clip_hi = scales (output / input)
-    BMM      // batched MatMul of two row activations: out [S][Cp pitch C] = in [S][gidx of ld[0]] x
+    BMM,     // batched MatMul of two row activations: out [S][Cp pitch C] = in [S][gidx of ld[0]] x
              // in2 [gidx][ld[1]]; Cp = logical N
+    GAP_FC   // global pool (gidx = mode) of in [H*W][C] + the 1x1 GEMM that is its only reader, in one
+             // launch: out_f32 [Cp] = act(pool . w + bias); conv describes the GEMM (Kpad, wplane)
   } kind;
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
@@ -114,8 +116,9 @@ struct Plan {
 // a second stream (PlanOp::join; extends their inputs' lifetimes).  split: fp32 mode (Plan::split).
 // fuse_pairs: lower expand -> reduce 1x1 conv pairs to CONV_PAIR ops (EngineOptions::fuse_pairs).
 // fuse_stem_pool: stem conv + max pool in one STEM op (EngineOptions::fuse_stem_pool).
+// fuse_gap_fc: global pool + the FC head reading it in one GAP_FC op (EngineOptions::fuse_gap_fc).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
-                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true);
+                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = true);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

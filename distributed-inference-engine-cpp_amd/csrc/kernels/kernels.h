@@ -105,6 +105,16 @@ hipError_t pool2d(const uint16_t* x, uint16_t* y, int B, int H, int W, int C, in
 hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, const float* scale, const float* shift,
                           int relu, int B, int HW, int C, hipStream_t s, const long long* live = nullptr,
                           int split = 0, int mode = 0);
+// Global pool (mode as above) fused with the fully-connected layer that reads it (misc.hip
+// gap_fc_kernel): x [B, HW, C] -> out f32 [B][N] = act(pool(x) . w[n] + bias[n]); w = [>= N][Kpad]
+// GEMM weights (split: lo plane at +wplane).  Partials [C/cs][B][N] f32 go through `ws` (ws_bytes),
+// one counter per group of 128 classes (counters_n available, left at 0).  gap_fc_slice: the
+// channel slice the launcher uses for this shape (0 = unsupported: C % 8, workspace too small).
+int gap_fc_slice(int C, int B, int N, size_t ws_bytes);
+constexpr size_t kSplitKWorkspaceBytes = size_t(64) << 20;  // the engine's split-K / GAP_FC workspace
+hipError_t gap_fc(const uint16_t* x, int B, int HW, int C, int mode, const uint16_t* w, long long wplane, int Kpad,
+                  const float* bias, int N, int act, float* out, float* ws, size_t ws_bytes, int* counters,
+                  int counters_n, hipStream_t s, const long long* live = nullptr, int split = 0);
 // Elementwise over [M][C] bf16: y = act(x * scale[c] + shift[c] (+ z))   (scale/shift/z optional;
 // act 1 = ReLU, 3 = Clip(clip_lo, clip_hi))
 hipError_t affine_act(const uint16_t* x, const uint16_t* z, const float* scale, const float* shift, int act,

@@ -169,6 +169,111 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
   }
 }
 
+// Global pool + fully-connected head in one launch (ResNet: [B, 7x7, 2048] -> mean -> 2048 x 1000
+// GEMM at B ~ 20, where the GEMM is far too small for MFMA tiles and two launches cost ~30 us).
+// Block (slice, group): pools channels [c0, c0 + CS) of every live sample into LDS in fp32 (hi + lo
+// planes), dots them with the group's <= kGfcCls weight rows (hi + lo -> fp32, VALU FMAs), and
+// writes the partial logits [slice][b][n] with write-through (sc1) stores.  The last slice block of
+// a group to arrive (one agent-scope ticket per group, the hand-off of the fused split-K epilogue in
+// conv_igemm_impl.h) sums the slices in slice order -- deterministic -- adds the bias (+ ReLU) and
+// writes the fp32 logits.
+constexpr int kGfcRows = 64;   // samples per LDS chunk
+constexpr int kGfcCls = 128;   // classes per block: 2 threads per class, each half of the samples
+constexpr int kCpolSc1Gfc = 16;
+
+template <int CS>
+__global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict__ x, long long xplane, int HW, int C,
+                                                     int mode, const uint16_t* __restrict__ w, long long wplane, int Kpad,
+                                                     const float* __restrict__ bias, int N, int act,
+                                                     float* __restrict__ out, float* ws, int* counters,
+                                                     const long long* __restrict__ live, int B, int split) {
+  __shared__ float pooled[kGfcRows][CS];
+  __shared__ int flag;
+  const int slice = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
+  const int c0 = slice * CS, n0 = grp * kGfcCls;
+  const int Bl = live ? static_cast<int>(min(*live, static_cast<long long>(B))) : B;
+  const int nl = tid % kGfcCls, half = tid / kGfcCls;
+  const int n = n0 + nl;
+  const float inv = mode == 0 ? 1.f / HW : 1.f;
+  const float init = mode == 2 ? -INFINITY : 0.f;
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+  constexpr int GPR = CS / 8;
+  constexpr int JC = CS < 64 ? CS : 64;  // weights held in registers per pass
+  for (int b0 = 0; b0 < Bl; b0 += kGfcRows) {
+    const int nb = min(kGfcRows, Bl - b0);
+    for (int it = tid; it < nb * GPR; it += 256) {
+      const int bi = it / GPR, g = it - bi * GPR;
+      const uint16_t* src = x + static_cast<long long>(b0 + bi) * HW * C + c0 + g * 8;
+      float acc[8] = {init, init, init, init, init, init, init, init};
+#pragma unroll 7
+      for (int p = 0; p < HW; ++p) {
+        float v[8];
+        load8v(src + static_cast<long long>(p) * C, xplane, split != 0, v);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mode == 2 ? fmaxf(acc[t], v[t]) : acc[t] + v[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pooled[bi][g * 8 + t] = acc[t] * inv;
+    }
+    __syncthreads();
+    if (n < N) {
+      float acc[kGfcRows / 2];
+#pragma unroll
+      for (int r = 0; r < kGfcRows / 2; ++r) acc[r] = 0.f;
+      for (int j0 = 0; j0 < CS; j0 += JC) {
+        float wv[JC];
+        const uint16_t* wr = w + static_cast<long long>(n) * Kpad + c0 + j0;
+#pragma unroll
+        for (int q = 0; q < JC / 8; ++q) load8v(wr + q * 8, wplane, split != 0, wv + q * 8);
+#pragma unroll
+        for (int r = 0; r < kGfcRows / 2; ++r) {
+          const int bi = half + 2 * r;
+          if (bi >= nb) break;
+          const float4* pr = reinterpret_cast<const float4*>(&pooled[bi][j0]);
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < JC / 4; ++q) {
+            const float4 u = pr[q];
+            s += u.x * wv[4 * q] + u.y * wv[4 * q + 1] + u.z * wv[4 * q + 2] + u.w * wv[4 * q + 3];
+          }
+          acc[r] += s;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kGfcRows / 2; ++r) {
+        const int bi = half + 2 * r;
+        if (bi >= nb) break;
+        const unsigned off = static_cast<unsigned>(((static_cast<long long>(slice) * B + b0 + bi) * N + n) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[r]), wsr, off, 0, kCpolSc1Gfc);
+      }
+    }
+    __syncthreads();  // pooled is rewritten by the next chunk
+  }
+  // hand-off: every wave drains its write-through stores, one lane takes the group's ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(counters + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == static_cast<int>(gridDim.x) - 1;
+    if (last) __hip_atomic_store(counters + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = last;
+  }
+  __syncthreads();
+  if (!flag) return;
+  const int ncls = min(kGfcCls, N - n0);
+  for (int it = tid; it < Bl * ncls; it += 256) {
+    const int bi = it / ncls, nn = n0 + (it - bi * ncls);
+    float s = 0.f;
+    for (int sl = 0; sl < static_cast<int>(gridDim.x); ++sl) {
+      const unsigned off = static_cast<unsigned>(((static_cast<long long>(sl) * B + bi) * N + nn) * 4);
+      s += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, off, 0, kCpolSc1Gfc));
+    }
+    if (bias) s += bias[nn];
+    if (act == 1) s = fmaxf(s, 0.f);
+    out[static_cast<long long>(bi) * N + nn] = s;
+  }
+}
+
 // act: 0 none, 1 relu.  One thread per 8 elements of a row of C (C % 8 == 0).
 __global__ void affine_act_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ z,
                                   const float* __restrict__ scale, const float* __restrict__ shift, int act,
@@ -259,6 +364,49 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
   const int CG = C / 8;
   dim3 grid((CG + 7) / 8, B);  // 8 channel groups x 32 pixel slices per block
   hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split, mode);
+  return hipGetLastError();
+}
+
+// Channel slice: the narrowest that divides C with at most 32 slices (ResNet50: 64 -> 32 x 8 =
+// 256 blocks), else the narrowest that divides C; the partials [C/cs][B][N] must fit `ws`.
+int gap_fc_slice(int C, int B, int N, size_t ws_bytes) {
+  static const int kSlices[] = {8, 16, 32, 64, 128};
+  auto fits = [&](int cs) {
+    const size_t bytes = static_cast<size_t>(C / cs) * B * N * 4;
+    return C % cs == 0 && bytes <= ws_bytes && bytes < (size_t(1) << 31);
+  };
+  for (int cs : kSlices)
+    if (C / cs <= 32 && fits(cs)) return cs;
+  for (int cs : kSlices)
+    if (fits(cs)) return cs;
+  return 0;
+}
+
+hipError_t gap_fc(const uint16_t* x, int B, int HW, int C, int mode, const uint16_t* w, long long wplane, int Kpad,
+                  const float* bias, int N, int act, float* out, float* ws, size_t ws_bytes, int* counters,
+                  int counters_n, hipStream_t s, const long long* live, int split) {
+  const int cs = gap_fc_slice(C, B, N, ws_bytes);
+  const int groups = (N + kGfcCls - 1) / kGfcCls;
+  if (!cs || mode < 0 || mode > 2 || Kpad < C || Kpad % 8 || groups > counters_n || act < 0 || act > 1 || !counters ||
+      !ws)
+    return hipErrorInvalidValue;
+  const long long xplane = static_cast<long long>(B) * HW * C;
+  dim3 grid(C / cs, groups);
+#define GAP_FC_CASE(CSV)                                                                                          \
+  case CSV:                                                                                                        \
+    hipLaunchKernelGGL(gap_fc_kernel<CSV>, grid, dim3(256), 0, s, x, xplane, HW, C, mode, w, wplane, Kpad, bias, N, \
+                       act, out, ws, counters, live, B, split);                                                    \
+    break;
+  switch (cs) {
+    GAP_FC_CASE(8)
+    GAP_FC_CASE(16)
+    GAP_FC_CASE(32)
+    GAP_FC_CASE(64)
+    GAP_FC_CASE(128)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef GAP_FC_CASE
   return hipGetLastError();
 }
 

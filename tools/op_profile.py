@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--tune-warm-input", action="store_true", help="autotune with each conv's producer run first")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0, help="prefer fused split-K within this fraction")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
+    ap.add_argument("--no-fuse-gap-fc", action="store_true", help="global pool and FC head as two launches (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true", help="stem and max pool as two launches (EngineOptions::fuse_stem_pool)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
@@ -41,7 +42,7 @@ def main():
     e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision,
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
                       splitk_fused_margin=a.splitk_fused_margin,
-                      fuse_stem_pool=not a.no_fuse_stem_pool)
+                      fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=not a.no_fuse_gap_fc)
     p = e.profile(a.batch, a.iters)
     e.close()
     lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
