@@ -161,6 +161,8 @@ int die_kern_gather_rows(uint64_t x, uint64_t y, int B, int Sq, int idx, int C, 
   return static_cast<int>(kern::gather_rows(P<const uint16_t>(x), P<uint16_t>(y), B, Sq, idx, C, S(stream), split));
 }
 
+void die_kern_set_attention_variant(int v) { kern::set_attention_variant(v); }
+
 int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,
                        int ldv, int ldo, float scale, uint64_t stream, int split) {
   return static_cast<int>(kern::attention(P<const uint16_t>(q), P<const uint16_t>(k), P<const uint16_t>(v),

@@ -285,6 +285,9 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // LayerNorm over the last dim of bf16 rows [rows][C] (C % 8 == 0: the stored pitch), fp32
 // statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
 // true when the streaming attention kernel is built in (any sequence length; else S <= 256)
+// Streaming attention variant (measurement switch, process-wide): 0 = K/V staged one tile ahead
+// (default), 1 = two tiles ahead.
+void set_attention_variant(int v);
 bool attention_any_length();
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.

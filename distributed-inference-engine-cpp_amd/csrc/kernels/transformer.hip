@@ -376,7 +376,10 @@ __global__ __launch_bounds__(512) void attention_kernel(const uint16_t* __restri
 // of one (image, head) pair: ViT-B/16 at B = 32 is 768 blocks, all resident at 4 blocks per CU.
 // The per-tile math (S^T = K Q^T, online exp2 softmax, O^T += V^T P^T with transposed V reads, split
 // hi/lo MFMAs) is the kernel above's, with tile-local K/V rows.
-template <bool SPLIT>
+// DEEP: two register sets of staged K/V -- tile kt+2's loads are issued while tile kt computes and
+// tile kt+1 (loaded one step earlier) goes to LDS, so each load has two tiles of MFMAs to land
+// (+16 VGPRs; still 3 waves per SIMD).
+template <bool SPLIT, bool DEEP>
 __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t* __restrict__ q,
                                                                const uint16_t* __restrict__ k,
                                                                const uint16_t* __restrict__ v,
@@ -393,8 +396,9 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
   const int nkt = (S + KT - 1) / KT;
   // tile loader: thread = (key row ls, 16-B chunk lc) of every tensor plane
   const int ls = tid >> 3, lc = tid & 7;
-  uint4 kr[NP], vr[NP];
-  auto fetch = [&](int kt) {
+  typedef uint4 Stage[NP];
+  Stage kr0, vr0, kr1, vr1;
+  auto fetch = [&](int kt, Stage& kr, Stage& vr) {
     const int s = kt * KT + ls;
     const bool ok = s < S;
 #pragma unroll
@@ -405,7 +409,7 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
                   : make_uint4(0, 0, 0, 0);
     }
   };
-  auto put = [&](int buf) {
+  auto put = [&](int buf, const Stage& kr, const Stage& vr) {
 #pragma unroll
     for (int pl = 0; pl < NP; ++pl) {
       *reinterpret_cast<uint4*>(Ks[buf][pl] + ls * AT_D + ((lc ^ ((ls >> 1) & 7)) << 3)) = kr[pl];
@@ -430,17 +434,23 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
   }
   // K/V tile 0 after the query loads: put(0)'s wait for the tile also covers the query fragments, so
   // the loop's MFMAs never wait on vmcnt (which would drain the NEXT tile's in-flight loads each step)
-  fetch(0);
-  put(0);
+  fetch(0, kr0, vr0);
+  put(0, kr0, vr0);
   __syncthreads();
+  if (DEEP && nkt > 1) fetch(1, kr1, vr1);
   f32x16 o0, o1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-  for (int kt = 0; kt < nkt; ++kt) {
+  // one key tile; (ka, va): the register set free for a new fetch, (kb, vb): tile kt+1 when DEEP
+  auto step = [&](int kt, Stage& ka, Stage& va, Stage& kb, Stage& vb) {
     const int buf = kt & 1;
-    if (kt + 1 < nkt) fetch(kt + 1);  // in flight under this tile's MFMAs
+    if (DEEP) {
+      if (kt + 2 < nkt) fetch(kt + 2, ka, va);  // in flight under this tile's and the next tile's MFMAs
+    } else {
+      if (kt + 1 < nkt) fetch(kt + 1, ka, va);  // in flight under this tile's MFMAs
+    }
     if (active) {
       f32x16 sc;
 #pragma unroll
@@ -516,8 +526,16 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
         }
       }
     }
-    if (kt + 1 < nkt) put(buf ^ 1);  // that buffer's last readers passed the previous barrier
+    // the other LDS buffer's last readers passed the previous barrier
+    if (kt + 1 < nkt) {
+      if (DEEP) put(buf ^ 1, kb, vb);
+      else put(buf ^ 1, ka, va);
+    }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    step(kt, kr0, vr0, kr1, vr1);
+    if (kt + 1 < nkt) step(kt + 1, kr1, vr1, kr0, vr0);
   }
   if (!active) return;
   l += __shfl_xor(l, 32, 64);
@@ -643,6 +661,11 @@ hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long 
 
 bool attention_any_length() { return kAttnStream; }
 
+namespace {
+int g_attn_variant = 0;  // 0: K/V staged one tile ahead, 1: two tiles ahead (DEEP)
+}
+void set_attention_variant(int v) { g_attn_variant = v; }
+
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
   if (D != AT_D || S <= 0 || (!kAttnStream && S > 256) || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4)
@@ -650,8 +673,15 @@ hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, ui
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
   if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S)
     dim3 grid((S + 127) / 128, H, B);
-    if (split) hipLaunchKernelGGL(attention_stream_kernel<true>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else hipLaunchKernelGGL(attention_stream_kernel<false>, grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    const bool deep = g_attn_variant == 1;
+    if (split && deep)
+      hipLaunchKernelGGL((attention_stream_kernel<true, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (split)
+      hipLaunchKernelGGL((attention_stream_kernel<true, false>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else if (deep)
+      hipLaunchKernelGGL((attention_stream_kernel<false, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+    else
+      hipLaunchKernelGGL((attention_stream_kernel<false, false>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
     return hipGetLastError();
   }
   dim3 grid(1, H, B);  // one 8-wave block per (image, head): wave w = query tile w (S <= 256)

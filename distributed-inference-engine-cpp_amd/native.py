@@ -664,6 +664,8 @@ def _sig_kernels():
     L.die_kern_gather_rows.argtypes = [u64, u64] + [i] * 4 + [u64, i]
     L.die_kern_attention.restype = i
     L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64, i]
+    L.die_kern_set_attention_variant.restype = None
+    L.die_kern_set_attention_variant.argtypes = [i]
     L.die_decode_scratch_bytes.restype = C.c_longlong
     L.die_decode_scratch_bytes.argtypes = [i, C.c_longlong]
     L.die_kern_decode.restype = i

@@ -342,6 +342,12 @@ def attention(q, k, v, heads, scale=None):
     return out
 
 
+def set_attention_variant(v):
+    """Process-wide streaming-attention variant (kernels.h set_attention_variant): 0 = K/V staged one
+    tile ahead (default), 1 = two tiles ahead."""
+    native.kernels().die_kern_set_attention_variant(int(v))
+
+
 def attention_qkv_split(qkv, heads, scale=None):
     """fp32 mode: qkv [B, S, 3*C] float (Q | K | V columns) -> fp32 [B, S, C] through the split kernel
     (planes of the packed QKV rows, like the engine's fused QKV GEMM output)."""
