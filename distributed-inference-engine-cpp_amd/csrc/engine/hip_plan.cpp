@@ -912,8 +912,9 @@ class Planner {
     const Val& k = vals_[ctx.k];
     const Val& v = vals_[ctx.v];
     const int S = q.H, C = q.nh * q.hd;
-    if (q.hd != 64 || k.H != S || v.H != S || (!kern::attention_any_length() && S > 256))
-      throw std::runtime_error("attention " + name + ": needs head dim 64 (and <= 256 tokens without the streaming kernel)");
+    if (!kern::attention_supported(q.hd, S) || k.H != S || v.H != S)
+      throw std::runtime_error("attention " + name + ": needs head dim 32, 64, 96 or 128 (64 and <= 256 tokens " +
+                               "without the streaming kernel)");
     PlanOp p;
     p.kind = PlanOp::ATTENTION;
     p.name = name;

@@ -289,6 +289,9 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // (default), 1 = two tiles ahead.
 void set_attention_variant(int v);
 bool attention_any_length();
+// Head dim / sequence length the attention launcher takes (streaming kernel: head dim 32, 64, 96
+// or 128, any length; the whole-K/V kernel: 64 and <= 256 tokens).
+bool attention_supported(int D, int S);
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
@@ -299,8 +302,8 @@ hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const floa
 // y[b,:] = x[b, idx, :]   (x is [B][S][C])
 hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s, int split = 0);
 // Multi-head attention: out[b,s,h*D:(h+1)*D] = softmax(scale * Q_h K_h^T) V_h with Q/K/V rows
-// [B*S][ld*] (head h at columns h*D).  D == 64, S <= 256 (split: S <= 224; q/k/v/out planes are
-// B*S*ld of their pitch).
+// [B*S][ld*] (head h at columns h*D).  D and S as attention_supported() takes them (split: q/k/v/out
+// planes are B*S*ld of their pitch).
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split = 0);
 

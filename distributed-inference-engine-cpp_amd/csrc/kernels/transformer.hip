@@ -378,57 +378,79 @@ __global__ __launch_bounds__(512) void attention_kernel(const uint16_t* __restri
 // hi/lo MFMAs) is the kernel above's, with tile-local K/V rows.
 // DEEP: two register sets of staged K/V -- tile kt+2's loads are issued while tile kt computes and
 // tile kt+1 (loaded one step earlier) goes to LDS, so each load has two tiles of MFMAs to land
-// (+16 VGPRs; still 3 waves per SIMD).
-template <bool SPLIT, bool DEEP>
-__global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t* __restrict__ q,
-                                                               const uint16_t* __restrict__ k,
-                                                               const uint16_t* __restrict__ v,
-                                                               uint16_t* __restrict__ out, int S, int ldq, int ldk,
-                                                               int ldv, int ldo, float scale_log2) {
+// (+16 VGPRs; still 3 waves per SIMD at head dim 64).
+// HD: head dim 32, 64, 96 or 128 -- HD/16 k-steps of the K Q^T product, HD/32 output accumulators
+// (32 rows of D each) for O^T; K rows of HD/8 16-B chunks (XOR-swizzled when that is a power of two),
+// V rows padded to HD + 32.  Past 64 the registers allow 2 waves per SIMD (1 for split at 128).
+template <int HD, bool SPLIT>
+struct AttnGeom {
+  static constexpr int CPR = HD / 8;                             // 16-B chunks per K/V row
+  static constexpr int SW = (CPR & (CPR - 1)) == 0 ? (CPR < 8 ? CPR - 1 : 7) : 0;  // K chunk swizzle mask
+  static constexpr int VPD = HD + 32;                            // V row pitch (elements)
+  static constexpr int LPT = (32 * CPR + 255) / 256;             // 16-B loads per thread per plane per tile
+  static constexpr int NKS = HD / 16, NDT = HD / 32;
+  static constexpr int WAVES_PER_SIMD = HD > 96 && SPLIT ? 1 : (HD > 64 ? 2 : 3);
+};
+
+template <bool SPLIT, bool DEEP, int HD>
+__global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void attention_stream_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    uint16_t* __restrict__ out, int S, int ldq, int ldk, int ldv, int ldo, float scale_log2) {
+  using G = AttnGeom<HD, SPLIT>;
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int KT = 32;  // keys per tile
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][NP][KT * AT_D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][NP][KT * VP];
+  constexpr int CPR = G::CPR, SW = G::SW, VPD = G::VPD, LPT = G::LPT, NKS = G::NKS, NDT = G::NDT;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][NP][KT * HD];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][NP][KT * VPD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.y, b = blockIdx.z;
   const long long rowbase = static_cast<long long>(b) * S;
   const long long rows = static_cast<long long>(gridDim.z) * S;  // plane distances: rows x pitch
   const int nkt = (S + KT - 1) / KT;
-  // tile loader: thread = (key row ls, 16-B chunk lc) of every tensor plane
-  const int ls = tid >> 3, lc = tid & 7;
-  typedef uint4 Stage[NP];
+  // tile loader: load j of a thread = (key row, 16-B chunk) index tid + 256 j of every tensor plane
+  typedef uint4 Stage[NP][LPT];
   Stage kr0, vr0, kr1, vr1;
   auto fetch = [&](int kt, Stage& kr, Stage& vr) {
-    const int s = kt * KT + ls;
-    const bool ok = s < S;
 #pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      kr[pl] = ok ? *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * AT_D + lc * 8)
-                  : make_uint4(0, 0, 0, 0);
-      vr[pl] = ok ? *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * AT_D + lc * 8)
-                  : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < LPT; ++j) {
+      const int idx = tid + 256 * j, ls = idx / CPR, lc = idx % CPR;
+      const int s = kt * KT + ls;
+      const bool ok = idx < KT * CPR && s < S;
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        kr[pl][j] = ok ? *reinterpret_cast<const uint4*>(k + pl * rows * ldk + (rowbase + s) * ldk + h * HD + lc * 8)
+                       : make_uint4(0, 0, 0, 0);
+        vr[pl][j] = ok ? *reinterpret_cast<const uint4*>(v + pl * rows * ldv + (rowbase + s) * ldv + h * HD + lc * 8)
+                       : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto put = [&](int buf, const Stage& kr, const Stage& vr) {
 #pragma unroll
-    for (int pl = 0; pl < NP; ++pl) {
-      *reinterpret_cast<uint4*>(Ks[buf][pl] + ls * AT_D + ((lc ^ ((ls >> 1) & 7)) << 3)) = kr[pl];
-      *reinterpret_cast<uint4*>(Vs[buf][pl] + ls * VP + lc * 8) = vr[pl];
+    for (int j = 0; j < LPT; ++j) {
+      const int idx = tid + 256 * j, ls = idx / CPR, lc = idx % CPR;
+      if (idx < KT * CPR) {
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl) {
+          *reinterpret_cast<uint4*>(Ks[buf][pl] + ls * HD + ((lc ^ ((ls >> 1) & SW)) << 3)) = kr[pl][j];
+          *reinterpret_cast<uint4*>(Vs[buf][pl] + ls * VPD + lc * 8) = vr[pl][j];
+        }
+      }
     }
   };
   const int q0 = blockIdx.x * 128 + wave * 32;
   const bool active = q0 < S;  // wave-uniform; an idle wave still loads tiles and meets every barrier
   const int r = lane & 31, hh = lane >> 5;
-  bf16x8 qf[NP][4];
+  bf16x8 qf[NP][NKS];
   {
     const int qr = q0 + r;
 #pragma unroll
     for (int pl = 0; pl < NP; ++pl)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < NKS; ++ks) {
         uint4 t = make_uint4(0, 0, 0, 0);
         if (qr < S)
-          t = *reinterpret_cast<const uint4*>(q + pl * rows * ldq + (rowbase + qr) * ldq + h * AT_D + ks * 16 + hh * 8);
+          t = *reinterpret_cast<const uint4*>(q + pl * rows * ldq + (rowbase + qr) * ldq + h * HD + ks * 16 + hh * 8);
         qf[pl][ks] = __builtin_bit_cast(bf16x8, t);
       }
   }
@@ -438,9 +460,11 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
   put(0, kr0, vr0);
   __syncthreads();
   if (DEEP && nkt > 1) fetch(1, kr1, vr1);
-  f32x16 o0, o1;
+  f32x16 o[NDT];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
   // one key tile; (ka, va): the register set free for a new fetch, (kb, vb): tile kt+1 when DEEP
@@ -456,9 +480,9 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
 #pragma unroll
       for (int i = 0; i < 16; ++i) sc[i] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < NKS; ++ks) {
         const int chunk = 2 * ks + hh;
-        const int ko = r * AT_D + ((chunk ^ ((r >> 1) & 7)) << 3);
+        const int ko = r * HD + ((chunk ^ ((r >> 1) & SW)) << 3);
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks[buf][0] + ko);
         if constexpr (SPLIT) {
           const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Ks[buf][1] + ko);
@@ -488,10 +512,9 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
       const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first tile: 0
       l *= alpha;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o0[i] *= alpha;
-        o1[i] *= alpha;
-      }
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(sc[i] - mn);  // raw v_exp_f32 (args <= 0)
@@ -507,22 +530,21 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
           pf[j] = static_cast<__bf16>(sc[8 * st + j]);
           if constexpr (SPLIT) pfl[j] = static_cast<__bf16>(sc[8 * st + j] - static_cast<float>(pf[j]));
         }
-        const int vo = (16 * st + 4 * hh + qq) * VP + 16 * g + 4 * pp;
+        const int vo = (16 * st + 4 * hh + qq) * VPD + 16 * g + 4 * pp;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
+        for (int dt = 0; dt < NDT; ++dt) {
           const s16x4 lo = ds_read_tr16(Vs[buf][0] + vo + dt * 32);
-          const s16x4 hi = ds_read_tr16(Vs[buf][0] + vo + 8 * VP + dt * 32);
+          const s16x4 hi = ds_read_tr16(Vs[buf][0] + vo + 8 * VPD + dt * 32);
           const bf16x8 af = __builtin_bit_cast(bf16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-          f32x16& o = dt == 0 ? o0 : o1;
           if constexpr (SPLIT) {
             const s16x4 lo2 = ds_read_tr16(Vs[buf][NP - 1] + vo + dt * 32);
-            const s16x4 hi2 = ds_read_tr16(Vs[buf][NP - 1] + vo + 8 * VP + dt * 32);
+            const s16x4 hi2 = ds_read_tr16(Vs[buf][NP - 1] + vo + 8 * VPD + dt * 32);
             const bf16x8 al =
                 __builtin_bit_cast(bf16x8, s16x8{lo2[0], lo2[1], lo2[2], lo2[3], hi2[0], hi2[1], hi2[2], hi2[3]});
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, pf, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pfl, o, 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, pf, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pfl, o[dt], 0, 0, 0);
           }
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o, 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o[dt], 0, 0, 0);
         }
       }
     }
@@ -542,15 +564,15 @@ __global__ __launch_bounds__(256, 3) void attention_stream_kernel(const uint16_t
   const int qr = q0 + r;
   if (qr >= S) return;
   const float inv = 1.f / l;
-  uint16_t* orow = out + (rowbase + qr) * ldo + h * AT_D;
+  uint16_t* orow = out + (rowbase + qr) * ldo + h * HD;
   const long long oplane = rows * ldo;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
     const int d = 8 * g4 + 4 * hh;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const f32x16& o = half ? o1 : o0;
-      float w[4] = {o[4 * g4] * inv, o[4 * g4 + 1] * inv, o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv};
+    for (int half = 0; half < NDT; ++half) {
+      const f32x16& oh = o[half];
+      float w[4] = {oh[4 * g4] * inv, oh[4 * g4 + 1] * inv, oh[4 * g4 + 2] * inv, oh[4 * g4 + 3] * inv};
       uint16_t* dst = orow + 32 * half + d;
       if constexpr (SPLIT) {
         uint16_t hv[4], lv[4];
@@ -661,6 +683,12 @@ hipError_t softmax_rows(const uint16_t* x, uint16_t* y, float* y_f32, long long 
 
 bool attention_any_length() { return kAttnStream; }
 
+bool attention_supported(int D, int S) {
+  if (S <= 0) return false;
+  if (kAttnStream) return D == 32 || D == 64 || D == 96 || D == 128;
+  return D == AT_D && S <= 256;
+}
+
 namespace {
 int g_attn_variant = 0;  // 0: K/V staged one tile ahead, 1: two tiles ahead (DEEP)
 }
@@ -668,20 +696,27 @@ void set_attention_variant(int v) { g_attn_variant = v; }
 
 hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, int B, int S, int H,
                      int D, int ldq, int ldk, int ldv, int ldo, float scale, hipStream_t s, int split) {
-  if (D != AT_D || S <= 0 || (!kAttnStream && S > 256) || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4)
-    return hipErrorInvalidValue;
+  if (!attention_supported(D, S) || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;  // softmax in exp2
   if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S)
     dim3 grid((S + 127) / 128, H, B);
     const bool deep = g_attn_variant == 1;
-    if (split && deep)
-      hipLaunchKernelGGL((attention_stream_kernel<true, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else if (split)
-      hipLaunchKernelGGL((attention_stream_kernel<true, false>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else if (deep)
-      hipLaunchKernelGGL((attention_stream_kernel<false, true>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
-    else
-      hipLaunchKernelGGL((attention_stream_kernel<false, false>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, sl2);
+#define ATTN_LAUNCH(SP, DP, HDV)                                                                                   \
+  hipLaunchKernelGGL((attention_stream_kernel<SP, DP, HDV>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, \
+                     sl2)
+#define ATTN_HD(HDV)                          \
+  if (split && deep) ATTN_LAUNCH(true, true, HDV);    \
+  else if (split) ATTN_LAUNCH(true, false, HDV);      \
+  else if (deep) ATTN_LAUNCH(false, true, HDV);       \
+  else ATTN_LAUNCH(false, false, HDV);
+    switch (D) {
+      case 32: ATTN_HD(32) break;
+      case 64: ATTN_HD(64) break;
+      case 96: ATTN_HD(96) break;
+      default: ATTN_HD(128) break;
+    }
+#undef ATTN_HD
+#undef ATTN_LAUNCH
     return hipGetLastError();
   }
   dim3 grid(1, H, B);  // one 8-wave block per (image, head): wave w = query tile w (S <= 256)

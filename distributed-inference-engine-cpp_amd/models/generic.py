@@ -29,6 +29,8 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
 * `ln_wide`    LayerNormalization over 20 features (stored with 24: pad columns out of the
               statistics) and over 2560 features (wider than the register-resident kernels hold).
 * `bert_long`  the `bert` encoder at 320 tokens: attention past 256 keys (streaming kernel).
+* `bert_hd32`, `bert_hd128`  the `bert` encoder with head dim 32 (4 heads of 128 features, 40 tokens)
+              and 128 (2 heads of 256 features, 24 tokens).
 `synthetic_input(model, batch)` gives inputs of the right shape.  The CPU executor is the fp32
 oracle for all of them (tests/test_gpu_general.py).
 """
@@ -51,6 +53,8 @@ SPECS = {
     "token_mixer": dict(seq=24, dim=40, classes=10),
     "ln_wide": dict(seq=6, dim=20, wide=2560, classes=10),
     "bert_long": dict(seq=320, dim=128, heads=2, ffn=256, layers=1, classes=3),
+    "bert_hd32": dict(seq=40, dim=128, heads=4, ffn=256, layers=2, classes=3),
+    "bert_hd128": dict(seq=24, dim=256, heads=2, ffn=512, layers=2, classes=3),
 }
 
 
@@ -357,7 +361,9 @@ def build_ln_wide(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.n
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
             "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer,
             "ln_wide": build_ln_wide,
-            "bert_long": lambda seed=0: build_bert(seed, spec="bert_long")}
+            "bert_long": lambda seed=0: build_bert(seed, spec="bert_long"),
+            "bert_hd32": lambda seed=0: build_bert(seed, spec="bert_hd32"),
+            "bert_hd128": lambda seed=0: build_bert(seed, spec="bert_hd128")}
 
 
 def build_onnx(name: str, seed: int = 0) -> bytes:
@@ -368,7 +374,7 @@ def input_shape(name: str):
     s = SPECS[name]
     if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
-    if name in ("bert", "bert_long", "token_mixer", "ln_wide"):
+    if name in ("bert", "bert_long", "bert_hd32", "bert_hd128", "token_mixer", "ln_wide"):
         return (s["seq"] * s["dim"],)
     return (s["in_ch"], s["image"], s["image"])
 

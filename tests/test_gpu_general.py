@@ -13,7 +13,8 @@ from conftest import gpu_available
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long",
+           "bert_hd32", "bert_hd128"]
 
 
 @pytest.fixture(scope="module")

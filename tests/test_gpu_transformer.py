@@ -92,9 +92,51 @@ def test_attention_rejects_bad_shapes(K):
 
     from die_amd import native
 
-    x = torch.zeros(1, 64, 96, device="cuda", dtype=torch.bfloat16)  # 2 heads of 48: head dim must be 64
+    x = torch.zeros(1, 64, 96, device="cuda", dtype=torch.bfloat16)  # 2 heads of 48: not a supported head dim
     with pytest.raises(native.NativeError):
         K.attention(x, x, x, 2)
+
+
+@pytest.mark.parametrize("D", [32, 96, 128])
+@pytest.mark.parametrize("S", [17, 197, 300])
+def test_attention_head_dims(K, D, S):
+    """The streaming kernel takes head dims 32, 64, 96 and 128 (HD/16 k-steps of K Q^T, HD/32
+    output accumulators): bf16 against torch, and fp32 (split) against float64 at rel 1e-5."""
+    import torch
+
+    g = torch.Generator(device="cuda").manual_seed(S * 7 + D)
+    B, H = 2, 2
+    C = H * D
+    qkv = torch.randn(B, S, 3 * C, device="cuda", generator=g)
+    qb = qkv.bfloat16()
+    q, k, v = qb[..., :C], qb[..., C:2 * C], qb[..., 2 * C:]
+    scale = 1.0 / math.sqrt(D)
+    out = K.attention(q, k, v, H, scale)
+    assert rel_l2(out, _attn_ref(q, k, v, H, scale)) < 2e-2
+    got = K.attention_qkv_split(qkv, H, scale)
+    qd, kd, vd = (qkv[..., i * C:(i + 1) * C].double().reshape(B, S, H, D).transpose(1, 2) for i in range(3))
+    ref = (torch.softmax(qd @ kd.transpose(-1, -2) * scale, -1) @ vd).transpose(1, 2).reshape(B, S, C)
+    err = float((got.double() - ref).norm() / ref.norm())
+    assert err <= 1e-5, err
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_deep_variant_bitwise(K, D):
+    """Variant 1 (K/V staged two tiles ahead) computes the same tiles in the same order."""
+    import torch
+
+    g = torch.Generator(device="cuda").manual_seed(D)
+    B, S, H = 3, 197, 2
+    C = H * D
+    qkv = torch.randn(B, S, 3 * C, device="cuda", generator=g)
+    try:
+        K.set_attention_variant(0)
+        a = K.attention_qkv_split(qkv, H)
+        K.set_attention_variant(1)
+        b = K.attention_qkv_split(qkv, H)
+    finally:
+        K.set_attention_variant(0)
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("S", [300, 520])

@@ -8,7 +8,8 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long"]
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long",
+           "bert_hd32", "bert_hd128"]
 
 
 @pytest.fixture(scope="module")
