@@ -99,6 +99,7 @@ EngineOptions engine_opts(const Json& j) {
   e.fuse_pairs = jget<bool>(j, "fuse_pairs", e.fuse_pairs);
   e.fuse_stem_pool = jget<bool>(j, "fuse_stem_pool", e.fuse_stem_pool);
   e.fuse_gap_fc = jget<bool>(j, "fuse_gap_fc", e.fuse_gap_fc);
+  e.fold_layernorm = jget<bool>(j, "fold_layernorm", e.fold_layernorm);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));

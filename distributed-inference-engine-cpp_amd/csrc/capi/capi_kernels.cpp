@@ -291,11 +291,11 @@ char* die_hybrid_partition(const char* model_path, int max_batch, int split, cha
   }
 }
 
-// fuse: bit 0 conv pairs, bit 1 stem + pool, bit 2 global pool + FC head
+// fuse: bit 0 conv pairs, bit 1 stem + pool, bit 2 global pool + FC head, bit 3 LayerNorm folding
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse, char** err) {
   try {
     Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, (fuse & 1) != 0,
-                        (fuse & 2) != 0, (fuse & 4) != 0);
+                        (fuse & 2) != 0, (fuse & 4) != 0, (fuse & 8) != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -338,7 +338,9 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["relu2"] = o.conv.relu2;
         e["act"] = o.conv.relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
+        e["layernorm_folded"] = o.colsum_off != SIZE_MAX;
       }
+      if (o.kind == PlanOp::LAYERNORM) e["stats_only"] = o.stats_only != 0;
       if (o.kind == PlanOp::STEM) {
         e["pool_fused"] = o.is_max != 0;
         e["rows"] = o.is_max ? o.Ho * o.Wo : o.conv.Ho * o.conv.Wo;

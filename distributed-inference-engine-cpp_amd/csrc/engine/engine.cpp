@@ -291,6 +291,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["fuse_pairs"] = o.fuse_pairs;
   j["fuse_stem_pool"] = o.fuse_stem_pool;
   j["fuse_gap_fc"] = o.fuse_gap_fc;
+  j["fold_layernorm"] = o.fold_layernorm;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;

@@ -229,6 +229,7 @@ struct EngineOptions {
   bool fuse_pairs = true;         // expand conv + next reduce conv -> one CONV_PAIR launch (kernels/conv_pair.hip)
   bool fuse_stem_pool = true;     // stem conv + max pool (+ its BN/ReLU) -> one launch (kernels/stem.hip)
   bool fuse_gap_fc = true;        // global pool + the FC head reading it -> one launch (kernels/misc.hip)
+  bool fold_layernorm = false;    // LayerNorm -> GEMM readers: statistics only, the normalisation in the GEMM epilogue
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
   // autotune: take the fastest in-kernel (fused) split-K candidate when it is within this fraction

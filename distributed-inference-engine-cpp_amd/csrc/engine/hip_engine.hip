@@ -64,7 +64,7 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
     plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
-                       opt.fuse_pairs, opt.fuse_stem_pool, opt.fuse_gap_fc);
+                       opt.fuse_pairs, opt.fuse_stem_pool, opt.fuse_gap_fc, opt.fold_layernorm);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -839,6 +839,8 @@ class HipEngine : public Engine {
     a.in_scale = prm_ptr(op.in_scale_off);
     a.in_shift = prm_ptr(op.in_shift_off);
     a.in_relu = op.in_relu;
+    a.row_stats = op.in3 >= 0 ? static_cast<const float*>(buf_ptr(op.in3, s)) : nullptr;
+    a.col_sum = prm_ptr(op.colsum_off);
     return a;
   }
 
@@ -1168,9 +1170,14 @@ class HipEngine : public Engine {
                                  op.conv.relu, st, live, sp_);
           break;
         case PlanOp::LAYERNORM:
-          e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
-                                   prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_,
-                                   op.Cp);
+          if (op.stats_only)
+            e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), nullptr, prm(op.scale_off),
+                                     prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_, op.Cp, 0,
+                                     static_cast<float*>(buf(op.out)));
+          else
+            e = kern::layernorm_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)),
+                                     prm(op.scale_off), prm(op.shift_off), op.eps, op.rows_per_sample * B, op.C, st, sp_,
+                                     op.Cp);
           break;
         case PlanOp::TOKENS:
           e = kern::tokens_assemble(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),

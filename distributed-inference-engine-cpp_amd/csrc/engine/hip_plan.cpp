@@ -29,6 +29,13 @@ uint16_t to_bf16(float f) {
 
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+float from_bf16(uint16_t h) {
+  const uint32_t u = static_cast<uint32_t>(h) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
 constexpr int64_t kBatchDim = INT64_MIN;  // symbolic batch size inside SHAPE values
 
 // A planner value.  Besides materialised tensors (NHWC images, bf16/f32 rows) the planner keeps
@@ -80,9 +87,10 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 class Planner {
  public:
   Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true,
-          bool fuse_stem_pool = true, bool fuse_gap_fc = true)
+          bool fuse_stem_pool = true, bool fuse_gap_fc = true, bool fold_layernorm = false)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
-        fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool), fuse_gap_fc_(fuse_gap_fc) {}
+        fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool), fuse_gap_fc_(fuse_gap_fc),
+        fold_layernorm_(fold_layernorm) {}
 
   // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
   // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
@@ -125,6 +133,7 @@ class Planner {
     if (fuse_stem_pool_) fuse_stem_pool();
     if (fuse_pairs_) fuse_conv_pairs();
     if (fuse_gap_fc_) fuse_gap_fc();
+    if (fold_layernorm_) fold_layernorm();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
@@ -2415,6 +2424,83 @@ class Planner {
     plan_.ops = std::move(out);
   }
 
+  // LayerNorm -> GEMMs (ViT / BERT pre-norm blocks: the norm feeds the QKV or the first MLP GEMM
+  // only).  LN(x) W + b = rstd (x (gamma W) - mean colsum(gamma W)) + (beta W + b) per row, so the
+  // GEMMs read x itself with gamma folded into their weights, beta into their bias, and apply the
+  // per-row (mean, rstd) in the epilogue (ConvArgs::row_stats); the LayerNorm only computes the
+  // statistics -- the normalised rows are never written or read.  Exact in real arithmetic; in
+  // fp32 the error grows with |mean| / std of a row (ViT residual rows: mean ~ 0).
+  double weight_at(size_t w_off, long long plane, int kpad, int n, int k) const {
+    const uint16_t* w = reinterpret_cast<const uint16_t*>(plan_.params.data() + w_off);
+    const size_t i = static_cast<size_t>(n) * kpad + k;
+    double v = from_bf16(w[i]);
+    if (plane > 0) v += from_bf16(w[i + plane]);
+    return v;
+  }
+  void set_weight(size_t w_off, long long plane, int kpad, int n, int k, float v) {
+    uint16_t* w = reinterpret_cast<uint16_t*>(plan_.params.data() + w_off);
+    const size_t i = static_cast<size_t>(n) * kpad + k;
+    const uint16_t hi = to_bf16(v);
+    w[i] = hi;
+    if (plane > 0) w[i + plane] = to_bf16(v - static_cast<float>(from_bf16(hi)));
+  }
+  void fold_layernorm() {
+    const int nops = static_cast<int>(plan_.ops.size());
+    std::vector<std::vector<int>> readers(plan_.bufs.size());
+    for (int i = 0; i < nops; ++i)
+      for (int b : {plan_.ops[i].in, plan_.ops[i].in2, plan_.ops[i].in3})
+        if (b >= 0) readers[b].push_back(i);
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      if (p.kind != PlanOp::LAYERNORM || p.stats_only || p.out < 0 || p.in < 0 || p.C != p.Cp || p.join >= 0 ||
+          readers[p.out].empty())
+        continue;
+      bool ok = true;
+      for (int j : readers[p.out]) {
+        const PlanOp& q = plan_.ops[j];
+        const kern::ConvArgs& c = q.conv;
+        ok = ok && j > i && q.kind == PlanOp::CONV && q.in == p.out && q.in2 != p.out && q.in3 < 0 && q.join < 0 &&
+             q.in_scale_off == SIZE_MAX && c.KH == 1 && c.KW == 1 && c.stride == 1 && c.pad_h == 0 && c.pad_w == 0 &&
+             c.K == p.C && c.Cin == p.C && c.Kpad == c.K && c.Ho * c.Wo == p.rows_per_sample;
+      }
+      if (!ok) continue;
+      const float* gamma = reinterpret_cast<const float*>(plan_.params.data() + p.scale_off);
+      const float* beta = reinterpret_cast<const float*>(plan_.params.data() + p.shift_off);
+      const std::vector<float> g(gamma, gamma + p.C), be(beta, beta + p.C);
+      const int stats = new_buf(static_cast<size_t>(p.rows_per_sample) * 2 * 4);
+      for (int j : readers[p.out]) {
+        PlanOp& q = plan_.ops[j];
+        const kern::ConvArgs& c = q.conv;
+        const int Npad = static_cast<int>(round_up(c.N, 128));
+        std::vector<float> bias(Npad, 0.f), colsum(round_up(c.N, 8), 0.f);
+        if (q.bias_off != SIZE_MAX) {
+          const float* b0 = reinterpret_cast<const float*>(plan_.params.data() + q.bias_off);
+          std::copy(b0, b0 + c.N, bias.begin());
+        }
+        for (int n = 0; n < c.N; ++n) {
+          double bsum = bias[n], csum = 0.0;
+          for (int k = 0; k < c.K; ++k) {
+            const double w = weight_at(q.w_off, c.wplane, c.Kpad, n, k);
+            bsum += static_cast<double>(be[k]) * w;
+            set_weight(q.w_off, c.wplane, c.Kpad, n, k, static_cast<float>(w * g[k]));
+            csum += weight_at(q.w_off, c.wplane, c.Kpad, n, k);  // what the GEMM multiplies by
+          }
+          bias[n] = static_cast<float>(bsum);
+          colsum[n] = static_cast<float>(csum);
+        }
+        bias.resize(round_up(c.N, 8));
+        q.bias_off = push_f32(bias);
+        q.colsum_off = push_f32(colsum);
+        q.conv.bias = nullptr;
+        q.in = p.in;
+        q.in3 = stats;
+        q.name = p.name + "+" + q.name;
+      }
+      p.stats_only = 1;
+      p.out = stats;
+    }
+  }
+
   // Back-to-back 1x1 pair (ResNet-v2 bottleneck boundary).  A dual-store expand conv P writes the
   // raw sum x (next residual) and a = act(bn(x)); when a's ONLY reader is a plain 1x1/s1 reduce conv
   // Q, both become one CONV_PAIR op at P's position (Q has no other input, so computing it early is
@@ -2598,6 +2684,7 @@ class Planner {
   bool fuse_pairs_ = true;   // EngineOptions::fuse_pairs
   bool fuse_stem_pool_ = true;  // EngineOptions::fuse_stem_pool
   bool fuse_gap_fc_ = true;     // EngineOptions::fuse_gap_fc
+  bool fold_layernorm_ = false;  // EngineOptions::fold_layernorm
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -2698,12 +2785,14 @@ onnx::Model rewrite_conv_transpose(const onnx::Model& src) {
 }  // namespace
 
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs,
-                bool fuse_stem_pool, bool fuse_gap_fc) {
+                bool fuse_stem_pool, bool fuse_gap_fc, bool fold_layernorm) {
   if (has_conv_transpose(m)) {
     const onnx::Model r = rewrite_conv_transpose(m);
-    return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc).run();
+    return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc,
+                   fold_layernorm).run();
   }
-  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc).run();
+  return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc,
+                 fold_layernorm).run();
 }
 
 std::string PlanReport::text() const {

@@ -93,6 +93,12 @@ struct PlanOp {
   size_t w2_off = 0, bias2_off = SIZE_MAX;
   long long w2plane = 0;
   int n2 = 0, pair_relu = 0;
+  // LayerNorm folded into its GEMM readers (EngineOptions::fold_layernorm): the LAYERNORM op has
+  // stats_only = 1 and out = a [rows][2] f32 (mean, rstd) buffer; each reading CONV has in = the
+  // LayerNorm's input, in3 = that statistics buffer, gamma folded into its weights, beta into its
+  // bias and colsum_off = the per-column sums of its weights (ConvArgs::row_stats / col_sum).
+  int stats_only = 0;
+  size_t colsum_off = SIZE_MAX;
 };
 
 struct Plan {
@@ -117,8 +123,10 @@ struct Plan {
 // fuse_pairs: lower expand -> reduce 1x1 conv pairs to CONV_PAIR ops (EngineOptions::fuse_pairs).
 // fuse_stem_pool: stem conv + max pool in one STEM op (EngineOptions::fuse_stem_pool).
 // fuse_gap_fc: global pool + the FC head reading it in one GAP_FC op (EngineOptions::fuse_gap_fc).
+// fold_layernorm: LayerNorms read only by GEMMs become statistics ops (EngineOptions::fold_layernorm).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
-                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = true);
+                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = true,
+                bool fold_layernorm = false);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

@@ -49,6 +49,13 @@ __device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byt
 __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
   const size_t o = static_cast<size_t>(m) * p.N + n;
   const bool split = p.split != 0;
+  if (p.row_stats) {
+    const float mean = p.row_stats[2 * static_cast<size_t>(m)], rstd = p.row_stats[2 * static_cast<size_t>(m) + 1];
+    const float4 c0 = ldf4(p.col_sum + n), c1 = ldf4(p.col_sum + n + 4);
+    const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = rstd * (v[t] - mean * cs[t]);
+  }
   if (p.bias) {
     const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
     v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
@@ -399,7 +406,10 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
       for (int r = 0; r < 4; ++r) {
         if (n + r >= p.N) break;
         const size_t o = static_cast<size_t>(m) * p.N + n + r;
-        float v = acc[i][j][r] + (p.bias ? p.bias[n + r] : 0.f);
+        float v = acc[i][j][r];
+        if (p.row_stats)
+          v = p.row_stats[2 * static_cast<size_t>(m) + 1] * (v - p.row_stats[2 * static_cast<size_t>(m)] * p.col_sum[n + r]);
+        v += p.bias ? p.bias[n + r] : 0.f;
         if (p.res) v += load1v(p.res + o, p.oplane, p.split);
         if (p.relu) v = act_fn(v, p.relu, p.clip_lo, p.clip_hi);
         if (p.out) store1v(p.out + o, p.oplane, p.split, v);

@@ -54,6 +54,11 @@ struct ConvArgs {
   int in_relu = 0;
   // relu == 3: Clip(clip_lo, clip_hi) (ReLU6 = Clip(0, 6)) instead of ReLU / GELU
   float clip_lo = 0.f, clip_hi = 0.f;
+  // LayerNorm folded into the GEMM (rows GEMMs): x is the LayerNorm INPUT, the weights carry gamma,
+  // and before the bias v = rstd[m] * (v - mean[m] * col_sum[n]); row_stats = [M][2] (mean, rstd)
+  // from layernorm_rows' stats mode, col_sum[n] = sum_k of the (gamma-scaled) weight row n.
+  const float* row_stats = nullptr;
+  const float* col_sum = nullptr;
   // fp32 mode (common.h "split" tensors): x, res, out and out2 are split (hi, lo) bf16 planes and w
   // holds the weights' hi plane followed by their lo plane `wplane` elements later.  The planes of
   // the activations follow from the shapes (x: B*H*W*Cin, res/out/out2: M*N; the launcher fills
@@ -294,8 +299,11 @@ bool attention_any_length();
 bool attention_supported(int D, int S);
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.
+// stats != nullptr: statistics mode -- (mean, rstd) of each row to stats[2 row], 2 row + 1 and y is
+// not written (the normalisation is folded into the consuming GEMM: ConvArgs::row_stats).
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split = 0, int Cl = 0, int variant = 0);
+                          long long rows, int C, hipStream_t s, int split = 0, int Cl = 0, int variant = 0,
+                          float* stats = nullptr);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
                            int C, hipStream_t s, int split = 0);

@@ -34,10 +34,13 @@ __device__ __forceinline__ float group_sum(float v) {
 // statistics run over the first Cl (logical) columns and the pad columns are written 0.  C = 768
 // (ViT-B) runs as 32 lanes x 3 chunks: every lane busy and two rows' loads in flight per wave (one
 // row per wave with 64 x 2 chunks left half the lanes idle in the second round).
+// stats != nullptr: statistics mode -- (mean, rstd) per row to stats[2 row], y is not written (the
+// normalisation is folded into the consuming GEMM, ConvArgs::row_stats).
 template <int CPL, int LPR = 64>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         const float* __restrict__ g, const float* __restrict__ b,
-                                                        float eps, long long rows, int C, int split, int Cl) {
+                                                        float eps, long long rows, int C, int split, int Cl,
+                                                        float* __restrict__ stats) {
   constexpr int RPB = 256 / LPR;  // rows per block
   const int lane = threadIdx.x & (LPR - 1);
   const long long row = static_cast<long long>(blockIdx.x) * RPB + (threadIdx.x / LPR);
@@ -79,6 +82,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
       }
     }
   const float inv = rsqrtf(group_sum<LPR>(q2) / Cl + eps);
+  if (stats) {
+    if (lane == 0) *reinterpret_cast<float2*>(stats + 2 * row) = make_float2(mean, inv);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + LPR * i;
@@ -97,7 +104,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
 // reductions through LDS.
 __global__ __launch_bounds__(256) void layernorm_wide_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                              const float* __restrict__ g, const float* __restrict__ b,
-                                                             float eps, long long rows, int C, int split, int Cl) {
+                                                             float eps, long long rows, int C, int split, int Cl,
+                                                             float* __restrict__ stats) {
   __shared__ float red[8];
   const long long row = blockIdx.x;
   const long long plane = rows * C;
@@ -129,6 +137,10 @@ __global__ __launch_bounds__(256) void layernorm_wide_kernel(const uint16_t* __r
     }
   }
   const float inv = rsqrtf(block_sum(q2) / Cl + eps);
+  if (stats) {
+    if (tid == 0) *reinterpret_cast<float2*>(stats + 2 * row) = make_float2(mean, inv);
+    return;
+  }
   for (int c = tid; c < nch; c += 256) {
     float v[8];
     load8v(xr + c * 8, plane, split != 0, v);
@@ -625,35 +637,36 @@ inline int grid_for(long long work, int cap = 4096) {
 }  // namespace
 
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
-                          long long rows, int C, hipStream_t s, int split, int Cl, int variant) {
+                          long long rows, int C, hipStream_t s, int split, int Cl, int variant, float* stats) {
+  if (!stats && !y) return hipErrorInvalidValue;
   if (C % 8 || Cl < 0 || Cl > C || variant < 0 || variant > 2) return hipErrorInvalidValue;
   if (Cl == 0) Cl = C;
   const int blocks = static_cast<int>((rows + 3) / 4);
   if (variant == 1) {
     if (C > 16 * 8 * 6) return hipErrorInvalidValue;
     hipLaunchKernelGGL((layernorm_kernel<6, 16>), dim3(static_cast<int>((rows + 15) / 16)), dim3(256), 0, s, x, y, gamma,
-                       beta, eps, rows, C, split, Cl);
+                       beta, eps, rows, C, split, Cl, stats);
     return hipGetLastError();
   }
   if (variant == 2) {
     hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
-                       rows, C, split, Cl);
+                       rows, C, split, Cl, stats);
     return hipGetLastError();
   }
   if (C > 512 && C <= 32 * 8 * 3) {  // 513..768 (ViT-B: 768): 32 lanes x 3 chunks, 2 rows per wave
     hipLaunchKernelGGL((layernorm_kernel<3, 32>), dim3(static_cast<int>((rows + 7) / 8)), dim3(256), 0, s, x, y, gamma,
-                       beta, eps, rows, C, split, Cl);
+                       beta, eps, rows, C, split, Cl, stats);
     return hipGetLastError();
   }
   if (C <= 64 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+    hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
   else if (C <= 128 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+    hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
   else if (C <= 256 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl);
+    hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
   else
     hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
-                       rows, C, split, Cl);
+                       rows, C, split, Cl, stats);
   return hipGetLastError();
 }
 

@@ -223,3 +223,38 @@ def test_vit_base_engine_vs_torch(native, models):
     assert err < 1e-4, err  # fp32 engine (default precision)
     assert (got.argmax(1) == ref.argmax(1)).all()
     e.close()
+
+
+@pytest.mark.parametrize("size", ["tiny", "base"])
+def test_vit_fold_layernorm_vs_torch(native, models, size):
+    """EngineOptions::fold_layernorm: every pre-norm LayerNorm computes row statistics only and the
+    QKV / first-MLP GEMMs read the residual rows with gamma folded into their weights, beta into
+    their bias and (mean, rstd) applied in the epilogue -- same accuracy bar as the unfolded engine
+    (fp32 rel-L2 <= 1e-4 against torch, same top-1), in the autotuned and untuned paths."""
+    import torch
+
+    from die_amd.models import vit
+
+    path, w, cfg = models["get_vit"](size)
+    s = native.plan_summary(path, 8, precision="fp32", fold_layernorm=True)
+    assert sum(1 for o in s["ops"] if o.get("stats_only")) == 2 * cfg.depth
+    assert sum(1 for o in s["ops"] if o.get("layernorm_folded")) == 2 * cfg.depth
+    x = vit.synthetic_input(5, cfg)
+    with torch.no_grad():
+        ref = vit.torch_forward(w, x, cfg, device="cuda").cpu().numpy()
+    for autotune in ((False, True) if size == "tiny" else (False,)):
+        e = native.Engine(path, device="hip", max_batch=8, fold_layernorm=True, autotune=autotune)
+        try:
+            assert e.refresh_info()["options"]["fold_layernorm"] is True
+            got = e.run(x.reshape(5, -1))
+            err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+            assert err < 1e-4, (autotune, err)
+            assert (got.argmax(1) == ref.argmax(1)).all()
+        finally:
+            e.close()
+    e = native.Engine(path, device="hip", max_batch=8, precision="bf16", fold_layernorm=True, autotune=False)
+    try:
+        got = e.run(x.reshape(5, -1))
+        assert float(np.linalg.norm(got - ref) / np.linalg.norm(ref)) < 5e-2
+    finally:
+        e.close()

@@ -50,3 +50,26 @@ def test_vit_base_plan(native, models):
     # 86M parameters in bf16 (+ fp32 biases / LN params)
     assert 160e6 < p["param_bytes"] < 190e6
     assert abs(p["gflop_per_sample"] - 35.1) < 0.5
+
+
+def test_fold_layernorm_plan(native, tmp_path):
+    """fold_layernorm: ViT's pre-norm LayerNorms (each read only by a GEMM) become statistics ops and
+    their GEMMs read the residual rows; BERT's post-norm LayerNorms also feed residual adds, so they
+    stay (models/generic.py bert)."""
+    from die_amd.models import generic, vit
+
+    c = vit.tiny_vit_config()
+    p = str(tmp_path / "vit.onnx")
+    open(p, "wb").write(vit.build_onnx(c)[0])
+    plain = native.plan_summary(p, 8, precision="fp32")
+    folded = native.plan_summary(p, 8, precision="fp32", fold_layernorm=True)
+    stats = [o for o in folded["ops"] if o.get("stats_only")]
+    assert len(stats) == 2 * c.depth and not any(o.get("stats_only") for o in plain["ops"])
+    convs = [o for o in folded["ops"] if o.get("layernorm_folded")]
+    assert len(convs) == 2 * c.depth and all(o["name"].startswith("encoder.layer.") for o in convs)
+    # the statistics buffers are tiny: the folded arena is no larger
+    assert folded["arena_bytes"] <= plain["arena_bytes"]
+    b = str(tmp_path / "bert.onnx")
+    open(b, "wb").write(generic.build_onnx("bert"))
+    s = native.plan_summary(b, 8, precision="fp32", fold_layernorm=True)
+    assert not any(o.get("stats_only") for o in s["ops"])
