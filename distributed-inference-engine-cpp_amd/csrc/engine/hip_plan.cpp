@@ -922,7 +922,7 @@ class Planner {
     const Val& v = vals_[ctx.v];
     const int S = q.H, C = q.nh * q.hd;
     if (!kern::attention_supported(q.hd, S) || k.H != S || v.H != S)
-      throw std::runtime_error("attention " + name + ": needs head dim 32, 64, 96 or 128 (64 and <= 256 tokens " +
+      throw std::runtime_error("attention " + name + ": needs head dim 32, 64, 80, 96 or 128 (64 and <= 256 tokens " +
                                "without the streaming kernel)");
     PlanOp p;
     p.kind = PlanOp::ATTENTION;

@@ -294,8 +294,8 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // (default), 1 = two tiles ahead.
 void set_attention_variant(int v);
 bool attention_any_length();
-// Head dim / sequence length the attention launcher takes (streaming kernel: head dim 32, 64, 96
-// or 128, any length; the whole-K/V kernel: 64 and <= 256 tokens).
+// Head dim / sequence length the attention launcher takes (streaming kernel: head dim 32, 64, 80,
+// 96 or 128, any length; the whole-K/V kernel: 64 and <= 256 tokens).
 bool attention_supported(int D, int S);
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.

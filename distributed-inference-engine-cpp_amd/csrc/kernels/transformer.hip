@@ -391,16 +391,17 @@ __global__ __launch_bounds__(512) void attention_kernel(const uint16_t* __restri
 // DEEP: two register sets of staged K/V -- tile kt+2's loads are issued while tile kt computes and
 // tile kt+1 (loaded one step earlier) goes to LDS, so each load has two tiles of MFMAs to land
 // (+16 VGPRs; still 3 waves per SIMD at head dim 64).
-// HD: head dim 32, 64, 96 or 128 -- HD/16 k-steps of the K Q^T product, HD/32 output accumulators
-// (32 rows of D each) for O^T; K rows of HD/8 16-B chunks (XOR-swizzled when that is a power of two),
-// V rows padded to HD + 32.  Past 64 the registers allow 2 waves per SIMD (1 for split at 128).
+// HD: head dim 32, 64, 80, 96 or 128 -- HD/16 k-steps of the K Q^T product, ceil(HD/32) output
+// accumulators (32 rows of D each) for O^T (at 80 the third one's rows 80..95 read the V rows' pad
+// columns and are never stored); K rows of HD/8 16-B chunks (XOR-swizzled when that is a power of
+// two), V rows padded to HD + 32.  Past 64 the registers allow 2 waves per SIMD (1 for split at 128).
 template <int HD, bool SPLIT>
 struct AttnGeom {
   static constexpr int CPR = HD / 8;                             // 16-B chunks per K/V row
   static constexpr int SW = (CPR & (CPR - 1)) == 0 ? (CPR < 8 ? CPR - 1 : 7) : 0;  // K chunk swizzle mask
   static constexpr int VPD = HD + 32;                            // V row pitch (elements)
   static constexpr int LPT = (32 * CPR + 255) / 256;             // 16-B loads per thread per plane per tile
-  static constexpr int NKS = HD / 16, NDT = HD / 32;
+  static constexpr int NKS = HD / 16, NDT = (HD + 31) / 32;
   static constexpr int WAVES_PER_SIMD = HD > 96 && SPLIT ? 1 : (HD > 64 ? 2 : 3);
 };
 
@@ -583,6 +584,7 @@ __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void at
     const int d = 8 * g4 + 4 * hh;
 #pragma unroll
     for (int half = 0; half < NDT; ++half) {
+      if (32 * half + d >= HD) continue;  // head dim 80: the last accumulator's upper rows
       const f32x16& oh = o[half];
       float w[4] = {oh[4 * g4] * inv, oh[4 * g4 + 1] * inv, oh[4 * g4 + 2] * inv, oh[4 * g4 + 3] * inv};
       uint16_t* dst = orow + 32 * half + d;
@@ -698,7 +700,7 @@ bool attention_any_length() { return kAttnStream; }
 
 bool attention_supported(int D, int S) {
   if (S <= 0) return false;
-  if (kAttnStream) return D == 32 || D == 64 || D == 96 || D == 128;
+  if (kAttnStream) return D == 32 || D == 64 || D == 80 || D == 96 || D == 128;
   return D == AT_D && S <= 256;
 }
 
@@ -725,6 +727,7 @@ hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, ui
     switch (D) {
       case 32: ATTN_HD(32) break;
       case 64: ATTN_HD(64) break;
+      case 80: ATTN_HD(80) break;
       case 96: ATTN_HD(96) break;
       default: ATTN_HD(128) break;
     }

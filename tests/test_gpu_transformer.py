@@ -97,11 +97,11 @@ def test_attention_rejects_bad_shapes(K):
         K.attention(x, x, x, 2)
 
 
-@pytest.mark.parametrize("D", [32, 96, 128])
+@pytest.mark.parametrize("D", [32, 80, 96, 128])
 @pytest.mark.parametrize("S", [17, 197, 300])
 def test_attention_head_dims(K, D, S):
-    """The streaming kernel takes head dims 32, 64, 96 and 128 (HD/16 k-steps of K Q^T, HD/32
-    output accumulators): bf16 against torch, and fp32 (split) against float64 at rel 1e-5."""
+    """The streaming kernel takes head dims 32, 64, 80, 96 and 128 (HD/16 k-steps of K Q^T,
+    ceil(HD/32) output accumulators): bf16 against torch, and fp32 (split) against float64 at rel 1e-5."""
     import torch
 
     g = torch.Generator(device="cuda").manual_seed(S * 7 + D)
