@@ -171,7 +171,8 @@ def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int
 def build_random_rows(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int], List[str]]:
     """Random token-row graphs: input [N, S*D] reshaped to [N, S, D], then linear layers with
     activations, LayerNorm, residuals, gated units, data-dependent token mixing (softmax(h W) h: a
-    MatMul of two activations), channel split / concat, and a mean over tokens into a classifier.
+    MatMul of two activations), multi-head self-attention (head dim 32 / 64 / 80), channel split /
+    concat, and a mean over tokens into a classifier.
     -> (model bytes, input (S*D,), the block kinds used)."""
     rng = np.random.default_rng(10_000 + seed)
     S = int(rng.choice([5, 9, 16, 20]))
@@ -213,7 +214,7 @@ def build_random_rows(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int], Li
                       name=nm("ln"), axis=-1, epsilon=1e-5)
 
     for _ in range(blocks):
-        kind = str(rng.choice(["linear", "linear", "ln", "residual", "gate", "mix", "splitcat"]))
+        kind = str(rng.choice(["linear", "linear", "ln", "residual", "gate", "mix", "splitcat", "attn"]))
         if kind == "linear":
             d2 = int(rng.choice([16, 24, 32, 40, 48]))
             h, D = act(linear(h, D, d2)), d2
@@ -227,6 +228,25 @@ def build_random_rows(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int], Li
             a = g.node("Softmax", [g.node("MatMul", [h, g.init(nm("wm"), lin((D, S), D))], name=nm("ml"))],
                        name=nm("sm"), axis=-1)
             h = g.node("MatMul", [a, h], name=nm("mix"))
+        elif kind == "attn":
+            # multi-head self-attention in the torch export's form (Q/K/V linears, head Reshape +
+            # Transpose, MatMul -> Div -> Softmax -> MatMul, merge), head dim 32 / 64 / 80, then back
+            # to D with an output linear and a residual
+            hd = int(rng.choice([32, 64, 80]))
+            nh = int(rng.choice([1, 2]))
+            E = hd * nh
+            heads = g.const(np.array([0, 0, nh, hd], np.int64), nm("hs"))
+            merge = g.const(np.array([0, 0, E], np.int64), nm("ms"))
+            qh, kh, vh = (g.node("Reshape", [linear(h, D, E), heads], name=nm("heads")) for _ in range(3))
+            qh = g.node("Transpose", [qh], name=nm("qp"), perm=[0, 2, 1, 3])
+            kh = g.node("Transpose", [kh], name=nm("kp"), perm=[0, 2, 3, 1])
+            vh = g.node("Transpose", [vh], name=nm("vp"), perm=[0, 2, 1, 3])
+            sc = g.node("Div", [g.node("MatMul", [qh, kh], name=nm("scores")),
+                                g.const(np.array(math.sqrt(hd), np.float32), nm("c"))], name=nm("scale"))
+            sc = g.node("Softmax", [sc], name=nm("softmax"), axis=-1)
+            c = g.node("MatMul", [sc, vh], name=nm("context"))
+            c = g.node("Reshape", [g.node("Transpose", [c], name=nm("cp"), perm=[0, 2, 1, 3]), merge], name=nm("merge"))
+            h = g.node("Add", [h, linear(c, E, D)], name=nm("res"))
         elif kind == "splitcat":
             if D % 16:
                 continue

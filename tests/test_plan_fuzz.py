@@ -54,7 +54,7 @@ def test_rows_fuzz_covers_every_block_kind():
     kinds = set()
     for seed in SEEDS:
         kinds.update(fuzz.build_random_rows(seed)[2])
-    assert kinds >= {"linear", "ln", "residual", "gate", "mix", "splitcat"}, kinds
+    assert kinds >= {"linear", "ln", "residual", "gate", "mix", "splitcat", "attn"}, kinds
 
 
 def test_reshape_element_count_is_checked(native, tmp_path):
