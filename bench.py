@@ -97,11 +97,11 @@ def main():
                     help="pacing lead: 1 = measured input path + adaptive margin; other values = input path x this")
     ap.add_argument("--branch-streams", action="store_true",
                     help="run the projection-shortcut convs on a side stream (measured slower; off by default)")
-    ap.add_argument("--fold-layernorm", action="store_true",
-                    help="LayerNorms read only by GEMMs compute row statistics; the GEMM epilogue normalises "
+    ap.add_argument("--no-fold-layernorm", action="store_true",
+                    help="standalone LayerNorms instead of statistics + GEMM-epilogue normalisation "
                          "(EngineOptions::fold_layernorm)")
-    ap.add_argument("--no-fuse-gap-fc", action="store_true",
-                    help="keep the global pool and the FC head as two launches (EngineOptions::fuse_gap_fc)")
+    ap.add_argument("--fuse-gap-fc", action="store_true",
+                    help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true",
                     help="keep ResNet's stem conv and max pool as two launches (EngineOptions::fuse_stem_pool)")
     ap.add_argument("--no-fuse-pairs", action="store_true",
@@ -209,7 +209,7 @@ def main():
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
-                   "fuse_gap_fc": not args.no_fuse_gap_fc, "fold_layernorm": args.fold_layernorm}
+                   "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

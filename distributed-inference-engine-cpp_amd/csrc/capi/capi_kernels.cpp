@@ -161,6 +161,17 @@ int die_kern_gather_rows(uint64_t x, uint64_t y, int B, int Sq, int idx, int C, 
   return static_cast<int>(kern::gather_rows(P<const uint16_t>(x), P<uint16_t>(y), B, Sq, idx, C, S(stream), split));
 }
 
+void die_kern_set_gap_fc_stop(int v) { kern::set_gap_fc_stop(v); }
+
+int die_kern_gap_fc(uint64_t x, int B, int HW, int C, int mode, uint64_t w, long long wplane, int Kpad, uint64_t bias,
+                    int N, int act, uint64_t out, uint64_t ws, long long ws_bytes, uint64_t counters, int counters_n,
+                    uint64_t stream, int split) {
+  return static_cast<int>(kern::gap_fc(P<const uint16_t>(x), B, HW, C, mode, P<const uint16_t>(w), wplane, Kpad,
+                                       P<const float>(bias), N, act, P<float>(out), P<float>(ws),
+                                       static_cast<size_t>(ws_bytes), P<int>(counters), counters_n, S(stream), nullptr,
+                                       split));
+}
+
 void die_kern_set_attention_variant(int v) { kern::set_attention_variant(v); }
 
 int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,

@@ -228,8 +228,13 @@ struct EngineOptions {
   bool bn_on_load = false;        // bf16 plans: next unit's BN+ReLU applied on the 1x1 conv operand load
   bool fuse_pairs = true;         // expand conv + next reduce conv -> one CONV_PAIR launch (kernels/conv_pair.hip)
   bool fuse_stem_pool = true;     // stem conv + max pool (+ its BN/ReLU) -> one launch (kernels/stem.hip)
-  bool fuse_gap_fc = true;        // global pool + the FC head reading it -> one launch (kernels/misc.hip)
-  bool fold_layernorm = false;    // LayerNorm -> GEMM readers: statistics only, the normalisation in the GEMM epilogue
+  // global pool + the FC head reading it -> one launch (kernels/misc.hip gap_fc_kernel).  Off: at
+  // ResNet50's head (B = 20) the fused kernel's slice hand-off is slower than GAP + split-K GEMM
+  // (45.5 vs ~28.7 us, profiles/r4_gap_fc.md)
+  bool fuse_gap_fc = false;
+  // LayerNorm -> GEMM readers: statistics only, the normalisation in the GEMM epilogue (ViT-B/16
+  // B=32: 5,143 -> 5,075 us per forward on one box, profiles/r4_fold_layernorm.md)
+  bool fold_layernorm = true;
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
   // autotune: take the fastest in-kernel (fused) split-K candidate when it is within this fraction

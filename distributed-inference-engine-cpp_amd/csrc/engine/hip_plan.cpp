@@ -87,7 +87,7 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 class Planner {
  public:
   Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true,
-          bool fuse_stem_pool = true, bool fuse_gap_fc = true, bool fold_layernorm = false)
+          bool fuse_stem_pool = true, bool fuse_gap_fc = false, bool fold_layernorm = true)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
         fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool), fuse_gap_fc_(fuse_gap_fc),
         fold_layernorm_(fold_layernorm) {}
@@ -2683,8 +2683,8 @@ class Planner {
   bool bn_on_load_ = false;  // EngineOptions::bn_on_load (bf16 plans only)
   bool fuse_pairs_ = true;   // EngineOptions::fuse_pairs
   bool fuse_stem_pool_ = true;  // EngineOptions::fuse_stem_pool
-  bool fuse_gap_fc_ = true;     // EngineOptions::fuse_gap_fc
-  bool fold_layernorm_ = false;  // EngineOptions::fold_layernorm
+  bool fuse_gap_fc_ = false;    // EngineOptions::fuse_gap_fc
+  bool fold_layernorm_ = true;  // EngineOptions::fold_layernorm
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;

@@ -125,8 +125,8 @@ struct Plan {
 // fuse_gap_fc: global pool + the FC head reading it in one GAP_FC op (EngineOptions::fuse_gap_fc).
 // fold_layernorm: LayerNorms read only by GEMMs become statistics ops (EngineOptions::fold_layernorm).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
-                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = true,
-                bool fold_layernorm = false);
+                bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = false,
+                bool fold_layernorm = true);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

@@ -116,6 +116,7 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
 // one counter per group of 128 classes (counters_n available, left at 0).  gap_fc_slice: the
 // channel slice the launcher uses for this shape (0 = unsupported: C % 8, workspace too small).
 int gap_fc_slice(int C, int B, int N, size_t ws_bytes);
+void set_gap_fc_stop(int v);  // measurement only (tools/gap_fc_bench.py): phase at which blocks return
 constexpr size_t kSplitKWorkspaceBytes = size_t(64) << 20;  // the engine's split-K / GAP_FC workspace
 hipError_t gap_fc(const uint16_t* x, int B, int HW, int C, int mode, const uint16_t* w, long long wplane, int Kpad,
                   const float* bias, int N, int act, float* out, float* ws, size_t ws_bytes, int* counters,

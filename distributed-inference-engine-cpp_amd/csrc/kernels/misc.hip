@@ -177,17 +177,24 @@ __global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict_
 // a group to arrive (one agent-scope ticket per group, the hand-off of the fused split-K epilogue in
 // conv_igemm_impl.h) sums the slices in slice order -- deterministic -- adds the bias (+ ReLU) and
 // writes the fp32 logits.
-constexpr int kGfcRows = 64;   // samples per LDS chunk
+constexpr int kGfcRows = 32;   // samples per LDS chunk
 constexpr int kGfcCls = 128;   // classes per block: 2 threads per class, each half of the samples
+constexpr int kGfcPS = 4;      // pixel slices per (sample, 8-channel group) in the pooling
 constexpr int kCpolSc1Gfc = 16;
 
+// CS <= 64: a thread holds its class's CS weights in registers and finishes each sample's partial
+// in one pass (a 64-row accumulator array plus 64 weights spilled 6 KB per lane to scratch: 49 us of
+// a 73 us kernel).  The pooling splits each (sample, 8-channel group) over kGfcPS pixel slices whose
+// sums meet in LDS in slice order (deterministic).
 template <int CS>
 __global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict__ x, long long xplane, int HW, int C,
                                                      int mode, const uint16_t* __restrict__ w, long long wplane, int Kpad,
                                                      const float* __restrict__ bias, int N, int act,
                                                      float* __restrict__ out, float* ws, int* counters,
-                                                     const long long* __restrict__ live, int B, int split) {
-  __shared__ float pooled[kGfcRows][CS];
+                                                     const long long* __restrict__ live, int B, int split,
+                                                     int stop) {
+  static_assert(CS % 8 == 0 && CS <= 64, "channel slice");
+  __shared__ __attribute__((aligned(16))) float part[kGfcPS][kGfcRows][CS];
   __shared__ int flag;
   const int slice = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
   const int c0 = slice * CS, n0 = grp * kGfcCls;
@@ -198,57 +205,55 @@ __global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict_
   const float init = mode == 2 ? -INFINITY : 0.f;
   const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
   constexpr int GPR = CS / 8;
-  constexpr int JC = CS < 64 ? CS : 64;  // weights held in registers per pass
+  float wv[CS];  // this thread's class row of the weights (hi + lo), loaded once
+  if (n < N) {
+    const uint16_t* wr = w + static_cast<long long>(n) * Kpad + c0;
+#pragma unroll
+    for (int q = 0; q < GPR; ++q) load8v(wr + q * 8, wplane, split != 0, wv + q * 8);
+  }
   for (int b0 = 0; b0 < Bl; b0 += kGfcRows) {
     const int nb = min(kGfcRows, Bl - b0);
-    for (int it = tid; it < nb * GPR; it += 256) {
-      const int bi = it / GPR, g = it - bi * GPR;
+    // pooling: item = (sample, pixel slice, 8-channel group), the group fastest (128-B rows)
+    for (int it = tid; it < nb * GPR * kGfcPS; it += 256) {
+      const int g = it % GPR, rest = it / GPR, ps = rest % kGfcPS, bi = rest / kGfcPS;
       const uint16_t* src = x + static_cast<long long>(b0 + bi) * HW * C + c0 + g * 8;
       float acc[8] = {init, init, init, init, init, init, init, init};
-#pragma unroll 7
-      for (int p = 0; p < HW; ++p) {
+#pragma unroll 4
+      for (int p = ps; p < HW; p += kGfcPS) {
         float v[8];
         load8v(src + static_cast<long long>(p) * C, xplane, split != 0, v);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = mode == 2 ? fmaxf(acc[t], v[t]) : acc[t] + v[t];
       }
 #pragma unroll
-      for (int t = 0; t < 8; ++t) pooled[bi][g * 8 + t] = acc[t] * inv;
+      for (int t = 0; t < 8; ++t) part[ps][bi][g * 8 + t] = acc[t];
     }
     __syncthreads();
+    for (int e = tid; e < nb * CS; e += 256) {
+      const int bi = e / CS, j = e - bi * CS;
+      float v = part[0][bi][j];
+#pragma unroll
+      for (int ps = 1; ps < kGfcPS; ++ps) v = mode == 2 ? fmaxf(v, part[ps][bi][j]) : v + part[ps][bi][j];
+      part[0][bi][j] = v * inv;
+    }
+    __syncthreads();
+    if (stop == 1) return;
     if (n < N) {
-      float acc[kGfcRows / 2];
+      for (int bi = half; bi < nb; bi += 2) {
+        const float4* pr = reinterpret_cast<const float4*>(&part[0][bi][0]);
+        float s = 0.f;
 #pragma unroll
-      for (int r = 0; r < kGfcRows / 2; ++r) acc[r] = 0.f;
-      for (int j0 = 0; j0 < CS; j0 += JC) {
-        float wv[JC];
-        const uint16_t* wr = w + static_cast<long long>(n) * Kpad + c0 + j0;
-#pragma unroll
-        for (int q = 0; q < JC / 8; ++q) load8v(wr + q * 8, wplane, split != 0, wv + q * 8);
-#pragma unroll
-        for (int r = 0; r < kGfcRows / 2; ++r) {
-          const int bi = half + 2 * r;
-          if (bi >= nb) break;
-          const float4* pr = reinterpret_cast<const float4*>(&pooled[bi][j0]);
-          float s = 0.f;
-#pragma unroll
-          for (int q = 0; q < JC / 4; ++q) {
-            const float4 u = pr[q];
-            s += u.x * wv[4 * q] + u.y * wv[4 * q + 1] + u.z * wv[4 * q + 2] + u.w * wv[4 * q + 3];
-          }
-          acc[r] += s;
+        for (int q = 0; q < CS / 4; ++q) {
+          const float4 u = pr[q];
+          s += u.x * wv[4 * q] + u.y * wv[4 * q + 1] + u.z * wv[4 * q + 2] + u.w * wv[4 * q + 3];
         }
-      }
-#pragma unroll
-      for (int r = 0; r < kGfcRows / 2; ++r) {
-        const int bi = half + 2 * r;
-        if (bi >= nb) break;
         const unsigned off = static_cast<unsigned>(((static_cast<long long>(slice) * B + b0 + bi) * N + n) * 4);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[r]), wsr, off, 0, kCpolSc1Gfc);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), wsr, off, 0, kCpolSc1Gfc);
       }
     }
-    __syncthreads();  // pooled is rewritten by the next chunk
+    __syncthreads();  // part is rewritten by the next chunk
   }
+  if (stop == 2) return;
   // hand-off: every wave drains its write-through stores, one lane takes the group's ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -259,15 +264,68 @@ __global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict_
     flag = last;
   }
   __syncthreads();
-  if (!flag) return;
+  if (!flag || stop == 3) return;
+  // The slices' partials are summed in slice order, 8 slices' loads in flight at a time (a serial
+  // load -> add chain over 32 slices x 10 items per thread took 165 us at ResNet50's B = 20); with
+  // N % 4 == 0 each item is 4 consecutive classes (16-B loads and stores).
   const int ncls = min(kGfcCls, N - n0);
+  const int KS = static_cast<int>(gridDim.x);
+  const unsigned slab = static_cast<unsigned>(static_cast<long long>(B) * N * 4);  // bytes per slice
+  if ((N & 3) == 0) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int nq = ncls / 4;
+    for (int it = tid; it < Bl * nq; it += 256) {
+      const int bi = it / nq, nn = n0 + 4 * (it - bi * nq);
+      const unsigned base = static_cast<unsigned>((static_cast<long long>(bi) * N + nn) * 4);
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      int sl = 0;
+      for (; sl + 8 <= KS; sl += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wsr, base + (sl + u) * slab, 0,
+                                                                                  kCpolSc1Gfc));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc.x += v[u].x;
+          acc.y += v[u].y;
+          acc.z += v[u].z;
+          acc.w += v[u].w;
+        }
+      }
+      for (; sl < KS; ++sl) {
+        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wsr, base + sl * slab, 0,
+                                                                                          kCpolSc1Gfc));
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      float r[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (bias) r[t] += bias[nn + t];
+        if (act == 1) r[t] = fmaxf(r[t], 0.f);
+      }
+      *reinterpret_cast<float4*>(out + static_cast<long long>(bi) * N + nn) = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    return;
+  }
   for (int it = tid; it < Bl * ncls; it += 256) {
     const int bi = it / ncls, nn = n0 + (it - bi * ncls);
+    const unsigned base = static_cast<unsigned>((static_cast<long long>(bi) * N + nn) * 4);
     float s = 0.f;
-    for (int sl = 0; sl < static_cast<int>(gridDim.x); ++sl) {
-      const unsigned off = static_cast<unsigned>(((static_cast<long long>(sl) * B + bi) * N + nn) * 4);
-      s += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, off, 0, kCpolSc1Gfc));
+    int sl = 0;
+    for (; sl + 8 <= KS; sl += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, base + (sl + u) * slab, 0, kCpolSc1Gfc));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
+    for (; sl < KS; ++sl)
+      s += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, base + sl * slab, 0, kCpolSc1Gfc));
     if (bias) s += bias[nn];
     if (act == 1) s = fmaxf(s, 0.f);
     out[static_cast<long long>(bi) * N + nn] = s;
@@ -369,8 +427,13 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
 
 // Channel slice: the narrowest that divides C with at most 32 slices (ResNet50: 64 -> 32 x 8 =
 // 256 blocks), else the narrowest that divides C; the partials [C/cs][B][N] must fit `ws`.
+namespace {
+int g_gfc_stop = 0;  // measurement: 1 / 2 / 3 = return after the pooling / the partials / the ticket
+}
+void set_gap_fc_stop(int v) { g_gfc_stop = v; }
+
 int gap_fc_slice(int C, int B, int N, size_t ws_bytes) {
-  static const int kSlices[] = {8, 16, 32, 64, 128};
+  static const int kSlices[] = {8, 16, 32, 64};
   auto fits = [&](int cs) {
     const size_t bytes = static_cast<size_t>(C / cs) * B * N * 4;
     return C % cs == 0 && bytes <= ws_bytes && bytes < (size_t(1) << 31);
@@ -395,14 +458,13 @@ hipError_t gap_fc(const uint16_t* x, int B, int HW, int C, int mode, const uint1
 #define GAP_FC_CASE(CSV)                                                                                          \
   case CSV:                                                                                                        \
     hipLaunchKernelGGL(gap_fc_kernel<CSV>, grid, dim3(256), 0, s, x, xplane, HW, C, mode, w, wplane, Kpad, bias, N, \
-                       act, out, ws, counters, live, B, split);                                                    \
+                       act, out, ws, counters, live, B, split, g_gfc_stop);                                        \
     break;
   switch (cs) {
     GAP_FC_CASE(8)
     GAP_FC_CASE(16)
     GAP_FC_CASE(32)
     GAP_FC_CASE(64)
-    GAP_FC_CASE(128)
     default:
       return hipErrorInvalidValue;
   }

@@ -666,6 +666,11 @@ def _sig_kernels():
     L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64, i]
     L.die_kern_set_attention_variant.restype = None
     L.die_kern_set_attention_variant.argtypes = [i]
+    L.die_kern_set_gap_fc_stop.restype = None
+    L.die_kern_set_gap_fc_stop.argtypes = [i]
+    L.die_kern_gap_fc.restype = i
+    L.die_kern_gap_fc.argtypes = [u64] + [i] * 4 + [u64, C.c_longlong, i, u64, i, i, u64, u64, C.c_longlong, u64, i,
+                                                      u64, i]
     L.die_decode_scratch_bytes.restype = C.c_longlong
     L.die_decode_scratch_bytes.argtypes = [i, C.c_longlong]
     L.die_kern_decode.restype = i
@@ -678,7 +683,7 @@ def _sig_kernels():
 
 def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False,
                  precision: str = "bf16", fuse_pairs: bool = True, fuse_stem_pool: bool = True,
-                 fuse_gap_fc: bool = True, fold_layernorm: bool = False) -> Dict[str, Any]:
+                 fuse_gap_fc: bool = False, fold_layernorm: bool = True) -> Dict[str, Any]:
     """precision "fp32" plans the split (hi, lo) kernels of the HIP engine's default mode.
     fuse_pairs: expand + next reduce 1x1 convs as one conv_pair op (EngineOptions::fuse_pairs);
     fuse_stem_pool: stem conv + max pool as one stem op (EngineOptions::fuse_stem_pool);

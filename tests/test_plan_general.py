@@ -36,10 +36,8 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
     if name == "mlp":
         assert kinds[0] == "rows_prep" and "binary" in kinds and "unary" in kinds and kinds[-1] == "softmax"
     if name == "bert":
-        assert kinds[0] == "rows_prep" and kinds.count("attention") == 2 and "gap_fc" in kinds
-        # mean over tokens + the 3-class head (stored as 8 columns, then cast) -> one gap_fc op that
-        # writes the 3 f32 logits directly
-        assert kinds[-1] == "gap_fc" and "bf16_to_f32" not in kinds
+        assert kinds[0] == "rows_prep" and kinds.count("attention") == 2 and "gap" in kinds
+        assert kinds[-1] == "bf16_to_f32"  # 3 classes stored as 8 columns: the cast drops the pads
     if name == "se_cnn":
         assert kinds[0] == "input_prep" and "binary" in kinds and kinds.count("copy_cols") == 3
     if name == "ops_zoo":

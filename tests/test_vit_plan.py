@@ -53,7 +53,7 @@ def test_vit_base_plan(native, models):
 
 
 def test_fold_layernorm_plan(native, tmp_path):
-    """fold_layernorm: ViT's pre-norm LayerNorms (each read only by a GEMM) become statistics ops and
+    """fold_layernorm (default on): ViT's pre-norm LayerNorms (each read only by a GEMM) become statistics ops and
     their GEMMs read the residual rows; BERT's post-norm LayerNorms also feed residual adds, so they
     stay (models/generic.py bert)."""
     from die_amd.models import generic, vit
@@ -61,8 +61,8 @@ def test_fold_layernorm_plan(native, tmp_path):
     c = vit.tiny_vit_config()
     p = str(tmp_path / "vit.onnx")
     open(p, "wb").write(vit.build_onnx(c)[0])
-    plain = native.plan_summary(p, 8, precision="fp32")
-    folded = native.plan_summary(p, 8, precision="fp32", fold_layernorm=True)
+    plain = native.plan_summary(p, 8, precision="fp32", fold_layernorm=False)
+    folded = native.plan_summary(p, 8, precision="fp32")  # the default
     stats = [o for o in folded["ops"] if o.get("stats_only")]
     assert len(stats) == 2 * c.depth and not any(o.get("stats_only") for o in plain["ops"])
     convs = [o for o in folded["ops"] if o.get("layernorm_folded")]

@@ -20,8 +20,8 @@ def main():
     ap.add_argument("--tune-warm-input", action="store_true", help="autotune with each conv's producer run first")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0, help="prefer fused split-K within this fraction")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
-    ap.add_argument("--fold-layernorm", action="store_true", help="LayerNorm statistics + GEMM-epilogue normalisation (EngineOptions::fold_layernorm)")
-    ap.add_argument("--no-fuse-gap-fc", action="store_true", help="global pool and FC head as two launches (EngineOptions::fuse_gap_fc)")
+    ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
+    ap.add_argument("--fuse-gap-fc", action="store_true", help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true", help="stem and max pool as two launches (EngineOptions::fuse_stem_pool)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
@@ -43,7 +43,7 @@ def main():
     e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision,
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
                       splitk_fused_margin=a.splitk_fused_margin,
-                      fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=not a.no_fuse_gap_fc, fold_layernorm=a.fold_layernorm)
+                      fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm)
     p = e.profile(a.batch, a.iters)
     e.close()
     lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
