@@ -47,9 +47,13 @@ __global__ __launch_bounds__(256) void bmm_kernel(const uint16_t* __restrict__ A
       const int m = m0 + ar, k = k0 + ak;
       if (m < M && k < K) {
         av = *reinterpret_cast<const uint4*>(Ab + pl * aplane + static_cast<long long>(m) * lda + k);
-        if (k + 8 > K) {  // mask the columns past the logical K (pad columns)
-          uint16_t* e = reinterpret_cast<uint16_t*>(&av);
-          for (int t = K - k; t < 8; ++t) e[t] = 0;
+        if (k + 8 > K) {  // mask the columns past the logical K (pad columns), in registers
+          const int valid = K - k;
+          uint32_t wd[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            wd[q] &= (2 * q < valid ? 0x0000FFFFu : 0u) | (2 * q + 1 < valid ? 0xFFFF0000u : 0u);
+          av = make_uint4(wd[0], wd[1], wd[2], wd[3]);
         }
       }
       *reinterpret_cast<uint4*>(&As[pl][ar][ak]) = av;
