@@ -233,7 +233,7 @@ struct EngineOptions {
   // (45.5 vs ~28.7 us, profiles/r4_gap_fc.md)
   bool fuse_gap_fc = false;
   // LayerNorm -> GEMM readers: statistics only, the normalisation in the GEMM epilogue (ViT-B/16
-  // B=32: 5,143 -> 5,075 us per forward on one box, profiles/r4_fold_layernorm.md)
+  // B=32: 5,143 -> 5,075 us per forward on one box, profiles/r4_fold_layernorm.md); fp32 mode only
   bool fold_layernorm = true;
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing

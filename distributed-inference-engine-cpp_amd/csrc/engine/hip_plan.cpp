@@ -133,7 +133,9 @@ class Planner {
     if (fuse_stem_pool_) fuse_stem_pool();
     if (fuse_pairs_) fuse_conv_pairs();
     if (fuse_gap_fc_) fuse_gap_fc();
-    if (fold_layernorm_) fold_layernorm();
+    // fp32 (split) mode only: in bf16 the weights re-rounded with gamma folded in and the mean
+    // subtracted after a bf16-input GEMM cost ViT-B/16 ~3 % of its rel-L2 budget
+    if (fold_layernorm_ && split_) fold_layernorm();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();

@@ -252,9 +252,5 @@ def test_vit_fold_layernorm_vs_torch(native, models, size):
             assert (got.argmax(1) == ref.argmax(1)).all()
         finally:
             e.close()
-    e = native.Engine(path, device="hip", max_batch=8, precision="bf16", fold_layernorm=True, autotune=False)
-    try:
-        got = e.run(x.reshape(5, -1))
-        assert float(np.linalg.norm(got - ref) / np.linalg.norm(ref)) < 5e-2
-    finally:
-        e.close()
+    # bf16 mode plans without folding (fp32 mode only)
+    assert not any(o.get("stats_only") for o in native.plan_summary(path, 8, precision="bf16")["ops"])
