@@ -5,7 +5,8 @@ the CPU: every graph plans; tests/test_gpu_fuzz.py: every graph matches the fp32
 A graph is a chain of randomly chosen blocks on an NCHW image -- conv (1x1 / 3x3, stride 1 / 2,
 optional BN, one of several activations), residual add, squeeze-excitation gate, max / average
 pool, Pad + conv, nearest / linear resize, transposed conv, elementwise unary chains, channel
-concat + slice, Where / comparison masks -- then a global pool and a Gemm classifier.  Channel
+concat + slice, Where / comparison masks, inverted-residual blocks (1x1 expand, depthwise 3x3, SiLU
+as x * Sigmoid(x), 1x1 project) -- then a global pool and a Gemm classifier.  Channel
 counts include values that are not multiples of 8 where the planner allows them.  Deterministic in
 the seed.
 """
@@ -70,7 +71,7 @@ def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int
     used.append("stem")
     saved = [(h, C, H)]  # tensors a residual can join
     for _ in range(blocks):
-        kinds = ["conv", "conv", "residual", "se", "pool", "padconv", "unary", "concat", "where"]
+        kinds = ["conv", "conv", "residual", "se", "pool", "padconv", "unary", "concat", "where", "mbconv"]
         if H >= 8:
             kinds += ["down"]
         if H <= 12:
@@ -155,6 +156,19 @@ def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int
             h = g.node("Slice", [h, g.const(np.array([0], np.int64), nm("s0")), g.const(np.array([keep], np.int64), nm("s1")),
                                  g.const(np.array([1], np.int64), nm("ax"))], name=nm("slice"))
             C = keep if keep <= Cc else Cc
+        elif kind == "mbconv":  # inverted residual (MobileNetV2 / EfficientNet): 1x1 expand, depthwise 3x3, SiLU, 1x1 project
+            if C % 8:
+                continue
+            E = 2 * C
+
+            def silu(t):
+                return g.node("Mul", [t, g.node("Sigmoid", [t], name=nm("sg"))], name=nm("silu"))
+
+            e = silu(bn(conv(h, C, E, 1, 1, 0, bias=False), E))
+            wd = g.init(nm("dw"), lin((E, 1, 3, 3), 9))
+            d = g.node("Conv", [e, wd], name=nm("dwconv"), kernel_shape=[3, 3], strides=[1, 1], pads=[1, 1, 1, 1], group=E)
+            d = silu(bn(d, E))
+            h = g.node("Add", [h, bn(conv(d, E, C, 1, 1, 0, bias=False), C)], name=nm("res"))
         elif kind == "where":  # max(h, g(h)) through a comparison mask (continuous)
             other = g.node("Tanh", [h], name=nm("tanh"))
             h = g.node("Where", [g.node("Greater", [h, other], name=nm("gt")), h, other], name=nm("where"))

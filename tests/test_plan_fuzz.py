@@ -30,7 +30,7 @@ def test_fuzz_covers_every_block_kind():
     for seed in SEEDS:
         kinds.update(fuzz.build_random(seed)[2])
     assert kinds >= {"stem", "conv", "down", "residual", "se", "pool", "padconv", "resize", "convT", "unary", "concat",
-                     "where"}, kinds
+                     "where", "mbconv"}, kinds
 
 
 @pytest.mark.parametrize("seed", SEEDS)
