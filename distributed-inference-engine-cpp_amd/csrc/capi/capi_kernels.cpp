@@ -326,9 +326,9 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
       e["join"] = o.join;
       // arena ranges [offset, offset + bytes) at max_batch of the op's buffers, by role
       Json bufs = Json::object();
-      const char* roles[] = {"in", "in2", "in3", "out", "out2"};
-      const int ids[] = {o.in, o.in2, o.in3, o.out, o.out2};
-      for (int r = 0; r < 5; ++r)
+      const char* roles[] = {"in", "in2", "in3", "out", "out2", "out3"};
+      const int ids[] = {o.in, o.in2, o.in3, o.out, o.out2, o.out3};
+      for (int r = 0; r < 6; ++r)
         if (ids[r] >= 0) {
           Json range = Json::array();
           range.push_back(static_cast<long long>(p.bufs[ids[r]].offset));
@@ -362,6 +362,7 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["N2"] = o.n2;
         e["residual"] = o.in2 >= 0;
         e["store_main"] = o.out >= 0;
+        e["store_preact"] = o.out3 >= 0;
         e["relu"] = o.pair_relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
       }

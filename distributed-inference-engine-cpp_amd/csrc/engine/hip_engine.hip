@@ -903,7 +903,8 @@ class HipEngine : public Engine {
         if (opt_.tune_warm_input)
           for (int j = static_cast<int>(oi) - 1; j >= 0 && producer < 0; --j) {
             const PlanOp& q = plan_.ops[static_cast<size_t>(j)];
-            if ((q.out >= 0 && q.out == op.in) || (q.out2 >= 0 && q.out2 == op.in)) producer = j;
+            if ((q.out >= 0 && q.out == op.in) || (q.out2 >= 0 && q.out2 == op.in) || (q.out3 >= 0 && q.out3 == op.in))
+              producer = j;
           }
         // identical problems (repeated blocks) share one measurement
         char key[256];
@@ -1080,6 +1081,7 @@ class HipEngine : public Engine {
           a.bias1 = prm(op.bias_off);
           a.res = static_cast<const uint16_t*>(buf(op.in2));
           a.xout = static_cast<uint16_t*>(buf(op.out));
+          a.aout = static_cast<uint16_t*>(buf(op.out3));
           a.scale2 = prm(op.s2_off);
           a.shift2 = prm(op.b2_off);
           a.relu2 = op.conv.relu2;

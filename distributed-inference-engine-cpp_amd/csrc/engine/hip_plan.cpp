@@ -2523,30 +2523,39 @@ class Planner {
     return c.KH == 1 && c.KW == 1 && c.stride == 1 && c.pad_h == 0 && c.pad_w == 0 && c.dil == 1 && c.H == c.Ho &&
            c.W == c.Wo && c.K == c.Cin && c.Kpad == c.K;
   }
+  // With other readers of `a` (a stage boundary: the next stage's projection shortcut reads it
+  // too) the pair also stores a (PlanOp::out3) and those readers keep reading it.
   void fuse_conv_pairs() {
-    std::vector<int> readers(plan_.bufs.size(), 0), reader_op(plan_.bufs.size(), -1);
     const int nops = static_cast<int>(plan_.ops.size());
+    std::vector<std::vector<int>> readers(plan_.bufs.size());
     for (int i = 0; i < nops; ++i)
       for (int b : {plan_.ops[i].in, plan_.ops[i].in2, plan_.ops[i].in3})
-        if (b >= 0) {
-          readers[b]++;
-          reader_op[b] = i;
-        }
+        if (b >= 0) readers[b].push_back(i);
     std::vector<bool> drop(nops, false);
+    auto reduce_ok = [&](const PlanOp& p, const PlanOp& q) {
+      return q.kind == PlanOp::CONV && q.in == p.out2 && q.in2 < 0 && q.in3 < 0 && q.out >= 0 && q.out2 < 0 &&
+             q.out_f32 < 0 && q.conv.relu <= 1 && q.in_scale_off == SIZE_MAX && plain_1x1(q.conv) &&
+             q.conv.Cin == p.conv.N && q.conv.H == p.conv.Ho && q.conv.W == p.conv.Wo && q.join < 0 &&
+             kern::conv_pair_supported(p.conv.K, p.conv.N, q.conv.N);
+    };
     for (int i = 0; i < nops; ++i) {
       PlanOp& p = plan_.ops[i];
       if (p.kind != PlanOp::CONV || p.in2 < 0 || p.out2 < 0 || p.s2_off == SIZE_MAX || p.out_f32 >= 0 ||
           p.conv.relu != 0 || p.in_scale_off != SIZE_MAX || !plain_1x1(p.conv) || p.join >= 0)
         continue;
-      if (readers[p.out2] != 1) continue;
-      const int j = reader_op[p.out2];
-      if (j <= i || drop[j]) continue;
+      const std::vector<int>& rd = readers[p.out2];
+      int j = -1;
+      for (int r : rd)
+        if (r > i && !drop[r] && reduce_ok(p, plan_.ops[r])) {
+          j = r;
+          break;
+        }
+      if (j < 0) continue;
+      bool others_ok = true;  // every other reader runs after the pair (at P's position) and reads a as an input
+      for (int r : rd)
+        if (r != j && (r <= i || plan_.ops[r].join >= 0)) others_ok = false;
+      if (!others_ok) continue;
       const PlanOp& q = plan_.ops[j];
-      if (q.kind != PlanOp::CONV || q.in != p.out2 || q.in2 >= 0 || q.in3 >= 0 || q.out < 0 || q.out2 >= 0 ||
-          q.out_f32 >= 0 || q.conv.relu > 1 || q.in_scale_off != SIZE_MAX || !plain_1x1(q.conv) ||
-          q.conv.Cin != p.conv.N || q.conv.H != p.conv.Ho || q.conv.W != p.conv.Wo || q.join >= 0 ||
-          !kern::conv_pair_supported(p.conv.K, p.conv.N, q.conv.N))
-        continue;
       permute_weight_rows(p.w_off, static_cast<int>(round_up(p.conv.N, 128)), p.conv.Kpad, p.conv.wplane);
       permute_weight_rows(q.w_off, static_cast<int>(round_up(q.conv.N, 128)), q.conv.Kpad, q.conv.wplane);
       p.kind = PlanOp::CONV_PAIR;
@@ -2556,7 +2565,8 @@ class Planner {
       p.w2plane = q.conv.wplane;
       p.n2 = q.conv.N;
       p.pair_relu = q.conv.relu;
-      p.out2 = q.out;  // the pre-activation buffer is dropped (no op references it any more)
+      p.out3 = rd.size() > 1 ? p.out2 : -1;  // a stored for its other readers, else dropped
+      p.out2 = q.out;
       p.flops_per_sample += q.flops_per_sample;
       drop[j] = true;
     }
@@ -2630,9 +2640,9 @@ class Planner {
     const int nops = static_cast<int>(plan_.ops.size());
     for (int i = 0; i < nops; ++i) {
       const PlanOp& p = plan_.ops[i];
-      for (int b : {p.out, p.out2})
+      for (int b : {p.out, p.out2, p.out3})
         if (b >= 0 && plan_.bufs[b].first_use < 0) plan_.bufs[b].first_use = i;
-      for (int b : {p.in, p.in2, p.in3, p.out, p.out2})
+      for (int b : {p.in, p.in2, p.in3, p.out, p.out2, p.out3})
         if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, i);
       // a side branch may still be reading its inputs until its join
       if (p.join >= 0)

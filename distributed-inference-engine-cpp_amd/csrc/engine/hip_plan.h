@@ -60,6 +60,7 @@ struct PlanOp {
   std::string name;
   // buffers (-1 = none).  -2 = the graph input (f32 NCHW), -3 = the graph output (f32).
   int in = -1, in2 = -1, in3 = -1, out = -1, out2 = -1, out_f32 = -1;
+  int out3 = -1;  // CONV_PAIR: the pre-activation `a` when ops other than the fused reduce conv read it
   // parameter offsets (bytes) into the device parameter blob
   size_t w_off = 0, bias_off = SIZE_MAX, s2_off = SIZE_MAX, b2_off = SIZE_MAX, scale_off = SIZE_MAX,
          shift_off = SIZE_MAX;

@@ -233,6 +233,7 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
         u[t] = v[t] * ss[t] + hh[t];
         if (p.relu2) u[t] = fmaxf(u[t], 0.f);
       }
+      if (p.aout && pv[j]) store8v(p.aout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, u);
       const int row = wm * 32 + j * 16 + l16;
       uint4 hi, lo;
       if constexpr (SPLIT) {

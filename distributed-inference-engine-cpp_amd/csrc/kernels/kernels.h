@@ -221,6 +221,9 @@ struct PairArgs {
   const float* bias1 = nullptr;
   const uint16_t* res = nullptr;
   uint16_t* xout = nullptr;
+  // the pre-activation a = act2(x * scale2 + shift2) [M][N1], stored too when other ops read it
+  // (a stage boundary whose projection shortcut also reads a); nullptr: a stays in LDS only
+  uint16_t* aout = nullptr;
   const float* scale2 = nullptr;
   const float* shift2 = nullptr;
   int relu2 = 1;

@@ -128,7 +128,7 @@ def test_pair_bf16(native, shape):
 
 
 def test_engine_fused_pairs_match_unfused_plan(native, models):
-    """ResNet50-v2 fp32: the default plan (5 expand+reduce pairs fused) vs the unfused plan and torch
+    """ResNet50-v2 fp32: the default plan (6 expand+reduce pairs fused) vs the unfused plan and torch
     fp32, at a full and a partial batch bucket."""
     import numpy as np
 
@@ -139,8 +139,12 @@ def test_engine_fused_pairs_match_unfused_plan(native, models):
     ef = native.Engine(path, device="hip", max_batch=20, precision="fp32")
     eu = native.Engine(path, device="hip", max_batch=20, precision="fp32", fuse_pairs=False)
     try:
-        kinds = [o["kind"] for o in native.plan_summary(path, 20, precision="fp32")["ops"]]
-        assert kinds.count("conv_pair") == 5, kinds
+        ops = native.plan_summary(path, 20, precision="fp32")["ops"]
+        kinds = [o["kind"] for o in ops]
+        # 5 unit boundaries inside stages 1/2 + the stage-1 -> stage-2 boundary, whose pre-activation
+        # the stage-2 projection shortcut also reads (stored by the pair kernel: store_preact)
+        assert kinds.count("conv_pair") == 6, kinds
+        assert sum(1 for o in ops if o.get("store_preact")) == 1
         assert ef.refresh_info()["options"]["fuse_pairs"] is True
         for B in (20, 13):
             x = r.synthetic_input(B, cfg, seed=90 + B)
