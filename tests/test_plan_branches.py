@@ -18,7 +18,7 @@ def _check_branches(plan):
         for k in range(i + 1, j):
             mid = ops[k]["bufs"]
             assert all(side["out"] != mid.get(r) for r in ("in", "in2", "in3")), "op inside the branch reads it"
-            for wr in ("out", "out2"):  # concurrent writes never touch the branch's buffers
+            for wr in ("out", "out2", "out3"):  # concurrent writes never touch the branch's buffers
                 if wr in mid:
                     for r, rng in side.items():
                         assert not _overlap(mid[wr], rng), (ops[k]["name"], wr, ops[i]["name"], r)
@@ -34,7 +34,11 @@ def test_resnet50_projection_shortcuts_are_branches(native, models):
     names = [plan["ops"][i]["name"] for i, _ in branches]
     assert len(branches) == 4, names  # one projection conv per stage
     for i, j in branches:
-        assert plan["ops"][j]["residual"] and j == i + 3  # reduce, 3x3, then the expand conv joins
+        # reduce, 3x3, then the expand conv joins; at the stage-1 -> stage-2 boundary the reduce conv
+        # is inside the conv_pair before the branch, so only the 3x3 runs beside it
+        assert plan["ops"][j]["residual"] and j in (i + 2, i + 3)
+        if j == i + 2:
+            assert plan["ops"][i - 1]["kind"] == "conv_pair" and plan["ops"][i - 1]["store_preact"]
 
 
 @pytest.mark.parametrize("B", [1, 8])
