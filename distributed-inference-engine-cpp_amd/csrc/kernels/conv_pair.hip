@@ -306,8 +306,10 @@ void launch_pair(const PairArgs& a, hipStream_t s) {
 
 }  // namespace
 
+// N2 = 256 (the stage-2 -> stage-3 boundary of ResNet-v2): the W2 slice is 64 KiB in split mode,
+// 144 KiB of LDS in all at K1 = 128.
 bool conv_pair_supported(int K1, int N1, int N2) {
-  return (K1 == 64 || K1 == 128) && (N2 == 64 || N2 == 128) && N1 % BK == 0 && N1 >= BK;
+  return (K1 == 64 || K1 == 128) && (N2 == 64 || N2 == 128 || N2 == 256) && N1 % BK == 0 && N1 >= BK;
 }
 
 hipError_t conv_pair(const PairArgs& a, hipStream_t s) {
@@ -316,10 +318,15 @@ hipError_t conv_pair(const PairArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   if (a.split && (a.wplane1 <= 0 || a.wplane2 <= 0)) return hipErrorInvalidValue;
   if (a.live && a.rows_per_sample <= 0) return hipErrorInvalidValue;
-  if (a.K1 == 64 && a.N2 == 64) launch_pair<64, 64>(a, s);
-  else if (a.K1 == 64) launch_pair<64, 128>(a, s);
-  else if (a.N2 == 64) launch_pair<128, 64>(a, s);
-  else launch_pair<128, 128>(a, s);
+  if (a.K1 == 64) {
+    if (a.N2 == 64) launch_pair<64, 64>(a, s);
+    else if (a.N2 == 128) launch_pair<64, 128>(a, s);
+    else launch_pair<64, 256>(a, s);
+  } else {
+    if (a.N2 == 64) launch_pair<128, 64>(a, s);
+    else if (a.N2 == 128) launch_pair<128, 128>(a, s);
+    else launch_pair<128, 256>(a, s);
+  }
   return hipGetLastError();
 }
 

@@ -182,11 +182,13 @@ def _pack_pair_weight(w, split):
     return split_planes(full) if split else full.to(torch.bfloat16)
 
 
-def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False, store_x=True):
+def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False, store_x=True, store_a=False):
     """Fused expand + next-reduce 1x1 pair (kernels/conv_pair.hip) over rows.
     y [M, K1], w1 [N1, K1], b1 [N1], res [M, N1], s2/h2 [N1], w2 [N2, N1], b2 [N2] (float).
     Returns (x, out): x = y @ w1.T + b1 + res  [M, N1] (None unless store_x) and
-    out = act(act2(x * s2 + h2) @ w2.T + b2)  [M, N2], as fp32 (split planes joined) or bf16."""
+    out = act(act2(x * s2 + h2) @ w2.T + b2)  [M, N2], as fp32 (split planes joined) or bf16;
+    store_a: also the stored pre-activation a = act2(x * s2 + h2) [M, N1] (PairArgs::aout), as a
+    third element."""
     import torch
 
     M, K1 = y.shape
@@ -202,6 +204,9 @@ def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False
     out = torch.empty(np_ + (M, N2), dtype=torch.bfloat16, device=dev)
     zeros = torch.zeros(4096, dtype=torch.int16, device=dev)
     g = dict(M=M, K1=K1, N1=N1, N2=N2, relu=int(relu), relu2=int(relu2), split=int(split), zeros=int(zeros.data_ptr()))
+    ao = torch.empty(np_ + (M, N1), dtype=torch.bfloat16, device=dev) if store_a else None
+    if store_a:
+        g["aout"] = int(ao.data_ptr())
     if split:
         g.update(wplane1=int(wp1[0].numel()), wplane2=int(wp2[0].numel()))
     bb1, ss2, hh2, bb2 = f(b1), f(s2), f(h2), f(b2)
@@ -209,6 +214,8 @@ def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False
                                              _ptr(xo), _ptr(ss2), _ptr(hh2), _ptr(wp2), _ptr(bb2), _ptr(out),
                                              _stream())
     _check(rc, "conv_pair")
+    if store_a:
+        return (None if xo is None else _out(xo, split)), _out(out, split), _out(ao, split)
     return (None if xo is None else _out(xo, split)), _out(out, split)
 
 

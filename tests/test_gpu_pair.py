@@ -59,6 +59,8 @@ PAIR_SHAPES = [
     (130, 128, 512, 128),            # three blocks, two of them partial
     (512, 64, 128, 128),             # mixed combination
     (448, 128, 256, 64),
+    (20 * 28 * 28 - 5, 128, 512, 256),  # the stage-2 -> stage-3 boundary (256 reduce channels)
+    (700, 64, 256, 256),
 ]
 
 
@@ -74,7 +76,8 @@ def test_pair_split_matches_fp64(native, shape):
     assert rel_err(out, outr) <= 2e-5, rel_err(out, outr)
 
 
-@pytest.mark.parametrize("shape", [(2 * 56 * 56, 64, 256, 64), (3 * 28 * 28 - 17, 128, 512, 128)])
+@pytest.mark.parametrize("shape", [(2 * 56 * 56, 64, 256, 64), (3 * 28 * 28 - 17, 128, 512, 128),
+                                   (2 * 28 * 28 - 3, 128, 512, 256)])
 def test_pair_bit_exact_vs_unfused_kernels(native, shape):
     """The fused launch must reproduce the two unfused launches bit for bit (split mode)."""
     torch = _t()
@@ -93,8 +96,11 @@ def test_pair_bit_exact_vs_unfused_kernels(native, shape):
     reduce_.x = expand.out2  # the stored hi/lo planes themselves (re-splitting hi + lo is not always exact)
     assert reduce_.launch(cfg) == 0
     o2, _ = reduce_.results()
-    xf, of = K.conv_pair(y, w1, b1, res, s2, h2, w2, b2, split=True)
+    xf, of, af = K.conv_pair(y, w1, b1, res, s2, h2, w2, b2, split=True, store_a=True)
     assert torch.equal(xf, xo.reshape(M, N1)), (xf - xo.reshape(M, N1)).abs().max().item()
+    # the stored pre-activation (a stage boundary's projection shortcut reads it) = the expand's out2
+    ao = K.join_planes(expand.out2).reshape(M, N1)
+    assert torch.equal(af, ao), (af - ao).abs().max().item()
     assert torch.equal(of, o2.reshape(M, N2)), (of - o2.reshape(M, N2)).abs().max().item()
 
 
@@ -128,7 +134,7 @@ def test_pair_bf16(native, shape):
 
 
 def test_engine_fused_pairs_match_unfused_plan(native, models):
-    """ResNet50-v2 fp32: the default plan (6 expand+reduce pairs fused) vs the unfused plan and torch
+    """ResNet50-v2 fp32: the default plan (7 expand+reduce pairs fused) vs the unfused plan and torch
     fp32, at a full and a partial batch bucket."""
     import numpy as np
 
@@ -141,10 +147,11 @@ def test_engine_fused_pairs_match_unfused_plan(native, models):
     try:
         ops = native.plan_summary(path, 20, precision="fp32")["ops"]
         kinds = [o["kind"] for o in ops]
-        # 5 unit boundaries inside stages 1/2 + the stage-1 -> stage-2 boundary, whose pre-activation
-        # the stage-2 projection shortcut also reads (stored by the pair kernel: store_preact)
-        assert kinds.count("conv_pair") == 6, kinds
-        assert sum(1 for o in ops if o.get("store_preact")) == 1
+        # 5 unit boundaries inside stages 1/2 + the stage-1 -> 2 and stage-2 -> 3 boundaries, whose
+        # pre-activation the next stage's projection shortcut also reads (stored by the pair kernel:
+        # store_preact; the second with 256 reduce channels)
+        assert kinds.count("conv_pair") == 7, kinds
+        assert sum(1 for o in ops if o.get("store_preact")) == 2
         assert ef.refresh_info()["options"]["fuse_pairs"] is True
         for B in (20, 13):
             x = r.synthetic_input(B, cfg, seed=90 + B)
