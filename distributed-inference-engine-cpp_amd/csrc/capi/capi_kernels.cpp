@@ -70,7 +70,6 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     a.order = geti(j, "order", 0);
     if (auto* v = j.find("ws")) a.ws = P<float>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
-    if (auto* v = j.find("aout")) a.aout = P<uint16_t>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("counters")) a.counters = P<int>(static_cast<uint64_t>(v->as_int()));
     a.counters_n = geti(j, "counters_n", 0);
     a.split = geti(j, "split", 0);
@@ -98,6 +97,7 @@ int die_kern_conv_pair(const char* geom, uint64_t x, uint64_t w1, uint64_t bias1
     if (auto* v = j.find("wplane1")) a.wplane1 = v->as_int();
     if (auto* v = j.find("wplane2")) a.wplane2 = v->as_int();
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("aout")) a.aout = P<uint16_t>(static_cast<uint64_t>(v->as_int()));
     a.x = P<const uint16_t>(x);
     a.w1 = P<const uint16_t>(w1);
     a.bias1 = P<const float>(bias1);
