@@ -2525,6 +2525,9 @@ class Planner {
   }
   // With other readers of `a` (a stage boundary: the next stage's projection shortcut reads it
   // too) the pair also stores a (PlanOp::out3) and those readers keep reading it.
+  // Reduce widths up to 128: the kernel takes 256 (stage 2 -> 3) but at one block per CU it is
+  // faster than the two convs only at small batches (B=20: 43.3 vs 51.1 us; B=32: 76.4 vs 69.1).
+  static constexpr int kMaxPairN2 = 128;
   void fuse_conv_pairs() {
     const int nops = static_cast<int>(plan_.ops.size());
     std::vector<std::vector<int>> readers(plan_.bufs.size());
@@ -2536,7 +2539,7 @@ class Planner {
       return q.kind == PlanOp::CONV && q.in == p.out2 && q.in2 < 0 && q.in3 < 0 && q.out >= 0 && q.out2 < 0 &&
              q.out_f32 < 0 && q.conv.relu <= 1 && q.in_scale_off == SIZE_MAX && plain_1x1(q.conv) &&
              q.conv.Cin == p.conv.N && q.conv.H == p.conv.Ho && q.conv.W == p.conv.Wo && q.join < 0 &&
-             kern::conv_pair_supported(p.conv.K, p.conv.N, q.conv.N);
+             q.conv.N <= kMaxPairN2 && kern::conv_pair_supported(p.conv.K, p.conv.N, q.conv.N);
     };
     for (int i = 0; i < nops; ++i) {
       PlanOp& p = plan_.ops[i];
