@@ -142,10 +142,12 @@ def build_random(seed: int, blocks: int = 6) -> Tuple[bytes, Tuple[int, int, int
             elif chain == "softsign":  # x / (1 + |x|)
                 den = g.node("Add", [g.node("Abs", [h], name=nm("abs")), const(1.0)], name=nm("den"))
                 h = g.node("Div", [h, den], name=nm("softsign"))
-            else:  # sqrt(x^2 + 1) - 1
+            else:  # sqrt(x^2 + 1) - 0.5 (not - 1: x^2 + 1 rounds to 1 in bf16 for |x| < 0.06, and the
+                # cancellation made a bf16 engine's output 75 % off the fp32 oracle -- an ill-conditioned
+                # graph, not a kernel error)
                 h = g.node("Sub", [g.node("Sqrt", [g.node("Add", [g.node("Pow", [h, const(2.0)], name=nm("sq")),
                                                                   const(1.0)], name=nm("p1"))], name=nm("sqrt")),
-                                   const(1.0)], name=nm("m1"))
+                                   const(0.5)], name=nm("m1"))
         elif kind == "concat":
             if C % 8:
                 continue
