@@ -295,7 +295,7 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
 // true when the streaming attention kernel is built in (any sequence length; else S <= 256)
 // Streaming attention variant (measurement switch, process-wide): 0 = K/V staged one tile ahead
-// (default), 1 = two tiles ahead.
+// (default), 1 = two tiles ahead, 2 = 0 with the natural (not XCD-aware) block mapping.
 void set_attention_variant(int v);
 bool attention_any_length();
 // Head dim / sequence length the attention launcher takes (streaming kernel: head dim 32, 64, 80,

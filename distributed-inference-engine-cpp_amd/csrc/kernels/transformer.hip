@@ -408,7 +408,7 @@ struct AttnGeom {
 template <bool SPLIT, bool DEEP, int HD>
 __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void attention_stream_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
-    uint16_t* __restrict__ out, int S, int ldq, int ldk, int ldv, int ldo, float scale_log2) {
+    uint16_t* __restrict__ out, int S, int ldq, int ldk, int ldv, int ldo, float scale_log2, int xcd_map) {
   using G = AttnGeom<HD, SPLIT>;
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int KT = 32;  // keys per tile
@@ -416,7 +416,23 @@ __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void at
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][NP][KT * HD];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[2][NP][KT * VPD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // XCD-aware block -> (query block, head, image): blocks are dealt round-robin over the 8 XCDs
+  // (linear id % 8), so with the natural mapping the query blocks of one (image, head) pair land on
+  // different XCDs and each reads the pair's K/V from the Infinity Cache / HBM (ViT-B/16: 117 MB
+  // per layer, 3.7 TB/s).  Here a pair's query blocks take consecutive slots of ONE XCD, so the
+  // second reads K/V from that XCD's L2.
+  int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  {
+    const int nqb = gridDim.x, pairs = gridDim.y * gridDim.z;
+    if (xcd_map && (pairs & 7) == 0) {
+      const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+      const int slot = lin >> 3;
+      const int pair = (lin & 7) + 8 * (slot / nqb);
+      qblk = slot % nqb;
+      h = pair % gridDim.y;
+      b = pair / gridDim.y;
+    }
+  }
   const long long rowbase = static_cast<long long>(b) * S;
   const long long rows = static_cast<long long>(gridDim.z) * S;  // plane distances: rows x pitch
   const int nkt = (S + KT - 1) / KT;
@@ -451,7 +467,7 @@ __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void at
       }
     }
   };
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = qblk * 128 + wave * 32;
   const bool active = q0 < S;  // wave-uniform; an idle wave still loads tiles and meets every barrier
   const int r = lane & 31, hh = lane >> 5;
   bf16x8 qf[NP][NKS];
@@ -705,7 +721,7 @@ bool attention_supported(int D, int S) {
 }
 
 namespace {
-int g_attn_variant = 0;  // 0: K/V staged one tile ahead, 1: two tiles ahead (DEEP)
+int g_attn_variant = 0;  // 0: K/V staged one tile ahead, 1: two tiles ahead (DEEP), 2: 0 without the XCD map
 }
 void set_attention_variant(int v) { g_attn_variant = v; }
 
@@ -716,9 +732,10 @@ hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, ui
   if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S)
     dim3 grid((S + 127) / 128, H, B);
     const bool deep = g_attn_variant == 1;
+    const int xcd_map = g_attn_variant == 2 ? 0 : 1;  // variant 2: the natural block mapping (measurement)
 #define ATTN_LAUNCH(SP, DP, HDV)                                                                                   \
   hipLaunchKernelGGL((attention_stream_kernel<SP, DP, HDV>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, \
-                     sl2)
+                     sl2, xcd_map)
 #define ATTN_HD(HDV)                          \
   if (split && deep) ATTN_LAUNCH(true, true, HDV);    \
   else if (split) ATTN_LAUNCH(true, false, HDV);      \

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Streaming-attention variants (kernels.h set_attention_variant) on ViT-B/16's attention: packed
+"""Streaming-attention variants (kernels.h set_attention_variant: 0 default, 1 K/V two tiles ahead,
+2 without the XCD-aware pair mapping) on ViT-B/16's attention: packed
 QKV rows [B * 197, 3 * 768] as the fused QKV GEMM writes them, 12 heads of 64, fp32 split mode and
 bf16; each a captured hipGraph of 20 launches, median of 5 trials; outputs checked against the
 default variant (bitwise) and against torch float64.
@@ -53,7 +54,7 @@ def main():
             assert rc == 0, rc
 
         first = None
-        for var in (0, 1):
+        for var in (0, 1, 2):
             K.set_attention_variant(var)
             launch()
             torch.cuda.synchronize()
