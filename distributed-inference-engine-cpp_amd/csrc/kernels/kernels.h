@@ -303,6 +303,9 @@ bool attention_any_length();
 bool attention_supported(int D, int S);
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.
+// LayerNorm row order (measurement switch, process-wide, read at launch): 1 (default) = XCD-affine
+// (rows read on the XCD whose GEMM tiles wrote them), 0 = natural block order.
+void set_layernorm_xcd(int v);
 // stats != nullptr: statistics mode -- (mean, rstd) of each row to stats[2 row], 2 row + 1 and y is
 // not written (the normalisation is folded into the consuming GEMM: ConvArgs::row_stats).
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,

@@ -29,6 +29,17 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// XCD affinity for row kernels that read what a GEMM just wrote: the GEMM's XCD-aware mapping
+// (conv_igemm_impl.h block_coords) gives XCD x roughly the x-th eighth of the output rows, and
+// blocks are dealt round-robin over the 8 XCDs (id % 8).  Block id b -> logical block: XCD b % 8
+// takes the (b % 8)-th contiguous eighth of the blocks, so the rows are read where they were
+// written (that XCD's L2) instead of through the Infinity Cache.  Bijective for any block count.
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb, int xcd) {
+  if (!xcd) return b;
+  const unsigned x = b & 7, k = b >> 3, q = nb >> 3, r = nb & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 // LPR lanes per row (64 / LPR rows per wave); each lane holds up to CPL 8-element chunks of the row
 // in registers (two-pass mean/variance in fp32).  C % 8 == 0 (stored pitch), C <= LPR*8*CPL; the
 // statistics run over the first Cl (logical) columns and the pad columns are written 0.  C = 768
@@ -40,10 +51,10 @@ template <int CPL, int LPR = 64>
 __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         const float* __restrict__ g, const float* __restrict__ b,
                                                         float eps, long long rows, int C, int split, int Cl,
-                                                        float* __restrict__ stats) {
+                                                        float* __restrict__ stats, int xcd) {
   constexpr int RPB = 256 / LPR;  // rows per block
   const int lane = threadIdx.x & (LPR - 1);
-  const long long row = static_cast<long long>(blockIdx.x) * RPB + (threadIdx.x / LPR);
+  const long long row = static_cast<long long>(xcd_block(blockIdx.x, gridDim.x, xcd)) * RPB + (threadIdx.x / LPR);
   if (row >= rows) return;  // a whole row group; the shuffles below stay inside it
   const long long plane = rows * C;
   const int nch = C / 8;
@@ -105,9 +116,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const uint16_t* __restri
 __global__ __launch_bounds__(256) void layernorm_wide_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                              const float* __restrict__ g, const float* __restrict__ b,
                                                              float eps, long long rows, int C, int split, int Cl,
-                                                             float* __restrict__ stats) {
+                                                             float* __restrict__ stats, int xcd) {
   __shared__ float red[8];
-  const long long row = blockIdx.x;
+  const long long row = xcd_block(blockIdx.x, gridDim.x, xcd);
   const long long plane = rows * C;
   const uint16_t* xr = x + row * C;
   const int nch = C / 8, tid = threadIdx.x;
@@ -419,15 +430,16 @@ __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void at
   // XCD-aware block -> (query block, head, image): blocks are dealt round-robin over the 8 XCDs
   // (linear id % 8), so with the natural mapping the query blocks of one (image, head) pair land on
   // different XCDs and each reads the pair's K/V from the Infinity Cache / HBM (ViT-B/16: 117 MB
-  // per layer, 3.7 TB/s).  Here a pair's query blocks take consecutive slots of ONE XCD, so the
-  // second reads K/V from that XCD's L2.
+  // per layer, 3.7 TB/s).  Here XCD x takes the x-th contiguous eighth of the pairs (= of the
+  // images: the rows its QKV GEMM tiles wrote, conv_igemm_impl.h block_coords) and a pair's query
+  // blocks take consecutive slots of that XCD, so Q/K/V come from its L2.
   int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   {
     const int nqb = gridDim.x, pairs = gridDim.y * gridDim.z;
     if (xcd_map && (pairs & 7) == 0) {
       const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
       const int slot = lin >> 3;
-      const int pair = (lin & 7) + 8 * (slot / nqb);
+      const int pair = (lin & 7) * (pairs >> 3) + slot / nqb;
       qblk = slot % nqb;
       h = pair % gridDim.y;
       b = pair / gridDim.y;
@@ -654,6 +666,11 @@ inline int grid_for(long long work, int cap = 4096) {
 
 }  // namespace
 
+namespace {
+int g_ln_xcd = 1;  // LayerNorm rows read on the XCD that wrote them (xcd_block); 0: natural order
+}
+void set_layernorm_xcd(int v) { g_ln_xcd = v; }
+
 hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, const float* beta, float eps,
                           long long rows, int C, hipStream_t s, int split, int Cl, int variant, float* stats) {
   if (!stats && !y) return hipErrorInvalidValue;
@@ -663,28 +680,28 @@ hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, co
   if (variant == 1) {
     if (C > 16 * 8 * 6) return hipErrorInvalidValue;
     hipLaunchKernelGGL((layernorm_kernel<6, 16>), dim3(static_cast<int>((rows + 15) / 16)), dim3(256), 0, s, x, y, gamma,
-                       beta, eps, rows, C, split, Cl, stats);
+                       beta, eps, rows, C, split, Cl, stats, g_ln_xcd);
     return hipGetLastError();
   }
   if (variant == 2) {
     hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
-                       rows, C, split, Cl, stats);
+                       rows, C, split, Cl, stats, g_ln_xcd);
     return hipGetLastError();
   }
   if (C > 512 && C <= 32 * 8 * 3) {  // 513..768 (ViT-B: 768): 32 lanes x 3 chunks, 2 rows per wave
     hipLaunchKernelGGL((layernorm_kernel<3, 32>), dim3(static_cast<int>((rows + 7) / 8)), dim3(256), 0, s, x, y, gamma,
-                       beta, eps, rows, C, split, Cl, stats);
+                       beta, eps, rows, C, split, Cl, stats, g_ln_xcd);
     return hipGetLastError();
   }
   if (C <= 64 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
+    hipLaunchKernelGGL(layernorm_kernel<1>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats, g_ln_xcd);
   else if (C <= 128 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
+    hipLaunchKernelGGL(layernorm_kernel<2>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats, g_ln_xcd);
   else if (C <= 256 * 8)
-    hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats);
+    hipLaunchKernelGGL(layernorm_kernel<4>, dim3(blocks), dim3(256), 0, s, x, y, gamma, beta, eps, rows, C, split, Cl, stats, g_ln_xcd);
   else
     hipLaunchKernelGGL(layernorm_wide_kernel, dim3(static_cast<unsigned>(rows)), dim3(256), 0, s, x, y, gamma, beta, eps,
-                       rows, C, split, Cl, stats);
+                       rows, C, split, Cl, stats, g_ln_xcd);
   return hipGetLastError();
 }
 
