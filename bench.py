@@ -99,8 +99,8 @@ def main():
                     help="run the projection-shortcut convs on a side stream (measured slower; off by default)")
     ap.add_argument("--attn-variant", type=int, default=0,
                     help="measurement: streaming attention variant (kernels.h set_attention_variant)")
-    ap.add_argument("--ln-xcd", type=int, default=1,
-                    help="measurement: LayerNorm rows read on the XCD that wrote them (1, default) or in natural order (0)")
+    ap.add_argument("--ln-xcd", type=int, default=0,
+                    help="measurement: LayerNorm rows read on the XCD that wrote them (1) or in natural order (0, default)")
     ap.add_argument("--no-fold-layernorm", action="store_true",
                     help="standalone LayerNorms instead of statistics + GEMM-epilogue normalisation "
                          "(EngineOptions::fold_layernorm)")
@@ -145,7 +145,7 @@ def main():
 
     import die_amd  # noqa: F401
     from die_amd import native
-    if args.device == "hip" and args.ln_xcd != 1:
+    if args.device == "hip" and args.ln_xcd != 0:
         native.kernels().die_kern_set_layernorm_xcd(int(args.ln_xcd))
     if args.device == "hip" and args.attn_variant != 0:
         native.kernels().die_kern_set_attention_variant(int(args.attn_variant))

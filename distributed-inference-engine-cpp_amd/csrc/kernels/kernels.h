@@ -295,7 +295,8 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
 // statistics over the first Cl columns (0 = C; pad columns written 0); any C (> 2048: a block per row).
 // true when the streaming attention kernel is built in (any sequence length; else S <= 256)
 // Streaming attention variant (measurement switch, process-wide): 0 = K/V staged one tile ahead
-// (default), 1 = two tiles ahead, 2 = 0 with the natural (not XCD-aware) block mapping.
+// (default), 1 = two tiles ahead, 2 = 0 with the natural (not XCD-aware) block mapping, 3 = 0 with
+// contiguous pair ranges per XCD.
 void set_attention_variant(int v);
 bool attention_any_length();
 // Head dim / sequence length the attention launcher takes (streaming kernel: head dim 32, 64, 80,
@@ -303,8 +304,9 @@ bool attention_any_length();
 bool attention_supported(int D, int S);
 // variant (measurement): 0 = the default choice, 1 = 16 lanes x 6 chunks per row (C <= 768: 4 rows
 // per wave, twice the loads in flight per lane), 2 = the block-per-row kernel.
-// LayerNorm row order (measurement switch, process-wide, read at launch): 1 (default) = XCD-affine
-// (rows read on the XCD whose GEMM tiles wrote them), 0 = natural block order.
+// LayerNorm row order (measurement switch, process-wide, read at launch): 1 = XCD-affine (rows read
+// on the XCD whose GEMM tiles wrote them), 0 (default) = natural block order -- the ViT forward A/B
+// was inside the run-to-run noise (profiles/r4_attention_xcd_map.md).
 void set_layernorm_xcd(int v);
 // stats != nullptr: statistics mode -- (mean, rstd) of each row to stats[2 row], 2 row + 1 and y is
 // not written (the normalisation is folded into the consuming GEMM: ConvArgs::row_stats).

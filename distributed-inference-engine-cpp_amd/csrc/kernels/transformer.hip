@@ -430,16 +430,18 @@ __global__ __launch_bounds__(256, (AttnGeom<HD, SPLIT>::WAVES_PER_SIMD)) void at
   // XCD-aware block -> (query block, head, image): blocks are dealt round-robin over the 8 XCDs
   // (linear id % 8), so with the natural mapping the query blocks of one (image, head) pair land on
   // different XCDs and each reads the pair's K/V from the Infinity Cache / HBM (ViT-B/16: 117 MB
-  // per layer, 3.7 TB/s).  Here XCD x takes the x-th contiguous eighth of the pairs (= of the
-  // images: the rows its QKV GEMM tiles wrote, conv_igemm_impl.h block_coords) and a pair's query
-  // blocks take consecutive slots of that XCD, so Q/K/V come from its L2.
+  // per layer, 3.7 TB/s).  Here a pair's query blocks take consecutive slots of ONE XCD (pairs
+  // interleaved over the XCDs), so the second reads K/V from that XCD's L2.  xcd_map 2 gives XCD x
+  // the x-th contiguous eighth of the pairs instead (the images whose rows its QKV GEMM tiles wrote):
+  // not measurably different inside the ViT forward (profiles/r4_attention_xcd_map.md).
   int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   {
     const int nqb = gridDim.x, pairs = gridDim.y * gridDim.z;
     if (xcd_map && (pairs & 7) == 0) {
       const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
       const int slot = lin >> 3;
-      const int pair = (lin & 7) * (pairs >> 3) + slot / nqb;
+      const int pair = xcd_map == 2 ? (lin & 7) * (pairs >> 3) + slot / nqb  // contiguous pair ranges
+                                    : (lin & 7) + 8 * (slot / nqb);              // interleaved (default)
       qblk = slot % nqb;
       h = pair % gridDim.y;
       b = pair / gridDim.y;
@@ -667,7 +669,7 @@ inline int grid_for(long long work, int cap = 4096) {
 }  // namespace
 
 namespace {
-int g_ln_xcd = 1;  // LayerNorm rows read on the XCD that wrote them (xcd_block); 0: natural order
+int g_ln_xcd = 0;  // 1: LayerNorm rows read on the XCD that wrote them (xcd_block); 0 (default): natural order
 }
 void set_layernorm_xcd(int v) { g_ln_xcd = v; }
 
@@ -749,7 +751,8 @@ hipError_t attention(const uint16_t* q, const uint16_t* k, const uint16_t* v, ui
   if (kAttnStream) {  // 4-wave blocks of 128 queries, K/V streamed in 32-key tiles (any S)
     dim3 grid((S + 127) / 128, H, B);
     const bool deep = g_attn_variant == 1;
-    const int xcd_map = g_attn_variant == 2 ? 0 : 1;  // variant 2: the natural block mapping (measurement)
+    // variant 2: the natural block mapping, 3: contiguous pair ranges per XCD (measurement)
+    const int xcd_map = g_attn_variant == 2 ? 0 : g_attn_variant == 3 ? 2 : 1;
 #define ATTN_LAUNCH(SP, DP, HDV)                                                                                   \
   hipLaunchKernelGGL((attention_stream_kernel<SP, DP, HDV>), grid, dim3(256), 0, s, q, k, v, out, S, ldq, ldk, ldv, ldo, \
                      sl2, xcd_map)

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--tune-warm-input", action="store_true", help="autotune with each conv's producer run first")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0, help="prefer fused split-K within this fraction")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
-    ap.add_argument("--ln-xcd", type=int, default=1, help="LayerNorm row order: 1 XCD-affine (default), 0 natural")
+    ap.add_argument("--ln-xcd", type=int, default=0, help="LayerNorm row order: 1 XCD-affine, 0 natural (default)")
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
     ap.add_argument("--fuse-gap-fc", action="store_true", help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true", help="stem and max pool as two launches (EngineOptions::fuse_stem_pool)")
