@@ -92,7 +92,9 @@ def main():
     ap.add_argument("--trace-device", action="store_true",
                     help="sample the engine's per-batch device time every 50 ms during the timed pass (tail attribution)")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0,
-                    help="autotune: prefer in-kernel split-K when within this fraction of the best (EngineOptions)")
+                    help="--splitk-two-kernel only: prefer in-kernel split-K within this fraction of the best")
+    ap.add_argument("--splitk-two-kernel", action="store_true",
+                    help="autotune may pick the two-kernel split-K form (partials + reduction kernel; EngineOptions)")
     ap.add_argument("--pace-lead-scale", type=float, default=1.0,
                     help="pacing lead: 1 = measured input path + adaptive margin; other values = input path x this")
     ap.add_argument("--branch-streams", action="store_true",
@@ -205,7 +207,9 @@ def main():
 
         v4 = r.synthetic_input(8, cfg, seed=4242).astype(np.float32)
         vx = v4.reshape(8, -1).copy()
-        vx[:, 0], vx[:, 1] = 0.5, 0.75  # plain decimals: the load generator pads them with zeros
+        # plain decimals: the load generator pads them with 0-15 zeros each (unique texts that stay on
+        # the device decoder's fast path: no host re-parse, csrc/serve/loadgen.cpp verify_body)
+        vx[:, 0], vx[:, 1], vx[:, 2] = 0.5, 0.75, 0.25
         vref = native.cpu_run(model, vx.reshape(v4.shape)).reshape(8, -1)
         verify = dict(verify_inputs=vx, verify_expected=vref, verify_every=args.verify_every,
                       verify_tol=1e-3 if args.precision == "fp32" else 5e-2)
@@ -213,7 +217,7 @@ def main():
                    "pipeline_depth": args.pipeline_depth, "stage_slots": args.stage_slots,
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                    "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
-                   "splitk_fused_margin": args.splitk_fused_margin,
+                   "splitk_fused_margin": args.splitk_fused_margin, "splitk_two_kernel": args.splitk_two_kernel,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
@@ -457,8 +461,7 @@ def main():
     else:
         import numpy as np
 
-        eng = native.Engine(model, device=args.device, device_id=dev, max_batch=B, precision=args.precision,
-                            pipeline_depth=args.pipeline_depth, branch_streams=args.branch_streams)
+        eng = native.Engine(model, **engine_opts)
         x = r.synthetic_input(B, cfg, seed=rank).reshape(B, -1)
         for _ in range(args.warmup):
             eng.run(x)
@@ -469,7 +472,9 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         ok, failed = args.steps * B, 0
-        extra = {"engine": eng.refresh_info()["name"], "device_ms_per_batch": eng.info.get("avg_device_ms")}
+        # device_ms_per_batch: the in-graph forward (hipGraph replay of bucket B, events around it)
+        extra = {"engine": eng.refresh_info()["name"], "device_ms_per_batch": eng.info.get("avg_device_ms"),
+                 "engine_options": eng.info.get("options")}
         eng.close()
 
     if world > 1:

@@ -103,6 +103,7 @@ EngineOptions engine_opts(const Json& j) {
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
+  e.splitk_two_kernel = jget<bool>(j, "splitk_two_kernel", e.splitk_two_kernel);
   e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);
   return e;
 }

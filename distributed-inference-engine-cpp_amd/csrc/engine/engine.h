@@ -237,10 +237,14 @@ struct EngineOptions {
   bool fold_layernorm = true;
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
-  // autotune: take the fastest in-kernel (fused) split-K candidate when it is within this fraction
-  // of the overall best (a separate reduction kernel is one more graph node: launch + drain)
-  float splitk_fused_margin = 0.f;
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
+  // Split-K reductions run in-kernel (the last-arriving split block of a tile sums the partials and
+  // runs the epilogue: kernels/conv_igemm_impl.h tile_epilogue).  true also lets the autotuner pick
+  // the two-kernel form (partials, then splitk_epilogue_kernel: one more graph node per conv).
+  bool splitk_two_kernel = false;
+  // splitk_two_kernel only: take the fastest in-kernel (fused) split-K candidate when it is within
+  // this fraction of the overall best
+  float splitk_fused_margin = 0.f;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;

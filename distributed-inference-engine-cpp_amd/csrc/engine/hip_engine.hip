@@ -858,6 +858,7 @@ class HipEngine : public Engine {
     Tune t;
     t.tile = kern::choose_tile(M, op.conv.N, op.conv.K);
     t.splits = kern::choose_splits(M, op.conv.N, op.conv.K, t.tile);
+    t.fused = t.splits > 1 && !opt_.splitk_two_kernel;
     return t;
   }
 
@@ -909,7 +910,7 @@ class HipEngine : public Engine {
         // identical problems (repeated blocks) share one measurement
         char key[256];
         std::snprintf(key, sizeof(key), "o%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "",
-                      opt_.splitk_fused_margin > 0.f ? "fm:" : "", base.M, base.N, base.K, base.Cin,
+                      opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
         auto memo = tuned_shapes.find(key);
@@ -924,7 +925,8 @@ class HipEngine : public Engine {
         for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
           for (int sp = 1; sp <= 16; sp *= 2) {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
-            for (int fused = 0; fused < (sp > 1 ? 2 : 1); ++fused)
+            // split-K candidates reduce in-kernel unless the two-kernel form is allowed
+            for (int fused = sp > 1 && !opt_.splitk_two_kernel ? 1 : 0; fused < (sp > 1 ? 2 : 1); ++fused)
             // Tile order stays the heuristic (ConvArgs::order 0): tuning N- vs M-fastest per shape
             // picked M-fastest for ~30 % of shapes behind a cold L2 but made the in-graph forwards
             // 1-2 % slower (profiles/r3_gemm_feed.md section 6).

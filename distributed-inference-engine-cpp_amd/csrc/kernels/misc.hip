@@ -254,13 +254,20 @@ __global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict_
     __syncthreads();  // part is rewritten by the next chunk
   }
   if (stop == 2) return;
-  // hand-off: every wave drains its write-through stores, one lane takes the group's ticket
+  // hand-off: every wave drains its write-through stores, one lane takes the group's ticket; the
+  // last arriver's lane runs ONE agent acquire and waits for it before the barrier that releases
+  // the other waves onto the partials (MI355X_MICROARCH "Valid forms", "Consumer, always": several
+  // blocks share a CU here, so sc1 loads alone do not qualify; same form as conv tile_epilogue)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     const int prev = __hip_atomic_fetch_add(counters + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == static_cast<int>(gridDim.x) - 1;
-    if (last) __hip_atomic_store(counters + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) {
+      __hip_atomic_store(counters + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     flag = last;
   }
   __syncthreads();
@@ -272,7 +279,6 @@ __global__ __launch_bounds__(256) void gap_fc_kernel(const uint16_t* __restrict_
   const int KS = static_cast<int>(gridDim.x);
   const unsigned slab = static_cast<unsigned>(static_cast<long long>(B) * N * 4);  // bytes per slice
   if ((N & 3) == 0) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const int nq = ncls / 4;
     for (int it = tid; it < Bl * nq; it += 256) {
       const int bi = it / nq, nn = n0 + 4 * (it - bi * nq);

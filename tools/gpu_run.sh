@@ -64,6 +64,17 @@ case "$TASK" in
         bench "${n}_$r" $a || exit 1
       done
     done ;;
+  abdir)  # abdir N NAME=DIR=ARGS...: as ab, each variant's bench.py run from its own tree DIR (same box)
+    rounds=$1; shift
+    for r in $(seq 1 "$rounds"); do
+      for v in "$@"; do
+        n=${v%%=*}; rest=${v#*=}; d=${rest%%=*}; a=${rest#*=}
+        # shellcheck disable=SC2086
+        (cd "$R/$d" && DIE_TUNE_CACHE=$O/tune_$n.json timeout -k 10 600 python3 bench.py $a > "$O/${n}_$r.json" 2> "$O/${n}_$r.err") \
+          || { tail -20 "$O/${n}_$r.err"; exit 1; }
+        summ "$O/${n}_$r.json" "${n}_$r"
+      done
+    done ;;
   ops)  # ops ARCH B PREC [TAG [op_profile.py args]]
     A=$1; B=$2; P=$3; T=${4:-}; shift 3; [ $# -gt 0 ] && shift
     timeout -k 10 300 python3 -u tools/op_profile.py --arch "$A" --batch "$B" --precision "$P" --out "$O/ops_${A}_${P}_b$B$T" "$@" \

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--tune-warm-input", action="store_true", help="autotune with each conv's producer run first")
     ap.add_argument("--splitk-fused-margin", type=float, default=0.0, help="prefer fused split-K within this fraction")
+    ap.add_argument("--splitk-two-kernel", action="store_true", help="allow the two-kernel split-K form")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
     ap.add_argument("--ln-xcd", type=int, default=0, help="LayerNorm row order: 1 XCD-affine, 0 natural (default)")
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
@@ -44,7 +45,7 @@ def main():
     native.kernels().die_kern_set_layernorm_xcd(int(a.ln_xcd))
     e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision,
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
-                      splitk_fused_margin=a.splitk_fused_margin,
+                      splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
                       fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm)
     p = e.profile(a.batch, a.iters)
     e.close()
