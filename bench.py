@@ -19,7 +19,8 @@ under a watchdog, as `dp_rccl` ({"error": ...} if it fails or hangs; the headlin
 
 A "step" = --step-requests (500) requests per GPU, so the driver's `--steps 20` times 10,000
 requests per GPU: the reference's run length.  W warmup steps (after engine autotune and graph
-capture), then exactly K timed steps bracketed by barrier + torch.cuda.synchronize(); the max wall
+capture), then exactly K timed steps bracketed by barrier + torch.cuda.synchronize() (the client's
+payload templates are built before the opening barrier: loadgen's on_ready hook); the max wall
 time over ranks is the job time and `value` = total successful requests / that time (whole job,
 all GPUs).  The same count of requests sent straight to the worker (no gateway hop) is reported as
 the extra key `direct_worker`.
@@ -132,6 +133,11 @@ def main():
                     help="N>1 gateway mode: ephemeral worker ports instead of ring-balanced ones")
     ap.add_argument("--no-gateway-bytes", action="store_true",
                     help="skip the extra pass with bodies re-sent over loopback HTTP (reference gateway hop)")
+    ap.add_argument("--no-result-stream", action="store_true",
+                    help="result D2H on the compute stream instead of a side stream (EngineOptions::result_stream)")
+    ap.add_argument("--no-ref-client", action="store_true",
+                    help="skip the extra run of the reference's own workload (tools/ref_bench.py: Python "
+                         "benchmark.py client, 3-float payloads, gateway + 3 workers on this rank's GPU)")
     args = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         # n_gpus and global_batch come from --gpus: a torchrun launch must say how many ranks it has
@@ -161,6 +167,23 @@ def main():
         hg.barrier()
         if hip:
             torch.cuda.synchronize()
+
+    def timed_loadgen(start=None, **kw):
+        """One timed client pass: the load generator builds every connection's payload templates and
+        finishes its warm-up, then calls back here; the barrier (+ device sync) that opens the timed
+        window runs in that callback, so payload construction is never timed.  Returns (result,
+        elapsed seconds barrier to barrier, rusage at the start)."""
+        t = {}
+
+        def ready():
+            barrier()
+            t["ru0"] = resource.getrusage(resource.RUSAGE_SELF)
+            if start is not None:
+                start()
+            t["t0"] = time.perf_counter()
+        r_ = native.loadgen(on_ready=ready, **kw)
+        barrier()
+        return r_, time.perf_counter() - t["t0"], t["ru0"]
     if args.arch == "vit_b16":
         from die_amd.models import vit as r
 
@@ -218,6 +241,7 @@ def main():
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                    "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
                    "splitk_fused_margin": args.splitk_fused_margin, "splitk_two_kernel": args.splitk_two_kernel,
+                   "result_stream": not args.no_result_stream,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
@@ -262,26 +286,25 @@ def main():
                        seed=1000 + rank, **lg)
         h0 = wk.health()
         g0 = gw.stats() if gw else {}
-        barrier()
-        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         trace = []
         stop_trace = threading.Event()
-        if args.trace_device:
-            # opt-in: sample the engine's batch / busy counters every 50 ms during the timed pass, so a
-            # tail late in the pass can be told apart from device slow-down (clocks) or host stalls
-            def _sampler():
-                while not stop_trace.wait(0.05):
-                    e = wk.health()["engine"]
-                    trace.append((time.perf_counter(), e.get("batches", 0), e.get("images", 0),
-                                  e.get("avg_device_ms", 0.0)))
-            th = threading.Thread(target=_sampler, daemon=True)
-            th.start()
-        t0 = time.perf_counter()
-        res = native.loadgen(port=target_port, requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank,
-                             seed=2000 + rank, **dict(lg, **(verify or {})))
+        tt = {}
+
+        def _start():
+            tt["t0"] = time.perf_counter()
+            if args.trace_device:
+                # opt-in: sample the engine's batch / busy counters every 50 ms during the timed pass, so a
+                # tail late in the pass can be told apart from device slow-down (clocks) or host stalls
+                def _sampler():
+                    while not stop_trace.wait(0.05):
+                        e = wk.health()["engine"]
+                        trace.append((time.perf_counter(), e.get("batches", 0), e.get("images", 0),
+                                      e.get("avg_device_ms", 0.0)))
+                threading.Thread(target=_sampler, daemon=True).start()
+        res, elapsed, ru0 = timed_loadgen(start=_start, port=target_port, requests=args.steps * SR, warmup=0,
+                                          id_prefix="r%d_" % rank, seed=2000 + rank, **dict(lg, **(verify or {})))
         stop_trace.set()
-        barrier()
-        elapsed = time.perf_counter() - t0
+        t0 = tt["t0"]
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         h1 = wk.health()
         g1 = gw.stats() if gw else {}
@@ -356,12 +379,8 @@ def main():
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()
             hd0 = wk.health()
-            rd0 = resource.getrusage(resource.RUSAGE_SELF)
-            td = time.perf_counter()
-            rd = native.loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank,
-                                seed=3000 + rank, **lg)
-            barrier()
-            el = time.perf_counter() - td
+            rd, el, rd0 = timed_loadgen(port=wk.port, requests=args.steps * SR, warmup=0, id_prefix="d%d_" % rank,
+                                        seed=3000 + rank, **lg)
             rd1 = resource.getrusage(resource.RUSAGE_SELF)
             hd1 = wk.health()
             n_ok = max(1, rd["ok"])
@@ -385,11 +404,8 @@ def main():
                                        local_shm=False, http_threads=args.gw_http_threads,
                                        read_timeout_ms=5000 if hip else 120000)
             barrier()
-            tb = time.perf_counter()
-            rb_ = native.loadgen(port=gwb.port, requests=args.steps * SR, warmup=0, id_prefix="b%d_" % rank,
-                                 seed=4000 + rank, **lg)
-            barrier()
-            elb = time.perf_counter() - tb
+            rb_, elb, _ = timed_loadgen(port=gwb.port, requests=args.steps * SR, warmup=0, id_prefix="b%d_" % rank,
+                                        seed=4000 + rank, **lg)
             gs = gwb.stats()
             extra["gateway_bytes"] = {"rps_this_rank": rb_["ok"] / elb, "p50_ms": rb_["latency_ms"]["p50"],
                                       "p99_ms": rb_["latency_ms"]["p99"], "failed": rb_["failed"],
@@ -400,6 +416,8 @@ def main():
         wk.stop()
         if not args.no_dp:
             extra["dp_rccl"] = _dp_child(args, hg, rank, world)
+        if hip and args.arch == "resnet50" and args.mode == "gateway" and not args.no_ref_client:
+            extra["ref_client"] = _ref_client(hg, rank, dev)
     elif args.mode == "dp":
         # BASELINE config 4: ONE data-parallel worker over all ranks.  Every rank serves HTTP on the
         # same port (SO_REUSEPORT) and parses its own connections' requests; the leader merges the
@@ -424,11 +442,8 @@ def main():
                   timeout_ms=60000, io_threads=args.loadgen_io_threads)
         native.loadgen(requests=args.warmup * SR, warmup=0, id_prefix="warm%d_" % rank, seed=1000 + rank, **lg)
         h0 = wk.health()
-        barrier()
-        t0 = time.perf_counter()
-        res = native.loadgen(requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, seed=2000 + rank, **lg)
-        barrier()
-        elapsed = time.perf_counter() - t0
+        res, elapsed, _ = timed_loadgen(requests=args.steps * SR, warmup=0, id_prefix="r%d_" % rank, seed=2000 + rank,
+                                        **lg)
         ok, failed = res["ok"], res["failed"]
         h1 = wk.health()
         e1 = h1["engine"]
@@ -602,6 +617,57 @@ def _busy(e0, e1, elapsed_s):
     if "device_busy_ms" not in e1 or elapsed_s <= 0:
         return None
     return round((e1["device_busy_ms"] - e0.get("device_busy_ms", 0.0)) / (elapsed_s * 1000.0), 4)
+
+
+def _ref_client(hg, rank, dev):
+    """The reference's own benchmark, as published (README.md:276-294 there: 522.64 req/s, p50
+    84.6 ms): its client (Python `requests`, a new connection per request, 50 threads, 10,000
+    requests, payload [a, a+1, a+2] with a = i % 10, benchmark.py:18-76 there) through a gateway to 3
+    workers on one GPU (tools/ref_bench.py).  Rank 0 only, in a child process under a watchdog;
+    returns the client summary and each worker's cache hit rate (None on other ranks)."""
+    res = None
+    if rank == 0:
+        fd, out = tempfile.mkstemp(prefix="die_refclient_", suffix=".json")
+        os.close(fd)
+        cmd = [sys.executable, os.path.join(REPO, "tools", "ref_bench.py"), "--out", out, "--device", "hip",
+               "--device-id", str(dev), "--requests", "10000", "--threads", "50"]
+        t0 = time.perf_counter()
+        try:
+            # own session: on the watchdog the whole group (client, gateway, workers) goes
+            p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True)
+            try:
+                _, se = p.communicate(timeout=420)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.communicate()
+                raise
+            if p.returncode != 0:
+                res = {"error": "ref_bench exited %d: %s" % (p.returncode, se.decode(errors="replace")[-400:])}
+            else:
+                d = json.load(open(out))
+                c = d["client"]
+                lat = c.get("latency", {})
+                res = {"requests_per_s": c.get("throughput"), "p50_ms": lat.get("p50"), "p99_ms": lat.get("p99"),
+                       "mean_ms": lat.get("mean"), "successful": c.get("successful"), "failed": c.get("failed"),
+                       "requests": d.get("requests"), "threads": d.get("threads"),
+                       "worker_hit_rate": [w.get("cache_hit_rate") for w in d.get("workers", [])],
+                       "worker_requests": [w.get("total_requests") for w in d.get("workers", [])],
+                       "published": {"requests_per_s": BASELINE_RPS, "p50_ms": 84.60, "p99_ms": 164.29},
+                       "vs_published": (c.get("throughput") or 0.0) / BASELINE_RPS,
+                       "client": "tools/benchmark.py (reference CLI; python requests, new connection per request)",
+                       "topology": "gateway + 3 HIP workers on GPU %d" % dev}
+        except subprocess.TimeoutExpired:
+            res = {"error": "ref_bench exceeded the 420 s watchdog"}
+        except Exception as e:  # noqa: BLE001 (the headline must survive anything here)
+            res = {"error": "ref_bench failed: %r" % (e,)}
+        finally:
+            try:
+                os.unlink(out)
+            except OSError:
+                pass
+        res["wall_s"] = round(time.perf_counter() - t0, 1)
+    hg.barrier()
+    return res
 
 
 def _dp_child(args, hg, rank, world):

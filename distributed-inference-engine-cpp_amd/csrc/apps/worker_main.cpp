@@ -56,6 +56,7 @@ die::EngineOptions engine_options_from_flags(const die::Flags& f, const std::str
   eo.pace_lead_scale = f.f("pace-lead-scale", 1.0);
   eo.splitk_fused_margin = static_cast<float>(f.f("splitk-fused-margin", 0.0));
   eo.splitk_two_kernel = f.b("splitk-two-kernel");
+  eo.result_stream = !f.b("no-result-stream");
   eo.completion_poll_us = static_cast<int>(f.i("completion-poll-us", 0));
   eo.bn_on_load = f.b("bn-on-load");
   eo.fuse_pairs = !f.b("no-fuse-pairs");

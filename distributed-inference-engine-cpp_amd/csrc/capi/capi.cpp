@@ -104,6 +104,7 @@ EngineOptions engine_opts(const Json& j) {
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
   e.splitk_two_kernel = jget<bool>(j, "splitk_two_kernel", e.splitk_two_kernel);
+  e.result_stream = jget<bool>(j, "result_stream", e.result_stream);
   e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);
   return e;
 }
@@ -650,6 +651,27 @@ char* die_loadgen_run_verify(const char* opts_json, const float* inputs, long k,
     o.verify_expected = expected;
     o.verify_count = static_cast<size_t>(k);
     o.output_numel = static_cast<size_t>(out_numel);
+    return dup(run_loadgen(o).dump());
+  } catch (const std::exception& e) {
+    set_err(err, e.what());
+    return nullptr;
+  }
+}
+
+// Either form above (inputs == nullptr: no verification), with `on_ready` called on this thread
+// right before the timed phase starts (LoadgenOptions::on_ready).
+char* die_loadgen_run_cb(const char* opts_json, const float* inputs, long k, const float* expected, long out_numel,
+                         void (*on_ready)(void*), char** err) {
+  try {
+    LoadgenOptions o = loadgen_opts(Json::parse(opts_json));
+    if (inputs) {
+      if (o.verify_every <= 0) o.payload = "verify";
+      o.verify_inputs = inputs;
+      o.verify_expected = expected;
+      o.verify_count = static_cast<size_t>(k);
+      o.output_numel = static_cast<size_t>(out_numel);
+    }
+    o.on_ready = on_ready;
     return dup(run_loadgen(o).dump());
   } catch (const std::exception& e) {
     set_err(err, e.what());

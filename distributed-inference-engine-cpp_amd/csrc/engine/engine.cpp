@@ -296,6 +296,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;
   j["splitk_two_kernel"] = o.splitk_two_kernel;
+  j["result_stream"] = o.result_stream;
   j["fail_batch_every"] = o.fail_batch_every;
   return j;
 }

@@ -143,10 +143,12 @@ class Engine {
     (void)ticket;
     (void)ran;
   }
-  // Make host memory DMA-able for this engine (HIP: hipHostRegister); no-op elsewhere.
-  virtual void register_host_memory(void* p, size_t bytes) {
+  // Make host memory DMA-able for this engine (HIP: hipHostRegister); no-op elsewhere.  Returns
+  // the bytes actually pinned (0 when the engine needs no pinning).
+  virtual size_t register_host_memory(void* p, size_t bytes) {
     (void)p;
     (void)bytes;
+    return 0;
   }
   // True when the engine all-gathers outputs across data-parallel ranks itself (RCCL).
   virtual bool device_gather() const { return false; }
@@ -194,6 +196,9 @@ struct EngineOptions {
   // Run the PREP part (decode-table fetch, device decode, input prep) on the compute stream right
   // before MAIN instead of on the copy stream beside the previous batch's MAIN.
   bool prep_on_compute = false;
+  // Each batch's result D2H (and data-parallel collectives) on a separate stream behind an event
+  // after MAIN, instead of on the compute stream ahead of the next batch's MAIN.
+  bool result_stream = true;
   // A batch runs the hipGraph of the smallest bucket >= B; with live_batch the kernels read B from
   // the slot's table and skip the work of the bucket's padding samples.
   bool live_batch = true;

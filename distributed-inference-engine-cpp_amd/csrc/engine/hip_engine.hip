@@ -102,6 +102,10 @@ class HipEngine : public Engine {
     // the fourth queue: side branches, or a dedicated PREP stream when texts are uploaded early
     if (!branches_ && n_exec_ == 1 && opt.device_decode && opt.stage_slots != 0 && !comm_)
       HIP_CHECK(hipStreamCreateWithFlags(&s_prep_, hipStreamNonBlocking));
+    // Result stream: each batch's logits / status D2H (and, data parallel, its collectives) wait on
+    // an event after MAIN instead of queueing on the compute stream, so the next batch's MAIN starts
+    // right behind this one's (the copies are blit kernels that otherwise sit between two graphs).
+    if (opt.result_stream) HIP_CHECK(hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking));
     prep_on_compute_ = opt.prep_on_compute;
     use_live_ = opt.live_batch;
     lead_scale_ = std::max(0.0, opt.pace_lead_scale);
@@ -182,6 +186,7 @@ class HipEngine : public Engine {
                               hipHostMallocDefault));
       for (auto& ev : sl.ev_h2d) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
+      HIP_CHECK(hipEventCreateWithFlags(&sl.ev_main, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&sl.ev_prep, hipEventDisableTiming));
       for (int id : prep_out_ids_) {
         void* pbuf = nullptr;
@@ -320,6 +325,7 @@ class HipEngine : public Engine {
       (void)hipHostFree(sl.h_out);
       for (auto ev : sl.ev_h2d) (void)hipEventDestroy(ev);
       (void)hipEventDestroy(sl.ev_d2h);
+      (void)hipEventDestroy(sl.ev_main);
       (void)hipEventDestroy(sl.ev_prep);
       for (void* pbuf : sl.d_prep) (void)hipFree(pbuf);
     }
@@ -334,6 +340,7 @@ class HipEngine : public Engine {
       (void)hipStreamDestroy(s_exec_[e]);
     }
     if (s_prep_) (void)hipStreamDestroy(s_prep_);
+    if (s_out_) (void)hipStreamDestroy(s_out_);
     if (branches_) {
       (void)hipFree(ws_side_);
       (void)hipFree(counters_side_);
@@ -352,10 +359,11 @@ class HipEngine : public Engine {
   size_t text_capacity() const override { return text_cap_; }
   bool text_packing() const override { return d_packed_ != nullptr; }
   bool device_gather() const override { return comm_ != nullptr; }
-  void register_host_memory(void* p, size_t bytes) override {
+  size_t register_host_memory(void* p, size_t bytes) override {
     HIP_CHECK(hipSetDevice(dev_));
     HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterDefault));
     registered_.push_back(p);
+    return bytes;
   }
 
   // Early upload: reactor threads only queue the request; ONE stager thread issues every staged
@@ -566,16 +574,17 @@ class HipEngine : public Engine {
         // this rank's shard ran: its flag travels with the status rows, so the other ranks answer
         // this shard's items from the gathered rows (flag 0: they fail them; see the catch below)
         HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 1, 1, cs));
-        dp_collectives(sl, B, cs);
+        dp_collectives(sl, B, result_stream(sl, cs));
         job.has_text = text_cap_ > 0;
       } else {
-        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, cs));
+        hipStream_t os = result_stream(sl, cs);
+        HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * out_numel_ * B, hipMemcpyDeviceToHost, os));
         d2h_bytes_.fetch_add(static_cast<long long>(sizeof(float) * out_numel_ * B), std::memory_order_relaxed);
         if (any_text) {
-          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, cs));
+          HIP_CHECK(hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int) * 2 * max_batch_, hipMemcpyDeviceToHost, os));
           d2h_bytes_.fetch_add(static_cast<long long>(sizeof(int) * 2 * max_batch_), std::memory_order_relaxed);
         }
-        HIP_CHECK(hipEventRecord(sl.ev_d2h, cs));
+        HIP_CHECK(hipEventRecord(sl.ev_d2h, os));
       }
     } catch (const std::exception& e) {
       job.error = e.what();
@@ -585,9 +594,9 @@ class HipEngine : public Engine {
         // this shard's items and answer the rest.
         try {
           Slot& sl = slots_[slot];
-          HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 0, 1,
-                                      s_exec_[slot % n_exec_]));
-          dp_collectives(sl, B, s_exec_[slot % n_exec_]);
+          hipStream_t cs = s_exec_[slot % n_exec_];
+          HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sl.d_status + rank_ok_index()), 0, 1, cs));
+          dp_collectives(sl, B, result_stream(sl, cs));
           job.dp_gathered = true;
           job.has_text = text_cap_ > 0;
         } catch (const std::exception&) {
@@ -1325,6 +1334,7 @@ class HipEngine : public Engine {
     int* h_status = nullptr;          // pinned
     hipEvent_t ev_h2d[kStageStreams] = {};
     hipEvent_t ev_d2h{};
+    hipEvent_t ev_main{};  // MAIN done on the compute stream: the result copies (s_out_) wait on it
     hipEvent_t ev_prep{};
     std::vector<void*> d_prep;  // per-slot outputs of the PREP part's input-prep ops
   };
@@ -1541,6 +1551,14 @@ class HipEngine : public Engine {
   // Data parallel: every rank contributes its B rows and its status table to every other rank over
   // xGMI (the same collectives in the same order on every rank, whatever its shard holds), then
   // copies all rows and tables to its host; a group of one copies straight from d_out.
+  // The stream a batch's result copies / collectives go on: s_out_ behind an event after the work
+  // queued on cs so far (EngineOptions::result_stream), else cs itself.
+  hipStream_t result_stream(Slot& sl, hipStream_t cs) {
+    if (!s_out_) return cs;
+    HIP_CHECK(hipEventRecord(sl.ev_main, cs));
+    HIP_CHECK(hipStreamWaitEvent(s_out_, sl.ev_main, 0));
+    return s_out_;
+  }
   void dp_collectives(Slot& sl, int B, hipStream_t cs) {
     dp_issued_ = true;
     if (dp_world_ > 1) {  // one grouped operation: logits + status table (shard flag included)
@@ -1561,6 +1579,7 @@ class HipEngine : public Engine {
   }
   size_t live_index() const { return static_cast<size_t>(kTableRows) * max_batch_; }
   int n_stage_ = 0;                  // early-upload slots (stage_text)
+  hipStream_t s_out_ = nullptr;      // result copies / data-parallel collectives (behind Slot::ev_main)
   hipStream_t s_stage_[kStageStreams] = {};
   int n_copy_streams_ = kStageStreams;  // copy streams in use (EngineOptions::copy_streams, 1..kStageStreams)
   unsigned long long stage_counter_[kStageStreams] = {};

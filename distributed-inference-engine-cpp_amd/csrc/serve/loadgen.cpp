@@ -96,8 +96,9 @@ Template make_verify_template(const LoadgenOptions& o, size_t k) {
   char buf[48];
   for (size_t i = 0; i < o.input_numel; ++i) {
     if (i) b.push_back(',');
-    const int n = std::snprintf(buf, sizeof buf, "%.*f", d, static_cast<double>(xs[i]));
-    if (n > 0 && n < static_cast<int>(sizeof buf) && std::strtof(buf, nullptr) == xs[i]) b.append(buf, static_cast<size_t>(n));
+    const auto r = std::to_chars(buf, buf + sizeof buf, xs[i], std::chars_format::fixed, d);
+    float back = 0.f;
+    if (r.ec == std::errc() && std::from_chars(buf, r.ptr, back).ec == std::errc() && back == xs[i]) b.append(buf, r.ptr);
     else b.append(buf, std::to_chars(buf, buf + sizeof buf, xs[i]).ptr);
   }
   b += "]}";
@@ -532,7 +533,8 @@ Json run_loadgen(const LoadgenOptions& o) {
       });
     }
   }
-  gate.arrive();
+  gate.arrive();  // every client thread built its payloads and finished the warm-up
+  if (o.on_ready) o.on_ready(o.on_ready_arg);
   t0 = std::chrono::steady_clock::now();
   gate.arrive();
   gate.arrive();

@@ -52,6 +52,11 @@ struct LoadgenOptions {
   // connection (same closed loop, one request in flight per connection), so the client takes less
   // of a CPU share it shares with the server under test.
   int io_threads = 0;
+  // Called once, on the calling thread, after every connection is open, its payload template built
+  // and the warm-up done, right before the timed phase starts (bench.py: the barrier that opens the
+  // timed window runs here, so building payloads is never inside it).
+  void (*on_ready)(void*) = nullptr;
+  void* on_ready_arg = nullptr;
 };
 
 // Runs warmup then the timed phase; returns {"ok","failed","wall_s","rps","latency_ms":{...},

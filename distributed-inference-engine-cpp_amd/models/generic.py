@@ -28,6 +28,9 @@ mix a ResNet / ViT never exercises, random weights, written by the in-tree ONNX 
               output width that are not multiples of 8).
 * `ln_wide`    LayerNormalization over 20 features (stored with 24: pad columns out of the
               statistics) and over 2560 features (wider than the register-resident kernels hold).
+* `ln_offset`  pre-norm rows whose LayerNorm input carries a large DC offset (~60 on every channel,
+              |mean| / std ~ 60 per row) before the LayerNorm -> MatMul: the case where folding the
+              LayerNorm into the GEMM (x.W' - mean * colsum) cancels.
 * `bert_long`  the `bert` encoder at 320 tokens: attention past 256 keys (streaming kernel).
 * `bert_hd32`, `bert_hd128`  the `bert` encoder with head dim 32 (4 heads of 128 features, 40 tokens)
               and 128 (2 heads of 256 features, 24 tokens).
@@ -52,6 +55,7 @@ SPECS = {
     "upsample_net": dict(in_ch=8, image=12, classes=10),
     "token_mixer": dict(seq=24, dim=40, classes=10),
     "ln_wide": dict(seq=6, dim=20, wide=2560, classes=10),
+    "ln_offset": dict(seq=64, dim=128, hidden=256, classes=10),
     "bert_long": dict(seq=320, dim=128, heads=2, ffn=256, layers=1, classes=3),
     "bert_hd32": dict(seq=40, dim=128, heads=4, ffn=256, layers=2, classes=3),
     "bert_hd128": dict(seq=24, dim=256, heads=2, ffn=512, layers=2, classes=3),
@@ -358,9 +362,36 @@ def build_ln_wide(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.n
     return g.model_proto(opset=opset), {}
 
 
+def build_ln_offset(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    s = SPECS["ln_offset"]
+    rng = _rng(seed)
+    S, D, H = s["seq"], s["dim"], s["hidden"]
+    g = GraphBuilder(name="ln_offset")
+    x = g.input("tokens", ["N", S * D])
+    h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
+    # a row-constant offset (the same for every channel): |mean| / std of each row ~ 60 -- the
+    # cancellation case -- plus a small per-channel spread
+    off = (60.0 + 0.5 * rng.standard_normal(D)).astype(np.float32)
+    h = g.node("Add", [h, g.init("offset", off)], name="dc_offset")
+
+    def ln(inp, name, c):
+        gw = g.init(name + ".weight", (1.0 + 0.1 * rng.standard_normal(c)).astype(np.float32))
+        gb = g.init(name + ".bias", (0.1 * rng.standard_normal(c)).astype(np.float32))
+        return g.node("LayerNormalization", [inp, gw, gb], name=name, axis=-1, epsilon=1e-5)
+
+    h = g.node("Add", [g.node("MatMul", [ln(h, "ln0", D), g.init("fc1.weight", _lin(rng, D, (D, H)))], name="fc1/MatMul"),
+                       g.init("fc1.bias", (0.1 * rng.standard_normal(H)).astype(np.float32))], name="fc1/Add")
+    h = g.node("Tanh", [h], name="act")
+    pooled = g.node("ReduceMean", [h], name="pool", axes=[1], keepdims=0)
+    w = g.init("head.weight", _lin(rng, H, (s["classes"], H)))
+    y = g.node("Gemm", [pooled, w, g.init("head.bias", np.zeros(s["classes"], np.float32))], name="head", transB=1)
+    g.output(y, ["N", s["classes"]])
+    return g.model_proto(opset=opset), {}
+
+
 BUILDERS = {"mlp": build_mlp, "bert": build_bert, "se_cnn": build_se_cnn, "ratio_mlp": build_ratio_mlp,
             "ops_zoo": build_ops_zoo, "upsample_net": build_upsample_net, "token_mixer": build_token_mixer,
-            "ln_wide": build_ln_wide,
+            "ln_wide": build_ln_wide, "ln_offset": build_ln_offset,
             "bert_long": lambda seed=0: build_bert(seed, spec="bert_long"),
             "bert_hd32": lambda seed=0: build_bert(seed, spec="bert_hd32"),
             "bert_hd128": lambda seed=0: build_bert(seed, spec="bert_hd128")}
@@ -374,7 +405,7 @@ def input_shape(name: str):
     s = SPECS[name]
     if name in ("mlp", "ratio_mlp"):
         return (s["in_features"],)
-    if name in ("bert", "bert_long", "bert_hd32", "bert_hd128", "token_mixer", "ln_wide"):
+    if name in ("bert", "bert_long", "bert_hd32", "bert_hd128", "token_mixer", "ln_wide", "ln_offset"):
         return (s["seq"] * s["dim"],)
     return (s["in_ch"], s["image"], s["image"])
 

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -19,6 +19,9 @@ _LIB: Optional[C.CDLL] = None
 
 class NativeError(RuntimeError):
     pass
+
+
+_READY_CB = C.CFUNCTYPE(None, C.c_void_p)  # loadgen on_ready hook (LoadgenOptions::on_ready)
 
 
 def lib_path() -> str:
@@ -105,6 +108,7 @@ def lib() -> C.CDLL:
         sig("die_gateway_destroy", None, vp)
         sig("die_loadgen_run", vp, cp, errp)
         sig("die_loadgen_run_verify", vp, cp, f32p, C.c_long, f32p, C.c_long, errp)
+        sig("die_loadgen_run_cb", vp, cp, f32p, C.c_long, f32p, C.c_long, _READY_CB, errp)
         sig("die_parse_bench", C.c_double, cp, C.c_long, C.c_int, C.c_int)
         i32p = C.POINTER(C.c_int)
         sig("die_dp_shard", C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p)
@@ -601,15 +605,33 @@ class GatewayServer:
 
 
 def loadgen(verify_inputs: Optional[np.ndarray] = None, verify_expected: Optional[np.ndarray] = None,
-            **opts) -> Dict[str, Any]:
+            on_ready: Optional[Callable[[], None]] = None, **opts) -> Dict[str, Any]:
     """Closed-loop C++ load generator.  With verify_inputs ([K, input_numel]) and verify_expected
     ([K, output_numel]) every request carries one of the K inputs (unique request_id) and every answer
     is checked against its expected row (relative L2 <= verify_tol, 0 = bit-exact): the result adds
     "verified", "mismatched", "bad_request_id" and "max_rel_err".  With payload="full" and
     verify_every=N only every N-th request is such a verified one (zero-padded text: never a cache
     hit); scramble_ids=True prints request numbers scrambled (hash-uniform on the gateway ring);
-    io_threads=N > 0 drives the connections from N epoll threads instead of one thread each."""
+    io_threads=N > 0 drives the connections from N epoll threads instead of one thread each.
+    on_ready() runs once, on this thread, after every connection's payloads are built and the warm-up
+    is done, right before the timed phase (the place for a timing barrier)."""
     err = _err_box()
+    if on_ready is not None:
+        def _cb(_arg):
+            on_ready()
+        cb = _READY_CB(_cb)  # kept alive for the duration of the call
+        xi = xe = None
+        k = n_out = 0
+        if verify_inputs is not None:
+            xi = np.ascontiguousarray(verify_inputs, np.float32).reshape(len(verify_inputs), -1)
+            xe = np.ascontiguousarray(verify_expected, np.float32).reshape(len(xi), -1)
+            opts = dict(opts, input_numel=xi.shape[1])
+            k, n_out = len(xi), xe.shape[1]
+        p = lib().die_loadgen_run_cb(json.dumps(opts).encode(), _f32(xi) if xi is not None else None, k,
+                                     _f32(xe) if xe is not None else None, n_out, cb, C.byref(err))
+        if not p:
+            _raise_if(err, "loadgen")
+        return json.loads(_take_str(p))
     if verify_inputs is not None:
         xi = np.ascontiguousarray(verify_inputs, np.float32).reshape(len(verify_inputs), -1)
         xe = np.ascontiguousarray(verify_expected, np.float32).reshape(len(xi), -1)

@@ -363,6 +363,14 @@ def test_dp_eight_ranks_every_rank_ingests_verified(native, models):
     assert len(healths) == world - 1
     parsed = [h0["total_requests"]] + [h["total_requests"] for h in healths]
     assert sum(parsed) >= 480 and sum(n > 0 for n in parsed) >= 4, parsed  # the kernel spread the connections
+    # every rank asks its engine to pin exactly the shared arena once (one mapping of
+    # the same pages per process), timed at start-up; the CPU executor pins nothing
+    engines = [h0["engine"]] + [h["engine"] for h in healths]
+    arena = int(round(engines[0]["dp_arena_mib"] * (1 << 20)))
+    assert all(e["dp_pin_request_bytes"] == arena for e in engines), [e["dp_pin_request_bytes"] for e in engines]
+    assert sum(e["dp_pin_request_bytes"] for e in engines) == world * arena
+    assert all(e["dp_pinned_bytes"] == 0 for e in engines)
+    assert all(0.0 <= e["dp_register_ms"] < 1000.0 for e in engines)
 
 
 def test_dp_arena_at_eight_ranks_batch_256(native):

@@ -13,7 +13,7 @@ from conftest import gpu_available
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long",
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "ln_offset", "bert_long",
            "bert_hd32", "bert_hd128"]
 
 
@@ -52,6 +52,29 @@ def test_generic_model_matches_cpu_executor(native, gen_models, name, precision,
             assert err <= tol, (name, precision, B, err)
             if precision == "fp32":
                 assert (got.argmax(1) == ref.argmax(1)).all()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("fold", [False, True])
+def test_fold_layernorm_offset_rows(native, gen_models, fold):
+    """a folded LayerNorm computes rstd * (x.W' - mean * colsum) from the raw rows, whose
+    split-bf16 representation error (~2^-17 |x|) is amplified by |mean| / std.  Rows with a DC offset
+    of 20-100 and one channel at 400 (models/generic.py ln_offset): the default plan (no folding)
+    meets the fp32 bar; the opt-in fold is measured against it and must stay inside the looser
+    bar reported in docs/DESIGN.md (it is not the default for that reason)."""
+    from die_amd.models import generic as G
+
+    path = gen_models["ln_offset"]
+    eng = native.Engine(path, device="hip", max_batch=8, precision="fp32", autotune=False, fold_layernorm=fold)
+    try:
+        assert eng.refresh_info()["options"]["fold_layernorm"] is fold
+        x = G.synthetic_input("ln_offset", 8, seed=3)
+        ref = native.cpu_run(path, x).reshape(8, -1)
+        got = eng.run(x.reshape(8, -1))
+        err = _rel_l2(got, ref)
+        print("fold_layernorm=%s offset rows rel-L2 %.3e" % (fold, err))
+        assert err <= (1e-4 if not fold else 5e-2), (fold, err)
     finally:
         eng.close()
 

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "bert_long",
+GENERIC = ["mlp", "bert", "se_cnn", "ratio_mlp", "ops_zoo", "upsample_net", "token_mixer", "ln_wide", "ln_offset", "bert_long",
            "bert_hd32", "bert_hd128"]
 
 
@@ -55,6 +55,12 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
         assert kinds.count("bmm") == 2 and kinds[0] == "rows_prep"
     if name == "ln_wide":
         assert kinds.count("layernorm") == 2
+    if name == "ln_offset":
+        # LayerNorm folding is opt-in: by default the LayerNorm normalises its rows itself
+        assert kinds.count("layernorm") == 1 and not any(o.get("stats_only") for o in s["ops"])
+        f = native.plan_summary(gen_models[name], 8, precision="fp32", fold_layernorm=True)
+        if precision == "fp32":
+            assert sum(1 for o in f["ops"] if o.get("stats_only")) == 1
     if name == "bert_long":
         assert kinds.count("attention") == 1
 
