@@ -374,7 +374,10 @@ def main():
                 ids = [x for k in range(world) for x in rb.request_ids("r%d_" % k, args.steps * SR)]
                 extra["ring"] = dict(rb.predict(names, ids), balanced_ports=not args.no_ring_balance,
                                      ports=list(ports),
-                                     arc_max_over_fair=round(float(rb.arc_shares(names).max() * world), 3))
+                                     arc_max_over_fair=round(float(rb.arc_shares(names).max() * world), 3),
+                                     # the same routing on the reference's own layout (ports
+                                     # 8001.., sequential "req_<i>" ids), next to the tuned deployment
+                                     reference_layout=rb.reference_layout(world, args.steps * SR * world))
         if gw and not args.no_direct:
             # informative: the same request count straight to this rank's worker (no gateway hop)
             barrier()

@@ -1,5 +1,6 @@
 #include <pthread.h>
 #include "engine.h"
+#include "hip_plan.h"
 
 #include "../core/log.h"
 
@@ -317,10 +318,12 @@ std::unique_ptr<Engine> create_engine(const std::string& model_path, const Engin
     bool unlowerable = false;
     try {
       e = create_hip_engine(model_path, opt, &why);
+    } catch (const PlanUnsupported& ex) {
+      why = ex.what();
+      unlowerable = true;
     } catch (const std::exception& ex) {
       why = ex.what();
-      unlowerable = why.find("cannot lower") != std::string::npos;
-      if (opt.device == "hip" && !unlowerable) throw;
+      if (opt.device == "hip") throw;
     }
     if (e) return e;
     if (unlowerable) {
@@ -332,7 +335,13 @@ std::unique_ptr<Engine> create_engine(const std::string& model_path, const Engin
       } catch (const std::exception& ex) {
         why2 = ex.what();
       }
-      if (e) return e;
+      if (e) {
+        // device "hip" asked for GPU execution: say loudly that part of the graph runs on the CPU
+        if (opt.device == "hip")
+          DIE_LOG(WARN, "device=hip: the graph has nodes the HIP planner cannot lower; serving it as " << e->name()
+                                                                                                      << " (CPU islands)");
+        return e;
+      }
       DIE_LOG(WARN, "hybrid HIP + CPU partition unavailable: " << why2);
       if (opt.device == "hip") throw std::runtime_error(why);
     }

@@ -127,7 +127,7 @@ class Planner {
         mark_unknown(n);
       }
     }
-    if (!report_.supported) throw std::runtime_error("HIP engine cannot lower this graph:\n" + report_.text());
+    if (!report_.supported) throw PlanUnsupported("HIP engine cannot lower this graph:\n" + report_.text());
     finalize_output();
     fuse_pool_affine();
     if (fuse_stem_pool_) fuse_stem_pool();

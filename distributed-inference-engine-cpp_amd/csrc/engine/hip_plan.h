@@ -21,6 +21,7 @@
 #pragma once
 
 #include <cstdint>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -118,7 +119,13 @@ struct Plan {
   std::string summary() const;
 };
 
-// Build the plan for batches up to max_batch.  Throws on unsupported graphs, listing EVERY node
+// Thrown by build_plan for a graph with nodes the HIP planner cannot lower (what() lists them all):
+// the engine factory's cue for the hybrid HIP + CPU partition (engine.cpp create_engine).
+struct PlanUnsupported : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Build the plan for batches up to max_batch.  Throws PlanUnsupported on unsupported graphs, listing EVERY node
 // the engine cannot lower (not only the first).  side_branches: mark independent convs to run on
 // a second stream (PlanOp::join; extends their inputs' lifetimes).  split: fp32 mode (Plan::split).
 // fuse_pairs: lower expand -> reduce 1x1 conv pairs to CONV_PAIR ops (EngineOptions::fuse_pairs).

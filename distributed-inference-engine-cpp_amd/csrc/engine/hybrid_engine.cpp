@@ -81,8 +81,12 @@ std::vector<Cut> cut_points(const onnx::Model& m) {
     for (const auto& x : m.nodes[static_cast<size_t>(k)].inputs)
       if (!x.empty() && !m.initializers.count(x)) last_use[x] = k;
   for (const auto& o : m.outputs) last_use[o.name] = N;
+  // every graph input that is read (not only input 0): a second input live across a candidate cut
+  // makes it a two-tensor point, so it is no cut; initializers listed as graph inputs
+  // (IR v3 models) are weights, not live state
   std::unordered_set<std::string> live;
-  if (!m.inputs.empty() && last_use.count(m.inputs[0].name)) live.insert(m.inputs[0].name);
+  for (const auto& in : m.inputs)
+    if (!m.initializers.count(in.name) && last_use.count(in.name)) live.insert(in.name);
   std::vector<Cut> cuts;
   if (live.size() == 1) cuts.push_back(Cut{-1, *live.begin()});
   for (int k = 0; k < N; ++k) {

@@ -47,6 +47,20 @@ uint64_t splitmix64(uint64_t x) {
 
 constexpr int kIdDigits = 10;
 
+// Bijection of [0, 10^10) (parallel/ring_balance.py scramble_id): a 4-round Feistel network on the
+// two 5-digit halves with splitmix64 round functions, so distinct request numbers print distinct
+// ids that FNV-1a spreads over the gateway ring like random ones.
+uint64_t scramble_id(uint64_t i) {
+  constexpr uint64_t kHalf = 100000;
+  uint64_t left = (i % 10000000000ull) / kHalf, right = i % kHalf;
+  for (uint64_t k = 0; k < 4; ++k) {
+    const uint64_t next = (left + splitmix64(right * 4 + k) % kHalf) % kHalf;
+    left = right;
+    right = next;
+  }
+  return left * kHalf + right;
+}
+
 Template make_full_template(const LoadgenOptions& o, uint64_t seed) {
   Template t;
   std::mt19937_64 rng(seed);
@@ -210,7 +224,7 @@ Json run_loadgen(const LoadgenOptions& o) {
   std::vector<Template> vt;  // verify mode: one shared template per distinct input
   for (size_t k = 0; (verify || sampled) && k < o.verify_count; ++k) vt.push_back(make_verify_template(o, k));
   auto printed = [&](long id) -> uint64_t {
-    return o.scramble_ids ? splitmix64(static_cast<uint64_t>(id)) % 10000000000ull : static_cast<uint64_t>(id);
+    return o.scramble_ids ? scramble_id(static_cast<uint64_t>(id)) : static_cast<uint64_t>(id);
   };
   auto is_verify = [&](long id) { return verify || (sampled && id % o.verify_every == 0); };
   auto verify_k = [&](long id) -> size_t {

@@ -45,7 +45,7 @@ struct LoadgenOptions {
   // answer is checked like verify mode, and its text is made unique by zero-padding the first two
   // values (0.5 -> 0.5000...: same floats, another cache key), so it is computed, never a cache hit.
   long verify_every = 0;
-  // Print request numbers scrambled (splitmix64(id) mod 10^10, fixed width) instead of in order:
+  // Print request numbers scrambled (a bijection of [0, 10^10), fixed width) instead of in order:
   // FNV-1a of consecutive decimal strings clusters on the gateway's ring (bench.py ring analysis).
   bool scramble_ids = false;
   // > 0: drive the connections from this many epoll threads instead of one blocking thread per

@@ -91,9 +91,32 @@ def splitmix64(x: int) -> int:
     return x ^ (x >> 31)
 
 
+_HALF = 10 ** 5
+
+
+def scramble_id(i: int) -> int:
+    """A bijection of [0, 10^10) (csrc/serve/loadgen.cpp scramble_id): a 4-round Feistel network on
+    the two 5-digit halves with splitmix64 round functions -- distinct request numbers stay distinct
+    (splitmix64(i) % 10^10 collided a few times in a few hundred thousand ids) and their
+    decimal strings spread over the FNV-1a ring like random ids."""
+    left, right = divmod(i % 10 ** 10, _HALF)
+    for k in range(4):
+        left, right = right, (left + splitmix64(right * 4 + k) % _HALF) % _HALF
+    return left * _HALF + right
+
+
 def request_ids(prefix: str, n: int, scramble: bool = True) -> List[str]:
-    """The ids csrc/serve/loadgen.cpp sends: prefix + 10 digits (scrambled: splitmix64(i) % 10^10)."""
-    return [prefix + "%010d" % ((splitmix64(i) % 10 ** 10) if scramble else i) for i in range(n)]
+    """The ids csrc/serve/loadgen.cpp sends: prefix + 10 digits (scrambled: scramble_id(i))."""
+    return [prefix + "%010d" % (scramble_id(i) if scramble else i) for i in range(n)]
+
+
+def reference_layout(world: int, n: int) -> Dict[str, object]:
+    """What the reference's own deployment would route: workers on consecutive ports from 8001
+    (/root/reference/README.md:103-109) and sequential ids "req_<i>" (/root/reference/benchmark.py:22),
+    i.e. the ring without bench.py's port choice and id scramble."""
+    names = ["127.0.0.1:%d" % (8001 + k) for k in range(world)]
+    return dict(predict(names, ["req_%d" % i for i in range(n)]), ports=[8001 + k for k in range(world)],
+                ids="req_<i>, sequential")
 
 
 def route_shares(names: Sequence[str], ids: Iterable[str]) -> np.ndarray:

@@ -56,27 +56,29 @@ def test_generic_model_matches_cpu_executor(native, gen_models, name, precision,
         eng.close()
 
 
-@pytest.mark.parametrize("fold", [False, True])
-def test_fold_layernorm_offset_rows(native, gen_models, fold):
-    """a folded LayerNorm computes rstd * (x.W' - mean * colsum) from the raw rows, whose
-    split-bf16 representation error (~2^-17 |x|) is amplified by |mean| / std.  Rows with a DC offset
-    of 20-100 and one channel at 400 (models/generic.py ln_offset): the default plan (no folding)
-    meets the fp32 bar; the opt-in fold is measured against it and must stay inside the looser
-    bar reported in docs/DESIGN.md (it is not the default for that reason)."""
+def test_fold_layernorm_offset_rows(native, gen_models):
+    """a folded LayerNorm computes rstd * (x.W' - mean * colsum) from the raw rows, so the
+    split-bf16 representation error of x (~2^-17 |x|) is amplified by |mean| / std.  The unfolded
+    LayerNorm reads the same stored x (x - mean formed from the same split planes), so it carries the
+    same amplified error; the fold adds only the fp32 accumulation of x.W' (~2^-24 |x|).  Measured on
+    rows with |mean| / std ~ 60 (models/generic.py ln_offset, MI355X): unfolded 2.1e-5, folded 3.6e-5
+    rel-L2.  Both must meet the fp32 bar, and the fold may not be much worse than the unfolded plan."""
     from die_amd.models import generic as G
 
     path = gen_models["ln_offset"]
-    eng = native.Engine(path, device="hip", max_batch=8, precision="fp32", autotune=False, fold_layernorm=fold)
-    try:
-        assert eng.refresh_info()["options"]["fold_layernorm"] is fold
-        x = G.synthetic_input("ln_offset", 8, seed=3)
-        ref = native.cpu_run(path, x).reshape(8, -1)
-        got = eng.run(x.reshape(8, -1))
-        err = _rel_l2(got, ref)
-        print("fold_layernorm=%s offset rows rel-L2 %.3e" % (fold, err))
-        assert err <= (1e-4 if not fold else 5e-2), (fold, err)
-    finally:
-        eng.close()
+    x = G.synthetic_input("ln_offset", 8, seed=3)
+    ref = native.cpu_run(path, x).reshape(8, -1)
+    errs = {}
+    for fold in (False, True):
+        eng = native.Engine(path, device="hip", max_batch=8, precision="fp32", autotune=False, fold_layernorm=fold)
+        try:
+            assert eng.refresh_info()["options"]["fold_layernorm"] is fold
+            errs[fold] = _rel_l2(eng.run(x.reshape(8, -1)), ref)
+        finally:
+            eng.close()
+    print("offset rows rel-L2: unfolded %.3e, folded %.3e" % (errs[False], errs[True]))
+    assert errs[False] <= 1e-4 and errs[True] <= 1e-4, errs
+    assert errs[True] <= 4 * errs[False] + 1e-6, errs
 
 
 def test_generic_mlp_served_over_http(native, gen_models):

@@ -56,11 +56,11 @@ def test_generic_models_plan_for_the_device(native, gen_models, name, precision)
     if name == "ln_wide":
         assert kinds.count("layernorm") == 2
     if name == "ln_offset":
-        # LayerNorm folding is opt-in: by default the LayerNorm normalises its rows itself
-        assert kinds.count("layernorm") == 1 and not any(o.get("stats_only") for o in s["ops"])
-        f = native.plan_summary(gen_models[name], 8, precision="fp32", fold_layernorm=True)
-        if precision == "fp32":
-            assert sum(1 for o in f["ops"] if o.get("stats_only")) == 1
+        # fp32 plans fold the LayerNorm into the MatMul (statistics only); bf16 plans never fold
+        assert kinds.count("layernorm") == 1
+        assert sum(1 for o in s["ops"] if o.get("stats_only")) == (1 if precision == "fp32" else 0)
+        f = native.plan_summary(gen_models[name], 8, precision=precision, fold_layernorm=False)
+        assert not any(o.get("stats_only") for o in f["ops"])
     if name == "bert_long":
         assert kinds.count("attention") == 1
 
@@ -102,9 +102,13 @@ def test_report_lists_every_unsupported_node(native, tmp_path):
     assert ops == ["Cos", "Sin"], r
     assert r["blocked"] == 2  # join + relu depend on them
     assert "Sin 'sin'" in r["text"] and "Cos 'cos'" in r["text"]
-    # an engine on "auto" keeps the reference's EP-style fallback and runs it on the CPU executor
+    # an engine on "auto" keeps the reference's EP-style fallback: without a GPU the whole graph runs
+    # on the CPU executor, with one the hybrid partition keeps the lowerable pieces on the GPU
+    # (tests/test_hybrid.py)
+    from conftest import gpu_available
+
     eng = native.Engine(p, device="auto", max_batch=2)
-    assert eng.refresh_info()["name"] == "cpu"
+    assert eng.refresh_info()["name"] == ("hybrid(hip,cpu)" if gpu_available() else "cpu")
     x = np.random.default_rng(1).standard_normal((2, 3 * 8 * 8)).astype(np.float32)
     np.testing.assert_allclose(eng.run(x), native.cpu_run(p, x.reshape(2, 3, 8, 8)).reshape(2, -1), rtol=1e-6)
     eng.close()

@@ -89,3 +89,33 @@ def test_scrambled_ids_match_the_load_generator(native):
     # the "ref" payload prints the number unpadded (like the reference's "req_N"); "full" and
     # "verify" bodies carry the fixed 10 digits request_ids() returns
     assert seen == ["r3_%d" % int(x[3:]) for x in rb.request_ids("r3_", 20)]
+
+
+def test_scramble_is_a_bijection():
+    """the id scramble must be injective (splitmix64(i) % 10^10 was not): the Feistel map
+    permutes [0, 10^10); checked exhaustively on a window and by inverting a sample."""
+    from die_amd.parallel import ring_balance as rb
+
+    n = 300000
+    xs = [rb.scramble_id(i) for i in range(n)]
+    assert len(set(xs)) == n and all(0 <= x < 10 ** 10 for x in xs)
+    half = 10 ** 5
+
+    def unscramble(y):  # run the 4 rounds backwards
+        left, right = divmod(y, half)
+        for k in reversed(range(4)):
+            left, right = (right - rb.splitmix64(left * 4 + k) % half) % half, left
+        return left * half + right
+
+    for i in (0, 1, 99999, 123456789, 10 ** 10 - 1):
+        assert unscramble(rb.scramble_id(i)) == i
+
+
+def test_reference_layout_prediction(native):
+    """bench.py reports the ring the reference's own deployment would get (ports 8001.., sequential
+    req_<i> ids) next to the balanced one."""
+    from die_amd.parallel import ring_balance as rb
+
+    r = rb.reference_layout(3, 3000)
+    assert r["ports"] == [8001, 8002, 8003] and abs(sum(r["shares"]) - 1.0) < 1e-6
+    assert r["max_over_fair"] >= 1.0
