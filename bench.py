@@ -102,6 +102,8 @@ def main():
                     help="run the projection-shortcut convs on a side stream (measured slower; off by default)")
     ap.add_argument("--attn-variant", type=int, default=0,
                     help="measurement: streaming attention variant (kernels.h set_attention_variant)")
+    ap.add_argument("--decode-variant", type=int, default=0,
+                    help="measurement: device JSON decode kernels, 0 symbol-level (default), 1 character-level (round 4)")
     ap.add_argument("--ln-xcd", type=int, default=0,
                     help="measurement: LayerNorm rows read on the XCD that wrote them (1) or in natural order (0, default)")
     ap.add_argument("--no-fold-layernorm", action="store_true",
@@ -133,6 +135,8 @@ def main():
                     help="N>1 gateway mode: ephemeral worker ports instead of ring-balanced ones")
     ap.add_argument("--no-gateway-bytes", action="store_true",
                     help="skip the extra pass with bodies re-sent over loopback HTTP (reference gateway hop)")
+    ap.add_argument("--conv-order", type=int, default=0,
+                    help="measurement: force every conv's XCD tile order (1 N-fastest, 2 M-fastest; EngineOptions)")
     ap.add_argument("--no-result-stream", action="store_true",
                     help="result D2H on the compute stream instead of a side stream (EngineOptions::result_stream)")
     ap.add_argument("--no-ref-client", action="store_true",
@@ -155,6 +159,8 @@ def main():
     from die_amd import native
     if args.device == "hip" and args.ln_xcd != 0:
         native.kernels().die_kern_set_layernorm_xcd(int(args.ln_xcd))
+    if args.device == "hip" and args.decode_variant != 0:
+        native.kernels().die_kern_set_decode_variant(int(args.decode_variant))
     if args.device == "hip" and args.attn_variant != 0:
         native.kernels().die_kern_set_attention_variant(int(args.attn_variant))
     from die_amd.parallel.launch import HostGroup
@@ -241,7 +247,7 @@ def main():
                    "exec_streams": args.exec_streams, "pace": not args.no_pace,
                    "pace_lead_scale": args.pace_lead_scale, "tune_warm_input": args.tune_warm_input,
                    "splitk_fused_margin": args.splitk_fused_margin, "splitk_two_kernel": args.splitk_two_kernel,
-                   "result_stream": not args.no_result_stream,
+                   "result_stream": not args.no_result_stream, "conv_order": args.conv_order,
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,

@@ -105,6 +105,7 @@ EngineOptions engine_opts(const Json& j) {
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
   e.splitk_two_kernel = jget<bool>(j, "splitk_two_kernel", e.splitk_two_kernel);
   e.result_stream = jget<bool>(j, "result_stream", e.result_stream);
+  e.conv_order = jget<int>(j, "conv_order", e.conv_order);
   e.fail_batch_every = jget<int>(j, "fail_batch_every", e.fail_batch_every);
   return e;
 }

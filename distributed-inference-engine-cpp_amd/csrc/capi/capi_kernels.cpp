@@ -174,6 +174,7 @@ int die_kern_gap_fc(uint64_t x, int B, int HW, int C, int mode, uint64_t w, long
 }
 
 void die_kern_set_attention_variant(int v) { kern::set_attention_variant(v); }
+void die_kern_set_decode_variant(int v) { kern::set_decode_variant(v); }
 void die_kern_set_layernorm_xcd(int v) { kern::set_layernorm_xcd(v); }
 
 int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,

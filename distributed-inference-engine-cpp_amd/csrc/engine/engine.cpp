@@ -298,6 +298,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["splitk_fused_margin"] = o.splitk_fused_margin;
   j["splitk_two_kernel"] = o.splitk_two_kernel;
   j["result_stream"] = o.result_stream;
+  j["conv_order"] = o.conv_order;
   j["fail_batch_every"] = o.fail_batch_every;
   return j;
 }

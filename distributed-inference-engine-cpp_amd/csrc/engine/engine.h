@@ -199,6 +199,9 @@ struct EngineOptions {
   // Each batch's result D2H (and data-parallel collectives) on a separate stream behind an event
   // after MAIN, instead of on the compute stream ahead of the next batch's MAIN.
   bool result_stream = true;
+  // Measurement: force every conv/GEMM's XCD tile order (ConvArgs::order; 0 = autotuned heuristic,
+  // 1 = N-fastest: each XCD owns the same row range in every layer, 2 = M-fastest).
+  int conv_order = 0;
   // A batch runs the hipGraph of the smallest bucket >= B; with live_batch the kernels read B from
   // the slot's table and skip the work of the bucket's padding samples.
   bool live_batch = true;

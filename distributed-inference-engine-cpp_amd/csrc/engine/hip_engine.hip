@@ -1078,7 +1078,7 @@ class HipEngine : public Engine {
           if (!use_live_) a.live = nullptr;
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
-          a.order = t.order;
+          a.order = opt_.conv_order > 0 ? opt_.conv_order : t.order;
           a.ws = side ? ws_side_ : wss_[s % n_exec_];
           if (side) a.counters = counters_side_;
           if (!t.fused) a.counters = nullptr;

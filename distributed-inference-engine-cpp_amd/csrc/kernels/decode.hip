@@ -633,7 +633,355 @@ __global__ __launch_bounds__(256) void dec_parse(const unsigned char* __restrict
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// 4-bit packed samples, decoded at the symbol (nibble) level.  The worker packs every request text
+// it can (core/textpack.cpp): symbols 0-9 digits, 10 ',', 11 '.', 12 '-', 13 '+', 14 'e', 15 ' '
+// (also the pad of an odd final symbol); symbol k of a sample = nibble k & 1 of packed byte k >> 1.
+// The kernels above expand those nibbles to characters first and then scan bytes (~3.9k VALU
+// instructions per 4 KiB chunk item); here separators, token starts and the common number shape
+// are found with 8-symbols-per-word SWAR on the nibbles themselves, and the token's digits, already
+// values 0-9, become the mantissa by a three-step BCD multiply-add.  Unusual tokens (exponents, > 8
+// digits, interior blanks, malformed) take the byte-wise converter through a nibble -> character
+// accessor, so acceptance, values and status bits are those of the character path (bit-identical
+// to the host parser).  Work item = one wave per PCH symbols, as above.
+// ------------------------------------------------------------------------------------------------
+constexpr int PCH = 4096;    // symbols per work item (2 KiB packed); = CHUNK: the same scratch layout
+constexpr int PHALO = 128;   // symbols past the chunk end the chunk's last token may reach
+constexpr int PPRE = 32;     // symbols staged before the chunk (16 bytes)
+constexpr int kPkStaged = (PPRE + PCH + PHALO) / 2;  // staged bytes per wave
+// LDS position of staged byte L: every lane's 32-byte region (the 64 symbols it scans for starts)
+// is followed by a 16-byte gap, so the 16 lanes of a ds_read_b128 group hit distinct banks
+__device__ __forceinline__ int ppos(int L) { return L + 16 * ((L + 16) >> 5); }
+constexpr int kPkLds = kPkStaged + 16 * ((kPkStaged + 16) / 32) + 16;
+
+// 0x8 in each nibble of x equal to v
+__device__ __forceinline__ uint32_t nib_eq(uint32_t x, uint32_t v) {
+  const uint32_t t = x ^ (v * 0x11111111u);
+  return ~(((t & 0x77777777u) + 0x77777777u) | t) & 0x88888888u;
+}
+__device__ __forceinline__ uint64_t nib_eq64(uint64_t x, uint64_t v) {
+  const uint64_t t = x ^ (v * 0x1111111111111111ull);
+  return ~(((t & 0x7777777777777777ull) + 0x7777777777777777ull) | t) & 0x8888888888888888ull;
+}
+// 8-bit mask (bit i = nibble i) from a 0x8-per-nibble word
+__device__ __forceinline__ uint32_t nib_mask8(uint32_t z) {
+  uint32_t m = (z >> 3) & 0x11111111u;
+  m = (m | (m >> 3)) & 0x03030303u;
+  m = (m | (m >> 6)) & 0x000F000Fu;
+  return (m | (m >> 12)) & 0xFFu;
+}
+// nibbles of w at symbol positions >= n (n = valid symbols of this 8-symbol word) set to 15 (blank)
+__device__ __forceinline__ uint32_t blank_from(uint32_t w, long long n) {
+  if (n >= 8) return w;
+  if (n <= 0) return 0xFFFFFFFFu;
+  return w | (0xFFFFFFFFu << (4 * static_cast<int>(n)));
+}
+__device__ __forceinline__ unsigned sym2chr(unsigned v) {
+  return v < 10 ? '0' + v : static_cast<unsigned>((0x20652B2D2E2Cull >> (8 * (v - 10))) & 0xFFu);
+}
+
+// Common number shape on a 64-bit window (symbol i = nibble i), n symbols before the separator:
+// [' '][-](0|[1-9][0-9]*)[.[0-9]+] with <= 8 digits -- one optional leading blank is json.dumps'
+// ", " separator.  Same single fp32 rounding as convert_token (mant <= 2^24 scaled by an exact
+// power of ten), so the bits equal the character path's.  false: let the byte-wise converter decide.
+__device__ __forceinline__ bool pk_fast(uint64_t w, int n, float& out) {
+  if (n >= 1 && (w & 0xFu) == 15u) {
+    w >>= 4;
+    --n;
+  }
+  const bool neg = n >= 1 && (w & 0xFu) == 12u;
+  if (neg) {
+    w >>= 4;
+    --n;
+  }
+  if (n < 1 || n > 10) return false;
+  const uint64_t in8 = ((1ull << (4 * n)) - 1) & 0x8888888888888888ull;  // bit 3 of the body's nibbles
+  const uint64_t ge10 = w & ((w << 1) | (w << 2)) & in8;                 // symbols 10-15
+  const uint64_t dots = nib_eq64(w, 11) & in8;
+  if (ge10 != dots || __popcll(dots) > 1) return false;  // every non-digit is the one '.'
+  const int dp = dots ? (__builtin_ctzll(dots) >> 2) : -1;
+  const int nd = n - (dp >= 0 ? 1 : 0);
+  if (nd < 1 || nd > 8 || dp == 0 || dp == n - 1) return false;
+  if ((w & 0xFu) == 0 && n > 1 && dp != 1) return false;  // a leading 0 is the whole integer part
+  uint64_t d = w;
+  if (dp >= 0) {
+    const uint64_t below = (1ull << (4 * dp)) - 1;
+    d = (w & below) | ((w >> 4) & ~below);
+  }
+  // the nd digits (most significant first = lowest nibble) right-aligned in 8 nibbles, leading zeros
+  // below them, then pairs -> hundreds -> the 8-digit value
+  uint32_t x = static_cast<uint32_t>(d << (4 * (8 - nd)));
+  x = (x & 0x0F0F0F0Fu) * 10u + ((x >> 4) & 0x0F0F0F0Fu);
+  x = (x & 0x00FF00FFu) * 100u + ((x >> 8) & 0x00FF00FFu);
+  const uint32_t mant = (x & 0xFFFFu) * 10000u + (x >> 16);
+  if (mant > (1u << 24)) return false;
+  const int frac = dp >= 0 ? n - dp - 1 : 0;
+  const float v = mant == 0 ? 0.f : (frac > 0 ? static_cast<float>(mant) / pow10f_small(frac) : static_cast<float>(mant));
+  out = __uint_as_float(__float_as_uint(v) | (static_cast<uint32_t>(neg) << 31));
+  return true;
+}
+
+// Packed sample b: 16 packed bytes at byte offset `bo` of the sample (bo % 16 == 0), symbols at or
+// beyond len blank; bytes before the sample read as separators (the symbol before 0 starts token 0).
+__device__ __forceinline__ uint4 pk_load16(const unsigned char* pk, long long bo, long long len) {
+  if (bo < 0) return make_uint4(0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu);
+  const long long s0 = 2 * bo;  // first symbol of these 16 bytes
+  if (s0 >= len) return make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  uint4 q = *reinterpret_cast<const uint4*>(pk + bo);
+  if (s0 + 32 > len) {
+    q.x = blank_from(q.x, len - s0);
+    q.y = blank_from(q.y, len - s0 - 8);
+    q.z = blank_from(q.z, len - s0 - 16);
+    q.w = blank_from(q.w, len - s0 - 24);
+  }
+  return q;
+}
+
+// A raw (unpacked) sample's character as a symbol: the packer's alphabet, plus 'E' as 'e' and
+// '\t' '\n' '\r' as ' ' (JSON gives them the same meaning in a number list); any other character is
+// `invalid` (the sample then goes to the host parser, which decides and reports).
+__device__ __forceinline__ uint32_t chr_to_sym(uint32_t c, bool& invalid) {
+  if (c - '0' <= 9u) return c - '0';
+  if (c == ',') return 10;
+  if (c == '.') return 11;
+  if (c == '-') return 12;
+  if (c == '+') return 13;
+  if ((c | 0x20u) == 'e') return 14;
+  if (c == ' ' || c == '\t' || c == '\n' || c == '\r') return 15;
+  invalid = true;
+  return 15;
+}
+
+// 32 symbols of sample b starting at symbol 2 * bo (bo % 16 == 0), packed (pk != nullptr) or
+// translated from raw characters at raw + 2 * bo (the rare unpackable texts); the blank /
+// separator rules of pk_load16.
+__device__ __forceinline__ uint4 sym_load16(const unsigned char* pk, const unsigned char* raw, long long bo,
+                                            long long len, bool& invalid) {
+  if (pk) return pk_load16(pk, bo, len);
+  if (bo < 0) return make_uint4(0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu);
+  const long long s0 = 2 * bo;
+  if (s0 >= len) return make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  const uint4 a = *reinterpret_cast<const uint4*>(raw + s0), c = *reinterpret_cast<const uint4*>(raw + s0 + 16);
+  const uint32_t ch[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    bool inv = false;
+    const uint32_t v = chr_to_sym((ch[k >> 2] >> (8 * (k & 3))) & 0xFFu, inv);
+    if (inv && s0 + k < len) invalid = true;  // bytes past the text are blanked below
+    w[k >> 3] |= v << (4 * (k & 7));
+  }
+  return make_uint4(blank_from(w[0], len - s0), blank_from(w[1], len - s0 - 8), blank_from(w[2], len - s0 - 16),
+                    blank_from(w[3], len - s0 - 24));
+}
+
+// the packed bytes of sample b (nullptr: raw characters at its text slot)
+__device__ __forceinline__ const unsigned char* pk_ptr(const unsigned char* packed, const long long* poffs, int b) {
+  return poffs[b] >= 0 ? packed + poffs[b] : nullptr;
+}
+
+// Separator count and "any non-blank" per PCH-symbol chunk of every packed sample; resets status
+// (and ntok of skipped samples) for EVERY sample -- this kernel runs first in a packed launch.
+__global__ __launch_bounds__(256) void pk_count(const unsigned char* __restrict__ packed,
+                                                const long long* __restrict__ poffs,
+                                                const unsigned char* __restrict__ text, long long cap,
+                                                const long long* __restrict__ offs,
+                                                const long long* __restrict__ lens, int B, int* __restrict__ counts,
+                                                int* __restrict__ blank, int* __restrict__ status,
+                                                int* __restrict__ ntok, int max_chunks) {
+  __shared__ int red[4];
+  __shared__ int pre[kDecMaxB];
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < B; b += 256) {
+      status[b] = 0;
+      if (lens[b] < 0) ntok[b] = -1;
+    }
+  }
+  int carry = 0;
+  for (int i0 = 0; i0 < B; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    int v = 0;
+    if (i < B) {
+      const long long len = lens[i];
+      v = len < 0 ? 0 : len == 0 ? 1 : static_cast<int>((len + PCH - 1) / PCH);
+    }
+    int tot;
+    const int ex = block_excl_scan(v, red, tot);
+    if (i < B) pre[i] = carry + ex;
+    carry += tot;
+  }
+  __syncthreads();
+  const int items = carry;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {
+    const int b = item_sample(pre, B, it), chunk = it - pre[b];
+    const long long len = lens[b];
+    const unsigned char* pk = pk_ptr(packed, poffs, b);
+    const unsigned char* raw = text + (offs ? offs[b] : b * cap);
+    // lane: 64 symbols (32 packed bytes) as two 16-byte words (a misaligned packed slot is not read:
+    // pk_parse sends that sample to the host parser)
+    const long long bo = static_cast<long long>(chunk) * (PCH / 2) + 32 * lane;
+    int c = 0, nb = 0;
+    bool inv = false;
+#pragma unroll
+    for (int k = 0; k < ((pk && (poffs[b] & 15)) ? 0 : 2); ++k) {
+      const uint4 q = sym_load16(pk, raw, bo + 16 * k, len, inv);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c += __popc(nib_eq(w[j], 10));
+        nb |= nib_eq(w[j], 15) != 0x88888888u;
+      }
+    }
+    c = wave_sum(c);
+    nb = wave_sum(nb);
+    if (lane == 0) {
+      counts[b * max_chunks + chunk] = c;
+      blank[b * max_chunks + chunk] = nb == 0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pk_parse(const unsigned char* __restrict__ packed,
+                                                const long long* __restrict__ poffs,
+                                                const unsigned char* __restrict__ text, long long cap,
+                                                const long long* __restrict__ offs,
+                                                const long long* __restrict__ lens, int B,
+                                                const int* __restrict__ counts, const int* __restrict__ blank,
+                                                int* __restrict__ status, int* __restrict__ ntok,
+                                                float* __restrict__ out, long long numel, int max_chunks) {
+  __shared__ __attribute__((aligned(16))) unsigned char sbuf[4][kPkLds];
+  __shared__ int red[4];
+  __shared__ int pre[kDecMaxB];
+  int carry = 0;
+  for (int i0 = 0; i0 < B; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    int v = 0;
+    if (i < B) {
+      const long long len = lens[i];
+      v = len < 0 ? 0 : len == 0 ? 1 : static_cast<int>((len + PCH - 1) / PCH);
+    }
+    int tot;
+    const int ex = block_excl_scan(v, red, tot);
+    if (i < B) pre[i] = carry + ex;
+    carry += tot;
+  }
+  __syncthreads();
+  const int items = carry;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char* buf = sbuf[wave];
+  // symbol j of the staged window (j = chunk symbol + PPRE)
+  auto sym = [&](int j) -> unsigned { return (buf[ppos(j >> 1)] >> (4 * (j & 1))) & 0xFu; };
+  auto word = [&](int L) -> uint32_t { return *reinterpret_cast<const uint32_t*>(buf + ppos(L)); };  // L % 4 == 0
+  constexpr int kNone = 1 << 30;
+  for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {
+    const int b = item_sample(pre, B, it), chunk = it - pre[b];
+    const long long len = lens[b];
+    const long long c0 = static_cast<long long>(chunk) * PCH;
+    const bool last = c0 + PCH >= len;
+    const int* crow = counts + static_cast<size_t>(b) * max_chunks;
+    int s = 0, nbv = 0;
+    for (int c = lane; c < chunk; c += 64) s += crow[c];
+    if (last)
+      for (int c = lane; c <= chunk; c += 64) nbv |= !blank[static_cast<size_t>(b) * max_chunks + c];
+    const int prefix = wave_sum(s);
+    const int anynb = last ? wave_sum(nbv) : 0;
+    const unsigned char* pk = pk_ptr(packed, poffs, b);
+    const unsigned char* raw = text + (offs ? offs[b] : b * cap);
+    bool bad = false;
+    if (pk && (poffs[b] & 15) != 0) {  // the kernels read 16-byte words: a misaligned slot goes to the host parser
+      bad = lane == 0;
+    } else if (c0 < len) {
+      const int lim = static_cast<int>(len - c0 < PCH + PHALO ? len - c0 : PCH + PHALO);  // chunk symbols of text
+      // stage the symbols [c0 - 32, c0 + PCH + PHALO) (packed bytes; raw samples translated on load)
+      bool inv = false;
+      for (int i = lane; i < kPkStaged / 16; i += 64) {
+        const uint4 q = sym_load16(pk, raw, c0 / 2 - PPRE / 2 + 16ll * i, len, inv);
+        *reinterpret_cast<uint4*>(buf + ppos(16 * i)) = q;
+      }
+      bad = inv;  // a character outside the number alphabet: the host parser decides (and reports it)
+      wave_lds_sync();
+      // Token starts among my 64 symbols [64 lane, 64 lane + 64) of the chunk (the symbol after a ','),
+      // kept in a register mask: each lane converts the tokens that start in its own region, in order,
+      // so no start list is compacted through LDS.  A token ends at the next start (mine, or the first
+      // one of a later lane: a suffix minimum over the lanes); the chunk's last token at the next ','
+      // in the staged halo or the end of the text.
+      const int L0 = PPRE / 2 + 32 * lane;  // staged byte of my first symbol
+      const uint4 q0 = *reinterpret_cast<const uint4*>(buf + ppos(L0));
+      const uint4 q1 = *reinterpret_cast<const uint4*>(buf + ppos(L0 + 16));
+      const uint64_t cm = static_cast<uint64_t>(nib_mask8(nib_eq(q0.x, 10)) | (nib_mask8(nib_eq(q0.y, 10)) << 8) |
+                                                (nib_mask8(nib_eq(q0.z, 10)) << 16) | (nib_mask8(nib_eq(q0.w, 10)) << 24)) |
+                          (static_cast<uint64_t>(nib_mask8(nib_eq(q1.x, 10)) | (nib_mask8(nib_eq(q1.y, 10)) << 8) |
+                                                 (nib_mask8(nib_eq(q1.z, 10)) << 16) | (nib_mask8(nib_eq(q1.w, 10)) << 24))
+                           << 32);
+      const int lo = 64 * lane;  // chunk symbol of bit 0
+      uint64_t sm = (cm << 1) | (sym(PPRE + lo - 1) == 10u ? 1ull : 0ull);
+      if (lo + 64 > lim) sm &= lim > lo ? (1ull << (lim - lo)) - 1ull : 0ull;
+      if (lo + 64 > PCH) sm &= lo < PCH ? (1ull << (PCH - lo)) - 1ull : 0ull;  // starts past the chunk: next item's
+      int total;
+      const int k0 = wave_excl_scan(__popcll(sm), total);
+      // first start of the lanes after me
+      int nxt = sm ? lo + __builtin_ctzll(sm) : kNone;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_down(nxt, o, 64);
+        if (lane + o < 64) nxt = min(nxt, y);
+      }
+      nxt = __shfl_down(nxt, 1, 64);
+      if (lane == 63) nxt = kNone;
+      const long long base = static_cast<long long>(prefix) + (sym(PPRE - 1) != 10u ? 1 : 0) + k0;
+      bad |= lane == 0 && last && len > 0 && sym(PPRE + static_cast<int>(len - c0) - 1) == 10u;  // trailing ','
+      float* orow = out + b * numel;
+      for (long long idx = base; sm; ++idx) {  // idx >= numel: validated, not stored
+        const int p = lo + __builtin_ctzll(sm);
+        sm &= sm - 1;
+        const int e_start = sm ? lo + __builtin_ctzll(sm) : nxt;  // the next token's start
+        int n;
+        bool too_long = false;
+        if (e_start != kNone) {
+          n = e_start - 1 - p;
+        } else {  // the chunk's last token: up to the next ',' in the staged halo, or the end of the text
+          int e = p;
+          while (e < lim && sym(PPRE + e) != 10u) ++e;
+          n = e - p;
+          too_long = e == lim && lim == PCH + PHALO && len - c0 > PCH + PHALO;  // runs past the halo
+        }
+        float v = 0.f;
+        bool good = false;
+        if (!too_long) {
+          if (n <= 16) {  // 64-bit window from three staged words
+            const int j = PPRE + p, L = j >> 1, a4 = L & ~3;
+            const uint64_t w01 = static_cast<uint64_t>(word(a4)) | (static_cast<uint64_t>(word(a4 + 4)) << 32);
+            const uint64_t w2 = word(a4 + 8);
+            const int sh = 8 * (L & 3) + 4 * (j & 1);
+            const uint64_t w = sh ? (w01 >> sh) | (w2 << (64 - sh)) : w01;
+            good = pk_fast(w, n, v);
+          }
+          if (!good) good = convert_token([&](int i) -> unsigned { return sym2chr(sym(PPRE + p + i)); }, n, v);
+        }
+        if (good && idx < numel) orow[idx] = v;
+        bad |= !good;
+      }
+    }
+    if (bad) atomicOr(status + b, 1);
+    if (last) {  // the sample's token count, overflow status and zero-filled tail
+      const long long n = anynb ? static_cast<long long>(prefix) + crow[chunk] + 1 : 0;
+      if (lane == 0) {
+        ntok[b] = static_cast<int>(n);
+        if (n > numel) atomicOr(status + b, 2);
+      }
+      float* o = out + b * numel;
+      for (long long i = n + lane; i < numel; i += 64) o[i] = 0.f;
+    }
+    wave_lds_sync();  // every lane done reading buf before the next item's staging
+  }
+}
+int g_decode_variant = 0;
+
 }  // namespace
+
+void set_decode_variant(int v) { g_decode_variant = v; }
 
 size_t decode_scratch_bytes(int max_batch, size_t text_cap) {
   const size_t chunks = (text_cap + CHUNK - 1) / CHUNK;
@@ -655,6 +1003,15 @@ hipError_t decode_json_numbers(const unsigned char* text, const long long* offs,
     const long long* o = offs ? offs + b0 : nullptr;
     const long long* po = poffs ? poffs + b0 : nullptr;
     const int grid = static_cast<int>(std::min<long long>((static_cast<long long>(max_chunks) * nb + 3) / 4, kDecGrid));
+    if (packed && po && g_decode_variant == 0) {
+      // the symbol-level kernels: packed samples read as nibbles, raw ones translated on load
+      hipLaunchKernelGGL(pk_count, dim3(grid), dim3(256), 0, s, packed, po, t, static_cast<long long>(text_cap), o,
+                         lens + b0, nb, counts, blank, status + b0, ntok + b0, max_chunks);
+      hipLaunchKernelGGL(pk_parse, dim3(grid), dim3(256), 0, s, packed, po, t, static_cast<long long>(text_cap), o,
+                         lens + b0, nb, counts, blank, status + b0, ntok + b0, out + static_cast<size_t>(b0) * numel, numel,
+                         max_chunks);
+      continue;
+    }
     hipLaunchKernelGGL(dec_count, dim3(grid), dim3(256), 0, s, t, static_cast<long long>(text_cap), o, packed, po,
                        lens + b0, nb, counts, blank, status + b0, ntok + b0, max_chunks);
     hipLaunchKernelGGL(dec_parse, dim3(grid), dim3(256), 0, s, t, static_cast<long long>(text_cap), o, packed, po,

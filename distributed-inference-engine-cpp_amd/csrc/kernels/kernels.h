@@ -285,6 +285,9 @@ size_t decode_scratch_bytes(int max_batch, size_t text_cap);
 // packed/poffs (optional): sample b's lens[b] characters are 4-bit packed (core/textpack.h) at
 // packed + poffs[b] (8-byte aligned, in a slot of text_cap / 2 bytes) and expanded in registers as
 // the decode kernels load them; poffs[b] < 0 (or packed == nullptr) reads raw text at text + offs[b].
+// Measurement switch (process-wide): 0 = packed launches decode on the symbol (nibble) kernels
+// (default), 1 = the character kernels for every launch (the round-4 path).
+void set_decode_variant(int v);
 hipError_t decode_json_numbers(const unsigned char* text, const long long* offs, size_t text_cap,
                                const long long* lens, int B, float* out, long long numel, int* status, int* ntok,
                                void* scratch, hipStream_t s, const unsigned char* packed = nullptr,

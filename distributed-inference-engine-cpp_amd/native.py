@@ -688,6 +688,8 @@ def _sig_kernels():
     L.die_kern_attention.argtypes = [u64] * 4 + [i] * 8 + [C.c_float, u64, i]
     L.die_kern_set_attention_variant.restype = None
     L.die_kern_set_attention_variant.argtypes = [i]
+    L.die_kern_set_decode_variant.restype = None
+    L.die_kern_set_decode_variant.argtypes = [i]
     L.die_kern_set_layernorm_xcd.restype = None
     L.die_kern_set_layernorm_xcd.argtypes = [i]
     L.die_kern_set_gap_fc_stop.restype = None

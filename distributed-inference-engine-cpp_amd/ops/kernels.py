@@ -375,10 +375,12 @@ def attention_qkv_split(qkv, heads, scale=None):
 
 # ---- device JSON decode (csrc/kernels/decode.hip) ---------------------------------------------------
 
-def decode_json_numbers(texts, numel, text_cap=None, slot_order=None):
+def decode_json_numbers(texts, numel, text_cap=None, slot_order=None, packed=False):
     """Decode number-list texts (bytes, the inside of a JSON array; None = skipped sample) on the GPU.
     slot_order: optional permutation; sample i's text is then placed in arena slot slot_order[i]
     and located through the per-sample offset table (the engine's staged-upload layout).
+    packed: upload every text that packs (core/textpack.h) 4-bit packed, the worker's default (the
+    nibble-level kernels decode those; the rest stays raw).
     Returns (values [B, numel] f32, status [B] int32, ntok [B] int32) as torch tensors."""
     import torch
 
@@ -406,8 +408,23 @@ def decode_json_numbers(texts, numel, text_cap=None, slot_order=None):
     status = torch.full((B,), -7, dtype=torch.int32, device="cuda")
     ntok = torch.zeros(B, dtype=torch.int32, device="cuda")
     scratch = torch.empty(int(L.die_decode_scratch_bytes(B, text_cap)), dtype=torch.uint8, device="cuda")
-    rc = L.die_kern_decode(_ptr(d_text), _ptr(d_offs), text_cap, _ptr(d_lens), B, _ptr(out), numel, _ptr(status),
-                           _ptr(ntok), _ptr(scratch), _stream())
+    if packed:
+        hp = np.zeros(nslots * text_cap // 2, np.uint8)
+        poffs = np.full(B, -1, np.int64)
+        for i, t in enumerate(texts):
+            pk = native.pack_nibbles(t) if t is not None else None
+            if pk is not None:
+                poffs[i] = slots[i] * (text_cap // 2)
+                hp[poffs[i]:poffs[i] + len(pk)] = np.frombuffer(pk, np.uint8)
+        d_packed = torch.from_numpy(hp).cuda()
+        d_poffs = torch.from_numpy(poffs).cuda()
+        if d_offs is None:
+            d_offs = torch.from_numpy(offs).cuda()
+        rc = L.die_kern_decode_packed(_ptr(d_text), _ptr(d_offs), _ptr(d_packed), _ptr(d_poffs), text_cap, _ptr(d_lens),
+                                      B, _ptr(out), numel, _ptr(status), _ptr(ntok), _ptr(scratch), _stream())
+    else:
+        rc = L.die_kern_decode(_ptr(d_text), _ptr(d_offs), text_cap, _ptr(d_lens), B, _ptr(out), numel, _ptr(status),
+                               _ptr(ntok), _ptr(scratch), _stream())
     _check(rc, "decode_json_numbers")
     return out, status, ntok
 

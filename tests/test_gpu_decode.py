@@ -311,3 +311,66 @@ def test_decode_long_tokens_across_lanes_and_chunks(native):
     assert st in (0, 1)  # 1: a double-rounding hazard sent the sample to the host parser
     if st == 0:
         np.testing.assert_array_equal(vals.cpu().numpy()[0].view(np.uint32), hv.view(np.uint32))
+
+
+def _pk_cases():
+    t = _texts()
+    rng = np.random.default_rng(5)
+    extra = {
+        "neg_4dec": ",".join("%.4f" % x for x in rng.random(3000) * 2 - 1),
+        "dumps": ", ".join(repr(float(x)) for x in np.round(rng.random(3000), 4).astype(np.float32)),
+        "mixed_len": ",".join(str(round(float(x), int(k))) for x, k in zip(rng.random(3000) * 100, rng.integers(0, 8, 3000))),
+        "eight_digits": ",".join("%.8f" % x for x in rng.random(2000)) + ",16777216,16777217,99999999,0.00000001",
+        "trailing_comma": "1,2,3,",
+        "empty": "",
+        "blank": " ",
+        "lead_blank": " 1.5, -2.25,  3",
+        "leading_zero": "0.5,01,0.25",
+        "one": "7",
+    }
+    for k, v in extra.items():
+        t[k] = v.encode()
+    for j, bad in enumerate([b"1.", b".5", b"1,,2", b"1e", b"+1", b"--1", b"1" * 70, b"1e-50", b"3e39", b"1 2"]):
+        t["bad%d" % j] = b"0.5," + bad + b",0.25"
+    return t
+
+
+@pytest.mark.parametrize("cap", [None, 256 * 1024])
+def test_decode_packed_nibble_path_matches_raw(native, cap):
+    """The nibble-level kernels (pk_count / pk_parse) that decode 4-bit packed samples give exactly the
+    status, token count and value bits of the character kernels on the same texts: number shapes,
+    json.dumps ", " separators, > 8 digits, exponents, blanks, and every error class (round 5)."""
+    from die_amd.ops import kernels as K
+
+    cases = _pk_cases()
+    names = list(cases)
+    texts = [cases[k] for k in names] + [None]
+    assert native.pack_nibbles(cases["4dec_unit"]) is not None and native.pack_nibbles(cases["spaces"]) is None
+    numel = 6000
+    raw = [x.cpu().numpy() for x in K.decode_json_numbers(texts, numel, text_cap=cap)]
+    pk = [x.cpu().numpy() for x in K.decode_json_numbers(texts, numel, text_cap=cap, packed=True)]
+    for i, k in enumerate(names + ["skipped"]):
+        assert pk[1][i] == raw[1][i], (k, pk[1][i], raw[1][i])
+        assert pk[2][i] == raw[2][i], (k, pk[2][i], raw[2][i])
+        if raw[1][i] == 0:
+            np.testing.assert_array_equal(pk[0][i].view(np.uint32), raw[0][i].view(np.uint32), err_msg=k)
+    st = dict(zip(names, raw[1]))
+    assert st["4dec_unit"] == 0 and st["dumps"] == 0 and st["lead_blank"] == 0 and st["neg_4dec"] == 0
+    assert st["trailing_comma"] & 1 and st["leading_zero"] & 1 and all(st["bad%d" % j] & 1 for j in range(10))
+
+
+def test_decode_packed_long_text_multi_chunk(native):
+    """A ResNet-sized packed sample (~1 MB of text, ~257 chunks, tokens straddling chunk edges) and a
+    slot-permuted batch: bit-exact against the host parser."""
+    from die_amd.ops import kernels as K
+
+    rng = np.random.default_rng(9)
+    text = ",".join("%.4f" % v for v in rng.random(150528)).encode()
+    short = b"1,2,3"
+    vals, status, ntok = K.decode_json_numbers([text, short, text], 150528, packed=True, slot_order=[2, 0, 1])
+    hv, hn = _host(native, text, 150528)
+    assert status.cpu().tolist() == [0, 0, 0] and ntok.cpu().tolist() == [150528, 3, 150528]
+    got = vals.cpu().numpy()
+    np.testing.assert_array_equal(got[0].view(np.uint32), hv.view(np.uint32))
+    np.testing.assert_array_equal(got[2], got[0])
+    assert list(got[1, :4]) == [1.0, 2.0, 3.0, 0.0] and not got[1, 3:].any()
