@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--no-fold-layernorm", action="store_true",
                     help="standalone LayerNorms instead of statistics + GEMM-epilogue normalisation "
                          "(EngineOptions::fold_layernorm)")
+    ap.add_argument("--no-ln-stats-epilogue", action="store_true",
+                    help="measurement: LayerNorm statistics by their own launch instead of the producing "
+                         "GEMM's epilogue (EngineOptions::ln_stats_epilogue)")
     ap.add_argument("--fuse-gap-fc", action="store_true",
                     help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true",
@@ -251,7 +254,8 @@ def main():
                    "pack_text": not args.no_pack_text, "branch_streams": args.branch_streams,
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
-                   "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm}
+                   "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
+                   "ln_stats_epilogue": not args.no_ln_stats_epilogue}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

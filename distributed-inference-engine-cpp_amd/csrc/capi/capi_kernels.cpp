@@ -74,6 +74,12 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     a.counters_n = geti(j, "counters_n", 0);
     a.split = geti(j, "split", 0);
     if (auto* v = j.find("wplane")) a.wplane = v->as_int();
+    // LayerNorm folding / statistics (ConvArgs::row_stats, col_sum, row_parts, stats_out, ln_eps)
+    if (auto* v = j.find("row_stats")) a.row_stats = P<const float>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("col_sum")) a.col_sum = P<const float>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("row_parts")) a.row_parts = P<const float>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("stats_out")) a.stats_out = P<float>(static_cast<uint64_t>(v->as_int()));
+    if (auto* v = j.find("ln_eps")) a.ln_eps = static_cast<float>(v->as_double());
     if (tile < 0) tile = kern::choose_tile(a.M, a.N, a.K);
     return static_cast<int>(kern::conv_igemm(a, tile, S(stream)));
   } catch (...) {
@@ -305,11 +311,12 @@ char* die_hybrid_partition(const char* model_path, int max_batch, int split, cha
   }
 }
 
-// fuse: bit 0 conv pairs, bit 1 stem + pool, bit 2 global pool + FC head, bit 3 LayerNorm folding
+// fuse: bit 0 conv pairs, bit 1 stem + pool, bit 2 global pool + FC head, bit 3 LayerNorm folding,
+// bit 4 LayerNorm statistics from the producing GEMM's epilogue
 char* die_plan_summary(const char* model_path, int max_batch, int side_branches, int split, int fuse, char** err) {
   try {
     Plan p = build_plan(onnx::load_onnx(model_path), max_batch, side_branches != 0, split != 0, false, (fuse & 1) != 0,
-                        (fuse & 2) != 0, (fuse & 4) != 0, (fuse & 8) != 0);
+                        (fuse & 2) != 0, (fuse & 4) != 0, (fuse & 8) != 0, (fuse & 16) != 0);
     Json j = Json::object();
     j["summary"] = p.summary();
     j["arena_bytes"] = static_cast<long long>(p.arena_bytes);
@@ -329,9 +336,9 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
       e["join"] = o.join;
       // arena ranges [offset, offset + bytes) at max_batch of the op's buffers, by role
       Json bufs = Json::object();
-      const char* roles[] = {"in", "in2", "in3", "out", "out2", "out3"};
-      const int ids[] = {o.in, o.in2, o.in3, o.out, o.out2, o.out3};
-      for (int r = 0; r < 6; ++r)
+      const char* roles[] = {"in", "in2", "in3", "out", "out2", "out3", "out_stats"};
+      const int ids[] = {o.in, o.in2, o.in3, o.out, o.out2, o.out3, o.out_stats};
+      for (int r = 0; r < 7; ++r)
         if (ids[r] >= 0) {
           Json range = Json::array();
           range.push_back(static_cast<long long>(p.bufs[ids[r]].offset));
@@ -353,6 +360,8 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["act"] = o.conv.relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
         e["layernorm_folded"] = o.colsum_off != SIZE_MAX;
+        e["stats_out"] = o.out_stats >= 0;            // writes LayerNorm statistics partials
+        e["stats_from_producer"] = o.in3_parts != 0;  // reads (merges) them
       }
       if (o.kind == PlanOp::LAYERNORM) e["stats_only"] = o.stats_only != 0;
       if (o.kind == PlanOp::STEM) {

@@ -243,6 +243,9 @@ struct EngineOptions {
   // LayerNorm -> GEMM readers: statistics only, the normalisation in the GEMM epilogue (ViT-B/16
   // B=32: 5,143 -> 5,075 us per forward on one box, profiles/r4_fold_layernorm.md); fp32 mode only
   bool fold_layernorm = true;
+  // ... and the statistics of a LayerNorm whose input a GEMM produces come from that GEMM's
+  // epilogue (per-64-column partials, ConvArgs::stats_out / row_parts): no statistics launch
+  bool ln_stats_epilogue = true;
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)

@@ -64,7 +64,8 @@ class HipEngine : public Engine {
     depth_ = std::max(1, std::min(opt.pipeline_depth, 4));
     // fp32 (the reference's ORT numerics): split hi/lo bf16 operands on the matrix cores
     plan_ = build_plan(model, max_batch_, opt.branch_streams && opt.exec_streams <= 1, opt.precision == "fp32", opt.bn_on_load,
-                       opt.fuse_pairs, opt.fuse_stem_pool, opt.fuse_gap_fc, opt.fold_layernorm);
+                       opt.fuse_pairs, opt.fuse_stem_pool, opt.fuse_gap_fc, opt.fold_layernorm,
+                       opt.ln_stats_epilogue);
     sp_ = plan_.split ? 1 : 0;
     while (n_prep_ops_ < plan_.ops.size() && plan_.ops[n_prep_ops_].kind == PlanOp::INPUT_PREP) {
       prep_out_ids_.push_back(plan_.ops[n_prep_ops_].out);
@@ -848,7 +849,11 @@ class HipEngine : public Engine {
     a.in_scale = prm_ptr(op.in_scale_off);
     a.in_shift = prm_ptr(op.in_shift_off);
     a.in_relu = op.in_relu;
-    a.row_stats = op.in3 >= 0 ? static_cast<const float*>(buf_ptr(op.in3, s)) : nullptr;
+    const float* in3 = op.in3 >= 0 ? static_cast<const float*>(buf_ptr(op.in3, s)) : nullptr;
+    a.row_stats = op.in3_parts ? nullptr : in3;
+    a.row_parts = op.in3_parts ? in3 : nullptr;
+    a.ln_eps = op.eps;
+    a.stats_out = op.out_stats >= 0 ? static_cast<float*>(buf_ptr(op.out_stats, s)) : nullptr;
     a.col_sum = prm_ptr(op.colsum_off);
     return a;
   }
@@ -918,7 +923,8 @@ class HipEngine : public Engine {
           }
         // identical problems (repeated blocks) share one measurement
         char key[256];
-        std::snprintf(key, sizeof(key), "o%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "",
+        std::snprintf(key, sizeof(key), "o%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "",
+                      base.stats_out || base.row_parts ? "ls:" : "",
                       opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : "", base.M, base.N, base.K, base.Cin,
                       base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
                       base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);

@@ -87,10 +87,11 @@ int round8(int c) { return (c + 7) / 8 * 8; }
 class Planner {
  public:
   Planner(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs = true,
-          bool fuse_stem_pool = true, bool fuse_gap_fc = false, bool fold_layernorm = true)
+          bool fuse_stem_pool = true, bool fuse_gap_fc = false, bool fold_layernorm = true,
+          bool ln_stats_epilogue = true)
       : m_(m), max_batch_(max_batch), side_branches_(side_branches), split_(split), bn_on_load_(bn_on_load),
         fuse_pairs_(fuse_pairs), fuse_stem_pool_(fuse_stem_pool), fuse_gap_fc_(fuse_gap_fc),
-        fold_layernorm_(fold_layernorm) {}
+        fold_layernorm_(fold_layernorm), ln_stats_epilogue_(ln_stats_epilogue) {}
 
   // Every node is tried; a node that cannot be lowered is recorded (with its error) and its
   // outputs become UNKNOWN, so the walk goes on and the report lists every unsupported node.
@@ -136,6 +137,7 @@ class Planner {
     // fp32 (split) mode only: in bf16 the weights re-rounded with gamma folded in and the mean
     // subtracted after a bf16-input GEMM cost ViT-B/16 ~3 % of its rel-L2 budget
     if (fold_layernorm_ && split_) fold_layernorm();
+    if (fold_layernorm_ && split_ && ln_stats_epilogue_) stats_from_producer();
     if (bn_on_load_ && !split_) preact_on_load();  // measured slower (profiles/r1_preact_on_load.md)
     if (side_branches_) mark_side_branches();
     assign_arena();
@@ -2503,6 +2505,56 @@ class Planner {
     }
   }
 
+  // Statistics-only LayerNorm whose input is the stored output of a rows GEMM (ViT pre-norm
+  // blocks: the attention-out and MLP2 GEMMs, residual add in their epilogue) -> deleted.  That GEMM
+  // also writes per-(row, 64-column group) (mean, M2) partials from the values it holds in registers
+  // (ConvArgs::stats_out), and every block of a folded reader merges its rows' groups in a fixed
+  // order while its first operand tiles load (ConvArgs::row_parts): no launch, no re-read of the rows.
+  // The block-0 LayerNorm (input from the token assembly) keeps its statistics op.
+  void stats_from_producer() {
+    const int nops = static_cast<int>(plan_.ops.size());
+    std::vector<std::vector<int>> readers(plan_.bufs.size());
+    for (int i = 0; i < nops; ++i)
+      for (int b : {plan_.ops[i].in, plan_.ops[i].in2, plan_.ops[i].in3})
+        if (b >= 0) readers[b].push_back(i);
+    std::vector<int> writer(plan_.bufs.size(), -1);  // latest op writing each buffer
+    std::vector<bool> drop(nops, false);
+    for (int i = 0; i < nops; ++i) {
+      PlanOp& p = plan_.ops[i];
+      const int w = p.kind == PlanOp::LAYERNORM && p.stats_only && p.in >= 0 ? writer[p.in] : -1;
+      if (w >= 0 && p.C == p.Cp && p.C % 64 == 0 && p.C <= 2048 && p.join < 0) {
+        PlanOp& q = plan_.ops[w];
+        const kern::ConvArgs& c = q.conv;
+        bool ok = q.kind == PlanOp::CONV && q.out == p.in && q.out_stats < 0 && q.join < 0 && c.N == p.C &&
+                  c.Ho * c.Wo == p.rows_per_sample && q.out2 < 0;
+        for (int j : readers[p.out]) {
+          const PlanOp& r = plan_.ops[j];
+          ok = ok && j > i && r.kind == PlanOp::CONV && r.in3 == p.out && r.colsum_off != SIZE_MAX &&
+               r.conv.N % 8 == 0 && r.conv.K == p.C && r.join < 0;
+        }
+        if (ok && !readers[p.out].empty()) {
+          const int st = new_buf(static_cast<size_t>(p.rows_per_sample) * (p.C / 64) * 2 * 4);
+          q.out_stats = st;
+          q.name += "+stats";
+          for (int j : readers[p.out]) {
+            PlanOp& r = plan_.ops[j];
+            r.in3 = st;
+            r.in3_parts = 1;
+            r.eps = p.eps;
+          }
+          drop[i] = true;
+        }
+      }
+      for (int b : {p.out, p.out2, p.out3, p.out_f32})
+        if (b >= 0) writer[b] = i;
+    }
+    std::vector<PlanOp> out;
+    out.reserve(plan_.ops.size());
+    for (int i = 0; i < nops; ++i)
+      if (!drop[i]) out.push_back(std::move(plan_.ops[i]));
+    plan_.ops = std::move(out);
+  }
+
   // Back-to-back 1x1 pair (ResNet-v2 bottleneck boundary).  A dual-store expand conv P writes the
   // raw sum x (next residual) and a = act(bn(x)); when a's ONLY reader is a plain 1x1/s1 reduce conv
   // Q, both become one CONV_PAIR op at P's position (Q has no other input, so computing it early is
@@ -2626,7 +2678,7 @@ class Planner {
     int open_until = -1;
     for (int i = 0; i < nops; ++i) {
       PlanOp& p = plan_.ops[i];
-      if (i <= open_until || p.kind != PlanOp::CONV || p.out < 0 || p.out_f32 >= 0) continue;
+      if (i <= open_until || p.kind != PlanOp::CONV || p.out < 0 || p.out_f32 >= 0 || p.out_stats >= 0) continue;
       int j = -1;
       for (int k = i + 1; k < nops && j < 0; ++k) {
         const PlanOp& q = plan_.ops[k];
@@ -2643,9 +2695,9 @@ class Planner {
     const int nops = static_cast<int>(plan_.ops.size());
     for (int i = 0; i < nops; ++i) {
       const PlanOp& p = plan_.ops[i];
-      for (int b : {p.out, p.out2, p.out3})
+      for (int b : {p.out, p.out2, p.out3, p.out_stats})
         if (b >= 0 && plan_.bufs[b].first_use < 0) plan_.bufs[b].first_use = i;
-      for (int b : {p.in, p.in2, p.in3, p.out, p.out2, p.out3})
+      for (int b : {p.in, p.in2, p.in3, p.out, p.out2, p.out3, p.out_stats})
         if (b >= 0) plan_.bufs[b].last_use = std::max(plan_.bufs[b].last_use, i);
       // a side branch may still be reading its inputs until its join
       if (p.join >= 0)
@@ -2700,6 +2752,7 @@ class Planner {
   bool fuse_stem_pool_ = true;  // EngineOptions::fuse_stem_pool
   bool fuse_gap_fc_ = false;    // EngineOptions::fuse_gap_fc
   bool fold_layernorm_ = true;  // EngineOptions::fold_layernorm
+  bool ln_stats_epilogue_ = true;  // EngineOptions::ln_stats_epilogue
   Plan plan_;
   std::vector<Val> vals_;
   std::unordered_map<std::string, int> vid_;
@@ -2800,14 +2853,14 @@ onnx::Model rewrite_conv_transpose(const onnx::Model& src) {
 }  // namespace
 
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches, bool split, bool bn_on_load, bool fuse_pairs,
-                bool fuse_stem_pool, bool fuse_gap_fc, bool fold_layernorm) {
+                bool fuse_stem_pool, bool fuse_gap_fc, bool fold_layernorm, bool ln_stats_epilogue) {
   if (has_conv_transpose(m)) {
     const onnx::Model r = rewrite_conv_transpose(m);
     return Planner(r, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc,
-                   fold_layernorm).run();
+                   fold_layernorm, ln_stats_epilogue).run();
   }
   return Planner(m, max_batch, side_branches, split, bn_on_load, fuse_pairs, fuse_stem_pool, fuse_gap_fc,
-                 fold_layernorm).run();
+                 fold_layernorm, ln_stats_epilogue).run();
 }
 
 std::string PlanReport::text() const {

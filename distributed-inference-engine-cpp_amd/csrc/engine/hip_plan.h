@@ -101,6 +101,12 @@ struct PlanOp {
   // bias and colsum_off = the per-column sums of its weights (ConvArgs::row_stats / col_sum).
   int stats_only = 0;
   size_t colsum_off = SIZE_MAX;
+  // LayerNorm statistics from the producer's epilogue (stats_from_producer): the CONV that writes a
+  // statistics-only LayerNorm's input also writes out_stats = the [M][N/64] (mean, M2) column-group
+  // partials (ConvArgs::stats_out), the LayerNorm op is gone, and its folded readers have
+  // in3 = out_stats, in3_parts = 1 (ConvArgs::row_parts) and eps = the LayerNorm's epsilon.
+  int out_stats = -1;
+  int in3_parts = 0;
 };
 
 struct Plan {
@@ -132,9 +138,11 @@ struct PlanUnsupported : std::runtime_error {
 // fuse_stem_pool: stem conv + max pool in one STEM op (EngineOptions::fuse_stem_pool).
 // fuse_gap_fc: global pool + the FC head reading it in one GAP_FC op (EngineOptions::fuse_gap_fc).
 // fold_layernorm: LayerNorms read only by GEMMs become statistics ops (EngineOptions::fold_layernorm).
+// ln_stats_epilogue: ... and those statistics come from the epilogue of the GEMM producing the
+// LayerNorm's input where one does (EngineOptions::ln_stats_epilogue).
 Plan build_plan(const onnx::Model& m, int max_batch, bool side_branches = false, bool split = false,
                 bool bn_on_load = false, bool fuse_pairs = true, bool fuse_stem_pool = true, bool fuse_gap_fc = false,
-                bool fold_layernorm = true);
+                bool fold_layernorm = true, bool ln_stats_epilogue = true);
 
 // Load-time support report: which nodes the HIP planner cannot lower, and why.  `blocked` counts
 // nodes not tried because an input came from an unsupported node.

@@ -72,7 +72,11 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (a.Cin % 4 != 0 || a.Kpad % BK != 0 || a.K > a.Kpad) return hipErrorInvalidValue;
   if (!a.out && !a.out_f32 && !a.out2) return hipErrorInvalidValue;
   if (a.out2 && (!a.scale2 || !a.shift2)) return hipErrorInvalidValue;
-  if (a.row_stats && !a.col_sum) return hipErrorInvalidValue;
+  if ((a.row_stats || a.row_parts) && !a.col_sum) return hipErrorInvalidValue;
+  // epilogue statistics: whole 64-column groups in one 8-lane DPP group; readers: the fp32 (split)
+  // kernels' LDS-staged epilogue (the launcher also rules out the two-kernel split-K form)
+  if (a.stats_out && a.N % 64 != 0) return hipErrorInvalidValue;
+  if (a.row_parts && (a.row_stats || !a.split || a.N % 8 != 0 || a.K % 64 != 0)) return hipErrorInvalidValue;
   if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
   if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
   const int variant = cfg / NUM_TILES;

@@ -44,13 +44,96 @@ __device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byt
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kCpolSc1));
 }
 
+// Cross-lane moves on the VALU (DPP), no LDS round trip (ds_bpermute, which __shfl_xor compiles to,
+// put ~3 dependent LDS latencies per 8-channel chunk on the epilogue's path).  CTRL: quad_perm
+// [1,0,3,2] = 0xB1 (lane ^ 1), [2,3,0,1] = 0x4E (lane ^ 2); row_half_mirror = 0x141 (lane i <-> 7-i
+// within each 8 lanes).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// Chan et al. merge of two (count, mean, M2) summaries in a form symmetric in its operands, so the
+// two lanes of a DPP exchange compute bit-identical results (empty summaries: count 0).
+__device__ __forceinline__ void chan_sym(float& mean, float& m2, float& cnt, float mean_o, float m2_o, float cnt_o) {
+  const float tot = cnt + cnt_o, d = mean_o - mean;
+  const float inv = tot > 0.f ? 1.f / tot : 0.f;
+  m2 = (m2 + m2_o) + d * d * (cnt * cnt_o * inv);
+  mean = (cnt * mean + cnt_o * mean_o) * inv;
+  cnt = tot;
+}
+// Left-to-right merge of 64-column (mean, M2) groups into a running (mean, M2, count).
+__device__ __forceinline__ void chan_add64(float& mean, float& m2, float& cnt, float2 g) {
+  const float d = g.x - mean, tot = cnt + 64.f;
+  mean += d * (64.f / tot);
+  m2 += g.y + d * d * (cnt * 64.f / tot);
+  cnt = tot;
+}
+
+// ConvArgs::row_parts reader: the LayerNorm statistics of the block's BM rows.  TPR = 256 / BM
+// adjacent threads per row, each holding a contiguous run of the row's K/64 groups.  issue() at the
+// block's start puts the loads in flight with the first operand loads; merge() (every thread of the
+// block) after the prologue returns (mean, rstd) of the thread's row on all its TPR lanes: each run
+// merged left to right, then the runs by a fixed DPP tree -- bitwise repeatable.
+template <int BM>
+struct RowParts {
+  static constexpr int TPR = 256 / BM, MAXG = 8;  // groups held per thread (more: loaded in merge)
+  static_assert(TPR == 2 || TPR == 4, "one quad per row");
+  float2 q[MAXG];
+  const float2* src = nullptr;
+  int g0 = 0, g1 = 0;
+  __device__ __forceinline__ void issue(const ConvArgs& p, int m0, int tid) {
+    const int ng = p.K >> 6, row = tid / TPR, sub = tid % TPR;
+    const int m = m0 + row < p.M ? m0 + row : 0;  // tail rows: any valid row, result unused
+    g0 = sub * ng / TPR;
+    g1 = (sub + 1) * ng / TPR;
+    src = reinterpret_cast<const float2*>(p.row_parts) + static_cast<size_t>(m) * ng;
+#pragma unroll
+    for (int j = 0; j < MAXG; ++j) q[j] = g0 + j < g1 ? src[g0 + j] : make_float2(0.f, 0.f);
+  }
+  __device__ __forceinline__ float2 merge(const ConvArgs& p) const {
+    float mean = q[0].x, m2 = q[0].y, cnt = g1 > g0 ? 64.f : 0.f;  // K < 64 * TPR: some runs empty
+#pragma unroll
+    for (int j = 1; j < MAXG; ++j)
+      if (g0 + j < g1) chan_add64(mean, m2, cnt, q[j]);
+    for (int j = g0 + MAXG; j < g1; ++j) chan_add64(mean, m2, cnt, src[j]);
+    chan_sym(mean, m2, cnt, dpp<0xB1>(mean), dpp<0xB1>(m2), dpp<0xB1>(cnt));
+    if constexpr (TPR == 4) chan_sym(mean, m2, cnt, dpp<0x4E>(mean), dpp<0x4E>(m2), dpp<0x4E>(cnt));
+    return make_float2(mean, rsqrtf(m2 / cnt + p.ln_eps));
+  }
+};
+// The same for one row by one thread (the two-kernel split-K epilogue; no prefetch).
+__device__ __forceinline__ float2 row_parts_direct(const ConvArgs& p, int m) {
+  const int ng = p.K >> 6;
+  const float2* src = reinterpret_cast<const float2*>(p.row_parts) + static_cast<size_t>(m) * ng;
+  float mean = 0.f, m2 = 0.f, cnt = 0.f;
+  for (int j = 0; j < ng; ++j) chan_add64(mean, m2, cnt, src[j]);
+  return make_float2(mean, rsqrtf(m2 / cnt + p.ln_eps));
+}
+
 // Epilogue for 8 consecutive channels [n, n+8) of output pixel m.  Requires N % 8 == 0.
 // fp32 mode (p.split): the residual is read as hi + lo and out/out2 are stored as split planes.
-__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v) {
+// ms: (mean, rstd) of row m for a p.row_parts reader (tile_epilogue's LDS row cache; null: merged
+// here, the two-kernel split-K path).
+// p.stats_out: the 8 lanes holding one 64-column group (consecutive lanes, group-aligned n -- every
+// caller maps consecutive threads to consecutive 8-channel chunks of one row, and N % 64 == 0)
+// merge their (mean, M2) by DPP; the formula is symmetric, so all 8 lanes agree and the result does
+// not depend on which lane stores it.
+__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v, const float* ms = nullptr) {
   const size_t o = static_cast<size_t>(m) * p.N + n;
   const bool split = p.split != 0;
-  if (p.row_stats) {
-    const float mean = p.row_stats[2 * static_cast<size_t>(m)], rstd = p.row_stats[2 * static_cast<size_t>(m) + 1];
+  if (p.row_stats || p.row_parts) {
+    float mean, rstd;
+    if (p.row_stats) {
+      mean = p.row_stats[2 * static_cast<size_t>(m)];
+      rstd = p.row_stats[2 * static_cast<size_t>(m) + 1];
+    } else if (ms) {
+      mean = ms[0];
+      rstd = ms[1];
+    } else {
+      const float2 r = row_parts_direct(p, m);
+      mean = r.x;
+      rstd = r.y;
+    }
     const float4 c0 = ldf4(p.col_sum + n), c1 = ldf4(p.col_sum + n + 4);
     const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
@@ -70,6 +153,29 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   if (p.relu) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu, p.clip_lo, p.clip_hi);
+  }
+  if (p.stats_out) {
+    float mu = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) mu += v[t];
+    mu *= 0.125f;
+    float m2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) m2 += (v[t] - mu) * (v[t] - mu);
+    // lane ^ 1, lane ^ 2, then the two quads of the 8 (each quad uniform by then, so the mirror
+    // pairing is the xor-4 pairing); equal counts: mean = (a + b) / 2, M2 = M2a + M2b + d^2 n / 2
+    float cnt = 8.f;
+    auto round = [&](float mu_o, float m2_o) {
+      const float d = mu_o - mu;
+      m2 = (m2 + m2_o) + d * d * (0.5f * cnt);
+      mu = 0.5f * (mu + mu_o);
+      cnt *= 2.f;
+    };
+    round(dpp<0xB1>(mu), dpp<0xB1>(m2));
+    round(dpp<0x4E>(mu), dpp<0x4E>(m2));
+    round(dpp<0x141>(mu), dpp<0x141>(m2));
+    if ((n & 63) == 0)
+      reinterpret_cast<float2*>(p.stats_out)[static_cast<size_t>(m) * (p.N >> 6) + (n >> 6)] = make_float2(mu, m2);
   }
   if (p.out) store8v(p.out + o, p.oplane, split, v);
   if (p.out_f32) {
@@ -98,7 +204,7 @@ struct LinearRows {
 template <int BM, int BN, typename RowMap = LinearRows>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
                                               int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
-                                              RowMap rows = RowMap{0, 0});
+                                              RowMap rows = RowMap{0, 0}, float2 rms = float2{0.f, 0.f});
 
 // XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
 // id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
@@ -129,13 +235,13 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   // input 9 times (stage-4 3x3 at batch 16-32: weights 4.7x the input, so M-fastest).
   const long long wts = static_cast<long long>(p.N) * p.K;
   const long long acts = static_cast<long long>(p.B) * p.H * p.W * p.Cin;
-  if (p.order == 1 || (p.order == 0 && wts <= acts)) {
-    tile_m = tile / ntn;
-    tile_n = tile - tile_m * ntn;
-  } else {
-    tile_n = tile / ntm;
-    tile_m = tile - tile_n * ntm;
-  }
+  // One division and selects, no branch: with the outputs assigned on two paths the compiler kept
+  // them in scratch (a private-memory round trip at the start of every block).
+  const bool nfast = p.order == 1 || (p.order == 0 && wts <= acts);
+  const int minor = nfast ? ntn : ntm;
+  const int hi = tile / minor, lo = tile - hi * minor;
+  tile_m = nfast ? hi : lo;
+  tile_n = nfast ? lo : hi;
   return true;
 }
 
@@ -150,6 +256,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
   constexpr int W_CH = BN / 32;                       // 16-B weight chunks per thread per stage
   constexpr int X_CH = VEC == 8 ? BM / 32 : BM / 16;  // activation units per thread per stage
   static_assert(2 * STAGE * NP * 2 >= BM * BN * 4, "epilogue staging must fit in the operand LDS");
+  static_assert(!SPLIT || 2 * STAGE * NP >= BM * BN * 2 + BM * 4, "... and the row_parts row cache (fp32)");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE * NP];
 
   const int tid = threadIdx.x;
@@ -264,8 +371,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  RowParts<BM> rp;  // row_parts reader (fp32 only): loads in flight with the first stage's
+  float2 rms = make_float2(0.f, 0.f);
+  if (SPLIT && p.row_parts) rp.issue(p, m0, tid);
+  if (kt_begin < kt_end) load_stage(kt_begin * BK);
+  if (SPLIT && p.row_parts) rms = rp.merge(p);
   if (kt_begin < kt_end) {
-    load_stage(kt_begin * BK);
     store_stage(0);
     __syncthreads();
   }
@@ -302,7 +413,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     if (more) store_stage(cur ^ 1);
     __syncthreads();
   }
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms);
 }
 
 // Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
@@ -310,7 +421,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
 template <int BM, int BN, typename RowMap>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
                                               int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
-                                              RowMap rows) {
+                                              RowMap rows, float2 rms) {
   if constexpr (std::is_same_v<RowMap, LinearRows>) rows = LinearRows{m0, p.M};
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -320,6 +431,13 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     // ---- LDS-staged, coalesced epilogue ----
     constexpr int CPR = BN / 4;  // 16-B chunks per staged row
     float* st = reinterpret_cast<float*>(lds);
+    // row_parts reader: the tile rows' (mean, rstd) (merged by the kernel, RowParts) into the LDS row
+    // cache past the staging tile, published by the staging barrier below
+    float* rowc = nullptr;
+    if (p.row_parts) {
+      rowc = st + BM * BN;
+      if (tid % (256 / BM) == 0) *reinterpret_cast<float2*>(rowc + 2 * (tid / (256 / BM))) = rms;
+    }
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -352,7 +470,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         *reinterpret_cast<float4*>(o + 4) = b;
       } else {
         float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        epilogue8(p, m, n, v);
+        epilogue8(p, m, n, v, rowc ? rowc + 2 * row : nullptr);
       }
     }
     if (!fused) return;
@@ -396,7 +514,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
         v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       }
-      epilogue8(p, m, n, v);
+      epilogue8(p, m, n, v, rowc ? rowc + 2 * row : nullptr);
     }
     return;
   }
@@ -521,7 +639,9 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_ELEMS = BN * BKS, B_ELEMS = BM * BKS, PLANE = A_ELEMS + B_ELEMS, STAGE = NP * PLANE;
   constexpr int GA = BN / 4 / RPI, GB = BM / 4 / RPI, G = NP * (GA + GB);  // DMA instructions per wave per stage
-  constexpr int LDS_ELEMS = STAGES * STAGE > BM * BN * 2 ? STAGES * STAGE : BM * BN * 2;
+  // epilogue: the f32 tile, plus (fp32: ConvArgs::row_parts readers) the BM (mean, rstd) row cache
+  constexpr int EPI_ELEMS = BM * BN * 2 + (SPLIT ? BM * 4 : 0);
+  constexpr int LDS_ELEMS = STAGES * STAGE > EPI_ELEMS ? STAGES * STAGE : EPI_ELEMS;
   // One LDS array: the stage ring / epilogue tile, then (BNL) the channel table.  No separate
   // dummy arrays: a 1-stage split 64x64 block is exactly 32 KiB.
   constexpr int BNL_ELEMS = BNL ? 2 * 2 * kBnlMaxK : 0;
@@ -709,13 +829,26 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     }
   };
 
+  // row_parts reader (fp32 only): the rows' statistics groups are loaded ahead of the first
+  // K-step's DMA and merged while it is in flight
+  RowParts<BM> rp;
+  float2 rms = make_float2(0.f, 0.f);
+  const bool rp_on = SPLIT && p.row_parts;
+  if (rp_on) rp.issue(p, m0, tid);
+
   if constexpr (STAGES == 1) {
     // No ring: load, wait, compute, once per K-step.  Meant for nk == 1 (K <= 64: the expand /
     // reduce convs of stage 1), where a ring buys nothing and a 1-stage LDS footprint lets 2-4x
     // more blocks share a CU to hide the load and epilogue latency.
+    // (the first K-step's DMA issued ahead of the loop, so that the row_parts merge runs under it
+    // outside the loop -- merged inside it, at t == 0, the 64-row tiles' statistics came out wrong)
+    if (nk > 0) issue(0);
+    if (rp_on) rms = rp.merge(p);
     for (int t = 0; t < nk; ++t) {
-      if (t) __syncthreads();  // everyone done reading the previous K-step
-      issue(0);
+      if (t) {
+        __syncthreads();  // everyone done reading the previous K-step
+        issue(0);
+      }
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -724,6 +857,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   } else {
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nk) issue(s);
+    if (rp_on) rms = rp.merge(p);
     int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
     for (int t = 0; t < nk; ++t) {
       // Stage t has landed for this wave once at most min(STAGES-2, nk-1-t) younger stages (G DMA
@@ -740,7 +874,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -955,6 +1089,8 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   // fused split-K reduction needs a zeroed counter per output tile
   const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
   if (!fused) b.counters = nullptr;
+  // LayerNorm statistics (ConvArgs::stats_out / row_parts): rows GEMMs, not the spatially tiled 3x3
+  if ((a.stats_out || a.row_parts) && variant == 6) return hipErrorInvalidValue;
   dim3 grid(tiles, eff);
   if (a.in_scale) {  // pre-activation on load: 1x1 convs in the LDS-DMA loop only
     if (a.KH != 1 || a.KW != 1 || a.pad_h || a.pad_w || a.K != a.Cin || a.K > kBnlMaxK || a.Cin % BK || !a.in_shift)

@@ -59,6 +59,16 @@ struct ConvArgs {
   // from layernorm_rows' stats mode, col_sum[n] = sum_k of the (gamma-scaled) weight row n.
   const float* row_stats = nullptr;
   const float* col_sum = nullptr;
+  // LayerNorm statistics produced by the epilogue of the GEMM that writes the LayerNorm's input (ViT:
+  // the attention-out / MLP2 GEMMs with the residual add; N % 64 == 0): stats_out = [M][N/64] float2
+  // (mean, M2) of every row's 64-column groups of the output.  A folded reader (fp32 mode) takes
+  // row_parts (that buffer, [M][K/64]) instead of row_stats: each block fetches its rows' groups at
+  // its start (in flight with the first operand loads), merges them in a fixed order (Chan et al.)
+  // into mean and rstd = 1/sqrt(M2/K + ln_eps), and keeps them in LDS for the epilogue.  No
+  // standalone statistics pass over the rows.
+  float* stats_out = nullptr;
+  const float* row_parts = nullptr;
+  float ln_eps = 0.f;
   // fp32 mode (common.h "split" tensors): x, res, out and out2 are split (hi, lo) bf16 planes and w
   // holds the weights' hi plane followed by their lo plane `wplane` elements later.  The planes of
   // the activations follow from the shapes (x: B*H*W*Cin, res/out/out2: M*N; the launcher fills

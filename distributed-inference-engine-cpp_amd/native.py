@@ -709,16 +709,19 @@ def _sig_kernels():
 
 def plan_summary(model_path: str, max_batch: int = 32, side_branches: bool = False,
                  precision: str = "bf16", fuse_pairs: bool = True, fuse_stem_pool: bool = True,
-                 fuse_gap_fc: bool = False, fold_layernorm: bool = True) -> Dict[str, Any]:
+                 fuse_gap_fc: bool = False, fold_layernorm: bool = True,
+                 ln_stats_epilogue: bool = True) -> Dict[str, Any]:
     """precision "fp32" plans the split (hi, lo) kernels of the HIP engine's default mode.
     fuse_pairs: expand + next reduce 1x1 convs as one conv_pair op (EngineOptions::fuse_pairs);
     fuse_stem_pool: stem conv + max pool as one stem op (EngineOptions::fuse_stem_pool);
     fuse_gap_fc: global pool + FC head as one gap_fc op (EngineOptions::fuse_gap_fc);
-    fold_layernorm: LayerNorms read only by GEMMs compute statistics only (EngineOptions::fold_layernorm)."""
+    fold_layernorm: LayerNorms read only by GEMMs compute statistics only (EngineOptions::fold_layernorm);
+    ln_stats_epilogue: ... from the epilogue of the GEMM producing their input (EngineOptions::ln_stats_epilogue)."""
     L = _sig_kernels()
     err = _err_box()
     p = L.die_plan_summary(model_path.encode(), max_batch, int(side_branches), int(precision == "fp32"),
-                           int(fuse_pairs) | 2 * int(fuse_stem_pool) | 4 * int(fuse_gap_fc) | 8 * int(fold_layernorm), C.byref(err))
+                           int(fuse_pairs) | 2 * int(fuse_stem_pool) | 4 * int(fuse_gap_fc) | 8 * int(fold_layernorm)
+                           | 16 * int(ln_stats_epilogue), C.byref(err))
     if not p:
         _raise_if(err, "plan")
     return json.loads(_take_str(p))

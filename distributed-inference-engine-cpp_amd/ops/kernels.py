@@ -124,10 +124,13 @@ class ConvProblem:
         self.flops = 2.0 * B * Ho * Wo * cout * cin * kh * kw
         self._L = native.kernels()
 
-    def launch(self, tile=-1, splits=1, fused_splitk=True, order=0) -> int:
+    def launch(self, tile=-1, splits=1, fused_splitk=True, order=0, extra=None) -> int:
         """Launch on torch's current stream; returns the hipError code (1 = config not applicable).
-        order: XCD tile order (ConvArgs::order: 0 heuristic, 1 N-fastest, 2 M-fastest)."""
+        order: XCD tile order (ConvArgs::order: 0 heuristic, 1 N-fastest, 2 M-fastest).
+        extra: more ConvArgs fields by geometry-JSON key (device pointers as ints), e.g. the LayerNorm
+        statistics row_stats / col_sum / row_parts / stats_out and ln_eps."""
         g = dict(self.geom, splits=int(splits), order=int(order))
+        g.update(extra or {})
         if splits > 1:
             g["ws"] = int(self.ws.data_ptr())
             if fused_splitk:

@@ -225,30 +225,40 @@ def test_vit_base_engine_vs_torch(native, models):
     e.close()
 
 
-@pytest.mark.parametrize("size", ["tiny", "base"])
-def test_vit_fold_layernorm_vs_torch(native, models, size):
+@pytest.mark.parametrize("size,stats_epi", [("tiny", False), ("tiny", True), ("base", False), ("base", True)])
+def test_vit_fold_layernorm_vs_torch(native, models, size, stats_epi):
     """EngineOptions::fold_layernorm: every pre-norm LayerNorm computes row statistics only and the
     QKV / first-MLP GEMMs read the residual rows with gamma folded into their weights, beta into
     their bias and (mean, rstd) applied in the epilogue -- same accuracy bar as the unfolded engine
-    (fp32 rel-L2 <= 1e-4 against torch, same top-1), in the autotuned and untuned paths."""
+    (fp32 rel-L2 <= 1e-4 against torch, same top-1), in the autotuned and untuned paths.
+    stats_epi (EngineOptions::ln_stats_epilogue, default on): the statistics of all but block 0's
+    LayerNorm come from the attention-out / MLP2 GEMM epilogues as per-64-column (mean, M2)
+    partials -- covered in the fused split-K, two-kernel split-K and plain epilogues."""
     import torch
 
     from die_amd.models import vit
 
     path, w, cfg = models["get_vit"](size)
-    s = native.plan_summary(path, 8, precision="fp32", fold_layernorm=True)
-    assert sum(1 for o in s["ops"] if o.get("stats_only")) == 2 * cfg.depth
+    s = native.plan_summary(path, 8, precision="fp32", fold_layernorm=True, ln_stats_epilogue=stats_epi)
+    assert sum(1 for o in s["ops"] if o.get("stats_only")) == (1 if stats_epi else 2 * cfg.depth)
+    assert sum(1 for o in s["ops"] if o.get("stats_out")) == (2 * cfg.depth - 1 if stats_epi else 0)
     assert sum(1 for o in s["ops"] if o.get("layernorm_folded")) == 2 * cfg.depth
     x = vit.synthetic_input(5, cfg)
     with torch.no_grad():
         ref = vit.torch_forward(w, x, cfg, device="cuda").cpu().numpy()
-    for autotune in ((False, True) if size == "tiny" else (False,)):
-        e = native.Engine(path, device="hip", max_batch=8, fold_layernorm=True, autotune=autotune)
+    runs = [dict(autotune=False)]
+    if size == "tiny":
+        runs += [dict(autotune=True), dict(autotune=True, splitk_two_kernel=True)]
+    for kw in runs:
+        e = native.Engine(path, device="hip", max_batch=8, fold_layernorm=True, ln_stats_epilogue=stats_epi, **kw)
         try:
             assert e.refresh_info()["options"]["fold_layernorm"] is True
+            assert e.refresh_info()["options"]["ln_stats_epilogue"] is stats_epi
             got = e.run(x.reshape(5, -1))
+            # the statistics hand-off merges in a fixed order: bitwise repeatable
+            assert np.array_equal(got, e.run(x.reshape(5, -1)))
             err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
-            assert err < 1e-4, (autotune, err)
+            assert err < 1e-4, (kw, err)
             assert (got.argmax(1) == ref.argmax(1)).all()
         finally:
             e.close()

@@ -62,13 +62,31 @@ def test_fold_layernorm_plan(native, tmp_path):
     p = str(tmp_path / "vit.onnx")
     open(p, "wb").write(vit.build_onnx(c)[0])
     plain = native.plan_summary(p, 8, precision="fp32", fold_layernorm=False)
-    folded = native.plan_summary(p, 8, precision="fp32")  # the default
+    folded = native.plan_summary(p, 8, precision="fp32", ln_stats_epilogue=False)
     stats = [o for o in folded["ops"] if o.get("stats_only")]
     assert len(stats) == 2 * c.depth and not any(o.get("stats_only") for o in plain["ops"])
     convs = [o for o in folded["ops"] if o.get("layernorm_folded")]
     assert len(convs) == 2 * c.depth and all(o["name"].startswith("encoder.layer.") for o in convs)
+    assert not any(o.get("stats_out") for o in folded["ops"])
     # the statistics buffers are tiny: the folded arena is no larger
     assert folded["arena_bytes"] <= plain["arena_bytes"]
+    # default: the statistics come from the epilogues of the GEMMs that write the LayerNorm inputs
+    # (attention-out and MLP2, residual add fused); only block 0's LayerNorm (input from the token
+    # assembly) keeps a statistics op
+    d = native.plan_summary(p, 8, precision="fp32")
+    assert [o["name"] for o in d["ops"] if o.get("stats_only")] == [stats[0]["name"]]
+    prod = [o for o in d["ops"] if o.get("stats_out")]
+    assert len(prod) == 2 * c.depth - 1 and all(o["residual"] and o["N"] == c.dim for o in prod)
+    assert all("out_stats" in o["bufs"] for o in prod)
+    assert len(d["ops"]) == len(folded["ops"]) - (2 * c.depth - 1)
+    cons = [o for o in d["ops"] if o.get("stats_from_producer")]
+    assert len(cons) == 2 * c.depth - 1 and all(o["layernorm_folded"] for o in cons)
+    # each producer's partials are read (in3) by the next op, the QKV or MLP1 GEMM, which arena
+    # planning keeps them live for
+    idx = {o["name"]: i for i, o in enumerate(d["ops"])}
+    for o in prod:
+        nxt = d["ops"][idx[o["name"]] + 1]
+        assert nxt.get("stats_from_producer") and nxt["bufs"]["in3"] == o["bufs"]["out_stats"], nxt["name"]
     b = str(tmp_path / "bert.onnx")
     open(b, "wb").write(generic.build_onnx("bert"))
     s = native.plan_summary(b, 8, precision="fp32", fold_layernorm=True)

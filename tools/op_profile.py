@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
     ap.add_argument("--ln-xcd", type=int, default=0, help="LayerNorm row order: 1 XCD-affine, 0 natural (default)")
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
+    ap.add_argument("--no-ln-stats-epilogue", action="store_true",
+                    help="LayerNorm statistics launches instead of producer-epilogue partials (EngineOptions::ln_stats_epilogue)")
     ap.add_argument("--fuse-gap-fc", action="store_true", help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
     ap.add_argument("--no-fuse-stem-pool", action="store_true", help="stem and max pool as two launches (EngineOptions::fuse_stem_pool)")
     a = ap.parse_args()
@@ -46,7 +48,8 @@ def main():
     e = native.Engine(path, device="hip", max_batch=a.batch, precision=a.precision,
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
                       splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
-                      fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm)
+                      fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm,
+                      ln_stats_epilogue=not a.no_ln_stats_epilogue)
     p = e.profile(a.batch, a.iters)
     e.close()
     lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
