@@ -80,6 +80,7 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
   if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
   const int variant = cfg / NUM_TILES;
+  if (variant == 7) return igemm::launch_tile_wide(a, s, cfg % NUM_TILES);
   switch (cfg % NUM_TILES) {
     case TILE_128x128: return igemm::launch_tile_128x128(a, s, variant);
     case TILE_128x64: return igemm::launch_tile_128x64(a, s, variant);

@@ -69,14 +69,14 @@ __device__ __forceinline__ void chan_add64(float& mean, float& m2, float& cnt, f
   cnt = tot;
 }
 
-// ConvArgs::row_parts reader: the LayerNorm statistics of the block's BM rows.  TPR = 256 / BM
+// ConvArgs::row_parts reader: the LayerNorm statistics of the block's BM rows.  TPR = NT / BM
 // adjacent threads per row, each holding a contiguous run of the row's K/64 groups.  issue() at the
 // block's start puts the loads in flight with the first operand loads; merge() (every thread of the
 // block) after the prologue returns (mean, rstd) of the thread's row on all its TPR lanes: each run
 // merged left to right, then the runs by a fixed DPP tree -- bitwise repeatable.
-template <int BM>
+template <int BM, int NT = 256>
 struct RowParts {
-  static constexpr int TPR = 256 / BM, MAXG = 8;  // groups held per thread (more: loaded in merge)
+  static constexpr int TPR = NT / BM, MAXG = 8;  // groups held per thread (more: loaded in merge)
   static_assert(TPR == 2 || TPR == 4, "one quad per row");
   float2 q[MAXG];
   const float2* src = nullptr;
@@ -201,10 +201,14 @@ struct LinearRows {
   __device__ __forceinline__ int operator()(int r) const { return m0 + r < M ? m0 + r : -1; }
 };
 
-template <int BM, int BN, typename RowMap = LinearRows>
-__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
-                                              RowMap rows = RowMap{0, 0}, float2 rms = float2{0.f, 0.f});
+// NT threads = (NT / 64) waves, WAVES_M along the tile's rows (pixels) x NT / 64 / WAVES_M along its
+// channels; acc[i][j]: the wave's i-th 16-channel x j-th 16-pixel fragment.
+template <int BM, int BN, typename RowMap = LinearRows, int NT = 256, int WAVES_M = 2>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
+                                              f32x4 (&acc)[BN / 16 / (NT / 64 / WAVES_M)][BM / 16 / WAVES_M],
+                                              uint16_t* lds, int m0, int n0, int wm, int wn, int lane, int tid,
+                                              int tile, int split, RowMap rows = RowMap{0, 0},
+                                              float2 rms = float2{0.f, 0.f});
 
 // XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
 // id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
@@ -418,12 +422,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
 
 // Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
 // past their last operand read).
-template <int BM, int BN, typename RowMap>
-__device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN / 32][BM / 32], uint16_t* lds,
-                                              int m0, int n0, int wm, int wn, int lane, int tid, int tile, int split,
-                                              RowMap rows, float2 rms) {
+template <int BM, int BN, typename RowMap, int NT, int WAVES_M>
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
+                                              f32x4 (&acc)[BN / 16 / (NT / 64 / WAVES_M)][BM / 16 / WAVES_M],
+                                              uint16_t* lds, int m0, int n0, int wm, int wn, int lane, int tid,
+                                              int tile, int split, RowMap rows, float2 rms) {
   if constexpr (std::is_same_v<RowMap, LinearRows>) rows = LinearRows{m0, p.M};
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WAVES_M, WN = BN / (NT / 64 / WAVES_M);
   constexpr int TM = WM / 16, TN = WN / 16;
   const int lm = lane & 15;
   const int ln = (lane >> 4) * 4;
@@ -436,7 +441,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     float* rowc = nullptr;
     if (p.row_parts) {
       rowc = st + BM * BN;
-      if (tid % (256 / BM) == 0) *reinterpret_cast<float2*>(rowc + 2 * (tid / (256 / BM))) = rms;
+      if (tid % (NT / BM) == 0) *reinterpret_cast<float2*>(rowc + 2 * (tid / (NT / BM))) = rms;
     }
 #pragma unroll
     for (int i = 0; i < TN; ++i)
@@ -452,7 +457,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     const bool fused = partial && p.counters;
     float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
     const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
-    for (int g = tid; g < BM * GPR; g += 256) {
+    for (int g = tid; g < BM * GPR; g += NT) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
       const int m = rows(row);
@@ -501,7 +506,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f32x4 (&acc)[BN
     __syncthreads();
     if (!*flag) return;
     const unsigned slab = static_cast<unsigned>(static_cast<size_t>(p.M) * p.N * 4);  // bytes
-    for (int g = tid; g < BM * GPR; g += 256) {
+    for (int g = tid; g < BM * GPR; g += NT) {
       const int row = g / GPR;
       const int cg = g - row * GPR;
       const int m = rows(row);
@@ -1171,6 +1176,155 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wide-tile GEMM for the fp32 (split) rows GEMMs of transformers (MODE 0 only: dense rows, K % 64
+// == 0).  256 pixels x BN = 128 channels per block, 512 threads = 8 waves in a 4 (pixels) x 2
+// (channels) grid, each wave a 64 x 64 output, so two waves share every SIMD and hide each other's
+// LDS reads under their MFMAs (the 4-wave 128x128 kernel has one).  32-wide K-steps (hi + lo planes
+// of both operands = 48 KiB per stage) in a 3-deep LDS-DMA ring (144 KiB, one block per CU): two
+// K-steps stay in flight across every barrier (counted vmcnt, raw s_barrier, as conv_glds_kernel).
+// Per K-step a wave issues 16 ds_read_b128 for 48 MFMAs (1 : 3); the 256-row tile halves the weight
+// bytes per output row against the 128-row tiles.
+template <int BN>
+__global__ __launch_bounds__(512) void gemm_wide_kernel(const ConvArgs p, const int kt_per_split) {
+  constexpr int BM = 256, BKS = 32, NT = 512, WAVES_M = 4, WAVES_N = 2, STAGES = 3;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int CPR = BKS / 8, RPI = 512 / BKS;  // 16-B chunks per LDS row; rows per 1 KiB DMA instruction
+  constexpr int A_ELEMS = BN * BKS, B_ELEMS = BM * BKS, PLANE = A_ELEMS + B_ELEMS, STAGE = 2 * PLANE;
+  constexpr int GA = BN / 8 / RPI, GB = BM / 8 / RPI;  // DMA instructions per wave per plane
+  constexpr int G = 2 * (GA + GB);
+  static_assert(GA >= 1 && GB >= 1, "8 waves x 16 rows per DMA instruction");
+  constexpr int EPI_ELEMS = BM * BN * 2 + BM * 4;  // f32 staging tile + row_parts row cache
+  constexpr int LDS_ELEMS = STAGES * STAGE > EPI_ELEMS ? STAGES * STAGE : EPI_ELEMS;
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
+  auto sw = [](int row, int chunk) { return row * BKS + ((chunk ^ ((row >> 1) & (CPR - 1))) << 3); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  int tile_m, tile_n, split, tile;
+  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk_total = p.Kpad / BKS;
+  const int kt_begin = split * kt_per_split * 2;  // kt_per_split counts 64-wide K-steps
+  const int kt_end = min(nk_total, kt_begin + kt_per_split * 2);
+  const int nk = kt_end - kt_begin;
+
+  // per-lane DMA sources (lane L -> row L / CPR of its 16-row group, physical chunk L % CPR; the
+  // swizzle goes on the source address); M-tail rows read the zero page
+  const uint16_t* asrc[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int r = wave * (BN / 8) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
+    asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
+  }
+  const uint16_t* bsrc[GB];
+  long long bdel[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int r = wave * (BM / 8) + i * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ ((r >> 1) & (CPR - 1));
+    const bool v = m0 + r < p.M;
+    bsrc[i] = (v ? p.x + static_cast<size_t>(m0 + r) * p.Cin : p.zeros) + c * 8;
+    bdel[i] = v ? p.xplane : 0;
+  }
+  int nx_k0 = kt_begin * BKS;
+  auto issue = [&](int buf) {
+    uint16_t* A = lds + buf * STAGE;
+    uint16_t* Bt = A + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      glds16(asrc[i] + nx_k0, A + (wave * (BN / 8) + i * RPI) * BKS);
+      glds16(asrc[i] + p.wplane + nx_k0, A + PLANE + (wave * (BN / 8) + i * RPI) * BKS);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      glds16(bsrc[i] + nx_k0, Bt + (wave * (BM / 8) + i * RPI) * BKS);
+      glds16(bsrc[i] + bdel[i] + nx_k0, Bt + PLANE + (wave * (BM / 8) + i * RPI) * BKS);
+    }
+    nx_k0 += BKS;
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const uint16_t* A) {
+    const uint16_t* Bt = A + A_ELEMS;
+    const int chunk = lane >> 4;
+    bf16x8 af[TN], afl[TN], bfr[TM], bfl[TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int o = sw(wn * WN + i * 16 + (lane & 15), chunk);
+      af[i] = *reinterpret_cast<const bf16x8*>(A + o);
+      afl[i] = *reinterpret_cast<const bf16x8*>(A + PLANE + o);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int o = sw(wm * WM + j * 16 + (lane & 15), chunk);
+      bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + o);
+      bfl[j] = *reinterpret_cast<const bf16x8*>(Bt + PLANE + o);
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  RowParts<BM, NT> rp;  // row_parts reader: loads ahead of the prologue DMA, merged under it
+  float2 rms = make_float2(0.f, 0.f);
+  if (p.row_parts) rp.issue(p, m0, tid);
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+  if (p.row_parts) rms = rp.merge(p);
+  int rd = 0, wr = STAGES - 1;
+  for (int t = 0; t < nk; ++t) {
+    wait_stages<G, STAGES - 2>(nk - 1 - t);  // stage t landed for this wave ...
+    __builtin_amdgcn_s_barrier();             // ... and every wave; all done reading stage t - 1
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(wr);
+    wr = wr + 1 == STAGES ? 0 : wr + 1;
+    const uint16_t* A = lds + rd * STAGE;
+    rd = rd + 1 == STAGES ? 0 : rd + 1;
+    compute(A);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // all operand reads done before the epilogue reuses the LDS
+  tile_epilogue<BM, BN, LinearRows, NT, WAVES_M>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split,
+                                                 LinearRows{0, 0}, rms);
+}
+
+// 256 x 128 wide tile (gemm_wide_kernel): fp32 dense-rows GEMMs only.
+inline hipError_t launch_wide(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = 256, BN = 128;
+  const bool dense = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
+                     a.W == a.Wo && a.K % BK == 0 && a.Cin == a.K && a.Kpad == a.K;
+  if (!dense || !a.split || a.in_scale || !a.zeros || a.wplane <= 0 || a.N % 8) return hipErrorInvalidValue;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int nk = a.Kpad / BK;
+  const int splits = std::max(1, std::min(a.splits, nk));
+  const int kt_per = (nk + splits - 1) / splits;
+  const int eff = (nk + kt_per - 1) / kt_per;
+  ConvArgs b = a;
+  b.splits = eff;
+  b.xplane = static_cast<long long>(a.B) * a.H * a.W * a.Cin;
+  b.oplane = static_cast<long long>(a.M) * a.N;
+  const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
+  if (!fused) b.counters = nullptr;
+  hipLaunchKernelGGL(gemm_wide_kernel<BN>, dim3(tiles, eff), dim3(512), 0, s, b, kt_per);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || eff == 1 || fused) return e;
+  const long long groups = static_cast<long long>(b.M) * (b.N / 8);
+  const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
 
 }  // namespace
 
@@ -1179,6 +1333,8 @@ hipError_t launch_tile_128x128(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_128x64(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_64x128(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_64x64(const ConvArgs& a, hipStream_t s, int variant);
+// conv_tile_wide.hip: variant 7 (256-row, 8-wave tiles)
+hipError_t launch_tile_wide(const ConvArgs& a, hipStream_t s, int tile);
 
 }  // namespace igemm
 }  // namespace kern

@@ -89,7 +89,9 @@ struct ConvArgs {
 // Variant 5 = the LDS-DMA loop with ONE stage (no ring): for K <= 64 layers, where the smaller LDS
 // footprint fits more blocks per CU.  Variant 6 = spatially tiled 3x3/s1/p1 kernel (8x8 pixels x 64
 // channels per block, input patch staged once per 64-channel slice; 64x64 tile config only).
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 28 };
+// Variant 7 = the 8-wave wide-tile GEMM (fp32 dense rows only): tile 0 -> 256 pixels x 128 channels
+// (conv_igemm_impl.h gemm_wide_kernel); the other tiles of variant 7 are not instantiated.
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 32 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

@@ -30,8 +30,14 @@ def _group_stats(y):
     return np.stack([mean, ((g - mean[..., None]) ** 2).sum(-1)], -1)
 
 
+def K_NUM_CFGS():
+    from die_amd.ops import kernels as K
+
+    return K.NUM_CFGS
+
+
 def _configs(splits_list=(1, 2)):
-    for tile in range(28):
+    for tile in range(K_NUM_CFGS()):
         for splits in splits_list:
             for fused in ((True, False) if splits > 1 else (True,)):
                 yield tile, splits, fused

@@ -55,11 +55,13 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1000.0 / a.reps)
         return statistics.median(ts)
 
-    cfgs = [int(c) for c in a.cfgs.split(",")]
+    # "cfg" or "cfg:splits" (fused split-K)
+    cfgs = [tuple(int(v) for v in (c.split(":") + ["1"])[:2]) for c in a.cfgs.split(",")]
     split = not a.bf16
     M = a.batch * a.tokens
     lines = ["# GEMM config sweep, ViT-B/16 shapes, M = %d rows (%s)" % (M, "fp32 split" if split else "bf16"), "",
-             "| shape | K | N | " + " | ".join("cfg %d" % c for c in cfgs) + " | hipBLASLt bf16 | hipBLASLt fp32 |",
+             "| shape | K | N | " + " | ".join("cfg %d" % c if s == 1 else "cfg %d/%d" % (c, s) for c, s in cfgs) +
+             " | hipBLASLt bf16 | hipBLASLt fp32 |",
              "|---|---:|---:|" + "---:|" * (len(cfgs) + 2)]
     for name, Kd, N, epi in SHAPES:
         x = torch.randn(a.batch, a.tokens, 1, Kd, device="cuda")
@@ -71,11 +73,11 @@ def main():
             kw["res"] = torch.randn(a.batch, a.tokens, 1, N, device="cuda")
             if not split:
                 kw["res"] = kw["res"].to(torch.bfloat16)
-        pr = K.ConvProblem(x, w, relu=(epi == "gelu"), split=split, **kw)
+        pr = K.ConvProblem(x, w, relu=(epi == "gelu"), split=split, max_splits=max(s for _, s in cfgs), **kw)
         row = []
-        for c in cfgs:
-            rc = pr.launch(c, 1)
-            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, 1)))
+        for c, sp in cfgs:
+            rc = pr.launch(c, sp)
+            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, sp)))
         A_ = torch.randn(M, Kd, device="cuda")
         W_ = torch.randn(Kd, N, device="cuda")
         ab, wb = A_.to(torch.bfloat16), W_.to(torch.bfloat16)
