@@ -68,6 +68,7 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     a.out2 = P<uint16_t>(out2);
     a.splits = geti(j, "splits", 1);
     a.order = geti(j, "order", 0);
+    a.probe = geti(j, "probe", 0);
     if (auto* v = j.find("ws")) a.ws = P<float>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("counters")) a.counters = P<int>(static_cast<uint64_t>(v->as_int()));

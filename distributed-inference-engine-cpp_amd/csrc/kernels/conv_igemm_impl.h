@@ -847,21 +847,23 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
     // more blocks share a CU to hide the load and epilogue latency.
     // (the first K-step's DMA issued ahead of the loop, so that the row_parts merge runs under it
     // outside the loop -- merged inside it, at t == 0, the 64-row tiles' statistics came out wrong)
-    if (nk > 0) issue(0);
+    const bool dma = p.probe != 1, mfma = p.probe != 2;  // ConvArgs::probe (measurement only)
+    if (nk > 0 && dma) issue(0);
     if (rp_on) rms = rp.merge(p);
     for (int t = 0; t < nk; ++t) {
       if (t) {
         __syncthreads();  // everyone done reading the previous K-step
-        issue(0);
+        if (dma) issue(0);
       }
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      compute(lds, t);
+      if (mfma) compute(lds, t);
     }
   } else {
+    const bool dma = p.probe != 1, mfma = p.probe != 2;
     for (int s = 0; s < STAGES - 1; ++s)
-      if (s < nk) issue(s);
+      if (s < nk && dma) issue(s);
     if (rp_on) rms = rp.merge(p);
     int rd = 0, wr = STAGES - 1;  // ring indices of the stage read this step / the stage issued next
     for (int t = 0; t < nk; ++t) {
@@ -870,11 +872,11 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
       wait_stages<G, STAGES - 2>(nk - 1 - t);
       __builtin_amdgcn_s_barrier();  // ... and for every wave; also: everyone is done reading stage t-1
       asm volatile("" ::: "memory");
-      if (t + STAGES - 1 < nk) issue(wr);
+      if (t + STAGES - 1 < nk && dma) issue(wr);
       wr = wr + 1 == STAGES ? 0 : wr + 1;
       const uint16_t* A = lds + rd * STAGE;
       rd = rd + 1 == STAGES ? 0 : rd + 1;
-      compute(A, t);
+      if (mfma) compute(A, t);
     }
   }
   wait_vmcnt<0>();
@@ -1280,19 +1282,20 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(const ConvArgs p, const 
   RowParts<BM, NT> rp;  // row_parts reader: loads ahead of the prologue DMA, merged under it
   float2 rms = make_float2(0.f, 0.f);
   if (p.row_parts) rp.issue(p, m0, tid);
+  const bool dma = p.probe != 1, mfma = p.probe != 2;  // ConvArgs::probe (measurement only)
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s);
+    if (s < nk && dma) issue(s);
   if (p.row_parts) rms = rp.merge(p);
   int rd = 0, wr = STAGES - 1;
   for (int t = 0; t < nk; ++t) {
     wait_stages<G, STAGES - 2>(nk - 1 - t);  // stage t landed for this wave ...
     __builtin_amdgcn_s_barrier();             // ... and every wave; all done reading stage t - 1
     asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(wr);
+    if (t + STAGES - 1 < nk && dma) issue(wr);
     wr = wr + 1 == STAGES ? 0 : wr + 1;
     const uint16_t* A = lds + rd * STAGE;
     rd = rd + 1 == STAGES ? 0 : rd + 1;
-    compute(A);
+    if (mfma) compute(A);
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS

@@ -80,6 +80,10 @@ struct ConvArgs {
   // operand on every XCD), 1 = N-fastest (an XCD owns a range of pixel rows, reads all weights),
   // 2 = M-fastest (an XCD owns a range of output channels, reads all activations).
   int order = 0;
+  // Measurement only (tools/gemm_sweep.py --probe; gemm_wide_kernel and conv_glds_kernel): 1 = no
+  // operand DMA (MFMAs on whatever the LDS holds), 2 = no MFMAs (DMA + waits + barriers only).  The
+  // outputs are garbage; the engine never sets it.
+  int probe = 0;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),

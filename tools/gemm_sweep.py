@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--trials", type=int, default=5)
     ap.add_argument("--bf16", action="store_true", help="bf16 operands instead of split fp32")
     ap.add_argument("--md", default="")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--no-blas", action="store_true", help="skip the hipBLASLt reference columns")
+    ap.add_argument("--probe", type=int, default=0,
+                    help="ConvArgs::probe: 1 = MFMAs without operand DMA, 2 = DMA without MFMAs (LDS-DMA kernels)")
     a = ap.parse_args()
     import torch
 
@@ -64,6 +68,8 @@ def main():
              " | hipBLASLt bf16 | hipBLASLt fp32 |",
              "|---|---:|---:|" + "---:|" * (len(cfgs) + 2)]
     for name, Kd, N, epi in SHAPES:
+        if a.shapes and name not in a.shapes.split(","):
+            continue
         x = torch.randn(a.batch, a.tokens, 1, Kd, device="cuda")
         if not split:
             x = x.to(torch.bfloat16)
@@ -76,14 +82,17 @@ def main():
         pr = K.ConvProblem(x, w, relu=(epi == "gelu"), split=split, max_splits=max(s for _, s in cfgs), **kw)
         row = []
         for c, sp in cfgs:
-            rc = pr.launch(c, sp)
-            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, sp)))
-        A_ = torch.randn(M, Kd, device="cuda")
-        W_ = torch.randn(Kd, N, device="cuda")
-        ab, wb = A_.to(torch.bfloat16), W_.to(torch.bfloat16)
-        tb = timed(lambda: torch.matmul(ab, wb))
-        torch.backends.cuda.matmul.allow_tf32 = False
-        tf = timed(lambda: torch.matmul(A_, W_))
+            ex = {"probe": a.probe} if a.probe else None
+            rc = pr.launch(c, sp, extra=ex)
+            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, sp, extra=ex)))
+        tb = tf = float("nan")
+        if not a.no_blas:
+            A_ = torch.randn(M, Kd, device="cuda")
+            W_ = torch.randn(Kd, N, device="cuda")
+            ab, wb = A_.to(torch.bfloat16), W_.to(torch.bfloat16)
+            tb = timed(lambda: torch.matmul(ab, wb))
+            torch.backends.cuda.matmul.allow_tf32 = False
+            tf = timed(lambda: torch.matmul(A_, W_))
         lines.append("| %s | %d | %d | %s | %.1f | %.1f |" % (name, Kd, N, " | ".join(row), tb, tf))
         print(lines[-1], flush=True)
     if a.md:
