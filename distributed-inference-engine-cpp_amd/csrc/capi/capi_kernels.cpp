@@ -361,10 +361,10 @@ char* die_plan_summary(const char* model_path, int max_batch, int side_branches,
         e["act"] = o.conv.relu;
         e["rows"] = o.conv.Ho * o.conv.Wo;
         e["layernorm_folded"] = o.colsum_off != SIZE_MAX;
-        e["stats_out"] = o.out_stats >= 0;            // writes LayerNorm statistics partials
-        e["stats_from_producer"] = o.in3_parts != 0;  // reads (merges) them
+        e["stats_from_producer"] = o.in3_parts != 0;  // reads (merges) LayerNorm statistics partials
       }
       if (o.kind == PlanOp::LAYERNORM) e["stats_only"] = o.stats_only != 0;
+      if (o.kind == PlanOp::CONV || o.kind == PlanOp::TOKENS) e["stats_out"] = o.out_stats >= 0;  // writes the partials
       if (o.kind == PlanOp::STEM) {
         e["pool_fused"] = o.is_max != 0;
         e["rows"] = o.is_max ? o.Ho * o.Wo : o.conv.Ho * o.conv.Wo;

@@ -1200,7 +1200,8 @@ class HipEngine : public Engine {
           break;
         case PlanOp::TOKENS:
           e = kern::tokens_assemble(static_cast<const uint16_t*>(buf(op.in)), prm(op.scale_off), prm(op.shift_off),
-                                    static_cast<uint16_t*>(buf(op.out)), B, op.S, op.C, st, sp_);
+                                    static_cast<uint16_t*>(buf(op.out)), B, op.S, op.C, st, sp_,
+                                    op.out_stats >= 0 ? static_cast<float*>(buf(op.out_stats)) : nullptr);
           break;
         case PlanOp::GATHER_ROWS:
           e = kern::gather_rows(static_cast<const uint16_t*>(buf(op.in)), static_cast<uint16_t*>(buf(op.out)), B, op.S,

@@ -2510,7 +2510,7 @@ class Planner {
   // also writes per-(row, 64-column group) (mean, M2) partials from the values it holds in registers
   // (ConvArgs::stats_out), and every block of a folded reader merges its rows' groups in a fixed
   // order while its first operand tiles load (ConvArgs::row_parts): no launch, no re-read of the rows.
-  // The block-0 LayerNorm (input from the token assembly) keeps its statistics op.
+  // The block-0 LayerNorm's input comes from the token assembly, which emits the same partials.
   void stats_from_producer() {
     const int nops = static_cast<int>(plan_.ops.size());
     std::vector<std::vector<int>> readers(plan_.bufs.size());
@@ -2525,8 +2525,10 @@ class Planner {
       if (w >= 0 && p.C == p.Cp && p.C % 64 == 0 && p.C <= 2048 && p.join < 0) {
         PlanOp& q = plan_.ops[w];
         const kern::ConvArgs& c = q.conv;
-        bool ok = q.kind == PlanOp::CONV && q.out == p.in && q.out_stats < 0 && q.join < 0 && c.N == p.C &&
-                  c.Ho * c.Wo == p.rows_per_sample && q.out2 < 0;
+        // rows GEMM (attention-out / MLP2), or the token assembly (block 0)
+        const bool gemm = q.kind == PlanOp::CONV && c.N == p.C && c.Ho * c.Wo == p.rows_per_sample && q.out2 < 0;
+        const bool tokens = q.kind == PlanOp::TOKENS && q.C == p.C && q.S + 1 == p.rows_per_sample;
+        bool ok = (gemm || tokens) && q.out == p.in && q.out_stats < 0 && q.join < 0;
         for (int j : readers[p.out]) {
           const PlanOp& r = plan_.ops[j];
           ok = ok && j > i && r.kind == PlanOp::CONV && r.in3 == p.out && r.colsum_off != SIZE_MAX &&

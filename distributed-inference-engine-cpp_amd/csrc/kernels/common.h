@@ -120,5 +120,39 @@ __device__ __forceinline__ void store1v(uint16_t* p, long long plane, bool split
   }
 }
 
+// Cross-lane moves on the VALU (DPP), no LDS round trip (ds_bpermute, which __shfl_xor compiles to,
+// puts a dependent LDS latency on every exchange).  CTRL: quad_perm [1,0,3,2] = 0xB1 (lane ^ 1),
+// [2,3,0,1] = 0x4E (lane ^ 2); row_half_mirror = 0x141 (lane i <-> 7-i within each 8 lanes).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// LayerNorm statistics partials (kernels.h ConvArgs::stats_out): the 8 consecutive, 8-aligned
+// lanes that each hold 8 consecutive channels of one 64-channel group merge (mean, M2) of the 64
+// values by three DPP exchanges (lane ^ 1, lane ^ 2, then the two quads, each uniform by then, so
+// the mirror pairing is the xor-4 pairing).  Equal counts: mean = (a + b) / 2, M2 = M2a + M2b +
+// d^2 n / 2 -- symmetric, so all 8 lanes end with identical bits.  Every lane of the 8 must call it.
+__device__ __forceinline__ float2 group64_stats(const float* v) {
+  float mu = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) mu += v[t];
+  mu *= 0.125f;
+  float m2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) m2 += (v[t] - mu) * (v[t] - mu);
+  float cnt = 8.f;
+  auto round = [&](float mu_o, float m2_o) {
+    const float d = mu_o - mu;
+    m2 = (m2 + m2_o) + d * d * (0.5f * cnt);
+    mu = 0.5f * (mu + mu_o);
+    cnt *= 2.f;
+  };
+  round(dpp<0xB1>(mu), dpp<0xB1>(m2));
+  round(dpp<0x4E>(mu), dpp<0x4E>(m2));
+  round(dpp<0x141>(mu), dpp<0x141>(m2));
+  return make_float2(mu, m2);
+}
+
 }  // namespace k
 }  // namespace die

@@ -44,14 +44,6 @@ __device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byt
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kCpolSc1));
 }
 
-// Cross-lane moves on the VALU (DPP), no LDS round trip (ds_bpermute, which __shfl_xor compiles to,
-// put ~3 dependent LDS latencies per 8-channel chunk on the epilogue's path).  CTRL: quad_perm
-// [1,0,3,2] = 0xB1 (lane ^ 1), [2,3,0,1] = 0x4E (lane ^ 2); row_half_mirror = 0x141 (lane i <-> 7-i
-// within each 8 lanes).
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
 // Chan et al. merge of two (count, mean, M2) summaries in a form symmetric in its operands, so the
 // two lanes of a DPP exchange compute bit-identical results (empty summaries: count 0).
 __device__ __forceinline__ void chan_sym(float& mean, float& m2, float& cnt, float mean_o, float m2_o, float cnt_o) {
@@ -155,27 +147,8 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
     for (int t = 0; t < 8; ++t) v[t] = act_fn(v[t], p.relu, p.clip_lo, p.clip_hi);
   }
   if (p.stats_out) {
-    float mu = 0.f;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) mu += v[t];
-    mu *= 0.125f;
-    float m2 = 0.f;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) m2 += (v[t] - mu) * (v[t] - mu);
-    // lane ^ 1, lane ^ 2, then the two quads of the 8 (each quad uniform by then, so the mirror
-    // pairing is the xor-4 pairing); equal counts: mean = (a + b) / 2, M2 = M2a + M2b + d^2 n / 2
-    float cnt = 8.f;
-    auto round = [&](float mu_o, float m2_o) {
-      const float d = mu_o - mu;
-      m2 = (m2 + m2_o) + d * d * (0.5f * cnt);
-      mu = 0.5f * (mu + mu_o);
-      cnt *= 2.f;
-    };
-    round(dpp<0xB1>(mu), dpp<0xB1>(m2));
-    round(dpp<0x4E>(mu), dpp<0x4E>(m2));
-    round(dpp<0x141>(mu), dpp<0x141>(m2));
-    if ((n & 63) == 0)
-      reinterpret_cast<float2*>(p.stats_out)[static_cast<size_t>(m) * (p.N >> 6) + (n >> 6)] = make_float2(mu, m2);
+    const float2 st = group64_stats(v);
+    if ((n & 63) == 0) reinterpret_cast<float2*>(p.stats_out)[static_cast<size_t>(m) * (p.N >> 6) + (n >> 6)] = st;
   }
   if (p.out) store8v(p.out + o, p.oplane, split, v);
   if (p.out_f32) {

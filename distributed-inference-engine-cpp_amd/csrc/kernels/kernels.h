@@ -333,8 +333,10 @@ hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, co
                           long long rows, int C, hipStream_t s, int split = 0, int Cl = 0, int variant = 0,
                           float* stats = nullptr);
 // out[b,0,:] = cls + pos[0]; out[b,1+s,:] = patches[b,s,:] + pos[1+s]   (cls/pos optional, f32)
+// stats (nullable, C % 64 == 0): also the rows' LayerNorm statistics partials, [B*(S0+1)][C/64] float2
+// (mean, M2) as ConvArgs::stats_out writes them
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
-                           int C, hipStream_t s, int split = 0);
+                           int C, hipStream_t s, int split = 0, float* stats = nullptr);
 // y[b,:] = x[b, idx, :]   (x is [B][S][C])
 hipError_t gather_rows(const uint16_t* x, uint16_t* y, int B, int S, int idx, int C, hipStream_t s, int split = 0);
 // Multi-head attention: out[b,s,h*D:(h+1)*D] = softmax(scale * Q_h K_h^T) V_h with Q/K/V rows

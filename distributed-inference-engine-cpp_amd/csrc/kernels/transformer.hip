@@ -162,9 +162,12 @@ __global__ __launch_bounds__(256) void layernorm_wide_kernel(const uint16_t* __r
 }
 
 // out[b, 0, :] = cls + pos[0];  out[b, 1 + s, :] = patches[b, s, :] + pos[1 + s]
+// stats (nullable, C % 64 == 0): LayerNorm statistics partials of the assembled rows, [B*S][C/64]
+// float2 (mean, M2) -- ConvArgs::stats_out's layout, for a folded reader's row_parts.  The grid-stride
+// loop keeps 8-aligned lane groups on one 64-channel group (256-thread blocks, total % 8 == 0).
 __global__ void tokens_kernel(const uint16_t* __restrict__ patches, const float* __restrict__ cls,
                               const float* __restrict__ pos, uint16_t* __restrict__ out, int B, int S0, int C,
-                              int split) {
+                              int split, float* __restrict__ stats) {
   const int S = S0 + 1;
   const int CG = C / 8;
   const long long total = static_cast<long long>(B) * S * CG;
@@ -184,6 +187,10 @@ __global__ void tokens_kernel(const uint16_t* __restrict__ patches, const float*
     if (pos) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] += pos[static_cast<long long>(s) * C + cg * 8 + t];
+    }
+    if (stats) {
+      const float2 st = group64_stats(v);
+      if ((cg & 7) == 0) reinterpret_cast<float2*>(stats)[r * (C / 64) + cg / 8] = st;
     }
     store8v(out + i * 8, oplane, split != 0, v);
   }
@@ -708,10 +715,10 @@ hipError_t layernorm_rows(const uint16_t* x, uint16_t* y, const float* gamma, co
 }
 
 hipError_t tokens_assemble(const uint16_t* patches, const float* cls, const float* pos, uint16_t* out, int B, int S0,
-                           int C, hipStream_t s, int split) {
-  if (C % 8) return hipErrorInvalidValue;
+                           int C, hipStream_t s, int split, float* stats) {
+  if (C % 8 || (stats && C % 64)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(tokens_kernel, dim3(grid_for(static_cast<long long>(B) * (S0 + 1) * (C / 8))), dim3(256), 0, s,
-                     patches, cls, pos, out, B, S0, C, split);
+                     patches, cls, pos, out, B, S0, C, split, stats);
   return hipGetLastError();
 }
 

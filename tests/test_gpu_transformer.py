@@ -231,17 +231,17 @@ def test_vit_fold_layernorm_vs_torch(native, models, size, stats_epi):
     QKV / first-MLP GEMMs read the residual rows with gamma folded into their weights, beta into
     their bias and (mean, rstd) applied in the epilogue -- same accuracy bar as the unfolded engine
     (fp32 rel-L2 <= 1e-4 against torch, same top-1), in the autotuned and untuned paths.
-    stats_epi (EngineOptions::ln_stats_epilogue, default on): the statistics of all but block 0's
-    LayerNorm come from the attention-out / MLP2 GEMM epilogues as per-64-column (mean, M2)
-    partials -- covered in the fused split-K, two-kernel split-K and plain epilogues."""
+    stats_epi (EngineOptions::ln_stats_epilogue, default on): the statistics come as per-64-column
+    (mean, M2) partials from the token assembly (block 0) and the attention-out / MLP2 GEMM
+    epilogues -- covered in the fused split-K, two-kernel split-K and plain epilogues."""
     import torch
 
     from die_amd.models import vit
 
     path, w, cfg = models["get_vit"](size)
     s = native.plan_summary(path, 8, precision="fp32", fold_layernorm=True, ln_stats_epilogue=stats_epi)
-    assert sum(1 for o in s["ops"] if o.get("stats_only")) == (1 if stats_epi else 2 * cfg.depth)
-    assert sum(1 for o in s["ops"] if o.get("stats_out")) == (2 * cfg.depth - 1 if stats_epi else 0)
+    assert sum(1 for o in s["ops"] if o.get("stats_only")) == (0 if stats_epi else 2 * cfg.depth)
+    assert sum(1 for o in s["ops"] if o.get("stats_out")) == (2 * cfg.depth if stats_epi else 0)
     assert sum(1 for o in s["ops"] if o.get("layernorm_folded")) == 2 * cfg.depth
     x = vit.synthetic_input(5, cfg)
     with torch.no_grad():
