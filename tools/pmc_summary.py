@@ -43,7 +43,8 @@ def load(pass_dir):
 
 
 def short(name):
-    n = name.replace("die::kern::(anonymous namespace)::", "").replace("void ", "")
+    n = name.replace("die::kern::igemm::(anonymous namespace)::", "").replace("die::kern::(anonymous namespace)::", "")
+    n = n.replace("void ", "")
     n = n.split("(")[0]
     return n.replace("conv_igemm_kernel", "igemm").replace("conv_glds_kernel", "glds")
 
