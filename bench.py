@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--no-fold-layernorm", action="store_true",
                     help="standalone LayerNorms instead of statistics + GEMM-epilogue normalisation "
                          "(EngineOptions::fold_layernorm)")
+    ap.add_argument("--tune-in-graph", action="store_true",
+                    help="after the isolated-launch autotune, time each conv's front runners in place inside "
+                         "eager forwards and keep the fastest (EngineOptions::tune_in_graph)")
     ap.add_argument("--no-ln-stats-epilogue", action="store_true",
                     help="measurement: LayerNorm statistics by their own launch instead of the producing "
                          "GEMM's epilogue (EngineOptions::ln_stats_epilogue)")
@@ -255,7 +258,7 @@ def main():
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
-                   "ln_stats_epilogue": not args.no_ln_stats_epilogue}
+                   "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with
@@ -502,7 +505,8 @@ def main():
         ok, failed = args.steps * B, 0
         # device_ms_per_batch: the in-graph forward (hipGraph replay of bucket B, events around it)
         extra = {"engine": eng.refresh_info()["name"], "device_ms_per_batch": eng.info.get("avg_device_ms"),
-                 "engine_options": eng.info.get("options")}
+                 "engine_options": eng.info.get("options"),
+                 "tune_in_graph": {"timed": eng.info.get("tune_in_graph_timed"), "changed": eng.info.get("tune_in_graph_changed")}}
         eng.close()
 
     if world > 1:

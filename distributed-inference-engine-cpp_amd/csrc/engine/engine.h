@@ -247,6 +247,10 @@ struct EngineOptions {
   // epilogue (per-64-column partials, ConvArgs::stats_out / row_parts): no statistics launch
   bool ln_stats_epilogue = true;
   bool tune_cold = true;          // autotune with an L2 scrub before each timing (false: back-to-back)
+  // after the isolated-launch autotune, time each conv's front runners in place inside eager
+  // forwards (input warm from its producer, weights where the previous forward left them) and keep
+  // the fastest (hip_engine.hip tune_in_graph)
+  bool tune_in_graph = false;
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Split-K reductions run in-kernel (the last-arriving split block of a tile sums the partials and

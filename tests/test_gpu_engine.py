@@ -104,6 +104,32 @@ def test_tune_cache_roundtrip(native, models, tmp_path):
     print("engine init with tuning %.2fs, from cache %.2fs" % (t1 - t0, time.time() - t2 + (t2 - t1)))
 
 
+def test_tune_in_graph(native, models, tmp_path):
+    """EngineOptions::tune_in_graph: each conv's isolated-launch front runners are re-timed in place
+    inside eager forwards.  The engine reports what it timed, the outputs stay those of the
+    untuned engine within the fp32 bar, and the in-place choices persist in the tuning file (a second
+    engine with the same file re-times nothing)."""
+    path, w, cfg = models["tiny"]
+    cache = str(tmp_path / "tune.json")
+    x = np.random.default_rng(1).random((5, 3 * 64 * 64), dtype=np.float32)
+    ref = native.Engine(path, device="hip", max_batch=8, autotune=False, tune_cache="")
+    want = ref.run(x)
+    ref.close()
+    e1 = native.Engine(path, device="hip", max_batch=8, tune_cache=cache, tune_in_graph=True)
+    i1 = e1.refresh_info()
+    assert i1["options"]["tune_in_graph"] is True
+    assert i1["tune_in_graph_timed"] > 0 and 0 <= i1["tune_in_graph_changed"] <= i1["tune_in_graph_timed"]
+    got = e1.run(x)
+    e1.close()
+    assert np.linalg.norm(got - want) / np.linalg.norm(want) < 1e-5
+    data = json.load(open(cache))
+    assert any(k.startswith("g") for v in data.values() for k in v)
+    e2 = native.Engine(path, device="hip", max_batch=8, tune_cache=cache, tune_in_graph=True)
+    i2 = e2.refresh_info()
+    assert i2["tune_in_graph_timed"] == 0 and i2["tile_split_at_max_batch"] == i1["tile_split_at_max_batch"]
+    e2.close()
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_branch_streams_bit_identical(native, models, graphs):
     """Projection shortcuts on the side stream (hipGraph branches, or eager fork/join events) give

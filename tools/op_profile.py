@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--no-fuse-pairs", action="store_true", help="unfused expand/reduce convs (EngineOptions::fuse_pairs)")
     ap.add_argument("--ln-xcd", type=int, default=0, help="LayerNorm row order: 1 XCD-affine, 0 natural (default)")
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
+    ap.add_argument("--tune-in-graph", action="store_true", help="EngineOptions::tune_in_graph")
     ap.add_argument("--no-ln-stats-epilogue", action="store_true",
                     help="LayerNorm statistics launches instead of producer-epilogue partials (EngineOptions::ln_stats_epilogue)")
     ap.add_argument("--fuse-gap-fc", action="store_true", help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
@@ -49,12 +50,15 @@ def main():
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
                       splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
                       fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm,
-                      ln_stats_epilogue=not a.no_ln_stats_epilogue)
+                      ln_stats_epilogue=not a.no_ln_stats_epilogue, tune_in_graph=a.tune_in_graph)
     p = e.profile(a.batch, a.iters)
+    info = e.refresh_info()
     e.close()
     lines = ["# %s per-op device time, batch %d (MI355X, %s, tuned kernels)" % (a.arch, p["batch"], a.precision), "",
              "Total %.1f us per forward = %.1f TFLOP/s over the whole graph; %.0f images/s device-bound." % (
                  p["total_us"], p["tflops"], p["batch"] / p["total_us"] * 1e6), "",
+             "In-graph retune: %s (%s candidates timed in place, %s convs changed)." % (
+                 "on" if a.tune_in_graph else "off", info.get("tune_in_graph_timed"), info.get("tune_in_graph_changed")), "",
              "| # | op | kind | us | GFLOP | TFLOP/s | tile/splits |", "|---:|---|---|---:|---:|---:|---|"]
     for i, o in enumerate(p["ops"]):
         ts = ("%d/%d" % (o["tile"], o["splits"]) + ("f" if o.get("fused_splitk") else "")) if "tile" in o else ""
