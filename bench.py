@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--no-fold-layernorm", action="store_true",
                     help="standalone LayerNorms instead of statistics + GEMM-epilogue normalisation "
                          "(EngineOptions::fold_layernorm)")
+    ap.add_argument("--no-tune-orders", action="store_true",
+                    help="measurement: autotune with the heuristic XCD tile order only (EngineOptions::tune_orders)")
     ap.add_argument("--tune-in-graph", action="store_true",
                     help="after the isolated-launch autotune, time each conv's front runners in place inside "
                          "eager forwards and keep the fastest (EngineOptions::tune_in_graph)")
@@ -258,7 +260,8 @@ def main():
                    "device_decode": not args.no_device_decode, "fuse_pairs": not args.no_fuse_pairs,
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
-                   "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph}
+                   "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph,
+                   "tune_orders": not args.no_tune_orders}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

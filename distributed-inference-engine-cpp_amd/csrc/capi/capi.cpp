@@ -102,6 +102,7 @@ EngineOptions engine_opts(const Json& j) {
   e.fold_layernorm = jget<bool>(j, "fold_layernorm", e.fold_layernorm);
   e.ln_stats_epilogue = jget<bool>(j, "ln_stats_epilogue", e.ln_stats_epilogue);
   e.tune_in_graph = jget<bool>(j, "tune_in_graph", e.tune_in_graph);
+  e.tune_orders = jget<bool>(j, "tune_orders", e.tune_orders);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));

@@ -251,6 +251,9 @@ struct EngineOptions {
   // forwards (input warm from its producer, weights where the previous forward left them) and keep
   // the fastest (hip_engine.hip tune_in_graph)
   bool tune_in_graph = false;
+  // autotune the XCD tile order too: the 2- and 4-panel orders (ConvArgs::order 3 / 4) next to the
+  // heuristic, for convs that replicate their weights on every XCD (profiles/r5_xcd_panels.md)
+  bool tune_orders = true;
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Split-K reductions run in-kernel (the last-arriving split block of a tile sums the partials and

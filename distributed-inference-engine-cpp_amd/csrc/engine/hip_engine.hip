@@ -885,6 +885,17 @@ class HipEngine : public Engine {
   // its input just written by the previous layer and its weights from the Infinity Cache, never a
   // warm L2 -- warm back-to-back timing favoured shallow LDS rings whose load latency is exposed
   // once the operands come from further away (stage-3 3x3 convs: 17.5 us tuned, 27 us in the graph).
+  // Tune-cache / memo key of a conv problem: the shape, its epilogue, and the tuning regime.
+  std::string shape_key(const kern::ConvArgs& base, bool warm_input) const {
+    char key[256];
+    std::snprintf(key, sizeof(key), "o%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_cold ? "c:" : "",
+                  warm_input ? "w:" : "", sp_ ? "f32:" : "", base.stats_out || base.row_parts ? "ls:" : "",
+                  opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : (opt_.tune_orders ? "" : "o0:"),
+                  base.M, base.N, base.K, base.Cin, base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu,
+                  base.res != nullptr, base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
+    return key;
+  }
+
   void autotune() {
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
@@ -924,12 +935,7 @@ class HipEngine : public Engine {
               producer = j;
           }
         // identical problems (repeated blocks) share one measurement
-        char key[256];
-        std::snprintf(key, sizeof(key), "o%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", cold ? "c:" : "", producer >= 0 ? "w:" : "", sp_ ? "f32:" : "",
-                      base.stats_out || base.row_parts ? "ls:" : "",
-                      opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : "", base.M, base.N, base.K, base.Cin,
-                      base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu, base.res != nullptr,
-                      base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
+        const std::string key = shape_key(base, producer >= 0);
         auto memo = tuned_shapes.find(key);
         // (a cached result without this run's candidate list is re-measured when the in-graph pass
         // needs the front runners -- unless that pass's own results are cached too)
@@ -947,10 +953,24 @@ class HipEngine : public Engine {
             if (sp > 1 && (base.N % 8 || sp > nk || kern::splitk_workspace_bytes(base.M, base.N, sp) > ws_bytes_)) break;
             // split-K candidates reduce in-kernel unless the two-kernel form is allowed
             for (int fused = sp > 1 && !opt_.splitk_two_kernel ? 1 : 0; fused < (sp > 1 ? 2 : 1); ++fused)
-            // Tile order stays the heuristic (ConvArgs::order 0): tuning N- vs M-fastest per shape
-            // picked M-fastest for ~30 % of shapes behind a cold L2 but made the in-graph forwards
-            // 1-2 % slower (profiles/r3_gemm_feed.md section 6).
-            for (int order = 0; order <= 0; ++order) {
+            // Tile order: the heuristic (ConvArgs::order 0; tuning N- vs M-fastest per shape picked
+            // M-fastest for ~30 % of shapes behind a cold L2 but made the in-graph forwards 1-2 %
+            // slower, profiles/r3_gemm_feed.md section 6), plus -- where the heuristic replicates the
+            // weights on every XCD, there are >= 4 N-tiles and the activations are at most 3x the
+            // weights (a panel order reads every activation row once per panel: ViT's MLP2, 8x,
+            // won in isolation and lost 16 % in the graph) -- the 2- and 4-panel orders, whose
+            // XCDs each read one panel of the weights (profiles/r5_xcd_panels.md)
+            for (int order : {0, 3, 4}) {
+              if (order > 0 && !opt_.tune_orders) continue;
+              if (order > 0) {
+                int bm, bn;
+                kern::tile_dims(tile, bm, bn);
+                const long long wts = static_cast<long long>(base.N) * base.K;
+                const long long acts = static_cast<long long>(base.B) * base.H * base.W * base.Cin;
+                if (tile / kern::NUM_TILES == 6 || tile / kern::NUM_TILES == 7 || wts > acts || acts > 3 * wts ||
+                    (base.N + bn - 1) / bn < 4 * (order == 4 ? 2 : 1))
+                  continue;
+              }
               kern::ConvArgs a = base;
               a.splits = sp;
               a.order = order;
@@ -1052,13 +1072,7 @@ class HipEngine : public Engine {
           continue;
         }
         kern::ConvArgs base = conv_args(op, B, 0);
-        char key[256];  // the isolated-launch key of this shape (autotune), for its candidates
-        std::snprintf(key, sizeof(key), "o%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_cold ? "c:" : "", "",
-                      sp_ ? "f32:" : "", base.stats_out || base.row_parts ? "ls:" : "",
-                      opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : "", base.M, base.N,
-                      base.K, base.Cin, base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu,
-                      base.res != nullptr, base.out2 != nullptr, base.out_f32 != nullptr, base.out != nullptr);
-        const auto c = cands_.find(key);
+        const auto c = cands_.find(shape_key(base, false));  // the isolated-launch front runners
         if (c == cands_.end() || c->second.size() < 2) continue;
         float best = 1e30f;
         Tune bt = tune_[bi][oi];

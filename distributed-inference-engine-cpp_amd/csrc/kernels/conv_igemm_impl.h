@@ -214,11 +214,21 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   const long long acts = static_cast<long long>(p.B) * p.H * p.W * p.Cin;
   // One division and selects, no branch: with the outputs assigned on two paths the compiler kept
   // them in scratch (a private-memory round trip at the start of every block).
-  const bool nfast = p.order == 1 || (p.order == 0 && wts <= acts);
-  const int minor = nfast ? ntn : ntm;
-  const int hi = tile / minor, lo = tile - hi * minor;
+  const bool nfast = p.order == 1 || (p.order == 0 && wts <= acts) || p.order >= 3;
+  // order 3 / 4: N split into 2 / 4 panels, tiles panel-major (N-fastest inside a panel), so the
+  // contiguous id range an XCD gets needs only its panel's weight rows (a panel of a large GEMM's
+  // weights fits the XCD's 4 MiB L2 where all of them do not).  Full panels first; the last panel
+  // may be narrower.
+  const int P = p.order == 3 ? 2 : p.order == 4 ? 4 : 1;
+  const int pw = (ntn + P - 1) / P;               // panel width (N-tiles)
+  const int full = ntn / pw;                      // panels of full width
+  const int pk = min(tile / (pw * ntm), full);    // panel index (the last one may be partial)
+  const int rem = tile - pk * pw * ntm;
+  const int w = min(pw, ntn - pk * pw);           // this panel's width
+  const int minor = P > 1 ? w : nfast ? ntn : ntm;
+  const int hi = rem / minor, lo = rem - hi * minor;
   tile_m = nfast ? hi : lo;
-  tile_n = nfast ? lo : hi;
+  tile_n = nfast ? lo + pk * pw : hi;
   return true;
 }
 

@@ -78,7 +78,8 @@ struct ConvArgs {
   long long xplane = 0, oplane = 0;
   // Tile order of the XCD-aware block mapping (autotuned): 0 = heuristic (replicate the smaller
   // operand on every XCD), 1 = N-fastest (an XCD owns a range of pixel rows, reads all weights),
-  // 2 = M-fastest (an XCD owns a range of output channels, reads all activations).
+  // 2 = M-fastest (an XCD owns a range of output channels, reads all activations), 3 / 4 = N in 2 / 4
+  // panels, panel-major (an XCD's range reads one panel of the weights).
   int order = 0;
   // Measurement only (tools/gemm_sweep.py --probe; gemm_wide_kernel and conv_glds_kernel): 1 = no
   // operand DMA (MFMAs on whatever the LDS holds), 2 = no MFMAs (DMA + waits + barriers only).  The

@@ -136,7 +136,7 @@ def test_split_conv_tile_order_bitwise(native):
             if pr.launch(cfg, splits, True, 0) == 1:
                 continue
             ref = pr.out.clone()
-            for order in (1, 2):
+            for order in (1, 2, 3, 4):
                 assert pr.launch(cfg, splits, True, order) == 0
                 assert torch.equal(ref.view(torch.int16), pr.out.view(torch.int16)), (cfg, splits, order)
 

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="bf16 operands instead of split fp32")
     ap.add_argument("--md", default="")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--order", type=int, default=0, help="ConvArgs::order (XCD tile order)")
     ap.add_argument("--no-blas", action="store_true", help="skip the hipBLASLt reference columns")
     ap.add_argument("--probe", type=int, default=0,
                     help="ConvArgs::probe: 1 = MFMAs without operand DMA, 2 = DMA without MFMAs (LDS-DMA kernels)")
@@ -83,8 +84,8 @@ def main():
         row = []
         for c, sp in cfgs:
             ex = {"probe": a.probe} if a.probe else None
-            rc = pr.launch(c, sp, extra=ex)
-            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, sp, extra=ex)))
+            rc = pr.launch(c, sp, order=a.order, extra=ex)
+            row.append("n/a" if rc == 1 else "%.1f" % timed(lambda: pr.launch(c, sp, order=a.order, extra=ex)))
         tb = tf = float("nan")
         if not a.no_blas:
             A_ = torch.randn(M, Kd, device="cuda")

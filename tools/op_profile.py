@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--ln-xcd", type=int, default=0, help="LayerNorm row order: 1 XCD-affine, 0 natural (default)")
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
     ap.add_argument("--tune-in-graph", action="store_true", help="EngineOptions::tune_in_graph")
+    ap.add_argument("--no-tune-orders", action="store_true", help="heuristic XCD tile order only (EngineOptions::tune_orders)")
+    ap.add_argument("--conv-order", type=int, default=0, help="EngineOptions::conv_order (XCD tile order override)")
     ap.add_argument("--no-ln-stats-epilogue", action="store_true",
                     help="LayerNorm statistics launches instead of producer-epilogue partials (EngineOptions::ln_stats_epilogue)")
     ap.add_argument("--fuse-gap-fc", action="store_true", help="global pool and FC head as one launch (EngineOptions::fuse_gap_fc)")
@@ -50,7 +52,8 @@ def main():
                       tune_warm_input=a.tune_warm_input, fuse_pairs=not a.no_fuse_pairs,
                       splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
                       fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm,
-                      ln_stats_epilogue=not a.no_ln_stats_epilogue, tune_in_graph=a.tune_in_graph)
+                      ln_stats_epilogue=not a.no_ln_stats_epilogue, tune_in_graph=a.tune_in_graph, conv_order=a.conv_order,
+                      tune_orders=not a.no_tune_orders)
     p = e.profile(a.batch, a.iters)
     info = e.refresh_info()
     e.close()
