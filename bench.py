@@ -125,6 +125,9 @@ def main():
                     help="keep ResNet's expand and next reduce convs as two launches (EngineOptions::fuse_pairs)")
     ap.add_argument("--no-pack-text", action="store_true",
                     help="upload input text as-is instead of 4-bit packed (device decode)")
+    ap.add_argument("--prep-on-compute", action="store_true",
+                    help="measurement: run each batch's decode/prep on the compute stream before its forward "
+                         "instead of on the copy stream under the previous forward (EngineOptions::prep_on_compute)")
     ap.add_argument("--no-device-decode", action="store_true",
                     help="parse input_data on the host CPU instead of decoding the JSON text on the GPU")
     ap.add_argument("--device", choices=["hip", "cpu"], default="hip",
@@ -261,7 +264,7 @@ def main():
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
                    "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph,
-                   "tune_orders": not args.no_tune_orders}
+                   "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with
