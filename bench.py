@@ -125,6 +125,11 @@ def main():
                     help="keep ResNet's expand and next reduce convs as two launches (EngineOptions::fuse_pairs)")
     ap.add_argument("--no-pack-text", action="store_true",
                     help="upload input text as-is instead of 4-bit packed (device decode)")
+    ap.add_argument("--no-efficient-batch", action="store_true",
+                    help="dispatch everything queued (up to --batch) instead of cutting a batch back to just "
+                         "below a per-image device-time step (EngineOptions::efficient_batch)")
+    ap.add_argument("--efficient-batch-tol", type=float, default=0.03,
+                    help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
     ap.add_argument("--prep-on-compute", action="store_true",
                     help="measurement: run each batch's decode/prep on the compute stream before its forward "
                          "instead of on the copy stream under the previous forward (EngineOptions::prep_on_compute)")
@@ -264,7 +269,8 @@ def main():
                    "fuse_stem_pool": not args.no_fuse_stem_pool,
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
                    "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph,
-                   "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute}
+                   "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute,
+                   "efficient_batch": not args.no_efficient_batch, "efficient_batch_tol": args.efficient_batch_tol}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with
@@ -340,6 +346,9 @@ def main():
                      "slowest_ms": res.get("slowest_ms", []), "device_trace": _device_trace(trace, t0)},
             "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
+            # EngineOptions::efficient_batch: batches cut below the queue to stay under a per-image step
+            "trimmed_batches": bp1.get("trimmed_batches", 0) - bp0.get("trimmed_batches", 0),
+            "trimmed_requests": bp1.get("trimmed_requests", 0) - bp0.get("trimmed_requests", 0),
             "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
             "precision": e1.get("precision"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),

@@ -103,6 +103,8 @@ EngineOptions engine_opts(const Json& j) {
   e.ln_stats_epilogue = jget<bool>(j, "ln_stats_epilogue", e.ln_stats_epilogue);
   e.tune_in_graph = jget<bool>(j, "tune_in_graph", e.tune_in_graph);
   e.tune_orders = jget<bool>(j, "tune_orders", e.tune_orders);
+  e.efficient_batch = jget<bool>(j, "efficient_batch", e.efficient_batch);
+  e.efficient_batch_tol = jget<double>(j, "efficient_batch_tol", e.efficient_batch_tol);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
@@ -232,7 +234,8 @@ struct TestBatcher {
   std::vector<int> sizes;
   int delay_ms = 0;
 };
-void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int delay_ms) {
+// size_cap > 0: a batch-size function (Engine::preferred_batch's hook) that takes at most size_cap
+void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int delay_ms, int size_cap) {
   auto* t = new TestBatcher();
   t->delay_ms = delay_ms;
   t->bp = std::make_unique<BatchProcessor<int, int>>(
@@ -251,6 +254,8 @@ void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int
         return out;
       },
       deadline_policy ? BatchPolicy::DEADLINE : BatchPolicy::GREEDY);
+  if (size_cap > 0)
+    t->bp->set_size_fn([cap = static_cast<size_t>(size_cap)](size_t q) { return q > cap ? cap : q; });
   t->bp->start();
   return t;
 }
@@ -271,6 +276,8 @@ char* die_batcher_metrics(void* p) {
   j["timeout_batches"] = static_cast<long long>(m.timeout_batches);
   j["full_batches"] = static_cast<long long>(m.full_batches);
   j["avg_batch_size"] = m.avg_batch_size;
+  j["trimmed_batches"] = t->bp->trimmed_batches();
+  j["trimmed_requests"] = t->bp->trimmed_requests();
   Json s = Json::array();
   {
     std::lock_guard<std::mutex> g(t->mu);
@@ -325,6 +332,7 @@ int die_engine_run(void* p, const float* in, long B, long len, float* out, char*
 // 4-bit text packing (core/textpack.h): returns 1 if packed, 0 if a byte is outside the alphabet.
 int die_pack_nibbles(const char* src, long long n, unsigned char* dst) { return pack_nibbles(src, static_cast<size_t>(n), dst) ? 1 : 0; }
 void die_unpack_nibbles(const unsigned char* src, long long n, char* dst) { unpack_nibbles(src, static_cast<size_t>(n), dst); }
+int die_engine_preferred_batch(void* p, int queued) { return static_cast<Engine*>(p)->preferred_batch(queued); }
 int die_engine_text_packing(void* p) { return static_cast<Engine*>(p)->text_packing() ? 1 : 0; }
 
 // Device-decode path: B texts (concatenated, lens[b] bytes each) -> outputs [B][out] and status[b]

@@ -296,6 +296,8 @@ Json engine_options_json(const EngineOptions& o) {
   j["ln_stats_epilogue"] = o.ln_stats_epilogue;
   j["tune_in_graph"] = o.tune_in_graph;
   j["tune_orders"] = o.tune_orders;
+  j["efficient_batch"] = o.efficient_batch;
+  j["efficient_batch_tol"] = o.efficient_batch_tol;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;

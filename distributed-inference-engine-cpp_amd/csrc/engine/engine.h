@@ -117,6 +117,10 @@ class Engine {
   // An engine that knows when the batch in flight will drain returns (drain - lead), where lead
   // covers the next batch's copies; dispatching earlier only makes the next batch smaller.
   virtual std::chrono::steady_clock::time_point dispatch_not_before() { return std::chrono::steady_clock::now(); }
+  // Batch size to dispatch when `queued` requests are waiting (1 <= result <= queued): an engine
+  // whose per-image cost steps up at some batch sizes (tile grids spilling into another round of
+  // blocks) may take fewer and leave the rest for the next batch.
+  virtual int preferred_batch(int queued) const { return queued; }
   // Drain everything in flight.
   virtual void synchronize() = 0;
 
@@ -263,6 +267,12 @@ struct EngineOptions {
   // splitk_two_kernel only: take the fastest in-kernel (fused) split-K candidate when it is within
   // this fraction of the overall best
   float splitk_fused_margin = 0.f;
+  // Efficient batch sizes (HIP, graphs): time the captured forward of every batch size once at
+  // start-up; with Q requests queued, dispatch the largest B <= Q whose per-image device time is
+  // within efficient_batch_tol of the best B' <= Q (ResNet50 fp32: B = 21 costs 19 % more than
+  // B = 20 for 5 % more images, profiles/r5_batch_curve.md).  0 tolerance = always the best.
+  bool efficient_batch = true;
+  double efficient_batch_tol = 0.03;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;

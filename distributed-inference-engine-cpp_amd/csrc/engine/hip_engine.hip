@@ -13,6 +13,7 @@
 #include <pthread.h>
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <chrono>
 #include <condition_variable>
 #include <unistd.h>
@@ -269,6 +270,7 @@ class HipEngine : public Engine {
       // warm the graph path once
       HIP_CHECK(hipGraphLaunch(graphs_.back(), s_compute_));
       HIP_CHECK(hipStreamSynchronize(s_compute_));
+      if (opt.efficient_batch && n_exec_ == 1 && !comm_) measure_batch_curve();
     }
     for (auto& e : tev_) HIP_CHECK(hipEventCreate(&e));
     completion_ = std::thread([this] {
@@ -662,6 +664,22 @@ class HipEngine : public Engine {
     return t;
   }
 
+  // EngineOptions::efficient_batch: the largest B <= queued whose per-image device time (the
+  // start-up curve) is within efficient_batch_tol of the best B' <= queued.  Per-image time falls
+  // with B except where a layer's tile grid spills into one more round of blocks (ResNet50 fp32:
+  // 61.6 us per image at B = 20, 69.6 at 21, profiles/r5_batch_curve.md), so this only ever cuts a
+  // batch back to just below such a step; the requests left over lead the next batch.
+  int preferred_batch(int queued) const override {
+    const int q = std::min(queued, max_batch_);
+    if (batch_ms_.empty() || q <= 1) return std::max(1, q);
+    double best = 1e30;
+    for (int b = 1; b <= q; ++b) best = std::min(best, batch_ms_[static_cast<size_t>(b)] / b);
+    const double lim = best * (1.0 + std::max(0.0, opt_.efficient_batch_tol));
+    for (int b = q; b > 1; --b)
+      if (batch_ms_[static_cast<size_t>(b)] / b <= lim) return b;
+    return 1;
+  }
+
   void synchronize() override {
     std::unique_lock<std::mutex> lk(mu_);
     slot_cv_.wait(lk, [&] { return inflight_ == 0 && callbacks_running_ == 0; });
@@ -699,6 +717,12 @@ class HipEngine : public Engine {
       j["pace_margin_ms"] = margin_ms_;
     }
     j["hip_graphs"] = !graphs_.empty();
+    j["efficient_batch"] = !batch_ms_.empty();
+    if (!batch_ms_.empty()) {
+      Json c = Json::array();  // device ms of the captured forward at batch 1, 2, ..., max_batch
+      for (size_t b = 1; b < batch_ms_.size(); ++b) c.push_back(std::round(batch_ms_[b] * 1e4) / 1e4);
+      j["batch_curve_ms"] = c;
+    }
     j["pipeline_depth"] = depth_;
     j["executors"] = n_exec_;
     j["copy_streams"] = n_copy_streams_;
@@ -858,6 +882,36 @@ class HipEngine : public Engine {
     a.stats_out = op.out_stats >= 0 ? static_cast<float*>(buf_ptr(op.out_stats, s)) : nullptr;
     a.col_sum = prm_ptr(op.colsum_off);
     return a;
+  }
+
+  // Device time of the captured forward at every batch size 1..max_batch (EngineOptions::
+  // efficient_batch): slot 0's MAIN graph of the batch's bucket with the live count set to B, one
+  // warm-up and three timed back-to-back replays (the serving loop runs graphs back to back).
+  void measure_batch_curve() {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    Slot& sl = slots_[0];
+    long long* lv = sl.h_lens + live_index();
+    batch_ms_.assign(static_cast<size_t>(max_batch_) + 1, 0.0);
+    for (int b = 1; b <= max_batch_; ++b) {
+      hipGraphExec_t g = graphs_[bucket_index(b) * static_cast<size_t>(depth_)];
+      *lv = use_live_ ? b : max_batch_;
+      HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
+      HIP_CHECK(hipGraphLaunch(g, s_compute_));
+      HIP_CHECK(hipEventRecord(e0, s_compute_));
+      for (int r = 0; r < 3; ++r) HIP_CHECK(hipGraphLaunch(g, s_compute_));
+      HIP_CHECK(hipEventRecord(e1, s_compute_));
+      HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      batch_ms_[static_cast<size_t>(b)] = ms / 3.0;
+    }
+    *lv = max_batch_;
+    HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
+    HIP_CHECK(hipStreamSynchronize(s_compute_));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   }
 
   size_t bucket_index(int B) const {
@@ -1771,6 +1825,7 @@ class HipEngine : public Engine {
   int last_ev_ = -1, last_bi_ = 0;  // most recent submitted job (guarded by mu_)
   mutable std::mutex pace_mu_;
   std::vector<double> est_ms_;      // EMA device ms per bucket (pace_mu_)
+  std::vector<double> batch_ms_;    // start-up device ms per batch size (efficient_batch; empty = off)
   double lead_ms_ = 0.3, lead_ms_total_ = 0.0, input_ms_ = 0.0, margin_ms_ = 0.08;
   std::chrono::steady_clock::time_point pace_drain_{};  // predicted drain of the batch in flight
   bool pace_armed_ = false;

@@ -47,6 +47,9 @@ class BatchProcessor {
   // Optional pacing (GREEDY): after ReadyFn, requests keep accumulating until the returned time or
   // until a full batch is queued, whichever comes first.
   using PaceFn = std::function<std::chrono::steady_clock::time_point()>;
+  // Optional batch sizing: given the requests queued (capped at max_batch_size), how many to take
+  // (Engine::preferred_batch); the rest stay queued, oldest first out, for the next batch.
+  using SizeFn = std::function<size_t(size_t)>;
 
   struct Metrics {
     int64_t total_requests = 0;
@@ -150,6 +153,12 @@ class BatchProcessor {
     return m;
   }
 
+  // Set before start().
+  void set_size_fn(SizeFn fn) { size_ = std::move(fn); }
+  // Batches the size function cut below the queue (and the requests it left queued).
+  long long trimmed_batches() const { return trimmed_batches_.load(); }
+  long long trimmed_requests() const { return trimmed_requests_.load(); }
+
   // Total time the batcher held dispatches back for pacing.
   double paced_ms() const { return paced_ns_.load() / 1e6; }
 
@@ -197,7 +206,14 @@ class BatchProcessor {
       {
         std::lock_guard<std::mutex> g(mu_);
         if (!running_) return;
-        while (!queue_.empty() && batch.size() < max_batch_) {
+        const size_t q = std::min(queue_.size(), max_batch_);
+        size_t take = q;
+        if (size_ && q > 1) take = std::max<size_t>(1, std::min(q, size_(q)));
+        if (take < q) {
+          trimmed_batches_.fetch_add(1, std::memory_order_relaxed);
+          trimmed_requests_.fetch_add(static_cast<long long>(q - take), std::memory_order_relaxed);
+        }
+        while (!queue_.empty() && batch.size() < take) {
           batch.push_back(std::move(queue_.front()));
           queue_.pop_front();
         }
@@ -248,7 +264,9 @@ class BatchProcessor {
   AsyncBatchFn async_;
   ReadyFn ready_;
   PaceFn pace_;
+  SizeFn size_;
   std::atomic<long long> paced_ns_{0};
+  std::atomic<long long> trimmed_batches_{0}, trimmed_requests_{0};
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Item> queue_;

@@ -77,7 +77,7 @@ def lib() -> C.CDLL:
         sig("die_cache_put", None, vp, f32p, C.c_long, f32p, C.c_long)
         sig("die_cache_get", C.c_long, vp, f32p, C.c_long, f32p, C.c_long)
         sig("die_cache_stats", vp, vp)
-        sig("die_batcher_create", vp, C.c_int, C.c_int, C.c_int, C.c_int)
+        sig("die_batcher_create", vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int)
         sig("die_batcher_process", C.c_int, vp, C.c_int, errp)
         sig("die_batcher_metrics", vp, vp)
         sig("die_batcher_stop", None, vp)
@@ -90,6 +90,7 @@ def lib() -> C.CDLL:
         sig("die_pack_nibbles", C.c_int, C.c_char_p, C.c_longlong, C.c_char_p)
         sig("die_unpack_nibbles", None, C.c_char_p, C.c_longlong, C.c_char_p)
         sig("die_engine_text_packing", C.c_int, vp)
+        sig("die_engine_preferred_batch", C.c_int, vp, C.c_int)
         sig("die_engine_profile", vp, vp, C.c_int, C.c_int)
         sig("die_dp_follower_start", vp, cp, errp)
         sig("die_dp_follower_status", vp, vp)
@@ -320,8 +321,9 @@ class Cache:
 class TestBatcher:
     """BatchProcessor<int,int> doubling each request (unit tests)."""
 
-    def __init__(self, max_batch: int, timeout_ms: int, deadline: bool = False, delay_ms: int = 0):
-        self.h = lib().die_batcher_create(max_batch, timeout_ms, int(deadline), delay_ms)
+    def __init__(self, max_batch: int, timeout_ms: int, deadline: bool = False, delay_ms: int = 0, size_cap: int = 0):
+        """size_cap > 0: a batch-size hook (as Engine::preferred_batch) that takes at most size_cap."""
+        self.h = lib().die_batcher_create(max_batch, timeout_ms, int(deadline), delay_ms, size_cap)
 
     def process(self, v: int) -> int:
         err = _err_box()
@@ -388,6 +390,10 @@ class Engine:
     def profile(self, batch: int = 32, iters: int = 10) -> Dict[str, Any]:
         """Per-op device time (µs) of one forward at `batch` (HIP engine; {} for the CPU engine)."""
         return json.loads(_take_str(lib().die_engine_profile(self.h, batch, iters)))
+
+    def preferred_batch(self, queued: int) -> int:
+        """Batch size the worker dispatches with `queued` requests waiting (EngineOptions::efficient_batch)."""
+        return int(lib().die_engine_preferred_batch(self.h, int(queued)))
 
     @property
     def text_packing(self) -> bool:

@@ -227,6 +227,28 @@ def test_batcher_greedy_semantics(native):
     b.stop()
 
 
+def test_batcher_size_hook_trims_batches(native):
+    """The batch-size hook (the worker wires Engine::preferred_batch into it) may take fewer than
+    queued: the rest stay queued, oldest first out, and every request still completes once."""
+    b = native.TestBatcher(max_batch=8, timeout_ms=20, deadline=False, delay_ms=30, size_cap=3)
+    results = [None] * 20
+
+    def run(i):
+        results[i] = b.process(i)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(20)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert results == [2 * i for i in range(20)]
+    m = b.metrics()
+    assert sum(m["sizes"]) == 20 and max(m["sizes"]) <= 3
+    # with 30 ms per batch the queue outgrows the cap, so some batches were cut
+    assert m["trimmed_batches"] >= 1 and m["trimmed_requests"] >= m["trimmed_batches"]
+    b.stop()
+
+
 def test_batcher_deadline_waits_for_full_batch(native):
     b = native.TestBatcher(max_batch=8, timeout_ms=200, deadline=True)
     out = []

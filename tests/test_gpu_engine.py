@@ -130,6 +130,36 @@ def test_tune_in_graph(native, models, tmp_path):
     e2.close()
 
 
+def test_efficient_batch_curve(native, models):
+    """EngineOptions::efficient_batch: the engine times its captured forward at every batch size at
+    start-up and preferred_batch(Q) is the largest B <= Q within efficient_batch_tol of the best
+    per-image time over 1..Q; a batch it cuts back still runs correctly at that size.  Off: no curve
+    and every queue is taken whole."""
+    path, w, cfg = models["tiny"]
+    tol = 0.03
+    e = native.Engine(path, device="hip", max_batch=16, autotune=False, tune_cache="", efficient_batch_tol=tol)
+    info = e.refresh_info()
+    curve = info["batch_curve_ms"]
+    assert info["efficient_batch"] is True and len(curve) == 16 and all(c > 0 for c in curve)
+    per = [c / (b + 1) for b, c in enumerate(curve)]
+    for q in range(1, 17):
+        b = e.preferred_batch(q)
+        assert 1 <= b <= q
+        assert per[b - 1] <= min(per[:q]) * (1 + tol) + 1e-9
+        assert all(per[c - 1] > min(per[:q]) * (1 + tol) for c in range(b + 1, q + 1))
+    assert e.preferred_batch(40) <= 16
+    x = np.random.default_rng(2).random((16, 3 * 64 * 64), dtype=np.float32)
+    full = e.run(x)
+    b = e.preferred_batch(16)
+    part = e.run(x[:b])  # another bucket's graph: its own tile configs, so fp32-close rather than bitwise
+    assert np.linalg.norm(part - full[:b]) / np.linalg.norm(full[:b]) < 1e-5
+    e.close()
+    off = native.Engine(path, device="hip", max_batch=16, autotune=False, tune_cache="", efficient_batch=False)
+    assert off.refresh_info()["efficient_batch"] is False and "batch_curve_ms" not in off.refresh_info()
+    assert [off.preferred_batch(q) for q in (1, 7, 16)] == [1, 7, 16]
+    off.close()
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_branch_streams_bit_identical(native, models, graphs):
     """Projection shortcuts on the side stream (hipGraph branches, or eager fork/join events) give

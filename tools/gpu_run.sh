@@ -32,7 +32,7 @@ dw = d.get("direct_worker", {})
 dp = d.get("dp_rccl") or {}
 print(sys.argv[2], round(d["value"]), "p50", d.get("p50_ms"), "p99", d.get("p99_ms"), "batch", d.get("avg_batch") or d.get("avg_dp_batch"),
       "dev_ms", d.get("device_ms_per_batch"), "gap_ms", d.get("gpu_gap_ms_per_batch"), "cache_hits", d.get("cache_hits_timed"),
-      "direct", round(dw.get("rps_this_rank", 0)), dw.get("p99_ms"), "dp_rccl", dp.get("requests_per_s"), dp.get("p99_ms"), dp.get("error", ""))
+      "trim", d.get("trimmed_batches"), "direct", round(dw.get("rps_this_rank", 0)), dw.get("p99_ms"), "dp_rccl", dp.get("requests_per_s"), dp.get("p99_ms"), dp.get("error", ""))
 EOF
 }
 

@@ -18,13 +18,60 @@ def short(name: str) -> str:
     return n.replace("conv_glds_kernel", "glds").replace("conv_igemm_kernel", "igemm")[:110]
 
 
+SIDE = ("pk_count", "pk_parse", "copyBuffer", "fillBuffer", "copy_i64", "unpack", "decode")
+
+
+def forwards(con, first, md):
+    """A forward = the compute-stream kernels from one FIRST_KERNEL launch to the next (decode and
+    copy kernels, which run on the copy stream under the previous forward, are left out).  span =
+    first start -> last end; busy = summed kernel time; gap = span - busy (the compute stream idle
+    inside the forward: launch/enqueue delays, not device work)."""
+    rows = con.execute("select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d "
+                       "join rocpd_info_kernel_symbol s on d.kernel_id = s.id order by d.start").fetchall()
+    fw, cur = [], None
+    for name, b, e in rows:
+        if any(k in name for k in SIDE):
+            continue
+        if first in name:
+            if cur:
+                fw.append(cur)
+            cur = [b, e, 0.0, 0, 0.0]
+        if cur is None:
+            continue
+        cur[1] = max(cur[1], e)
+        cur[2] += (e - b) / 1e3
+        cur[3] += 1
+    if cur:
+        fw.append(cur)
+    n = max((f[3] for f in fw), default=0)
+    fw = [f for f in fw if f[3] == n]  # whole forwards only (autotune launches the first kernel alone)
+    if not fw:
+        return
+    span = sorted((f[1] - f[0]) / 1e3 for f in fw)
+    busy = sorted(f[2] for f in fw)
+    gap = sorted((f[1] - f[0]) / 1e3 - f[2] for f in fw)
+    med = lambda v: v[len(v) // 2]
+    line = ("%d forwards of %d kernels: span us median %.1f mean %.1f; kernel-busy median %.1f mean %.1f; "
+            "idle inside the forward median %.1f mean %.1f p90 %.1f" % (
+                len(fw), n, med(span), sum(span) / len(span), med(busy), sum(busy) / len(busy), med(gap),
+                sum(gap) / len(gap), gap[int(0.9 * (len(gap) - 1))]))
+    print(line)
+    if md:
+        open(md + ".forwards.txt", "w").write(line + "\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--md", default="")
+    ap.add_argument("--forwards", default="", metavar="FIRST_KERNEL",
+                    help="also split the trace into forwards, each starting at a kernel whose name contains "
+                         "FIRST_KERNEL, and report per-forward span, kernel-busy time and idle gaps")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
+    if a.forwards:
+        forwards(con, a.forwards, a.md)
     rows = con.execute("select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d "
                        "join rocpd_info_kernel_symbol s on d.kernel_id = s.id").fetchall()
     st = defaultdict(lambda: [0, 0.0, 1e30, 0.0])
