@@ -125,6 +125,8 @@ def main():
                     help="keep ResNet's expand and next reduce convs as two launches (EngineOptions::fuse_pairs)")
     ap.add_argument("--no-pack-text", action="store_true",
                     help="upload input text as-is instead of 4-bit packed (device decode)")
+    ap.add_argument("--tune-tail", action="store_true",
+                    help="autotune tail split-K candidates too (EngineOptions::tune_tail)")
     ap.add_argument("--no-efficient-batch", action="store_true",
                     help="dispatch everything queued (up to --batch) instead of cutting a batch back to just "
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
@@ -270,7 +272,7 @@ def main():
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
                    "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph,
                    "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute,
-                   "efficient_batch": not args.no_efficient_batch, "efficient_batch_tol": args.efficient_batch_tol}
+                   "efficient_batch": not args.no_efficient_batch, "tune_tail": args.tune_tail, "efficient_batch_tol": args.efficient_batch_tol}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

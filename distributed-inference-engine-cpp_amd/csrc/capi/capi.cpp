@@ -103,6 +103,7 @@ EngineOptions engine_opts(const Json& j) {
   e.ln_stats_epilogue = jget<bool>(j, "ln_stats_epilogue", e.ln_stats_epilogue);
   e.tune_in_graph = jget<bool>(j, "tune_in_graph", e.tune_in_graph);
   e.tune_orders = jget<bool>(j, "tune_orders", e.tune_orders);
+  e.tune_tail = jget<bool>(j, "tune_tail", e.tune_tail);
   e.efficient_batch = jget<bool>(j, "efficient_batch", e.efficient_batch);
   e.efficient_batch_tol = jget<double>(j, "efficient_batch_tol", e.efficient_batch_tol);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);

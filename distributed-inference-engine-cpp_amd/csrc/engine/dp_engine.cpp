@@ -73,7 +73,7 @@ std::string plan_signature(const std::string& path, const EngineOptions& o, int 
   std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(file_hash(path)));
   return std::string(h) + "|" + (o.device == "cpu" ? "cpu" : "hip") + "|" + o.precision + "|b" +
          std::to_string(local_max) + "|" + o.dp_backend + "|dec" + std::to_string(o.device_decode) + "|pk" +
-         std::to_string(o.pack_text) + "|br" + std::to_string(o.branch_streams) + "|bn" + std::to_string(o.bn_on_load) + "|fp" + std::to_string(o.fuse_pairs) + "|sp" + std::to_string(o.fuse_stem_pool) + "|gf" + std::to_string(o.fuse_gap_fc) + "|fl" + std::to_string(o.fold_layernorm) + "|le" + std::to_string(o.ln_stats_epilogue) + "|tg" + std::to_string(o.tune_in_graph) + "|to" + std::to_string(o.tune_orders);
+         std::to_string(o.pack_text) + "|br" + std::to_string(o.branch_streams) + "|bn" + std::to_string(o.bn_on_load) + "|fp" + std::to_string(o.fuse_pairs) + "|sp" + std::to_string(o.fuse_stem_pool) + "|gf" + std::to_string(o.fuse_gap_fc) + "|fl" + std::to_string(o.fold_layernorm) + "|le" + std::to_string(o.ln_stats_epilogue) + "|tg" + std::to_string(o.tune_in_graph) + "|to" + std::to_string(o.tune_orders) + "|tt" + std::to_string(o.tune_tail);
 }
 
 size_t model_input_numel(const std::string& path) {

@@ -296,6 +296,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["ln_stats_epilogue"] = o.ln_stats_epilogue;
   j["tune_in_graph"] = o.tune_in_graph;
   j["tune_orders"] = o.tune_orders;
+  j["tune_tail"] = o.tune_tail;
   j["efficient_batch"] = o.efficient_batch;
   j["efficient_batch_tol"] = o.efficient_batch_tol;
   j["tune_cold"] = o.tune_cold;

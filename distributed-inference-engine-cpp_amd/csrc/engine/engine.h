@@ -258,6 +258,11 @@ struct EngineOptions {
   // autotune the XCD tile order too: the 2- and 4-panel orders (ConvArgs::order 3 / 4) next to the
   // heuristic, for convs that replicate their weights on every XCD (profiles/r5_xcd_panels.md)
   bool tune_orders = true;
+  // autotune tail split-K too (ConvArgs::tail): whole tiles for the full 256-tile rounds, fused
+  // split-K slices for the tiles of the last partial round only.  Off by default: behind the cold-L2
+  // isolated timing it won 3 of ~1,200 ResNet/ViT shapes and left the per-batch-size forward time
+  // unchanged (profiles/r5_batch_curve.md)
+  bool tune_tail = false;
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Split-K reductions run in-kernel (the last-arriving split block of a tile sums the partials and

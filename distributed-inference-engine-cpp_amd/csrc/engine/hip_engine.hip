@@ -720,7 +720,7 @@ class HipEngine : public Engine {
     j["efficient_batch"] = !batch_ms_.empty();
     if (!batch_ms_.empty()) {
       Json c = Json::array();  // device ms of the captured forward at batch 1, 2, ..., max_batch
-      for (size_t b = 1; b < batch_ms_.size(); ++b) c.push_back(std::round(batch_ms_[b] * 1e4) / 1e4);
+      for (size_t b = 1; b < batch_ms_.size(); ++b) c.push_back(batch_ms_[b]);
       j["batch_curve_ms"] = c;
     }
     j["pipeline_depth"] = depth_;
@@ -759,7 +759,7 @@ class HipEngine : public Engine {
         if (plan_.ops[oi].kind == PlanOp::CONV) {
           const Tune& x = tune_.back()[oi];
           t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits) + (x.fused ? "f" : "") +
-                      (x.order == 2 ? "m" : x.order == 1 ? "n" : ""));
+                      (x.order == 2 ? "m" : x.order == 1 ? "n" : "") + (x.tail ? "t" : ""));
         }
       j["tile_split_at_max_batch"] = t;
     }
@@ -771,6 +771,7 @@ class HipEngine : public Engine {
     int splits = 1;
     bool fused = false;  // split-K reduced in-kernel by the last split block (else a second kernel)
     int order = 0;       // ConvArgs::order (0 heuristic, 1 N-fastest, 2 M-fastest)
+    int tail = 0;        // ConvArgs::tail (> 0: split-K on the last partial round's tiles only)
   };
 
   // ---- autotune persistence (kernel configs cached in a tuning file) ----
@@ -796,7 +797,8 @@ class HipEngine : public Engine {
         const auto& a = kv.second.as_array();
         if (a.size() < 4) continue;
         out[kv.first] = {Tune{static_cast<int>(a[0].as_int()), static_cast<int>(a[1].as_int()), a[2].as_bool(),
-                              a.size() > 4 ? static_cast<int>(a[4].as_int()) : 0},
+                              a.size() > 4 ? static_cast<int>(a[4].as_int()) : 0,
+                              a.size() > 5 ? static_cast<int>(a[5].as_int()) : 0},
                          a[3].as_double()};
       }
     } catch (const std::exception&) {
@@ -824,6 +826,7 @@ class HipEngine : public Engine {
         a.push_back(kv.second.first.fused);
         a.push_back(kv.second.second);
         a.push_back(kv.second.first.order);
+        a.push_back(kv.second.first.tail);
         arch[kv.first] = a;
       }
       root[arch_] = arch;
@@ -942,7 +945,8 @@ class HipEngine : public Engine {
   // Tune-cache / memo key of a conv problem: the shape, its epilogue, and the tuning regime.
   std::string shape_key(const kern::ConvArgs& base, bool warm_input) const {
     char key[256];
-    std::snprintf(key, sizeof(key), "o%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_cold ? "c:" : "",
+    std::snprintf(key, sizeof(key), "o%s%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_tail ? "t:" : "",
+                  opt_.tune_cold ? "c:" : "",
                   warm_input ? "w:" : "", sp_ ? "f32:" : "", base.stats_out || base.row_parts ? "ls:" : "",
                   opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : (opt_.tune_orders ? "" : "o0:"),
                   base.M, base.N, base.K, base.Cin, base.H, base.W, base.KH, base.KW, base.stride, base.pad_h, base.relu,
@@ -1014,7 +1018,21 @@ class HipEngine : public Engine {
             // weights (a panel order reads every activation row once per panel: ViT's MLP2, 8x,
             // won in isolation and lost 16 % in the graph) -- the 2- and 4-panel orders, whose
             // XCDs each read one panel of the weights (profiles/r5_xcd_panels.md)
-            for (int order : {0, 3, 4}) {
+            for (int order : {0, 3, 4})
+            // Tail split-K (ConvArgs::tail = 256, one tile per CU per round): next to each fused
+            // split-K candidate of an LDS-DMA config, heuristic order, when the tile grid spills a
+            // few tiles (at most 160) past a whole number of 256-tile rounds -- the steps of the
+            // per-batch-size forward time (profiles/r5_batch_curve.md)
+            for (int tail : {0, 256}) {
+              if (tail > 0) {
+                int bm, bn;
+                kern::tile_dims(tile, bm, bn);
+                const int T = ((base.M + bm - 1) / bm) * ((base.N + bn - 1) / bn);
+                const int v = tile / kern::NUM_TILES;
+                if (!opt_.tune_tail || !fused || order != 0 || v == 0 || v >= 6 || T <= tail || T % tail == 0 ||
+                    T % tail > 160)
+                  continue;
+              }
               if (order > 0 && !opt_.tune_orders) continue;
               if (order > 0) {
                 int bm, bn;
@@ -1028,6 +1046,7 @@ class HipEngine : public Engine {
               kern::ConvArgs a = base;
               a.splits = sp;
               a.order = order;
+              a.tail = tail;
               if (!fused) a.counters = nullptr;
               if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;  // warm-up / validity
               float ms = 0;
@@ -1056,14 +1075,14 @@ class HipEngine : public Engine {
                 HIP_CHECK(hipEventSynchronize(e1));
                 HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
               }
-              measured.push_back({ms, Tune{tile, sp, fused != 0, order}});
+              measured.push_back({ms, Tune{tile, sp, fused != 0, order, tail}});
               if (ms < best) {
                 best = ms;
-                bt = Tune{tile, sp, fused != 0, order};
+                bt = Tune{tile, sp, fused != 0, order, tail};
               }
               if (fused && ms < best_fused) {
                 best_fused = ms;
-                bt_fused = Tune{tile, sp, true, order};
+                bt_fused = Tune{tile, sp, true, order, tail};
               }
             }
           }
@@ -1244,6 +1263,7 @@ class HipEngine : public Engine {
           if (!use_live_) a.live = nullptr;
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
+          a.tail = t.tail;
           a.order = opt_.conv_order > 0 ? opt_.conv_order : t.order;
           a.ws = side ? ws_side_ : wss_[s % n_exec_];
           if (side) a.counters = counters_side_;
@@ -1471,6 +1491,7 @@ class HipEngine : public Engine {
         o["splits"] = t.splits;
         o["fused_splitk"] = t.fused;
         o["tile_order"] = t.order;
+        o["tail_splitk"] = t.tail > 0;
       }
       total += us[i];
       ops.push_back(o);

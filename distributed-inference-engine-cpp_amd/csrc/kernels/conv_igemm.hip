@@ -78,8 +78,11 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (a.stats_out && a.N % 64 != 0) return hipErrorInvalidValue;
   if (a.row_parts && (a.row_stats || !a.split || a.N % 8 != 0 || a.K % 64 != 0)) return hipErrorInvalidValue;
   if (a.splits > 1 && (a.N % 8 != 0 || !a.ws)) return hipErrorInvalidValue;
+  // tail split-K: the LDS-DMA loops (variants 1-5) with the in-kernel reduction only
+  if (a.tail < 0 || (a.tail > 0 && (a.splits < 2 || !a.counters))) return hipErrorInvalidValue;
   if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
   const int variant = cfg / NUM_TILES;
+  if (a.tail > 0 && (variant == 0 || variant >= 6)) return hipErrorInvalidValue;
   if (variant == 7) return igemm::launch_tile_wide(a, s, cfg % NUM_TILES);
   switch (cfg % NUM_TILES) {
     case TILE_128x128: return igemm::launch_tile_128x128(a, s, variant);

@@ -193,20 +193,25 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
 // smaller operand, M-fastest otherwise (stage-4 3x3 / expand / FC shapes).
 // With a live batch (ConvArgs::live) only the tiles holding real samples get work: the first
 // live_tiles * S blocks (spread evenly over the XCDs) are remapped over them and the rest exit.
+// Tail split-K (ConvArgs::tail): the first Tw = T - T % tail tiles are whole (split = -1: the full
+// K range, direct epilogue) and the T - Tw tiles of the last partial round get S slices each.
 // Returns false for a block without work.
 __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
                                              int& tile) {
-  const int S = gridDim.y;  // split-K slices
+  const int S = p.tail > 0 ? p.splits : static_cast<int>(gridDim.y);  // split-K slices
   const int ntn = (p.N + BN - 1) / BN;
   const int Ml = p.live ? min(p.M, static_cast<int>(*p.live) * p.Ho * p.Wo) : p.M;
   const int ntm = (Ml + BM - 1) / BM;
-  const int nwg = min(static_cast<int>(gridDim.x * gridDim.y), ntm * ntn * S);
+  const int T = ntm * ntn;
+  const int Tw = p.tail > 0 ? (T > p.tail ? T - T % p.tail : T) : 0;  // whole tiles (tail split-K)
+  const int nwg = min(static_cast<int>(gridDim.x * gridDim.y), Tw + (T - Tw) * S);
   const int b = blockIdx.x + blockIdx.y * gridDim.x;
   if (b >= nwg) return false;
   const int q = nwg >> 3, r = nwg & 7, x = b & 7;
   const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-  tile = id / S;
-  split = id - tile * S;
+  const int sid = id - Tw, st = sid / S;
+  tile = id < Tw ? id : Tw + st;
+  split = id < Tw ? -1 : sid - st * S;
   // Replicate (read on every XCD) the operand with fewer bytes: the weights are N x K, the
   // activations the INPUT tensor, B*H*W*Cin -- not the im2col M x K, which counts a 3x3 conv's
   // input 9 times (stage-4 3x3 at batch 16-32: weights 4.7x the input, so M-fastest).
@@ -436,7 +441,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
       }
     __syncthreads();
     constexpr int GPR = BN / 8;
-    const bool partial = p.splits > 1;
+    const bool partial = p.splits > 1 && split >= 0;  // (split < 0: a tail split-K launch's whole tile)
     const bool fused = partial && p.counters;
     float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
     const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
@@ -643,8 +648,9 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BKS;
-  const int kt_begin = split * kt_per_split * KR;  // kt_per_split counts 64-wide K-steps
-  const int kt_end = min(nk_total, kt_begin + kt_per_split * KR);
+  // kt_per_split counts 64-wide K-steps; split < 0: a whole tile of a tail split-K launch
+  const int kt_begin = split < 0 ? 0 : split * kt_per_split * KR;
+  const int kt_end = split < 0 ? nk_total : min(nk_total, kt_begin + kt_per_split * KR);
   const int nk = kt_end - kt_begin;
   // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
   float* bnl = reinterpret_cast<float*>(lds + LDS_ELEMS);  // BNL only: [scale | shift] x kBnlMaxK
@@ -1082,6 +1088,18 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   // LayerNorm statistics (ConvArgs::stats_out / row_parts): rows GEMMs, not the spatially tiled 3x3
   if ((a.stats_out || a.row_parts) && variant == 6) return hipErrorInvalidValue;
   dim3 grid(tiles, eff);
+  if (a.tail > 0) {
+    // tail split-K: 1-D grid sized for the worst live batch (the whole-tile count steps down at
+    // every multiple of `tail`, so fewer live tiles can need more blocks)
+    if (!fused || variant == 0 || variant >= 6) return hipErrorInvalidValue;
+    const int ntn = (a.N + BN - 1) / BN, ntm = (a.M + BM - 1) / BM;
+    int g = 0;
+    for (int m = 1; m <= ntm; ++m) {
+      const int T = m * ntn, Tw = T > a.tail ? T - T % a.tail : T;
+      g = std::max(g, Tw + (T - Tw) * eff);
+    }
+    grid = dim3(g, 1);
+  }
   if (a.in_scale) {  // pre-activation on load: 1x1 convs in the LDS-DMA loop only
     if (a.KH != 1 || a.KW != 1 || a.pad_h || a.pad_w || a.K != a.Cin || a.K > kBnlMaxK || a.Cin % BK || !a.in_shift)
       return hipErrorInvalidValue;

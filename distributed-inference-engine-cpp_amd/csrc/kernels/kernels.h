@@ -85,6 +85,12 @@ struct ConvArgs {
   // operand DMA (MFMAs on whatever the LDS holds), 2 = no MFMAs (DMA + waits + barriers only).  The
   // outputs are garbage; the engine never sets it.
   int probe = 0;
+  // Tail split-K (LDS-DMA loops, fused split-K only): with T output tiles, the first T - T % tail
+  // tiles run whole (no split-K, direct epilogue) and only the last partial round's tiles are cut
+  // into `splits` K-slices, reduced in-kernel.  A grid of 257-300 tiles then costs one round plus
+  // a sliver instead of two rounds on the busiest CUs (tail = 256: one tile per CU per round).  0 =
+  // uniform split-K.
+  int tail = 0;
 };
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--out", default="")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="EngineOptions::fuse_pairs off")
+    ap.add_argument("--tune-tail", action="store_true", help="EngineOptions::tune_tail on")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (one HIP runtime)
@@ -39,7 +40,7 @@ def main():
     path = os.path.join(tempfile.mkdtemp(), a.arch + ".onnx")
     open(path, "wb").write(m.build_onnx(cfg)[0])
     e = native.Engine(path, device="hip", max_batch=a.hi, precision=a.precision,
-                      fuse_pairs=not a.no_fuse_pairs)
+                      fuse_pairs=not a.no_fuse_pairs, tune_tail=a.tune_tail)
     x = m.synthetic_input(a.hi, cfg, seed=3).reshape(a.hi, -1).astype(np.float32)
     rows = []
     for B in range(a.lo, a.hi + 1):
@@ -56,7 +57,7 @@ def main():
     buckets = e.refresh_info().get("buckets")
     e.close()
     lines = ["# %s %s%s: captured-forward device time per batch size" % (
-        a.arch, a.precision, ", unfused pairs" if a.no_fuse_pairs else ""), "",
+        a.arch, a.precision, (", unfused pairs" if a.no_fuse_pairs else "") + (", tail split-K tuned" if a.tune_tail else "")), "",
              "Graph buckets: %s." % buckets, "", "| batch | device ms | us / image |", "|---:|---:|---:|"]
     lines += ["| %d | %.3f | %.1f |" % (r["batch"], r["device_ms"], r["us_per_image"]) for r in rows]
     text = "\n".join(lines) + "\n"

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--no-fold-layernorm", action="store_true", help="standalone LayerNorms (EngineOptions::fold_layernorm)")
     ap.add_argument("--tune-in-graph", action="store_true", help="EngineOptions::tune_in_graph")
     ap.add_argument("--no-tune-orders", action="store_true", help="heuristic XCD tile order only (EngineOptions::tune_orders)")
+    ap.add_argument("--tune-tail", action="store_true", help="tail split-K candidates too (EngineOptions::tune_tail)")
     ap.add_argument("--conv-order", type=int, default=0, help="EngineOptions::conv_order (XCD tile order override)")
     ap.add_argument("--no-ln-stats-epilogue", action="store_true",
                     help="LayerNorm statistics launches instead of producer-epilogue partials (EngineOptions::ln_stats_epilogue)")
@@ -53,7 +54,7 @@ def main():
                       splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
                       fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm,
                       ln_stats_epilogue=not a.no_ln_stats_epilogue, tune_in_graph=a.tune_in_graph, conv_order=a.conv_order,
-                      tune_orders=not a.no_tune_orders)
+                      tune_orders=not a.no_tune_orders, tune_tail=a.tune_tail)
     p = e.profile(a.batch, a.iters)
     info = e.refresh_info()
     e.close()
@@ -64,7 +65,7 @@ def main():
                  "on" if a.tune_in_graph else "off", info.get("tune_in_graph_timed"), info.get("tune_in_graph_changed")), "",
              "| # | op | kind | us | GFLOP | TFLOP/s | tile/splits |", "|---:|---|---|---:|---:|---:|---|"]
     for i, o in enumerate(p["ops"]):
-        ts = ("%d/%d" % (o["tile"], o["splits"]) + ("f" if o.get("fused_splitk") else "")) if "tile" in o else ""
+        ts = ("%d/%d" % (o["tile"], o["splits"]) + ("f" if o.get("fused_splitk") else "") + ("t" if o.get("tail_splitk") else "")) if "tile" in o else ""
         lines.append("| %d | %s | %s | %.1f | %.2f | %.0f | %s |" % (i, o["name"][:48], o["kind"], o["us"], o["gflop"],
                                                                     o["tflops"], ts))
     kinds = {}
