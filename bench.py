@@ -132,6 +132,8 @@ def main():
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
     ap.add_argument("--efficient-batch-tol", type=float, default=0.03,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
+    ap.add_argument("--parse-spin-us", type=int, default=0,
+                    help="idle parse threads poll the queue this long before sleeping (WorkerOptions::parse_spin_us)")
     ap.add_argument("--prep-on-compute", action="store_true",
                     help="measurement: run each batch's decode/prep on the compute stream before its forward "
                          "instead of on the copy stream under the previous forward (EngineOptions::prep_on_compute)")
@@ -286,12 +288,14 @@ def main():
         t_init = time.perf_counter()
         try:
             wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts, port=want_port,
-                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
+                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads,
+                               parse_spin_us=args.parse_spin_us)
         except native.NativeError:
             if not want_port:
                 raise
             wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
-                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads)
+                               parse_threads=args.parse_threads, http_threads=args.worker_http_threads,
+                               parse_spin_us=args.parse_spin_us)
         t_ready = time.perf_counter()
         gw = None
         target_port = wk.port

@@ -138,7 +138,7 @@ int main(int argc, char** argv) {
               << "  --no-pace  --no-pack-text  --branch-streams  --copy-streams N (0 = auto)  --bucket-div N (8)  --coarse-buckets\n"
               << "  --pace-lead-scale X (1)  --splitk-fused-margin X (0)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --fuse-gap-fc  --no-fold-layernorm  --no-ln-stats-epilogue  --tune-in-graph  --no-tune-orders  --tune-tail  --tune-warm  --no-efficient-batch  --efficient-batch-tol X (0.03)  --tune-cache PATH|auto|''\n"
               << "  --dp-backend rccl|host (rccl)  --dp-force-merge  --fail-batch-every N (fault injection, 0 = off)\n"
-              << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --host ADDR (0.0.0.0)\n"
+              << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --parse-spin-us N (0)  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
               << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose\n"
@@ -176,6 +176,7 @@ int main(int argc, char** argv) {
   o.policy = f.b("deadline") ? die::BatchPolicy::DEADLINE : die::BatchPolicy::GREEDY;
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.parse_threads = static_cast<int>(f.i("parse-threads", -1));
+  o.parse_spin_us = static_cast<int>(f.i("parse-spin-us", 0));
   o.engine = engine_options_from_flags(f, "auto");
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);

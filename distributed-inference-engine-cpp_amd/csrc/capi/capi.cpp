@@ -482,6 +482,7 @@ void* die_worker_create(const char* opts_json, char** err) {
     o.policy = jget<std::string>(j, "policy", "greedy") == "deadline" ? BatchPolicy::DEADLINE : BatchPolicy::GREEDY;
     o.http_threads = jget<int>(j, "http_threads", 0);
     o.parse_threads = jget<int>(j, "parse_threads", -1);
+    o.parse_spin_us = jget<int>(j, "parse_spin_us", 0);
     o.engine = engine_opts(j.contains("engine") ? j.at("engine") : Json::object());
     o.fault_fail_rate = jget<double>(j, "fault_fail_rate", 0.0);
     o.fault_latency_ms = jget<int>(j, "fault_latency_ms", 0);

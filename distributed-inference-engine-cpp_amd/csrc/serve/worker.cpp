@@ -128,6 +128,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
       {
         std::lock_guard<std::mutex> g(parse_mu_);
         parse_q_.push_back(std::move(j));
+        parse_pending_.fetch_add(1, std::memory_order_release);
       }
       parse_cv_.notify_one();
     });
@@ -171,12 +172,18 @@ void WorkerNode::stop() {
 void WorkerNode::parse_loop() {
   while (true) {
     ParseJob j;
+    if (opt_.parse_spin_us > 0) {  // WorkerOptions::parse_spin_us: poll before sleeping
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(opt_.parse_spin_us);
+      while (parse_pending_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+        __builtin_ia32_pause();
+    }
     {
       std::unique_lock<std::mutex> lk(parse_mu_);
       parse_cv_.wait(lk, [&] { return parse_stop_ || !parse_q_.empty(); });
       if (parse_q_.empty()) return;  // stopping and drained
       j = std::move(parse_q_.front());
       parse_q_.pop_front();
+      parse_pending_.fetch_sub(1, std::memory_order_relaxed);
     }
     try {
       handle_infer(*j.req, j.res);

@@ -52,6 +52,9 @@ struct WorkerOptions {
   // instead of the connection's reactor, so a reactor busy parsing a 1 MB body never holds a
   // finished response back.  0 = parse on the reactor; -1 = auto (a quarter of the CPUs, >= 2).
   int parse_threads = -1;
+  // An idle parse thread polls the queue this long before it sleeps on the condition variable: a
+  // request that arrives meanwhile is taken without a futex wake-up (0 = sleep at once).
+  int parse_spin_us = 0;
 };
 
 class WorkerNode {
@@ -124,6 +127,7 @@ class WorkerNode {
   std::mutex parse_mu_;
   std::condition_variable parse_cv_;
   std::deque<ParseJob> parse_q_;
+  std::atomic<int> parse_pending_{0};  // parse_q_.size(), readable without the lock (parse_spin_us)
   bool parse_stop_ = false;
   std::vector<std::thread> parse_threads_;
 };
