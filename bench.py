@@ -44,6 +44,14 @@ import die_amd  # noqa: E402,F401  (first: sets the HIP runtime environment befo
 BASELINE_RPS = 522.64  # BASELINE.md / README.md:282
 
 
+def _hist_window(h0, h1):
+    """Per-size batch counts over the timed window (lifetime histograms h1 - h0, zero-padded)."""
+    n = max(len(h0), len(h1))
+    h0 = list(h0) + [0] * (n - len(h0))
+    h1 = list(h1) + [0] * (n - len(h1))
+    return [b - a for a, b in zip(h0, h1)]
+
+
 def _cpu_quota():
     try:
         q, p = open("/sys/fs/cgroup/cpu.max").read().split()
@@ -132,6 +140,9 @@ def main():
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
     ap.add_argument("--efficient-batch-tol", type=float, default=0.03,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
+    ap.add_argument("--no-batch-balance", action="store_true",
+                    help="dispatch everything queued instead of the mean of the queue and the previous batch "
+                         "(WorkerOptions::batch_balance)")
     ap.add_argument("--parse-spin-us", type=int, default=0,
                     help="idle parse threads poll the queue this long before sleeping (WorkerOptions::parse_spin_us)")
     ap.add_argument("--prep-on-compute", action="store_true",
@@ -289,13 +300,13 @@ def main():
         try:
             wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts, port=want_port,
                                parse_threads=args.parse_threads, http_threads=args.worker_http_threads,
-                               parse_spin_us=args.parse_spin_us)
+                               parse_spin_us=args.parse_spin_us, batch_balance=not args.no_batch_balance)
         except native.NativeError:
             if not want_port:
                 raise
             wk = native.Worker(model, node_id="gpu%d" % local_rank, max_batch=B, engine=engine_opts,
                                parse_threads=args.parse_threads, http_threads=args.worker_http_threads,
-                               parse_spin_us=args.parse_spin_us)
+                               parse_spin_us=args.parse_spin_us, batch_balance=not args.no_batch_balance)
         t_ready = time.perf_counter()
         gw = None
         target_port = wk.port
@@ -355,6 +366,8 @@ def main():
             # EngineOptions::efficient_batch: batches cut below the queue to stay under a per-image step
             "trimmed_batches": bp1.get("trimmed_batches", 0) - bp0.get("trimmed_batches", 0),
             "trimmed_requests": bp1.get("trimmed_requests", 0) - bp0.get("trimmed_requests", 0),
+            # batches per size over the timed pass: [count at size 1, size 2, ...]
+            "batch_size_histogram": _hist_window(bp0.get("size_histogram", []), bp1.get("size_histogram", [])),
             "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
             "precision": e1.get("precision"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),

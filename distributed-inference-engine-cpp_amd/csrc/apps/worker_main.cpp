@@ -110,7 +110,7 @@ int follower_main(die::Flags& f, sigset_t& sigs) {
 const std::vector<std::string> kBoolFlags = {"verbose", "deadline", "no-graphs", "no-device-decode", "dp-follower",
                                              "no-shm", "reuse-port", "dp-no-ingest", "no-pace", "no-pack-text",
                                              "branch-streams", "coarse-buckets", "bn-on-load", "no-fuse-pairs", "no-fuse-stem-pool", "fuse-gap-fc", "no-fold-layernorm", "no-ln-stats-epilogue", "tune-in-graph", "no-tune-orders", "tune-tail", "tune-warm",
-                                             "no-efficient-batch",
+                                             "no-efficient-batch", "no-batch-balance",
                                              "dp-force-merge"};
 
 }  // namespace
@@ -138,7 +138,7 @@ int main(int argc, char** argv) {
               << "  --no-pace  --no-pack-text  --branch-streams  --copy-streams N (0 = auto)  --bucket-div N (8)  --coarse-buckets\n"
               << "  --pace-lead-scale X (1)  --splitk-fused-margin X (0)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --fuse-gap-fc  --no-fold-layernorm  --no-ln-stats-epilogue  --tune-in-graph  --no-tune-orders  --tune-tail  --tune-warm  --no-efficient-batch  --efficient-batch-tol X (0.03)  --tune-cache PATH|auto|''\n"
               << "  --dp-backend rccl|host (rccl)  --dp-force-merge  --fail-batch-every N (fault injection, 0 = off)\n"
-              << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --parse-spin-us N (0)  --host ADDR (0.0.0.0)\n"
+              << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --parse-spin-us N (0)  --no-batch-balance  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"
               << "      every rank serves HTTP on <port> (SO_REUSEPORT) unless --dp-no-ingest\n"
               << "  --fault-fail-rate P  --fault-latency-ms N  --verbose\n"
@@ -177,6 +177,7 @@ int main(int argc, char** argv) {
   o.http_threads = static_cast<int>(f.i("http-threads", 0));
   o.parse_threads = static_cast<int>(f.i("parse-threads", -1));
   o.parse_spin_us = static_cast<int>(f.i("parse-spin-us", 0));
+  o.batch_balance = !f.b("no-batch-balance");
   o.engine = engine_options_from_flags(f, "auto");
   o.engine.shard_id = o.port % 3;  // reference: InferenceEngine(model_path, port % 3) (unused there too)
   o.fault_fail_rate = f.f("fault-fail-rate", 0.0);

@@ -279,6 +279,10 @@ char* die_batcher_metrics(void* p) {
   j["avg_batch_size"] = m.avg_batch_size;
   j["trimmed_batches"] = t->bp->trimmed_batches();
   j["trimmed_requests"] = t->bp->trimmed_requests();
+  Json hist = Json::array();
+  const auto sh = t->bp->size_histogram();
+  for (size_t i = 1; i < sh.size(); ++i) hist.push_back(sh[i]);
+  j["size_histogram"] = hist;
   Json s = Json::array();
   {
     std::lock_guard<std::mutex> g(t->mu);
@@ -483,6 +487,7 @@ void* die_worker_create(const char* opts_json, char** err) {
     o.http_threads = jget<int>(j, "http_threads", 0);
     o.parse_threads = jget<int>(j, "parse_threads", -1);
     o.parse_spin_us = jget<int>(j, "parse_spin_us", 0);
+    o.batch_balance = jget<bool>(j, "batch_balance", true);
     o.engine = engine_opts(j.contains("engine") ? j.at("engine") : Json::object());
     o.fault_fail_rate = jget<double>(j, "fault_fail_rate", 0.0);
     o.fault_latency_ms = jget<int>(j, "fault_latency_ms", 0);

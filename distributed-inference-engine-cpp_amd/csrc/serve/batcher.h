@@ -155,6 +155,17 @@ class BatchProcessor {
 
   // Set before start().
   void set_size_fn(SizeFn fn) { size_ = std::move(fn); }
+  // Balanced batches (GREEDY): when more requests are queued than the previous batch carried, take
+  // the mean of the two (rounded up), leaving the rest to lead the next batch.  In a closed loop the
+  // queue at each dispatch is what the previous batch left outstanding, so consecutive batches
+  // otherwise alternate large / small (sizes 26, 12, 26, ... with 50 clients), and a small batch
+  // costs far more per image than the large one saves (profiles/r5_batch_curve.md).
+  void set_balance(bool on) { balance_ = on; }
+  // Batches dispatched per size (index = batch size, 0 unused).
+  std::vector<long long> size_histogram() const {
+    std::lock_guard<std::mutex> g(metrics_mu_);
+    return size_hist_;
+  }
   // Batches the size function cut below the queue (and the requests it left queued).
   long long trimmed_batches() const { return trimmed_batches_.load(); }
   long long trimmed_requests() const { return trimmed_requests_.load(); }
@@ -208,7 +219,8 @@ class BatchProcessor {
         if (!running_) return;
         const size_t q = std::min(queue_.size(), max_batch_);
         size_t take = q;
-        if (size_ && q > 1) take = std::max<size_t>(1, std::min(q, size_(q)));
+        if (balance_ && policy_ == BatchPolicy::GREEDY && last_n_ > 0 && q > last_n_) take = (q + last_n_ + 1) / 2;
+        if (size_ && take > 1) take = std::max<size_t>(1, std::min(take, size_(take)));
         if (take < q) {
           trimmed_batches_.fetch_add(1, std::memory_order_relaxed);
           trimmed_requests_.fetch_add(static_cast<long long>(q - take), std::memory_order_relaxed);
@@ -219,6 +231,7 @@ class BatchProcessor {
         }
       }
       if (batch.empty()) continue;
+      last_n_ = batch.size();
       dispatch(std::move(batch));
     }
   }
@@ -231,6 +244,8 @@ class BatchProcessor {
       batched_requests_ += static_cast<int64_t>(n);
       if (n >= max_batch_) ++full_batches_;
       else ++timeout_batches_;
+      if (size_hist_.size() <= n) size_hist_.resize(n + 1, 0);
+      ++size_hist_[n];
     }
     std::vector<Request> reqs;
     reqs.reserve(n);
@@ -265,6 +280,8 @@ class BatchProcessor {
   ReadyFn ready_;
   PaceFn pace_;
   SizeFn size_;
+  bool balance_ = false;
+  size_t last_n_ = 0;  // size of the previous batch (batcher thread only)
   std::atomic<long long> paced_ns_{0};
   std::atomic<long long> trimmed_batches_{0}, trimmed_requests_{0};
   mutable std::mutex mu_;
@@ -276,6 +293,7 @@ class BatchProcessor {
   std::atomic<int64_t> total_requests_{0};
   mutable std::mutex metrics_mu_;
   int64_t total_batches_ = 0, timeout_batches_ = 0, full_batches_ = 0, batched_requests_ = 0;
+  std::vector<long long> size_hist_;  // guarded by metrics_mu_
 };
 
 }  // namespace die

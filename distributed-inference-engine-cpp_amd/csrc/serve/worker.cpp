@@ -112,6 +112,7 @@ WorkerNode::WorkerNode(WorkerOptions opt, std::unique_ptr<Engine> engine)
   batcher_ = std::make_unique<BatchProcessor<Pending, Result>>(
       static_cast<size_t>(std::max(1, std::min(opt_.max_batch, engine_->max_batch()))), opt_.batch_timeout, batch_fn,
       [eng] { eng->wait_for_slot(); }, opt_.policy, [eng] { return eng->dispatch_not_before(); });
+  batcher_->set_balance(opt_.batch_balance);
   if (opt_.policy == BatchPolicy::GREEDY)
     batcher_->set_size_fn([eng](size_t q) { return static_cast<size_t>(eng->preferred_batch(static_cast<int>(q))); });
   batcher_->start();
@@ -506,6 +507,12 @@ Json WorkerNode::getHealth() const {
   b["queue_depth"] = static_cast<long long>(batcher_->queue_depth());
   b["trimmed_batches"] = batcher_->trimmed_batches();    // batches cut below the queue (preferred_batch)
   b["trimmed_requests"] = batcher_->trimmed_requests();  // requests those cuts left for the next batch
+  {
+    Json hist = Json::array();  // batches per size: [count at size 1, count at size 2, ...]
+    const auto sh = batcher_->size_histogram();
+    for (size_t i = 1; i < sh.size(); ++i) hist.push_back(sh[i]);
+    b["size_histogram"] = hist;
+  }
   h["batch_processor"] = b;
   // extras (superset of the reference keys)
   h["errors"] = static_cast<long long>(errors_.load());

@@ -38,6 +38,9 @@ struct WorkerOptions {
   int max_batch = 32;                                    // :35
   std::chrono::milliseconds batch_timeout{20};           // :36
   BatchPolicy policy = BatchPolicy::GREEDY;
+  // GREEDY: when the queue holds more than the previous batch carried, dispatch the mean of the two
+  // (BatchProcessor::set_balance) instead of everything -- evens out closed-loop batch sizes
+  bool batch_balance = true;
   int http_threads = 0;
   EngineOptions engine;
   // fault injection (tests / fault drills)

@@ -224,6 +224,9 @@ def test_batcher_greedy_semantics(native):
     assert m["full_batches"] + m["timeout_batches"] == m["total_batches"]
     assert m["full_batches"] == sum(1 for s in m["sizes"] if s == 4)
     assert abs(m["avg_batch_size"] - 20 / m["total_batches"]) < 1e-9
+    h = m["size_histogram"]  # batches per size, index 0 = size 1
+    assert sum(h) == m["total_batches"] and sum((i + 1) * c for i, c in enumerate(h)) == 20
+    assert all(h[s - 1] == m["sizes"].count(s) for s in set(m["sizes"]))
     b.stop()
 
 
