@@ -138,7 +138,7 @@ def main():
     ap.add_argument("--no-efficient-batch", action="store_true",
                     help="dispatch everything queued (up to --batch) instead of cutting a batch back to just "
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
-    ap.add_argument("--efficient-batch-tol", type=float, default=0.03,
+    ap.add_argument("--efficient-batch-tol", type=float, default=0.0,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
     ap.add_argument("--no-batch-balance", action="store_true",
                     help="dispatch everything queued instead of the mean of the queue and the previous batch "

@@ -69,7 +69,7 @@ die::EngineOptions engine_options_from_flags(const die::Flags& f, const std::str
   eo.tune_tail = f.b("tune-tail");
   eo.tune_cold = !f.b("tune-warm");
   eo.efficient_batch = !f.b("no-efficient-batch");
-  eo.efficient_batch_tol = f.f("efficient-batch-tol", 0.03);
+  eo.efficient_batch_tol = f.f("efficient-batch-tol", 0.0);
   eo.dp_backend = f.str("dp-backend", "rccl");
   eo.dp_force_merge = f.b("dp-force-merge");
   eo.fail_batch_every = static_cast<int>(f.i("fail-batch-every", 0));
@@ -136,7 +136,7 @@ int main(int argc, char** argv) {
               << "  --device auto|hip|cpu (auto)  --device-id N (0)  --precision fp32|bf16 (fp32)\n"
               << "  --pipeline-depth N (3)  --no-graphs  --no-device-decode  --stage-slots N (0 = off, -1 = auto)  --exec-streams N (1)\n"
               << "  --no-pace  --no-pack-text  --branch-streams  --copy-streams N (0 = auto)  --bucket-div N (8)  --coarse-buckets\n"
-              << "  --pace-lead-scale X (1)  --splitk-fused-margin X (0)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --fuse-gap-fc  --no-fold-layernorm  --no-ln-stats-epilogue  --tune-in-graph  --no-tune-orders  --tune-tail  --tune-warm  --no-efficient-batch  --efficient-batch-tol X (0.03)  --tune-cache PATH|auto|''\n"
+              << "  --pace-lead-scale X (1)  --splitk-fused-margin X (0)  --completion-poll-us N (0)  --bn-on-load  --no-fuse-pairs  --no-fuse-stem-pool  --fuse-gap-fc  --no-fold-layernorm  --no-ln-stats-epilogue  --tune-in-graph  --no-tune-orders  --tune-tail  --tune-warm  --no-efficient-batch  --efficient-batch-tol X (0)  --tune-cache PATH|auto|''\n"
               << "  --dp-backend rccl|host (rccl)  --dp-force-merge  --fail-batch-every N (fault injection, 0 = off)\n"
               << "  --http-threads N  --parse-threads N (-1 = auto, 0 = parse on the I/O threads)  --parse-spin-us N (0)  --no-batch-balance  --host ADDR (0.0.0.0)\n"
               << "  --devices 0,1,..  data parallel over these GPUs (one process each; --max-batch = whole batch);\n"

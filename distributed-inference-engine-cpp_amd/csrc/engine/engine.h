@@ -275,9 +275,11 @@ struct EngineOptions {
   // Efficient batch sizes (HIP, graphs): time the captured forward of every batch size once at
   // start-up; with Q requests queued, dispatch the largest B <= Q whose per-image device time is
   // within efficient_batch_tol of the best B' <= Q (ResNet50 fp32: B = 21 costs 19 % more than
-  // B = 20 for 5 % more images, profiles/r5_batch_curve.md).  0 tolerance = always the best.
+  // B = 20 for 5 % more images, profiles/r5_batch_curve.md).  0 = the best itself: a bucket's
+  // forward costs about the same at every live size, so that is a bucket's full size (20, 24, ...);
+  // measured +2.9 % over 0.03, which let a batch of 25 run bucket 26's graph.
   bool efficient_batch = true;
-  double efficient_batch_tol = 0.03;
+  double efficient_batch_tol = 0.0;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;
