@@ -112,6 +112,9 @@ def main():
                     help="measurement: streaming attention variant (kernels.h set_attention_variant)")
     ap.add_argument("--decode-variant", type=int, default=0,
                     help="measurement: device JSON decode kernels, 0 symbol-level (default), 1 character-level (round 4)")
+    ap.add_argument("--pair-shared-w", type=int, default=-2,
+                    help="measurement: force PairArgs::shared_w for every expand+reduce pair launch (-1 auto, "
+                         "0 separate W1 / W2 LDS buffers, 1 one shared buffer; -2 = the engine's choice)")
     ap.add_argument("--ln-xcd", type=int, default=0,
                     help="measurement: LayerNorm rows read on the XCD that wrote them (1) or in natural order (0, default)")
     ap.add_argument("--no-fold-layernorm", action="store_true",
@@ -194,6 +197,8 @@ def main():
         native.kernels().die_kern_set_decode_variant(int(args.decode_variant))
     if args.device == "hip" and args.attn_variant != 0:
         native.kernels().die_kern_set_attention_variant(int(args.attn_variant))
+    if args.device == "hip" and args.pair_shared_w != -2:
+        native.kernels().die_kern_set_pair_shared_w(int(args.pair_shared_w))
     from die_amd.parallel.launch import HostGroup
 
     hg = HostGroup()  # gloo: host-side barriers and reductions over the ranks

@@ -103,6 +103,7 @@ int die_kern_conv_pair(const char* geom, uint64_t x, uint64_t w1, uint64_t bias1
     a.relu = geti(j, "relu", 1);
     a.relu2 = geti(j, "relu2", 1);
     a.split = geti(j, "split", 0);
+    a.shared_w = geti(j, "shared_w", -1);
     if (auto* v = j.find("wplane1")) a.wplane1 = v->as_int();
     if (auto* v = j.find("wplane2")) a.wplane2 = v->as_int();
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));
@@ -185,6 +186,7 @@ int die_kern_gap_fc(uint64_t x, int B, int HW, int C, int mode, uint64_t w, long
 void die_kern_set_attention_variant(int v) { kern::set_attention_variant(v); }
 void die_kern_set_decode_variant(int v) { kern::set_decode_variant(v); }
 void die_kern_set_layernorm_xcd(int v) { kern::set_layernorm_xcd(v); }
+void die_kern_set_pair_shared_w(int v) { kern::set_pair_shared_w(v); }
 
 int die_kern_attention(uint64_t q, uint64_t k, uint64_t v, uint64_t out, int B, int Sq, int H, int D, int ldq, int ldk,
                        int ldv, int ldo, float scale, uint64_t stream, int split) {

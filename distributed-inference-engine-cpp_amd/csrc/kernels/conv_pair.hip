@@ -36,6 +36,7 @@ namespace {
 
 constexpr int BM = 64;  // pixel rows per block
 constexpr int BK = 64;  // K-step (one LDS row = 128 bytes)
+int g_pair_shared_w = -2;  // set_pair_shared_w (host side, read at launch)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
@@ -61,7 +62,11 @@ __device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& ah, const bf16x8
 
 // K1: expand input channels; N2: reduce output channels.  256 threads = 4 waves in a 2 x 2 grid
 // (wm: 32-pixel half, wn: 32-channel half of a 64-channel expand chunk / N2/2 reduce channels).
-template <int K1, int N2, bool SPLIT>
+// WS (PairArgs::shared_w): the W1 chunk and the W2 slice share one LDS buffer, loaded in turn --
+// W2 slice ci during the epilogue of chunk ci, W1 chunk ci+1 during the next chunk's residual
+// load -- so a block needs less LDS and two blocks fit a CU; the x / a stores then move behind the
+// barrier that publishes the A tile (a counted wait for the W2 slice must not also wait for them).
+template <int K1, int N2, bool SPLIT, bool WS = false>
 __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int KS1 = K1 / BK;                 // K-steps of the expand GEMM
@@ -72,11 +77,12 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
   constexpr int A_EL = NP * PL;                // [NP][64 px][64]
   constexpr int GW2 = NP * (N2 / 8) / 4;      // W2 DMA instructions per wave
   constexpr int NF2 = N2 / 32;                 // reduce fragments (16 channels) per wave
-  __shared__ __attribute__((aligned(16))) uint16_t lds[Y_EL + W1_EL + W2_EL + A_EL];
+  constexpr int W_EL = WS ? (W1_EL > W2_EL ? W1_EL : W2_EL) : W1_EL + W2_EL;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[Y_EL + W_EL + A_EL];
   uint16_t* const Ys = lds;
   uint16_t* const W1s = lds + Y_EL;
-  uint16_t* const W2s = W1s + W1_EL;
-  uint16_t* const As = W2s + W2_EL;
+  uint16_t* const W2s = WS ? W1s : W1s + W1_EL;
+  uint16_t* const As = W1s + W_EL;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -163,12 +169,13 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
   // returns, before B1.  (Empty asm statements with a memory clobber pin the issue order.)
   issue_y();
   issue_w1(0);
-  issue_w2(0);
+  if constexpr (!WS) issue_w2(0);
   for (int ci = 0; ci < NC; ++ci) {
     asm volatile("" ::: "memory");
     load_res(ci);
     asm volatile("" ::: "memory");
-    wait_vmcnt<GW2 + 2 * NP>();
+    // outstanding after the wait: the residual (and, without WS, the W2 slice issued before it)
+    wait_vmcnt<(WS ? 0 : GW2) + 2 * NP>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
@@ -197,6 +204,13 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
           for (int j = 0; j < 2; ++j) mfma3(acc1[i][j], af[0][i], af[NP - 1][i], bf[0][j], bf[NP - 1][j], SPLIT);
       }
 
+    if constexpr (WS) {
+      __syncthreads();  // every wave done with the W1 chunk: the buffer takes the W2 slice
+      issue_w2(ci);
+      asm volatile("" ::: "memory");
+      wait_vmcnt<GW2>();  // the residual (issued before the W2 slice) has landed
+    }
+
     // ---- 2. epilogue: x_{u+1} and the pre-activation tile ----
     const int c0 = ci * BK + cg;  // this lane's 8 logical channels
     const float4 b0 = *reinterpret_cast<const float4*>(p.bias1 + c0);
@@ -208,9 +222,11 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
     const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
     const float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float vv[WS ? 2 : 1][8], uu[WS ? 2 : 1][8];  // WS: x_{u+1} and a of both pixels, stored after the barrier
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      float v[8], r[8];
+      float* const v = vv[WS ? j : 0];
+      float r[8];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         v[t] = acc1[0][j][t];
@@ -226,14 +242,14 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
       // x_{u+1} = v rounded exactly as the expand conv's epilogue rounds it: (acc + bias) + (hi + lo)
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = (v[t] + bb[t]) + r[t];
-      if (p.xout && pv[j]) store8v(p.xout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, v);
-      float u[8];
+      if (!WS && p.xout && pv[j]) store8v(p.xout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, v);
+      float* const u = uu[WS ? j : 0];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         u[t] = v[t] * ss[t] + hh[t];
         if (p.relu2) u[t] = fmaxf(u[t], 0.f);
       }
-      if (p.aout && pv[j]) store8v(p.aout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, u);
+      if (!WS && p.aout && pv[j]) store8v(p.aout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, u);
       const int row = wm * 32 + j * 16 + l16;
       uint4 hi, lo;
       if constexpr (SPLIT) {
@@ -244,8 +260,18 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
       }
       *reinterpret_cast<uint4*>(As + swz(row, cg >> 3)) = hi;
     }
-    __syncthreads();  // A tile visible; every wave done with W1 slice ci (and W2 slice ci landed)
-    if (ci + 1 < NC) issue_w1(ci + 1);
+    if constexpr (WS) {
+      wait_vmcnt<0>();  // the W2 slice has landed (no stores issued since it)
+      __syncthreads();  // A tile and W2 slice visible to every wave
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (p.xout && pv[j]) store8v(p.xout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, vv[WS ? j : 0]);
+        if (p.aout && pv[j]) store8v(p.aout + static_cast<size_t>(pix[j]) * p.N1 + c0, rplane, SPLIT, uu[WS ? j : 0]);
+      }
+    } else {
+      __syncthreads();  // A tile visible; every wave done with W1 slice ci (and W2 slice ci landed)
+      if (ci + 1 < NC) issue_w1(ci + 1);
+    }
 
     // ---- 3. reduce: one K-step ----
 #pragma unroll
@@ -267,7 +293,11 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
         for (int j = 0; j < 2; ++j) mfma3(acc2[i][j], af[0][i], af[NP - 1][i], bf[0][j], bf[NP - 1][j], SPLIT);
     }
     __syncthreads();  // every wave done with W2 slice ci and the A tile
-    if (ci + 1 < NC) issue_w2(ci + 1);
+    if constexpr (WS) {
+      if (ci + 1 < NC) issue_w1(ci + 1);
+    } else {
+      if (ci + 1 < NC) issue_w2(ci + 1);
+    }
   }
 
   // ---- reduce epilogue: + bias2, act, 16-byte stores of 8 consecutive channels ----
@@ -295,16 +325,35 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
   }
 }
 
+// LDS bytes of one block (bf16 elements: Y + W1 chunk + W2 slice + A tile, or Y + shared W + A)
+template <int K1, int N2>
+constexpr int pair_lds_bytes(bool split, bool ws) {
+  const int np = split ? 2 : 1, w1 = (K1 / BK) * np * BM * BK, w2 = np * N2 * BK;
+  return 2 * ((K1 / BK) * np * BM * BK + (ws ? (w1 > w2 ? w1 : w2) : w1 + w2) + np * BM * BK);
+}
+
 template <int K1, int N2>
 void launch_pair(const PairArgs& a, hipStream_t s) {
-  const dim3 grid((a.M + BM - 1) / BM);
-  if (a.split)
-    hipLaunchKernelGGL((conv_pair_kernel<K1, N2, true>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_pair_kernel<K1, N2, false>), grid, dim3(256), 0, s, a);
+  const int blocks = (a.M + BM - 1) / BM;
+  const dim3 grid(blocks);
+  // shared W: only where it turns one block per CU into two (160 KiB of LDS per CU) and the grid
+  // needs more than one block per CU (256 CUs) -- below that the overlapped W loads are faster
+  constexpr int kCuLds = 160 * 1024, kCus = 256;
+  const bool helps = pair_lds_bytes<K1, N2>(a.split, false) > kCuLds / 2 && pair_lds_bytes<K1, N2>(a.split, true) <= kCuLds / 2;
+  const int mode = g_pair_shared_w >= -1 ? g_pair_shared_w : a.shared_w;
+  const bool ws = mode == 1 || (mode < 0 && helps && blocks > kCus);
+  if (a.split) {
+    if (ws) hipLaunchKernelGGL((conv_pair_kernel<K1, N2, true, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_pair_kernel<K1, N2, true>), grid, dim3(256), 0, s, a);
+  } else {
+    if (ws) hipLaunchKernelGGL((conv_pair_kernel<K1, N2, false, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_pair_kernel<K1, N2, false>), grid, dim3(256), 0, s, a);
+  }
 }
 
 }  // namespace
+
+void set_pair_shared_w(int v) { g_pair_shared_w = v; }
 
 // N2 = 256 (the stage-2 -> stage-3 boundary of ResNet-v2): the W2 slice is 64 KiB in split mode,
 // 144 KiB of LDS in all at K1 = 128.

@@ -260,6 +260,10 @@ struct PairArgs {
   const uint16_t* zeros = nullptr;    // zero page >= K1 + 64 elements (M-tail rows)
   int split = 0;
   long long wplane1 = 0, wplane2 = 0;
+  // One LDS buffer for the W1 chunk and the W2 slice (used in turn, not overlapped): 80 KiB per
+  // block instead of 112 / 96 at K1 = 128 in fp32, so two blocks share a CU.  -1 = when the grid
+  // exceeds one block per CU (M / 64 > 256, e.g. stage 2 above batch 20), 0 = never, 1 = always.
+  int shared_w = -1;
 };
 // Physical row of logical output channel n in a pair weight matrix (a permutation inside each
 // block of 32 rows; the inverse maps physical -> logical).
@@ -269,6 +273,9 @@ inline int pair_permute_row(int n) {
   return b + 16 * h + 4 * g + t;
 }
 bool conv_pair_supported(int K1, int N1, int N2);
+// Measurement switch (process-wide, read at launch): >= -1 overrides every launch's
+// PairArgs::shared_w (-1 auto, 0 never, 1 always); -2 (default) leaves it to the caller.
+void set_pair_shared_w(int v);
 hipError_t conv_pair(const PairArgs& a, hipStream_t s);
 
 // 7x7 / stride 2 / pad 3 conv, 4 input channels (NHWC, 3 real + 1 zero), 64 output channels:

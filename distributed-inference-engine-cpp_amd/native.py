@@ -698,6 +698,8 @@ def _sig_kernels():
     L.die_kern_set_decode_variant.argtypes = [i]
     L.die_kern_set_layernorm_xcd.restype = None
     L.die_kern_set_layernorm_xcd.argtypes = [i]
+    L.die_kern_set_pair_shared_w.restype = None
+    L.die_kern_set_pair_shared_w.argtypes = [i]
     L.die_kern_set_gap_fc_stop.restype = None
     L.die_kern_set_gap_fc_stop.argtypes = [i]
     L.die_kern_gap_fc.restype = i

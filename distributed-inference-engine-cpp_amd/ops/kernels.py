@@ -185,13 +185,14 @@ def _pack_pair_weight(w, split):
     return split_planes(full) if split else full.to(torch.bfloat16)
 
 
-def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False, store_x=True, store_a=False):
+def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False, store_x=True, store_a=False,
+              shared_w=-1):
     """Fused expand + next-reduce 1x1 pair (kernels/conv_pair.hip) over rows.
     y [M, K1], w1 [N1, K1], b1 [N1], res [M, N1], s2/h2 [N1], w2 [N2, N1], b2 [N2] (float).
     Returns (x, out): x = y @ w1.T + b1 + res  [M, N1] (None unless store_x) and
     out = act(act2(x * s2 + h2) @ w2.T + b2)  [M, N2], as fp32 (split planes joined) or bf16;
     store_a: also the stored pre-activation a = act2(x * s2 + h2) [M, N1] (PairArgs::aout), as a
-    third element."""
+    third element.  shared_w: PairArgs::shared_w (-1 auto, 0 separate W1 / W2 buffers, 1 one shared buffer)."""
     import torch
 
     M, K1 = y.shape
@@ -206,7 +207,8 @@ def conv_pair(y, w1, b1, res, s2, h2, w2, b2, relu=True, relu2=True, split=False
     xo = torch.empty(np_ + (M, N1), dtype=torch.bfloat16, device=dev) if store_x else None
     out = torch.empty(np_ + (M, N2), dtype=torch.bfloat16, device=dev)
     zeros = torch.zeros(4096, dtype=torch.int16, device=dev)
-    g = dict(M=M, K1=K1, N1=N1, N2=N2, relu=int(relu), relu2=int(relu2), split=int(split), zeros=int(zeros.data_ptr()))
+    g = dict(M=M, K1=K1, N1=N1, N2=N2, relu=int(relu), relu2=int(relu2), split=int(split), zeros=int(zeros.data_ptr()),
+             shared_w=int(shared_w))
     ao = torch.empty(np_ + (M, N1), dtype=torch.bfloat16, device=dev) if store_a else None
     if store_a:
         g["aout"] = int(ao.data_ptr())

@@ -104,6 +104,32 @@ def test_pair_bit_exact_vs_unfused_kernels(native, shape):
     assert torch.equal(of, o2.reshape(M, N2)), (of - o2.reshape(M, N2)).abs().max().item()
 
 
+@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("shape", [(24 * 28 * 28 - 9, 128, 512, 128), (2 * 56 * 56 - 1, 64, 256, 64),
+                                   (3 * 28 * 28, 128, 512, 64), (1000, 128, 512, 256)])
+def test_pair_shared_w_bitwise(native, shape, split):
+    """PairArgs::shared_w: the W1 chunk and the W2 slice loaded in turn through one LDS buffer (two
+    blocks per CU in fp32 at K1 = 128) is the same arithmetic in the same order -- x, a and the output
+    equal the separate-buffer launch bit for bit, also when repeated (race screen), in both modes;
+    auto (-1) picks it only above one block per CU for the shapes it helps."""
+    torch = _t()
+    from die_amd.ops import kernels as K
+
+    M, K1, N1, N2 = shape
+    prob = list(_problem(M, K1, N1, N2, seed=M + N2))
+    if not split:
+        for i in (0, 3):
+            prob[i] = prob[i].to(torch.bfloat16)
+    ref = K.conv_pair(*prob, split=split, store_a=True, shared_w=0)
+    for _ in range(3):
+        got = K.conv_pair(*prob, split=split, store_a=True, shared_w=1)
+        for g, r in zip(got, ref):
+            assert torch.equal(g, r), (g.float() - r.float()).abs().max().item()
+    auto = K.conv_pair(*prob, split=split, store_a=True)
+    for g, r in zip(auto, ref):
+        assert torch.equal(g, r)
+
+
 def test_pair_without_raw_store_and_repeatable(native):
     torch = _t()
     from die_amd.ops import kernels as K

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--no-fuse-pairs", action="store_true", help="EngineOptions::fuse_pairs off")
     ap.add_argument("--tune-tail", action="store_true", help="EngineOptions::tune_tail on")
+    ap.add_argument("--pair-shared-w", type=int, default=-2,
+                    help="measurement: force PairArgs::shared_w for every pair launch (-1 auto, 0 never, 1 always)")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (one HIP runtime)
@@ -37,6 +39,7 @@ def main():
         from die_amd.models import resnet_v2 as m
 
         cfg = m.ResNetConfig()
+    native.kernels().die_kern_set_pair_shared_w(int(a.pair_shared_w))
     path = os.path.join(tempfile.mkdtemp(), a.arch + ".onnx")
     open(path, "wb").write(m.build_onnx(cfg)[0])
     e = native.Engine(path, device="hip", max_batch=a.hi, precision=a.precision,
@@ -57,7 +60,8 @@ def main():
     buckets = e.refresh_info().get("buckets")
     e.close()
     lines = ["# %s %s%s: captured-forward device time per batch size" % (
-        a.arch, a.precision, (", unfused pairs" if a.no_fuse_pairs else "") + (", tail split-K tuned" if a.tune_tail else "")), "",
+        a.arch, a.precision, (", unfused pairs" if a.no_fuse_pairs else "") + (", tail split-K tuned" if a.tune_tail else "") + (
+            ", pair shared_w %d" % a.pair_shared_w if a.pair_shared_w >= -1 else "")), "",
              "Graph buckets: %s." % buckets, "", "| batch | device ms | us / image |", "|---:|---:|---:|"]
     lines += ["| %d | %.3f | %.1f |" % (r["batch"], r["device_ms"], r["us_per_image"]) for r in rows]
     text = "\n".join(lines) + "\n"
