@@ -113,6 +113,28 @@ def test_concurrent_load_and_batching(cluster, native):
     assert sum(b["total_batches"] for b in batches) > 0
 
 
+@pytest.mark.parametrize("balance", [True, False])
+def test_batch_histogram_and_balance(native, models, balance):
+    """/health batch_processor: the per-size histogram accounts for every batch and request, and
+    batch_balance (WorkerOptions, default on) cuts a long queue to the mean of the queue and the
+    previous batch -- reported as trimmed batches / requests; off, nothing is ever cut (the CPU
+    engine has no preferred batch size of its own)."""
+    path = models["tiny"][0]
+    w = native.Worker(path, node_id="hist", engine={"device": "cpu"}, batch_balance=balance)
+    try:
+        res = native.loadgen(port=w.port, connections=24, requests=480, payload="full", input_numel=3 * 64 * 64)
+        assert res["ok"] == 480, res
+        bp = w.health()["batch_processor"]
+        h = bp["size_histogram"]
+        assert sum(h) == bp["total_batches"]
+        assert sum((i + 1) * c for i, c in enumerate(h)) == bp["total_requests"]
+        assert bp["trimmed_requests"] >= bp["trimmed_batches"] >= 0
+        if not balance:
+            assert bp["trimmed_batches"] == 0
+    finally:
+        w.stop()
+
+
 def test_full_payload_unique_requests(native, models):
     path = models["tiny"][0]
     w = native.Worker(path, node_id="solo", engine={"device": "cpu"})
