@@ -114,11 +114,16 @@ __global__ void pool2d_kernel(const uint16_t* __restrict__ x, uint16_t* __restri
 // head (B~20, 7x7x2048) gets 16x more blocks than one-block-per-64-groups and each thread issues
 // its ~3 16-byte loads back to back, so the 4 MB read is not latency-bound on ~80 blocks.
 // mode 0 mean, 1 sum, 2 max over the HW pixels of each (sample, channel)
-__global__ void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out, float* __restrict__ out_f32,
-                           const float* __restrict__ scale, const float* __restrict__ shift, int relu, int HW, int C,
-                           const long long* __restrict__ live, int split, int mode) {
+// G 8-channel groups x S = 256 / G pixel slices per block.  G = 32 for wide maps (ResNet50's 2048
+// channels): a wave reads 512 contiguous bytes of one pixel row per plane and the slice reduction is
+// 8 deep; G = 8 keeps narrow maps (C < 256) from idling most of the block.
+template <int G>
+__global__ __launch_bounds__(256) void gap_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ out,
+                                                  float* __restrict__ out_f32, const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, int relu, int HW, int C,
+                                                  const long long* __restrict__ live, int split, int mode) {
   const long long xplane = static_cast<long long>(gridDim.y) * HW * C, oplane = static_cast<long long>(gridDim.y) * C;
-  constexpr int G = 8, S = 32;
+  constexpr int S = 256 / G;
   __shared__ float part[S][G][9];  // +1 pad: the reduction reads S slices of one group
   const int b = blockIdx.y;
   if (live && b >= *live) return;  // whole block: before any barrier
@@ -426,8 +431,13 @@ hipError_t global_avgpool(const uint16_t* x, uint16_t* out, float* out_f32, cons
                           int relu, int B, int HW, int C, hipStream_t s, const long long* live, int split, int mode) {
   if (C % 8 || mode < 0 || mode > 2) return hipErrorInvalidValue;
   const int CG = C / 8;
-  dim3 grid((CG + 7) / 8, B);  // 8 channel groups x 32 pixel slices per block
-  hipLaunchKernelGGL(gap_kernel, grid, dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW, C, live, split, mode);
+  if (CG >= 32) {  // 32 channel groups x 8 pixel slices per block
+    hipLaunchKernelGGL(gap_kernel<32>, dim3((CG + 31) / 32, B), dim3(256), 0, s, x, out, out_f32, scale, shift, relu,
+                       HW, C, live, split, mode);
+  } else {  // 8 channel groups x 32 pixel slices per block
+    hipLaunchKernelGGL(gap_kernel<8>, dim3((CG + 7) / 8, B), dim3(256), 0, s, x, out, out_f32, scale, shift, relu, HW,
+                       C, live, split, mode);
+  }
   return hipGetLastError();
 }
 
