@@ -1039,7 +1039,7 @@ class HipEngine : public Engine {
                 kern::tile_dims(tile, bm, bn);
                 const long long wts = static_cast<long long>(base.N) * base.K;
                 const long long acts = static_cast<long long>(base.B) * base.H * base.W * base.Cin;
-                if (tile / kern::NUM_TILES == 6 || tile / kern::NUM_TILES == 7 || wts > acts || acts > 3 * wts ||
+                if (tile / kern::NUM_TILES >= 6 || wts > acts || acts > 3 * wts ||
                     (base.N + bn - 1) / bn < 4 * (order == 4 ? 2 : 1))
                   continue;
               }

@@ -84,6 +84,7 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   const int variant = cfg / NUM_TILES;
   if (a.tail > 0 && (variant == 0 || variant >= 6)) return hipErrorInvalidValue;
   if (variant == 7) return igemm::launch_tile_wide(a, s, cfg % NUM_TILES);
+  if (variant == 8) return igemm::launch_tile_skinny(a, s, cfg % NUM_TILES);
   switch (cfg % NUM_TILES) {
     case TILE_128x128: return igemm::launch_tile_128x128(a, s, variant);
     case TILE_128x64: return igemm::launch_tile_128x64(a, s, variant);

@@ -1339,6 +1339,8 @@ hipError_t launch_tile_64x128(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_64x64(const ConvArgs& a, hipStream_t s, int variant);
 // conv_tile_wide.hip: variant 7 (256-row, 8-wave tiles)
 hipError_t launch_tile_wide(const ConvArgs& a, hipStream_t s, int tile);
+// conv_skinny.hip: variant 8 (<= 32 dense rows, 16 channels per block, K split over 8 waves)
+hipError_t launch_tile_skinny(const ConvArgs& a, hipStream_t s, int tile);
 
 }  // namespace igemm
 }  // namespace kern

@@ -102,7 +102,9 @@ struct ConvArgs {
 // channels per block, input patch staged once per 64-channel slice; 64x64 tile config only).
 // Variant 7 = the 8-wave wide-tile GEMM (fp32 dense rows only): tile 0 -> 256 pixels x 128 channels
 // (conv_igemm_impl.h gemm_wide_kernel); the other tiles of variant 7 are not instantiated.
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 32 };
+// Variant 8 = the skinny dense GEMM (<= 32 rows, e.g. a classifier head at the serving batch):
+// tile 0 only (conv_skinny.hip), 16 channels per block, K split over 8 waves, no split-K.
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 36 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

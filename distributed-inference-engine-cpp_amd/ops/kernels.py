@@ -72,7 +72,7 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split:
 
 
 # launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg)
-NUM_CFGS = 32  # kernels.h TileCfg (variant 7 = the 8-wave wide tile, cfg 28 only)
+NUM_CFGS = 36  # kernels.h TileCfg (variant 7 = the 8-wave wide tile, cfg 28 only; variant 8 = skinny rows, cfg 32 only)
 
 
 class ConvProblem:

@@ -343,3 +343,64 @@ def test_patchify_conv_lds_dma_mode(native, split):
         ran.append(cfg)
     assert any(4 <= c < 8 for c in ran), ran    # 2-stage LDS-DMA ring
     assert any(20 <= c < 24 for c in ran), ran  # 1-stage LDS-DMA loop
+
+
+@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("M,K,N", [(1, 2048, 1000), (7, 2048, 1000), (20, 2048, 1000), (32, 512, 64), (24, 256, 1008)])
+def test_skinny_gemm(native, M, K, N, split):
+    """Variant 8 (cfg 32, conv_skinny.hip): <= 32 dense rows, 16 channels per block, K split over 8
+    waves and summed in wave order.  fp32 (split) against float64 at the layer bar, bf16 against
+    torch; with the residual / dual-store epilogue, a live batch, bitwise repeatable; shapes it
+    does not take (33 rows, K not a multiple of 256, split-K) are refused."""
+    torch = _t()
+    from die_amd.ops import kernels as K_
+
+    g = torch.Generator(device="cuda").manual_seed(M * 13 + K + N)
+    x = torch.randn(M, 1, 1, K, device="cuda", generator=g)
+    w = torch.randn(N, K, 1, 1, device="cuda", generator=g) / K ** 0.5
+    bias = torch.randn(N, device="cuda", generator=g)
+    res = torch.randn(M, 1, 1, N, device="cuda", generator=g)
+    s2 = torch.rand(N, device="cuda", generator=g) + 0.5
+    b2 = torch.randn(N, device="cuda", generator=g)
+    if not split:
+        x, res = x.to(torch.bfloat16), res.to(torch.bfloat16)
+    v = torch.relu(x.double().reshape(M, K) @ w.double().reshape(N, K).T + bias.double() + res.double().reshape(M, N))
+    u = torch.relu(v * s2.double() + b2.double())
+    pr = K_.ConvProblem(x, w, bias=bias, relu=True, res=res, scale2=s2, shift2=b2, relu2=True, max_splits=2, split=split)
+    assert pr.launch(32, 1, False) == 0
+    torch.cuda.synchronize()
+    out, out2 = pr.results()
+    tol = TOL if split else 2e-2
+    assert rel_err(out.reshape(M, N), v) < tol, rel_err(out.reshape(M, N), v)
+    assert rel_err(out2.reshape(M, N), u) < tol
+    first = out.clone()
+    for _ in range(3):
+        assert pr.launch(32, 1, False) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(pr.results()[0], first)
+    # live batch: rows past it keep what was there
+    if M > 1:
+        lv = torch.tensor([M // 2], dtype=torch.int64, device="cuda")
+        pr.out.zero_()
+        assert pr.launch(32, 1, False, extra={"live": lv.data_ptr()}) == 0
+        torch.cuda.synchronize()
+        got = pr.results()[0].reshape(M, N)
+        assert torch.equal(got[: M // 2], first.reshape(M, N)[: M // 2])
+        assert not got[M // 2:].any()
+    assert pr.launch(32, 2, False) != 0  # no split-K
+    for cfg in (33, 34, 35):
+        assert pr.launch(cfg, 1, False) != 0  # tile 0 only
+
+
+def test_skinny_gemm_refuses_other_shapes(native):
+    torch = _t()
+    from die_amd.ops import kernels as K_
+
+    for M, K in ((33, 2048), (8, 2000)):
+        x = torch.randn(M, 1, 1, K, device="cuda")
+        w = torch.randn(64, K, 1, 1, device="cuda")
+        pr = K_.ConvProblem(x, w, split=True)
+        assert pr.launch(32, 1, False) != 0, (M, K)
+    x = torch.randn(2, 4, 4, 256, device="cuda")  # not a dense row problem (3x3)
+    pr = K_.ConvProblem(x, torch.randn(64, 256, 3, 3, device="cuda"), pad=1, split=True)
+    assert pr.launch(32, 1, False) != 0

@@ -17,6 +17,7 @@ SHAPES = [  # name, K (Cin), N (Cout), epilogue
     ("attn_out", 768, 768, "res"),
     ("mlp1", 768, 3072, "gelu"),
     ("mlp2", 3072, 768, "res"),
+    ("fc", 2048, 1000, "plain"),  # a classifier head (ResNet50: --tokens 1 --batch <serving batch>)
 ]
 
 
