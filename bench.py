@@ -373,6 +373,8 @@ def main():
             "trimmed_requests": bp1.get("trimmed_requests", 0) - bp0.get("trimmed_requests", 0),
             # batches per size over the timed pass: [count at size 1, size 2, ...]
             "batch_size_histogram": _hist_window(bp0.get("size_histogram", []), bp1.get("size_histogram", [])),
+            # the engine's start-up forward time per batch size (ms at 1, 2, ...; EngineOptions::efficient_batch)
+            "batch_curve_ms": [round(v, 3) for v in e1.get("batch_curve_ms", [])],
             "device_ms_per_batch": _win(e0, e1, "avg_device_ms"), "engine": e1.get("device"),
             "precision": e1.get("precision"),
             "client_connections_per_gpu": args.connections, "body_bytes": res.get("body_bytes"),
