@@ -166,7 +166,7 @@ class BatchProcessor {
     std::lock_guard<std::mutex> g(metrics_mu_);
     return size_hist_;
   }
-  // Batches the size function cut below the queue (and the requests it left queued).
+  // Batches cut below the queue by balancing or the size function (and the requests left queued).
   long long trimmed_batches() const { return trimmed_batches_.load(); }
   long long trimmed_requests() const { return trimmed_requests_.load(); }
 

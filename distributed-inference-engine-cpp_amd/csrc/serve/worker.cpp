@@ -505,7 +505,7 @@ Json WorkerNode::getHealth() const {
   b["full_batches"] = static_cast<long long>(m.full_batches);
   b["total_requests"] = static_cast<long long>(m.total_requests);
   b["queue_depth"] = static_cast<long long>(batcher_->queue_depth());
-  b["trimmed_batches"] = batcher_->trimmed_batches();    // batches cut below the queue (preferred_batch)
+  b["trimmed_batches"] = batcher_->trimmed_batches();    // batches cut below the queue (balance / preferred_batch)
   b["trimmed_requests"] = batcher_->trimmed_requests();  // requests those cuts left for the next batch
   {
     Json hist = Json::array();  // batches per size: [count at size 1, count at size 2, ...]
