@@ -368,7 +368,8 @@ def main():
                      "slowest_ms": res.get("slowest_ms", []), "device_trace": _device_trace(trace, t0)},
             "cache_hits_timed": h1["cache_hits"] - h0["cache_hits"],
             "avg_batch": (bp1["total_requests"] - bp0["total_requests"]) / max(nb, 1),
-            # EngineOptions::efficient_batch: batches cut below the queue to stay under a per-image step
+            # batches cut below the queue: balanced batches (WorkerOptions::batch_balance) and bucket-end
+            # sizes (EngineOptions::efficient_batch)
             "trimmed_batches": bp1.get("trimmed_batches", 0) - bp0.get("trimmed_batches", 0),
             "trimmed_requests": bp1.get("trimmed_requests", 0) - bp0.get("trimmed_requests", 0),
             # batches per size over the timed pass: [count at size 1, size 2, ...]
