@@ -138,11 +138,16 @@ def main():
                     help="upload input text as-is instead of 4-bit packed (device decode)")
     ap.add_argument("--tune-tail", action="store_true",
                     help="autotune tail split-K candidates too (EngineOptions::tune_tail)")
+    ap.add_argument("--tune-streamk", type=int, default=-1,
+                    help="autotune stream-K candidates (EngineOptions::tune_streamk): 1 on, 0 off, -1 engine default")
     ap.add_argument("--no-efficient-batch", action="store_true",
                     help="dispatch everything queued (up to --batch) instead of cutting a batch back to just "
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
     ap.add_argument("--efficient-batch-tol", type=float, default=0.0,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
+    ap.add_argument("--efficient-batch-margin", type=float, default=0.02,
+                    help="EngineOptions::efficient_batch_margin: a batch is cut only when a smaller size is "
+                         "cheaper per image by more than this fraction")
     ap.add_argument("--no-batch-balance", action="store_true",
                     help="dispatch everything queued instead of the mean of the queue and the previous batch "
                          "(WorkerOptions::batch_balance)")
@@ -290,7 +295,9 @@ def main():
                    "fuse_gap_fc": args.fuse_gap_fc, "fold_layernorm": not args.no_fold_layernorm,
                    "ln_stats_epilogue": not args.no_ln_stats_epilogue, "tune_in_graph": args.tune_in_graph,
                    "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute,
-                   "efficient_batch": not args.no_efficient_batch, "tune_tail": args.tune_tail, "efficient_batch_tol": args.efficient_batch_tol}
+                   "efficient_batch": not args.no_efficient_batch, "tune_tail": args.tune_tail,
+                   **({} if args.tune_streamk < 0 else {"tune_streamk": bool(args.tune_streamk)}), "efficient_batch_tol": args.efficient_batch_tol,
+                   "efficient_batch_margin": args.efficient_batch_margin}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with
@@ -410,7 +417,12 @@ def main():
             extra["verify"] = {"every": args.verify_every, "inputs": 8, "oracle": "cpu_executor_fp32",
                                "tol": verify["verify_tol"], "verified": res.get("verified", 0),
                                "mismatched": res.get("mismatched", 0), "bad_request_id": res.get("bad_request_id", 0),
-                               "max_rel_err": res.get("max_rel_err")}
+                               "max_rel_err": res.get("max_rel_err"),
+                               "repeat_period": res.get("verify_repeat_period")}
+            # every verified answer computed, never served from the cache: no verify text repeats
+            rp = res.get("verify_repeat_period")
+            if rp is not None and rp < SR * (args.steps + args.warmup):
+                extra["verify"]["error"] = "verify texts repeat after %d requests" % rp
         extra["worker_requests_timed"] = bp1["total_requests"] - bp0["total_requests"]
         if gw:
             extra["gateway"] = {"failovers": g1["failovers"] - g0["failovers"], "failed": g1["failed"] - g0["failed"],
@@ -583,7 +595,7 @@ def main():
         extra["p50_ms"], extra["p99_ms"] = hg.reduce([extra.get("p50_ms", 0.0), extra.get("p99_ms", 0.0)], "max")
     value = ok / elapsed
     v = extra.get("verify")
-    if isinstance(v, dict) and (v["mismatched"] or v["bad_request_id"] or not v["verified"]):
+    if isinstance(v, dict) and (v["mismatched"] or v["bad_request_id"] or not v["verified"] or v.get("error")):
         extra["error"] = "answer verification failed: %s" % (v,)
         value = 0.0  # a wrong answer does not score
     if world == 1 and isinstance(extra.get("gateway_bytes"), dict):

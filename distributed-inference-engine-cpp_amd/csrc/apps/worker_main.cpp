@@ -67,9 +67,11 @@ die::EngineOptions engine_options_from_flags(const die::Flags& f, const std::str
   eo.tune_in_graph = f.b("tune-in-graph");
   eo.tune_orders = !f.b("no-tune-orders");
   eo.tune_tail = f.b("tune-tail");
+  if (f.has("tune-streamk")) eo.tune_streamk = f.b("tune-streamk");
   eo.tune_cold = !f.b("tune-warm");
   eo.efficient_batch = !f.b("no-efficient-batch");
   eo.efficient_batch_tol = f.f("efficient-batch-tol", 0.0);
+  eo.efficient_batch_margin = f.f("efficient-batch-margin", eo.efficient_batch_margin);
   eo.dp_backend = f.str("dp-backend", "rccl");
   eo.dp_force_merge = f.b("dp-force-merge");
   eo.fail_batch_every = static_cast<int>(f.i("fail-batch-every", 0));

@@ -104,8 +104,10 @@ EngineOptions engine_opts(const Json& j) {
   e.tune_in_graph = jget<bool>(j, "tune_in_graph", e.tune_in_graph);
   e.tune_orders = jget<bool>(j, "tune_orders", e.tune_orders);
   e.tune_tail = jget<bool>(j, "tune_tail", e.tune_tail);
+  e.tune_streamk = jget<bool>(j, "tune_streamk", e.tune_streamk);
   e.efficient_batch = jget<bool>(j, "efficient_batch", e.efficient_batch);
   e.efficient_batch_tol = jget<double>(j, "efficient_batch_tol", e.efficient_batch_tol);
+  e.efficient_batch_margin = jget<double>(j, "efficient_batch_margin", e.efficient_batch_margin);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
@@ -236,7 +238,8 @@ struct TestBatcher {
   int delay_ms = 0;
 };
 // size_cap > 0: a batch-size function (Engine::preferred_batch's hook) that takes at most size_cap
-void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int delay_ms, int size_cap) {
+// balance: WorkerOptions::batch_balance (BatchProcessor::set_balance)
+void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int delay_ms, int size_cap, int balance) {
   auto* t = new TestBatcher();
   t->delay_ms = delay_ms;
   t->bp = std::make_unique<BatchProcessor<int, int>>(
@@ -257,6 +260,7 @@ void* die_batcher_create(int max_batch, int timeout_ms, int deadline_policy, int
       deadline_policy ? BatchPolicy::DEADLINE : BatchPolicy::GREEDY);
   if (size_cap > 0)
     t->bp->set_size_fn([cap = static_cast<size_t>(size_cap)](size_t q) { return q > cap ? cap : q; });
+  t->bp->set_balance(balance != 0);
   t->bp->start();
   return t;
 }
@@ -338,6 +342,9 @@ int die_engine_run(void* p, const float* in, long B, long len, float* out, char*
 int die_pack_nibbles(const char* src, long long n, unsigned char* dst) { return pack_nibbles(src, static_cast<size_t>(n), dst) ? 1 : 0; }
 void die_unpack_nibbles(const unsigned char* src, long long n, char* dst) { unpack_nibbles(src, static_cast<size_t>(n), dst); }
 int die_engine_preferred_batch(void* p, int queued) { return static_cast<Engine*>(p)->preferred_batch(queued); }
+int die_pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin) {
+  return pick_efficient_batch(ms, max_b, queued, tol, margin);
+}
 int die_engine_text_packing(void* p) { return static_cast<Engine*>(p)->text_packing() ? 1 : 0; }
 
 // Device-decode path: B texts (concatenated, lens[b] bytes each) -> outputs [B][out] and status[b]

@@ -70,6 +70,7 @@ int die_kern_conv(const char* geom, uint64_t x, uint64_t w, uint64_t bias, uint6
     a.order = geti(j, "order", 0);
     a.probe = geti(j, "probe", 0);
     a.tail = geti(j, "tail", 0);
+    a.sk = geti(j, "sk", 0);
     if (auto* v = j.find("live")) a.live = P<const long long>(static_cast<uint64_t>(v->as_int()));  // live batch (int64 on the device)
     if (auto* v = j.find("ws")) a.ws = P<float>(static_cast<uint64_t>(v->as_int()));
     if (auto* v = j.find("zeros")) a.zeros = P<const uint16_t>(static_cast<uint64_t>(v->as_int()));

@@ -381,6 +381,14 @@ class DpEngine : public Engine {
       pace_wait_us_ = pace_wait_us_.load() + std::chrono::duration<double, std::micro>(tp3 - tp2).count();
       b->B = 0;
       b->nsub = 0;
+      // Efficient batch sizes (EngineOptions::efficient_batch, as the plain worker's batcher): the
+      // local engine's start-up curve says which per-rank size to run for what is queued now; the
+      // merge stops at that many items per rank (sub-batches stay whole, the rest leads the next
+      // batch).  VERDICT r5 item 5: without it the DP path ran whatever was queued (21.6 images per
+      // batch at world 1 against the plain worker's bucket-end 23-24, -5.7 %).
+      const int queued = std::min(cap, s->n + group_->queued_items());
+      const int per_q = (queued + world_ - 1) / world_;
+      const int target = std::max(s->n, std::min(cap, local_->preferred_batch(per_q) * world_));
       while (true) {
         DpSubRef& ref = b->subs[b->nsub++];
         ref.rank = rank;
@@ -391,7 +399,7 @@ class DpEngine : public Engine {
         b->B += s->n;
         subs_merged_++;
         const int next = group_->peek_sub_items();
-        if (next < 0 || b->B + next > cap || b->nsub >= kDpMaxSubs) break;
+        if (next < 0 || b->B + next > target || b->nsub >= kDpMaxSubs) break;
         if (!group_->pop_sub(*s, rank, 0)) break;
       }
       b->per = (b->B + world_ - 1) / world_;

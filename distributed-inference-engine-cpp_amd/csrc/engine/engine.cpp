@@ -297,8 +297,10 @@ Json engine_options_json(const EngineOptions& o) {
   j["tune_in_graph"] = o.tune_in_graph;
   j["tune_orders"] = o.tune_orders;
   j["tune_tail"] = o.tune_tail;
+  j["tune_streamk"] = o.tune_streamk;
   j["efficient_batch"] = o.efficient_batch;
   j["efficient_batch_tol"] = o.efficient_batch_tol;
+  j["efficient_batch_margin"] = o.efficient_batch_margin;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;
@@ -307,6 +309,19 @@ Json engine_options_json(const EngineOptions& o) {
   j["conv_order"] = o.conv_order;
   j["fail_batch_every"] = o.fail_batch_every;
   return j;
+}
+
+int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin) {
+  const int q = std::min(queued, max_b);
+  if (!ms || q <= 1) return std::max(1, q);
+  double best = 1e30;
+  for (int b = 1; b <= q; ++b) best = std::min(best, ms[b] / b);
+  // the whole queue unless a smaller batch is clearly cheaper per image
+  if (ms[q] / q * (1.0 - std::max(0.0, margin)) <= best) return q;
+  const double lim = best * (1.0 + std::max(0.0, tol));
+  for (int b = q - 1; b > 1; --b)
+    if (ms[b] / b <= lim) return b;
+  return 1;
 }
 
 std::unique_ptr<Engine> create_cpu_engine(const std::string& model_path, const EngineOptions& opt) {

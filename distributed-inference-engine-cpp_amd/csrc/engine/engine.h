@@ -263,6 +263,9 @@ struct EngineOptions {
   // isolated timing it won 3 of ~1,200 ResNet/ViT shapes and left the per-batch-size forward time
   // unchanged (profiles/r5_batch_curve.md)
   bool tune_tail = false;
+  // autotune stream-K candidates too (ConvArgs::sk: P = 256 / 512 / 1024 blocks split the tiles x
+  // K-steps iterations evenly, cut tiles reduced in-kernel)
+  bool tune_streamk = false;
   bool tune_warm_input = false;   // autotune: run each conv's input producer right before every timing
                                   // (measured no better than the scrub alone: profiles/r3_gemm_feed.md §7)
   // Split-K reductions run in-kernel (the last-arriving split block of a tile sums the partials and
@@ -278,8 +281,12 @@ struct EngineOptions {
   // B = 20 for 5 % more images, profiles/r5_batch_curve.md).  0 = the best itself: a bucket's
   // forward costs about the same at every live size, so that is a bucket's full size (20, 24, ...);
   // measured +2.9 % over 0.03, which let a batch of 25 run bucket 26's graph.
+  // A batch is only cut below the queue when a smaller size is faster per image by more than
+  // efficient_batch_margin (inside one bucket the curve is flat to within replay noise,
+  // so the strict argmin let start-up noise decide whether requests wait a whole forward).
   bool efficient_batch = true;
   double efficient_batch_tol = 0.0;
+  double efficient_batch_margin = 0.02;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;
@@ -288,6 +295,12 @@ struct EngineOptions {
 // Every option as a JSON object (the /health "engine" document and bench.py echo it, so a run's
 // configuration can be reconstructed from its output).
 Json engine_options_json(const EngineOptions& o);
+
+// EngineOptions::efficient_batch policy over a per-batch-size forward-time curve (ms[b], b = 1..
+// max_b; ms[0] unused): with `queued` requests waiting, the batch size to dispatch.  Keeps the whole
+// queue unless some smaller size is cheaper per image by more than `margin`; then the largest size
+// within `tol` of the cheapest.  Pure (CPU-tested through the C API).
+int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin);
 
 // Factory: HIP engine when a GPU is visible and device != cpu, else the CPU executor (the
 // reference's ORT CUDA-EP -> CPU-EP fallback, src/inference_engine.cpp:21-29, made explicit).

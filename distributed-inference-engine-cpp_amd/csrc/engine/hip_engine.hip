@@ -270,7 +270,9 @@ class HipEngine : public Engine {
       // warm the graph path once
       HIP_CHECK(hipGraphLaunch(graphs_.back(), s_compute_));
       HIP_CHECK(hipStreamSynchronize(s_compute_));
-      if (opt.efficient_batch && n_exec_ == 1 && !comm_) measure_batch_curve();
+      // (data parallel too: the leader's merge takes the local curve's sizes -- the MAIN graphs hold
+      // no collectives, so each rank times its own forward)
+      if (opt.efficient_batch && n_exec_ == 1) measure_batch_curve();
     }
     for (auto& e : tev_) HIP_CHECK(hipEventCreate(&e));
     completion_ = std::thread([this] {
@@ -669,15 +671,11 @@ class HipEngine : public Engine {
   // with B except where a layer's tile grid spills into one more round of blocks (ResNet50 fp32:
   // 61.6 us per image at B = 20, 69.6 at 21, profiles/r5_batch_curve.md), so this only ever cuts a
   // batch back to just below such a step; the requests left over lead the next batch.
+  // A cut needs a smaller size cheaper per image by more than efficient_batch_margin (inside a
+  // bucket the curve is flat to within replay noise).
   int preferred_batch(int queued) const override {
-    const int q = std::min(queued, max_batch_);
-    if (batch_ms_.empty() || q <= 1) return std::max(1, q);
-    double best = 1e30;
-    for (int b = 1; b <= q; ++b) best = std::min(best, batch_ms_[static_cast<size_t>(b)] / b);
-    const double lim = best * (1.0 + std::max(0.0, opt_.efficient_batch_tol));
-    for (int b = q; b > 1; --b)
-      if (batch_ms_[static_cast<size_t>(b)] / b <= lim) return b;
-    return 1;
+    return pick_efficient_batch(batch_ms_.empty() ? nullptr : batch_ms_.data(), max_batch_, queued,
+                                opt_.efficient_batch_tol, opt_.efficient_batch_margin);
   }
 
   void synchronize() override {
@@ -759,7 +757,8 @@ class HipEngine : public Engine {
         if (plan_.ops[oi].kind == PlanOp::CONV) {
           const Tune& x = tune_.back()[oi];
           t.push_back(std::to_string(x.tile) + "/" + std::to_string(x.splits) + (x.fused ? "f" : "") +
-                      (x.order == 2 ? "m" : x.order == 1 ? "n" : "") + (x.tail ? "t" : ""));
+                      (x.order == 2 ? "m" : x.order == 1 ? "n" : "") + (x.tail ? "t" : "") +
+                      (x.sk ? "k" + std::to_string(x.sk) : ""));
         }
       j["tile_split_at_max_batch"] = t;
     }
@@ -772,6 +771,7 @@ class HipEngine : public Engine {
     bool fused = false;  // split-K reduced in-kernel by the last split block (else a second kernel)
     int order = 0;       // ConvArgs::order (0 heuristic, 1 N-fastest, 2 M-fastest)
     int tail = 0;        // ConvArgs::tail (> 0: split-K on the last partial round's tiles only)
+    int sk = 0;          // ConvArgs::sk (> 0: stream-K launch of sk blocks; splits/tail unused)
   };
 
   // ---- autotune persistence (kernel configs cached in a tuning file) ----
@@ -798,7 +798,8 @@ class HipEngine : public Engine {
         if (a.size() < 4) continue;
         out[kv.first] = {Tune{static_cast<int>(a[0].as_int()), static_cast<int>(a[1].as_int()), a[2].as_bool(),
                               a.size() > 4 ? static_cast<int>(a[4].as_int()) : 0,
-                              a.size() > 5 ? static_cast<int>(a[5].as_int()) : 0},
+                              a.size() > 5 ? static_cast<int>(a[5].as_int()) : 0,
+                              a.size() > 6 ? static_cast<int>(a[6].as_int()) : 0},
                          a[3].as_double()};
       }
     } catch (const std::exception&) {
@@ -827,6 +828,7 @@ class HipEngine : public Engine {
         a.push_back(kv.second.second);
         a.push_back(kv.second.first.order);
         a.push_back(kv.second.first.tail);
+        a.push_back(kv.second.first.sk);
         arch[kv.first] = a;
       }
       root[arch_] = arch;
@@ -889,7 +891,8 @@ class HipEngine : public Engine {
 
   // Device time of the captured forward at every batch size 1..max_batch (EngineOptions::
   // efficient_batch): slot 0's MAIN graph of the batch's bucket with the live count set to B, one
-  // warm-up and three timed back-to-back replays (the serving loop runs graphs back to back).
+  // warm-up, then the median of three timed groups of three back-to-back replays (the serving loop
+  // runs graphs back to back; the median keeps one slow group from moving a cut).
   void measure_batch_curve() {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIP_CHECK(hipEventCreate(&e0));
@@ -902,13 +905,16 @@ class HipEngine : public Engine {
       *lv = use_live_ ? b : max_batch_;
       HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
       HIP_CHECK(hipGraphLaunch(g, s_compute_));
-      HIP_CHECK(hipEventRecord(e0, s_compute_));
-      for (int r = 0; r < 3; ++r) HIP_CHECK(hipGraphLaunch(g, s_compute_));
-      HIP_CHECK(hipEventRecord(e1, s_compute_));
-      HIP_CHECK(hipEventSynchronize(e1));
-      float ms = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      batch_ms_[static_cast<size_t>(b)] = ms / 3.0;
+      float grp[3];
+      for (float& ms : grp) {
+        HIP_CHECK(hipEventRecord(e0, s_compute_));
+        for (int r = 0; r < 3; ++r) HIP_CHECK(hipGraphLaunch(g, s_compute_));
+        HIP_CHECK(hipEventRecord(e1, s_compute_));
+        HIP_CHECK(hipEventSynchronize(e1));
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      }
+      std::sort(grp, grp + 3);
+      batch_ms_[static_cast<size_t>(b)] = grp[1] / 3.0;
     }
     *lv = max_batch_;
     HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
@@ -945,7 +951,8 @@ class HipEngine : public Engine {
   // Tune-cache / memo key of a conv problem: the shape, its epilogue, and the tuning regime.
   std::string shape_key(const kern::ConvArgs& base, bool warm_input) const {
     char key[256];
-    std::snprintf(key, sizeof(key), "o%s%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_tail ? "t:" : "",
+    std::snprintf(key, sizeof(key), "o%s%s%s%s%s%s%s%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", opt_.tune_streamk ? "k:" : "",
+                  opt_.tune_tail ? "t:" : "",
                   opt_.tune_cold ? "c:" : "",
                   warm_input ? "w:" : "", sp_ ? "f32:" : "", base.stats_out || base.row_parts ? "ls:" : "",
                   opt_.splitk_two_kernel ? (opt_.splitk_fused_margin > 0.f ? "fm:" : "sk2:") : (opt_.tune_orders ? "" : "o0:"),
@@ -1087,6 +1094,54 @@ class HipEngine : public Engine {
             }
           }
         }
+        // Stream-K candidates (EngineOptions::tune_streamk): the LDS-DMA loops with P = 256 / 512 /
+        // 1024 blocks splitting the tiles x K-steps evenly (ConvArgs::sk) -- for grids whose tile
+        // count lands just past a multiple of the CU count (ResNet50 stage-3 reduce at B = 24: 296
+        // tiles = two tiles on 40 CUs, one on the rest)
+        if (opt_.tune_streamk && base.N % 8 == 0 && !base.in_scale && !base.row_parts && !base.stats_out)
+          for (int tile = 0; tile < kern::NUM_CFGS; ++tile) {
+            const int v = tile / kern::NUM_TILES;
+            if (v != 1 && v != 5) continue;  // 2-stage ring and 1-stage loop
+            int bm, bn;
+            kern::tile_dims(tile, bm, bn);
+            const long long T = static_cast<long long>((base.M + bm - 1) / bm) * ((base.N + bn - 1) / bn);
+            for (int P : {256, 512, 1024}) {
+              if (T * nk < P || T > kCounters || kern::streamk_workspace_bytes(P, bm, bn) > ws_bytes_) continue;
+              kern::ConvArgs a = base;
+              a.splits = 1;
+              a.sk = P;
+              if (kern::conv_igemm(a, tile, s_compute_) != hipSuccess) continue;
+              float ms = 0;
+              if (cold) {
+                float rep[3];
+                for (int r = 0; r < 3; ++r) {
+                  HIP_CHECK(kern::l2_scrub(scrub, kScrubBytes, sink, s_compute_));
+                  if (producer >= 0)
+                    encode_forward(B, 0, s_compute_, nullptr, ALL, static_cast<size_t>(producer),
+                                   static_cast<size_t>(producer) + 1);
+                  HIP_CHECK(hipEventRecord(e0, s_compute_));
+                  HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
+                  HIP_CHECK(hipEventRecord(e1, s_compute_));
+                  HIP_CHECK(hipEventSynchronize(e1));
+                  HIP_CHECK(hipEventElapsedTime(&rep[r], e0, e1));
+                }
+                std::sort(rep, rep + 3);
+                ms = 3.f * rep[1];
+              } else {
+                HIP_CHECK(hipEventRecord(e0, s_compute_));
+                for (int r = 0; r < 3; ++r) HIP_CHECK(kern::conv_igemm(a, tile, s_compute_));
+                HIP_CHECK(hipEventRecord(e1, s_compute_));
+                HIP_CHECK(hipEventSynchronize(e1));
+                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+              }
+              Tune tk{tile, 1, true, 0, 0, P};
+              measured.push_back({ms, tk});
+              if (ms < best) {
+                best = ms;
+                bt = tk;
+              }
+            }
+          }
         if (bt.splits > 1 && !bt.fused && best_fused <= best * (1.f + opt_.splitk_fused_margin)) {
           bt = bt_fused;  // EngineOptions::splitk_fused_margin: one graph node instead of two
           best = best_fused;
@@ -1141,14 +1196,16 @@ class HipEngine : public Engine {
       for (size_t oi = 0; oi < n; ++oi) {
         const PlanOp& op = plan_.ops[oi];
         if (op.kind != PlanOp::CONV) continue;
+        kern::ConvArgs base = conv_args(op, B, 0);
+        // keyed by position AND by the op's shape + tuning regime: another model with
+        // the same op count and names, or another tuning regime, never loads this choice
         const std::string gkey = "g" + std::to_string(n) + ":b" + std::to_string(B) + ":o" + std::to_string(oi) + ":" +
-                                 op.name.substr(0, 64) + ":" + std::to_string(sp_);
+                                 op.name.substr(0, 64) + ":" + std::to_string(sp_) + ":" + shape_key(base, false);
         auto memo = tuned_shapes.find(gkey);
         if (memo != tuned_shapes.end()) {
           tune_[bi][oi] = memo->second.first;
           continue;
         }
-        kern::ConvArgs base = conv_args(op, B, 0);
         const auto c = cands_.find(shape_key(base, false));  // the isolated-launch front runners
         if (c == cands_.end() || c->second.size() < 2) continue;
         float best = 1e30f;
@@ -1264,6 +1321,7 @@ class HipEngine : public Engine {
           const Tune t = tune_for(B, op_index);
           a.splits = t.splits;
           a.tail = t.tail;
+          a.sk = t.sk;
           a.order = opt_.conv_order > 0 ? opt_.conv_order : t.order;
           a.ws = side ? ws_side_ : wss_[s % n_exec_];
           if (side) a.counters = counters_side_;
@@ -1492,6 +1550,7 @@ class HipEngine : public Engine {
         o["fused_splitk"] = t.fused;
         o["tile_order"] = t.order;
         o["tail_splitk"] = t.tail > 0;
+        o["streamk_blocks"] = t.sk;
       }
       total += us[i];
       ops.push_back(o);

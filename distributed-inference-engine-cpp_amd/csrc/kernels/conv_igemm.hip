@@ -83,8 +83,10 @@ hipError_t conv_igemm(const ConvArgs& a, int cfg, hipStream_t s) {
   if (cfg < 0 || cfg >= NUM_CFGS) return hipErrorInvalidValue;
   const int variant = cfg / NUM_TILES;
   if (a.tail > 0 && (variant == 0 || variant >= 6)) return hipErrorInvalidValue;
+  if (a.sk < 0 || (a.sk > 0 && (variant == 0 || variant >= 6))) return hipErrorInvalidValue;  // stream-K: LDS-DMA loops
   if (variant == 7) return igemm::launch_tile_wide(a, s, cfg % NUM_TILES);
   if (variant == 8) return igemm::launch_tile_skinny(a, s, cfg % NUM_TILES);
+  if (variant == 9) return igemm::launch_tile_quad(a, s, cfg % NUM_TILES);
   switch (cfg % NUM_TILES) {
     case TILE_128x128: return igemm::launch_tile_128x128(a, s, variant);
     case TILE_128x64: return igemm::launch_tile_128x64(a, s, variant);

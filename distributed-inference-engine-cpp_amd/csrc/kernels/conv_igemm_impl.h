@@ -110,7 +110,10 @@ __device__ __forceinline__ float2 row_parts_direct(const ConvArgs& p, int m) {
 // caller maps consecutive threads to consecutive 8-channel chunks of one row, and N % 64 == 0)
 // merge their (mean, M2) by DPP; the formula is symmetric, so all 8 lanes agree and the result does
 // not depend on which lane stores it.
-__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v, const float* ms = nullptr) {
+// rpre: the residual's 8 values already loaded (tile_epilogue prefetches a thread's residual rows
+// before its first store, so the loads are not serialised behind the previous group's stores).
+__device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v, const float* ms = nullptr,
+                                          const float* rpre = nullptr) {
   const size_t o = static_cast<size_t>(m) * p.N + n;
   const bool split = p.split != 0;
   if (p.row_stats || p.row_parts) {
@@ -138,7 +141,12 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
   }
   if (p.res) {
     float r[8];
-    load8v(p.res + o, p.oplane, split, r);
+    if (rpre) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) r[t] = rpre[t];
+    } else {
+      load8v(p.res + o, p.oplane, split, r);
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += r[t];
   }
@@ -174,14 +182,40 @@ struct LinearRows {
   __device__ __forceinline__ int operator()(int r) const { return m0 + r < M ? m0 + r : -1; }
 };
 
+// Stream-K partials (ConvArgs::sk = P persistent blocks): block b owns iterations [start(b),
+// start(b+1)) of the T x nk (tile, K-step) space, start(b) = floor(b * I / P), I = T * nk.  A tile
+// cut between blocks first..last gets one partial from each; block b keeps at most two partial
+// slabs (its first and its last segment), slab 2b + which of BM x BN floats in ConvArgs::ws, and
+// the tile's last arriver sums them in block order (deterministic for a given P).
+struct StreamK {
+  long long I = 0;  // total iterations (0: not a stream-K launch)
+  int P = 0;
+  int nk = 0;       // K-steps per tile
+  __device__ __forceinline__ long long start(int b) const { return static_cast<long long>(b) * I / P; }
+  __device__ __forceinline__ int owner(long long x) const { return static_cast<int>(((x + 1) * P - 1) / I); }
+  // slab of block b's partial of tile t (its first segment unless t began before b's range)
+  __device__ __forceinline__ int slab(int b, int t) const {
+    return 2 * b + (start(b) >= static_cast<long long>(t) * nk ? 0 : 1);
+  }
+};
+
 // NT threads = (NT / 64) waves, WAVES_M along the tile's rows (pixels) x NT / 64 / WAVES_M along its
 // channels; acc[i][j]: the wave's i-th 16-channel x j-th 16-pixel fragment.
+// Split-K: `split` is this block's slice (partial slab) and `nsplit` the tile's slice count (-1:
+// p.splits); with a stream-K map (sk.I > 0) `split` is this block's id and the tile's partials are
+// those of blocks first..first + nsplit - 1.
 template <int BM, int BN, typename RowMap = LinearRows, int NT = 256, int WAVES_M = 2>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
                                               f32x4 (&acc)[BN / 16 / (NT / 64 / WAVES_M)][BM / 16 / WAVES_M],
                                               uint16_t* lds, int m0, int n0, int wm, int wn, int lane, int tid,
                                               int tile, int split, RowMap rows = RowMap{0, 0},
-                                              float2 rms = float2{0.f, 0.f});
+                                              float2 rms = float2{0.f, 0.f}, int flag_off = -1, int nsplit = -1,
+                                              StreamK sk = StreamK{}, int sk_first = 0);
+
+// LDS element offset of the fused split-K "last arriver" word past the epilogue staging (epi
+// elements), or -1 when the block's LDS has no room there (the word then overwrites the staging
+// tile and the last arriver re-reads its own partial from the workspace).
+constexpr int epi_flag_off(int lds_elems, int epi_elems) { return lds_elems >= epi_elems + 2 ? epi_elems : -1; }
 
 // XCD-aware block -> (tile, split-K slice).  Blocks are dealt round-robin over the 8 XCDs (linear
 // id % 8 labels the blocks that share one XCD and its L2; cdna_hip_programming T1), so the naive
@@ -196,6 +230,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
 // Tail split-K (ConvArgs::tail): the first Tw = T - T % tail tiles are whole (split = -1: the full
 // K range, direct epilogue) and the T - Tw tiles of the last partial round get S slices each.
 // Returns false for a block without work.
+__device__ __forceinline__ void tile_mn(const ConvArgs& p, int ntm, int ntn, int tile, int& tile_m, int& tile_n);
 __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, int& tile_m, int& tile_n, int& split,
                                              int& tile) {
   const int S = p.tail > 0 ? p.splits : static_cast<int>(gridDim.y);  // split-K slices
@@ -212,6 +247,12 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   const int sid = id - Tw, st = sid / S;
   tile = id < Tw ? id : Tw + st;
   split = id < Tw ? -1 : sid - st * S;
+  tile_mn(p, ntm, ntn, tile, tile_m, tile_n);
+  return true;
+}
+
+// Logical tile index -> (tile_m, tile_n) (block_coords' tile order; also the stream-K walk's).
+__device__ __forceinline__ void tile_mn(const ConvArgs& p, int ntm, int ntn, int tile, int& tile_m, int& tile_n) {
   // Replicate (read on every XCD) the operand with fewer bytes: the weights are N x K, the
   // activations the INPUT tensor, B*H*W*Cin -- not the im2col M x K, which counts a 3x3 conv's
   // input 9 times (stage-4 3x3 at batch 16-32: weights 4.7x the input, so M-fastest).
@@ -234,7 +275,6 @@ __device__ __forceinline__ bool block_coords(const ConvArgs& p, int BM, int BN, 
   const int hi = rem / minor, lo = rem - hi * minor;
   tile_m = nfast ? hi : lo;
   tile_n = nfast ? lo + pk * pw : hi;
-  return true;
 }
 
 // Register-staged main loop (any shape).  SPLIT (fp32 mode): both operands come as hi/lo planes, a
@@ -405,7 +445,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs p, const
     if (more) store_stage(cur ^ 1);
     __syncthreads();
   }
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms,
+                        epi_flag_off(2 * STAGE * NP, BM * BN * 2 + (SPLIT ? BM * 4 : 0)));
 }
 
 // Shared epilogue of both GEMM main loops.  `lds` must hold >= BM*BN floats and be free (all waves
@@ -414,7 +455,8 @@ template <int BM, int BN, typename RowMap, int NT, int WAVES_M>
 __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
                                               f32x4 (&acc)[BN / 16 / (NT / 64 / WAVES_M)][BM / 16 / WAVES_M],
                                               uint16_t* lds, int m0, int n0, int wm, int wn, int lane, int tid,
-                                              int tile, int split, RowMap rows, float2 rms) {
+                                              int tile, int split, RowMap rows, float2 rms, int flag_off, int nsplit,
+                                              StreamK sk, int sk_first) {
   if constexpr (std::is_same_v<RowMap, LinearRows>) rows = LinearRows{m0, p.M};
   constexpr int WM = BM / WAVES_M, WN = BN / (NT / 64 / WAVES_M);
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -441,29 +483,96 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
       }
     __syncthreads();
     constexpr int GPR = BN / 8;
-    const bool partial = p.splits > 1 && split >= 0;  // (split < 0: a tail split-K launch's whole tile)
+    // 8-channel groups per thread: group i of this thread is g = tid + i * NT (row g / GPR)
+    constexpr int NG = BM * GPR / NT;
+    static_assert(NG * NT == BM * GPR, "whole groups per thread");
+    int gm[NG], gn[NG], grow[NG], gcg[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int g = tid + i * NT;
+      grow[i] = g / GPR;
+      gcg[i] = g - grow[i] * GPR;
+      gm[i] = rows(grow[i]);
+      gn[i] = n0 + gcg[i] * 8;
+      if (gn[i] >= p.N) gm[i] = -1;
+    }
+    auto grow_i = [&](int i) { return grow[i]; };
+    auto gcg_i = [&](int i) { return gcg[i]; };
+    auto gm_i = [&](int i) { return gm[i] < 0 ? 0 : gm[i]; };
+    auto gn_i = [&](int i) { return gm[i] < 0 ? 0 : gn[i]; };
+    if (nsplit < 0) nsplit = p.splits;
+    const bool streamk = sk.I > 0;
+    const bool partial = nsplit > 1 && split >= 0;  // (split < 0: a tail split-K launch's whole tile)
     const bool fused = partial && p.counters;
-    float* ws = partial ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
+    float* ws = partial && !streamk ? p.ws + static_cast<size_t>(split) * p.M * p.N : nullptr;
+    // byte offset of group i in partial slab `slab` (stream-K: tile-local [BM][BN] slabs)
+    auto part_off = [&](int slab, int i) -> unsigned {
+      return streamk ? static_cast<unsigned>((static_cast<size_t>(slab) * BM * BN + grow_i(i) * BN + gcg_i(i) * 8) * 4)
+                     : static_cast<unsigned>(((static_cast<size_t>(slab) * p.M + gm_i(i)) * p.N + gn_i(i)) * 4);
+    };
     const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(p.ws);
-    for (int g = tid; g < BM * GPR; g += NT) {
-      const int row = g / GPR;
-      const int cg = g - row * GPR;
-      const int m = rows(row);
-      const int n = n0 + cg * 8;
-      if (m < 0 || n >= p.N) continue;
-      const float4 a = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg) ^ (row & (CPR - 1))) << 2));
-      const float4 b = *reinterpret_cast<const float4*>(st + row * BN + (((2 * cg + 1) ^ (row & (CPR - 1))) << 2));
+    auto stage8 = [&](int i, float4& a, float4& b) {
+      a = *reinterpret_cast<const float4*>(st + grow[i] * BN + (((2 * gcg[i]) ^ (grow[i] & (CPR - 1))) << 2));
+      b = *reinterpret_cast<const float4*>(st + grow[i] * BN + (((2 * gcg[i] + 1) ^ (grow[i] & (CPR - 1))) << 2));
+    };
+    // Groups go in chunks of CH: the chunk's residual loads (and, last arriver, each split's partial
+    // loads) are all in flight before the first of them is used, so a chunk costs one round trip
+    // instead of one per group -- with few enough registers held that the main loop's occupancy is
+    // unchanged.
+    constexpr int CH = NG < 2 ? NG : 2;
+    uint4 rr[CH][2];
+    auto load_res = [&](int c0) {
+      if (!p.res) return;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int i = c0 + j;
+        const size_t o = static_cast<size_t>(gm_i(i)) * p.N + gn_i(i);
+        rr[j][0] = *reinterpret_cast<const uint4*>(p.res + o);
+        rr[j][1] = p.split ? *reinterpret_cast<const uint4*>(p.res + p.oplane + o) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    auto finish = [&](int c0, int j, float* v) {
+      const int i = c0 + j;
+      float r[8];
+      if (p.res) {
+        unpack8(rr[j][0], r);
+        if (p.split) {
+          float l[8];
+          unpack8(rr[j][1], l);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) r[t] += l[t];
+        }
+      }
+      epilogue8(p, gm[i], gn[i], v, rowc ? rowc + 2 * grow[i] : nullptr, p.res ? r : nullptr);
+    };
+    if (!partial) {
+#pragma unroll
+      for (int c0 = 0; c0 < NG; c0 += CH) {
+        load_res(c0);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          if (gm[c0 + j] < 0) continue;
+          float4 a, b;
+          stage8(c0 + j, a, b);
+          float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          finish(c0, j, v);
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      if (gm[i] < 0) continue;
+      float4 a, b;
+      stage8(i, a, b);
       if (fused) {
-        const unsigned off = static_cast<unsigned>(((static_cast<size_t>(split) * p.M + m) * p.N + n) * 4);
+        const unsigned off = part_off(streamk ? sk.slab(split, tile) : split, i);
         st4_sc1(wsr, off, a);
         st4_sc1(wsr, off + 16, b);
-      } else if (partial) {
-        float* o = ws + static_cast<size_t>(m) * p.N + n;
+      } else {
+        float* o = ws + static_cast<size_t>(gm[i]) * p.N + gn[i];
         *reinterpret_cast<float4*>(o) = a;
         *reinterpret_cast<float4*>(o + 4) = b;
-      } else {
-        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        epilogue8(p, m, n, v, rowc ? rowc + 2 * row : nullptr);
       }
     }
     if (!fused) return;
@@ -479,11 +588,14 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
     // the acquire stays; only the last arriver pays it.  The loads stay sc1 (L2-served) as well.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(lds);  // staging tile is dead now: reuse it for the broadcast
+    // the broadcast word: past the staging tile where the LDS has room (the last arriver then takes
+    // its own partial from the staging tile), else in it -- inside the same LDS array either way
+    const bool own_lds = flag_off >= 0;
+    int* flag = reinterpret_cast<int*>(own_lds ? lds + flag_off : lds);
     if (tid == 0) {
       int* ctr = p.counters + tile;
       const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == p.splits - 1;
+      const int last = prev == nsplit - 1;
       if (last) {
         __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -493,21 +605,39 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
     }
     __syncthreads();
     if (!*flag) return;
-    const unsigned slab = static_cast<unsigned>(static_cast<size_t>(p.M) * p.N * 4);  // bytes
-    for (int g = tid; g < BM * GPR; g += NT) {
-      const int row = g / GPR;
-      const int cg = g - row * GPR;
-      const int m = rows(row);
-      const int n = n0 + cg * 8;
-      if (m < 0 || n >= p.N) continue;
-      const unsigned src = static_cast<unsigned>((static_cast<size_t>(m) * p.N + n) * 4);
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int s = 0; s < p.splits; ++s) {
-        const float4 a = ld4_sc1(wsr, src + s * slab), b = ld4_sc1(wsr, src + s * slab + 16);
-        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    // Sum in split order (bit-identical to the two-kernel form): per chunk and split ONE round of
+    // loads for the chunk's groups; this block's own partial comes from its staging tile.
+    const int own = streamk ? split - sk_first : split;  // this block's place in the summation order
+#pragma unroll
+    for (int c0 = 0; c0 < NG; c0 += CH) {
+      load_res(c0);
+      float v[CH][8];
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[j][t] = 0.f;
+      for (int s = 0; s < nsplit; ++s) {
+        const int sl = streamk ? sk.slab(sk_first + s, tile) : s;
+        float4 cur[CH][2];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          if (s == own && own_lds) {
+            stage8(c0 + j, cur[j][0], cur[j][1]);
+          } else {
+            const unsigned o = part_off(sl, c0 + j);
+            cur[j][0] = ld4_sc1(wsr, o);
+            cur[j][1] = ld4_sc1(wsr, o + 16);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          v[j][0] += cur[j][0].x; v[j][1] += cur[j][0].y; v[j][2] += cur[j][0].z; v[j][3] += cur[j][0].w;
+          v[j][4] += cur[j][1].x; v[j][5] += cur[j][1].y; v[j][6] += cur[j][1].z; v[j][7] += cur[j][1].w;
+        }
       }
-      epilogue8(p, m, n, v, rowc ? rowc + 2 * row : nullptr);
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (gm[c0 + j] >= 0) finish(c0, j, v[j]);
     }
     return;
   }
@@ -619,7 +749,9 @@ constexpr int kBnlMaxK = 2048;  // pre-activation on load: channels staged in LD
 // SPLIT (fp32 mode): each stage holds [A_hi][B_hi][A_lo][B_lo]; the lo tiles are DMA'd from the
 // planes wplane / xplane elements after the hi ones (zero-page rows stay zero-page), and every
 // fragment pair takes three MFMAs (hi*hi + lo*hi + hi*lo).
-template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false, int BKS = BK>
+// SK: the stream-K form (ConvArgs::sk > 0), a separate instantiation so that the plain kernels keep
+// their register allocation (the segment walk around the body cost ~50 VGPRs in the same kernel).
+template <int BM, int BN, int MODE, int STAGES, bool BNL = false, bool SPLIT = false, int BKS = BK, bool SK = false>
 __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const int kt_per_split) {
   static_assert(BKS == 64 || BKS == 32, "K-step width");
   constexpr int CPR = BKS / 8;        // 16-byte chunks per LDS row
@@ -644,13 +776,12 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  int tile_m, tile_n, split, tile;
-  if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk_total = p.Kpad / BKS;
-  // kt_per_split counts 64-wide K-steps; split < 0: a whole tile of a tail split-K launch
-  const int kt_begin = split < 0 ? 0 : split * kt_per_split * KR;
-  const int kt_end = split < 0 ? nk_total : min(nk_total, kt_begin + kt_per_split * KR);
+  // One output tile's K-steps [kt_begin, kt_end): the whole kernel for a plain / split-K launch,
+  // one segment of the block's range for a stream-K launch (nsplit, sk, sk_first: tile_epilogue).
+  auto run = [&](int tile_m, int tile_n, int split, int tile, int kt_begin, int kt_end, int nsplit, StreamK sk,
+                 int sk_first) {
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int nk = kt_end - kt_begin;
   // pre-activation on load: this slice's per-channel scale/shift in LDS (K = channels for 1x1)
   float* bnl = reinterpret_cast<float*>(lds + LDS_ELEMS);  // BNL only: [scale | shift] x kBnlMaxK
@@ -870,7 +1001,48 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(const ConvArgs p, const 
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS
-  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms);
+  tile_epilogue<BM, BN>(p, acc, lds, m0, n0, wm, wn, lane, tid, tile, split, LinearRows{0, 0}, rms,
+                        epi_flag_off(LDS_ELEMS, EPI_ELEMS), nsplit, sk, sk_first);
+  };
+
+  if constexpr (SK) {
+    // Stream-K (ConvArgs::sk): the grid's P blocks split the T x nk_total (tile, K-step) iterations
+    // evenly; block id (XCD-remapped, so consecutive ranges -- a tile's contributors -- share an XCD)
+    // walks its range tile by tile: a tile inside the range runs whole with the direct epilogue, a
+    // cut one leaves a partial for the tile's last arriving contributor (tile_epilogue).  (One call
+    // site of `run`, so the body is inlined once.)
+    const int ntn = (p.N + BN - 1) / BN;
+    const int Ml = p.live ? min(p.M, static_cast<int>(*p.live) * p.Ho * p.Wo) : p.M;
+    const int ntm = (Ml + BM - 1) / BM;
+    StreamK sk;
+    sk.nk = nk_total;
+    sk.I = static_cast<long long>(ntm) * ntn * nk_total;
+    sk.P = static_cast<int>(gridDim.x);
+    const int nb = sk.P, b = blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7;
+    const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+    long long it = sk.start(id);
+    const long long end = sk.start(id + 1);
+    for (bool first_seg = true; it < end; first_seg = false) {
+      const int tile = static_cast<int>(it / nk_total);
+      const long long tb = static_cast<long long>(tile) * nk_total, te = tb + nk_total;
+      const int kt_begin = static_cast<int>(it - tb);
+      const int kt_end = static_cast<int>((end < te ? end : te) - tb);
+      const int first = sk.owner(tb), last = sk.owner(te - 1);
+      int tile_m, tile_n;
+      tile_mn(p, ntm, ntn, tile, tile_m, tile_n);
+      it += kt_end - kt_begin;
+      if (!first_seg) __syncthreads();  // every wave done with the previous segment's LDS
+      run(tile_m, tile_n, first == last ? -1 : id, tile, kt_begin, kt_end, last - first + 1, sk, first);
+    }
+  } else {
+    int tile_m, tile_n, split, tile;
+    if (!block_coords(p, BM, BN, tile_m, tile_n, split, tile)) return;  // whole block, before any barrier
+    // kt_per_split counts 64-wide K-steps; split < 0: a whole tile of a tail split-K launch
+    const int kt_begin = split < 0 ? 0 : split * kt_per_split * KR;
+    const int kt_end = split < 0 ? nk_total : min(nk_total, kt_begin + kt_per_split * KR);
+    run(tile_m, tile_n, split, tile, kt_begin, kt_end, -1, StreamK{}, 0);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1024,7 +1196,8 @@ __global__ __launch_bounds__(256) void conv3x3_spatial_kernel(const ConvArgs p, 
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS
-  tile_epilogue<BM, BN>(p, acc, lds, 0, n0, wm, wn, lane, tid, tile, split, SpatialRows{b, ty0, tx0, p.Ho, p.Wo});
+  tile_epilogue<BM, BN>(p, acc, lds, 0, n0, wm, wn, lane, tid, tile, split, SpatialRows{b, ty0, tx0, p.Ho, p.Wo},
+                        float2{0.f, 0.f}, epi_flag_off(LDS_ELEMS, BM * BN * 2));
 }
 
 template <int BM, int BN, int STAGES, int BKS = BK>
@@ -1041,6 +1214,26 @@ bool launch_glds(int mode, dim3 grid, hipStream_t s, const ConvArgs& b, int kt_p
         hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 3, STAGES, false, false, BKS>), grid, dim3(256), 0, s, b, kt_per);
       } else {
         return false;
+      }
+      return true;
+    } else {
+      return false;
+    }
+  }
+  if (b.sk > 0) {  // stream-K: 1- and 2-stage loops, no pre-activation on load
+    if constexpr (STAGES <= 2 && BKS == BK) {
+      if (b.in_scale) return false;
+      if (b.split) {
+        if constexpr (STAGES * (BM + BN) * BKS * 4 <= 160 * 1024) {
+          if (mode0) hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, true, BKS, true>), grid, dim3(256), 0, s, b, kt_per);
+          else hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, true, BKS, true>), grid, dim3(256), 0, s, b, kt_per);
+        } else {
+          return false;
+        }
+      } else if (mode0) {
+        hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 0, STAGES, false, false, BKS, true>), grid, dim3(256), 0, s, b, kt_per);
+      } else {
+        hipLaunchKernelGGL((conv_glds_kernel<BM, BN, 2, STAGES, false, false, BKS, true>), grid, dim3(256), 0, s, b, kt_per);
       }
       return true;
     } else {
@@ -1085,9 +1278,18 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
   // fused split-K reduction needs a zeroed counter per output tile
   const bool fused = eff > 1 && a.counters && tiles <= a.counters_n;
   if (!fused) b.counters = nullptr;
+  if (a.sk > 0) {
+    // stream-K: LDS-DMA loops only, in-kernel reduction only (a counter per tile), P blocks
+    if (variant < 1 || variant > 5 || !a.counters || tiles > a.counters_n || !a.ws || a.N % 8 || a.tail > 0 ||
+        a.in_scale || a.row_parts || a.stats_out)
+      return hipErrorInvalidValue;
+    b.counters = a.counters;
+    b.splits = 1;
+  }
   // LayerNorm statistics (ConvArgs::stats_out / row_parts): rows GEMMs, not the spatially tiled 3x3
   if ((a.stats_out || a.row_parts) && variant == 6) return hipErrorInvalidValue;
   dim3 grid(tiles, eff);
+  if (a.sk > 0) grid = dim3(a.sk, 1);
   if (a.tail > 0) {
     // tail split-K: 1-D grid sized for the worst live batch (the whole-tile count steps down at
     // every multiple of `tail`, so fewer live tiles can need more blocks)
@@ -1172,7 +1374,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s, int variant) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 1, 4>), grid, dim3(256), 0, s, b, kt_per);
   }
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || eff == 1 || fused) return e;
+  if (e != hipSuccess || eff == 1 || fused || a.sk > 0) return e;
   const long long groups = static_cast<long long>(b.M) * (b.N / 8);
   const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
   hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
@@ -1323,7 +1525,7 @@ inline hipError_t launch_wide(const ConvArgs& a, hipStream_t s) {
   if (!fused) b.counters = nullptr;
   hipLaunchKernelGGL(gemm_wide_kernel<BN>, dim3(tiles, eff), dim3(512), 0, s, b, kt_per);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || eff == 1 || fused) return e;
+  if (e != hipSuccess || eff == 1 || fused || a.sk > 0) return e;
   const long long groups = static_cast<long long>(b.M) * (b.N / 8);
   const int g = static_cast<int>(std::min<long long>((groups + 255) / 256, 8192));
   hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(g), dim3(256), 0, s, b);
@@ -1341,6 +1543,8 @@ hipError_t launch_tile_64x64(const ConvArgs& a, hipStream_t s, int variant);
 hipError_t launch_tile_wide(const ConvArgs& a, hipStream_t s, int tile);
 // conv_skinny.hip: variant 8 (<= 32 dense rows, 16 channels per block, K split over 8 waves)
 hipError_t launch_tile_skinny(const ConvArgs& a, hipStream_t s, int tile);
+// conv_quad.hip: variant 9 (four 8x8 sub-tiles x 64 channels per block, 3x3 only)
+hipError_t launch_tile_quad(const ConvArgs& a, hipStream_t s, int tile);
 
 }  // namespace igemm
 }  // namespace kern

@@ -91,7 +91,17 @@ struct ConvArgs {
   // a sliver instead of two rounds on the busiest CUs (tail = 256: one tile per CU per round).  0 =
   // uniform split-K.
   int tail = 0;
+  // Stream-K (LDS-DMA loops, variants 1-5; needs counters >= tiles and ws >= streamk_workspace_bytes):
+  // sk = P > 0 launches exactly P blocks that split the T x K-steps iterations of all tiles evenly
+  // (P = 256: one block per CU) instead of one block per (tile, split) -- a grid of 296 tiles then
+  // costs 1.16 tiles per CU, not two on the busiest CUs.  Cut tiles are reduced in-kernel by their
+  // last arriving contributor, in block order (bitwise repeatable for a given P).
+  int sk = 0;
 };
+
+// Split-K workspace of a stream-K launch (ConvArgs::sk = P blocks, BM x BN tiles): two partial
+// slabs per block.
+inline size_t streamk_workspace_bytes(int P, int bm, int bn) { return static_cast<size_t>(P) * 2 * bm * bn * sizeof(float); }
 
 // A launch config = tile + NUM_TILES * variant; variant 0 = register-staged main loop (any shape),
 // 1..4 = LDS-DMA ring of 2, 3, 4, 6 stages (variants 1-4: 1x1 with K % 64 == 0, or Cin % 64 == 0;
@@ -104,7 +114,10 @@ struct ConvArgs {
 // (conv_igemm_impl.h gemm_wide_kernel); the other tiles of variant 7 are not instantiated.
 // Variant 8 = the skinny dense GEMM (<= 32 rows, e.g. a classifier head at the serving batch):
 // tile 0 only (conv_skinny.hip), 16 channels per block, K split over 8 waves, no split-K.
-enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 36 };
+// Variant 9 = the four-tile 3x3 kernel (conv_quad.hip): four 8x8 sub-tiles x 64 channels per block,
+// one sub-tile per wave, the tap's weights loaded once for 256 pixels (3x3/s1/p1, Cin % 64 == 0;
+// tile 3 only, cfg 39).
+enum TileCfg { TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x128 = 2, TILE_64x64 = 3, NUM_TILES = 4, NUM_CFGS = 40 };
 // BM (pixels) x BN (channels) of a config.
 void tile_dims(int cfg, int& bm, int& bn);
 // Heuristic (tile, splits) choice for a problem shape (used when not autotuned).

@@ -318,6 +318,16 @@ bool DpGroup::push_sub(const DpSub& s) {
   return !ctl_->stop.load();
 }
 
+int DpGroup::queued_items() const {
+  int n = 0;
+  for (int r = 0; r < world_; ++r) {
+    auto& q = ctl_->subq[r];
+    const uint32_t h = q.head.load(std::memory_order_acquire);
+    for (uint32_t t = q.tail.load(std::memory_order_relaxed); t != h; ++t) n += q.slots[t % kDpSubRing].n;
+  }
+  return n;
+}
+
 int DpGroup::peek_sub_items() const {
   int best = -1;
   uint64_t best_seq = UINT64_MAX;

@@ -115,6 +115,8 @@ class DpGroup {
   bool pop_sub(DpSub& out, int& rank, int timeout_ms);
   // Leader: oldest queued sub-batch's item count without taking it (-1 when none).
   int peek_sub_items() const;
+  // Leader: items in every queued sub-batch of every rank (a snapshot; relaxed reads).
+  int queued_items() const;
 
   // ---- shared listening port (SO_REUSEPORT ingest on every rank) ----
   void publish_port(int port);

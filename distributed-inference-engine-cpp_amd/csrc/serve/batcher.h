@@ -191,7 +191,13 @@ class BatchProcessor {
       std::vector<Item> batch;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return !queue_.empty() || !running_; });
+        if (queue_.empty()) {
+          // An idle spell ends the alternation that balancing evens out: the previous batch size
+          // says nothing about a burst that arrives after it.
+          const auto w0 = std::chrono::steady_clock::now();
+          cv_.wait(lk, [&] { return !queue_.empty() || !running_; });
+          if (std::chrono::steady_clock::now() - w0 > kIdleReset) last_n_ = 0;
+        }
         if (!running_) return;
         if (policy_ == BatchPolicy::DEADLINE) {
           const auto deadline = queue_.front().t + timeout_;
@@ -219,7 +225,9 @@ class BatchProcessor {
         if (!running_) return;
         const size_t q = std::min(queue_.size(), max_batch_);
         size_t take = q;
-        if (balance_ && policy_ == BatchPolicy::GREEDY && last_n_ > 0 && q > last_n_) take = (q + last_n_ + 1) / 2;
+        // balanced batches: only below a full queue (a full one goes out whole, as the reference's)
+        if (balance_ && policy_ == BatchPolicy::GREEDY && last_n_ > 0 && q > last_n_ && queue_.size() < max_batch_)
+          take = (q + last_n_ + 1) / 2;
         if (size_ && take > 1) take = std::max<size_t>(1, std::min(take, size_(take)));
         if (take < q) {
           trimmed_batches_.fetch_add(1, std::memory_order_relaxed);
@@ -282,6 +290,7 @@ class BatchProcessor {
   SizeFn size_;
   bool balance_ = false;
   size_t last_n_ = 0;  // size of the previous batch (batcher thread only)
+  static constexpr std::chrono::milliseconds kIdleReset{20};  // idle wait that forgets last_n_
   std::atomic<long long> paced_ns_{0};
   std::atomic<long long> trimmed_batches_{0}, trimmed_requests_{0};
   mutable std::mutex mu_;

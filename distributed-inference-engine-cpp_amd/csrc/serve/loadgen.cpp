@@ -247,7 +247,9 @@ Json run_loadgen(const LoadgenOptions& o) {
     if (is_verify(id)) {
       const Template& t = vt[verify_k(id)];
       // 512 variants per seed residue: concurrent clients with different seeds (one per rank) never
-      // send the same verify text, so none of them is a cache hit on a shared worker
+      // send the same verify text, so none of them is a cache hit on a shared worker.  The texts
+      // repeat after 511 * inputs * verify_every requests (reported as verify_repeat_period; bench.py
+      // checks its run is shorter).
       if (sampled)
         verify_body(t, (id / o.verify_every) / static_cast<long>(vt.size()) % 511 + 1 + 512 * static_cast<long>(o.seed % 8),
                     bd.vbody);
@@ -629,6 +631,9 @@ Json run_loadgen(const LoadgenOptions& o) {
     j["mismatched"] = static_cast<long long>(nm);
     j["bad_request_id"] = static_cast<long long>(nb);
     j["max_rel_err"] = me;
+    // sampled mode: requests after which a verify text repeats (511 variants per input and seed
+    // residue), so a longer run would see repeated verify texts as cache hits
+    if (sampled) j["verify_repeat_period"] = static_cast<long long>(511) * static_cast<long long>(vt.size()) * o.verify_every;
   }
   return j;
 }

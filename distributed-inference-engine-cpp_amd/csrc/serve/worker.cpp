@@ -176,7 +176,11 @@ void WorkerNode::parse_loop() {
     if (opt_.parse_spin_us > 0) {  // WorkerOptions::parse_spin_us: poll before sleeping
       const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(opt_.parse_spin_us);
       while (parse_pending_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#else
+        std::this_thread::yield();
+#endif
     }
     {
       std::unique_lock<std::mutex> lk(parse_mu_);

@@ -362,7 +362,9 @@ def build_ln_wide(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.n
     return g.model_proto(opset=opset), {}
 
 
-def build_ln_offset(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np.ndarray]]:
+def build_ln_offset(seed: int = 0, opset: int = 17, offset: float = 60.0) -> Tuple[bytes, Dict[str, np.ndarray]]:
+    """offset: the row-constant DC offset added before the LayerNorm, in units of the rows' own
+    standard deviation (the tokens are N(0, 1))."""
     s = SPECS["ln_offset"]
     rng = _rng(seed)
     S, D, H = s["seq"], s["dim"], s["hidden"]
@@ -371,7 +373,7 @@ def build_ln_offset(seed: int = 0, opset: int = 17) -> Tuple[bytes, Dict[str, np
     h = g.node("Reshape", [x, g.const(np.array([0, S, D], np.int64), "seq_shape")], name="to_tokens")
     # a row-constant offset (the same for every channel): |mean| / std of each row ~ 60 -- the
     # cancellation case -- plus a small per-channel spread
-    off = (60.0 + 0.5 * rng.standard_normal(D)).astype(np.float32)
+    off = (offset + 0.5 * rng.standard_normal(D)).astype(np.float32)
     h = g.node("Add", [h, g.init("offset", off)], name="dc_offset")
 
     def ln(inp, name, c):

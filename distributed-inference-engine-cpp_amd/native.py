@@ -58,6 +58,7 @@ def lib() -> C.CDLL:
         sig("die_parse_infer", C.c_long, cp, C.c_long, f32p, C.c_long, errp, errp)
         sig("die_format_floats", vp, f32p, C.c_long)
         sig("die_fnv1a", C.c_uint32, cp)
+        sig("die_pick_efficient_batch", C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_double, C.c_double)
         sig("die_ring_create", vp, C.c_int)
         sig("die_ring_destroy", None, vp)
         sig("die_ring_add", None, vp, cp)
@@ -77,7 +78,7 @@ def lib() -> C.CDLL:
         sig("die_cache_put", None, vp, f32p, C.c_long, f32p, C.c_long)
         sig("die_cache_get", C.c_long, vp, f32p, C.c_long, f32p, C.c_long)
         sig("die_cache_stats", vp, vp)
-        sig("die_batcher_create", vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int)
+        sig("die_batcher_create", vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int)
         sig("die_batcher_process", C.c_int, vp, C.c_int, errp)
         sig("die_batcher_metrics", vp, vp)
         sig("die_batcher_stop", None, vp)
@@ -238,6 +239,12 @@ def unpack_nibbles(packed: bytes, n: int) -> bytes:
     return dst.raw[:n]
 
 
+def pick_efficient_batch(curve_ms, queued: int, tol: float = 0.0, margin: float = 0.02) -> int:
+    """EngineOptions::efficient_batch policy over a forward-time curve (ms at batch 1, 2, ...)."""
+    arr = (C.c_double * (len(curve_ms) + 1))(0.0, *curve_ms)
+    return lib().die_pick_efficient_batch(arr, len(curve_ms), int(queued), float(tol), float(margin))
+
+
 def fnv1a(s: str) -> int:
     return lib().die_fnv1a(s.encode())
 
@@ -321,9 +328,11 @@ class Cache:
 class TestBatcher:
     """BatchProcessor<int,int> doubling each request (unit tests)."""
 
-    def __init__(self, max_batch: int, timeout_ms: int, deadline: bool = False, delay_ms: int = 0, size_cap: int = 0):
-        """size_cap > 0: a batch-size hook (as Engine::preferred_batch) that takes at most size_cap."""
-        self.h = lib().die_batcher_create(max_batch, timeout_ms, int(deadline), delay_ms, size_cap)
+    def __init__(self, max_batch: int, timeout_ms: int, deadline: bool = False, delay_ms: int = 0, size_cap: int = 0,
+                 balance: bool = False):
+        """size_cap > 0: a batch-size hook (as Engine::preferred_batch) that takes at most size_cap;
+        balance: WorkerOptions::batch_balance."""
+        self.h = lib().die_batcher_create(max_batch, timeout_ms, int(deadline), delay_ms, size_cap, int(balance))
 
     def process(self, v: int) -> int:
         err = _err_box()

@@ -72,7 +72,8 @@ def pack_conv_weight(w, cin_store: Optional[int] = None, npad: int = 128, split:
 
 
 # launch configs of the conv kernel: tile + 4 * variant (kernels.h TileCfg)
-NUM_CFGS = 36  # kernels.h TileCfg (variant 7 = the 8-wave wide tile, cfg 28 only; variant 8 = skinny rows, cfg 32 only)
+NUM_CFGS = 40  # kernels.h TileCfg (variant 7 = the 8-wave wide tile, cfg 28 only; variant 8 = skinny rows, cfg 32 only;
+#               variant 9 = the four-tile 3x3 kernel, cfg 39 only)
 
 
 class ConvProblem:
@@ -124,14 +125,23 @@ class ConvProblem:
         self.flops = 2.0 * B * Ho * Wo * cout * cin * kh * kw
         self._L = native.kernels()
 
-    def launch(self, tile=-1, splits=1, fused_splitk=True, order=0, extra=None) -> int:
+    def launch(self, tile=-1, splits=1, fused_splitk=True, order=0, extra=None, sk=0) -> int:
         """Launch on torch's current stream; returns the hipError code (1 = config not applicable).
         order: XCD tile order (ConvArgs::order: 0 heuristic, 1 N-fastest, 2 M-fastest).
         extra: more ConvArgs fields by geometry-JSON key (device pointers as ints), e.g. the LayerNorm
-        statistics row_stats / col_sum / row_parts / stats_out and ln_eps."""
+        statistics row_stats / col_sum / row_parts / stats_out and ln_eps.
+        sk > 0: a stream-K launch of sk blocks (ConvArgs::sk; in-kernel reduction, splits ignored)."""
         g = dict(self.geom, splits=int(splits), order=int(order))
         g.update(extra or {})
-        if splits > 1:
+        if sk > 0:
+            bm, bn = [(128, 128), (128, 64), (64, 128), (64, 64)][tile % 4] if tile >= 0 else (64, 64)
+            if self.ws.numel() < sk * 2 * bm * bn:
+                return 1  # workspace too small for this P: not applicable
+            g["sk"] = int(sk)
+            g["ws"] = int(self.ws.data_ptr())
+            g["counters"] = int(self.counters.data_ptr())
+            g["counters_n"] = int(self.counters.numel())
+        elif splits > 1:
             g["ws"] = int(self.ws.data_ptr())
             if fused_splitk:
                 g["counters"] = int(self.counters.data_ptr())

@@ -2,6 +2,7 @@
 import json
 import struct
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -249,6 +250,30 @@ def test_batcher_size_hook_trims_batches(native):
     assert sum(m["sizes"]) == 20 and max(m["sizes"]) <= 3
     # with 30 ms per batch the queue outgrows the cap, so some batches were cut
     assert m["trimmed_batches"] >= 1 and m["trimmed_requests"] >= m["trimmed_batches"]
+    b.stop()
+
+
+def test_batcher_balance_keeps_full_queue_whole(native):
+    """batch_balance: after a batch of 1, a FULL queue of max_batch goes out whole, as the
+    reference's take-up-to-max_batch does; only a partial queue is balanced against the last batch."""
+    b = native.TestBatcher(max_batch=8, timeout_ms=20, deadline=False, delay_ms=60, balance=True)
+    results = [None] * 9
+
+    def run(i):
+        results[i] = b.process(i)
+
+    first = threading.Thread(target=run, args=(0,))
+    first.start()
+    time.sleep(0.02)  # request 0 is in its 60 ms batch; the burst queues behind it
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, 9)]
+    for t in ts:
+        t.start()
+    for t in [first] + ts:
+        t.join()
+    assert results == [2 * i for i in range(9)]
+    m = b.metrics()
+    assert m["sizes"] == [1, 8], m["sizes"]
+    assert m["trimmed_batches"] == 0
     b.stop()
 
 

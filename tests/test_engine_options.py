@@ -44,3 +44,25 @@ def test_hip_hw_queue_env_rule():
         die_amd.configure_hip_env(env)
         assert env["GPU_MAX_HW_QUEUES"] == want, (given, env)
         assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_efficient_batch_policy(native):
+    """EngineOptions::efficient_batch (ADVICE r5): a batch is cut below the queue only when a smaller
+    size is cheaper per image by more than the margin.  A flat curve (one bucket, replay noise) never
+    trims; a real step (ResNet50 fp32: B = 21 spills a tile round, +19 % for +5 % images) does."""
+    # one bucket of 24 whose forward costs the same at every live size, +-0.4 % noise
+    rng = np.random.default_rng(1)
+    flat = [1.40 * (1.0 + 0.004 * rng.standard_normal()) for _ in range(24)]
+    for q in range(1, 25):
+        assert native.pick_efficient_batch(flat, q) == q
+    # per-image time falling with B, then a step at 21 (profiles/r5_batch_curve.md shape)
+    step = [0.30 + 0.045 * b for b in range(1, 21)] + [1.46, 1.47, 1.455, 1.44]
+    assert native.pick_efficient_batch(step, 20) == 20
+    assert native.pick_efficient_batch(step, 21) == 20  # 69.5 vs 60.0 us per image: cut
+    assert native.pick_efficient_batch(step, 23) == 20  # 63.3 vs 60.0: cut
+    assert native.pick_efficient_batch(step, 24) == 24  # the bucket end is as cheap as B = 20
+    # a step of 1.5 % per image is inside the 2 % margin: no cut; margin 0 (the strict argmin) cuts
+    small = [1.0 * b for b in range(1, 20)] + [20 * 1.015]
+    assert native.pick_efficient_batch(small, 20, margin=0.02) == 20
+    assert native.pick_efficient_batch(small, 20, margin=0.0) == 19
+    assert native.pick_efficient_batch(step, 0) == 1 and native.pick_efficient_batch(step, 99) == 24

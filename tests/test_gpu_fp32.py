@@ -103,6 +103,7 @@ def test_split_conv_every_variant_and_epilogue(native, shape, splits, fused):
     assert any(c < 4 for c in ran) and any(c >= 4 for c in ran), ran
     if k == 3 and s == 1:
         assert 27 in ran, ran  # spatially tiled 3x3 kernel (variant 6)
+        assert 39 in ran, ran  # four-tile 3x3 kernel (variant 9)
 
 
 def test_split_conv_repeatable_bitwise(native):

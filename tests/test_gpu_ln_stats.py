@@ -73,13 +73,18 @@ def test_epilogue_stats_producer_all_configs(native):
     assert ran >= 20
 
 
-@pytest.mark.parametrize("N", [768, 3072])
-def test_epilogue_stats_reader_all_configs(native, N):
+@pytest.mark.parametrize("N,offset", [(768, 0.0), (3072, 0.0), (768, 10.0), (768, 30.0), (768, 100.0)])
+def test_epilogue_stats_reader_all_configs(native, N, offset):
+    """offset > 0: every row also carries a DC offset of `offset` row sigmas (0.7)
+    with a random sign -- the fold's own error (against fp64 on the stored rows) stays at the fp32 bar."""
     torch = _torch()
     from die_amd.ops import kernels as K
 
     g = torch.Generator().manual_seed(5)
     xr = torch.randn(M, C, generator=g) * 0.7 + torch.randn(M, 1, generator=g) * 2.0  # row offsets
+    if offset:
+        sign = torch.where(torch.rand(M, 1, generator=g) < 0.5, -1.0, 1.0)
+        xr = xr + sign * offset * 0.7
     gamma = 1.0 + 0.1 * torch.randn(C, generator=g)
     beta = 0.1 * torch.randn(C, generator=g)
     w = torch.randn(N, C, generator=g) / C ** 0.5
@@ -125,7 +130,12 @@ def test_epilogue_stats_reader_all_configs(native, N):
         # the folded form's own error grows with |mean| / std of the rows (here ~3); the two ways of
         # delivering the statistics agree far more closely than that
         # (outputs are stored as hi + lo bf16 planes: ~2^-17 relative steps)
-        if not (e_stats < 5e-5 and e_parts < 5e-5 and rows.max() < 3e-5 and rep == 0.0):
+        # with a DC offset the fold's own error grows with |mean| / std: its GEMM accumulates x.W' at
+        # the offset's magnitude in fp32 before rstd * (acc - mean * colsum) cancels it (measured on
+        # MI355X: < 5e-5 at 10 sigma, 1.14e-4 at 30, 4.54e-4 at 100 -- ~4.5e-6 per sigma of offset,
+        # profiles/r6_fold_layernorm_offsets.md); the bound asserted is that law with 20 % margin
+        bar = 5e-5 + 5.5e-6 * offset
+        if not (e_stats < bar and e_parts < bar and rows.max() < 3e-5 + 1e-6 * offset and rep == 0.0):
             top = np.argsort(rows)[-4:][::-1]
             bad.append((tile, splits, fused, "%.2e %.2e" % (e_stats, e_parts), "repeat %.2e" % rep,
                         [(int(r), "%.2e" % rows[r]) for r in top]))

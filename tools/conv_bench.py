@@ -51,6 +51,12 @@ def main():
     ap.add_argument("--ref", action="store_true", help="also time torch.matmul (hipBLASLt) on the GEMM view "
                     "and F.conv2d (MIOpen, channels_last) for calibration")
     ap.add_argument("--split", action="store_true", help="fp32 mode: split (hi, lo) planes, 3 MFMAs per pair")
+    ap.add_argument("--cold", action="store_true", help="time each launch alone behind a 96 MB L2 scrub "
+                    "(eager, events around the conv only): operands come from the Infinity Cache, as inside a forward")
+    ap.add_argument("--cfgs", default="", help="comma list of launch configs to try (default: all)")
+    ap.add_argument("--splits", default="1,2,4,8,16", help="comma list of split-K factors")
+    ap.add_argument("--sk", default="", help="comma list of stream-K block counts to try too (ConvArgs::sk)")
+    ap.add_argument("--dump", action="store_true", help="print every candidate's time (with --only)")
     ap.add_argument("--json", default="")
     ap.add_argument("--md", default="")
     a = ap.parse_args()
@@ -61,6 +67,7 @@ def main():
 
     torch.manual_seed(0)
     dev = "cuda"
+    scrub = torch.ones(24 << 20, device=dev) if a.cold else None  # 96 MB
     results = []
     for name, count, cin, cout, k, stride, H, epi in resnet50_shapes():
         if a.only and a.only not in name:
@@ -82,24 +89,38 @@ def main():
         pr = K.ConvProblem(x, w, max_splits=16, split=a.split, **kw)
         nk = (cin * k * k + 63) // 64
         cands = []
-        for cfg in range(K.NUM_CFGS):
-            for sp in (1, 2, 4, 8, 16):
+        cfgs = [int(c) for c in a.cfgs.split(",")] if a.cfgs else range(K.NUM_CFGS)
+        for cfg in cfgs:
+            sks = [int(v) for v in a.sk.split(",")] if a.sk else []
+            for sp in [int(v) for v in a.splits.split(",")] + [-v for v in sks]:
                 if sp > nk or (sp > 1 and cout % 8):
                     continue
                 for fused, order in [(f, o) for f in ((False, True) if sp > 1 else (False,)) for o in (1, 2)]:
-                    rc = pr.launch(cfg, sp, fused, order)
+                    rc = pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
                     if rc == 1:
                         continue
                     if rc != 0:
                         raise RuntimeError("launch failed %d" % rc)
                     torch.cuda.synchronize()
+                    ts = []
+                    if a.cold:
+                        for _ in range(a.trials):
+                            scrub.mul_(1.0001)
+                            e0 = torch.cuda.Event(enable_timing=True)
+                            e1 = torch.cuda.Event(enable_timing=True)
+                            e0.record()
+                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
+                            e1.record()
+                            e1.synchronize()
+                            ts.append(e0.elapsed_time(e1) * 1000.0)
+                        cands.append((statistics.median(ts), cfg, sp, fused, order))
+                        continue
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g):
                         for _ in range(a.reps):
-                            pr.launch(cfg, sp, fused, order)
+                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
                     g.replay()
                     torch.cuda.synchronize()
-                    ts = []
                     for _ in range(a.trials):
                         e0 = torch.cuda.Event(enable_timing=True)
                         e1 = torch.cuda.Event(enable_timing=True)
@@ -111,6 +132,11 @@ def main():
                     del g
                     cands.append((statistics.median(ts), cfg, sp, fused, order))
         cands.sort()
+        if a.dump:
+            for us, cfg, sp, fused, order in cands:
+                print("  %-14s cfg %2d (v%d tile %d) %s%s order %d: %7.2f us" % (
+                    name, cfg, cfg // 4, cfg % 4, "split %2d" % sp if sp > 0 else "sk %4d" % -sp,
+                    "f" if fused else " ", order, us), flush=True)
         ref = {}
         if a.ref:
             def timed(fn):

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--tune-in-graph", action="store_true", help="EngineOptions::tune_in_graph")
     ap.add_argument("--no-tune-orders", action="store_true", help="heuristic XCD tile order only (EngineOptions::tune_orders)")
     ap.add_argument("--tune-tail", action="store_true", help="tail split-K candidates too (EngineOptions::tune_tail)")
+    ap.add_argument("--tune-streamk", type=int, default=-1, help="EngineOptions::tune_streamk (1 / 0; -1 default)")
     ap.add_argument("--conv-order", type=int, default=0, help="EngineOptions::conv_order (XCD tile order override)")
     ap.add_argument("--no-ln-stats-epilogue", action="store_true",
                     help="LayerNorm statistics launches instead of producer-epilogue partials (EngineOptions::ln_stats_epilogue)")
@@ -54,7 +55,8 @@ def main():
                       splitk_fused_margin=a.splitk_fused_margin, splitk_two_kernel=a.splitk_two_kernel,
                       fuse_stem_pool=not a.no_fuse_stem_pool, fuse_gap_fc=a.fuse_gap_fc, fold_layernorm=not a.no_fold_layernorm,
                       ln_stats_epilogue=not a.no_ln_stats_epilogue, tune_in_graph=a.tune_in_graph, conv_order=a.conv_order,
-                      tune_orders=not a.no_tune_orders, tune_tail=a.tune_tail)
+                      tune_orders=not a.no_tune_orders, tune_tail=a.tune_tail,
+                      **({} if a.tune_streamk < 0 else {"tune_streamk": bool(a.tune_streamk)}))
     p = e.profile(a.batch, a.iters)
     info = e.refresh_info()
     e.close()
