@@ -5,18 +5,20 @@
 // tile, so every 64 pixels re-read the whole 3x3 weight slab of their 64 output channels -- at
 // B = 24 a stage-3 3x3 moves ~230 MB of weights for 5 MB of activations, and each of its four waves
 // reads 8 LDS fragments for 12 MFMAs.  Here ONE block owns four 8x8 sub-tiles (a whole 14x14 image,
-// or four 7x7 images) x 64 output channels, and wave w computes sub-tile w entirely (64 pixels x 64
-// channels, 16 accumulators):
+// or four 7x7 images) x 64 output channels; its 8 waves (two per SIMD, so one wave's LDS reads and
+// waits hide under the other's MFMAs) each compute half a sub-tile (32 pixels x 64 channels):
 //   * the weights of a tap (64 channels x 64 K, 16 KiB in fp32 split mode) are loaded once for 256
 //     pixels instead of 64 -- 4x fewer weight bytes per output;
-//   * per 32-deep K substep a wave reads 16 fragments (4 weight + 4 pixel, hi and lo) for 48 MFMAs
+//   * per 32-deep K substep a wave reads 12 fragments (4 weight + 2 pixel, hi and lo) for 24 MFMAs
 //     (was 8 for 12);
-//   * the next tap's weights stream into the other half of a double buffer under this tap's MFMAs
-//     (one barrier per tap; the spatial kernel waited for every tap's DMA with nothing in flight).
+//   * the weights of the next two taps stream into a 3-deep ring under this tap's MFMAs (one barrier
+//     per tap, counted vmcnt; the spatial kernel waited for every tap's DMA with nothing in flight --
+//     a 2-deep ring measured 38.7 us on the stage-3 3x3 at B = 24, against 32.2 for the spatial
+//     kernel: one tap of MFMAs (0.64 us) does not cover a loaded weight fetch).
 // Patch LDS layout and swizzle are the spatial kernel's (patch_swz): sub-tile w's 10x10 input patch
 // of the current 64-channel slice sits at patch + w * SUB, 128 B per pixel, and the rows a wave reads
 // per fragment are the same pairs {0,1} .. {6,7} (+ dy) the swizzle tables were searched for.
-// LDS: 4 x 26 KiB patches + 2 x 16 KiB weights = 136 KiB (one block per CU; split mode).  Split-K
+// LDS: 4 x 26 KiB patches + 3 x 16 KiB weights = 152 KiB (one block per CU; split mode).  Split-K
 // over channel slices with the shared fused reduction (tile_epilogue, 256-row tile, 4 waves on M).
 #include "conv_igemm_impl.h"
 
@@ -39,21 +41,26 @@ struct QuadRows {
   }
 };
 
+constexpr int kQuadThreads = 512;  // 8 waves: wave w = half (w & 1) of sub-tile w >> 1
+
 template <bool SPLIT>
-__global__ __launch_bounds__(256) void conv3x3_quad_kernel(const ConvArgs p, const int sl_per_split) {
+__global__ __launch_bounds__(kQuadThreads) void conv3x3_quad_kernel(const ConvArgs p, const int sl_per_split) {
   constexpr int BM = 64 * kQuadSub, BN = 64, NP = SPLIT ? 2 : 1;
   constexpr int PW = 10, NPIX = 100, PINSTR = 13;            // patch pixels; 1 KiB (8-pixel) DMA pieces
   constexpr int PPLANE = PINSTR * 8 * 64, APLANE = BN * BK;  // elements per plane
   constexpr int SUB = NP * PPLANE;                           // one sub-tile's patch (both planes)
   constexpr int PATCH = kQuadSub * SUB, WBUF = NP * APLANE;
   constexpr int EPI = BM * BN * 2;                           // f32 staging tile (bf16 elements)
-  constexpr int LDS_ELEMS = PATCH + 2 * WBUF > EPI + 2 ? PATCH + 2 * WBUF : EPI + 2;
+  constexpr int NWB = 3;                                     // weight ring depth (taps)
+  constexpr int GW = NP;                                     // weight DMA instructions per wave per tap
+  constexpr int LDS_ELEMS = PATCH + NWB * WBUF > EPI + 2 ? PATCH + NWB * WBUF : EPI + 2;
   static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
   uint16_t* const patch = lds;
   uint16_t* const wb = lds + PATCH;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = wave >> 1, half = wave & 1;
   // block -> (group of 4 sub-tiles, N-tile, channel-slice range), XCD-aware as block_coords
   const int tiles_x = (p.Wo + 7) >> 3, tiles_y = (p.Ho + 7) >> 3, tpi = tiles_x * tiles_y;
   const int Bl = p.live ? min(p.B, static_cast<int>(*p.live)) : p.B;
@@ -78,95 +85,96 @@ __global__ __launch_bounds__(256) void conv3x3_quad_kernel(const ConvArgs p, con
   const int cs0 = split * sl_per_split, cs1 = min(nsl, cs0 + sl_per_split);
 
   // this wave's sub-tile: its 10x10 patch, piece I (0..12) = pixels I*8 .. I*8+7, lane -> pixel
-  // I*8 + lane/8, physical chunk lane%8.  Offsets (elements from the tensor base, -1 = zero page)
-  // are recomputed per slice from two ints per piece.
-  const int st = tile_m * kQuadSub + wave;
+  // I*8 + lane/8, physical chunk lane%8; the sub-tile's two waves load the even / odd pieces.
+  // Offsets: elements from the tensor base (+ the swizzled chunk), -1 = zero page.
+  constexpr int NPC = (PINSTR + 1) / 2;  // pieces per wave (the odd half has one fewer)
+  const int st = tile_m * kQuadSub + sub;
   const bool st_ok = st < nst;
   const int sb = st_ok ? st / tpi : 0, stt = st_ok ? st - sb * tpi : 0;
   const int ty0 = (stt / tiles_x) * 8, tx0 = (stt - (stt / tiles_x) * tiles_x) * 8;
-  int poff[PINSTR];  // element offset of the lane's pixel (+ its swizzled chunk), -1: zero page
+  int poff[NPC];
 #pragma unroll
-  for (int I = 0; I < PINSTR; ++I) {
+  for (int i = 0; i < NPC; ++i) {
+    const int I = 2 * i + half;
     const int q = I * 8 + (lane >> 3);
     const int py = q / PW, px = q - (q / PW) * PW;
     const int iy = ty0 - 1 + py, ix = tx0 - 1 + px;
     const bool v = st_ok && q < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
     const int c = (lane & 7) ^ (q < NPIX ? patch_swz(py, px) : 0);
-    poff[I] = v ? ((sb * p.H + iy) * p.W + ix) * p.Cin + c * 8 : -1;
+    poff[i] = v ? ((sb * p.H + iy) * p.W + ix) * p.Cin + c * 8 : -1;
   }
-  uint16_t* const mypatch = patch + wave * SUB;
-  // weight DMA sources: rows wave*16 + i*8 + lane/8 of this N-tile
-  const uint16_t* asrc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    asrc[i] = p.w + static_cast<size_t>(n0 + r) * p.Kpad + c * 8;
-  }
+  uint16_t* const mypatch = patch + sub * SUB;
+  // weight DMA source: rows wave*8 + lane/8 of this N-tile (one 1 KiB piece per plane per wave)
+  const int wr = wave * 8 + (lane >> 3);
+  const uint16_t* const asrc = p.w + static_cast<size_t>(n0 + wr) * p.Kpad + (((lane & 7) ^ ((wr >> 1) & 7)) * 8);
+  const bool dma = p.probe != 1, mfma = p.probe != 2;  // ConvArgs::probe (measurement only)
   auto issue_w = [&](int cs, int tap, int buf) {
+    if (!dma) return;
     const int k0 = tap * p.Cin + cs * BK;
-    uint16_t* dst = wb + buf * WBUF;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      glds16(asrc[i] + k0, dst + (wave * (BN / 4) + i * 8) * BK);
-      if constexpr (SPLIT) glds16(asrc[i] + p.wplane + k0, dst + APLANE + (wave * (BN / 4) + i * 8) * BK);
-    }
+    uint16_t* dst = wb + buf * WBUF + wave * 8 * BK;
+    glds16(asrc + k0, dst);
+    if constexpr (SPLIT) glds16(asrc + p.wplane + k0, dst + APLANE);
   };
   auto issue_patch = [&](int cs) {
+    if (!dma) return;
 #pragma unroll
-    for (int I = 0; I < PINSTR; ++I) {
-      const bool v = poff[I] >= 0;
-      const uint16_t* src = v ? p.x + poff[I] + cs * BK : p.zeros;
+    for (int i = 0; i < NPC; ++i) {
+      const int I = 2 * i + half;
+      if (I >= PINSTR) break;  // wave-uniform
+      const bool v = poff[i] >= 0;
+      const uint16_t* src = v ? p.x + poff[i] + cs * BK : p.zeros;
       glds16(src, mypatch + I * 512);
       if constexpr (SPLIT) glds16(v ? src + p.xplane : p.zeros, mypatch + PPLANE + I * 512);
     }
   };
 
-  f32x4 acc[4][4];  // [16-channel fragment][16-pixel fragment] of the wave's 64 x 64 sub-tile
+  f32x4 acc[4][2];  // [16-channel fragment][16-pixel fragment] of the wave's 32 pixels x 64 channels
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int buf = 0;
   for (int cs = cs0; cs < cs1; ++cs) {
     if (cs != cs0) __syncthreads();  // every wave done with the previous slice's patch and weights
     issue_patch(cs);
-    issue_w(cs, 0, buf);
+    issue_w(cs, 0, 0);
+    issue_w(cs, 1, 1);
     for (int tap = 0; tap < 9; ++tap) {
-      // this tap's weights (and, at tap 0, the patch) have landed for this wave; the barrier makes
-      // them visible to all and retires every wave's reads of the buffer issued into next
-      wait_vmcnt<0>();
+      // this tap's weights (and, at tap 0, the patch) have landed for this wave -- only the next
+      // tap's weights may still be in flight; the barrier makes them visible to all and retires
+      // every wave's reads of the ring slot issued into next (read at tap - 1)
+      if (tap < 8) wait_vmcnt<GW>();
+      else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (tap < 8) issue_w(cs, tap + 1, buf ^ 1);  // under this tap's MFMAs
-      const uint16_t* A = wb + buf * WBUF;
+      if (tap < 7) issue_w(cs, tap + 2, (tap + 2) % NWB);  // two taps ahead, under this tap's MFMAs
+      const uint16_t* A = wb + (tap % NWB) * WBUF;
       const int dy = tap / 3, dx = tap - dy * 3;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < 2 && mfma; ++s) {
         const int chunk = s * 4 + (lane >> 4);
-        bf16x8 af[4], bfr[4];
-        int boff[4];
+        bf16x8 af[4], bfr[2];
+        int boff[2];
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(A + swz(i * 16 + (lane & 15), chunk));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int pix = j * 16 + (lane & 15);
+        for (int j = 0; j < 2; ++j) {
+          const int pix = (half * 2 + j) * 16 + (lane & 15);
           const int row = (pix >> 3) + dy, col = (pix & 7) + dx;
           boff[j] = (row * PW + col) * BK + ((chunk ^ patch_swz(row, col)) << 3);
           bfr[j] = *reinterpret_cast<const bf16x8*>(mypatch + boff[j]);
         }
         if constexpr (SPLIT) {
-          bf16x8 afl[4], bfl[4];
+          bf16x8 afl[4], bfl[2];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             afl[i] = *reinterpret_cast<const bf16x8*>(A + APLANE + swz(i * 16 + (lane & 15), chunk));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bfl[j] = *reinterpret_cast<const bf16x8*>(mypatch + PPLANE + boff[j]);
+          for (int j = 0; j < 2; ++j) bfl[j] = *reinterpret_cast<const bf16x8*>(mypatch + PPLANE + boff[j]);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 2; ++j) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[j], acc[i][j], 0, 0, 0);
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfl[j], acc[i][j], 0, 0, 0);
             }
@@ -174,14 +182,13 @@ __global__ __launch_bounds__(256) void conv3x3_quad_kernel(const ConvArgs p, con
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-      buf ^= 1;
     }
   }
   wait_vmcnt<0>();
   __syncthreads();  // all operand reads done before the epilogue reuses the LDS
-  tile_epilogue<BM, BN, QuadRows, 256, 4>(p, acc, lds, 0, n0, wave, 0, lane, tid, tile, split,
+  tile_epilogue<BM, BN, QuadRows, kQuadThreads, 8>(p, acc, lds, 0, n0, wave, 0, lane, tid, tile, split,
                                           QuadRows{tile_m * kQuadSub, nst, tiles_x, tpi, p.Ho, p.Wo},
                                           float2{0.f, 0.f}, epi_flag_off(LDS_ELEMS, EPI));
 }
@@ -207,8 +214,8 @@ hipError_t launch_tile_quad(const ConvArgs& a, hipStream_t s, int tile) {
   c.splits = effs;
   const bool fused = effs > 1 && a.counters && qtiles <= a.counters_n;
   if (!fused) c.counters = nullptr;
-  if (c.split) hipLaunchKernelGGL(conv3x3_quad_kernel<true>, dim3(qtiles, effs), dim3(256), 0, s, c, per);
-  else hipLaunchKernelGGL(conv3x3_quad_kernel<false>, dim3(qtiles, effs), dim3(256), 0, s, c, per);
+  if (c.split) hipLaunchKernelGGL(conv3x3_quad_kernel<true>, dim3(qtiles, effs), dim3(kQuadThreads), 0, s, c, per);
+  else hipLaunchKernelGGL(conv3x3_quad_kernel<false>, dim3(qtiles, effs), dim3(kQuadThreads), 0, s, c, per);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || effs == 1 || fused) return e;
   const long long groups = static_cast<long long>(c.M) * (c.N / 8);

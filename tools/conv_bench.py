@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--cfgs", default="", help="comma list of launch configs to try (default: all)")
     ap.add_argument("--splits", default="1,2,4,8,16", help="comma list of split-K factors")
     ap.add_argument("--sk", default="", help="comma list of stream-K block counts to try too (ConvArgs::sk)")
+    ap.add_argument("--probe", type=int, default=0, help="ConvArgs::probe: 1 = no operand DMA, 2 = no MFMAs (outputs garbage)")
     ap.add_argument("--dump", action="store_true", help="print every candidate's time (with --only)")
     ap.add_argument("--json", default="")
     ap.add_argument("--md", default="")
@@ -96,7 +97,7 @@ def main():
                 if sp > nk or (sp > 1 and cout % 8):
                     continue
                 for fused, order in [(f, o) for f in ((False, True) if sp > 1 else (False,)) for o in (1, 2)]:
-                    rc = pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
+                    rc = pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp), extra={"probe": a.probe} if a.probe else None)
                     if rc == 1:
                         continue
                     if rc != 0:
@@ -109,7 +110,7 @@ def main():
                             e0 = torch.cuda.Event(enable_timing=True)
                             e1 = torch.cuda.Event(enable_timing=True)
                             e0.record()
-                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
+                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp), extra={"probe": a.probe} if a.probe else None)
                             e1.record()
                             e1.synchronize()
                             ts.append(e0.elapsed_time(e1) * 1000.0)
@@ -118,7 +119,7 @@ def main():
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g):
                         for _ in range(a.reps):
-                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp))
+                            pr.launch(cfg, max(sp, 1), fused, order, sk=max(0, -sp), extra={"probe": a.probe} if a.probe else None)
                     g.replay()
                     torch.cuda.synchronize()
                     for _ in range(a.trials):
