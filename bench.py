@@ -532,6 +532,9 @@ def main():
                  "gpu_gap_ms_per_batch": e1.get("avg_gpu_gap_ms"), "copy_wait_ms_per_batch": e1.get("avg_copy_wait_ms"),
                  "pace_lead_ms": e1.get("avg_pace_lead_ms"), "prep_ms_per_batch": e1.get("avg_prep_ms"),
                  "leader_wait_ms_per_batch": {k: e1.get("dp_%s_wait_ms_per_batch" % k) for k in ("pop", "slot", "pace")},
+                 # dispatch fairness: leader batches any rank's sub-batch waited before riding one
+                 "dp_max_sub_wait_batches": e1.get("dp_max_sub_wait_batches"),
+                 "dp_mean_sub_wait_batches": e1.get("dp_mean_sub_wait_batches"),
                  "submit_us_avg": e1.get("staging_diag", {}).get("submit_us_avg"),
                  "pace_input_ms": e1.get("pace_input_ms"), "pace_margin_ms": e1.get("pace_margin_ms"),
                  "stages_us": {k: round(v["avg_us"], 1) for k, v in h1.get("stages_us", {}).items()}}
@@ -789,7 +792,8 @@ def _dp_child(args, hg, rank, world):
     if rank != 0:
         return None
     keep = ("value", "p50_ms", "p99_ms", "failed", "avg_dp_batch", "dp_backend", "dp_world", "dp_solo",
-            "device_ms_per_batch", "engine", "cache_hits_timed", "dp_shard_failed_items", "error")
+            "device_ms_per_batch", "engine", "cache_hits_timed", "dp_shard_failed_items", "dp_max_sub_wait_batches",
+            "dp_mean_sub_wait_batches", "error")
     res = {k: out[k] for k in keep if k in out}
     if "value" in res:
         res["requests_per_s"] = res.pop("value")

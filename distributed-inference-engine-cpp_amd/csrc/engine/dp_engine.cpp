@@ -250,6 +250,9 @@ class DpEngine : public Engine {
       j["dp_pop_wait_ms_per_batch"] = pop_wait_us_.load() / nb / 1000.0;
       j["dp_slot_wait_ms_per_batch"] = slot_wait_us_.load() / nb / 1000.0;
       j["dp_pace_wait_ms_per_batch"] = pace_wait_us_.load() / nb / 1000.0;
+      // fairness: leader batches a sub-batch of any rank waited before riding one
+      j["dp_max_sub_wait_batches"] = max_sub_wait_.load();
+      j["dp_mean_sub_wait_batches"] = static_cast<double>(sub_wait_sum_.load()) / std::max<long long>(1, subs_merged_.load());
     }
     return j;
   }
@@ -390,6 +393,11 @@ class DpEngine : public Engine {
       const int per_q = (queued + world_ - 1) / world_;
       const int target = std::max(s->n, std::min(cap, local_->preferred_batch(per_q) * world_));
       while (true) {
+        // fairness: leader batches posted between this sub-batch's queueing and the batch it rides in
+        // (the next post is batch head + 1)
+        const long long waited = static_cast<long long>(group_->posted()) - s->posted_at;
+        if (waited > max_sub_wait_.load()) max_sub_wait_ = waited;
+        sub_wait_sum_ = sub_wait_sum_.load() + waited;
         DpSubRef& ref = b->subs[b->nsub++];
         ref.rank = rank;
         ref.sub_id = s->sub_id;
@@ -579,6 +587,7 @@ class DpEngine : public Engine {
   std::thread dispatcher_, shard_thread_;
   std::atomic<long long> batches_{0}, subs_sent_{0}, subs_merged_{0}, shard_failures_{0};
   std::atomic<double> pop_wait_us_{0.0}, slot_wait_us_{0.0}, pace_wait_us_{0.0};  // leader only
+  std::atomic<long long> max_sub_wait_{0}, sub_wait_sum_{0};                       // leader only
 };
 
 }  // namespace

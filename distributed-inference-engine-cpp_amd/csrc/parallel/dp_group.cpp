@@ -311,12 +311,15 @@ bool DpGroup::push_sub(const DpSub& s) {
   slot.gseq = ctl_->gseq.fetch_add(1) + 1;
   slot.sub_id = s.sub_id;
   slot.n = s.n;
+  slot.posted_at = ctl_->head.load(std::memory_order_acquire);
   std::memcpy(slot.items, s.items, sizeof(DpItem) * static_cast<size_t>(s.n));
   q.head.store(h + 1, std::memory_order_release);
   ctl_->subs_posted.fetch_add(1, std::memory_order_release);
   futex_wake(&ctl_->subs_posted);
   return !ctl_->stop.load();
 }
+
+uint32_t DpGroup::posted() const { return ctl_->head.load(std::memory_order_acquire); }
 
 int DpGroup::queued_items() const {
   int n = 0;
@@ -367,6 +370,7 @@ bool DpGroup::pop_sub(DpSub& out, int& rank, int timeout_ms) {
       out.gseq = s.gseq;
       out.sub_id = s.sub_id;
       out.n = s.n;
+      out.posted_at = s.posted_at;
       std::memcpy(out.items, s.items, sizeof(DpItem) * static_cast<size_t>(s.n));
       q.tail.store(t + 1, std::memory_order_release);
       ctl_->subs_taken.fetch_add(1, std::memory_order_release);

@@ -62,6 +62,7 @@ struct DpSub {
   uint64_t gseq = 0;  // group-wide queue order (the dispatcher takes the oldest first)
   uint32_t sub_id = 0;
   int32_t n = 0;
+  uint32_t posted_at = 0;  // DP batches the leader had posted when this sub-batch was queued (fairness)
   DpItem items[kDpSubMax];
 };
 
@@ -117,6 +118,8 @@ class DpGroup {
   int peek_sub_items() const;
   // Leader: items in every queued sub-batch of every rank (a snapshot; relaxed reads).
   int queued_items() const;
+  // DP batches posted so far (the leader's last posted seq).
+  uint32_t posted() const;
 
   // ---- shared listening port (SO_REUSEPORT ingest on every rank) ----
   void publish_port(int port);

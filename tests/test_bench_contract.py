@@ -87,6 +87,10 @@ def test_bench_eight_ranks_torchrun_cpu(mode):
     assert out["config"]["requests"] == 2 * 25 * 8
     pr = out["per_rank"]
     assert [r["rank"] for r in pr] == list(range(8)) and all(r["failed"] == 0 for r in pr)
+    if mode == "dp":
+        # per-rank dispatch fairness: the leader takes sub-batches oldest first
+        # across ranks, so none waits more than two leader batches
+        assert out["dp_max_sub_wait_batches"] is not None and out["dp_max_sub_wait_batches"] <= 2, out
     if mode == "gateway":
         v = out["verify"]
         assert v["verified"] == 8 * 5 and v["mismatched"] == 0 and v["bad_request_id"] == 0, v

@@ -195,9 +195,9 @@ def test_conv_repeatable_bitwise(native):
                 for _ in range(5):
                     assert pr.launch(cfg, splits) == 0
                     assert torch.equal(ref.view(torch.int16), pr.out.view(torch.int16)), (cfg, splits)
-                if splits == 1 and cfg // 4 != 6:  # same K order (tap-major) per output element: bit-identical
+                if splits == 1 and cfg // 4 not in (6, 9):  # same K order (tap-major) per output element: bit-identical
                     assert torch.equal(ref.view(torch.int16), first.view(torch.int16)), cfg
-                elif splits == 1:  # spatial 3x3 kernel sums channel-slice-major: same value up to rounding
+                elif splits == 1:  # spatial / four-tile 3x3 kernels sum channel-slice-major: same value up to rounding
                     assert rel_err(ref.float(), first.float()) < 1e-2, cfg
 
 
