@@ -145,7 +145,9 @@ def main():
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
     ap.add_argument("--efficient-batch-tol", type=float, default=0.0,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
-    ap.add_argument("--efficient-batch-margin", type=float, default=0.02,
+    ap.add_argument("--batch-curve-median", action="store_true",
+                    help="EngineOptions::batch_curve_median: median of three replay groups per batch size")
+    ap.add_argument("--efficient-batch-margin", type=float, default=0.0,
                     help="EngineOptions::efficient_batch_margin: a batch is cut only when a smaller size is "
                          "cheaper per image by more than this fraction")
     ap.add_argument("--no-batch-balance", action="store_true",
@@ -297,7 +299,8 @@ def main():
                    "tune_orders": not args.no_tune_orders, "prep_on_compute": args.prep_on_compute,
                    "efficient_batch": not args.no_efficient_batch, "tune_tail": args.tune_tail,
                    **({} if args.tune_streamk < 0 else {"tune_streamk": bool(args.tune_streamk)}), "efficient_batch_tol": args.efficient_batch_tol,
-                   "efficient_batch_margin": args.efficient_batch_margin}
+                   "efficient_batch_margin": args.efficient_batch_margin,
+                   "batch_curve_median": args.batch_curve_median}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

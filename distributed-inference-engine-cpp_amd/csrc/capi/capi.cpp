@@ -108,6 +108,7 @@ EngineOptions engine_opts(const Json& j) {
   e.efficient_batch = jget<bool>(j, "efficient_batch", e.efficient_batch);
   e.efficient_batch_tol = jget<double>(j, "efficient_batch_tol", e.efficient_batch_tol);
   e.efficient_batch_margin = jget<double>(j, "efficient_batch_margin", e.efficient_batch_margin);
+  e.batch_curve_median = jget<bool>(j, "batch_curve_median", e.batch_curve_median);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));

@@ -301,6 +301,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["efficient_batch"] = o.efficient_batch;
   j["efficient_batch_tol"] = o.efficient_batch_tol;
   j["efficient_batch_margin"] = o.efficient_batch_margin;
+  j["batch_curve_median"] = o.batch_curve_median;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;

@@ -284,9 +284,13 @@ struct EngineOptions {
   // A batch is only cut below the queue when a smaller size is faster per image by more than
   // efficient_batch_margin (inside one bucket the curve is flat to within replay noise,
   // so the strict argmin let start-up noise decide whether requests wait a whole forward).
+  // Measured (same-box A/B, profiles/r6_batch_policy.md): margin 0.02 and a median-of-groups curve
+  // each let batches of 25 (a cheaper-looking bucket-26 graph) break the loop's 24-request rhythm and
+  // cost ~4-5 % of the headline, so both stay opt-in and the round-5 strict rule is the default.
   bool efficient_batch = true;
   double efficient_batch_tol = 0.0;
-  double efficient_batch_margin = 0.02;
+  double efficient_batch_margin = 0.0;
+  bool batch_curve_median = false;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;

@@ -891,8 +891,8 @@ class HipEngine : public Engine {
 
   // Device time of the captured forward at every batch size 1..max_batch (EngineOptions::
   // efficient_batch): slot 0's MAIN graph of the batch's bucket with the live count set to B, one
-  // warm-up, then the median of three timed groups of three back-to-back replays (the serving loop
-  // runs graphs back to back; the median keeps one slow group from moving a cut).
+  // warm-up and three timed back-to-back replays (the serving loop runs graphs back to back), or
+  // (EngineOptions::batch_curve_median) the median of three such groups.
   void measure_batch_curve() {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIP_CHECK(hipEventCreate(&e0));
@@ -905,16 +905,26 @@ class HipEngine : public Engine {
       *lv = use_live_ ? b : max_batch_;
       HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
       HIP_CHECK(hipGraphLaunch(g, s_compute_));
-      float grp[3];
-      for (float& ms : grp) {
+      if (opt_.batch_curve_median) {  // median of three groups of three replays
+        float grp[3];
+        for (float& ms : grp) {
+          HIP_CHECK(hipEventRecord(e0, s_compute_));
+          for (int r = 0; r < 3; ++r) HIP_CHECK(hipGraphLaunch(g, s_compute_));
+          HIP_CHECK(hipEventRecord(e1, s_compute_));
+          HIP_CHECK(hipEventSynchronize(e1));
+          HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        }
+        std::sort(grp, grp + 3);
+        batch_ms_[static_cast<size_t>(b)] = grp[1] / 3.0;
+      } else {  // the mean of three replays right behind the warm-up (round 5)
+        float ms = 0.f;
         HIP_CHECK(hipEventRecord(e0, s_compute_));
         for (int r = 0; r < 3; ++r) HIP_CHECK(hipGraphLaunch(g, s_compute_));
         HIP_CHECK(hipEventRecord(e1, s_compute_));
         HIP_CHECK(hipEventSynchronize(e1));
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        batch_ms_[static_cast<size_t>(b)] = ms / 3.0;
       }
-      std::sort(grp, grp + 3);
-      batch_ms_[static_cast<size_t>(b)] = grp[1] / 3.0;
     }
     *lv = max_batch_;
     HIP_CHECK(hipMemcpyAsync(sl.d_lens + live_index(), lv, sizeof(long long), hipMemcpyHostToDevice, s_compute_));
