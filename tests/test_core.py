@@ -253,26 +253,26 @@ def test_batcher_size_hook_trims_batches(native):
     b.stop()
 
 
-def test_batcher_balance_keeps_full_queue_whole(native):
-    """batch_balance: after a batch of 1, a FULL queue of max_batch goes out whole, as the
-    reference's take-up-to-max_batch does; only a partial queue is balanced against the last batch."""
-    b = native.TestBatcher(max_batch=8, timeout_ms=20, deadline=False, delay_ms=60, balance=True)
-    results = [None] * 9
+def test_batcher_no_shaping_at_low_load(native):
+    """Batch shaping (balance, the engine's size hook) only while the queue holds at least half the
+    max batch: a short queue behind a batch of one goes out whole (profiles/r6_batch_policy.md)."""
+    b = native.TestBatcher(max_batch=8, timeout_ms=20, deadline=False, delay_ms=60, balance=True, size_cap=2)
+    results = [None] * 4
 
     def run(i):
         results[i] = b.process(i)
 
     first = threading.Thread(target=run, args=(0,))
     first.start()
-    time.sleep(0.02)  # request 0 is in its 60 ms batch; the burst queues behind it
-    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, 9)]
+    time.sleep(0.02)
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, 4)]
     for t in ts:
         t.start()
     for t in [first] + ts:
         t.join()
-    assert results == [2 * i for i in range(9)]
+    assert results == [0, 2, 4, 6]
     m = b.metrics()
-    assert m["sizes"] == [1, 8], m["sizes"]
+    assert m["sizes"] == [1, 3], m["sizes"]
     assert m["trimmed_batches"] == 0
     b.stop()
 
