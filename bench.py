@@ -145,6 +145,8 @@ def main():
                          "below a per-image device-time step (EngineOptions::efficient_batch)")
     ap.add_argument("--efficient-batch-tol", type=float, default=0.0,
                     help="EngineOptions::efficient_batch_tol: per-image time allowed above the best smaller batch")
+    ap.add_argument("--no-efficient-batch-ends", action="store_true",
+                    help="EngineOptions::efficient_batch_ends off: any size may be a cut target, not only bucket ends")
     ap.add_argument("--batch-curve-median", action="store_true",
                     help="EngineOptions::batch_curve_median: median of three replay groups per batch size")
     ap.add_argument("--efficient-batch-margin", type=float, default=0.0,
@@ -300,7 +302,8 @@ def main():
                    "efficient_batch": not args.no_efficient_batch, "tune_tail": args.tune_tail,
                    **({} if args.tune_streamk < 0 else {"tune_streamk": bool(args.tune_streamk)}), "efficient_batch_tol": args.efficient_batch_tol,
                    "efficient_batch_margin": args.efficient_batch_margin,
-                   "batch_curve_median": args.batch_curve_median}
+                   "batch_curve_median": args.batch_curve_median,
+                   "efficient_batch_ends": not args.no_efficient_batch_ends}
     if args.mode in ("gateway", "http"):
         # N > 1 behind the gateways: worker ports that balance the consistent-hash ring (routing itself
         # unchanged; parallel/ring_balance.py) -- arbitrary ports leave the busiest of 8 workers with

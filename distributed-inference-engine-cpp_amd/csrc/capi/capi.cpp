@@ -109,6 +109,7 @@ EngineOptions engine_opts(const Json& j) {
   e.efficient_batch_tol = jget<double>(j, "efficient_batch_tol", e.efficient_batch_tol);
   e.efficient_batch_margin = jget<double>(j, "efficient_batch_margin", e.efficient_batch_margin);
   e.batch_curve_median = jget<bool>(j, "batch_curve_median", e.batch_curve_median);
+  e.efficient_batch_ends = jget<bool>(j, "efficient_batch_ends", e.efficient_batch_ends);
   e.tune_cold = jget<bool>(j, "tune_cold", e.tune_cold);
   e.tune_warm_input = jget<bool>(j, "tune_warm_input", e.tune_warm_input);
   e.splitk_fused_margin = static_cast<float>(jget<double>(j, "splitk_fused_margin", e.splitk_fused_margin));
@@ -343,8 +344,9 @@ int die_engine_run(void* p, const float* in, long B, long len, float* out, char*
 int die_pack_nibbles(const char* src, long long n, unsigned char* dst) { return pack_nibbles(src, static_cast<size_t>(n), dst) ? 1 : 0; }
 void die_unpack_nibbles(const unsigned char* src, long long n, char* dst) { unpack_nibbles(src, static_cast<size_t>(n), dst); }
 int die_engine_preferred_batch(void* p, int queued) { return static_cast<Engine*>(p)->preferred_batch(queued); }
-int die_pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin) {
-  return pick_efficient_batch(ms, max_b, queued, tol, margin);
+int die_pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin, const int* ends,
+                             int n_ends) {
+  return pick_efficient_batch(ms, max_b, queued, tol, margin, ends, n_ends);
 }
 int die_engine_text_packing(void* p) { return static_cast<Engine*>(p)->text_packing() ? 1 : 0; }
 

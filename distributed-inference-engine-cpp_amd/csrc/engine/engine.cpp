@@ -302,6 +302,7 @@ Json engine_options_json(const EngineOptions& o) {
   j["efficient_batch_tol"] = o.efficient_batch_tol;
   j["efficient_batch_margin"] = o.efficient_batch_margin;
   j["batch_curve_median"] = o.batch_curve_median;
+  j["efficient_batch_ends"] = o.efficient_batch_ends;
   j["tune_cold"] = o.tune_cold;
   j["tune_warm_input"] = o.tune_warm_input;
   j["splitk_fused_margin"] = o.splitk_fused_margin;
@@ -312,9 +313,20 @@ Json engine_options_json(const EngineOptions& o) {
   return j;
 }
 
-int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin) {
+int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin, const int* ends,
+                         int n_ends) {
   const int q = std::min(queued, max_b);
   if (!ms || q <= 1) return std::max(1, q);
+  if (ends && n_ends > 0) {  // bucket ends only: the cheapest per image, the largest within tol of it
+    double best = 1e30;
+    for (int i = 0; i < n_ends && ends[i] <= q; ++i) best = std::min(best, ms[ends[i]] / ends[i]);
+    if (best >= 1e30) return q;
+    const double lim = best * (1.0 + std::max(0.0, tol));
+    int pick = 1;
+    for (int i = 0; i < n_ends && ends[i] <= q; ++i)
+      if (ms[ends[i]] / ends[i] <= lim) pick = ends[i];
+    return pick;
+  }
   double best = 1e30;
   for (int b = 1; b <= q; ++b) best = std::min(best, ms[b] / b);
   // the whole queue unless a smaller batch is clearly cheaper per image

@@ -291,6 +291,8 @@ struct EngineOptions {
   double efficient_batch_tol = 0.0;
   double efficient_batch_margin = 0.0;
   bool batch_curve_median = false;
+  // cut only to bucket ends (the graph sizes), never to a partly empty bucket (pick_efficient_batch)
+  bool efficient_batch_ends = true;
   // Fault injection: every Nth batch this engine runs fails before reaching the
   // device (0 = off).  Drives the data-parallel shard-failure tests.
   int fail_batch_every = 0;
@@ -303,8 +305,12 @@ Json engine_options_json(const EngineOptions& o);
 // EngineOptions::efficient_batch policy over a per-batch-size forward-time curve (ms[b], b = 1..
 // max_b; ms[0] unused): with `queued` requests waiting, the batch size to dispatch.  Keeps the whole
 // queue unless some smaller size is cheaper per image by more than `margin`; then the largest size
-// within `tol` of the cheapest.  Pure (CPU-tested through the C API).
-int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin);
+// within `tol` of the cheapest.  With `ends` (the engine's graph bucket sizes, ascending) only bucket
+// ends are candidates -- the queue itself only when it is one -- so a batch never runs a bucket's
+// graph partly empty (a batch of 25 on the 26-graph broke the serving loop's 24-request rhythm,
+// profiles/r6_batch_policy.md).  Pure (CPU-tested through the C API).
+int pick_efficient_batch(const double* ms, int max_b, int queued, double tol, double margin, const int* ends = nullptr,
+                         int n_ends = 0);
 
 // Factory: HIP engine when a GPU is visible and device != cpu, else the CPU executor (the
 // reference's ORT CUDA-EP -> CPU-EP fallback, src/inference_engine.cpp:21-29, made explicit).

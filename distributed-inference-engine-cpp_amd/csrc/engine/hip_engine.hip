@@ -675,7 +675,8 @@ class HipEngine : public Engine {
   // bucket the curve is flat to within replay noise).
   int preferred_batch(int queued) const override {
     return pick_efficient_batch(batch_ms_.empty() ? nullptr : batch_ms_.data(), max_batch_, queued,
-                                opt_.efficient_batch_tol, opt_.efficient_batch_margin);
+                                opt_.efficient_batch_tol, opt_.efficient_batch_margin,
+                                opt_.efficient_batch_ends ? buckets_.data() : nullptr, static_cast<int>(buckets_.size()));
   }
 
   void synchronize() override {

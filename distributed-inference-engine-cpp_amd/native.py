@@ -58,7 +58,8 @@ def lib() -> C.CDLL:
         sig("die_parse_infer", C.c_long, cp, C.c_long, f32p, C.c_long, errp, errp)
         sig("die_format_floats", vp, f32p, C.c_long)
         sig("die_fnv1a", C.c_uint32, cp)
-        sig("die_pick_efficient_batch", C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_double, C.c_double)
+        sig("die_pick_efficient_batch", C.c_int, C.POINTER(C.c_double), C.c_int, C.c_int, C.c_double, C.c_double,
+            C.POINTER(C.c_int), C.c_int)
         sig("die_ring_create", vp, C.c_int)
         sig("die_ring_destroy", None, vp)
         sig("die_ring_add", None, vp, cp)
@@ -239,10 +240,13 @@ def unpack_nibbles(packed: bytes, n: int) -> bytes:
     return dst.raw[:n]
 
 
-def pick_efficient_batch(curve_ms, queued: int, tol: float = 0.0, margin: float = 0.02) -> int:
-    """EngineOptions::efficient_batch policy over a forward-time curve (ms at batch 1, 2, ...)."""
+def pick_efficient_batch(curve_ms, queued: int, tol: float = 0.0, margin: float = 0.02, ends=None) -> int:
+    """EngineOptions::efficient_batch policy over a forward-time curve (ms at batch 1, 2, ...);
+    ends: the engine's bucket sizes (only they are cut targets)."""
     arr = (C.c_double * (len(curve_ms) + 1))(0.0, *curve_ms)
-    return lib().die_pick_efficient_batch(arr, len(curve_ms), int(queued), float(tol), float(margin))
+    e = (C.c_int * len(ends))(*ends) if ends else None
+    return lib().die_pick_efficient_batch(arr, len(curve_ms), int(queued), float(tol), float(margin), e,
+                                          len(ends) if ends else 0)
 
 
 def fnv1a(s: str) -> int:

@@ -66,3 +66,19 @@ def test_efficient_batch_policy(native):
     assert native.pick_efficient_batch(small, 20, margin=0.02) == 20
     assert native.pick_efficient_batch(small, 20, margin=0.0) == 19
     assert native.pick_efficient_batch(step, 0) == 1 and native.pick_efficient_batch(step, 99) == 24
+
+
+def test_efficient_batch_bucket_ends(native):
+    """efficient_batch_ends (default on): only the graph bucket sizes are cut targets.  Round-6 curve
+    shape: the bucket-26 graph at 25 live looks cheaper per image than 24, yet a queue of 25 goes
+    out as 24 (a batch of 25 broke the serving loop's 24-request rhythm); 26 queued runs whole."""
+    ends = [1, 2, 4, 6, 8, 12, 16, 18, 20, 22, 24, 26, 28, 30, 32]
+    curve = [0.62 + 0.03 * b for b in range(1, 21)]
+    curve[19] = 1.17                                    # B = 20: 58.5 us / image
+    curve += [1.366, 1.378, 1.389, 1.394, 1.429, 1.441]  # 21..26: step at 21, 24 = 58.1, 25 = 57.2, 26 = 55.4
+    curve += [1.50] * 6
+    assert native.pick_efficient_batch(curve, 25, margin=0.0) == 25           # any size: 25 wins
+    assert native.pick_efficient_batch(curve, 25, margin=0.0, ends=ends) == 24
+    assert native.pick_efficient_batch(curve, 23, margin=0.0, ends=ends) == 20
+    assert native.pick_efficient_batch(curve, 26, margin=0.0, ends=ends) == 26
+    assert native.pick_efficient_batch(curve, 24, margin=0.0, ends=ends) == 24
