@@ -317,12 +317,6 @@ __global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
   if ((live && b >= *live) || b >= B || p0 >= Hp) return;  // whole block, before any barrier
   const long long oplane = static_cast<long long>(B) * Hp * Wp * NCH;
   const long long ring_plane = static_cast<long long>(RING) * PXF * 4;
-  for (int i = tid; i < NP * NCH * (KS / 8); i += nthr) {
-    const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
-    const int r = q / (KS / 8), c = q % (KS / 8);
-    *reinterpret_cast<uint4*>(wl + pl * NCH * WP + r * WP + c * 8) =
-        *reinterpret_cast<const uint4*>(w + pl * NCH * KS + r * KS + c * 8);
-  }
   float sc[4], sh[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -347,19 +341,56 @@ __global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
     if constexpr (SPLIT)
       *reinterpret_cast<uint2*>(d + ring_plane) = make_uint2(l[0] | (uint32_t(l[1]) << 16), l[2] | (uint32_t(l[3]) << 16));
   };
+  // Branch-free: raw buffer loads of the image (num_records = its C planes), off-image pixels and
+  // channels past C at an offset past the end, which the buffer returns as 0 -- no per-lane branch
+  // around a load, so a round's loads all stay in flight (behind `inb ? x[..] : 0` the compiler
+  // sank each pixel's loads into a branch and waited for them before the next pixel's).
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xb), 0, static_cast<int>(C * HW * 4), 0x00020000);
   auto load_px = [&](int iy, int q, float* raw) -> bool {
     const int ix = q - 3;
     const bool inb = iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const unsigned pix = inb ? static_cast<unsigned>(iy * W + ix) * 4u : 0x80000000u;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) raw[c] = (inb && c < C) ? xb[c * HW + static_cast<size_t>(iy) * W + ix] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+      const unsigned off = c < C ? pix + static_cast<unsigned>(c * HW * 4) : 0x80000000u;
+      raw[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+    }
     return inb;
   };
-  // segment start: input rows 4 p0 - 5 .. 4 p0 + 5 (halo stem row 2 p0 - 1 and stem rows 2 p0, 2 p0 + 1)
-  for (int i = tid; i < RING * PXF; i += nthr) {
-    const int iy = 4 * p0 - 5 + i / PXF, q = i % PXF;
-    float raw[4];
-    const bool inb = load_px(iy, q, raw);
-    put(iy, q, raw, inb);
+  // Segment start: input rows 4 p0 - 5 .. 4 p0 + 5 (halo stem row 2 p0 - 1 and stem rows 2 p0,
+  // 2 p0 + 1) and the weights, all loads issued before the first LDS store.
+  constexpr int SPT = 7;  // RING * PXF <= 7 * 64 CG for every CG >= 1 (11 (32 CG + 6) <= 448 CG)
+  float sraw[SPT][4];
+  bool sin[SPT];
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) {
+    const int i = min(tid + k * nthr, RING * PXF - 1);
+    sin[k] = load_px(4 * p0 - 5 + i / PXF, i % PXF, sraw[k]);
+  }
+  {
+    constexpr int WR = 8;  // weight chunks per thread and round (one round at CG >= 7)
+    const int nw = NP * NCH * (KS / 8);
+    for (int i0 = 0; i0 < nw; i0 += WR * nthr) {
+      uint4 wv[WR];
+#pragma unroll
+      for (int k = 0; k < WR; ++k) {
+        const int i = min(i0 + tid + k * nthr, nw - 1);
+        const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
+        wv[k] = *reinterpret_cast<const uint4*>(w + pl * NCH * KS + (q / (KS / 8)) * KS + (q % (KS / 8)) * 8);
+      }
+#pragma unroll
+      for (int k = 0; k < WR; ++k) {  // past the end: the last chunk again (same bytes, no branch)
+        const int i = min(i0 + tid + k * nthr, nw - 1);
+        const int pl = i / (NCH * (KS / 8)), q = i % (NCH * (KS / 8));
+        *reinterpret_cast<uint4*>(wl + pl * NCH * WP + (q / (KS / 8)) * WP + (q % (KS / 8)) * 8) = wv[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) {
+    const int i = tid + k * nthr;
+    if (i < RING * PXF) put(4 * p0 - 5 + i / PXF, i % PXF, sraw[k], sin[k]);
   }
   __syncthreads();
   const int j = lane >> 4, px_l = lane & 15, sx = 16 * wave + px_l;
@@ -400,16 +431,26 @@ __global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
   // stem epilogue -> the value the unfused pool would read back (hi + lo, or bf16); -inf off the map
   // (max pool padding).  Physical fragment n, lane group j, element t = logical channel
   // 32 (n >> 1) + 8 j + 4 (n & 1) + t.
+  // This lane's 16 channels' bias and pooled-value BN, in registers for the whole walk (loaded in
+  // the epilogue they were dependent global round trips on every pool row)
+  float bb[4][4], psc[4][4], psh[4][4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int ch = 32 * (n >> 1) + 8 * j + 4 * (n & 1);
+    const float4 bv = *reinterpret_cast<const float4*>(bias + ch);
+    const float4 sv = pscale ? *reinterpret_cast<const float4*>(pscale + ch) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 hv = pscale ? *reinterpret_cast<const float4*>(pshift + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bb[n][0] = bv.x, bb[n][1] = bv.y, bb[n][2] = bv.z, bb[n][3] = bv.w;
+    psc[n][0] = sv.x, psc[n][1] = sv.y, psc[n][2] = sv.z, psc[n][3] = sv.w;
+    psh[n][0] = hv.x, psh[n][1] = hv.y, psh[n][2] = hv.z, psh[n][3] = hv.w;
+  }
   auto stem_val = [&](const f32x4 (&acc)[4][2], int m, int sy, float (&r)[4][4]) {
     const bool ok = sy >= 0 && sy < Hs && sx < Ws;
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      const int ch = 32 * (n >> 1) + 8 * j + 4 * (n & 1);
-      const float4 bv = *reinterpret_cast<const float4*>(bias + ch);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        float v = acc[n][m][t] + bb[t];
+        float v = acc[n][m][t] + bb[n][t];
         if (relu) v = fmaxf(v, 0.f);
         if constexpr (SPLIT) {
           uint16_t h, l;
@@ -441,8 +482,8 @@ __global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
 #pragma unroll
       for (int k = 0; k < PPT; ++k) {
         const int i = tid + k * nthr;
-        pin[k] = false;
-        if (i < 4 * PXF) pin[k] = load_px(4 * p + 6 + i / PXF, i % PXF, pre[k]);
+        const int ic = min(i, 4 * PXF - 1);
+        pin[k] = load_px(4 * p + 6 + ic / PXF, ic % PXF, pre[k]);
       }
     }
     stem_rows(2 * p, 2, acc);
@@ -483,7 +524,7 @@ __global__ __launch_bounds__(512) void stem_pool_nchw_kernel(
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           v[t] = pv[2 * blk + (t >> 2)][t & 3];
-          if (pscale) v[t] = v[t] * pscale[ch + t] + pshift[ch + t];
+          if (pscale) v[t] = v[t] * psc[2 * blk + (t >> 2)][t & 3] + psh[2 * blk + (t >> 2)][t & 3];
           if (pact == 1) v[t] = fmaxf(v[t], 0.f);
         }
         store8v(o + ch, oplane, SPLIT, v);
