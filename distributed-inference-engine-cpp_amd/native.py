@@ -25,7 +25,8 @@ _READY_CB = C.CFUNCTYPE(None, C.c_void_p)  # loadgen on_ready hook (LoadgenOptio
 
 
 def lib_path() -> str:
-    return os.path.join(LIB_DIR, "libdie.so")
+    # DIE_LIB_PATH: another build of the library (same-box A/B measurements, tools/ab_ops.sh)
+    return os.environ.get("DIE_LIB_PATH") or os.path.join(LIB_DIR, "libdie.so")
 
 
 def lib() -> C.CDLL:

@@ -134,10 +134,12 @@ def test_efficient_batch_curve(native, models):
     """EngineOptions::efficient_batch: the engine times its captured forward at every batch size at
     start-up and preferred_batch(Q) is the largest B <= Q within efficient_batch_tol of the best
     per-image time over 1..Q; a batch it cuts back still runs correctly at that size.  Off: no curve
-    and every queue is taken whole."""
+    and every queue is taken whole.  (Any-size cuts, efficient_batch_ends off: the default bucket-end
+    rule has its own test, tests/test_engine_options.py::test_efficient_batch_bucket_ends.)"""
     path, w, cfg = models["tiny"]
     tol = 0.03
-    e = native.Engine(path, device="hip", max_batch=16, autotune=False, tune_cache="", efficient_batch_tol=tol)
+    e = native.Engine(path, device="hip", max_batch=16, autotune=False, tune_cache="", efficient_batch_tol=tol,
+                      efficient_batch_ends=False)
     info = e.refresh_info()
     curve = info["batch_curve_ms"]
     assert info["efficient_batch"] is True and len(curve) == 16 and all(c > 0 for c in curve)
