@@ -112,8 +112,28 @@ __device__ __forceinline__ float2 row_parts_direct(const ConvArgs& p, int m) {
 // not depend on which lane stores it.
 // rpre: the residual's 8 values already loaded (tile_epilogue prefetches a thread's residual rows
 // before its first store, so the loads are not serialised behind the previous group's stores).
+// This thread's 8 output channels' epilogue parameters (bias, dual-store BN, LayerNorm column sums),
+// loaded once before the tile's first store: loaded per group inside epilogue8 they came after the
+// previous group's stores, and vmcnt counts loads and stores in issue order, so each group's wait
+// for them also drained the previous group's stores (one store round trip per group).
+struct EpiChan {
+  float b[8], s2[8], h2[8], cs[8];
+};
+__device__ __forceinline__ void load_epi_chan(const ConvArgs& p, int n, EpiChan& c) {
+  auto ld8 = [&](const float* src, float* d) {
+    const float4 a = ldf4(src + n), b = ldf4(src + n + 4);
+    d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
+  };
+  if (p.bias) ld8(p.bias, c.b);
+  if (p.out2) {
+    ld8(p.scale2, c.s2);
+    ld8(p.shift2, c.h2);
+  }
+  if (p.row_stats || p.row_parts) ld8(p.col_sum, c.cs);
+}
+
 __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float* v, const float* ms = nullptr,
-                                          const float* rpre = nullptr) {
+                                          const float* rpre = nullptr, const EpiChan* ec = nullptr) {
   const size_t o = static_cast<size_t>(m) * p.N + n;
   const bool split = p.split != 0;
   if (p.row_stats || p.row_parts) {
@@ -129,15 +149,26 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
       mean = r.x;
       rstd = r.y;
     }
-    const float4 c0 = ldf4(p.col_sum + n), c1 = ldf4(p.col_sum + n + 4);
-    const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    float cs[8];
+    if (ec) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) cs[t] = ec->cs[t];
+    } else {
+      const float4 c0 = ldf4(p.col_sum + n), c1 = ldf4(p.col_sum + n + 4);
+      cs[0] = c0.x, cs[1] = c0.y, cs[2] = c0.z, cs[3] = c0.w, cs[4] = c1.x, cs[5] = c1.y, cs[6] = c1.z, cs[7] = c1.w;
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = rstd * (v[t] - mean * cs[t]);
   }
   if (p.bias) {
-    const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    if (ec) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] += ec->b[t];
+    } else {
+      const float4 b0 = ldf4(p.bias + n), b1 = ldf4(p.bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
   }
   if (p.res) {
     float r[8];
@@ -164,10 +195,16 @@ __device__ __forceinline__ void epilogue8(const ConvArgs& p, int m, int n, float
     *reinterpret_cast<float4*>(p.out_f32 + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
   if (p.out2) {
-    const float4 s0 = ldf4(p.scale2 + n), s1 = ldf4(p.scale2 + n + 4);
-    const float4 h0 = ldf4(p.shift2 + n), h1 = ldf4(p.shift2 + n + 4);
-    float u[8] = {v[0] * s0.x + h0.x, v[1] * s0.y + h0.y, v[2] * s0.z + h0.z, v[3] * s0.w + h0.w,
-                  v[4] * s1.x + h1.x, v[5] * s1.y + h1.y, v[6] * s1.z + h1.z, v[7] * s1.w + h1.w};
+    float u[8];
+    if (ec) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) u[t] = v[t] * ec->s2[t] + ec->h2[t];
+    } else {
+      const float4 s0 = ldf4(p.scale2 + n), s1 = ldf4(p.scale2 + n + 4);
+      const float4 h0 = ldf4(p.shift2 + n), h1 = ldf4(p.shift2 + n + 4);
+      u[0] = v[0] * s0.x + h0.x, u[1] = v[1] * s0.y + h0.y, u[2] = v[2] * s0.z + h0.z, u[3] = v[3] * s0.w + h0.w;
+      u[4] = v[4] * s1.x + h1.x, u[5] = v[5] * s1.y + h1.y, u[6] = v[6] * s1.z + h1.z, u[7] = v[7] * s1.w + h1.w;
+    }
     if (p.relu2) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) u[t] = fmaxf(u[t], 0.f);
@@ -496,6 +533,11 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
       gn[i] = n0 + gcg[i] * 8;
       if (gn[i] >= p.N) gm[i] = -1;
     }
+    // every group of a thread has the same 8 channels (NT is a multiple of GPR): their parameters
+    // are loaded once, here, before any store of the tile (EpiChan)
+    static_assert(NT % GPR == 0, "a thread's groups share their channels");
+    EpiChan ec;
+    load_epi_chan(p, min(n0 + (tid % GPR) * 8, p.N - 8), ec);
     auto grow_i = [&](int i) { return grow[i]; };
     auto gcg_i = [&](int i) { return gcg[i]; };
     auto gm_i = [&](int i) { return gm[i] < 0 ? 0 : gm[i]; };
@@ -543,7 +585,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p,
           for (int t = 0; t < 8; ++t) r[t] += l[t];
         }
       }
-      epilogue8(p, gm[i], gn[i], v, rowc ? rowc + 2 * grow[i] : nullptr, p.res ? r : nullptr);
+      epilogue8(p, gm[i], gn[i], v, rowc ? rowc + 2 * grow[i] : nullptr, p.res ? r : nullptr, &ec);
     };
     if (!partial) {
 #pragma unroll

@@ -167,15 +167,47 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
   // the top = at most (W2 slice + residual) younger operations outstanding; the x stores of ci-1
   // are older still.  W2 slice ci has landed once the epilogue's wait for the residual (younger)
   // returns, before B1.  (Empty asm statements with a memory clobber pin the issue order.)
+  // The reduce epilogue's bias, loaded once up front (loaded at the end, its wait also drained the
+  // last chunk's x / a stores: vmcnt counts loads and stores in issue order).
+  // (without WS only: with WS the registers are at the 2-waves-per-SIMD limit)
+  float bb2[NF2 / 2][8];
+  auto load_bias2 = [&](int q) {
+    const int n = wn * (N2 / 2) + q * 32 + 8 * g;
+    const float4 b0 = *reinterpret_cast<const float4*>(p.bias2 + n);
+    const float4 b1 = *reinterpret_cast<const float4*>(p.bias2 + n + 4);
+    bb2[q][0] = b0.x, bb2[q][1] = b0.y, bb2[q][2] = b0.z, bb2[q][3] = b0.w;
+    bb2[q][4] = b1.x, bb2[q][5] = b1.y, bb2[q][6] = b1.z, bb2[q][7] = b1.w;
+  };
+  if constexpr (!WS) {
+#pragma unroll
+    for (int q = 0; q < NF2 / 2; ++q) load_bias2(q);
+  }
   issue_y();
   issue_w1(0);
   if constexpr (!WS) issue_w2(0);
   for (int ci = 0; ci < NC; ++ci) {
     asm volatile("" ::: "memory");
     load_res(ci);
+    // Chunk ci's expand-epilogue parameters.  Loaded in the epilogue (after issue_w2), their wait
+    // also waited for the W2 slice issued just before them, vmcnt counting in issue order.  Without
+    // WS they ride with the residual (6 loads, the youngest); with WS (whose registers are at the
+    // 2-waves-per-SIMD limit during the expand MFMAs) they are issued after the expand, before the
+    // W2 slice.
+    const int c0 = ci * BK + cg;  // this lane's 8 logical channels
+    float4 b0, b1, s0, s1, h0, h1;
+    auto load_par = [&]() {
+      b0 = *reinterpret_cast<const float4*>(p.bias1 + c0);
+      b1 = *reinterpret_cast<const float4*>(p.bias1 + c0 + 4);
+      s0 = *reinterpret_cast<const float4*>(p.scale2 + c0);
+      s1 = *reinterpret_cast<const float4*>(p.scale2 + c0 + 4);
+      h0 = *reinterpret_cast<const float4*>(p.shift2 + c0);
+      h1 = *reinterpret_cast<const float4*>(p.shift2 + c0 + 4);
+    };
+    if constexpr (!WS) load_par();
     asm volatile("" ::: "memory");
-    // outstanding after the wait: the residual (and, without WS, the W2 slice issued before it)
-    wait_vmcnt<(WS ? 0 : GW2) + 2 * NP>();
+    // outstanding after the wait: the residual (and, without WS, the parameters and the W2 slice
+    // issued before them)
+    wait_vmcnt<(WS ? 0 : GW2 + 6) + 2 * NP>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
@@ -206,19 +238,14 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
 
     if constexpr (WS) {
       __syncthreads();  // every wave done with the W1 chunk: the buffer takes the W2 slice
+      load_par();
+      asm volatile("" ::: "memory");
       issue_w2(ci);
       asm volatile("" ::: "memory");
       wait_vmcnt<GW2>();  // the residual (issued before the W2 slice) has landed
     }
 
     // ---- 2. epilogue: x_{u+1} and the pre-activation tile ----
-    const int c0 = ci * BK + cg;  // this lane's 8 logical channels
-    const float4 b0 = *reinterpret_cast<const float4*>(p.bias1 + c0);
-    const float4 b1 = *reinterpret_cast<const float4*>(p.bias1 + c0 + 4);
-    const float4 s0 = *reinterpret_cast<const float4*>(p.scale2 + c0);
-    const float4 s1 = *reinterpret_cast<const float4*>(p.scale2 + c0 + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(p.shift2 + c0);
-    const float4 h1 = *reinterpret_cast<const float4*>(p.shift2 + c0 + 4);
     const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
     const float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
@@ -304,9 +331,8 @@ __global__ __launch_bounds__(256) void conv_pair_kernel(const PairArgs p) {
 #pragma unroll
   for (int q = 0; q < NF2 / 2; ++q) {
     const int n = wn * (N2 / 2) + q * 32 + 8 * g;
-    const float4 b0 = *reinterpret_cast<const float4*>(p.bias2 + n);
-    const float4 b1 = *reinterpret_cast<const float4*>(p.bias2 + n + 4);
-    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    if constexpr (WS) load_bias2(q);
+    const float* bb = bb2[q];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (!pv[j]) continue;
