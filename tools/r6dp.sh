@@ -1,5 +1,6 @@
 # round-6: DP leader merge target balanced (default) vs not, world 1 with the merge path forced,
 # interleaved rounds on one box.  usage: bash tools/r6dp.sh <out-name> [rounds]
+# (the --no-dp-balance flag and EngineOptions::dp_balance were removed with the revert: profiles/r6_dp_balance_ab.md)
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 export DIE_TUNE_CACHE=${DIE_TUNE_CACHE:-$PWD/tools/tune_r6_final.json}
