@@ -9,7 +9,7 @@
 //     reads taps (2j, 2j+1) of that row: 16 contiguous, 16-byte-aligned bytes of the patch, and the
 //     16 lanes of a group read 16 consecutive output pixels = 256 contiguous bytes (no bank
 //     conflicts);
-//   * weights [64][224] (BN folded) sit in LDS with a 232-element pitch (conflict-free A reads);
+//   * weights [64][224] (BN folded) sit in LDS with a 240-element pitch (conflict-free A reads for the b128 lane groups);
 //   * epilogue: + bias, optional ReLU, bf16, staged through LDS (XOR-swizzled) so each output pixel's
 //     128 bytes go out as 16-byte stores.
 //   * SPLIT (fp32 mode, common.h): input, weights and output are hi/lo planes; both planes of the
@@ -28,7 +28,7 @@ namespace {
 
 constexpr int TY = 8, TX = 16;               // output tile
 constexpr int PY = 2 * TY + 5, PX = 2 * TX + 6;  // patch (PX even: kx padded to 8)
-constexpr int KS = 224, WP = 232;            // K and weight LDS pitch (elements)
+constexpr int KS = 224, WP = 240;            // K and weight LDS pitch (elements): conflict-free A reads
 constexpr int NCH = 64;
 
 template <bool SPLIT>
