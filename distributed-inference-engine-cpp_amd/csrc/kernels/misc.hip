@@ -134,21 +134,67 @@ __global__ __launch_bounds__(256) void gap_kernel(const uint16_t* __restrict__ x
   float acc[8] = {init, init, init, init, init, init, init, init};
   if (g < CG) {
     float sc[8], sf[8];
+    auto load_affine = [&]() {  // 16-B loads (g * 8 floats is 32-B aligned)
+      if (scale) {
+        const float4 s0 = *reinterpret_cast<const float4*>(scale + g * 8), s1 = *reinterpret_cast<const float4*>(scale + g * 8 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(shift + g * 8), h1 = *reinterpret_cast<const float4*>(shift + g * 8 + 4);
+        sc[0] = s0.x, sc[1] = s0.y, sc[2] = s0.z, sc[3] = s0.w, sc[4] = s1.x, sc[5] = s1.y, sc[6] = s1.z, sc[7] = s1.w;
+        sf[0] = h0.x, sf[1] = h0.y, sf[2] = h0.z, sf[3] = h0.w, sf[4] = h1.x, sf[5] = h1.y, sf[6] = h1.z, sf[7] = h1.w;
+      } else {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      sc[t] = scale ? scale[g * 8 + t] : 1.f;
-      sf[t] = scale ? shift[g * 8 + t] : 0.f;
-    }
+        for (int t = 0; t < 8; ++t) sc[t] = 1.f, sf[t] = 0.f;
+      }
+    };
     const uint16_t* src = x + static_cast<long long>(b) * HW * C + g * 8;
-#pragma unroll 4
-    for (int p = slice; p < HW; p += S) {
-      float v[8];
-      load8v(src + static_cast<long long>(p) * C, xplane, split != 0, v);
+    auto add = [&](const float* v) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         float u = v[t] * sc[t] + sf[t];
         if (relu) u = fmaxf(u, 0.f);
         acc[t] = mode == 2 ? fmaxf(acc[t], u) : acc[t] + u;
+      }
+    };
+    constexpr int MAXP = 8;  // pixels per thread in one round of loads (ResNet50's 7x7 map: 6-7 with S = 8)
+    if (HW <= MAXP * S) {
+      // Every load of the thread in flight at once (one memory round trip), as raw buffer loads: a
+      // pixel past the map (and the lo plane of a bf16 map) sits at an offset past num_records and
+      // reads as 0, so no per-lane branch surrounds a load (the loop below compiles to one wait per
+      // pixel).  Sums in pixel order, as the loop below.
+      const long long planeb = xplane * 2;  // bytes per plane
+      const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(x), 0, static_cast<int>(split ? 2 * planeb : planeb), 0x00020000);
+      const unsigned base = static_cast<unsigned>((static_cast<long long>(b) * HW * C + g * 8) * 2);
+      uint4 hi[MAXP], lo[MAXP];
+#pragma unroll
+      for (int k = 0; k < MAXP; ++k) {
+        const int p = slice + k * S;
+        const unsigned off = p < HW ? base + static_cast<unsigned>(p * C * 2) : 0x80000000u;
+        hi[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        lo[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              xr, split ? off + static_cast<unsigned>(planeb) : 0x80000000u, 0, 0));
+      }
+      load_affine();  // after the pixel loads: one round trip for both
+#pragma unroll
+      for (int k = 0; k < MAXP; ++k) {
+        if (slice + k * S < HW) {
+          float v[8];
+          unpack8(hi[k], v);
+          if (split) {
+            float w[8];
+            unpack8(lo[k], w);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] += w[t];
+          }
+          add(v);
+        }
+      }
+    } else {
+      load_affine();
+#pragma unroll 4
+      for (int p = slice; p < HW; p += S) {
+        float v[8];
+        load8v(src + static_cast<long long>(p) * C, xplane, split != 0, v);
+        add(v);
       }
     }
   }
