@@ -21,21 +21,18 @@ namespace igemm {
 namespace {
 
 constexpr int kSkRows = 32;   // pixel rows (two 16-row MFMA fragments)
+constexpr int kSkCols = 16;   // output channels per block
 constexpr int kSkWaves = 8;   // K split inside the block
 
-// COLS output channels per block: 16 (one MFMA fragment), or 8 (cfg tile 1: twice the blocks --
-// the FC head's 1000 classes on 125 CUs instead of 63 -- with the fragment's upper 8 weight rows
-// duplicating the lower 8 and their results dropped)
-template <bool SPLIT, int COLS>
+template <bool SPLIT>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const ConvArgs p) {
-  static_assert(COLS == 16 || COLS == 8, "channels per block");
-  __shared__ float red[kSkWaves][kSkRows][COLS + 1];
+  __shared__ float red[kSkWaves][kSkRows][kSkCols + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * COLS;
+  const int n0 = blockIdx.x * kSkCols;
   const int Ml = p.live ? min(p.M, static_cast<int>(*p.live) * p.Ho * p.Wo) : p.M;
   const int r = lane & 15, kq = (lane >> 4) * 8;
   // clamped rows read valid memory; their results are never stored
-  const int nrow = min(n0 + (r & (COLS - 1)), p.N - 1);
+  const int nrow = min(n0 + r, p.N - 1);
   const int ma = min(r, p.M - 1), mb = min(16 + r, p.M - 1);
   const int kper = p.K / kSkWaves;
   const int k0 = wave * kper + kq;
@@ -61,16 +58,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const ConvArgs p) {
     acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc1, 0, 0, 0);
   }
   // lane: channels 4 (lane >> 4) + t of pixel lane & 15 (acc0) / 16 + lane & 15 (acc1)
-  if ((lane >> 4) * 4 < COLS) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      red[wave][r][(lane >> 4) * 4 + t] = acc0[t];
-      red[wave][16 + r][(lane >> 4) * 4 + t] = acc1[t];
-    }
+  for (int t = 0; t < 4; ++t) {
+    red[wave][r][(lane >> 4) * 4 + t] = acc0[t];
+    red[wave][16 + r][(lane >> 4) * 4 + t] = acc1[t];
   }
   __syncthreads();
-  if (tid < kSkRows * (COLS / 8)) {
-    const int m = tid / (COLS / 8), c0 = (tid % (COLS / 8)) * 8, n = n0 + c0;
+  if (tid < kSkRows * 2) {
+    const int m = tid >> 1, c0 = (tid & 1) * 8, n = n0 + c0;
     if (m < Ml && n < p.N) {
       float v[8];
 #pragma unroll
@@ -88,7 +83,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const ConvArgs p) {
 }  // namespace
 
 hipError_t launch_tile_skinny(const ConvArgs& a, hipStream_t s, int tile) {
-  if (tile != TILE_128x128 && tile != TILE_128x64) return hipErrorInvalidValue;
+  if (tile != TILE_128x128) return hipErrorInvalidValue;
   const bool dense = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho &&
                      a.W == a.Wo && a.Cin == a.K && a.K <= a.Kpad;
   // rows <= 32, whole 32-wide K-steps per wave, 8-channel epilogue groups, no split-K, no LayerNorm
@@ -105,15 +100,9 @@ hipError_t launch_tile_skinny(const ConvArgs& a, hipStream_t s, int tile) {
   } else {
     b.xplane = b.oplane = 0;
   }
-  if (tile == TILE_128x128) {
-    const dim3 grid((a.N + 15) / 16);
-    if (a.split) hipLaunchKernelGGL((gemm_skinny_kernel<true, 16>), grid, dim3(512), 0, s, b);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<false, 16>), grid, dim3(512), 0, s, b);
-  } else {
-    const dim3 grid((a.N + 7) / 8);
-    if (a.split) hipLaunchKernelGGL((gemm_skinny_kernel<true, 8>), grid, dim3(512), 0, s, b);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<false, 8>), grid, dim3(512), 0, s, b);
-  }
+  const dim3 grid((a.N + kSkCols - 1) / kSkCols);
+  if (a.split) hipLaunchKernelGGL(gemm_skinny_kernel<true>, grid, dim3(512), 0, s, b);
+  else hipLaunchKernelGGL(gemm_skinny_kernel<false>, grid, dim3(512), 0, s, b);
   return hipGetLastError();
 }
 

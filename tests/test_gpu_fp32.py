@@ -346,11 +346,10 @@ def test_patchify_conv_lds_dma_mode(native, split):
     assert any(20 <= c < 24 for c in ran), ran  # 1-stage LDS-DMA loop
 
 
-@pytest.mark.parametrize("cfg", [32, 33])
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("M,K,N", [(1, 2048, 1000), (7, 2048, 1000), (20, 2048, 1000), (32, 512, 64), (24, 256, 1008)])
-def test_skinny_gemm(native, M, K, N, split, cfg):
-    """Variant 8 (cfg 32 / 33, conv_skinny.hip): <= 32 dense rows, 16 / 8 channels per block, K split over 8
+def test_skinny_gemm(native, M, K, N, split):
+    """Variant 8 (cfg 32, conv_skinny.hip): <= 32 dense rows, 16 channels per block, K split over 8
     waves and summed in wave order.  fp32 (split) against float64 at the layer bar, bf16 against
     torch; with the residual / dual-store epilogue, a live batch, bitwise repeatable; shapes it
     does not take (33 rows, K not a multiple of 256, split-K) are refused."""
@@ -369,7 +368,7 @@ def test_skinny_gemm(native, M, K, N, split, cfg):
     v = torch.relu(x.double().reshape(M, K) @ w.double().reshape(N, K).T + bias.double() + res.double().reshape(M, N))
     u = torch.relu(v * s2.double() + b2.double())
     pr = K_.ConvProblem(x, w, bias=bias, relu=True, res=res, scale2=s2, shift2=b2, relu2=True, max_splits=2, split=split)
-    assert pr.launch(cfg, 1, False) == 0
+    assert pr.launch(32, 1, False) == 0
     torch.cuda.synchronize()
     out, out2 = pr.results()
     tol = TOL if split else 2e-2
@@ -377,21 +376,21 @@ def test_skinny_gemm(native, M, K, N, split, cfg):
     assert rel_err(out2.reshape(M, N), u) < tol
     first = out.clone()
     for _ in range(3):
-        assert pr.launch(cfg, 1, False) == 0
+        assert pr.launch(32, 1, False) == 0
         torch.cuda.synchronize()
         assert torch.equal(pr.results()[0], first)
     # live batch: rows past it keep what was there
     if M > 1:
         lv = torch.tensor([M // 2], dtype=torch.int64, device="cuda")
         pr.out.zero_()
-        assert pr.launch(cfg, 1, False, extra={"live": lv.data_ptr()}) == 0
+        assert pr.launch(32, 1, False, extra={"live": lv.data_ptr()}) == 0
         torch.cuda.synchronize()
         got = pr.results()[0].reshape(M, N)
         assert torch.equal(got[: M // 2], first.reshape(M, N)[: M // 2])
         assert not got[M // 2:].any()
-    assert pr.launch(cfg, 2, False) != 0  # no split-K
-    for c in (34, 35):
-        assert pr.launch(c, 1, False) != 0  # tiles 0 and 1 only
+    assert pr.launch(32, 2, False) != 0  # no split-K
+    for cfg in (33, 34, 35):
+        assert pr.launch(cfg, 1, False) != 0  # tile 0 only
 
 
 def test_skinny_gemm_refuses_other_shapes(native):
